@@ -1,0 +1,202 @@
+// PyTorch bindings for the kubedl_amd HIP kernels (module ``kubedl_amd._C``).
+//
+// Kernels live in the *.hip translation units and take raw pointers plus a
+// hipStream_t; this file owns all tensor checks, output allocation (through
+// the PyTorch caching allocator) and stream selection.  Every launch goes to
+// PyTorch's current HIP stream so the ops compose with autograd, RCCL and
+// hipGraph capture.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kdl_api.h"
+
+namespace {
+
+int dtype_code(const at::Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  if (t.scalar_type() == at::kFloat) return 0;
+  TORCH_CHECK(false, "kubedl_amd: unsupported dtype ", t.scalar_type());
+  return -1;
+}
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "kubedl_amd: ", what, " failed: ", hipGetErrorString(e));
+}
+
+bool is_nhwc_dense(const at::Tensor& t) {
+  if (t.dim() == 4) return t.is_contiguous(at::MemoryFormat::ChannelsLast);
+  return t.is_contiguous();
+}
+
+// ------------------------------------------------------------------ BN + act
+std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight,
+                                   const at::Tensor& bias, const at::Tensor& running_mean,
+                                   const at::Tensor& running_var,
+                                   const c10::optional<at::Tensor>& residual, bool relu,
+                                   bool training, double momentum, double eps) {
+  TORCH_CHECK(x.is_cuda(), "bn_act_fwd: x must be on the GPU");
+  TORCH_CHECK(x.dim() == 4 || x.dim() == 2, "bn_act_fwd: x must be NHWC 4-D or [M, C]");
+  TORCH_CHECK(is_nhwc_dense(x), "bn_act_fwd: x must be channels_last-dense");
+  const c10::hip::HIPGuard guard(x.device());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(weight.numel() == C && bias.numel() == C, "bn_act_fwd: affine size mismatch");
+  TORCH_CHECK(weight.scalar_type() == bias.scalar_type(), "bn_act_fwd: weight/bias dtype mismatch");
+  TORCH_CHECK(running_mean.scalar_type() == at::kFloat && running_var.scalar_type() == at::kFloat,
+              "bn_act_fwd: running stats must be fp32");
+  const at::Tensor* res = nullptr;
+  if (residual.has_value()) {
+    res = &residual.value();
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type() &&
+                    is_nhwc_dense(*res),
+                "bn_act_fwd: residual must match x (shape, dtype, channels_last)");
+  }
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto save_mean = at::empty({C}, fopt);
+  auto save_invstd = at::empty({C}, fopt);
+  auto ws = at::empty({kdl::bn_workspace_floats(M, static_cast<int>(C), dtype_code(x))}, fopt);
+  check_hip(kdl::bn_act_forward(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(),
+                                weight.data_ptr(), bias.data_ptr(),
+                                training ? running_mean.data_ptr<float>() : running_mean.data_ptr<float>(),
+                                running_var.data_ptr<float>(), save_mean.data_ptr<float>(),
+                                save_invstd.data_ptr<float>(), ws.data_ptr<float>(), M,
+                                static_cast<int>(C), dtype_code(x), dtype_code(weight), relu,
+                                training, static_cast<float>(momentum), static_cast<float>(eps),
+                                cur_stream()),
+            "bn_act_forward");
+  return {y, save_mean, save_invstd};
+}
+
+std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& y,
+                                   const at::Tensor& weight, const at::Tensor& mean,
+                                   const at::Tensor& invstd, bool relu, bool has_residual,
+                                   bool training) {
+  TORCH_CHECK(is_nhwc_dense(dy) && is_nhwc_dense(x) && is_nhwc_dense(y),
+              "bn_act_bwd: tensors must be channels_last-dense");
+  TORCH_CHECK(dy.sizes() == x.sizes() && y.sizes() == x.sizes(), "bn_act_bwd: shape mismatch");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "bn_act_bwd: dtype mismatch");
+  const c10::hip::HIPGuard guard(x.device());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  auto dx = at::empty_like(x);
+  at::Tensor dres;
+  if (has_residual) dres = at::empty_like(x);
+  auto dgamma = at::empty_like(weight);
+  auto dbeta = at::empty_like(weight);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto ws = at::empty({kdl::bn_workspace_floats(M, static_cast<int>(C), dtype_code(x))}, fopt);
+  check_hip(kdl::bn_act_backward(dy.data_ptr(), y.data_ptr(), x.data_ptr(), weight.data_ptr(),
+                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), dx.data_ptr(),
+                                 has_residual ? dres.data_ptr() : nullptr, dgamma.data_ptr(),
+                                 dbeta.data_ptr(), ws.data_ptr<float>(), M, static_cast<int>(C),
+                                 dtype_code(x), dtype_code(weight), relu, training, cur_stream()),
+            "bn_act_backward");
+  return {dx, dgamma, dbeta, has_residual ? dres : at::Tensor()};
+}
+
+// ------------------------------------------------------------------ optimizers
+kdl::OptHyper make_hyper(double lr, double momentum, double dampening, double eps, double bc1,
+                         double bc2, double grad_scale, bool nesterov, bool first_step, bool adam_w,
+                         const std::vector<double>& wd, const std::vector<double>& lr_scale) {
+  kdl::OptHyper h{};
+  h.lr = static_cast<float>(lr);
+  h.momentum = static_cast<float>(momentum);
+  h.dampening = static_cast<float>(dampening);
+  h.eps = static_cast<float>(eps);
+  h.bc1 = static_cast<float>(bc1);
+  h.bc2 = static_cast<float>(bc2);
+  h.grad_scale = static_cast<float>(grad_scale);
+  h.nesterov = nesterov;
+  h.first_step = first_step;
+  h.adam_w = adam_w;
+  TORCH_CHECK(wd.size() <= 4 && lr_scale.size() <= 4, "at most 4 hyper-parameter groups");
+  for (int i = 0; i < 4; ++i) {
+    h.wd[i] = i < static_cast<int>(wd.size()) ? static_cast<float>(wd[i]) : 0.f;
+    h.lr_scale[i] = i < static_cast<int>(lr_scale.size()) ? static_cast<float>(lr_scale[i]) : 1.f;
+  }
+  return h;
+}
+
+void check_chunks(const at::Tensor& chunks) {
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong && chunks.dim() == 2 &&
+                  chunks.size(1) == 2,
+              "chunk table must be an int64 [n, 2] GPU tensor");
+  static_assert(sizeof(kdl::OptChunk) == 16, "OptChunk layout");
+}
+
+void sgd_step(const at::Tensor& chunks, at::Tensor master, at::Tensor mom, const at::Tensor& grad,
+              at::Tensor param, double lr, double momentum, double dampening, double grad_scale,
+              bool nesterov, bool first_step, const std::vector<double>& wd,
+              const std::vector<double>& lr_scale) {
+  check_chunks(chunks);
+  TORCH_CHECK(master.scalar_type() == at::kFloat && mom.scalar_type() == at::kFloat,
+              "sgd_step: master/momentum must be fp32");
+  TORCH_CHECK(master.numel() == grad.numel() && grad.numel() == param.numel() &&
+                  mom.numel() == master.numel(),
+              "sgd_step: flat buffer size mismatch");
+  const c10::hip::HIPGuard guard(master.device());
+  auto h = make_hyper(lr, momentum, dampening, 0, 1, 1, grad_scale, nesterov, first_step, false, wd,
+                      lr_scale);
+  check_hip(kdl::fused_sgd(reinterpret_cast<const kdl::OptChunk*>(chunks.data_ptr<int64_t>()),
+                           static_cast<int>(chunks.size(0)), master.data_ptr<float>(),
+                           mom.data_ptr<float>(), grad.data_ptr(), param.data_ptr(),
+                           dtype_code(grad), dtype_code(param), h, cur_stream()),
+            "fused_sgd");
+}
+
+void adam_step(const at::Tensor& chunks, at::Tensor master, at::Tensor m1, at::Tensor m2,
+               const at::Tensor& grad, at::Tensor param, double lr, double beta1, double beta2,
+               double eps, int64_t step, double grad_scale, bool adam_w,
+               const std::vector<double>& wd, const std::vector<double>& lr_scale) {
+  check_chunks(chunks);
+  TORCH_CHECK(master.numel() == grad.numel() && grad.numel() == param.numel() &&
+                  m1.numel() == master.numel() && m2.numel() == master.numel(),
+              "adam_step: flat buffer size mismatch");
+  const c10::hip::HIPGuard guard(master.device());
+  const double bc1 = 1.0 - std::pow(beta1, static_cast<double>(step));
+  const double bc2 = 1.0 - std::pow(beta2, static_cast<double>(step));
+  auto h = make_hyper(lr, beta1, beta2, eps, bc1, bc2, grad_scale, false, false, adam_w, wd, lr_scale);
+  check_hip(kdl::fused_adam(reinterpret_cast<const kdl::OptChunk*>(chunks.data_ptr<int64_t>()),
+                            static_cast<int>(chunks.size(0)), master.data_ptr<float>(),
+                            m1.data_ptr<float>(), m2.data_ptr<float>(), grad.data_ptr(),
+                            param.data_ptr(), dtype_code(grad), dtype_code(param), h, cur_stream()),
+            "fused_adam");
+}
+
+at::Tensor chunk_sumsq(const at::Tensor& chunks, const at::Tensor& x, double scale) {
+  check_chunks(chunks);
+  const c10::hip::HIPGuard guard(x.device());
+  auto out = at::empty({chunks.size(0)}, x.options().dtype(at::kFloat));
+  check_hip(kdl::chunk_sumsq(reinterpret_cast<const kdl::OptChunk*>(chunks.data_ptr<int64_t>()),
+                             static_cast<int>(chunks.size(0)), x.data_ptr(), dtype_code(x),
+                             static_cast<float>(scale), out.data_ptr<float>(), cur_stream()),
+            "chunk_sumsq");
+  return out;
+}
+
+void cast_copy(const at::Tensor& src, at::Tensor dst) {
+  TORCH_CHECK(src.numel() == dst.numel() && src.is_contiguous() && dst.is_contiguous(),
+              "cast_copy: size/contiguity mismatch");
+  TORCH_CHECK(src.numel() % 8 == 0, "cast_copy: numel must be a multiple of 8");
+  const c10::hip::HIPGuard guard(src.device());
+  check_hip(kdl::cast_copy(src.data_ptr(), dtype_code(src), dst.data_ptr(), dtype_code(dst),
+                           src.numel(), cur_stream()),
+            "cast_copy");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";
+  m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC");
+  m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC");
+  m.def("sgd_step", &sgd_step, "flat chunked fused SGD-momentum with fp32 master weights");
+  m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights");
+  m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");
+  m.def("cast_copy", &cast_copy, "flat dtype-casting copy");
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,112 @@
+// Common device helpers for the kubedl_amd CDNA4 (gfx950) kernels.
+//
+// Everything here is written for wave64 / 16-byte-per-lane vector memory
+// access (MI355X guide, Guideline 13: bf16 data is always moved as 8-element
+// 16-byte vectors).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KDL_CHECK_HIP(expr)                                                        \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) return _e;                                              \
+  } while (0)
+
+namespace kdl {
+
+constexpr int kWave = 64;
+
+typedef uint16_t bf16_t;  // raw bf16 bits
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+
+// round-to-nearest-even, NaN preserved
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return static_cast<bf16_t>((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<bf16_t>(u >> 16);
+}
+
+// Load/store VEC elements of type T as fp32.  VEC*sizeof(T) is 16 bytes on
+// the fast path (8 x bf16 or 4 x f32), so each lane issues one dwordx4.
+template <typename T, int VEC> struct Vec;
+
+template <> struct Vec<bf16_t, 8> {
+  __device__ __forceinline__ static void load(const bf16_t* p, float (&o)[8]) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = __uint_as_float(w[i] << 16);
+      o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float (&o)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = static_cast<uint32_t>(f32_to_bf16(o[2 * i])) |
+             (static_cast<uint32_t>(f32_to_bf16(o[2 * i + 1])) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+template <> struct Vec<float, 4> {
+  __device__ __forceinline__ static void load(const float* p, float (&o)[4]) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&o)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+};
+
+// scalar fallback (unaligned / odd channel counts)
+template <typename T> struct Vec1;
+template <> struct Vec1<bf16_t> {
+  __device__ __forceinline__ static float ld(const bf16_t* p) { return bf16_to_f32(*p); }
+  __device__ __forceinline__ static void st(bf16_t* p, float v) { *p = f32_to_bf16(v); }
+};
+template <> struct Vec1<float> {
+  __device__ __forceinline__ static float ld(const float* p) { return *p; }
+  __device__ __forceinline__ static void st(float* p, float v) { *p = v; }
+};
+
+template <typename T, int VEC> struct VecIO {
+  __device__ __forceinline__ static void load(const T* p, float (&o)[VEC]) {
+    if constexpr (VEC == 1) {
+      o[0] = Vec1<T>::ld(p);
+    } else {
+      Vec<T, VEC>::load(p, o);
+    }
+  }
+  __device__ __forceinline__ static void store(T* p, const float (&o)[VEC]) {
+    if constexpr (VEC == 1) {
+      Vec1<T>::st(p, o[0]);
+    } else {
+      Vec<T, VEC>::store(p, o);
+    }
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Grid sizing for memory-bound kernels (guide Guideline 11): enough blocks to
+// fill 256 CUs several times over, capped so each thread still loops.
+__host__ __forceinline__ int mem_bound_grid(int64_t work_items, int block, int cap = 2048) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
+}
+
+}  // namespace kdl

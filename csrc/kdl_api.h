@@ -1,0 +1,53 @@
+// Host-callable entry points of the kubedl_amd HIP kernels (raw pointers,
+// explicit stream).  Implemented in csrc/*.hip, bound in csrc/bindings.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kdl {
+
+// ---- bn_act.hip (dtype codes: 0 = f32, 1 = bf16)
+int64_t bn_workspace_floats(int64_t M, int C, int dtype);
+hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* gamma,
+                          const void* beta, float* rm, float* rv, float* save_mean,
+                          float* save_invstd, float* ws, int64_t M, int C, int dtype, int pdtype,
+                          bool relu, bool training, float momentum, float eps, hipStream_t s);
+hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const void* gamma,
+                           const float* mean, const float* invstd, void* dx, void* dres,
+                           void* dgamma, void* dbeta, float* ws, int64_t M, int C, int dtype,
+                           int pdtype, bool relu, bool training, hipStream_t s);
+
+// ---- optim.hip
+struct OptChunk {
+  int64_t start;
+  int32_t len;
+  int32_t group;
+};
+
+struct OptHyper {
+  float lr;
+  float momentum;
+  float dampening;
+  float eps;
+  float bc1;
+  float bc2;
+  float grad_scale;
+  int nesterov;
+  int first_step;
+  int adam_w;
+  float wd[4];
+  float lr_scale[4];
+};
+
+hipError_t fused_sgd(const OptChunk* chunks, int nchunks, float* master, float* mom,
+                     const void* grad, void* param, int gdtype, int pdtype, const OptHyper& h,
+                     hipStream_t s);
+hipError_t fused_adam(const OptChunk* chunks, int nchunks, float* master, float* m1, float* m2,
+                      const void* grad, void* param, int gdtype, int pdtype, const OptHyper& h,
+                      hipStream_t s);
+hipError_t chunk_sumsq(const OptChunk* chunks, int nchunks, const void* x, int dtype, float scale,
+                       float* out, hipStream_t s);
+hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
+
+}  // namespace kdl

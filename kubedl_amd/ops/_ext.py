@@ -1,0 +1,44 @@
+"""Loader for the in-tree HIP extension ``kubedl_amd._C``.
+
+Policy: on a machine with a GPU the HIP kernels are the ONLY path for the ops
+they implement -- if the extension is missing we fail loudly instead of
+silently falling back to eager PyTorch (set ``KDL_ALLOW_TORCH_FALLBACK=1`` to
+opt out, e.g. for A/B benchmarking).  On CPU-only hosts the PyTorch
+compositions are the implementation (and the numerics reference).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_mod = None
+_err: Exception | None = None
+
+
+def load():
+    global _mod, _err
+    if _mod is not None:
+        return _mod
+    try:
+        _mod = importlib.import_module("kubedl_amd._C")
+        return _mod
+    except Exception as e:  # pragma: no cover - depends on build state
+        _err = e
+        raise RuntimeError(
+            "kubedl_amd HIP extension is not built: run `python -m kubedl_amd.ops.build` "
+            f"(import error: {e})") from e
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except RuntimeError:
+        return False
+
+
+def require_on_gpu(op: str) -> None:
+    if os.environ.get("KDL_ALLOW_TORCH_FALLBACK") == "1":
+        return
+    raise RuntimeError(f"{op}: GPU tensor but the kubedl_amd HIP extension is unavailable ({_err}); "
+                       "build it with `python -m kubedl_amd.ops.build`")

@@ -1,0 +1,121 @@
+"""In-tree build of the kubedl_amd HIP extension for gfx950.
+
+No hipify, no CUDA sources: ``csrc/*.hip`` are compiled by ``hipcc
+--offload-arch=gfx950`` and ``csrc/*.cpp`` (pybind11/torch bindings, native
+runtime helpers) as host C++; everything is linked into
+``kubedl_amd/_C.so`` next to the package so the ``.so`` travels with the repo
+snapshot to the GPU box.  Objects are cached by content hash (source + flags
++ included headers), so a rebuild after a one-file edit recompiles one file.
+
+Usage: ``python -m kubedl_amd.ops.build [-j N] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "kdl_ext"
+OUT = ROOT / "kubedl_amd" / "_C.so"
+ARCH = os.environ.get("KDL_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = ce.include_paths(device_type="cuda")
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _common_flags(abi: int):
+    return [
+        "-O3", "-std=c++17", "-fPIC",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-DUSE_ROCM=1",
+        "-Wno-unused-result", "-Wno-deprecated-declarations",
+    ]
+
+
+def _headers_digest() -> str:
+    h = hashlib.sha256()
+    for p in sorted(CSRC.glob("*.h")):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _compile(src: Path, flags, hdr_digest: str, force: bool) -> Path:
+    key = hashlib.sha256(src.read_bytes() + " ".join(flags).encode() + hdr_digest.encode()).hexdigest()[:16]
+    obj = BUILD / f"{src.stem}.{src.suffix[1:]}.{key}.o"
+    if obj.exists() and not force:
+        return obj
+    for old in BUILD.glob(f"{src.stem}.{src.suffix[1:]}.*.o"):
+        old.unlink()
+    cmd = [HIPCC] + flags + ["-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    inc, lib, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    common = _common_flags(abi)
+    hip_flags = common + [f"--offload-arch={ARCH}", "-x", "hip", f"-I{CSRC}",
+                          "-munsafe-fp-atomics"]
+    cpp_flags = common + [f"-I{CSRC}", f"-I{py_inc}"] + [f"-I{p}" for p in inc] + [
+        "-D__HIP_PLATFORM_AMD__=1", "-DHIPBLAS_V2", "-DTORCH_API_INCLUDE_EXTENSION_H",
+        "-DTORCH_EXTENSION_NAME=_C", "-Wno-ignored-attributes"]
+    hdr = _headers_digest()
+    srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        futs = {ex.submit(_compile, s, hip_flags if s.suffix == ".hip" else cpp_flags, hdr, force): s
+                for s in srcs}
+        objs = []
+        for f in cf.as_completed(futs):
+            objs.append(f.result())
+            if verbose:
+                print(f"[kdl-build] {futs[f].name}", flush=True)
+    objs.sort()
+    link_key = hashlib.sha256(" ".join(str(o) for o in objs).encode()).hexdigest()[:16]
+    stamp = BUILD / "link.stamp"
+    if OUT.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
+        return OUT
+    tmp = OUT.with_suffix(".so.tmp")
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + [str(o) for o in objs] + [
+        f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
+        f"-Wl,-rpath,{lib}", "-Wl,--no-as-needed"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, OUT)
+    stamp.write_text(link_key)
+    if verbose:
+        print(f"[kdl-build] linked {OUT}", flush=True)
+    return OUT
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.jobs)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,115 @@
+"""Data-parallel gradient synchronisation over RCCL/xGMI with backward overlap.
+
+Works on a ``FlatParamSpace``: gradients already live in one flat buffer laid
+out in (approximately) the order backward produces them, so a bucket is just
+a contiguous slice ``grad[lo:hi]``.  A post-accumulate-grad hook per
+parameter counts down its bucket; when a bucket is complete its all-reduce
+(SUM, averaging is folded into the fused optimizer's ``grad_scale``) is
+issued asynchronously, overlapping the rest of backward.  ``finish()`` waits
+for the outstanding collectives before the optimizer step.
+
+Bucket sizing for MI355X: 8 GPUs on point-to-point xGMI (7 links x ~153 GB/s
+per GPU) means a ring all-reduce of B bytes costs ~2(n-1)/n * B / link-bw plus
+a per-collective latency of tens of microseconds.  ResNet-50 has 51 MB of
+bf16 gradients; ~12 MB buckets give 4-5 collectives, enough to overlap all but
+the last (smallest, first-layer) bucket with backward while staying far above
+the latency-bound regime.  The first bucket is capped smaller so the first
+collective starts early.
+
+The reference has no collective code; this is the DP
+strategy a PyTorchJob's env (``MASTER_ADDR/PORT``, ``WORLD_SIZE``, ``RANK``)
+exists to enable.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from kubedl_amd.ops.optim import FlatParamSpace
+
+
+class Bucket:
+    __slots__ = ("lo", "hi", "slots", "pending", "handle")
+
+    def __init__(self, lo: int, hi: int, slots):
+        self.lo, self.hi, self.slots = lo, hi, slots
+        self.pending = len(slots)
+        self.handle = None
+
+
+class FlatDDP:
+    def __init__(self, space: FlatParamSpace, world_size: int, process_group=None,
+                 bucket_cap_mb: float = 12.0, first_bucket_mb: float = 2.0,
+                 broadcast_from: int | None = 0):
+        self.space = space
+        self.world = world_size
+        self.pg = process_group
+        self.buckets: list[Bucket] = []
+        self._hooks = []
+        if world_size > 1:
+            if broadcast_from is not None:
+                with torch.no_grad():
+                    dist.broadcast(space.param, broadcast_from, group=process_group)
+                    space.sync_master_from_params()
+            self._build_buckets(bucket_cap_mb, first_bucket_mb)
+            self._install_hooks()
+
+    def _build_buckets(self, cap_mb: float, first_mb: float) -> None:
+        esz = self.space.grad.element_size()
+        cur, lo = [], None
+        cap = first_mb * 2 ** 20
+        for s in self.space.slots:
+            if lo is None:
+                lo = s.offset
+            cur.append(s)
+            hi = s.offset + s.numel
+            if (hi - lo) * esz >= cap:
+                self.buckets.append(Bucket(lo, _end(self.space, s), cur))
+                cur, lo = [], None
+                cap = cap_mb * 2 ** 20
+        if cur:
+            self.buckets.append(Bucket(lo, _end(self.space, cur[-1]), cur))
+        self._slot_bucket = {}
+        for b in self.buckets:
+            for s in b.slots:
+                self._slot_bucket[id(s.param)] = b
+
+    def _install_hooks(self) -> None:
+        for b in self.buckets:
+            for s in b.slots:
+                self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p: torch.Tensor) -> None:
+        b = self._slot_bucket[id(p)]
+        b.pending -= 1
+        if b.pending == 0:
+            b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
+
+    def finish(self) -> None:
+        """Wait for every bucket (launching any whose params got no gradient)."""
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            if b.handle is None:
+                b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
+        for b in self.buckets:
+            b.handle.wait()
+            b.handle = None
+            b.pending = len(b.slots)
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+
+
+def _end(space: FlatParamSpace, s) -> int:
+    """Bucket end = start of the next slot's region (include the zero pad)."""
+    idx = space.slots.index(s)
+    if idx + 1 < len(space.slots):
+        return space.slots[idx + 1].offset
+    return space.numel

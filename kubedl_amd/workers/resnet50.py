@@ -1,0 +1,130 @@
+"""PyTorchJob worker: ResNet-50 data-parallel bf16 training on MI355X.
+
+Run by the PyTorch launcher (``kubedl_amd.controllers.pytorch``) as one
+process per rank with the KubeDL rendezvous env, or directly by ``bench.py``.
+
+Per step (all on the rank's HIP stream):
+  zero flat grad (one memset) -> forward (MIOpen NHWC convs + fused BN/ReLU
+  HIP kernels) -> fp32 cross-entropy -> backward (bucketed RCCL all-reduce of
+  bf16 gradient slices overlapped with backward) -> one fused SGD-momentum
+  launch (fp32 master, writes bf16 weights).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.nn.functional as F
+
+from kubedl_amd.models.resnet import resnet50, resnet_tiny
+from kubedl_amd.ops.optim import FlatParamSpace, FusedSGD
+from kubedl_amd.parallel import dist as kdist
+from kubedl_amd.parallel.ddp import FlatDDP
+from kubedl_amd.workers import common
+
+
+class ResNetTrainer:
+    def __init__(self, info: kdist.DistInfo, batch: int = 256, image: int = 224,
+                 num_classes: int = 1000, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
+                 momentum: float = 0.9, weight_decay: float = 5e-5, tiny: bool = False,
+                 bn_backend: str = "auto", bucket_cap_mb: float = 12.0, seed: int = 0):
+        self.info = info
+        dev = info.device
+        torch.manual_seed(seed)
+        model = resnet_tiny(num_classes) if tiny else resnet50(num_classes)
+        model.set_bn_backend(bn_backend)
+        model = model.to(dev)
+        if dev.type == "cuda":
+            model = model.to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            for p in model.parameters():
+                p.data = p.data.to(dtype)
+        self.model = model
+        self.dtype = dtype
+        self.space = FlatParamSpace(model, dtype=dtype, device=dev)
+        self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb)
+        self.opt = FusedSGD(self.space, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        self.opt.grad_scale = self.ddp.grad_scale
+        g = torch.Generator(device="cpu").manual_seed(seed + 1000 + info.rank)
+        x = torch.randn(batch, 3, image, image, generator=g).to(dev, dtype)
+        if dev.type == "cuda":
+            x = x.contiguous(memory_format=torch.channels_last)
+        self.x = x
+        self.y = torch.randint(0, num_classes, (batch,), generator=g).to(dev)
+        self.batch = batch
+        self.last_loss = None
+
+    def step(self) -> torch.Tensor:
+        self.space.zero_grad()
+        out = self.model(self.x)
+        loss = F.cross_entropy(out.float(), self.y)
+        loss.backward()
+        self.ddp.finish()
+        self.opt.step()
+        self.last_loss = loss.detach()
+        return self.last_loss
+
+
+def sync(info: kdist.DistInfo) -> None:
+    if info.device.type == "cuda":
+        torch.cuda.synchronize(info.device)
+
+
+def run(args) -> dict:
+    t_start = time.time()
+    info = kdist.init_from_env("cpu" if args.cpu else None)
+    common.signal_ready({"rank": info.rank})
+    tr = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
+                       bn_backend=args.bn_backend)
+    for i in range(args.warmup):
+        tr.step()
+        common.maybe_inject_fault(info.rank, i)
+    sync(info)
+    kdist.barrier(info)
+    sync(info)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tr.step()
+        common.maybe_inject_fault(info.rank, args.warmup + i)
+    sync(info)
+    kdist.barrier(info)
+    sync(info)
+    dt = time.perf_counter() - t0
+    dt = kdist.all_reduce_max(dt, info)
+    loss = float(tr.last_loss.item()) if tr.last_loss is not None else float("nan")
+    res = {
+        "rank": info.rank, "world_size": info.world_size, "steps": args.steps,
+        "seconds": dt, "ms_per_step": dt / max(args.steps, 1) * 1e3,
+        "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
+        "images_per_sec": args.steps * args.batch * info.world_size / dt if dt > 0 else 0.0,
+        "loss": loss, "startup_s": t0 - t_start if False else None,
+    }
+    common.report_progress(args.warmup + args.steps, res["steps_per_sec"], loss=loss)
+    return res
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="ResNet-50 DP bf16 trainer (PyTorchJob worker)")
+    ap.add_argument("--steps", type=int, default=int(os.environ.get("KDL_STEPS", 20)))
+    ap.add_argument("--warmup", type=int, default=int(os.environ.get("KDL_WARMUP", 5)))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("KDL_BATCH", 256)))
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests)")
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
+    return ap
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    res = run(args)
+    if res["rank"] == 0:
+        print(json.dumps(res), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,40 @@
+#!/bin/bash
+# GPU-box check run via gpurun: numerics tests, bench A/B, rocprofv3 kernel stats.
+# Every GPU step has its own timeout; a crash/timeout (exit >= 124 or signal)
+# ends the script so nothing else touches the GPU after a fault.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS="${STEPS:-all}"
+
+fatal() {  # $1 = exit code, $2 = step name
+  local rc=$1
+  if [ "$rc" -ge 124 ] || [ "$rc" -gt 128 ]; then
+    echo "[gpu_check] step '$2' ended with fatal code $rc; stopping" | tee -a gpurun_out/summary.txt
+    exit "$rc"
+  fi
+}
+
+run_step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "[gpu_check] >>> $name" | tee -a gpurun_out/summary.txt
+  local t0=$(date +%s)
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[gpu_check] <<< $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a gpurun_out/summary.txt
+  tail -n 5 "gpurun_out/$name.log"
+  fatal $rc "$name"
+  return 0
+}
+
+want() { [ "$STEPS" = "all" ] || [[ ",$STEPS," == *",$1,"* ]]; }
+
+python -c "import kubedl_amd._C" 2>/dev/null || python -m kubedl_amd.ops.build > gpurun_out/build.log 2>&1
+
+want smoke  && run_step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+want pytest && run_step pytest 900 python -m pytest tests -m gpu -x -q
+want bench  && run_step bench_hip 600 python bench.py --steps 20 --warmup 8
+want benchab && run_step bench_torch 600 python bench.py --steps 20 --warmup 8 --bn-backend torch
+want prof   && run_step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 3
+exit 0

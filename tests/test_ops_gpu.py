@@ -1,0 +1,160 @@
+"""Numerics of the HIP kernels vs plain PyTorch fp32 references (MI355X only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ext():
+    from kubedl_amd.ops import _ext
+    return _ext.load()
+
+
+def _ref_bn_act(x, w, b, rm, rv, res, relu, training, momentum=0.1, eps=1e-5):
+    y = F.batch_norm(x.double(), rm, rv, w.double(), b.double(), training=training,
+                     momentum=momentum, eps=eps)
+    if res is not None:
+        y = y + res.double()
+    if relu:
+        y = F.relu(y)
+    return y
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 14), (2, 256, 7, 7), (3, 24, 5, 5), (8, 2048, 7, 7),
+                                   (2, 3000, 2, 2)])
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_act_matches_reference(dtype, shape, relu, residual, training):
+    from kubedl_amd.ops.bn import batch_norm_act
+    torch.manual_seed(0)
+    dev = "cuda"
+    N, C, H, W = shape
+    x = (torch.randn(shape, device=dev) * 2 + 3).to(dtype).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=dev).to(dtype).contiguous(memory_format=torch.channels_last) if residual else None
+    w = (torch.rand(C, device=dev) + 0.5).to(dtype)
+    b = torch.randn(C, device=dev).to(dtype)
+    rm = torch.randn(C, device=dev)
+    rv = torch.rand(C, device=dev) + 0.5
+    rm_ref, rv_ref = rm.double().clone(), rv.double().clone()
+    x.requires_grad_(True)
+    w.requires_grad_(True)
+    b.requires_grad_(True)
+    if r is not None:
+        r.requires_grad_(True)
+    y = batch_norm_act(x, w, b, rm, rv, residual=r, relu=relu, training=training, backend="hip")
+    xr = x.detach().double().requires_grad_(True)
+    wr = w.detach().double().requires_grad_(True)
+    br = b.detach().double().requires_grad_(True)
+    rr = r.detach().double().requires_grad_(True) if r is not None else None
+    yr = _ref_bn_act(xr, wr, br, rm_ref, rv_ref, rr, relu, training)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.double(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(rm.double(), rm_ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(rv.double(), rv_ref, atol=1e-3, rtol=1e-3)
+    g = torch.randn_like(y, dtype=torch.float32).to(dtype)
+    y.backward(g)
+    yr.backward(g.double())
+    gtol = 5e-2 if dtype == torch.bfloat16 else 2e-3
+    torch.testing.assert_close(x.grad.double(), xr.grad, atol=gtol, rtol=gtol)
+    scale = max(1.0, float(wr.grad.abs().max()))
+    torch.testing.assert_close(w.grad.double() / scale, wr.grad / scale, atol=gtol, rtol=gtol)
+    scale = max(1.0, float(br.grad.abs().max()))
+    torch.testing.assert_close(b.grad.double() / scale, br.grad / scale, atol=gtol, rtol=gtol)
+    if r is not None:
+        torch.testing.assert_close(r.grad.double(), rr.grad, atol=gtol, rtol=gtol)
+
+
+def test_bn_large_mean_stability():
+    """Shifted-sum stats must survive |mean| >> std (no catastrophic cancellation)."""
+    from kubedl_amd.ops.bn import batch_norm_act
+    torch.manual_seed(1)
+    x = (torch.randn(64, 64, 28, 28, device="cuda") * 0.01 + 100.0).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.ones(64, device="cuda")
+    b = torch.zeros(64, device="cuda")
+    y = batch_norm_act(x, w, b, torch.zeros(64, device="cuda"), torch.ones(64, device="cuda"),
+                       relu=False, backend="hip")
+    yr = _ref_bn_act(x, w, b, None, None, None, False, True)
+    torch.testing.assert_close(y.double(), yr, atol=2e-3, rtol=2e-3)
+
+
+def _flat_case(dev, dtype):
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(37, 64), torch.nn.ReLU(), torch.nn.Linear(64, 10),
+                            torch.nn.BatchNorm1d(10)).to(dev)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.data = p.data.to(dtype)
+    return m
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_sgd_matches_cpu_path(nesterov, dtype):
+    from kubedl_amd.ops.optim import FlatParamSpace, FusedSGD
+    res = {}
+    for dev in ["cpu", "cuda"]:
+        m = _flat_case(dev, dtype)
+        sp = FlatParamSpace(m)
+        opt = FusedSGD(sp, lr=0.05, momentum=0.9, weight_decay=1e-3, nesterov=nesterov)
+        opt.grad_scale = 0.5
+        g = torch.Generator().manual_seed(3)
+        for _ in range(3):
+            sp.grad.copy_(torch.randn(sp.numel, generator=g).to(dtype))
+            opt.step()
+        res[dev] = sp.master.cpu()
+        assert sp.param.dtype == dtype
+    torch.testing.assert_close(res["cuda"], res["cpu"], atol=1e-5, rtol=1e-5)
+
+
+def test_fused_sgd_matches_torch_optim():
+    from kubedl_amd.ops.optim import FlatParamSpace, FusedSGD
+    torch.manual_seed(0)
+    m1 = torch.nn.Linear(64, 32).cuda()
+    m2 = torch.nn.Linear(64, 32).cuda()
+    m2.load_state_dict(m1.state_dict())
+    sp = FlatParamSpace(m1, no_decay=lambda n, p: False)
+    opt = FusedSGD(sp, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ref = torch.optim.SGD(m2.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    x = torch.randn(16, 64, device="cuda")
+    for _ in range(4):
+        opt.zero_grad()
+        m1(x).square().sum().backward()
+        opt.step()
+        ref.zero_grad()
+        m2(x).square().sum().backward()
+        ref.step()
+    torch.testing.assert_close(m1.weight, m2.weight, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m1.bias, m2.bias, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("adam_w", [True, False])
+def test_fused_adam_matches_torch_optim(adam_w):
+    from kubedl_amd.ops.optim import FlatParamSpace, FusedAdam
+    torch.manual_seed(0)
+    m1 = torch.nn.Linear(64, 32).cuda()
+    m2 = torch.nn.Linear(64, 32).cuda()
+    m2.load_state_dict(m1.state_dict())
+    sp = FlatParamSpace(m1, no_decay=lambda n, p: False)
+    opt = FusedAdam(sp, lr=1e-2, weight_decay=1e-2, adam_w=adam_w)
+    cls = torch.optim.AdamW if adam_w else torch.optim.Adam
+    ref = cls(m2.parameters(), lr=1e-2, weight_decay=1e-2)
+    x = torch.randn(16, 64, device="cuda")
+    for _ in range(5):
+        opt.zero_grad()
+        m1(x).square().sum().backward()
+        opt.step()
+        ref.zero_grad()
+        m2(x).square().sum().backward()
+        ref.step()
+    torch.testing.assert_close(m1.weight, m2.weight, atol=1e-5, rtol=1e-4)
+
+
+def test_extension_is_native():
+    ext = _ext()
+    assert ext.arch == "gfx950"
+    import kubedl_amd
+    assert ext.__file__.startswith(kubedl_amd.__path__[0])
