@@ -47,6 +47,8 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--conv-benchmark", type=int, default=0,
+                    help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")
     args = ap.parse_args(argv)
@@ -61,7 +63,7 @@ def main(argv=None) -> int:
               file=sys.stderr)
 
     trainer = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
-                            bn_backend=args.bn_backend)
+                            bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark))
     sync(info)
     kdist.barrier(info)
     launch_delay = kdist.all_reduce_max(time.time() - T_PROC_START, info)
@@ -107,6 +109,7 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{n}",
                 "optimizer": "fused SGD-momentum (fp32 master)",
                 "bn_backend": args.bn_backend,
+                "conv_benchmark": bool(args.conv_benchmark),
             },
             "steps_per_sec": round(args.steps / dt, 4),
             "launch_delay_s": round(launch_delay, 3),

@@ -7,7 +7,8 @@
 // hipGraph capture.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "kdl_api.h"
 
@@ -20,7 +21,7 @@ int dtype_code(const at::Tensor& t) {
   return -1;
 }
 
-hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 void check_hip(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "kubedl_amd: ", what, " failed: ", hipGetErrorString(e));
@@ -32,23 +33,37 @@ bool is_nhwc_dense(const at::Tensor& t) {
 }
 
 // ------------------------------------------------------------------ BN + act
+// ``acc``: optional [2C] (fwd) / [2C] (bwd) fp32 accumulator, zero on entry
+// (the trainer zeroes one arena per step); allocated zeroed here if absent.
+at::Tensor get_acc(const c10::optional<at::Tensor>& acc, int64_t C, const at::Tensor& like) {
+  if (acc.has_value() && acc->defined()) {
+    TORCH_CHECK(acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() >= 2 * C &&
+                    acc->device() == like.device(),
+                "bn: acc must be a contiguous fp32 tensor of >= 2C elements on x's device");
+    return *acc;
+  }
+  return at::zeros({2 * C}, like.options().dtype(at::kFloat));
+}
+
 std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight,
                                    const at::Tensor& bias, const at::Tensor& running_mean,
                                    const at::Tensor& running_var,
                                    const c10::optional<at::Tensor>& residual, bool relu,
-                                   bool training, double momentum, double eps) {
+                                   bool training, double momentum, double eps,
+                                   const c10::optional<at::Tensor>& acc) {
   TORCH_CHECK(x.is_cuda(), "bn_act_fwd: x must be on the GPU");
   TORCH_CHECK(x.dim() == 4 || x.dim() == 2, "bn_act_fwd: x must be NHWC 4-D or [M, C]");
   TORCH_CHECK(is_nhwc_dense(x), "bn_act_fwd: x must be channels_last-dense");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(weight.numel() == C && bias.numel() == C, "bn_act_fwd: affine size mismatch");
   TORCH_CHECK(weight.scalar_type() == bias.scalar_type(), "bn_act_fwd: weight/bias dtype mismatch");
   TORCH_CHECK(running_mean.scalar_type() == at::kFloat && running_var.scalar_type() == at::kFloat,
               "bn_act_fwd: running stats must be fp32");
+  TORCH_CHECK(running_mean.numel() == C && running_var.numel() == C, "bn_act_fwd: stats size");
   const at::Tensor* res = nullptr;
-  if (residual.has_value()) {
+  if (residual.has_value() && residual->defined()) {
     res = &residual.value();
     TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type() &&
                     is_nhwc_dense(*res),
@@ -58,12 +73,11 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
   auto fopt = x.options().dtype(at::kFloat);
   auto save_mean = at::empty({C}, fopt);
   auto save_invstd = at::empty({C}, fopt);
-  auto ws = at::empty({kdl::bn_workspace_floats(M, static_cast<int>(C), dtype_code(x))}, fopt);
+  at::Tensor a = get_acc(acc, C, x);
   check_hip(kdl::bn_act_forward(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(),
-                                weight.data_ptr(), bias.data_ptr(),
-                                training ? running_mean.data_ptr<float>() : running_mean.data_ptr<float>(),
+                                weight.data_ptr(), bias.data_ptr(), running_mean.data_ptr<float>(),
                                 running_var.data_ptr<float>(), save_mean.data_ptr<float>(),
-                                save_invstd.data_ptr<float>(), ws.data_ptr<float>(), M,
+                                save_invstd.data_ptr<float>(), a.data_ptr<float>(), M,
                                 static_cast<int>(C), dtype_code(x), dtype_code(weight), relu,
                                 training, static_cast<float>(momentum), static_cast<float>(eps),
                                 cur_stream()),
@@ -72,28 +86,31 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
 }
 
 std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& y,
-                                   const at::Tensor& weight, const at::Tensor& mean,
-                                   const at::Tensor& invstd, bool relu, bool has_residual,
-                                   bool training) {
+                                   const at::Tensor& weight, const at::Tensor& bias,
+                                   const at::Tensor& mean, const at::Tensor& invstd, bool relu,
+                                   bool has_residual, bool training,
+                                   const c10::optional<at::Tensor>& acc) {
   TORCH_CHECK(is_nhwc_dense(dy) && is_nhwc_dense(x) && is_nhwc_dense(y),
               "bn_act_bwd: tensors must be channels_last-dense");
   TORCH_CHECK(dy.sizes() == x.sizes() && y.sizes() == x.sizes(), "bn_act_bwd: shape mismatch");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "bn_act_bwd: dtype mismatch");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
+  TORCH_CHECK(weight.numel() == C && bias.numel() == C && mean.numel() == C && invstd.numel() == C,
+              "bn_act_bwd: per-channel tensor size mismatch");
   auto dx = at::empty_like(x);
   at::Tensor dres;
   if (has_residual) dres = at::empty_like(x);
   auto dgamma = at::empty_like(weight);
   auto dbeta = at::empty_like(weight);
-  auto fopt = x.options().dtype(at::kFloat);
-  auto ws = at::empty({kdl::bn_workspace_floats(M, static_cast<int>(C), dtype_code(x))}, fopt);
+  at::Tensor a = get_acc(acc, C, x);
   check_hip(kdl::bn_act_backward(dy.data_ptr(), y.data_ptr(), x.data_ptr(), weight.data_ptr(),
-                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), dx.data_ptr(),
-                                 has_residual ? dres.data_ptr() : nullptr, dgamma.data_ptr(),
-                                 dbeta.data_ptr(), ws.data_ptr<float>(), M, static_cast<int>(C),
-                                 dtype_code(x), dtype_code(weight), relu, training, cur_stream()),
+                                 bias.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                 dx.data_ptr(), has_residual ? dres.data_ptr() : nullptr,
+                                 dgamma.data_ptr(), dbeta.data_ptr(), a.data_ptr<float>(), M,
+                                 static_cast<int>(C), dtype_code(x), dtype_code(weight), relu,
+                                 training, cur_stream()),
             "bn_act_backward");
   return {dx, dgamma, dbeta, has_residual ? dres : at::Tensor()};
 }
@@ -138,7 +155,7 @@ void sgd_step(const at::Tensor& chunks, at::Tensor master, at::Tensor mom, const
   TORCH_CHECK(master.numel() == grad.numel() && grad.numel() == param.numel() &&
                   mom.numel() == master.numel(),
               "sgd_step: flat buffer size mismatch");
-  const c10::hip::HIPGuard guard(master.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(master.device());
   auto h = make_hyper(lr, momentum, dampening, 0, 1, 1, grad_scale, nesterov, first_step, false, wd,
                       lr_scale);
   check_hip(kdl::fused_sgd(reinterpret_cast<const kdl::OptChunk*>(chunks.data_ptr<int64_t>()),
@@ -156,7 +173,7 @@ void adam_step(const at::Tensor& chunks, at::Tensor master, at::Tensor m1, at::T
   TORCH_CHECK(master.numel() == grad.numel() && grad.numel() == param.numel() &&
                   m1.numel() == master.numel() && m2.numel() == master.numel(),
               "adam_step: flat buffer size mismatch");
-  const c10::hip::HIPGuard guard(master.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(master.device());
   const double bc1 = 1.0 - std::pow(beta1, static_cast<double>(step));
   const double bc2 = 1.0 - std::pow(beta2, static_cast<double>(step));
   auto h = make_hyper(lr, beta1, beta2, eps, bc1, bc2, grad_scale, false, false, adam_w, wd, lr_scale);
@@ -169,7 +186,7 @@ void adam_step(const at::Tensor& chunks, at::Tensor master, at::Tensor m1, at::T
 
 at::Tensor chunk_sumsq(const at::Tensor& chunks, const at::Tensor& x, double scale) {
   check_chunks(chunks);
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto out = at::empty({chunks.size(0)}, x.options().dtype(at::kFloat));
   check_hip(kdl::chunk_sumsq(reinterpret_cast<const kdl::OptChunk*>(chunks.data_ptr<int64_t>()),
                              static_cast<int>(chunks.size(0)), x.data_ptr(), dtype_code(x),
@@ -182,10 +199,27 @@ void cast_copy(const at::Tensor& src, at::Tensor dst) {
   TORCH_CHECK(src.numel() == dst.numel() && src.is_contiguous() && dst.is_contiguous(),
               "cast_copy: size/contiguity mismatch");
   TORCH_CHECK(src.numel() % 8 == 0, "cast_copy: numel must be a multiple of 8");
-  const c10::hip::HIPGuard guard(src.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
   check_hip(kdl::cast_copy(src.data_ptr(), dtype_code(src), dst.data_ptr(), dtype_code(dst),
                            src.numel(), cur_stream()),
             "cast_copy");
+}
+
+// ------------------------------------------------------------------ multi-tensor pack
+void pack_grads(const at::Tensor& chunks, const at::Tensor& src_ptrs, at::Tensor dst, double scale) {
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong && chunks.dim() == 2 &&
+                  chunks.size(1) == 3 && chunks.is_contiguous(),
+              "pack_grads: chunk table must be a contiguous int64 [n, 3] GPU tensor");
+  TORCH_CHECK(src_ptrs.is_cuda() && src_ptrs.scalar_type() == at::kLong && src_ptrs.is_contiguous(),
+              "pack_grads: src_ptrs must be a contiguous int64 GPU tensor");
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "pack_grads: dst must be contiguous on GPU");
+  static_assert(sizeof(kdl::PackChunk) == 24, "PackChunk layout");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  check_hip(kdl::pack_tensors(reinterpret_cast<const kdl::PackChunk*>(chunks.data_ptr<int64_t>()),
+                              static_cast<int>(chunks.size(0)), src_ptrs.data_ptr<int64_t>(),
+                              dst.data_ptr(), dtype_code(dst), static_cast<float>(scale),
+                              cur_stream()),
+            "pack_tensors");
 }
 
 }  // namespace
@@ -198,5 +232,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights");
   m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");
   m.def("cast_copy", &cast_copy, "flat dtype-casting copy");
+  m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
   m.attr("arch") = "gfx950";
 }

@@ -8,15 +8,16 @@
 namespace kdl {
 
 // ---- bn_act.hip (dtype codes: 0 = f32, 1 = bf16)
-int64_t bn_workspace_floats(int64_t M, int C, int dtype);
+// ``acc`` is a [2, C] fp32 accumulator that must be zero on entry.
+int64_t bn_acc_floats(int C);
 hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* gamma,
                           const void* beta, float* rm, float* rv, float* save_mean,
-                          float* save_invstd, float* ws, int64_t M, int C, int dtype, int pdtype,
+                          float* save_invstd, float* acc, int64_t M, int C, int dtype, int pdtype,
                           bool relu, bool training, float momentum, float eps, hipStream_t s);
 hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const void* gamma,
-                           const float* mean, const float* invstd, void* dx, void* dres,
-                           void* dgamma, void* dbeta, float* ws, int64_t M, int C, int dtype,
-                           int pdtype, bool relu, bool training, hipStream_t s);
+                           const void* beta, const float* mean, const float* invstd, void* dx,
+                           void* dres, void* dgamma, void* dbeta, float* acc, int64_t M, int C,
+                           int dtype, int pdtype, bool relu, bool training, hipStream_t s);
 
 // ---- optim.hip
 struct OptChunk {
@@ -48,6 +49,16 @@ hipError_t fused_adam(const OptChunk* chunks, int nchunks, float* master, float*
                       hipStream_t s);
 hipError_t chunk_sumsq(const OptChunk* chunks, int nchunks, const void* x, int dtype, float scale,
                        float* out, hipStream_t s);
+// ---- multi_tensor.hip
+struct PackChunk {
+  int32_t tensor;  // index into the per-step source pointer table
+  int32_t len;     // elements
+  int64_t src_off; // element offset inside the source tensor
+  int64_t dst_off; // element offset inside the flat destination
+};
+hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
+                        int dtype, float scale, hipStream_t s);
+
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 
 }  // namespace kdl

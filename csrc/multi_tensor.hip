@@ -1,0 +1,85 @@
+// Multi-tensor gradient pack: N autograd-owned gradient tensors -> one flat
+// (bucket) buffer in ONE launch (gfx950).
+//
+// Why: letting autograd accumulate into pre-existing ``.grad`` views of the
+// flat buffer costs one read-add-write elementwise launch per parameter
+// (rocprofv3: 177 ``CUDAFunctor_add`` launches, 2.1 ms of a 41 ms ResNet-50
+// step -- profiles/).  Instead ``.grad`` starts as None, autograd hands over
+// its freshly computed gradient tensors, and this kernel gathers them into
+// the flat buffer that the all-reduce buckets and the fused optimizer use:
+// ~51 MB of bf16 moved once at HBM rate.
+//
+// Work decomposition: a static chunk table (tensor index, offset in tensor,
+// length, destination offset) built once on the host; per step only the
+// per-tensor source pointer table changes (161 x 8 bytes for ResNet-50).  A
+// null source pointer writes zeros (parameters that received no gradient).
+// 16-byte vector loads/stores whenever source and destination are aligned.
+#include "common.h"
+#include "kdl_api.h"
+
+namespace kdl {
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_kernel(const PackChunk* __restrict__ chunks,
+                                                   const int64_t* __restrict__ src_ptrs,
+                                                   T* __restrict__ dst, float scale) {
+  const PackChunk c = chunks[blockIdx.x];
+  const T* src = reinterpret_cast<const T*>(src_ptrs[c.tensor]);
+  T* d = dst + c.dst_off;
+  constexpr int VEC = 16 / sizeof(T);
+  if (src == nullptr) {
+    for (int i = threadIdx.x * VEC; i < c.len; i += 256 * VEC) {
+      if (i + VEC <= c.len) {
+        *reinterpret_cast<uint4*>(d + i) = make_uint4(0, 0, 0, 0);
+      } else {
+        for (int k = i; k < c.len; ++k) d[k] = T(0);
+      }
+    }
+    return;
+  }
+  const T* s = src + c.src_off;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
+  if (aligned && scale == 1.f) {
+    for (int i = threadIdx.x * VEC; i < c.len; i += 256 * VEC) {
+      if (i + VEC <= c.len) {
+        *reinterpret_cast<uint4*>(d + i) = *reinterpret_cast<const uint4*>(s + i);
+      } else {
+        for (int k = i; k < c.len; ++k) d[k] = s[k];
+      }
+    }
+  } else if (aligned) {
+    for (int i = threadIdx.x * VEC; i < c.len; i += 256 * VEC) {
+      if (i + VEC <= c.len) {
+        float v[VEC];
+        VecIO<T, VEC>::load(s + i, v);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[k] *= scale;
+        VecIO<T, VEC>::store(d + i, v);
+      } else {
+        for (int k = i; k < c.len; ++k) {
+          float v[1] = {Vec1<T>::ld(s + k) * scale};
+          Vec1<T>::st(d + k, v[0]);
+        }
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < c.len; i += 256) Vec1<T>::st(d + i, Vec1<T>::ld(s + i) * scale);
+  }
+}
+
+}  // namespace
+
+hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
+                        int dtype, float scale, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  if (dtype == 1)
+    hipLaunchKernelGGL((pack_kernel<bf16_t>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs,
+                       static_cast<bf16_t*>(dst), scale);
+  else
+    hipLaunchKernelGGL((pack_kernel<float>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs,
+                       static_cast<float*>(dst), scale);
+  return hipGetLastError();
+}
+
+}  // namespace kdl

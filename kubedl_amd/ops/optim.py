@@ -46,10 +46,83 @@ def default_no_decay(name: str, p: torch.Tensor) -> bool:
     return p.dim() <= 1
 
 
+class _PinnedRing:
+    """Ring of pinned host int64 buffers for small per-step H2D uploads.
+
+    The host may run a full step ahead of the GPU, so a pinned buffer is only
+    rewritten after the event recorded behind its previous copy has fired.
+    """
+
+    def __init__(self, n: int, device, depth: int = 8):
+        self.bufs = [torch.zeros(n, dtype=torch.int64).pin_memory() for _ in range(depth)]
+        self.dev = torch.zeros(n, dtype=torch.int64, device=device)
+        self.devs = [torch.zeros(n, dtype=torch.int64, device=device) for _ in range(depth)]
+        self.events = [None] * depth
+        self.i = 0
+
+    def upload(self, values) -> torch.Tensor:
+        k = self.i
+        self.i = (self.i + 1) % len(self.bufs)
+        ev = self.events[k]
+        if ev is not None:
+            ev.synchronize()
+        hb = self.bufs[k]
+        hb.numpy()[:] = values
+        db = self.devs[k]
+        db.copy_(hb, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return db
+
+
+class GradPacker:
+    """Gathers the autograd-owned ``.grad`` tensors of ``slots`` into the flat
+    gradient buffer with one ``_C.pack_grads`` launch (csrc/multi_tensor.hip)."""
+
+    def __init__(self, space: "FlatParamSpace", slots):
+        self.space = space
+        self.slots = list(slots)
+        rows = []
+        for i, s in enumerate(self.slots):
+            for st in range(0, s.numel, CHUNK):
+                ln = min(CHUNK, s.numel - st)
+                rows.append((i | (ln << 32), st, s.offset + st))
+        self.nchunks = len(rows)
+        self.chunks = torch.tensor(rows, dtype=torch.int64, device=space.device)
+        self.ring = _PinnedRing(max(len(self.slots), 1), space.device) \
+            if space.device.type == "cuda" else None
+
+    def pack(self, scale: float = 1.0) -> None:
+        sp = self.space
+        if sp.device.type != "cuda":
+            with torch.no_grad():
+                for s in self.slots:
+                    dst = sp._view(sp.grad, s)
+                    if s.param.grad is None:
+                        dst.zero_()
+                    else:
+                        dst.copy_(s.param.grad * scale if scale != 1.0 else s.param.grad)
+            return
+        ptrs = []
+        for s in self.slots:
+            g = s.param.grad
+            if g is None:
+                ptrs.append(0)
+                continue
+            if g.dtype != sp.grad.dtype or g.stride() != s.param.stride() or g.device != sp.device:
+                g = torch.empty_strided(s.param.shape, s.param.stride(), dtype=sp.grad.dtype,
+                                        device=sp.device).copy_(g)
+                s.param.grad = g
+            ptrs.append(g.data_ptr())
+        src = self.ring.upload(ptrs)
+        _ext.load().pack_grads(self.chunks, src, sp.grad, float(scale))
+
+
 class FlatParamSpace:
     def __init__(self, module: torch.nn.Module, dtype: torch.dtype | None = None,
                  device: torch.device | None = None, no_decay=default_no_decay,
-                 reverse: bool = True):
+                 reverse: bool = True, grad_mode: str = "auto"):
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         if not named:
             raise ValueError("module has no trainable parameters")
@@ -68,12 +141,20 @@ class FlatParamSpace:
         self.numel = off
         self.param = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        # "pack": autograd owns .grad (no pre-set views => no per-parameter
+        # accumulate-add launches); gradients are gathered into ``grad`` by one
+        # multi-tensor launch.  "view": .grad are views of ``grad`` (CPU path).
+        if grad_mode == "auto":
+            grad_mode = "pack" if (self.device.type == "cuda" and _ext.available()) else "view"
+        self.grad_mode = grad_mode
+        self._gen = 0
+        self._packed_gen = -1
         with torch.no_grad():
             for s in self.slots:
                 view = self._view(self.param, s)
                 view.copy_(s.param.data)
                 s.param.data = view
-                s.param.grad = self._view(self.grad, s)
+                s.param.grad = self._view(self.grad, s) if grad_mode == "view" else None
         self.master = self.param.float()
         self.chunks_cpu = self._chunk_table()
         self.chunks = self.chunks_cpu.to(self.device) if self.device.type == "cuda" else self.chunks_cpu
@@ -92,7 +173,35 @@ class FlatParamSpace:
         return torch.tensor(rows, dtype=torch.int64)
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        self._gen += 1
+        if self.grad_mode == "pack":
+            for s in self.slots:
+                s.param.grad = None
+        else:
+            self.grad.zero_()
+
+    def packer(self, slots=None) -> GradPacker:
+        return GradPacker(self, self.slots if slots is None else slots)
+
+    def pack_grads(self) -> None:
+        """Make ``grad`` hold this step's gradients (no-op in view mode or when
+        already packed since the last ``zero_grad``, e.g. by the DP buckets).
+
+        If no parameter holds a ``.grad`` the flat buffer is assumed to have
+        been written directly and is left alone.  Parameters without a
+        gradient contribute zeros (the fused update still applies weight decay
+        and momentum to them, unlike ``torch.optim`` which skips them)."""
+        if self.grad_mode != "pack" or self._packed_gen == self._gen:
+            return
+        if all(s.param.grad is None for s in self.slots):
+            return
+        if getattr(self, "_packer", None) is None:
+            self._packer = self.packer()
+        self._packer.pack()
+        self._packed_gen = self._gen
+
+    def mark_packed(self) -> None:
+        self._packed_gen = self._gen
 
     def reattach_grads(self) -> None:
         """Re-point ``.grad`` at the flat buffer (after user code set it to None)."""
@@ -166,6 +275,7 @@ class FusedSGD(_FusedBase):
     @torch.no_grad()
     def step(self) -> None:
         sp = self.space
+        sp.pack_grads()
         first = self.step_count == 0
         if self._use_hip():
             _ext.load().sgd_step(sp.chunks, sp.master, self.mom, sp.grad, sp.param, float(self.lr),
@@ -200,6 +310,7 @@ class FusedAdam(_FusedBase):
     @torch.no_grad()
     def step(self) -> None:
         sp = self.space
+        sp.pack_grads()
         self.step_count += 1
         b1, b2 = self.betas
         if self._use_hip():

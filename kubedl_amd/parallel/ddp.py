@@ -29,12 +29,13 @@ from kubedl_amd.ops.optim import FlatParamSpace
 
 
 class Bucket:
-    __slots__ = ("lo", "hi", "slots", "pending", "handle")
+    __slots__ = ("lo", "hi", "slots", "pending", "handle", "packer")
 
     def __init__(self, lo: int, hi: int, slots):
         self.lo, self.hi, self.slots = lo, hi, slots
         self.pending = len(slots)
         self.handle = None
+        self.packer = None
 
 
 class FlatDDP:
@@ -69,6 +70,9 @@ class FlatDDP:
                 cap = cap_mb * 2 ** 20
         if cur:
             self.buckets.append(Bucket(lo, _end(self.space, cur[-1]), cur))
+        if self.space.grad_mode == "pack":
+            for b in self.buckets:
+                b.packer = self.space.packer(b.slots)
         self._slot_bucket = {}
         for b in self.buckets:
             for s in b.slots:
@@ -79,23 +83,31 @@ class FlatDDP:
             for s in b.slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_grad))
 
+    def _launch(self, b: Bucket) -> None:
+        if b.packer is not None:
+            b.packer.pack()
+            for s in b.slots:  # gradients now live in the bucket: free autograd's copies
+                s.param.grad = None
+        b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
+
     def _on_grad(self, p: torch.Tensor) -> None:
         b = self._slot_bucket[id(p)]
         b.pending -= 1
         if b.pending == 0:
-            b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
+            self._launch(b)
 
     def finish(self) -> None:
         """Wait for every bucket (launching any whose params got no gradient)."""
         if self.world == 1:
-            return
+            return  # the optimizer packs (FlatParamSpace.pack_grads)
         for b in self.buckets:
             if b.handle is None:
-                b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
+                self._launch(b)
         for b in self.buckets:
             b.handle.wait()
             b.handle = None
             b.pending = len(b.slots)
+        self.space.mark_packed()
 
     @property
     def grad_scale(self) -> float:

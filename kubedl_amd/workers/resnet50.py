@@ -30,9 +30,13 @@ class ResNetTrainer:
     def __init__(self, info: kdist.DistInfo, batch: int = 256, image: int = 224,
                  num_classes: int = 1000, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 5e-5, tiny: bool = False,
-                 bn_backend: str = "auto", bucket_cap_mb: float = 12.0, seed: int = 0):
+                 bn_backend: str = "auto", bucket_cap_mb: float = 12.0, seed: int = 0,
+                 conv_benchmark: bool = False):
         self.info = info
         dev = info.device
+        if dev.type == "cuda":
+            # MIOpen find (benchmark) vs immediate-mode heuristics: A/B'd in profiles/
+            torch.backends.cudnn.benchmark = bool(conv_benchmark)
         torch.manual_seed(seed)
         model = resnet_tiny(num_classes) if tiny else resnet50(num_classes)
         model.set_bn_backend(bn_backend)
@@ -43,6 +47,7 @@ class ResNetTrainer:
             for p in model.parameters():
                 p.data = p.data.to(dtype)
         self.model = model
+        self.arena = model.enable_bn_arena() if dev.type == "cuda" else None
         self.dtype = dtype
         self.space = FlatParamSpace(model, dtype=dtype, device=dev)
         self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb)
@@ -59,6 +64,8 @@ class ResNetTrainer:
 
     def step(self) -> torch.Tensor:
         self.space.zero_grad()
+        if self.arena is not None:
+            self.arena.zero_(self.info.device)
         out = self.model(self.x)
         loss = F.cross_entropy(out.float(), self.y)
         loss.backward()
