@@ -29,6 +29,13 @@ import time
 
 T_PROC_START = time.time()
 
+# MIOpen find-db / kernel cache shipped in-tree (populated on an MI355X by
+# scripts/gpu_check.sh): conv algorithm search and kernel compiles are not
+# repeated on every fresh box.
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db", "user"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_ROOT, "miopen_db", "cache"))
+
 import torch  # noqa: E402
 
 from kubedl_amd.parallel import dist as kdist  # noqa: E402
@@ -47,7 +54,7 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--conv-benchmark", type=int, default=0,
+    ap.add_argument("--conv-benchmark", type=int, default=1,
                     help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")

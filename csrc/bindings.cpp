@@ -33,17 +33,22 @@ bool is_nhwc_dense(const at::Tensor& t) {
 }
 
 // ------------------------------------------------------------------ BN + act
-// ``acc``: optional [2C] (fwd) / [2C] (bwd) fp32 accumulator, zero on entry
-// (the trainer zeroes one arena per step); allocated zeroed here if absent.
+// ``ws``: optional per-layer fp32 workspace (bn_workspace_floats(C) elements,
+// zero-initialised once by its owner and kept zero by the kernels); a fresh
+// zeroed one is allocated here if absent.
 at::Tensor get_acc(const c10::optional<at::Tensor>& acc, int64_t C, const at::Tensor& like) {
+  const int64_t n = kdl::bn_workspace_floats(static_cast<int>(C));
   if (acc.has_value() && acc->defined()) {
-    TORCH_CHECK(acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() >= 2 * C &&
+    TORCH_CHECK(acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() >= n &&
                     acc->device() == like.device(),
-                "bn: acc must be a contiguous fp32 tensor of >= 2C elements on x's device");
+                "bn: workspace must be a contiguous fp32 tensor of >= bn_workspace_floats(C) "
+                "elements on x's device");
     return *acc;
   }
-  return at::zeros({2 * C}, like.options().dtype(at::kFloat));
+  return at::zeros({n}, like.options().dtype(at::kFloat));
 }
+
+int64_t bn_ws_floats(int64_t C) { return kdl::bn_workspace_floats(static_cast<int>(C)); }
 
 std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight,
                                    const at::Tensor& bias, const at::Tensor& running_mean,
@@ -228,6 +233,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC");
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC");
+  m.def("bn_workspace_floats", &bn_ws_floats, "per-layer BN workspace size (fp32 elements)");
   m.def("sgd_step", &sgd_step, "flat chunked fused SGD-momentum with fp32 master weights");
   m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights");
   m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");

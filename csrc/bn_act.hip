@@ -6,33 +6,37 @@
 // loads are 16-byte vectors along the contiguous C axis and a lane's
 // channels (hence its per-channel coefficients) never change.
 //
-// Two kernels per direction, no separate finalize launch:
+// Three kernels per direction, no host-side memsets:
 //
-//   forward  (training): stats  -- per-block shifted sums  sum(x-K), sum((x-K)^2)
-//                                  (K = x[0,c], one global shift per channel, so
-//                                  |mean| >> std does not cancel) folded into a
-//                                  [2, C] fp32 accumulator with agent-scope
-//                                  float atomics (one add per channel per block);
-//                        apply  -- every lane finalises mean/invstd for its own
-//                                  VEC channels from the accumulator (a few
-//                                  flops), y = act(x*scale + shift [+ r]); block
-//                                  x == 0 publishes save_mean / save_invstd and
-//                                  the running-stat update.
-//   backward:            reduce -- sum(dz), sum(dz*(x-mean)) into a [2, C]
-//                                  accumulator; the ReLU mask comes from the
-//                                  saved output y when there is a residual, and
-//                                  is recomputed from x (x*scale+shift > 0, the
-//                                  same fp32 expression as forward) when there is
-//                                  not, which saves one activation read per pass;
-//                        apply  -- per-lane coefficients, dx = k*dz + c1*x + c0,
-//                                  d(residual) = dz; block x == 0 writes dgamma /
-//                                  dbeta.
+//   forward  (training): stats    -- per-block shifted sums  sum(x-K), sum((x-K)^2)
+//                                    (K = x[0,c], one global shift per channel, so
+//                                    |mean| >> std does not cancel), folded in LDS
+//                                    and added with no-return fp32 atomics into one
+//                                    of kReplicas copies of a [2, C] accumulator
+//                                    (block b -> replica b % kReplicas: every
+//                                    address sees P/kReplicas adds, not P --
+//                                    MI355X_MICROARCH.md "Global float atomics":
+//                                    all blocks on ONE row is 14x slower);
+//                        finalize -- one thread per channel sums the replicas,
+//                                    writes scale/shift, save_mean/invstd, the
+//                                    running-stat update, and re-zeroes the
+//                                    replicas (the workspace is self-cleaning);
+//                        apply    -- y = act(x*scale + shift [+ r]).
+//   backward:            reduce   -- sum(dz), sum(dz*(x-mean)) the same way; the
+//                                    ReLU mask comes from the saved output y when
+//                                    there is a residual and is recomputed from x
+//                                    (x*scale+shift > 0, the forward's fp32
+//                                    expression) when there is not, which saves
+//                                    one activation read per pass;
+//                        finalize -- dgamma/dbeta + the affine dx coefficients;
+//                        apply    -- dx = k*dz + c1*x + c0, d(residual) = dz.
 //
-// The accumulators must be zero on entry (the caller zeroes one arena per
-// training step, or passes a fresh zeroed buffer).  The previous version of
-// this file used a partial-sum buffer + a serial finalize kernel, which
-// rocprofv3 showed at 65-73 us per launch (a single block looping over 1024
-// partials for C = 64): 7.3 ms of a 41 ms ResNet-50 step (profiles/).
+// Workspace per BN layer (fp32, zero on first use, kept zero by finalize):
+//   [kReplicas][2C] forward accumulators | [kReplicas][2C] backward | [4C] coefs.
+// History (profiles/): v0 wrote [P][C] partials and finalised them with a
+// single-block serial loop (65-73 us per launch, 7.3 ms/step); v1 put all P
+// blocks' atomics on one [2C] row (165 us per stats launch: same-address
+// atomics serialise at the memory side).
 //
 // The reference has no kernels; this is the data-plane op
 // the PyTorchJob ResNet-50 worker spends most of its non-conv time in.
@@ -43,6 +47,7 @@ namespace kdl {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kReplicas = 32;
 
 template <typename PT> __device__ __forceinline__ float ldp(const PT* p, int i);
 template <> __device__ __forceinline__ float ldp<float>(const float* p, int i) { return p[i]; }
@@ -64,14 +69,23 @@ __host__ Tiling make_tiling(int C, int VEC) {
   return t;
 }
 
+// workspace views
+__host__ __device__ __forceinline__ float* ws_acc_fwd(float* ws, int C) { return ws; }
+__host__ __device__ __forceinline__ float* ws_acc_bwd(float* ws, int C) {
+  return ws + static_cast<int64_t>(kReplicas) * 2 * C;
+}
+__host__ __device__ __forceinline__ float* ws_coef(float* ws, int C) {
+  return ws + static_cast<int64_t>(kReplicas) * 4 * C;
+}
+
 __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
-  // no-return float atomic, executed at the memory side (MI355X_MICROARCH.md
-  // "Global float atomics"): one per channel per block, never contended hard.
+  // no-return fp32 atomic (global_atomic_add_f32 with -munsafe-fp-atomics),
+  // executed at the memory side.
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Block-level fold of per-lane VEC-wide sums over the RPI row groups, then one
-// atomic per channel from the r0 == 0 lanes.
+// atomic per channel (and per sum) from the r0 == 0 lanes into the block's replica.
 template <int VEC>
 __device__ __forceinline__ void block_fold_atomic(float (&a)[VEC], float (&b)[VEC], float* sh,
                                                   int t, int lc, int r0, int TPR, int RPI,
@@ -139,77 +153,79 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(
       }
     }
   }
-  block_fold_atomic<VEC>(s1, s2, sh, t, lc, r0, TPR, RPI, active && rb < re, acc + c0, acc + C + c0);
+  float* rep = acc + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
+  block_fold_atomic<VEC>(s1, s2, sh, t, lc, r0, TPR, RPI, active && rb < re, rep + c0, rep + C + c0);
 }
 
-// Per-lane finalize of the forward statistics for channels c0..c0+VEC.
-template <typename T, typename PT, int VEC>
-__device__ __forceinline__ void fwd_coeffs(const T* __restrict__ x, const float* __restrict__ acc,
-                                           const PT* __restrict__ gamma, const PT* __restrict__ beta,
-                                           const float* __restrict__ rm, const float* __restrict__ rv,
-                                           bool training, float Mf, float eps, int C, int c0,
-                                           float (&sc)[VEC], float (&sf)[VEC],
-                                           float (&mean)[VEC], float (&invstd)[VEC],
-                                           float (&var)[VEC]) {
-  if (training) {
-    float K[VEC];
-    VecIO<T, VEC>::load(x + c0, K);
-    const float inv_m = 1.f / Mf;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      const float m1 = acc[c0 + i] * inv_m;  // E[x - K]
-      float v = acc[C + c0 + i] * inv_m - m1 * m1;
-      v = v > 0.f ? v : 0.f;
-      mean[i] = K[i] + m1;
-      var[i] = v;
-      invstd[i] = rsqrtf(v + eps);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      mean[i] = rm[c0 + i];
-      var[i] = rv[c0 + i];
-      invstd[i] = rsqrtf(rv[c0 + i] + eps);
-    }
+// ---------------------------------------------------------------- forward finalize
+// One thread per channel: sum the replicas, re-zero them, publish coefficients.
+template <typename T, typename PT>
+__global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
+    const T* __restrict__ x, float* __restrict__ acc, int C, float Mf, const PT* __restrict__ gamma,
+    const PT* __restrict__ beta, float* __restrict__ rm, float* __restrict__ rv, float momentum,
+    float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+    float* __restrict__ coef) {
+  const int ch = blockIdx.x * kBlock + threadIdx.x;
+  if (ch >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+  for (int r = 0; r < kReplicas; ++r) {
+    float* row = acc + static_cast<int64_t>(r) * 2 * C;
+    s1 += row[ch];
+    s2 += row[C + ch];
+    row[ch] = 0.f;
+    row[C + ch] = 0.f;
   }
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    const float g = gamma ? ldp<PT>(gamma, c0 + i) : 1.f;
-    const float b = beta ? ldp<PT>(beta, c0 + i) : 0.f;
-    sc[i] = g * invstd[i];
-    sf[i] = b - mean[i] * sc[i];
+  const float K = Vec1<T>::ld(x + ch);
+  const float inv_m = 1.f / Mf;
+  const float m1 = s1 * inv_m;
+  float var = s2 * inv_m - m1 * m1;
+  var = var > 0.f ? var : 0.f;
+  const float mean = K + m1;
+  const float invstd = rsqrtf(var + eps);
+  save_mean[ch] = mean;
+  save_invstd[ch] = invstd;
+  if (rm != nullptr) {
+    const float unbiased = Mf > 1.f ? var * Mf / (Mf - 1.f) : var;
+    rm[ch] = (1.f - momentum) * rm[ch] + momentum * mean;
+    rv[ch] = (1.f - momentum) * rv[ch] + momentum * unbiased;
   }
+  const float g = gamma ? ldp<PT>(gamma, ch) : 1.f;
+  const float b = beta ? ldp<PT>(beta, ch) : 0.f;
+  const float sc = g * invstd;
+  coef[ch] = sc;
+  coef[C + ch] = b - mean * sc;
+}
+
+template <typename PT>
+__global__ void bn_eval_prep_kernel(int C, const PT* __restrict__ gamma, const PT* __restrict__ beta,
+                                    const float* __restrict__ rm, const float* __restrict__ rv,
+                                    float eps, float* __restrict__ save_mean,
+                                    float* __restrict__ save_invstd, float* __restrict__ coef) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= C) return;
+  const float invstd = rsqrtf(rv[ch] + eps);
+  const float g = gamma ? ldp<PT>(gamma, ch) : 1.f;
+  const float b = beta ? ldp<PT>(beta, ch) : 0.f;
+  save_mean[ch] = rm[ch];
+  save_invstd[ch] = invstd;
+  coef[ch] = g * invstd;
+  coef[C + ch] = b - rm[ch] * g * invstd;
 }
 
 // ---------------------------------------------------------------- forward apply
-template <typename T, typename PT, int VEC, bool RELU, bool RES>
+template <typename T, int VEC, bool RELU, bool RES>
 __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
-    const float* __restrict__ acc, const PT* __restrict__ gamma, const PT* __restrict__ beta,
-    float* __restrict__ rm, float* __restrict__ rv, float* __restrict__ save_mean,
-    float* __restrict__ save_invstd, bool training, float momentum, float eps, int64_t M, int C,
-    int TPR, int RPI) {
+    const float* __restrict__ coef, int64_t M, int C, int TPR, int RPI) {
   const int t = threadIdx.x;
   const int lc = t % TPR, r0 = t / TPR;
   const int cg = blockIdx.y * TPR + lc;
   if (r0 >= RPI || cg >= C / VEC) return;
   const int c0 = cg * VEC;
-  const float Mf = static_cast<float>(M);
-  float sc[VEC], sf[VEC], mean[VEC], invstd[VEC], var[VEC];
-  fwd_coeffs<T, PT, VEC>(x, acc, gamma, beta, rm, rv, training, Mf, eps, C, c0, sc, sf, mean,
-                         invstd, var);
-  if (blockIdx.x == 0 && r0 == 0) {
+  float sc[VEC], sf[VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      save_mean[c0 + i] = mean[i];
-      save_invstd[c0 + i] = invstd[i];
-      if (training && rm != nullptr) {
-        const float unbiased = Mf > 1.f ? var[i] * Mf / (Mf - 1.f) : var[i];
-        rm[c0 + i] = (1.f - momentum) * rm[c0 + i] + momentum * mean[i];
-        rv[c0 + i] = (1.f - momentum) * rv[c0 + i] + momentum * unbiased;
-      }
-    }
-  }
+  for (int i = 0; i < VEC; ++i) { sc[i] = coef[c0 + i]; sf[i] = coef[C + c0 + i]; }
   const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
   int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0;
   auto body = [&](int64_t row) {
@@ -247,7 +263,7 @@ __device__ __forceinline__ void mask_coeffs(const PT* __restrict__ gamma, const 
   for (int i = 0; i < VEC; ++i) {
     const float g = gamma ? ldp<PT>(gamma, c0 + i) : 1.f;
     const float b = beta ? ldp<PT>(beta, c0 + i) : 0.f;
-    sc[i] = g * invstd[c0 + i];  // identical fp32 expression to fwd_coeffs
+    sc[i] = g * invstd[c0 + i];  // identical fp32 expressions to the forward finalize
     sf[i] = b - mean[c0 + i] * sc[i];
   }
 }
@@ -301,7 +317,42 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(
     }
     if (r < re) body(r);
   }
-  block_fold_atomic<VEC>(sa, sb, sh, t, lc, r0, TPR, RPI, active && rb < re, acc + c0, acc + C + c0);
+  float* rep = acc + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
+  block_fold_atomic<VEC>(sa, sb, sh, t, lc, r0, TPR, RPI, active && rb < re, rep + c0, rep + C + c0);
+}
+
+// ---------------------------------------------------------------- backward finalize
+template <typename PT>
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(
+    float* __restrict__ acc, int C, float Mf, const PT* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ invstd, bool training,
+    PT* __restrict__ dgamma, PT* __restrict__ dbeta, float* __restrict__ coef) {
+  const int ch = blockIdx.x * kBlock + threadIdx.x;
+  if (ch >= C) return;
+  float a = 0.f, b = 0.f;
+#pragma unroll 8
+  for (int r = 0; r < kReplicas; ++r) {
+    float* row = acc + static_cast<int64_t>(r) * 2 * C;
+    a += row[ch];
+    b += row[C + ch];
+    row[ch] = 0.f;
+    row[C + ch] = 0.f;
+  }
+  const float is = invstd[ch];
+  const float db = a;
+  const float dg = b * is;
+  if (dgamma) stp<PT>(dgamma, ch, dg);
+  if (dbeta) stp<PT>(dbeta, ch, db);
+  const float g = gamma ? ldp<PT>(gamma, ch) : 1.f;
+  const float k = g * is;
+  float c1 = 0.f, c0 = 0.f;
+  if (training) {
+    c1 = -k * is * dg / Mf;
+    c0 = -k * db / Mf - c1 * mean[ch];
+  }
+  coef[ch] = k;
+  coef[C + ch] = c1;
+  coef[2 * C + ch] = c0;
 }
 
 // ---------------------------------------------------------------- backward apply
@@ -309,29 +360,19 @@ template <typename T, typename PT, int VEC, int MASK, bool RES>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
     const PT* __restrict__ gamma, const PT* __restrict__ beta, const float* __restrict__ mean,
-    const float* __restrict__ invstd, const float* __restrict__ acc, bool training,
-    T* __restrict__ dx, T* __restrict__ dres, PT* __restrict__ dgamma, PT* __restrict__ dbeta,
-    int64_t M, int C, int TPR, int RPI) {
+    const float* __restrict__ invstd, const float* __restrict__ coef, T* __restrict__ dx,
+    T* __restrict__ dres, int64_t M, int C, int TPR, int RPI) {
   const int t = threadIdx.x;
   const int lc = t % TPR, r0 = t / TPR;
   const int cg = blockIdx.y * TPR + lc;
   if (r0 >= RPI || cg >= C / VEC) return;
   const int c0 = cg * VEC;
-  const float inv_m = 1.f / static_cast<float>(M);
   float k[VEC], c1[VEC], c0v[VEC], sc[VEC], sf[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
-    const float is = invstd[c0 + i];
-    const float db = acc[c0 + i];
-    const float dg = acc[C + c0 + i] * is;
-    const float g = gamma ? ldp<PT>(gamma, c0 + i) : 1.f;
-    k[i] = g * is;
-    c1[i] = training ? -k[i] * is * dg * inv_m : 0.f;
-    c0v[i] = training ? -k[i] * db * inv_m - c1[i] * mean[c0 + i] : 0.f;
-    if (blockIdx.x == 0 && r0 == 0) {
-      if (dgamma) stp<PT>(dgamma, c0 + i, dg);
-      if (dbeta) stp<PT>(dbeta, c0 + i, db);
-    }
+    k[i] = coef[c0 + i];
+    c1[i] = coef[C + c0 + i];
+    c0v[i] = coef[2 * C + c0 + i];
     sc[i] = 0.f;
     sf[i] = 0.f;
   }
@@ -402,17 +443,26 @@ int apply_gx(int64_t M, const Tiling& tl) {
 
 template <typename T, int VEC, typename PT>
 hipError_t fwd_impl(const T* x, const T* res, T* y, const PT* gamma, const PT* beta, float* rm,
-                    float* rv, float* save_mean, float* save_invstd, float* acc, int64_t M, int C,
+                    float* rv, float* save_mean, float* save_invstd, float* ws, int64_t M, int C,
                     bool relu, bool training, float momentum, float eps, hipStream_t s) {
   ReducePlan rp = plan_reduce(M, C, VEC);
-  if (training)
+  float* acc = ws_acc_fwd(ws, C);
+  float* coef = ws_coef(ws, C);
+  const int fin_grid = (C + kBlock - 1) / kBlock;
+  if (training) {
     hipLaunchKernelGGL((bn_fwd_stats_kernel<T, VEC>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
                        x, M, C, rp.tl.TPR, rp.tl.RPI, rp.rows_per_block, acc);
+    hipLaunchKernelGGL((bn_fwd_finalize_kernel<T, PT>), dim3(fin_grid), dim3(kBlock), 0, s, x, acc,
+                       C, static_cast<float>(M), gamma, beta, rm, rv, momentum, eps, save_mean,
+                       save_invstd, coef);
+  } else {
+    hipLaunchKernelGGL((bn_eval_prep_kernel<PT>), dim3(fin_grid), dim3(kBlock), 0, s, C, gamma,
+                       beta, rm, rv, eps, save_mean, save_invstd, coef);
+  }
   dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
-#define KDL_FWD_APPLY(R, S)                                                                      \
-  hipLaunchKernelGGL((bn_fwd_apply_kernel<T, PT, VEC, R, S>), grid, dim3(kBlock), 0, s, x, res, y, \
-                     acc, gamma, beta, rm, rv, save_mean, save_invstd, training, momentum, eps, M, \
-                     C, rp.tl.TPR, rp.tl.RPI)
+#define KDL_FWD_APPLY(R, S)                                                                    \
+  hipLaunchKernelGGL((bn_fwd_apply_kernel<T, VEC, R, S>), grid, dim3(kBlock), 0, s, x, res, y, \
+                     coef, M, C, rp.tl.TPR, rp.tl.RPI)
   if (relu && res) KDL_FWD_APPLY(true, true);
   else if (relu) KDL_FWD_APPLY(true, false);
   else if (res) KDL_FWD_APPLY(false, true);
@@ -424,43 +474,48 @@ hipError_t fwd_impl(const T* x, const T* res, T* y, const PT* gamma, const PT* b
 template <typename T, int VEC, typename PT, int MASK>
 void bwd_launch(const ReducePlan& rp, const T* dy, const T* y, const T* x, const PT* gamma,
                 const PT* beta, const float* mean, const float* invstd, T* dx, T* dres, PT* dgamma,
-                PT* dbeta, float* acc, int64_t M, int C, bool training, hipStream_t s) {
+                PT* dbeta, float* ws, int64_t M, int C, bool training, hipStream_t s) {
+  float* acc = ws_acc_bwd(ws, C);
+  float* coef = ws_coef(ws, C);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, PT, VEC, MASK>), dim3(rp.gx, rp.tl.gy), dim3(kBlock),
                      0, s, dy, y, x, gamma, beta, mean, invstd, M, C, rp.tl.TPR, rp.tl.RPI,
                      rp.rows_per_block, acc);
+  hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     s, acc, C, static_cast<float>(M), gamma, mean, invstd, training, dgamma, dbeta,
+                     coef);
   dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
   if (dres)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PT, VEC, MASK, true>), grid, dim3(kBlock), 0, s, dy,
-                       y, x, gamma, beta, mean, invstd, acc, training, dx, dres, dgamma, dbeta, M,
-                       C, rp.tl.TPR, rp.tl.RPI);
+                       y, x, gamma, beta, mean, invstd, coef, dx, dres, M, C, rp.tl.TPR, rp.tl.RPI);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PT, VEC, MASK, false>), grid, dim3(kBlock), 0, s, dy,
-                       y, x, gamma, beta, mean, invstd, acc, training, dx, dres, dgamma, dbeta, M,
-                       C, rp.tl.TPR, rp.tl.RPI);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PT, VEC, MASK, false>), grid, dim3(kBlock), 0, s,
+                       dy, y, x, gamma, beta, mean, invstd, coef, dx, dres, M, C, rp.tl.TPR,
+                       rp.tl.RPI);
 }
 
 template <typename T, int VEC, typename PT>
 hipError_t bwd_impl(const T* dy, const T* y, const T* x, const PT* gamma, const PT* beta,
                     const float* mean, const float* invstd, T* dx, T* dres, PT* dgamma, PT* dbeta,
-                    float* acc, int64_t M, int C, bool relu, bool training, hipStream_t s) {
+                    float* ws, int64_t M, int C, bool relu, bool training, hipStream_t s) {
   ReducePlan rp = plan_reduce(M, C, VEC);
   if (!relu)
     bwd_launch<T, VEC, PT, kMaskNone>(rp, dy, y, x, gamma, beta, mean, invstd, dx, dres, dgamma,
-                                      dbeta, acc, M, C, training, s);
+                                      dbeta, ws, M, C, training, s);
   else if (dres || y == nullptr || beta == nullptr)
-    // with a residual the mask must come from y (it saw the residual); also
-    // used when beta is not available to recompute the pre-activation.
+    // with a residual the mask must come from y (it saw the residual)
     bwd_launch<T, VEC, PT, kMaskY>(rp, dy, y, x, gamma, beta, mean, invstd, dx, dres, dgamma,
-                                   dbeta, acc, M, C, training, s);
+                                   dbeta, ws, M, C, training, s);
   else
     bwd_launch<T, VEC, PT, kMaskX>(rp, dy, y, x, gamma, beta, mean, invstd, dx, dres, dgamma,
-                                   dbeta, acc, M, C, training, s);
+                                   dbeta, ws, M, C, training, s);
   return hipGetLastError();
 }
 
 }  // namespace
 
-int64_t bn_acc_floats(int C) { return 2 * static_cast<int64_t>(C); }
+int64_t bn_workspace_floats(int C) {
+  return static_cast<int64_t>(kReplicas) * 4 * C + 4 * static_cast<int64_t>(C);
+}
 
 #define KDL_DISPATCH_PT(pdtype, ...)              \
   do {                                           \
@@ -488,14 +543,14 @@ int64_t bn_acc_floats(int C) { return 2 * static_cast<int64_t>(C); }
 
 hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* gamma,
                           const void* beta, float* rm, float* rv, float* save_mean,
-                          float* save_invstd, float* acc, int64_t M, int C, int dtype, int pdtype,
+                          float* save_invstd, float* ws, int64_t M, int C, int dtype, int pdtype,
                           bool relu, bool training, float momentum, float eps, hipStream_t s) {
   if (M <= 0 || C <= 0) return hipSuccess;
   hipError_t e = hipSuccess;
   KDL_DISPATCH_PT(pdtype, KDL_DISPATCH_T(dtype, C, {
     e = fwd_impl<T, VEC, PT>(static_cast<const T*>(x), static_cast<const T*>(res),
                              static_cast<T*>(y), static_cast<const PT*>(gamma),
-                             static_cast<const PT*>(beta), rm, rv, save_mean, save_invstd, acc, M,
+                             static_cast<const PT*>(beta), rm, rv, save_mean, save_invstd, ws, M,
                              C, relu, training, momentum, eps, s);
   }));
   return e;
@@ -503,7 +558,7 @@ hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* g
 
 hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const void* gamma,
                            const void* beta, const float* mean, const float* invstd, void* dx,
-                           void* dres, void* dgamma, void* dbeta, float* acc, int64_t M, int C,
+                           void* dres, void* dgamma, void* dbeta, float* ws, int64_t M, int C,
                            int dtype, int pdtype, bool relu, bool training, hipStream_t s) {
   if (M <= 0 || C <= 0) return hipSuccess;
   hipError_t e = hipSuccess;
@@ -512,7 +567,7 @@ hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const v
                              static_cast<const T*>(x), static_cast<const PT*>(gamma),
                              static_cast<const PT*>(beta), mean, invstd, static_cast<T*>(dx),
                              static_cast<T*>(dres), static_cast<PT*>(dgamma),
-                             static_cast<PT*>(dbeta), acc, M, C, relu, training, s);
+                             static_cast<PT*>(dbeta), ws, M, C, relu, training, s);
   }));
   return e;
 }

@@ -8,15 +8,16 @@
 namespace kdl {
 
 // ---- bn_act.hip (dtype codes: 0 = f32, 1 = bf16)
-// ``acc`` is a [2, C] fp32 accumulator that must be zero on entry.
-int64_t bn_acc_floats(int C);
+// ``ws`` is a per-layer fp32 workspace of bn_workspace_floats(C) elements,
+// zero when first used; the kernels leave it zero again (self-cleaning).
+int64_t bn_workspace_floats(int C);
 hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* gamma,
                           const void* beta, float* rm, float* rv, float* save_mean,
-                          float* save_invstd, float* acc, int64_t M, int C, int dtype, int pdtype,
+                          float* save_invstd, float* ws, int64_t M, int C, int dtype, int pdtype,
                           bool relu, bool training, float momentum, float eps, hipStream_t s);
 hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const void* gamma,
                            const void* beta, const float* mean, const float* invstd, void* dx,
-                           void* dres, void* dgamma, void* dbeta, float* acc, int64_t M, int C,
+                           void* dres, void* dgamma, void* dbeta, float* ws, int64_t M, int C,
                            int dtype, int pdtype, bool relu, bool training, hipStream_t s);
 
 // ---- optim.hip

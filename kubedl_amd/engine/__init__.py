@@ -1,0 +1,1 @@
+"""Common job engine: ReconcileJobs, expectations, work queues, manager."""

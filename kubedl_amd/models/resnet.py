@@ -49,26 +49,18 @@ class BNAct(nn.Module):
         self.register_buffer("running_mean", torch.zeros(channels))
         self.register_buffer("running_var", torch.ones(channels))
         self.backend = "auto"
-        self.arena = None
-        self._arena_off = 0
-        self._gen_f = [-1]
-        self._gen_b = [-1]
-
-    def attach_arena(self, arena: "bn_ops.BNArena") -> None:
-        self.arena = arena
-        self._arena_off = arena.reserve(4 * self.channels)
+        self._ws = None
 
     def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None) -> torch.Tensor:
-        acc_f = acc_b = None
-        if self.arena is not None and self.training:
-            C = self.channels
-            acc_f = self.arena.take(self._arena_off, 2 * C, self._gen_f)
-            acc_b = self.arena.take(self._arena_off + 2 * C, 2 * C, self._gen_b)
+        ws = None
+        if x.is_cuda and self.backend != "torch":
+            if self._ws is None or self._ws.device != x.device:
+                self._ws = bn_ops.workspace_for(self.channels, x.device)
+            ws = self._ws
         return bn_ops.batch_norm_act(
             x, self.weight, self.bias, self.running_mean, self.running_var,
             residual=residual, relu=self.relu, training=self.training,
-            momentum=self.momentum, eps=self.eps, backend=self.backend,
-            acc_fwd=acc_f, acc_bwd=acc_b)
+            momentum=self.momentum, eps=self.eps, backend=self.backend, workspace=ws)
 
 
 class Bottleneck(nn.Module):
@@ -133,14 +125,6 @@ class ResNet(nn.Module):
             if isinstance(m, BNAct):
                 m.backend = backend
 
-    def enable_bn_arena(self) -> "bn_ops.BNArena":
-        """Give every BN layer a slice of one per-step-zeroed accumulator arena."""
-        arena = bn_ops.BNArena()
-        for m in self.modules():
-            if isinstance(m, BNAct):
-                m.attach_arena(arena)
-        self.bn_arena = arena
-        return arena
 
 
 def resnet50(num_classes: int = 1000) -> ResNet:

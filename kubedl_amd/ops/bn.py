@@ -43,48 +43,19 @@ def _torch_bn_act(x, weight, bias, running_mean, running_var, residual, relu,
     return y.to(x.dtype)
 
 
-class BNArena:
-    """One zero-initialised fp32 buffer holding every BN layer's [2C] forward and
-    [2C] backward accumulators, zeroed by ONE fill per training step
-    (``zero_()``) instead of one memset per BN call.
+def workspace_for(channels: int, device) -> torch.Tensor:
+    """Per-layer zeroed fp32 workspace (replicated stat accumulators + coefs).
 
-    Each slice may be used once per generation; a second use in the same
-    generation (e.g. gradient-accumulation micro-batches without a
-    ``zero_()``) falls back to a freshly zeroed buffer, so results never
-    depend on the caller remembering to zero.
-    """
-
-    def __init__(self):
-        self.buf = None
-        self.size = 0
-        self.generation = 0
-        self._owners = []
-
-    def reserve(self, n: int) -> int:
-        off = self.size
-        self.size += (n + 63) // 64 * 64
-        self.buf = None
-        return off
-
-    def zero_(self, device) -> None:
-        if self.buf is None or self.buf.device != torch.device(device):
-            self.buf = torch.zeros(self.size, dtype=torch.float32, device=device)
-        else:
-            self.buf.zero_()
-        self.generation += 1
-
-    def take(self, off: int, n: int, last_gen: list):
-        """Slice [off, off+n) if still unused this generation, else None."""
-        if self.buf is None or last_gen[0] == self.generation:
-            return None
-        last_gen[0] = self.generation
-        return self.buf[off:off + n]
+    The kernels leave it zeroed after every use, so a layer allocates it once
+    and keeps it (no per-call memset)."""
+    n = _ext.load().bn_workspace_floats(int(channels))
+    return torch.zeros(n, dtype=torch.float32, device=device)
 
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, relu, training,
-                momentum, eps, acc_fwd, acc_bwd):
+                momentum, eps, ws):
         ext = _ext.load()
         x = x.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else x.contiguous()
         if residual is not None:
@@ -92,9 +63,9 @@ class _BNActFn(torch.autograd.Function):
                 else residual.contiguous()
         y, mean, invstd = ext.bn_act_fwd(x, weight, bias, running_mean, running_var,
                                          residual, bool(relu), bool(training),
-                                         float(momentum), float(eps), acc_fwd)
+                                         float(momentum), float(eps), ws)
         ctx.save_for_backward(x, y, weight, bias, mean, invstd)
-        ctx.acc_bwd = acc_bwd
+        ctx.ws = ws
         ctx.relu = relu
         ctx.has_residual = residual is not None
         ctx.training = training
@@ -107,14 +78,13 @@ class _BNActFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
         dx, dgamma, dbeta, dres = ext.bn_act_bwd(dy, x, y, weight, bias, mean, invstd,
                                                  bool(ctx.relu), bool(ctx.has_residual),
-                                                 bool(ctx.training), ctx.acc_bwd)
+                                                 bool(ctx.training), ctx.ws)
         return dx, dgamma, dbeta, None, None, (dres if ctx.has_residual else None), \
-            None, None, None, None, None, None
+            None, None, None, None, None
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, residual=None, relu=True,
-                   training=True, momentum=0.1, eps=1e-5, backend="auto", acc_fwd=None,
-                   acc_bwd=None):
+                   training=True, momentum=0.1, eps=1e-5, backend="auto", workspace=None):
     if backend == "auto":
         backend = "hip" if (x.is_cuda and _ext.available()) else "torch"
         if x.is_cuda and backend == "torch":
@@ -123,4 +93,4 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, residual=None, re
         return _torch_bn_act(x, weight, bias, running_mean, running_var, residual, relu,
                              training, momentum, eps)
     return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, relu,
-                          training, momentum, eps, acc_fwd, acc_bwd)
+                          training, momentum, eps, workspace)

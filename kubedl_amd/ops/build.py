@@ -109,12 +109,47 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     return OUT
 
 
+NATIVE_OUT = ROOT / "kubedl_amd" / "_native.so"
+
+
+def build_native(force: bool = False, verbose: bool = True) -> Path:
+    """Host-only C++ runtime module (process supervisor + gang placement core).
+
+    Plain CPython C API, no torch/HIP dependency, so the controller process
+    never needs to import torch or touch the GPU."""
+    srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    py_inc = sysconfig.get_paths()["include"]
+    h = hashlib.sha256()
+    for p in srcs:
+        h.update(p.read_bytes())
+    key = h.hexdigest()[:16]
+    stamp = BUILD / "native.stamp"
+    BUILD.mkdir(parents=True, exist_ok=True)
+    if NATIVE_OUT.exists() and stamp.exists() and stamp.read_text() == key and not force:
+        return NATIVE_OUT
+    cxx = os.environ.get("CXX", "g++")
+    tmp = NATIVE_OUT.with_suffix(".so.tmp")
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{py_inc}", "-o", str(tmp)] + \
+        [str(p) for p in srcs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, NATIVE_OUT)
+    stamp.write_text(key)
+    if verbose:
+        print(f"[kdl-build] linked {NATIVE_OUT}", flush=True)
+    return NATIVE_OUT
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--native-only", action="store_true")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.jobs)
+    build_native(force=a.force)
+    if not a.native_only:
+        build(force=a.force, jobs=a.jobs)
 
 
 if __name__ == "__main__":

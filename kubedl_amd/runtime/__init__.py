@@ -1,0 +1,2 @@
+"""Local MI355X node runtime: scheduler (GPU binding), kubelet (rank-process
+supervisor), service resolver and the image registry."""

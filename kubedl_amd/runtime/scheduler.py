@@ -1,0 +1,228 @@
+"""Node scheduler: binds pending pods to this MI355X node's GPUs.
+
+Replaces kube-scheduler + kube-batch for one node:
+
+* a pod requests ``amd.com/gpu`` (or ``nvidia.com/gpu`` for unchanged
+  specs) per container; 0-GPU pods always fit;
+* pods bound to a gang (``spec.schedulerName`` = a registered gang scheduler
+  and the ``scheduling.k8s.io/group-name`` annotation) are admitted
+  all-or-nothing: only when ``PodGroup.spec.minMember`` members exist AND the
+  allocator can reserve every member's GPUs at once (``GPUAllocator``);
+  otherwise nothing is reserved and the pods stay Pending with
+  ``PodScheduled=False, reason=Unschedulable``;
+* queue order is FIFO by creation time with backfill: a later gang that fits
+  in the currently free GPUs may start while the head waits, until the head
+  has waited ``starvation_s`` -- then backfill stops so big gangs cannot starve;
+* binding writes ``spec.nodeName``, the ``kubedl.io/gpus`` annotation and the
+  ``PodScheduled`` condition; GPUs return to the pool when the pod is deleted
+  or reaches a terminal phase.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Dict, List, Optional, Tuple
+
+from kubedl_amd.api import common as c
+from kubedl_amd.gang import interface as gang_iface
+from kubedl_amd.gang.allocator import GPUAllocator
+from kubedl_amd.gang.local import GROUP_ANNOTATION
+from kubedl_amd.store import ADDED, DELETED, MODIFIED, NotFound, Store
+
+log = logging.getLogger("kubedl_amd.scheduler")
+
+GPU_ANNOTATION = "kubedl.io/gpus"
+NODE_NAME = "localhost"
+
+
+def pod_key(pod: dict) -> str:
+    md = pod["metadata"]
+    return f"{md['namespace']}/{md['name']}/{md.get('uid', '')}"
+
+
+def pod_gpus(pod: dict) -> int:
+    return c.pod_template_gpus({"spec": pod.get("spec") or {}})
+
+
+def is_terminal(pod: dict) -> bool:
+    return (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed")
+
+
+class NodeScheduler:
+    def __init__(self, store: Store, allocator: GPUAllocator, node_name: str = NODE_NAME,
+                 starvation_s: float = 30.0, metrics=None):
+        self.store = store
+        self.alloc = allocator
+        self.node = node_name
+        self.starvation_s = starvation_s
+        self.metrics = metrics
+        self._wake = threading.Event()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._owner_of_pod: Dict[str, str] = {}
+        self._unsched_marked: set = set()
+        self._lock = threading.Lock()
+        self._cancel = store.watch(self._on_event)
+
+    # ------------------------------------------------------------ lifecycle
+    def start(self) -> None:
+        self._thread = threading.Thread(target=self._loop, name="kdl-scheduler", daemon=True)
+        self._thread.start()
+        self._wake.set()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._wake.set()
+        self._cancel()
+        if self._thread:
+            self._thread.join(timeout=5)
+
+    def _on_event(self, etype: str, obj: dict) -> None:
+        kind = obj.get("kind")
+        if kind == "Pod":
+            if etype == DELETED or (etype == MODIFIED and is_terminal(obj)):
+                self._release(obj)
+            self._wake.set()
+        elif kind == "PodGroup":
+            self._wake.set()
+
+    def _release(self, pod: dict) -> None:
+        k = pod_key(pod)
+        with self._lock:
+            owner = self._owner_of_pod.pop(k, None)
+            self._unsched_marked.discard(k)
+        if owner is not None:
+            self.alloc.release(owner, k)
+            if self.metrics is not None:
+                self.metrics.gpus_allocated.set(self.alloc.used())
+            self._wake.set()
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            self._wake.wait(timeout=1.0)
+            self._wake.clear()
+            if self._stop.is_set():
+                break
+            try:
+                self.schedule_once()
+            except Exception:
+                log.exception("schedule pass failed")
+
+    # ------------------------------------------------------------ one pass
+    def _units(self) -> List[Tuple[float, str, List[dict], int]]:
+        """Pending scheduling units: (age key, owner, pods-to-bind, min members)."""
+        pods = self.store.list("Pod")
+        gangs: Dict[str, List[dict]] = {}
+        singles: List[dict] = []
+        for p in pods:
+            if p["metadata"].get("deletionTimestamp") or is_terminal(p):
+                continue
+            sched = (p.get("spec") or {}).get("schedulerName")
+            grp = (p["metadata"].get("annotations") or {}).get(GROUP_ANNOTATION)
+            if grp and sched and gang_iface.get(sched) is not None:
+                gangs.setdefault(f"{p['metadata']['namespace']}/{grp}", []).append(p)
+            elif not (p.get("spec") or {}).get("nodeName"):
+                singles.append(p)
+        units = []
+        for gkey, members in gangs.items():
+            unbound = [p for p in members if not (p.get("spec") or {}).get("nodeName")]
+            if not unbound:
+                continue
+            ns, name = gkey.split("/", 1)
+            pg = self.store.try_get("PodGroup", ns, name)
+            min_member = int(((pg or {}).get("spec") or {}).get("minMember", len(members)))
+            age = min(c.to_epoch(p["metadata"].get("creationTimestamp")) or 0 for p in members)
+            units.append((age, "gang:" + gkey, unbound, min_member if len(members) < min_member else 0))
+        for p in singles:
+            age = c.to_epoch(p["metadata"].get("creationTimestamp")) or 0
+            units.append((age, "pod:" + pod_key(p), [p], 0))
+        units.sort(key=lambda u: u[0])
+        return units
+
+    def schedule_once(self) -> int:
+        bound = 0
+        units = self._units()
+        head_blocked_since = None
+        now = time.time()
+        for age, owner, pods, missing in units:
+            if missing:
+                # gang incomplete: wait for all minMember pods to exist
+                self._mark_unschedulable(pods, f"PodGroup has fewer than {missing} members")
+                continue
+            if head_blocked_since is not None and now - head_blocked_since > self.starvation_s:
+                self._mark_unschedulable(pods, "waiting behind an older gang (FIFO after starvation)")
+                continue
+            req = {pod_key(p): pod_gpus(p) for p in pods}
+            alloc = self.alloc.allocate(owner, req)
+            if alloc is None:
+                free = len(self.alloc.free)
+                self._mark_unschedulable(
+                    pods, f"0/1 nodes available: insufficient amd.com/gpu (need {sum(req.values())}, "
+                          f"{free}/{self.alloc.inv.count} free)")
+                if head_blocked_since is None:
+                    head_blocked_since = age
+                continue
+            for p in pods:
+                k = pod_key(p)
+                if self._bind(p, alloc.pods.get(k, [])):
+                    with self._lock:
+                        self._owner_of_pod[k] = owner
+                        self._unsched_marked.discard(k)
+                    bound += 1
+                else:
+                    self.alloc.release(owner, k)
+            if owner.startswith("gang:"):
+                ns, name = owner[5:].split("/", 1)
+                self._set_group_phase(ns, name, "Running")
+        if self.metrics is not None:
+            self.metrics.gpus_allocated.set(self.alloc.used())
+        return bound
+
+    def _bind(self, pod: dict, gpus: List[int]) -> bool:
+        md = pod["metadata"]
+        ts = c.now()
+
+        def mutate(o):
+            if o["metadata"].get("uid") != md.get("uid"):
+                raise NotFound("pod replaced")
+            o.setdefault("spec", {})["nodeName"] = self.node
+            o["metadata"].setdefault("annotations", {})[GPU_ANNOTATION] = ",".join(map(str, gpus))
+            st = o.setdefault("status", {})
+            conds = [x for x in st.get("conditions") or [] if x.get("type") != "PodScheduled"]
+            conds.append({"type": "PodScheduled", "status": "True", "lastTransitionTime": ts})
+            st["conditions"] = conds
+        try:
+            self.store.patch("Pod", md["namespace"], md["name"], mutate)
+            return True
+        except NotFound:
+            return False
+
+    def _mark_unschedulable(self, pods: List[dict], msg: str) -> None:
+        for p in pods:
+            k = pod_key(p)
+            with self._lock:
+                if k in self._unsched_marked:
+                    continue
+                self._unsched_marked.add(k)
+            md = p["metadata"]
+            ts = c.now()
+
+            def mutate(o, msg=msg, ts=ts):
+                st = o.setdefault("status", {})
+                conds = [x for x in st.get("conditions") or [] if x.get("type") != "PodScheduled"]
+                conds.append({"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
+                              "message": msg, "lastTransitionTime": ts})
+                st["conditions"] = conds
+            try:
+                self.store.patch("Pod", md["namespace"], md["name"], mutate)
+            except NotFound:
+                pass
+
+    def _set_group_phase(self, ns: str, name: str, phase: str) -> None:
+        def mutate(o):
+            o.setdefault("status", {})["phase"] = phase
+        try:
+            self.store.patch("PodGroup", ns, name, mutate)
+        except NotFound:
+            pass

@@ -47,7 +47,6 @@ class ResNetTrainer:
             for p in model.parameters():
                 p.data = p.data.to(dtype)
         self.model = model
-        self.arena = model.enable_bn_arena() if dev.type == "cuda" else None
         self.dtype = dtype
         self.space = FlatParamSpace(model, dtype=dtype, device=dev)
         self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb)
@@ -64,8 +63,6 @@ class ResNetTrainer:
 
     def step(self) -> torch.Tensor:
         self.space.zero_grad()
-        if self.arena is not None:
-            self.arena.zero_(self.info.device)
         out = self.model(self.x)
         loss = F.cross_entropy(out.float(), self.y)
         loss.backward()

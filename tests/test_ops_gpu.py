@@ -105,7 +105,7 @@ def test_fused_sgd_matches_cpu_path(nesterov, dtype):
         for _ in range(3):
             sp.grad.copy_(torch.randn(sp.numel, generator=g).to(dtype))
             opt.step()
-        res[dev] = sp.master.cpu()
+        res[dev] = torch.cat([sp._view(sp.master, sl).reshape(-1) for sl in sp.slots]).cpu()
         assert sp.param.dtype == dtype
     torch.testing.assert_close(res["cuda"], res["cpu"], atol=1e-5, rtol=1e-5)
 
@@ -127,8 +127,8 @@ def test_fused_sgd_matches_torch_optim():
         ref.zero_grad()
         m2(x).square().sum().backward()
         ref.step()
-    torch.testing.assert_close(m1.weight, m2.weight, atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(m1.bias, m2.bias, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m1.weight, m2.weight, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(m1.bias, m2.bias, atol=1e-4, rtol=1e-4)
 
 
 @pytest.mark.parametrize("adam_w", [True, False])
@@ -186,25 +186,29 @@ def test_pack_grads_matches_views():
             torch.testing.assert_close(view, grads[s.name], atol=0, rtol=0)
 
 
-def test_bn_arena_matches_fresh_buffers():
-    """Per-step-zeroed arena accumulators give the same result as fresh zeros,
-    and a second forward in the same generation falls back safely."""
-    from kubedl_amd.models.resnet import resnet_tiny
+def test_bn_workspace_is_self_cleaning():
+    """A persistent per-layer workspace (replicated accumulators re-zeroed by the
+    finalize kernels) gives the same results on every reuse as a fresh one."""
+    from kubedl_amd.ops.bn import batch_norm_act, workspace_for
     torch.manual_seed(0)
-    outs = []
-    for use_arena in (False, True):
-        torch.manual_seed(0)
-        m = resnet_tiny(10).cuda().to(memory_format=torch.channels_last)
-        if use_arena:
-            arena = m.enable_bn_arena()
-            arena.zero_("cuda")
-        x = torch.randn(4, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
-        y1 = m(x)
-        y2 = m(x)  # same generation: must not reuse the dirty accumulators
-        (y1.sum() + y2.sum()).backward()
-        outs.append((y1.detach(), y2.detach(), m.conv1.weight.grad.clone()))
-    for a, b in zip(outs[0], outs[1]):
-        torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
+    C = 96
+    ws = workspace_for(C, "cuda")
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+    for it in range(3):
+        x = torch.randn(8, C, 6, 6, device="cuda").contiguous(memory_format=torch.channels_last)
+        outs = []
+        for use_ws in (None, ws):
+            xi = x.clone().requires_grad_(True)
+            wi = w.clone().requires_grad_(True)
+            bi = b.clone().requires_grad_(True)
+            y = batch_norm_act(xi, wi, bi, torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"),
+                               relu=True, backend="hip", workspace=use_ws)
+            y.backward(torch.ones_like(y) * (it + 1))
+            outs.append((y.detach(), xi.grad, wi.grad, bi.grad))
+        for p_, q_ in zip(*outs):
+            torch.testing.assert_close(p_, q_, atol=0, rtol=0)
+    assert torch.count_nonzero(ws[: ws.numel() - 4 * C]) == 0
 
 
 def test_resnet_hip_vs_torch_backend_step():
