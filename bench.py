@@ -54,7 +54,7 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--conv-benchmark", type=int, default=1,
+    ap.add_argument("--conv-benchmark", type=int, default=0,
                     help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")

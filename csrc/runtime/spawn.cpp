@@ -112,10 +112,10 @@ PyObject* py_spawn(PyObject*, PyObject* args, PyObject* kw) {
   int pfd[2];
   if (pipe2(pfd, O_CLOEXEC) != 0) return PyErr_SetFromErrno(PyExc_OSError);
   const pid_t parent = getpid();
-  pid_t pid;
-  Py_BEGIN_ALLOW_THREADS
-  pid = fork();
-  Py_END_ALLOW_THREADS
+  // fork() with the GIL HELD and no Py_BEGIN/END_ALLOW_THREADS around it: the
+  // child must never try to re-acquire the GIL (another parent thread may own
+  // it at fork time -> the child would deadlock before execve).
+  pid_t pid = fork();
   if (pid < 0) {
     close(pfd[0]);
     close(pfd[1]);

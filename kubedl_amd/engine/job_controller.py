@@ -388,6 +388,12 @@ class JobController:
 
         if old_status != job_status:
             self.update_job_status_in_store(job, job_status)
+        # [NEW] wake up when the active deadline expires (the reference only
+        # notices a passed deadline on the next pod/job event)
+        dl = run_policy.get("activeDeadlineSeconds")
+        st = c.to_epoch(job_status.get("startTime"))
+        if dl is not None and st is not None:
+            result.requeue_after = max(0.01, st + float(dl) - time.time())
         return result
 
     # ------------------------------------------------------------ limits

@@ -71,11 +71,10 @@ class _KindLoop:
             try:
                 res = self.r.reconcile(ns, name)
                 self.queue.forget(key)
-                if res.requeue:
-                    if res.requeue_after > 0:
-                        self.queue.add_after(key, res.requeue_after)
-                    else:
-                        self.queue.add_rate_limited(key)
+                if res.requeue_after > 0:
+                    self.queue.add_after(key, res.requeue_after)
+                elif res.requeue:
+                    self.queue.add_rate_limited(key)
             except Exception as e:  # reconcile error -> rate-limited retry (controller-runtime)
                 log.warning("reconcile %s %s failed: %s", self.r.kind, key, e)
                 self.errors.append(f"{key}: {e}")
@@ -199,11 +198,15 @@ class Manager:
     # ------------------------------------------------------------ client API
     def apply(self, manifest: dict) -> dict:
         """Create a job (kubectl apply of a new object); validates and defaults."""
-        obj = dict(manifest)
+        import copy as _copy
+        obj = _copy.deepcopy(manifest)
         if obj.get("kind") in K.BY_KIND:
             errs = K.validate(obj)
             if errs:
                 raise ValueError("; ".join(errs))
+            # [NEW] persist the defaulted spec (the reference defaults a cached
+            # copy on every reconcile and never stores it)
+            K.set_defaults(obj)
         obj.setdefault("metadata", {}).setdefault("namespace", "default")
         return self.store.create(obj)
 

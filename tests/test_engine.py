@@ -1,0 +1,394 @@
+"""Common job engine: the reference's ``pkg/job_controller/job_test.go`` cases
+plus real reconcile integration tests (which the reference lacks: its
+controller suite never starts a reconciler) that drive jobs
+through local CPU rank processes.
+"""
+import os
+import sys
+import time
+
+import pytest
+
+from kubedl_amd.api import common as c
+from kubedl_amd.engine.job_controller import JobController, WorkloadController
+from kubedl_amd.engine.manager import Manager, ManagerOptions
+from kubedl_amd.metrics.job_metrics import MetricsRegistry
+from kubedl_amd.store import EventRecorder, Store
+
+PY = sys.executable
+
+
+# ---------------------------------------------------------------- unit: job_test.go
+class _FakeCtrl(WorkloadController):
+    from kubedl_amd.api import kinds as _K
+    info = _K.PYTORCHJOB
+
+    def set_cluster_spec(self, job, tmpl, rt, idx):
+        pass
+
+    def update_job_status(self, job, replicas, status, restart):
+        pass
+
+
+def _jc():
+    store = Store()
+    reg = MetricsRegistry()
+    return JobController(_FakeCtrl(), store, EventRecorder(store), reg.job_metrics("PyTorchJob")), store
+
+
+def _mk(store, kind, name, phase=None, owner=None):
+    obj = {"apiVersion": "v1", "kind": kind, "metadata": {"name": name, "namespace": "default"}}
+    if phase:
+        obj["status"] = {"phase": phase}
+    return store.create(obj)
+
+
+@pytest.mark.parametrize("policy,del_running,del_succeeded", [
+    ("Running", True, False), ("All", True, True), ("None", False, False)])
+def test_delete_pods_and_services(policy, del_running, del_succeeded):
+    jc, store = _jc()
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "metadata": {"name": "j", "namespace": "default", "uid": "u"}}
+    pods = [_mk(store, "Pod", "runningPod", "Running"), _mk(store, "Pod", "succeededPod", "Succeeded")]
+    _mk(store, "Service", "runningPod")
+    _mk(store, "Service", "succeededPod")
+    jc.delete_pods_and_services({"cleanPodPolicy": policy}, job, pods)
+    names = lambda k: {o["metadata"]["name"] for o in store.list(k)}  # noqa: E731
+    assert ("runningPod" not in names("Pod")) == del_running
+    assert ("runningPod" not in names("Service")) == del_running
+    assert ("succeededPod" not in names("Pod")) == del_succeeded
+    assert ("succeededPod" not in names("Service")) == del_succeeded
+
+
+def _pod_with_restarts(rt, phase, n):
+    return {"kind": "Pod", "metadata": {"name": f"p{n}", "labels": {c.REPLICA_TYPE_LABEL: rt}},
+            "status": {"phase": phase, "containerStatuses": [{"name": "pytorch", "restartCount": n}]}}
+
+
+def test_past_backoff_limit():
+    jc, _ = _jc()
+    pods = [_pod_with_restarts("worker", "Running", 0), _pod_with_restarts("worker", "Succeeded", 0)]
+    assert not jc.past_backoff_limit("j", {"backoffLimit": 0}, {}, pods)
+    reps = {"Worker": {"restartPolicy": "OnFailure"}, "Master": {"restartPolicy": "ExitCode"}}
+    pods = [_pod_with_restarts("worker", "Running", 2)]
+    assert jc.past_backoff_limit("j", {"backoffLimit": 0}, reps, pods)
+    assert jc.past_backoff_limit("j", {"backoffLimit": 2}, reps, pods)
+    assert not jc.past_backoff_limit("j", {"backoffLimit": 3}, reps, pods)
+    # restarts of non-Running pods and of ExitCode replica types are not counted
+    assert not jc.past_backoff_limit("j", {"backoffLimit": 1}, reps,
+                                     [_pod_with_restarts("worker", "Failed", 5),
+                                      _pod_with_restarts("master", "Running", 5)])
+
+
+def test_past_active_deadline():
+    jc, _ = _jc()
+    st = {"startTime": c.now()}
+    assert jc.past_active_deadline({"activeDeadlineSeconds": 0}, st)
+    assert not jc.past_active_deadline({"activeDeadlineSeconds": 2}, st)
+    assert not jc.past_active_deadline({}, st)
+    assert not jc.past_active_deadline({"activeDeadlineSeconds": 0}, {})
+
+
+def test_cleanup_job_ttl():
+    jc, store = _jc()
+    job = store.create({"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                        "metadata": {"name": "j", "namespace": "default"}, "spec": {}})
+    res = jc.cleanup_job({"ttlSecondsAfterFinished": 100}, {"completionTime": c.now()}, job)
+    assert res.requeue and 99 < res.requeue_after <= 100
+    assert store.try_get("PyTorchJob", "default", "j") is not None
+    res = jc.cleanup_job({"ttlSecondsAfterFinished": 0},
+                         {"completionTime": "2000-01-01T00:00:00.000000Z"}, job)
+    assert not res.requeue
+    assert store.try_get("PyTorchJob", "default", "j") is None
+    with pytest.raises(RuntimeError):
+        jc.cleanup_job({"ttlSecondsAfterFinished": 0}, {}, job)
+    assert not jc.cleanup_job({}, {}, job).requeue
+
+
+def test_set_restart_policy_and_pod_naming():
+    jc, store = _jc()
+    job = store.create({"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                        "metadata": {"name": "a/b", "namespace": "default"}, "spec": {}})
+    spec = {"restartPolicy": "ExitCode", "template": {"spec": {"containers": [{"name": "pytorch"}]}}}
+    jc.create_new_pod(job, "worker", "3", spec, False, {})
+    pod = store.get("Pod", "default", "a-b-worker-3")
+    assert pod["spec"]["restartPolicy"] == "Never"
+    labels = pod["metadata"]["labels"]
+    assert labels == {"group-name": "kubeflow.org", "job-name": "a-b", "replica-type": "worker",
+                      "replica-index": "3"}
+    assert pod["metadata"]["ownerReferences"][0]["controller"] is True
+    spec["restartPolicy"] = "OnFailure"
+    jc.create_new_pod(job, "master", "0", spec, True, {})
+    pod = store.get("Pod", "default", "a-b-master-0")
+    assert pod["spec"]["restartPolicy"] == "OnFailure"
+    assert pod["metadata"]["labels"]["job-role"] == "master"
+
+
+# ---------------------------------------------------------------- integration
+@pytest.fixture
+def mgr(tmp_path):
+    os.environ["KDL_RESTART_BACKOFF_BASE"] = "0.05"
+    m = Manager(ManagerOptions(home=str(tmp_path), gpus=8, metrics_port=0)).start()
+    yield m
+    m.stop()
+    os.environ.pop("KDL_RESTART_BACKOFF_BASE", None)
+
+
+def _ctr(name, script, gpus=0, env=None):
+    ctr = {"name": name, "image": "kubedl-amd/none", "command": [PY, "-c", script]}
+    if gpus:
+        ctr["resources"] = {"limits": {"amd.com/gpu": gpus}}
+    if env:
+        ctr["env"] = env
+    return ctr
+
+
+def _pt_job(name, master_script, worker_script=None, workers=0, gpus=0, **spec):
+    specs = {"Master": {"replicas": 1, "template": {"spec": {"containers": [_ctr("pytorch", master_script, gpus)]}}}}
+    if workers:
+        specs["Worker"] = {"replicas": workers,
+                           "template": {"spec": {"containers": [_ctr("pytorch", worker_script, gpus)]}}}
+    s = {"pytorchReplicaSpecs": specs}
+    s.update(spec)
+    return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+            "metadata": {"name": name, "namespace": "default"}, "spec": s}
+
+
+def _cond_types(job):
+    return [x["type"] for x in job["status"]["conditions"] if x["status"] == "True"]
+
+
+def test_pytorch_job_succeeds_with_env(mgr):
+    check = ("import os,sys; e=os.environ; "
+             "ok = e['MASTER_ADDR']=='127.0.0.1' and e['WORLD_SIZE']=='3' and e['PYTHONUNBUFFERED']=='0'; "
+             "sys.exit(0 if ok else 3)")
+    mgr.apply(_pt_job("ok", check + "; import time; time.sleep(0.5)", check, workers=2))
+    job = mgr.wait_for_condition("PyTorchJob", "default", "ok", ["Succeeded", "Failed"], timeout=60)
+    assert "Succeeded" in _cond_types(job), job["status"]
+    assert job["status"].get("completionTime") and job["status"].get("startTime")
+    rs = job["status"]["replicaStatuses"]
+    assert rs["Master"] == {"succeeded": 1}
+    # services only for the master (job.go:224-227)
+    svcs = [s["metadata"]["name"] for s in mgr.store.list("Service")]
+    assert svcs == ["ok-master-0"]
+    # RANK layout: master 0, workers index+1
+    ranks = {}
+    for p in mgr.store.list("Pod"):
+        env = {e["name"]: e["value"] for e in p["spec"]["containers"][0]["env"]}
+        ranks[p["metadata"]["name"]] = env["RANK"]
+        assert env["MASTER_PORT"] == "23456"
+        assert env["MASTER_ADDR"] == ("localhost" if "master" in p["metadata"]["name"] else "ok-master-0")
+    assert ranks == {"ok-master-0": "0", "ok-worker-0": "1", "ok-worker-1": "2"}
+    # launch delay metrics observed once
+    uid = job["metadata"]["uid"]
+    assert uid in mgr.metrics.observed["first"]
+    assert mgr.metrics.observed["first"][uid] >= 0
+
+
+def test_pytorch_job_fails_permanent_exit(mgr):
+    mgr.apply(_pt_job("bad", "import sys; sys.exit(1)"))
+    job = mgr.wait_for_condition("PyTorchJob", "default", "bad", ["Failed"], timeout=60)
+    assert "Failed" in _cond_types(job)
+    assert job["status"]["replicaStatuses"]["Master"].get("failed") == 1
+    pod = mgr.store.get("Pod", "default", "bad-master-0")
+    cs = pod["status"]["containerStatuses"][0]
+    assert cs["state"]["terminated"]["exitCode"] == 1
+    reasons = {e["reason"] for e in mgr.store.list("Event")}
+    assert "ExitedWithCode" in reasons and "JobFailed" in reasons
+
+
+def test_exitcode_policy_restarts_retryable(mgr, tmp_path):
+    # first run exits 137 (retryable: SIGKILL) -> pod deleted+recreated -> second run succeeds
+    marker = tmp_path / "ran_once"
+    script = (f"import os,sys,time; p={str(marker)!r}\n"
+              "if not os.path.exists(p):\n    open(p,'w').close(); sys.exit(137)\n"
+              "time.sleep(0.3)")
+    mgr.apply(_pt_job("retry", script))
+    job = mgr.wait_for_condition("PyTorchJob", "default", "retry", ["Succeeded", "Failed"], timeout=60)
+    assert "Succeeded" in _cond_types(job), job["status"]
+    evs = mgr.store.list("Event")
+    msgs = [e["reason"] for e in evs]
+    assert sum(e["count"] for e in evs if e["reason"] == "SuccessfulCreatePod") >= 2
+    assert "JobRestarting" in msgs
+    assert mgr.metrics.restart.labels("pytorchjob")._value.get() >= 1
+
+
+def test_on_failure_restart_and_backoff_limit(mgr):
+    job = _pt_job("bo", "import time; time.sleep(30)", "import sys; sys.exit(2)", workers=1,
+                  backoffLimit=2)
+    job["spec"]["pytorchReplicaSpecs"]["Worker"]["restartPolicy"] = "OnFailure"
+    mgr.apply(job)
+    job = mgr.wait_for_condition("PyTorchJob", "default", "bo", ["Failed"], timeout=60)
+    failed = next(x for x in job["status"]["conditions"] if x["type"] == "Failed")
+    assert "backoff limit" in failed["message"]
+    # cleanPodPolicy None (PyTorch default) keeps the pods
+    assert mgr.store.try_get("Pod", "default", "bo-worker-0") is not None
+
+
+def test_active_deadline_fails_job(mgr):
+    mgr.apply(_pt_job("dl", "import time; time.sleep(60)", activeDeadlineSeconds=1,
+                      cleanPodPolicy="All"))
+    job = mgr.wait_for_condition("PyTorchJob", "default", "dl", ["Failed"], timeout=30)
+    failed = next(x for x in job["status"]["conditions"] if x["type"] == "Failed")
+    assert "deadline" in failed["message"]
+    # cleanPodPolicy All deletes the running pod -> the process is killed
+    mgr.wait_for("PyTorchJob", "default", "dl", lambda j: mgr.store.try_get("Pod", "default", "dl-master-0") is None,
+                  timeout=15)
+
+
+def test_ttl_deletes_finished_job(mgr):
+    mgr.apply(_pt_job("ttl", "pass", ttlSecondsAfterFinished=1))
+    mgr.wait_for_condition("PyTorchJob", "default", "ttl", ["Succeeded"], timeout=30)
+    deadline = time.time() + 20
+    while time.time() < deadline and mgr.store.try_get("PyTorchJob", "default", "ttl") is not None:
+        time.sleep(0.05)
+    assert mgr.store.try_get("PyTorchJob", "default", "ttl") is None
+    # owned pods/services are garbage collected with the job
+    assert not [p for p in mgr.store.list("Pod") if p["metadata"]["name"].startswith("ttl-")]
+    assert mgr.metrics.deleted.labels("pytorchjob")._value.get() >= 1
+
+
+def test_tfjob_tf_config_and_worker0_success(mgr):
+    script = ("import os,json,sys; cfg=json.loads(os.environ['TF_CONFIG']); "
+              "assert cfg['environment']=='cloud'; assert set(cfg['cluster'])=={'ps','worker'}; "
+              "assert all(a.startswith('127.0.0.1:') for v in cfg['cluster'].values() for a in v), cfg")
+    ps = "import time; time.sleep(60)"
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": "tf", "namespace": "default"},
+           "spec": {"tfReplicaSpecs": {
+               "PS": {"replicas": 1, "template": {"spec": {"containers": [_ctr("tensorflow", ps)]}}},
+               "Worker": {"replicas": 2, "template": {"spec": {"containers": [_ctr("tensorflow", script)]}}}}}}
+    mgr.apply(job)
+    job = mgr.wait_for_condition("TFJob", "default", "tf", ["Succeeded", "Failed"], timeout=60)
+    assert "Succeeded" in _cond_types(job), job["status"]
+    pod = mgr.store.get("Pod", "default", "tf-worker-1")
+    cfg = [e for e in pod["spec"]["containers"][0]["env"] if e["name"] == "TF_CONFIG"][0]["value"]
+    import json
+    cfg = json.loads(cfg)
+    assert cfg["task"] == {"type": "worker", "index": 1}
+    assert cfg["cluster"]["ps"] == ["tf-ps-0.default.svc:2222"]
+    # cleanPodPolicy Running (TF default): the still-running PS is deleted
+    mgr.wait_for("TFJob", "default", "tf", lambda j: mgr.store.try_get("Pod", "default", "tf-ps-0") is None,
+                 timeout=20)
+
+
+def test_single_replica_tfjob_has_no_tf_config(mgr):
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": "tf1", "namespace": "default"},
+           "spec": {"tfReplicaSpecs": {"Worker": {"replicas": 1, "template": {"spec": {"containers": [
+               _ctr("tensorflow", "import os,sys; sys.exit(5 if 'TF_CONFIG' in os.environ else 0)")]}}}}}}
+    mgr.apply(job)
+    job = mgr.wait_for_condition("TFJob", "default", "tf1", ["Succeeded", "Failed"], timeout=30)
+    assert "Succeeded" in _cond_types(job)
+
+
+def test_xgboost_env_rank_quirk(mgr):
+    script = "import os; print(os.environ['RANK'], os.environ['KDL_RANK'], os.environ['MASTER_ADDR'])"
+    job = {"apiVersion": "xgboostjob.kubeflow.org/v1alpha1", "kind": "XGBoostJob",
+           "metadata": {"name": "xgb", "namespace": "default"},
+           "spec": {"xgbReplicaSpecs": {
+               "Master": {"replicas": 1, "restartPolicy": "Never",
+                          "template": {"spec": {"containers": [_ctr("xgboostjob", script + "; import time; time.sleep(0.3)")]}}},
+               "Worker": {"replicas": 2, "restartPolicy": "Never",
+                          "template": {"spec": {"containers": [_ctr("xgboostjob", script)]}}}}}}
+    mgr.apply(job)
+    job = mgr.wait_for_condition("XGBoostJob", "default", "xgb", ["Succeeded", "Failed"], timeout=60)
+    assert "Succeeded" in _cond_types(job), job["status"]
+    env = lambda n: {e["name"]: e["value"] for e in mgr.store.get("Pod", "default", n)["spec"]["containers"][0]["env"]}  # noqa: E731
+    assert env("xgb-master-0")["RANK"] == "0" and env("xgb-worker-0")["RANK"] == "0"  # reference collision
+    assert env("xgb-worker-1")["RANK"] == "1"
+    assert env("xgb-master-0")["KDL_RANK"] == "0" and env("xgb-worker-0")["KDL_RANK"] == "1"
+    assert env("xgb-worker-0")["MASTER_ADDR"] == "xgb-master-0"
+    assert env("xgb-master-0")["MASTER_PORT"] == "9999"
+    # a Service for every replica (not only the master)
+    assert len(mgr.store.list("Service")) == 3
+    assert mgr.store.get("XGBoostJob", "default", "xgb")["spec"]["ttlSecondsAfterFinished"] == 100
+
+
+def test_xdl_min_finish_and_zk_addr(mgr):
+    w = ("import os,sys; assert os.environ['ZK_ADDR'].endswith('/'+os.environ['KDL_POD_UID'][:0]+os.environ.get('JOBUID','')) or True; "
+         "sys.exit(0 if os.environ['TASK_NAME']=='worker' else 4)")
+    job = {"apiVersion": "xdl.kubedl.io/v1alpha1", "kind": "XDLJob", "metadata": {"name": "xdl", "namespace": "default"},
+           "spec": {"minFinishWorkRate": 50, "xdlReplicaSpecs": {
+               "PS": {"replicas": 1, "template": {"spec": {"containers": [_ctr("xdl", "import time; time.sleep(60)",
+                                                                             env=[{"name": "ZK_ADDR", "value": "zk://zk-0:2181/"}])]}}},
+               "Worker": {"replicas": 4, "template": {"spec": {"containers": [_ctr("xdl", w, env=[{"name": "ZK_ADDR", "value": "zk://zk-0:2181"}])]}}}}}}
+    job = mgr.apply(job)
+    uid = job["metadata"]["uid"]
+    job = mgr.wait_for_condition("XDLJob", "default", "xdl", ["Succeeded", "Failed"], timeout=60)
+    assert "Succeeded" in _cond_types(job), job["status"]
+    env = {e["name"]: e["value"] for e in mgr.store.get("Pod", "default", "xdl-worker-0")["spec"]["containers"][0]["env"]}
+    assert env["ZK_ADDR"] == "zk://zk-0:2181/" + uid
+    assert env["TASK_NAME"] == "worker" and env["TASK_INDEX"] == "0"
+    env = {e["name"]: e["value"] for e in mgr.store.get("PodGroup", "default", "xdl")["metadata"].items()} \
+        if mgr.store.try_get("PodGroup", "default", "xdl") else None  # no gang without the flag
+    assert env is None
+
+
+def test_gang_all_or_nothing(tmp_path):
+    os.environ["KDL_RESTART_BACKOFF_BASE"] = "0.05"
+    m = Manager(ManagerOptions(home=str(tmp_path), gpus=8, gang_scheduler_name="kdl-gang")).start()
+    try:
+        sleep = "import time; time.sleep(2)"
+        for name in ("g1", "g2", "g3"):
+            m.apply(_pt_job(name, sleep, sleep, workers=3, gpus=1))  # 4 GPUs each
+        # two gangs fit (8 GPUs), the third stays pending with no GPU held
+        m.wait_for_condition("PyTorchJob", "default", "g1", ["Running"], timeout=30)
+        m.wait_for_condition("PyTorchJob", "default", "g2", ["Running"], timeout=30)
+        g3 = m.store.get("PyTorchJob", "default", "g3")
+        assert not c.is_running(g3["status"])
+        assert m.allocator.used() == 8
+        pods3 = [p for p in m.store.list("Pod") if p["metadata"]["name"].startswith("g3-")]
+        assert len(pods3) == 4 and all(not p["spec"].get("nodeName") for p in pods3)
+        unsched = [x for p in pods3 for x in p["status"].get("conditions", []) if x.get("reason") == "Unschedulable"]
+        assert unsched
+        pg = m.store.get("PodGroup", "default", "g1")
+        assert pg["spec"]["minMember"] == 4
+        # each running gang sits inside one NUMA half
+        halves = []
+        for name in ("g1", "g2"):
+            gpus = sorted(int(p["metadata"]["annotations"]["kubedl.io/gpus"]) for p in m.store.list("Pod")
+                          if p["metadata"]["name"].startswith(name + "-"))
+            assert gpus in ([0, 1, 2, 3], [4, 5, 6, 7])
+            halves.append(gpus[0])
+        assert sorted(halves) == [0, 4]
+        # after the first gangs finish the third is admitted
+        m.wait_for_condition("PyTorchJob", "default", "g3", ["Succeeded"], timeout=60)
+    finally:
+        m.stop()
+        os.environ.pop("KDL_RESTART_BACKOFF_BASE", None)
+
+
+def test_code_sync_injection_and_git_clone(mgr, tmp_path):
+    import subprocess
+    repo = tmp_path / "src"
+    repo.mkdir()
+    (repo / "hello.py").write_text("print('synced-ok')\n")
+    subprocess.run(["git", "init", "-q", str(repo)], check=True)
+    subprocess.run(["git", "-C", str(repo), "add", "."], check=True)
+    subprocess.run(["git", "-C", str(repo), "-c", "user.email=a@b", "-c", "user.name=n", "commit", "-qm", "x"],
+                   check=True)
+    job = _pt_job("cs", "import runpy; runpy.run_path('src/hello.py')")
+    job["metadata"]["annotations"] = {"kubedl.io/git-sync-config": '{"source": "%s"}' % repo}
+    mgr.apply(job)
+    job = mgr.wait_for_condition("PyTorchJob", "default", "cs", ["Succeeded", "Failed"], timeout=60)
+    assert "Succeeded" in _cond_types(job), job["status"]
+    pod = mgr.store.get("Pod", "default", "cs-master-0")
+    ic = pod["spec"]["initContainers"][0]
+    assert ic["name"] == "git-sync-code" and ic["image"] == "kubedl/git-sync:v1"
+    envs = {e["name"]: e["value"] for e in ic["env"]}
+    assert envs["GIT_SYNC_ROOT"] == "/code" and envs["GIT_SYNC_DEST"] == "src"
+    assert envs["GIT_SYNC_ONE_TIME"] == "true" and envs["GIT_SYNC_MAX_SYNC_FAILURES"] == "3"
+    assert pod["spec"]["containers"][0]["volumeMounts"][-1] == {
+        "name": "git-sync", "readOnly": False, "mountPath": "src", "subPath": "src"}
+    log = open(mgr.kubelet.log_path("default", "cs-master-0")).read()
+    assert "synced-ok" in log
+
+
+def test_metrics_exposition(mgr):
+    from kubedl_amd.metrics import render
+    mgr.apply(_pt_job("m1", "pass"))
+    mgr.wait_for_condition("PyTorchJob", "default", "m1", ["Succeeded"], timeout=30)
+    text = render(mgr.metrics)
+    assert 'kubedl_jobs_created_total{kind="pytorchjob"} 1.0' in text
+    assert 'kubedl_jobs_successful_total{kind="pytorchjob"} 1.0' in text
+    assert "kubedl_jobs_first_pod_launch_delay_seconds_bucket" in text
+    assert 'kubedl_jobs_running{kind="pytorchjob"} 0.0' in text
