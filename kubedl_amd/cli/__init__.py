@@ -1,0 +1,1 @@
+"""``kdl`` command line: manager daemon, kubectl-like client, one-shot runs, benchmarks."""

@@ -162,6 +162,7 @@ class JobController:
         # BackoffStatesQueue: only used to count retries per job (job.go:78-88,119)
         self.backoff_queue = queue or RateLimitingQueue()
         self._lock = threading.Lock()
+        self._launch_marks: Dict[str, set] = {}
 
     # ------------------------------------------------------------ labels/names
     def gen_labels(self, job_name: str) -> Dict[str, str]:
@@ -378,13 +379,24 @@ class JobController:
 
         self.controller.update_job_status(job, replicas, job_status, restart[0])
 
-        if c.is_created(old_status) and c.is_running(job_status) and not c.is_running(old_status):
-            self.metrics.first_pod_launch_delay(active_pods, job, job_status)
-        if (c.total_active(job_status.get("replicaStatuses")) == total_replicas
-                and c.total_active(old_status.get("replicaStatuses")) < total_replicas
-                and not c.is_restarting(old_status)):
-            # pods are re-read: status counts above reflect the latest pod phases
-            self.metrics.all_pods_launch_delay(self.get_pods_for_job(job), job, job_status)
+        # Launch-delay metrics (job.go:242-259).  The reference observes on the
+        # Created->Running / all-active transitions and reads whatever PodReady
+        # condition exists; a rank here becomes Ready only once its process
+        # group is up, which can be after the phase flips, so each histogram is
+        # observed exactly once per job, on the first reconcile where its
+        # condition holds with Ready=True pods (never after a Restarting phase
+        # for all-pods, as in the reference).
+        uid = job["metadata"].get("uid")
+        marks = self._launch_marks.setdefault(uid, set())
+        if "first" not in marks and c.is_created(job_status) and c.is_running(job_status):
+            if self.metrics.first_pod_launch_delay(active_pods, job, job_status) is not None:
+                marks.add("first")
+        if "all" not in marks and not c.is_restarting(old_status) and not c.is_restarting(job_status):
+            if c.total_active(job_status.get("replicaStatuses")) == total_replicas:
+                if self.metrics.all_pods_launch_delay(self.get_pods_for_job(job), job, job_status) is not None:
+                    marks.add("all")
+        elif c.is_restarting(job_status):
+            marks.add("all")
 
         if old_status != job_status:
             self.update_job_status_in_store(job, job_status)

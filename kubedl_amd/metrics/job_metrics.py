@@ -160,7 +160,7 @@ class JobMetrics:
                 return None
             t = _ready_time(pod)
             if t is None:
-                continue
+                return None  # not every rank is Ready yet: observe later
             if t > final:
                 final = t
         delay = final - created
@@ -171,10 +171,16 @@ class JobMetrics:
 
 
 def _ready_time(pod: dict) -> Optional[float]:
+    """lastTransitionTime of a TRUE Ready condition (a False one means the rank
+    has not signalled readiness yet and is not a launch-complete time)."""
     for cond in (pod.get("status") or {}).get("conditions") or []:
-        if cond.get("type") == "Ready":
+        if cond.get("type") == "Ready" and cond.get("status") == "True":
             return c.to_epoch(cond.get("lastTransitionTime"))
     return None
+
+
+def pod_ready(pod: dict) -> bool:
+    return _ready_time(pod) is not None
 
 
 _default: Optional[MetricsRegistry] = None

@@ -180,6 +180,10 @@ class PodWorker(threading.Thread):
                 raw[k] = mounts[v]
         env.update(raw)
         env["HIP_VISIBLE_DEVICES"] = ",".join(self.gpus) if self.gpus else "-1"
+        cpu = str(((ctr.get("resources") or {}).get("limits") or {}).get("cpu", ""))
+        if cpu:  # honour a CPU limit the way a cgroup quota would bound intra-op threads
+            n = float(cpu[:-1]) / 1000.0 if cpu.endswith("m") else float(cpu)
+            env["OMP_NUM_THREADS"] = str(max(1, int(n)))
         env.setdefault("LOCAL_RANK", "0")
         md = self.pod["metadata"]
         labels = md.get("labels") or {}

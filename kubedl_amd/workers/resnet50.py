@@ -107,6 +107,7 @@ def run(args) -> dict:
         "loss": loss, "startup_s": t0 - t_start if False else None,
     }
     common.report_progress(args.warmup + args.steps, res["steps_per_sec"], loss=loss)
+    kdist.shutdown(info)
     return res
 
 
