@@ -227,6 +227,69 @@ void pack_grads(const at::Tensor& chunks, const at::Tensor& src_ptrs, at::Tensor
             "pack_tensors");
 }
 
+// ------------------------------------------------------------------ GBDT
+void gbdt_hist(const at::Tensor& bins, const at::Tensor& grad, const at::Tensor& hess, int64_t gh_stride,
+               const at::Tensor& rows, const at::Tensor& seg, int64_t max_rows_per_node, int64_t num_bins,
+               at::Tensor hist) {
+  TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.dim() == 2 && bins.is_contiguous(),
+              "gbdt_hist: bins must be a contiguous uint8 [N, F] GPU tensor");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && hess.scalar_type() == at::kFloat, "gbdt_hist: g/h fp32");
+  TORCH_CHECK(rows.scalar_type() == at::kInt && seg.scalar_type() == at::kInt && rows.is_contiguous() &&
+                  seg.is_contiguous(),
+              "gbdt_hist: rows/seg must be contiguous int32");
+  const int64_t F = bins.size(1);
+  const int64_t nodes = seg.numel() - 1;
+  TORCH_CHECK(num_bins >= 2 && num_bins <= 256, "gbdt_hist: 2 <= num_bins <= 256");
+  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kFloat && hist.numel() == nodes * F * num_bins * 2,
+              "gbdt_hist: hist must be contiguous fp32 [nodes, F, B, 2]");
+  TORCH_CHECK(grad.numel() >= (bins.size(0) - 1) * gh_stride + 1 && hess.numel() == grad.numel(),
+              "gbdt_hist: grad/hess too small for the row stride");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
+  check_hip(kdl::gbdt_hist_build(bins.data_ptr<uint8_t>(), grad.data_ptr<float>(), hess.data_ptr<float>(),
+                                 gh_stride, rows.data_ptr<int32_t>(), seg.data_ptr<int32_t>(),
+                                 static_cast<int>(nodes), static_cast<int>(max_rows_per_node),
+                                 static_cast<int>(F), static_cast<int>(num_bins), hist.data_ptr<float>(),
+                                 cur_stream()),
+            "gbdt_hist_build");
+}
+
+std::vector<at::Tensor> gbdt_split(const at::Tensor& hist, double lambda, double min_child_weight) {
+  TORCH_CHECK(hist.is_cuda() && hist.dim() == 4 && hist.size(3) == 2 && hist.is_contiguous() &&
+                  hist.scalar_type() == at::kFloat,
+              "gbdt_split: hist must be contiguous fp32 [nodes, F, B, 2]");
+  TORCH_CHECK(hist.size(2) <= 256, "gbdt_split: at most 256 bins");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(hist.device());
+  const int64_t nodes = hist.size(0), F = hist.size(1), B = hist.size(2);
+  auto fo = hist.options();
+  auto gain = at::empty({nodes, F}, fo);
+  auto bin = at::empty({nodes, F}, fo.dtype(at::kInt));
+  auto gl = at::empty({nodes, F}, fo);
+  auto hl = at::empty({nodes, F}, fo);
+  check_hip(kdl::gbdt_split_find(hist.data_ptr<float>(), static_cast<int>(nodes), static_cast<int>(F),
+                                 static_cast<int>(B), static_cast<float>(lambda),
+                                 static_cast<float>(min_child_weight), gain.data_ptr<float>(),
+                                 bin.data_ptr<int32_t>(), gl.data_ptr<float>(), hl.data_ptr<float>(), cur_stream()),
+            "gbdt_split_find");
+  return {gain, bin, gl, hl};
+}
+
+at::Tensor gbdt_route(const at::Tensor& bins, const at::Tensor& rows, const at::Tensor& row_node,
+                      const at::Tensor& split_feat, const at::Tensor& split_bin) {
+  TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.is_contiguous(), "gbdt_route: bins");
+  TORCH_CHECK(rows.scalar_type() == at::kInt && row_node.scalar_type() == at::kInt &&
+                  split_feat.scalar_type() == at::kInt && split_bin.scalar_type() == at::kInt,
+              "gbdt_route: int32 tensors expected");
+  TORCH_CHECK(rows.numel() == row_node.numel(), "gbdt_route: rows/row_node size");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
+  auto out = at::empty_like(rows);
+  check_hip(kdl::gbdt_route_rows(bins.data_ptr<uint8_t>(), rows.data_ptr<int32_t>(), row_node.data_ptr<int32_t>(),
+                                 split_feat.data_ptr<int32_t>(), split_bin.data_ptr<int32_t>(),
+                                 static_cast<int>(bins.size(1)), static_cast<int>(rows.numel()),
+                                 out.data_ptr<int32_t>(), cur_stream()),
+            "gbdt_route_rows");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -239,5 +302,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");
   m.def("cast_copy", &cast_copy, "flat dtype-casting copy");
   m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
+  m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
+  m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
+  m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
   m.attr("arch") = "gfx950";
 }

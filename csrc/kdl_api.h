@@ -60,6 +60,17 @@ struct PackChunk {
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
                         int dtype, float scale, hipStream_t s);
 
+// ---- gbdt.hip (histogram GBDT for the XGBoostJob worker)
+hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
+                           const int32_t* rows, const int32_t* seg, int num_nodes, int max_rows_per_node,
+                           int F, int B, float* hist, hipStream_t s);
+hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float lambda,
+                           float min_child_weight, float* best_gain, int32_t* best_bin, float* best_gl,
+                           float* best_hl, hipStream_t s);
+hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32_t* row_node,
+                           const int32_t* split_feat, const int32_t* split_bin, int F, int n,
+                           int32_t* go_right, hipStream_t s);
+
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 
 }  // namespace kdl
