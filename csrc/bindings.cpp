@@ -290,6 +290,95 @@ at::Tensor gbdt_route(const at::Tensor& bins, const at::Tensor& rows, const at::
   return out;
 }
 
+// ------------------------------------------------------------------ CTR
+at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool relu) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+              "gemm_bias_act: bf16 GPU operands");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "gemm_bias_act: A [M,K], W [N,K]");
+  TORCH_CHECK(a.is_contiguous() && w.is_contiguous(), "gemm_bias_act: contiguous operands");
+  TORCH_CHECK(a.size(1) % 8 == 0, "gemm_bias_act: K must be a multiple of 8 (16-byte rows)");
+  const int64_t M = a.size(0), N = w.size(0), K = a.size(1);
+  const float* bp = nullptr;
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b.numel() == N, "gemm_bias_act: bias size");
+    bp = b.data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto c = at::empty({M, N}, a.options());
+  check_hip(kdl::gemm_bias_act(a.data_ptr(), w.data_ptr(), bp, c.data_ptr(), static_cast<int>(M),
+                               static_cast<int>(N), static_cast<int>(K), relu, cur_stream()),
+            "gemm_bias_act");
+  return c;
+}
+
+std::vector<at::Tensor> relu_bwd_dbias(const at::Tensor& dy, const c10::optional<at::Tensor>& y) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.is_contiguous(),
+              "relu_bwd_dbias: dy bf16 [M,N] contiguous");
+  TORCH_CHECK(dy.size(1) % 8 == 0, "relu_bwd_dbias: N % 8 == 0");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  const bool has_y = y.has_value() && y->defined();
+  at::Tensor dz = has_y ? at::empty_like(dy) : dy;
+  if (has_y) TORCH_CHECK(y->sizes() == dy.sizes() && y->is_contiguous(), "relu_bwd_dbias: y shape");
+  auto db = at::zeros({dy.size(1)}, dy.options().dtype(at::kFloat));
+  check_hip(kdl::relu_bwd_dbias(dy.data_ptr(), has_y ? y->data_ptr() : nullptr, dz.data_ptr(), db.data_ptr<float>(),
+                                static_cast<int>(dy.size(0)), static_cast<int>(dy.size(1)), cur_stream()),
+            "relu_bwd_dbias");
+  return {dz, db};
+}
+
+void embed_gather(const at::Tensor& table, const at::Tensor& idx, int64_t F, at::Tensor out, int64_t col0) {
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous(), "embed_gather: table [V, D]");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous(), "embed_gather: int64 idx");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == table.scalar_type(), "embed_gather: out");
+  const int64_t D = table.size(1), n = idx.numel();
+  TORCH_CHECK(n % F == 0 && out.size(0) * F == n && col0 + F * D <= out.size(1), "embed_gather: shapes");
+  TORCH_CHECK((D * table.element_size()) % 16 == 0 && (out.stride(0) * out.element_size()) % 16 == 0 &&
+                  (col0 * out.element_size()) % 16 == 0,
+              "embed_gather: rows must be 16-byte multiples");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  check_hip(kdl::embed_gather(table.data_ptr(), dtype_code(table), idx.data_ptr<int64_t>(), static_cast<int>(n),
+                              static_cast<int>(F), static_cast<int>(D), out.data_ptr(),
+                              static_cast<int>(out.stride(0)), static_cast<int>(col0), cur_stream()),
+            "embed_gather");
+}
+
+at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64_t D, const at::Tensor& order,
+                          const at::Tensor& seg) {
+  TORCH_CHECK(rows.is_cuda() && rows.dim() == 2 && rows.stride(1) == 1, "segment_reduce: rows [B, ld]");
+  TORCH_CHECK(order.scalar_type() == at::kLong && seg.scalar_type() == at::kLong && order.is_contiguous() &&
+                  seg.is_contiguous(),
+              "segment_reduce: int64 order/seg");
+  TORCH_CHECK(order.numel() == rows.size(0) * F && col0 + F * D <= rows.size(1), "segment_reduce: shapes");
+  const int64_t U = seg.numel() - 1;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(rows.device());
+  auto out = at::empty({U, D}, rows.options().dtype(at::kFloat));
+  check_hip(kdl::segment_reduce(rows.data_ptr(), dtype_code(rows), static_cast<int>(F), static_cast<int>(rows.stride(0)),
+                                static_cast<int>(col0), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
+                                static_cast<int>(U), static_cast<int>(D), out.data_ptr<float>(), cur_stream()),
+            "segment_reduce");
+  return out;
+}
+
+void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at::Tensor& seg,
+                     const at::Tensor& rows_local, at::Tensor table, at::Tensor accum, double lr, double eps,
+                     double scale) {
+  TORCH_CHECK(grads.is_cuda() && grads.scalar_type() == at::kFloat && grads.is_contiguous(), "segment_adagrad: grads");
+  TORCH_CHECK(table.scalar_type() == at::kFloat && accum.scalar_type() == at::kFloat && table.is_contiguous() &&
+                  accum.is_contiguous() && table.sizes() == accum.sizes(),
+              "segment_adagrad: fp32 table/accum");
+  TORCH_CHECK(grads.size(1) == table.size(1), "segment_adagrad: D mismatch");
+  TORCH_CHECK(rows_local.numel() == seg.numel() - 1 && order.numel() == grads.size(0), "segment_adagrad: shapes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  check_hip(kdl::segment_adagrad(grads.data_ptr<float>(), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
+                                 rows_local.data_ptr<int64_t>(), static_cast<int>(seg.numel() - 1),
+                                 static_cast<int>(table.size(1)), table.data_ptr<float>(), accum.data_ptr<float>(),
+                                 static_cast<float>(lr), static_cast<float>(eps), static_cast<float>(scale),
+                                 cur_stream()),
+            "segment_adagrad");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -305,5 +394,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
+  m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b)");
+  m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient");
+  m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
+  m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
+  m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.attr("arch") = "gfx950";
 }

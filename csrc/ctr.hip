@@ -1,0 +1,333 @@
+// CTR (XDLJob) data-plane kernels for gfx950: MFMA GEMM with fused bias+ReLU,
+// embedding row gather, and sort-based sparse gradient reduction fused with
+// the Adagrad update (no atomics: deterministic).
+//
+// gemm_bias_act:  C[M,N] = act(A[M,K] . B[N,K]^T + bias[N]) in bf16, fp32
+//   accumulation on v_mfma_f32_32x32x16_bf16.  Both operands are K-contiguous
+//   (A row-major activations, B = nn.Linear weight [out, in]), so every MFMA
+//   fragment row (8 consecutive k of one row) is one 16-byte LDS read.
+//   Tile 128x128x64, 256 threads = 4 waves as 2x2, each wave 64x64 = 2x2
+//   MFMA 32x32 blocks (4 x 16 accumulator VGPRs).  Register-staged double
+//   buffering: the next k-tile's global loads are issued before the MFMAs
+//   of the current one and written to the other LDS buffer after them.
+//   LDS rows are padded to 72 bf16 (144 B): lanes 0..31 of a 32x32 fragment
+//   read rows r with bank slot 9r mod 16 -> every 16-lane ds_read_b128 group
+//   hits 16 distinct slots (conflict-free) without breaking 16-B alignment.
+//   The blockIdx -> tile map keeps 8 consecutive N-tiles of one M-row panel
+//   on consecutive block ids (the A panel is re-read from L2 by its N-tiles).
+// embed_gather:   out[b, col0 + f*D : +D] = table[idx[b*F+f], :] (bf16 / f32),
+//   one wave per output row, 16-byte vector loads.
+// segment_reduce / segment_adagrad: rows sorted by key; one wave per unique
+//   key sums its segment (fixed order -> bitwise reproducible) and either
+//   writes the sum or applies Adagrad to the owned table row in place.
+#include "common.h"
+#include "kdl_api.h"
+
+namespace kdl {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int LDA = BK + 8;  // padded LDS row (bf16 elements)
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ uint4 ld16_or_zero(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+}
+
+template <bool RELU, bool HAS_BIAS>
+__global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, const float* __restrict__ bias,
+    bf16_t* __restrict__ C, int M, int N, int K, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][BM * LDA];  // [buf][A|B][rows*LDA]
+  // block -> (tile_m, tile_n): groups of 8 N-tiles share one A panel
+  const int bid = blockIdx.x;
+  const int group = 8;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int per_group = group * tiles_m;
+  const int g = bid / per_group;
+  const int first_n = g * group;
+  const int gsize = (tiles_n - first_n) < group ? (tiles_n - first_n) : group;
+  const int in_g = bid % per_group;
+  const int tile_m = in_g / gsize;
+  const int tile_n = first_n + in_g % gsize;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  // staging: each thread moves 4 x 16 B of A and of B per k-tile
+  // (128 rows x 8 chunks = 1024 chunks / 256 threads)
+  int srow[4], schunk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cidx = t + i * kThreads;
+    srow[i] = cidx >> 3;
+    schunk[i] = cidx & 7;
+  }
+  uint4 ra[4], rb[4];
+  const int nk = (K + BK - 1) / BK;
+
+  auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = k0 + schunk[i] * 8;
+      const int am = m0 + srow[i], bn = n0 + srow[i];
+      ra[i] = ld16_or_zero(A + static_cast<int64_t>(am) * K + kk, am < M && kk < K);
+      rb[i] = ld16_or_zero(B + static_cast<int64_t>(bn) * K + kk, bn < N && kk < K);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<uint4*>(&lds[buf][0][srow[i] * LDA + schunk[i] * 8]) = ra[i];
+      *reinterpret_cast<uint4*>(&lds[buf][1][srow[i] * LDA + schunk[i] * 8]) = rb[i];
+    }
+  };
+
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int fr = lane & 31, fh = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8_t af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&lds[cur][0][(wm + i * 32 + fr) * LDA + s * 16 + fh * 8]);
+        af[i] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&lds[cur][1][(wn + j * 32 + fr) * LDA + s * 16 + fh * 8]);
+        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    // buf cur^1 was last read in iteration kt-1, which ended with a barrier
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn + j * 32 + fr;
+    float bv = 0.f;
+    if (HAS_BIAS && col < N) bv = bias[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        if (row < M && col < N) {
+          float v = acc[i][j][r] + bv;
+          if (RELU) v = v > 0.f ? v : 0.f;
+          C[static_cast<int64_t>(row) * N + col] = f32_to_bf16(v);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- ReLU backward + dbias
+// dz = dy * (y > 0) (bf16 out), dbias[n] += sum_m dz[m, n]; 16 B along N per lane.
+__global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ y,
+                                                             bf16_t* __restrict__ dz, float* __restrict__ dbias,
+                                                             int M, int N, int rows_per_block) {
+  const int cg = blockIdx.y * 32 + (threadIdx.x & 31);  // 8-column group
+  const int r0 = threadIdx.x >> 5;                        // 8 row lanes
+  if (cg * 8 >= N) return;
+  float s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = 0.f;
+  const int mb = blockIdx.x * rows_per_block;
+  const int me = (mb + rows_per_block) < M ? (mb + rows_per_block) : M;
+  for (int m = mb + r0; m < me; m += 8) {
+    float g[8], yy[8];
+    const int64_t o = static_cast<int64_t>(m) * N + cg * 8;
+    Vec<bf16_t, 8>::load(dy + o, g);
+    if (y != nullptr) {
+      Vec<bf16_t, 8>::load(y + o, yy);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
+      Vec<bf16_t, 8>::store(dz + o, g);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += g[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (s[i] != 0.f) __hip_atomic_fetch_add(dbias + cg * 8 + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------- embeddings
+template <typename T>
+__global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__ table, const int64_t* __restrict__ idx,
+                                                           int n, int F, int D, T* __restrict__ out, int ld_out,
+                                                           int col0) {
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= n) return;
+  const int b = wave / F, f = wave % F;
+  const T* src = table + idx[wave] * static_cast<int64_t>(D);
+  T* dst = out + static_cast<int64_t>(b) * ld_out + col0 + f * D;
+  constexpr int VEC = 16 / sizeof(T);
+  for (int c = lane * VEC; c < D; c += 64 * VEC) {
+    if (c + VEC <= D) {
+      *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(src + c);
+    } else {
+      for (int k = c; k < D; ++k) dst[k] = src[k];
+    }
+  }
+}
+
+// Row j = b*F + f of a [B, ld] activation-gradient matrix lives at
+// rows + b*ld + col0 + f*D (the layout embed_gather wrote).  Rows order[j]
+// are summed per segment [seg[u], seg[u+1]); one wave per segment.
+template <typename T>
+__global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, int ld, int col0,
+                                                             const int64_t* __restrict__ order,
+                                                             const int64_t* __restrict__ seg, int U, int D,
+                                                             float* __restrict__ out) {
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (u >= U) return;
+  const int64_t s0 = seg[u], s1 = seg[u + 1];
+  for (int c = lane * 4; c < D; c += 256) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int64_t j = s0; j < s1; ++j) {
+      const int64_t jj = order[j];
+      const T* r = rows + (jj / F) * static_cast<int64_t>(ld) + col0 + (jj % F) * D + c;
+      a0 += Vec1<T>::ld(r);
+      if (c + 1 < D) a1 += Vec1<T>::ld(r + 1);
+      if (c + 2 < D) a2 += Vec1<T>::ld(r + 2);
+      if (c + 3 < D) a3 += Vec1<T>::ld(r + 3);
+    }
+    float* o = out + static_cast<int64_t>(u) * D + c;
+    o[0] = a0;
+    if (c + 1 < D) o[1] = a1;
+    if (c + 2 < D) o[2] = a2;
+    if (c + 3 < D) o[3] = a3;
+  }
+}
+
+// Owner side: sum the received gradient rows of each unique local row and
+// apply Adagrad in place: acc += g^2; w -= lr * g / (sqrt(acc) + eps).
+__global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __restrict__ grads,
+                                                              const int64_t* __restrict__ order,
+                                                              const int64_t* __restrict__ seg,
+                                                              const int64_t* __restrict__ rows_local, int U, int D,
+                                                              float* __restrict__ table, float* __restrict__ accum,
+                                                              float lr, float eps, float scale) {
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (u >= U) return;
+  const int64_t s0 = seg[u], s1 = seg[u + 1];
+  const int64_t row = rows_local[u];
+  float* w = table + row * static_cast<int64_t>(D);
+  float* a = accum + row * static_cast<int64_t>(D);
+  for (int c = lane * 4; c < D; c += 256) {
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t j = s0; j < s1; ++j) {
+      const float* r = grads + order[j] * static_cast<int64_t>(D) + c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < D) g[k] += r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (c + k >= D) continue;
+      const float gk = g[k] * scale;
+      const float ak = a[c + k] + gk * gk;
+      a[c + k] = ak;
+      w[c + k] -= lr * gk / (sqrtf(ak) + eps);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, bool relu,
+                         hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  dim3 grid(tiles_n * tiles_m);
+  auto a = static_cast<const bf16_t*>(A);
+  auto b = static_cast<const bf16_t*>(B);
+  auto c = static_cast<bf16_t*>(C);
+  if (relu && bias)
+    hipLaunchKernelGGL((gemm_bias_act_kernel<true, true>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K, tiles_n);
+  else if (relu)
+    hipLaunchKernelGGL((gemm_bias_act_kernel<true, false>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K, tiles_n);
+  else if (bias)
+    hipLaunchKernelGGL((gemm_bias_act_kernel<false, true>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_bias_act_kernel<false, false>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K,
+                       tiles_n);
+  return hipGetLastError();
+}
+
+hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* dbias, int M, int N, hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int rows_per_block = 256;
+  dim3 grid((M + rows_per_block - 1) / rows_per_block, (N / 8 + 31) / 32);
+  hipLaunchKernelGGL(relu_bwd_dbias_kernel, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dy),
+                     static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dz), dbias, M, N, rows_per_block);
+  return hipGetLastError();
+}
+
+hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
+                        int col0, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  dim3 grid((n + 3) / 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL((embed_gather_kernel<bf16_t>), grid, dim3(256), 0, s, static_cast<const bf16_t*>(table), idx,
+                       n, F, D, static_cast<bf16_t*>(out), ld_out, col0);
+  else
+    hipLaunchKernelGGL((embed_gather_kernel<float>), grid, dim3(256), 0, s, static_cast<const float*>(table), idx, n,
+                       F, D, static_cast<float*>(out), ld_out, col0);
+  return hipGetLastError();
+}
+
+hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
+                          const int64_t* seg, int U, int D, float* out, hipStream_t s) {
+  if (U <= 0) return hipSuccess;
+  dim3 grid((U + 3) / 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL((segment_reduce_kernel<bf16_t>), grid, dim3(256), 0, s, static_cast<const bf16_t*>(rows), F,
+                       ld, col0, order, seg, U, D, out);
+  else
+    hipLaunchKernelGGL((segment_reduce_kernel<float>), grid, dim3(256), 0, s, static_cast<const float*>(rows), F, ld,
+                       col0, order, seg, U, D, out);
+  return hipGetLastError();
+}
+
+hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
+                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s) {
+  if (U <= 0) return hipSuccess;
+  hipLaunchKernelGGL(segment_adagrad_kernel, dim3((U + 3) / 4), dim3(256), 0, s, grads, order, seg, rows_local, U, D,
+                     table, accum, lr, eps, scale);
+  return hipGetLastError();
+}
+
+}  // namespace kdl

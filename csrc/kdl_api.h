@@ -71,6 +71,17 @@ hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32
                            const int32_t* split_feat, const int32_t* split_bin, int F, int n,
                            int32_t* go_right, hipStream_t s);
 
+// ---- ctr.hip (XDLJob CTR model: MFMA GEMM, embeddings, sparse Adagrad)
+hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, bool relu,
+                         hipStream_t s);
+hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* dbias, int M, int N, hipStream_t s);
+hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
+                        int col0, hipStream_t s);
+hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
+                          const int64_t* seg, int U, int D, float* out, hipStream_t s);
+hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
+                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s);
+
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 
 }  // namespace kdl

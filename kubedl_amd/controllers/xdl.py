@@ -45,6 +45,7 @@ class XDLJobReconciler(BaseReconciler):
 
     def set_cluster_spec(self, job: dict, pod_template: dict, rtype: str, index: str) -> None:
         uid = job["metadata"]["uid"]
+        rdzv = self._rendezvous_env(job, rtype, int(index))
         for ctr in (pod_template.setdefault("spec", {}).get("containers") or []):
             env = ctr.setdefault("env", [])
             for e in env:
@@ -53,6 +54,33 @@ class XDLJobReconciler(BaseReconciler):
                     e["value"] = v + uid if v.endswith("/") else v + "/" + uid
             env.append({"name": TASK_NAME, "value": rtype.lower()})
             env.append({"name": TASK_INDEX, "value": index})
+            env.extend(rdzv)
+
+    @staticmethod
+    def _rendezvous_env(job: dict, rtype: str, index: int):
+        """[NEW] collective rendezvous for the bundled CTR worker (no ZooKeeper on
+        the node): PS, Worker, ExtendRole ranks form one process group in that
+        order; the Scheduler is not a member.  The endpoint is the first
+        member's Service, resolved to 127.0.0.1:<hostPort> by the runtime."""
+        specs = K.replica_specs(job)
+        order = [t for t in (K.XDL_PS, K.XDL_WORKER, K.XDL_EXTEND) if t in specs]
+        base, rank = 0, -1
+        for t in order:
+            if t.lower() == rtype.lower():
+                rank = base + index
+            base += c.replicas_of(specs[t])
+        if not order:
+            return []
+        first = order[0]
+        try:
+            port = c.port_from_job(specs, first, "xdl", "xdljob-port")
+        except LookupError:
+            port = 2222
+        host = c.gen_general_name(job["metadata"]["name"], first.lower(), "0")
+        n_ps = c.replicas_of(specs[K.XDL_PS]) if K.XDL_PS in specs else 0
+        return [{"name": "KDL_RANK", "value": str(rank)}, {"name": "KDL_WORLD_SIZE", "value": str(base)},
+                {"name": "KDL_NUM_PS", "value": str(n_ps)},
+                {"name": "KDL_RDZV_ENDPOINT", "value": f"{host}:{port}"}]
 
     def update_job_status(self, job, replicas, status, restart) -> None:
         name = job["metadata"]["name"]

@@ -1,0 +1,240 @@
+"""Sparse-embedding CTR model for the XDLJob data plane.
+
+XDL (the reference's XDLJob payload, ``example/xdl/xdl_job_mnist.yaml``) trains
+click-through-rate models whose sparse embeddings live on parameter servers.
+MI355X-first re-design:
+
+* **Embedding shards on GPUs, collective push/pull.**  The PS role becomes
+  "owner of a row shard" (row ``id % n_owners``): a pull is an RCCL
+  all-to-all of de-duplicated ids to their owners, a HIP row gather on the
+  owner (``embed_gather``), and an all-to-all of the rows back; a push is the
+  reverse with the owner summing duplicate contributions and applying the
+  sparse optimizer in ONE kernel (``segment_adagrad``: sort-based segment
+  sum + Adagrad on the owned rows, no atomics, bitwise reproducible).  With
+  PS replicas in the job the PS ranks own the shards; without, the workers do.
+* **De-duplication before communication.**  Each worker ``torch.unique``s
+  its batch ids; gradient rows of repeated ids are pre-summed locally
+  (``segment_reduce``) so only one row per unique id crosses xGMI.
+* **Dense tower on MFMA.**  ``FusedLinear`` runs forward as the hand-written
+  ``gemm_bias_act`` kernel (v_mfma_f32_32x32x16_bf16, bias + ReLU fused in the
+  epilogue); backward fuses ReLU-mask + bias-gradient (``relu_bwd_dbias``) and
+  uses hipBLASLt for the two plain GEMMs.
+
+On CPU (tests) every op has a torch composition with the same semantics.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from kubedl_amd.ops import _ext
+
+
+# ---------------------------------------------------------------- dense tower
+class _FusedLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        ext = _ext.load()
+        y = ext.gemm_bias_act(x.contiguous(), w.contiguous(), b, bool(relu))
+        ctx.save_for_backward(x, w, y)
+        ctx.relu = relu
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        ext = _ext.load()
+        dy = dy.contiguous()
+        dz, db = ext.relu_bwd_dbias(dy, y if ctx.relu else None)
+        dx = dz @ w
+        dw = dz.t() @ x
+        return dx, dw, (db.to(w.dtype) if ctx.has_b else None), None
+
+
+def fused_linear(x, w, b=None, relu=False):
+    if x.is_cuda and _ext.available() and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+        return _FusedLinearFn.apply(x, w, b, relu)
+    if x.is_cuda and not _ext.available():
+        _ext.require_on_gpu("fused_linear")
+    y = torch.nn.functional.linear(x, w, b)
+    return torch.relu(y) if relu else y
+
+
+class FusedLinear(nn.Module):
+    def __init__(self, fin: int, fout: int, relu: bool):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.bias = nn.Parameter(torch.zeros(fout))
+        self.relu = relu
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+
+    def forward(self, x):
+        return fused_linear(x, self.weight, self.bias, self.relu)
+
+
+class DenseTower(nn.Module):
+    def __init__(self, fin: int, hidden=(1024, 512, 256)):
+        super().__init__()
+        dims = [fin] + list(hidden)
+        self.layers = nn.ModuleList([FusedLinear(a, b, True) for a, b in zip(dims[:-1], dims[1:])])
+        self.head = nn.Linear(dims[-1], 1)
+
+    def forward(self, x):
+        for l in self.layers:
+            x = l(x)
+        return self.head(x).float().squeeze(-1)
+
+
+# ---------------------------------------------------------------- sparse embedding
+def _a2a(out_splits: List[int], in_splits: List[int], t: torch.Tensor, group) -> torch.Tensor:
+    out = t.new_empty((sum(out_splits),) + tuple(t.shape[1:]))
+    dist.all_to_all_single(out, t.contiguous(), out_splits, in_splits, group=group)
+    return out
+
+
+class ShardedEmbedding:
+    """One logical [vocab, dim] fp32 table sharded by ``id % n_owners`` across
+    the owner ranks of ``group``; Adagrad state lives next to each shard."""
+
+    def __init__(self, vocab: int, dim: int, owners: List[int], rank: int, world: int, device,
+                 group=None, lr: float = 0.05, eps: float = 1e-8, init_std: float = 0.01, seed: int = 0):
+        self.vocab, self.dim = vocab, dim
+        self.owners = list(owners)
+        self.n_own = len(owners)
+        self.rank, self.world = rank, world
+        self.device = torch.device(device)
+        self.group = group
+        self.lr, self.eps = lr, eps
+        self.is_owner = rank in self.owners
+        self.me = self.owners.index(rank) if self.is_owner else -1
+        rows = (vocab - self.me + self.n_own - 1) // self.n_own if self.is_owner else 0
+        g = torch.Generator(device="cpu").manual_seed(seed + 7919 * max(self.me, 0))
+        self.table = (torch.randn(rows, dim, generator=g) * init_std).to(self.device)
+        self.accum = torch.zeros(rows, dim, device=self.device)
+        self.use_hip = self.device.type == "cuda" and _ext.available()
+        self._ctx = None
+
+    # ------------------------------------------------------------ helpers
+    def _local_gather(self, local_rows: torch.Tensor) -> torch.Tensor:
+        if local_rows.numel() == 0:
+            return self.table.new_empty(0, self.dim)
+        if self.use_hip:
+            out = self.table.new_empty(local_rows.numel(), self.dim)
+            _ext.load().embed_gather(self.table, local_rows.contiguous(), 1, out, 0)
+            return out
+        return self.table[local_rows]
+
+    def _apply_updates(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:
+        """Sum duplicate rows and apply Adagrad on the owned shard."""
+        if ids_local.numel() == 0:
+            return
+        uniq, inv = torch.unique(ids_local, return_inverse=True)
+        order = torch.argsort(inv, stable=True)
+        counts = torch.bincount(inv, minlength=uniq.numel())
+        seg = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=self.device)
+        seg[1:] = torch.cumsum(counts, 0)
+        if self.use_hip:
+            _ext.load().segment_adagrad(grads.contiguous().float(), order, seg, uniq, self.table, self.accum,
+                                        self.lr, self.eps, scale)
+            return
+        g = torch.zeros(uniq.numel(), self.dim, device=self.device).index_add_(0, inv, grads.float()) * scale
+        a = self.accum[uniq] + g * g
+        self.accum[uniq] = a
+        self.table[uniq] -= self.lr * g / (a.sqrt() + self.eps)
+
+    # ------------------------------------------------------------ pull / push
+    def pull(self, ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """ids [n] int64 (any, may repeat) -> (unique rows [U, dim], inverse [n])."""
+        uniq, inv = torch.unique(ids, return_inverse=True)
+        owner = uniq % self.n_own
+        order = torch.argsort(owner, stable=True)
+        uniq_sorted = uniq[order]
+        send_counts = torch.bincount(owner, minlength=self.n_own)
+        if self.world == 1 or self.group is None and not dist.is_initialized():
+            rows = self._local_gather(uniq_sorted // self.n_own)
+            emb = torch.empty_like(rows)
+            emb[order] = rows
+            self._ctx = (uniq_sorted, order, None, None)
+            return emb, inv
+        # counts per destination RANK (owners are a subset of ranks)
+        full_send = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        full_send[torch.tensor(self.owners, device=self.device)] = send_counts
+        full_recv = torch.empty_like(full_send)
+        dist.all_to_all_single(full_recv, full_send, group=self.group)
+        send_l, recv_l = full_send.tolist(), full_recv.tolist()
+        req = _a2a(recv_l, send_l, uniq_sorted, self.group)           # ids asked of me
+        rows = self._local_gather(req // self.n_own) if self.is_owner else self.table.new_empty(0, self.dim)
+        got = _a2a(send_l, recv_l, rows, self.group)                    # rows for my ids
+        emb = torch.empty_like(got)
+        emb[order] = got
+        self._ctx = (uniq_sorted, order, send_l, recv_l, req)
+        return emb, inv
+
+    def push(self, grad_unique: torch.Tensor, scale: float = 1.0) -> None:
+        """grad rows aligned with the unique ids of the last pull."""
+        ctx = self._ctx
+        uniq_sorted, order = ctx[0], ctx[1]
+        g_sorted = grad_unique[order]
+        if ctx[2] is None:
+            self._apply_updates(uniq_sorted // self.n_own, g_sorted, scale)
+            return
+        send_l, recv_l, req = ctx[2], ctx[3], ctx[4]
+        g_recv = _a2a(recv_l, send_l, g_sorted.float(), self.group)
+        if self.is_owner:
+            self._apply_updates(req // self.n_own, g_recv, scale)
+
+    def participate(self) -> None:
+        """An owner without a batch of its own (PS rank) serves one pull+push round."""
+        empty = torch.empty(0, dtype=torch.int64, device=self.device)
+        self.pull(empty)
+        self.push(torch.empty(0, self.dim, device=self.device))
+
+
+# ---------------------------------------------------------------- model
+class CTRModel:
+    """Embeddings (F fields x dim) + dense features -> MLP tower -> logit."""
+
+    def __init__(self, n_fields: int, vocab_per_field: int, dim: int, n_dense: int, hidden, emb: ShardedEmbedding,
+                 device, dtype=torch.bfloat16):
+        self.F, self.V, self.D, self.nd = n_fields, vocab_per_field, dim, n_dense
+        self.k_in = n_fields * dim + n_dense
+        self.k_pad = (self.k_in + 7) // 8 * 8
+        self.emb = emb
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tower = DenseTower(self.k_pad, hidden).to(self.device)
+        with torch.no_grad():
+            for p in self.tower.parameters():
+                p.data = p.data.to(dtype)
+        self.field_off = (torch.arange(n_fields, device=self.device) * vocab_per_field)[None, :]
+
+    def build_input(self, ids: torch.Tensor, dense: torch.Tensor):
+        B = ids.shape[0]
+        gids = (ids + self.field_off).reshape(-1)
+        emb_u, inv = self.emb.pull(gids)
+        x = torch.zeros(B, self.k_pad, dtype=self.dtype, device=self.device)
+        emb_u_c = emb_u.to(self.dtype).contiguous()
+        if self.device.type == "cuda" and _ext.available():
+            _ext.load().embed_gather(emb_u_c, inv.contiguous(), self.F, x, 0)
+        else:
+            x[:, : self.F * self.D] = emb_u_c[inv].reshape(B, self.F * self.D)
+        x[:, self.F * self.D: self.k_in] = dense.to(self.dtype)
+        return x, inv, emb_u.shape[0]
+
+    def push_grads(self, xgrad: torch.Tensor, inv: torch.Tensor, U: int, scale: float) -> None:
+        B = xgrad.shape[0]
+        order = torch.argsort(inv, stable=True)
+        counts = torch.bincount(inv, minlength=U)
+        seg = torch.zeros(U + 1, dtype=torch.int64, device=self.device)
+        seg[1:] = torch.cumsum(counts, 0)
+        if self.device.type == "cuda" and _ext.available():
+            g_u = _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg)
+        else:
+            rows = xgrad[:, : self.F * self.D].reshape(B * self.F, self.D).float()
+            g_u = torch.zeros(U, self.D, device=self.device).index_add_(0, inv, rows)
+        self.emb.push(g_u, scale)

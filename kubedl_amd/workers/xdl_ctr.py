@@ -1,0 +1,162 @@
+"""XDLJob worker: sparse-embedding CTR training with PS / Worker / Scheduler roles.
+
+Role mapping (env from the XDL controller: ``TASK_NAME``, ``TASK_INDEX``,
+``ZK_ADDR`` + the runtime's ``KDL_RANK`` / ``KDL_WORLD_SIZE`` /
+``KDL_NUM_PS`` / ``KDL_RDZV_ENDPOINT``):
+
+* ``ps``        -- owns a row shard of every embedding table on its GPU and
+                   serves pull/push rounds (``ShardedEmbedding.participate``);
+* ``worker`` / ``extendrole`` -- generate a batch, pull embeddings, run the
+                   MFMA dense tower, push de-duplicated sparse gradients, and
+                   all-reduce dense gradients among workers (fused Adam);
+* ``scheduler`` -- coordination only: signals Ready and idles until the job
+                   completes (its pod is removed by cleanPodPolicy=Running).
+
+Without PS replicas the workers own the shards themselves.  Synthetic data:
+``--fields`` categorical fields with Zipf-distributed ids over
+``--vocab`` rows each, ``--dense`` dense features, labels from a hidden
+logistic model (so the loss visibly falls).  Prints one JSON line from the
+first worker: samples/s, steps/s, loss.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import os
+import signal
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from kubedl_amd.models.ctr import CTRModel, ShardedEmbedding
+from kubedl_amd.ops.optim import FlatParamSpace, FusedAdam
+from kubedl_amd.parallel.ddp import FlatDDP
+from kubedl_amd.workers import common
+
+
+def synth_batch(B, F, V, nd, gen, device, w_true):
+    # Zipf-like ids: heavy head, long tail (what makes de-duplication pay)
+    u = torch.rand(B, F, generator=gen)
+    ids = (V * u.pow(3.0)).long().clamp_(max=V - 1)
+    dense = torch.randn(B, nd, generator=gen)
+    logit = (w_true[ids % w_true.numel()].sum(1) * 0.5 + dense[:, 0]).clamp(-8, 8)
+    y = (torch.rand(B, generator=gen) < torch.sigmoid(logit)).float()
+    return ids.to(device), dense.to(device), y.to(device)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--fields", type=int, default=26)
+    ap.add_argument("--vocab", type=int, default=100000, help="rows per field")
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--dense", type=int, default=16)
+    ap.add_argument("--hidden", default="1024,512,256")
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--emb-lr", type=float, default=0.05)
+    ap.add_argument("--cpu", action="store_true")
+    args, _unknown = ap.parse_known_args(argv)
+
+    task = os.environ.get("TASK_NAME", "worker").lower()
+    if task == "scheduler":
+        common.signal_ready({"task": task})
+        stop = []
+        signal.signal(signal.SIGTERM, lambda *_: stop.append(1))
+        while not stop:
+            time.sleep(0.2)
+        return 0
+
+    rank = int(os.environ.get("KDL_RANK", os.environ.get("RANK", "0")))
+    world = int(os.environ.get("KDL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    n_ps = int(os.environ.get("KDL_NUM_PS", "0"))
+    ep = os.environ.get("KDL_RDZV_ENDPOINT")
+    if ep:
+        host, port = ep.rsplit(":", 1)
+        os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = host, port
+    use_gpu = (not args.cpu) and torch.cuda.is_available()
+    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    backend = "nccl" if use_gpu else "gloo"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+        if use_gpu:
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    common.signal_ready({"rank": rank, "task": task})
+    owners = list(range(n_ps)) if n_ps > 0 else list(range(world))
+    workers = [r for r in range(world) if r >= n_ps]
+    wgroup = dist.new_group(workers) if world > 1 else None
+    is_worker = rank in workers
+    emb = ShardedEmbedding(args.fields * args.vocab, args.dim, owners, rank, world, device,
+                           group=None, lr=args.emb_lr)
+    total = args.warmup + args.steps
+    if not is_worker:  # PS: serve pull/push rounds
+        for _ in range(total):
+            emb.participate()
+        dist.barrier()
+        dist.destroy_process_group()
+        return 0
+
+    hidden = tuple(int(h) for h in args.hidden.split(","))
+    torch.manual_seed(0)
+    model = CTRModel(args.fields, args.vocab, args.dim, args.dense, hidden, emb, device)
+    space = FlatParamSpace(model.tower, dtype=torch.bfloat16, device=device)
+    ddp = FlatDDP(space, len(workers), process_group=wgroup, broadcast_from=workers[0])
+    opt = FusedAdam(space, lr=args.lr)
+    opt.grad_scale = ddp.grad_scale
+    gen = torch.Generator().manual_seed(100 + rank)
+    w_true = torch.randn(4096, generator=torch.Generator().manual_seed(7)) * 0.5
+    bce = torch.nn.BCEWithLogitsLoss()
+    losses = []
+    t0 = None
+    for it in range(total):
+        if it == args.warmup:
+            if use_gpu:
+                torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier(group=wgroup)
+            t0 = time.perf_counter()
+        ids, dense, y = synth_batch(args.batch, args.fields, args.vocab, args.dense, gen, device, w_true)
+        space.zero_grad()
+        x, inv, U = model.build_input(ids, dense)
+        x.requires_grad_(True)
+        logit = model.tower(x)
+        loss = bce(logit, y)
+        loss.backward()
+        model.push_grads(x.grad, inv, U, scale=1.0 / len(workers))
+        ddp.finish()
+        opt.step()
+        losses.append(loss.detach())
+        common.report_progress(it + 1)
+    if use_gpu:
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0 if t0 is not None else 0.0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=wgroup)
+        dt = float(t.item())
+    first = float(torch.stack(losses[:5]).float().mean())
+    last = float(torch.stack(losses[-5:]).float().mean())
+    if rank == workers[0]:
+        print(json.dumps({"rank": rank, "world_size": world, "ps": n_ps, "workers": len(workers),
+                          "steps": args.steps, "batch_per_worker": args.batch, "seconds": dt,
+                          "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
+                          "samples_per_sec": args.steps * args.batch * len(workers) / dt if dt > 0 else 0.0,
+                          "loss_first": first, "loss_last": last, "device": str(device),
+                          "hip_kernels": emb.use_hip}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,154 @@
+"""CTR / XDLJob data plane: sharded embedding pull/push semantics (CPU, gloo
+multi-process) and the HIP kernels vs fp32 PyTorch references (GPU)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from kubedl_amd.models.ctr import ShardedEmbedding
+
+
+def _ref_adagrad(table, accum, ids, grads, lr, eps):
+    uniq, inv = torch.unique(ids, return_inverse=True)
+    g = torch.zeros(len(uniq), table.shape[1]).index_add_(0, inv, grads)
+    a = accum[uniq] + g * g
+    accum[uniq] = a
+    table[uniq] -= lr * g / (a.sqrt() + eps)
+
+
+def test_sharded_embedding_single_process():
+    emb = ShardedEmbedding(500, 8, [0], 0, 1, "cpu", lr=0.1)
+    t0 = emb.table.clone()
+    ids = torch.tensor([3, 7, 3, 499, 7, 7])
+    rows, inv = emb.pull(ids)
+    torch.testing.assert_close(rows[inv], t0[ids])
+    g = torch.randn(rows.shape[0], 8)
+    emb.push(g)
+    ref_t, ref_a = t0.clone(), torch.zeros_like(t0)
+    uniq = torch.unique(ids)
+    _ref_adagrad(ref_t, ref_a, uniq, g, 0.1, 1e-8)
+    torch.testing.assert_close(emb.table, ref_t)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ps_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    emb = ShardedEmbedding(60, 4, [0, 1], rank, world, "cpu", lr=0.5)  # ranks 0,1 own shards
+    ids = {0: torch.tensor([], dtype=torch.int64), 1: torch.tensor([], dtype=torch.int64),
+           2: torch.tensor([1, 2, 3, 2, 59]), 3: torch.tensor([2, 3, 40])}[rank]
+    rows, inv = emb.pull(ids)
+    out[f"rows{rank}"] = rows[inv].clone()
+    g = torch.full((rows.shape[0], 4), float(rank))  # worker r pushes grad = r per unique id
+    emb.push(g)
+    out[f"table{rank}"] = emb.table.clone()
+    dist.destroy_process_group()
+
+
+def test_ps_pull_push_multiprocess():
+    """2 PS shards + 2 workers: pulled rows match the initial table and pushes of
+    the same id from both workers are summed before one Adagrad step."""
+    port = _port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_ps_worker, args=(r, 4, port, out)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    init = {me: ShardedEmbedding(60, 4, [0, 1], me, 4, "cpu").table for me in (0, 1)}
+
+    def row(i):
+        return init[i % 2][i // 2]
+    torch.testing.assert_close(out["rows2"], torch.stack([row(i) for i in (1, 2, 3, 2, 59)]))
+    torch.testing.assert_close(out["rows3"], torch.stack([row(i) for i in (2, 3, 40)]))
+    # id 2 and 3: grads 2 (worker rank 2) + 3 (worker rank 3) = 5 ; id 1, 59: 2 ; id 40: 3
+    for gid, gsum in ((2, 5.0), (3, 5.0), (1, 2.0), (59, 2.0), (40, 3.0)):
+        owner, local = gid % 2, gid // 2
+        exp = row(gid) - 0.5 * gsum / (abs(gsum) + 1e-8)
+        torch.testing.assert_close(out[f"table{owner}"][local], exp, atol=1e-6, rtol=1e-6)
+
+
+# ---------------------------------------------------------------- GPU kernels
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 72), (4096, 1024, 1680), (1, 128, 64)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_gemm_bias_act_matches_fp32(M, N, K, relu):
+    from kubedl_amd.ops import _ext
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    y = _ext.load().gemm_bias_act(a, w, b, relu)
+    ref = a.float() @ w.float().t() + b
+    if relu:
+        ref = ref.relu()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_fused_linear_backward_matches_autograd():
+    from kubedl_amd.models.ctr import fused_linear
+    torch.manual_seed(0)
+    x = torch.randn(512, 256, device="cuda").bfloat16().requires_grad_(True)
+    w = (torch.randn(128, 256, device="cuda") / 16).bfloat16().requires_grad_(True)
+    b = torch.randn(128, device="cuda").bfloat16().requires_grad_(True)
+    y = fused_linear(x, w, b, relu=True)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.relu(xr @ wr.t() + br)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=2e-1, rtol=5e-2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=2e-1, rtol=5e-2)
+
+
+@pytest.mark.gpu
+def test_embedding_kernels_match_torch():
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(0)
+    V, D, B, F = 1000, 64, 333, 7
+    table = torch.randn(V, D, device="cuda")
+    idx = torch.randint(0, V, (B * F,), device="cuda")
+    out = torch.zeros(B, F * D + 32, device="cuda")
+    ext.embed_gather(table, idx, F, out, 0)
+    torch.testing.assert_close(out[:, : F * D], table[idx].reshape(B, F * D))
+    # segment reduce of (b, f) gradient rows by inverse index
+    uniq, inv = torch.unique(idx, return_inverse=True)
+    order = torch.argsort(inv, stable=True)
+    seg = torch.zeros(len(uniq) + 1, dtype=torch.int64, device="cuda")
+    seg[1:] = torch.cumsum(torch.bincount(inv, minlength=len(uniq)), 0)
+    gx = torch.randn(B, F * D + 32, device="cuda").bfloat16()
+    got = ext.segment_reduce(gx, F, 0, D, order, seg)
+    ref = torch.zeros(len(uniq), D, device="cuda").index_add_(0, inv, gx[:, : F * D].reshape(B * F, D).float())
+    torch.testing.assert_close(got, ref, atol=1e-3, rtol=1e-3)
+    # fused segment-sum + Adagrad
+    tab = torch.randn(V, D, device="cuda")
+    acc = torch.rand(V, D, device="cuda")
+    grads = torch.randn(B * F, D, device="cuda")
+    t_ref, a_ref = tab.clone().cpu(), acc.clone().cpu()
+    ext.segment_adagrad(grads, order, seg, uniq, tab, acc, 0.1, 1e-8, 0.5)
+    _ref_adagrad(t_ref, a_ref, idx.cpu(), grads.cpu() * 0.5, 0.1, 1e-8)
+    torch.testing.assert_close(tab.cpu(), t_ref, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(acc.cpu(), a_ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_ctr_worker_trains_on_gpu():
+    from kubedl_amd.workers.xdl_ctr import main
+    assert main(["--steps", "20", "--warmup", "2", "--batch", "1024", "--fields", "8", "--vocab", "5000",
+                 "--dim", "32", "--hidden", "256,128"]) == 0
