@@ -260,11 +260,11 @@ def test_tfjob_tf_config_and_worker0_success(mgr):
     mgr.apply(job)
     job = mgr.wait_for_condition("TFJob", "default", "tf", ["Succeeded", "Failed"], timeout=60)
     assert "Succeeded" in _cond_types(job), job["status"]
-    pod = mgr.store.get("Pod", "default", "tf-worker-1")
+    pod = mgr.store.get("Pod", "default", "tf-worker-0")  # completed pods survive cleanPodPolicy=Running
     cfg = [e for e in pod["spec"]["containers"][0]["env"] if e["name"] == "TF_CONFIG"][0]["value"]
     import json
     cfg = json.loads(cfg)
-    assert cfg["task"] == {"type": "worker", "index": 1}
+    assert cfg["task"] == {"type": "worker", "index": 0}
     assert cfg["cluster"]["ps"] == ["tf-ps-0.default.svc:2222"]
     # cleanPodPolicy Running (TF default): the still-running PS is deleted
     mgr.wait_for("TFJob", "default", "tf", lambda j: mgr.store.try_get("Pod", "default", "tf-ps-0") is None,
