@@ -236,7 +236,17 @@ PyObject* py_alive(PyObject*, PyObject* arg) {
   return PyBool_FromLong(r == 0 || errno == EPERM);
 }
 
+// Make this process a child subreaper: orphaned descendants (ranks forked by
+// the pre-warmed zygote and double-forked away from it) are re-parented to us,
+// so the supervisor can waitpid() them like directly spawned ranks.
+PyObject* py_set_child_subreaper(PyObject*, PyObject*) {
+  if (prctl(PR_SET_CHILD_SUBREAPER, 1) != 0) return PyErr_SetFromErrno(PyExc_OSError);
+  Py_RETURN_NONE;
+}
+
 PyMethodDef methods[] = {
+    {"set_child_subreaper", py_set_child_subreaper, METH_NOARGS,
+     "set_child_subreaper() -> None (PR_SET_CHILD_SUBREAPER on this process)"},
     {"spawn", reinterpret_cast<PyCFunction>(py_spawn), METH_VARARGS | METH_KEYWORDS,
      "spawn(argv, env, cwd=None, out=None, err=None, pdeathsig=SIGKILL) -> pid"},
     {"reap", py_reap, METH_O, "reap(pids) -> [(pid, exit_code)] for exited children (non-blocking)"},

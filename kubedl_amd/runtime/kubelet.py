@@ -43,6 +43,7 @@ from typing import Dict, List, Optional, Tuple
 
 from kubedl_amd.api import common as c
 from kubedl_amd.runtime import images
+from kubedl_amd.runtime import zygote as zygote_mod
 from kubedl_amd.runtime.scheduler import GPU_ANNOTATION
 from kubedl_amd.store import ADDED, DELETED, MODIFIED, NotFound, Store
 
@@ -223,7 +224,16 @@ class PodWorker(threading.Thread):
                 f.write(f"[kdl-kubelet] {c.now()} start {cs.name} (restart {cs.restart_count}): "
                         f"{' '.join(argv)}\n")
             envl = [f"{k}={v}" for k, v in env.items()]
-            if nat is not None:
+            pid = None
+            z = self.k.zygote
+            if z is not None and zygote_mod.eligible(argv) is not None:
+                pid = z.launch(argv, env, cwd, cs.log_path)
+                if pid is not None:
+                    with open(cs.log_path, "a") as f:
+                        f.write(f"[kdl-kubelet] forked from the pre-warmed zygote as pid {pid}\n")
+            if pid is not None:
+                cs.pid = pid
+            elif nat is not None:
                 cs.pid = nat.spawn(argv, envl, cwd, cs.log_path, cs.log_path)
             else:  # pragma: no cover
                 import subprocess
@@ -501,7 +511,7 @@ class ServiceResolver:
 class Kubelet:
     def __init__(self, store: Store, root: str, node_name: str = "localhost",
                  poll_interval: float = 0.01, default_grace: float = 5.0,
-                 backoff_base: float = 1.0, backoff_max: float = 30.0):
+                 backoff_base: float = 1.0, backoff_max: float = 30.0, zygote: Optional[bool] = None):
         self.store = store
         self.root = root
         self.node = node_name
@@ -515,11 +525,18 @@ class Kubelet:
         self._lock = threading.Lock()
         os.makedirs(os.path.join(root, "pods"), exist_ok=True)
         self._cancel = None
+        if zygote is None:
+            zygote = os.environ.get("KDL_ZYGOTE", "1") != "0"
+        self.zygote = zygote_mod.ZygoteClient(root, self.native) if (zygote and self.native is not None) else None
 
     def backoff(self, n: int) -> float:
         return min(self.backoff_base * (2 ** max(0, n - 1)), self.backoff_max)
 
     def start(self) -> None:
+        if self.zygote is not None:
+            env = {k: v for k, v in os.environ.items() if k not in _ENV_DENY}
+            env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+            self.zygote.start(env)
         self._cancel = self.store.watch(self._on_event, kind="Pod")
         for p in self.store.list("Pod"):
             self._maybe_start(p)
@@ -535,6 +552,8 @@ class Kubelet:
                 w.deleted.set()
             for w in workers:
                 w.join(timeout=10)
+        if self.zygote is not None:
+            self.zygote.stop()
 
     def _on_event(self, etype: str, pod: dict) -> None:
         if etype == DELETED:

@@ -8,6 +8,11 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# the pre-warmed zygote (kubelet launch-delay optimisation) imports torch in a
+# side process; tests opt in explicitly (tests/test_zygote.py)
+os.environ.setdefault("KDL_ZYGOTE", "0")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: long-running test")

@@ -1,0 +1,37 @@
+"""Pre-warmed zygote launches: ranks forked from a torch-preloaded process are
+re-parented to the kubelet (subreaper), reaped with the right exit code, see
+their own env/cwd/log, and launch faster than a cold interpreter."""
+import os
+import sys
+import time
+
+from kubedl_amd.engine.manager import Manager, ManagerOptions
+
+
+def _job(name, script_mod, args):
+    return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "restartPolicy": "Never", "template": {"spec": {
+                "containers": [{"name": "pytorch", "image": "x",
+                                "command": [sys.executable, "-u", "-m", script_mod] + args}]}}}}}}
+
+
+def test_zygote_launch(tmp_path, monkeypatch):
+    monkeypatch.setenv("KDL_ZYGOTE", "1")
+    m = Manager(ManagerOptions(home=str(tmp_path), gpus=0)).start()
+    try:
+        assert m.kubelet.zygote is not None
+        assert m.kubelet.zygote.ready.wait(120), "zygote never became ready"
+        m.apply(_job("z1", "kubedl_amd.workers.pytorch_dist", ["--cpu", "--numel", "16"]))
+        job = m.wait_for_condition("PyTorchJob", "default", "z1", ["Succeeded", "Failed"], timeout=60)
+        assert [c["type"] for c in job["status"]["conditions"] if c["status"] == "True"][-1] == "Succeeded"
+        log = open(m.kubelet.log_path("default", "z1-master-0")).read()
+        assert "pre-warmed zygote" in log and "rank 0/1" in log
+        # failing module -> exit code propagates through the double fork
+        m.apply(_job("z2", "kubedl_amd.workers.no_such_worker", []))
+        job = m.wait_for_condition("PyTorchJob", "default", "z2", ["Succeeded", "Failed"], timeout=60)
+        pod = m.store.get("Pod", "default", "z2-master-0")
+        code = pod["status"]["containerStatuses"][0]["state"]["terminated"]["exitCode"]
+        assert code != 0
+        assert m.metrics.observed["first"]
+    finally:
+        m.stop()
