@@ -266,8 +266,14 @@ def set_defaults(job: dict) -> dict:
 
 
 def replica_specs(job: dict) -> Dict[str, dict]:
-    info = BY_KIND[job["kind"]]
-    return (job.get("spec") or {}).get(info.spec_field) or {}
+    spec = job.get("spec") or {}
+    info = BY_KIND.get(job["kind"])
+    if info is None:  # a kind outside the four (e.g. the engine's TestJob): its single *ReplicaSpecs map
+        for k, v in spec.items():
+            if k.endswith("ReplicaSpecs") and isinstance(v, dict):
+                return v
+        return {}
+    return spec.get(info.spec_field) or {}
 
 
 RUN_POLICY_FIELDS = ("cleanPodPolicy", "ttlSecondsAfterFinished", "activeDeadlineSeconds",

@@ -40,6 +40,8 @@ from typing import Dict, List, Optional, Tuple
 from kubedl_amd.api import common as c
 from kubedl_amd.api import kinds as K
 from kubedl_amd import code_sync
+from kubedl_amd.engine.control import (ControllerRefManager, PodControl, ServiceControl,  # noqa: F401
+                                       controller_of)
 from kubedl_amd.engine.expectations import Expectations
 from kubedl_amd.engine.workqueue import RateLimitingQueue
 from kubedl_amd.store import NORMAL, WARNING, AlreadyExists, EventRecorder, NotFound, Store
@@ -47,13 +49,9 @@ from kubedl_amd.store import NORMAL, WARNING, AlreadyExists, EventRecorder, NotF
 log = logging.getLogger("kubedl_amd.engine")
 
 # event reasons (pkg/job_controller/pod_control.go, service_control.go, pod.go)
-SUCCESSFUL_CREATE_POD = "SuccessfulCreatePod"
-FAILED_CREATE_POD = "FailedCreatePod"
-SUCCESSFUL_DELETE_POD = "SuccessfulDeletePod"
-FAILED_DELETE_POD = "FailedDeletePod"
-SUCCESSFUL_CREATE_SERVICE = "SuccessfulCreateService"
-FAILED_CREATE_SERVICE = "FailedCreateService"
-SUCCESSFUL_DELETE_SERVICE = "SuccessfulDeleteService"
+from kubedl_amd.engine.control import (FAILED_CREATE_POD, FAILED_CREATE_SERVICE, FAILED_DELETE_POD,  # noqa: F401,E402
+                                       SUCCESSFUL_CREATE_POD, SUCCESSFUL_CREATE_SERVICE,
+                                       SUCCESSFUL_DELETE_POD, SUCCESSFUL_DELETE_SERVICE)
 EXITED_WITH_CODE = "ExitedWithCode"
 POD_TEMPLATE_RESTART_POLICY = "SettedPodTemplateRestartPolicy"
 EXIT_CODE_SENTINEL = 0xBEEF
@@ -84,13 +82,6 @@ def gen_owner_reference(job: dict) -> dict:
     md = job["metadata"]
     return {"apiVersion": job["apiVersion"], "kind": job["kind"], "name": md["name"],
             "uid": md["uid"], "controller": True, "blockOwnerDeletion": True}
-
-
-def controller_of(obj: dict) -> Optional[dict]:
-    for r in (obj.get("metadata") or {}).get("ownerReferences") or []:
-        if r.get("controller"):
-            return r
-    return None
 
 
 def pod_phase(pod: dict) -> str:
@@ -151,10 +142,12 @@ class WorkloadController:
 class JobController:
     def __init__(self, controller: WorkloadController, store: Store, recorder: EventRecorder,
                  metrics, config: Optional[JobControllerConfig] = None, gang=None,
-                 queue: Optional[RateLimitingQueue] = None):
+                 queue: Optional[RateLimitingQueue] = None, pod_control=None, service_control=None):
         self.controller = controller
         self.store = store
         self.recorder = recorder
+        self.pod_control = pod_control or PodControl(store, recorder)
+        self.service_control = service_control or ServiceControl(store, recorder)
         self.metrics = metrics
         self.config = config or JobControllerConfig()
         self.gang = gang
@@ -182,29 +175,17 @@ class JobController:
 
     # ------------------------------------------------------------ object access
     def get_pods_for_job(self, job: dict) -> List[dict]:
-        """List by label selector, then keep (adopt) only pods controlled by this job."""
+        """List by label selector, then claim (keep owned, adopt orphans)."""
         md = job["metadata"]
-        pods = self.store.list("Pod", md["namespace"], self.gen_labels(md["name"]))
-        out = []
-        for p in pods:
-            ref = controller_of(p)
-            if ref is None:
-                # adopt orphans that match our selector (ClaimPods)
-                try:
-                    p = self.store.patch("Pod", md["namespace"], p["metadata"]["name"],
-                                         lambda o: o["metadata"].setdefault("ownerReferences", []).append(
-                                             gen_owner_reference(job)))
-                except NotFound:
-                    continue
-                out.append(p)
-            elif ref.get("uid") == md["uid"]:
-                out.append(p)
-        return out
+        sel = self.gen_labels(md["name"])
+        pods = self.store.list("Pod", md["namespace"], sel)
+        return ControllerRefManager(self.pod_control, job, sel, gen_owner_reference(job)).claim(pods)
 
     def get_services_for_job(self, job: dict) -> List[dict]:
         md = job["metadata"]
-        svcs = self.store.list("Service", md["namespace"], self.gen_labels(md["name"]))
-        return [s for s in svcs if (controller_of(s) or {}).get("uid") in (md["uid"], None)]
+        sel = self.gen_labels(md["name"])
+        svcs = self.store.list("Service", md["namespace"], sel)
+        return ControllerRefManager(self.service_control, job, sel, gen_owner_reference(job)).claim(svcs)
 
     @staticmethod
     def filter_for_replica_type(objs: List[dict], rt: str) -> List[dict]:
@@ -240,15 +221,7 @@ class JobController:
 
     # ------------------------------------------------------------ pod/service control
     def create_pod(self, job: dict, pod: dict) -> dict:
-        try:
-            out = self.store.create(pod)
-        except AlreadyExists:
-            raise
-        except Exception as e:
-            self.recorder.event(job, WARNING, FAILED_CREATE_POD, f"Error creating: {e}")
-            raise
-        self.recorder.event(job, NORMAL, SUCCESSFUL_CREATE_POD, f"Created pod: {pod['metadata']['name']}")
-        return out
+        return self.pod_control.create(job, pod)
 
     def delete_pod(self, job: dict, pod: dict) -> None:
         md = pod["metadata"]
@@ -256,15 +229,12 @@ class JobController:
         key = c.gen_expectation_pods_key(job_key(job), rt)
         self.expectations.expect_deletions(key, 1)
         try:
-            self.store.delete("Pod", md["namespace"], md["name"])
+            self.pod_control.delete(job, md["namespace"], md["name"])
         except NotFound:
             self.expectations.deletion_observed(key)
-            return
-        except Exception as e:
+        except Exception:
             self.expectations.deletion_observed(key)
-            self.recorder.event(job, WARNING, FAILED_DELETE_POD, f"Error deleting: {e}")
             raise
-        self.recorder.event(job, NORMAL, SUCCESSFUL_DELETE_POD, f"Deleted pod: {md['name']}")
 
     def delete_service(self, job: dict, name: str, namespace: str) -> None:
         try:
@@ -275,11 +245,12 @@ class JobController:
         key = c.gen_expectation_services_key(job_key(job), rt)
         self.expectations.expect_deletions(key, 1)
         try:
-            self.store.delete("Service", namespace, name)
+            self.service_control.delete(job, namespace, name)
         except NotFound:
             self.expectations.deletion_observed(key)
-            return
-        self.recorder.event(job, NORMAL, SUCCESSFUL_DELETE_SERVICE, f"Deleted service: {name}")
+        except Exception:
+            self.expectations.deletion_observed(key)
+            raise
 
     def update_job_status_in_store(self, job: dict, status: dict) -> dict:
         cur = copy.deepcopy(job)
@@ -591,12 +562,10 @@ class JobController:
         host_port = self.store.host_port(ns, name, port)
         svc["metadata"]["annotations"] = {"kubedl.io/host-port": str(host_port)}
         try:
-            self.store.create(svc)
+            self.service_control.create(job, svc)
         except AlreadyExists:
             self.expectations.creation_observed(exp_key)
             return
-        except Exception as e:
+        except Exception:
             self.expectations.creation_observed(exp_key)
-            self.recorder.event(job, WARNING, FAILED_CREATE_SERVICE, f"Error creating: {e}")
             raise
-        self.recorder.event(job, NORMAL, SUCCESSFUL_CREATE_SERVICE, f"Created service: {name}")
