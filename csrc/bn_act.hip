@@ -112,29 +112,30 @@ __device__ __forceinline__ void block_fold_atomic(float (&a)[VEC], float (&b)[VE
 // ---------------------------------------------------------------- forward stats
 template <typename T, int VEC>
 __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(
-    const T* __restrict__ x, int64_t M, int C, int TPR, int RPI, int64_t rows_per_block,
-    float* __restrict__ acc) {
+    const T* __restrict__ x, int64_t M, int C, int TPR, int RPI, float* __restrict__ acc) {
   __shared__ float sh[2 * kBlock * VEC];
   const int t = threadIdx.x;
   const int lc = t % TPR, r0 = t / TPR;
   const int CG = C / VEC;
   const int cg = blockIdx.y * TPR + lc;
   const bool active = (r0 < RPI) && (cg < CG);
-  const int64_t rb = static_cast<int64_t>(blockIdx.x) * rows_per_block;
-  const int64_t re = (rb + rows_per_block < M) ? rb + rows_per_block : M;
+  // grid-stride rows: at any moment the whole grid streams one contiguous
+  // window of the activation (DRAM-page / TLB friendly), instead of every
+  // block walking its own distant chunk.
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
   const int c0 = cg * VEC;
   float K[VEC], s1[VEC], s2[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) { K[i] = 0.f; s1[i] = 0.f; s2[i] = 0.f; }
   if (active) {
     VecIO<T, VEC>::load(x + c0, K);  // global per-channel shift K = x[0, c]
-    int64_t r = rb + r0;
-    for (; r + 3 * RPI < re; r += 4 * RPI) {
+    int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0;
+    for (; r + 3 * step < M; r += 4 * step) {
       float v0[VEC], v1[VEC], v2[VEC], v3[VEC];
       VecIO<T, VEC>::load(x + r * C + c0, v0);
-      VecIO<T, VEC>::load(x + (r + RPI) * C + c0, v1);
-      VecIO<T, VEC>::load(x + (r + 2 * RPI) * C + c0, v2);
-      VecIO<T, VEC>::load(x + (r + 3 * RPI) * C + c0, v3);
+      VecIO<T, VEC>::load(x + (r + step) * C + c0, v1);
+      VecIO<T, VEC>::load(x + (r + 2 * step) * C + c0, v2);
+      VecIO<T, VEC>::load(x + (r + 3 * step) * C + c0, v3);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         float d0 = v0[i] - K[i], d1 = v1[i] - K[i], d2 = v2[i] - K[i], d3 = v3[i] - K[i];
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(
         s2[i] += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
       }
     }
-    for (; r < re; r += RPI) {
+    for (; r < M; r += step) {
       float v[VEC];
       VecIO<T, VEC>::load(x + r * C + c0, v);
 #pragma unroll
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_stats_kernel(
     }
   }
   float* rep = acc + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
-  block_fold_atomic<VEC>(s1, s2, sh, t, lc, r0, TPR, RPI, active && rb < re, rep + c0, rep + C + c0);
+  block_fold_atomic<VEC>(s1, s2, sh, t, lc, r0, TPR, RPI, active, rep + c0, rep + C + c0);
 }
 
 // ---------------------------------------------------------------- forward finalize
@@ -273,16 +274,14 @@ template <typename T, typename PT, int VEC, int MASK>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
     const PT* __restrict__ gamma, const PT* __restrict__ beta, const float* __restrict__ mean,
-    const float* __restrict__ invstd, int64_t M, int C, int TPR, int RPI,
-    int64_t rows_per_block, float* __restrict__ acc) {
+    const float* __restrict__ invstd, int64_t M, int C, int TPR, int RPI, float* __restrict__ acc) {
   __shared__ float sh[2 * kBlock * VEC];
   const int t = threadIdx.x;
   const int lc = t % TPR, r0 = t / TPR;
   const int CG = C / VEC;
   const int cg = blockIdx.y * TPR + lc;
   const bool active = (r0 < RPI) && (cg < CG);
-  const int64_t rb = static_cast<int64_t>(blockIdx.x) * rows_per_block;
-  const int64_t re = (rb + rows_per_block < M) ? rb + rows_per_block : M;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;  // grid-stride, as the stats kernel
   const int c0 = cg * VEC;
   float mu[VEC], sa[VEC], sb[VEC], sc[VEC], sf[VEC];
 #pragma unroll
@@ -291,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(
 #pragma unroll
     for (int i = 0; i < VEC; ++i) mu[i] = mean[c0 + i];
     if constexpr (MASK == kMaskX) mask_coeffs<PT, VEC>(gamma, beta, mean, invstd, c0, sc, sf);
-    int64_t r = rb + r0;
+    int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0;
     auto body = [&](int64_t row) {
       float g[VEC], xv[VEC];
       VecIO<T, VEC>::load(dy + row * C + c0, g);
@@ -311,14 +310,14 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(
         sb[i] = fmaf(g[i], xv[i] - mu[i], sb[i]);
       }
     };
-    for (; r + RPI < re; r += 2 * RPI) {
+    for (; r + step < M; r += 2 * step) {
       body(r);
-      body(r + RPI);
+      body(r + step);
     }
-    if (r < re) body(r);
+    if (r < M) body(r);
   }
   float* rep = acc + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
-  block_fold_atomic<VEC>(sa, sb, sh, t, lc, r0, TPR, RPI, active && rb < re, rep + c0, rep + C + c0);
+  block_fold_atomic<VEC>(sa, sb, sh, t, lc, r0, TPR, RPI, active, rep + c0, rep + C + c0);
 }
 
 // ---------------------------------------------------------------- backward finalize
@@ -451,7 +450,7 @@ hipError_t fwd_impl(const T* x, const T* res, T* y, const PT* gamma, const PT* b
   const int fin_grid = (C + kBlock - 1) / kBlock;
   if (training) {
     hipLaunchKernelGGL((bn_fwd_stats_kernel<T, VEC>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
-                       x, M, C, rp.tl.TPR, rp.tl.RPI, rp.rows_per_block, acc);
+                       x, M, C, rp.tl.TPR, rp.tl.RPI, acc);
     hipLaunchKernelGGL((bn_fwd_finalize_kernel<T, PT>), dim3(fin_grid), dim3(kBlock), 0, s, x, acc,
                        C, static_cast<float>(M), gamma, beta, rm, rv, momentum, eps, save_mean,
                        save_invstd, coef);
@@ -478,8 +477,7 @@ void bwd_launch(const ReducePlan& rp, const T* dy, const T* y, const T* x, const
   float* acc = ws_acc_bwd(ws, C);
   float* coef = ws_coef(ws, C);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, PT, VEC, MASK>), dim3(rp.gx, rp.tl.gy), dim3(kBlock),
-                     0, s, dy, y, x, gamma, beta, mean, invstd, M, C, rp.tl.TPR, rp.tl.RPI,
-                     rp.rows_per_block, acc);
+                     0, s, dy, y, x, gamma, beta, mean, invstd, M, C, rp.tl.TPR, rp.tl.RPI, acc);
   hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      s, acc, C, static_cast<float>(M), gamma, mean, invstd, training, dgamma, dbeta,
                      coef);

@@ -268,8 +268,8 @@ def build_parser() -> argparse.ArgumentParser:
     m.add_argument("--max-reconciles", type=int, default=1)
     m.add_argument("--workloads", default="auto")
     m.add_argument("--region", default="")
-    m.add_argument("--object-storage", default="", help="object backend: sqlite")
-    m.add_argument("--event-storage", default="", help="event backend: jsonl | sqlite")
+    m.add_argument("--object-storage", default="", help="object backend: sqlite | mysql")
+    m.add_argument("--event-storage", default="", help="event backend: jsonl | sqlite | aliyun-sls")
     m.add_argument("--api-addr", default=DEFAULT_API)
     m.add_argument("--home", default=os.environ.get("KDL_HOME", os.path.expanduser("~/.kubedl_amd")))
     m.add_argument("--gpus", type=int, default=None, help="override detected GPU count")

@@ -39,6 +39,7 @@ want benchab && run_step bench_torch 600 python bench.py --steps 20 --warmup 8 -
 want prof   && run_step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 3
 want benchfind && run_step bench_find 900 python bench.py --steps 20 --warmup 8 --conv-benchmark 1
 want launch && run_step bench_launch 600 python -m kubedl_amd.cli bench-launch --jobs 1 --gpus 1 --steps 20 --warmup 5
+want convgemm && run_step conv_vs_gemm 600 python scripts/conv_vs_gemm.py
 want benchimm && run_step bench_immediate 600 python bench.py --steps 20 --warmup 8 --conv-benchmark 0
 # ship the MIOpen find-db / kernel cache back (merged into gpurun_out/)
 if [ -d miopen_db ]; then mkdir -p gpurun_out/miopen_db && cp -r miopen_db/. gpurun_out/miopen_db/; du -sh gpurun_out/miopen_db; fi
