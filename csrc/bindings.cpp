@@ -55,7 +55,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
                                    const at::Tensor& running_var,
                                    const c10::optional<at::Tensor>& residual, bool relu,
                                    bool training, double momentum, double eps,
-                                   const c10::optional<at::Tensor>& acc) {
+                                   const c10::optional<at::Tensor>& acc, bool want_mask) {
   TORCH_CHECK(x.is_cuda(), "bn_act_fwd: x must be on the GPU");
   TORCH_CHECK(x.dim() == 4 || x.dim() == 2, "bn_act_fwd: x must be NHWC 4-D or [M, C]");
   TORCH_CHECK(is_nhwc_dense(x), "bn_act_fwd: x must be channels_last-dense");
@@ -75,42 +75,58 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const at::Tensor& weight
                 "bn_act_fwd: residual must match x (shape, dtype, channels_last)");
   }
   auto y = at::empty_like(x);
+  // packed ReLU mask (uint8 [M, C/8]) replaces y in the backward of relu+residual layers
+  const bool mask = want_mask && relu && res != nullptr && x.scalar_type() == at::kBFloat16 && C % 8 == 0;
+  at::Tensor mbits;
+  if (mask) mbits = at::empty({M, C / 8}, x.options().dtype(at::kByte));
   auto fopt = x.options().dtype(at::kFloat);
   auto save_mean = at::empty({C}, fopt);
   auto save_invstd = at::empty({C}, fopt);
   at::Tensor a = get_acc(acc, C, x);
   check_hip(kdl::bn_act_forward(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(),
-                                weight.data_ptr(), bias.data_ptr(), running_mean.data_ptr<float>(),
+                                mask ? mbits.data_ptr<uint8_t>() : nullptr, weight.data_ptr(), bias.data_ptr(), running_mean.data_ptr<float>(),
                                 running_var.data_ptr<float>(), save_mean.data_ptr<float>(),
                                 save_invstd.data_ptr<float>(), a.data_ptr<float>(), M,
                                 static_cast<int>(C), dtype_code(x), dtype_code(weight), relu,
                                 training, static_cast<float>(momentum), static_cast<float>(eps),
                                 cur_stream()),
             "bn_act_forward");
-  return {y, save_mean, save_invstd};
+  return {y, save_mean, save_invstd, mbits};
 }
 
-std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& y,
+std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
+                                   const c10::optional<at::Tensor>& y_opt,
                                    const at::Tensor& weight, const at::Tensor& bias,
                                    const at::Tensor& mean, const at::Tensor& invstd, bool relu,
                                    bool has_residual, bool training,
-                                   const c10::optional<at::Tensor>& acc) {
-  TORCH_CHECK(is_nhwc_dense(dy) && is_nhwc_dense(x) && is_nhwc_dense(y),
+                                   const c10::optional<at::Tensor>& acc,
+                                   const c10::optional<at::Tensor>& mask) {
+  const bool has_mask = mask.has_value() && mask->defined();
+  const bool has_y = y_opt.has_value() && y_opt->defined();
+  TORCH_CHECK(has_y || has_mask || !relu, "bn_act_bwd: relu needs y or the packed mask");
+  TORCH_CHECK(is_nhwc_dense(dy) && is_nhwc_dense(x) && (!has_y || is_nhwc_dense(*y_opt)),
               "bn_act_bwd: tensors must be channels_last-dense");
-  TORCH_CHECK(dy.sizes() == x.sizes() && y.sizes() == x.sizes(), "bn_act_bwd: shape mismatch");
+  TORCH_CHECK(dy.sizes() == x.sizes() && (!has_y || y_opt->sizes() == x.sizes()),
+              "bn_act_bwd: shape mismatch");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "bn_act_bwd: dtype mismatch");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(weight.numel() == C && bias.numel() == C && mean.numel() == C && invstd.numel() == C,
               "bn_act_bwd: per-channel tensor size mismatch");
+  if (has_mask)
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() == M * (C / 8) &&
+                    C % 8 == 0 && x.scalar_type() == at::kBFloat16,
+                "bn_act_bwd: mask must be uint8 [M, C/8] for bf16 x");
   auto dx = at::empty_like(x);
   at::Tensor dres;
   if (has_residual) dres = at::empty_like(x);
   auto dgamma = at::empty_like(weight);
   auto dbeta = at::empty_like(weight);
   at::Tensor a = get_acc(acc, C, x);
-  check_hip(kdl::bn_act_backward(dy.data_ptr(), y.data_ptr(), x.data_ptr(), weight.data_ptr(),
+  check_hip(kdl::bn_act_backward(dy.data_ptr(), has_y ? y_opt->data_ptr() : nullptr,
+                                 has_mask ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
+                                 weight.data_ptr(),
                                  bias.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                  dx.data_ptr(), has_residual ? dres.data_ptr() : nullptr,
                                  dgamma.data_ptr(), dbeta.data_ptr(), a.data_ptr<float>(), M,

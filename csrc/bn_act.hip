@@ -40,6 +40,8 @@
 //
 // The reference has no kernels; this is the data-plane op
 // the PyTorchJob ResNet-50 worker spends most of its non-conv time in.
+#include <cstdlib>
+
 #include "common.h"
 #include "kdl_api.h"
 
@@ -60,10 +62,15 @@ struct Tiling {
   int TPR, RPI, gy;
 };
 
+// At most 32 lanes (512 contiguous bytes) along C per row: wide layers split
+// their channels over gy blocks instead of over rows, which is what keeps the
+// reduction kernels' atomics per byte low when M is small (C=2048 at 7x7).
+constexpr int kMaxTPR = 32;
+
 __host__ Tiling make_tiling(int C, int VEC) {
   int CG = C / VEC;
   Tiling t;
-  t.TPR = CG < kBlock ? CG : kBlock;
+  t.TPR = CG < kMaxTPR ? CG : kMaxTPR;
   t.RPI = kBlock / t.TPR;
   t.gy = (CG + t.TPR - 1) / t.TPR;
   return t;
@@ -215,10 +222,11 @@ __global__ void bn_eval_prep_kernel(int C, const PT* __restrict__ gamma, const P
 }
 
 // ---------------------------------------------------------------- forward apply
-template <typename T, int VEC, bool RELU, bool RES>
+template <typename T, int VEC, bool RELU, bool RES, bool MOUT>
 __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
-    const float* __restrict__ coef, int64_t M, int C, int TPR, int RPI) {
+    uint8_t* __restrict__ mbits, const float* __restrict__ coef, int64_t M, int C, int TPR,
+    int RPI) {
   const int t = threadIdx.x;
   const int lc = t % TPR, r0 = t / TPR;
   const int cg = blockIdx.y * TPR + lc;
@@ -234,14 +242,19 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(
     VecIO<T, VEC>::load(x + row * C + c0, v);
     float rr[VEC];
     if constexpr (RES) VecIO<T, VEC>::load(res + row * C + c0, rr);
+    uint32_t bits = 0;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       float o = fmaf(v[i], sc[i], sf[i]);
       if constexpr (RES) o += rr[i];
+      if constexpr (MOUT) bits |= (o > 0.f ? 1u : 0u) << i;
       if constexpr (RELU) o = o > 0.f ? o : 0.f;
       v[i] = o;
     }
     VecIO<T, VEC>::store(y + row * C + c0, v);
+    // 1 bit per channel (VEC == 8: one byte per lane) = the ReLU mask the
+    // backward needs, at 1/16 of the bytes of re-reading y.
+    if constexpr (MOUT) mbits[row * (C / VEC) + cg] = static_cast<uint8_t>(bits);
   };
   for (; r + step < M; r += 2 * step) {  // two rows in flight per lane
     body(r);
@@ -254,6 +267,7 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_apply_kernel(
 constexpr int kMaskNone = 0;  // no activation
 constexpr int kMaskY = 1;     // mask = y > 0 (residual case: y saw the residual)
 constexpr int kMaskX = 2;     // mask = x*scale + shift > 0 (recomputed, saves reading y)
+constexpr int kMaskBits = 3;  // mask = bit i of the forward's packed byte (residual case, VEC 8)
 
 template <typename PT, int VEC>
 __device__ __forceinline__ void mask_coeffs(const PT* __restrict__ gamma, const PT* __restrict__ beta,
@@ -272,7 +286,8 @@ __device__ __forceinline__ void mask_coeffs(const PT* __restrict__ gamma, const 
 // ---------------------------------------------------------------- backward reduce
 template <typename T, typename PT, int VEC, int MASK>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(
-    const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
+    const T* __restrict__ dy, const T* __restrict__ y, const uint8_t* __restrict__ mbits,
+    const T* __restrict__ x,
     const PT* __restrict__ gamma, const PT* __restrict__ beta, const float* __restrict__ mean,
     const float* __restrict__ invstd, int64_t M, int C, int TPR, int RPI, float* __restrict__ acc) {
   __shared__ float sh[2 * kBlock * VEC];
@@ -303,6 +318,10 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(
       } else if constexpr (MASK == kMaskX) {
 #pragma unroll
         for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], sc[i], sf[i]) > 0.f ? g[i] : 0.f;
+      } else if constexpr (MASK == kMaskBits) {
+        const uint32_t m = mbits[row * (C / VEC) + cg];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) g[i] = (m >> i) & 1u ? g[i] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
@@ -357,7 +376,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(
 // ---------------------------------------------------------------- backward apply
 template <typename T, typename PT, int VEC, int MASK, bool RES>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(
-    const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
+    const T* __restrict__ dy, const T* __restrict__ y, const uint8_t* __restrict__ mbits,
+    const T* __restrict__ x,
     const PT* __restrict__ gamma, const PT* __restrict__ beta, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ coef, T* __restrict__ dx,
     T* __restrict__ dres, int64_t M, int C, int TPR, int RPI) {
@@ -389,6 +409,10 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(
     } else if constexpr (MASK == kMaskX) {
 #pragma unroll
       for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], sc[i], sf[i]) > 0.f ? g[i] : 0.f;
+    } else if constexpr (MASK == kMaskBits) {
+      const uint32_t m = mbits[row * (C / VEC) + cg];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) g[i] = (m >> i) & 1u ? g[i] : 0.f;
     }
     if constexpr (RES) VecIO<T, VEC>::store(dres + row * C + c0, g);
 #pragma unroll
@@ -410,14 +434,21 @@ struct ReducePlan {
   int64_t rows_per_block;
 };
 
-// Enough blocks to fill 256 CUs several times (Guideline 11) with >= 16 rows
-// per lane so the shifted sums amortise the fold + atomics.
+// Up to 1024 blocks to fill 256 CUs several times (Guideline 11), but every
+// block covers >= kMinRows rows: a block issues 2 atomics per channel it owns, so
+// rows-per-block IS the bytes-per-atomic ratio (v3 used 16 rows per lane:
+// C=2048 at 7x7 ran at 0.5 TB/s, bound by 3.2M memory-side atomics).
 ReducePlan plan_reduce(int64_t M, int C, int VEC) {
   ReducePlan p;
   p.tl = make_tiling(C, VEC);
   int64_t target = 1024 / p.tl.gy;
   if (target < 1) target = 1;
+  static const int64_t kMinRows = [] {
+    const char* e = getenv("KDL_BN_MIN_ROWS");  // tuning knob for sweeps; default measured best
+    return static_cast<int64_t>(e ? atoi(e) : 128);
+  }();
   int64_t min_rows = static_cast<int64_t>(p.tl.RPI) * 16;
+  if (min_rows < kMinRows) min_rows = kMinRows;
   int64_t gx = (M + min_rows - 1) / min_rows;
   if (gx > target) gx = target;
   if (gx < 1) gx = 1;
@@ -441,7 +472,7 @@ int apply_gx(int64_t M, const Tiling& tl) {
 }
 
 template <typename T, int VEC, typename PT>
-hipError_t fwd_impl(const T* x, const T* res, T* y, const PT* gamma, const PT* beta, float* rm,
+hipError_t fwd_impl(const T* x, const T* res, T* y, uint8_t* mbits, const PT* gamma, const PT* beta, float* rm,
                     float* rv, float* save_mean, float* save_invstd, float* ws, int64_t M, int C,
                     bool relu, bool training, float momentum, float eps, hipStream_t s) {
   ReducePlan rp = plan_reduce(M, C, VEC);
@@ -459,53 +490,58 @@ hipError_t fwd_impl(const T* x, const T* res, T* y, const PT* gamma, const PT* b
                        beta, rm, rv, eps, save_mean, save_invstd, coef);
   }
   dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
-#define KDL_FWD_APPLY(R, S)                                                                    \
-  hipLaunchKernelGGL((bn_fwd_apply_kernel<T, VEC, R, S>), grid, dim3(kBlock), 0, s, x, res, y, \
-                     coef, M, C, rp.tl.TPR, rp.tl.RPI)
-  if (relu && res) KDL_FWD_APPLY(true, true);
-  else if (relu) KDL_FWD_APPLY(true, false);
-  else if (res) KDL_FWD_APPLY(false, true);
-  else KDL_FWD_APPLY(false, false);
+#define KDL_FWD_APPLY(R, S, MO)                                                             \
+  hipLaunchKernelGGL((bn_fwd_apply_kernel<T, VEC, R, S, MO>), grid, dim3(kBlock), 0, s, x, res, \
+                     y, mbits, coef, M, C, rp.tl.TPR, rp.tl.RPI)
+  if constexpr (VEC == 8) {
+    if (relu && res && mbits) {
+      KDL_FWD_APPLY(true, true, true);
+      return hipGetLastError();
+    }
+  }
+  if (relu && res) KDL_FWD_APPLY(true, true, false);
+  else if (relu) KDL_FWD_APPLY(true, false, false);
+  else if (res) KDL_FWD_APPLY(false, true, false);
+  else KDL_FWD_APPLY(false, false, false);
 #undef KDL_FWD_APPLY
   return hipGetLastError();
 }
 
 template <typename T, int VEC, typename PT, int MASK>
-void bwd_launch(const ReducePlan& rp, const T* dy, const T* y, const T* x, const PT* gamma,
+void bwd_launch(const ReducePlan& rp, const T* dy, const T* y, const uint8_t* mbits, const T* x, const PT* gamma,
                 const PT* beta, const float* mean, const float* invstd, T* dx, T* dres, PT* dgamma,
                 PT* dbeta, float* ws, int64_t M, int C, bool training, hipStream_t s) {
   float* acc = ws_acc_bwd(ws, C);
   float* coef = ws_coef(ws, C);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, PT, VEC, MASK>), dim3(rp.gx, rp.tl.gy), dim3(kBlock),
-                     0, s, dy, y, x, gamma, beta, mean, invstd, M, C, rp.tl.TPR, rp.tl.RPI, acc);
+                     0, s, dy, y, mbits, x, gamma, beta, mean, invstd, M, C, rp.tl.TPR, rp.tl.RPI, acc);
   hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      s, acc, C, static_cast<float>(M), gamma, mean, invstd, training, dgamma, dbeta,
                      coef);
   dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
   if (dres)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PT, VEC, MASK, true>), grid, dim3(kBlock), 0, s, dy,
-                       y, x, gamma, beta, mean, invstd, coef, dx, dres, M, C, rp.tl.TPR, rp.tl.RPI);
+                       y, mbits, x, gamma, beta, mean, invstd, coef, dx, dres, M, C, rp.tl.TPR, rp.tl.RPI);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PT, VEC, MASK, false>), grid, dim3(kBlock), 0, s,
-                       dy, y, x, gamma, beta, mean, invstd, coef, dx, dres, M, C, rp.tl.TPR,
+                       dy, y, mbits, x, gamma, beta, mean, invstd, coef, dx, dres, M, C, rp.tl.TPR,
                        rp.tl.RPI);
 }
 
 template <typename T, int VEC, typename PT>
-hipError_t bwd_impl(const T* dy, const T* y, const T* x, const PT* gamma, const PT* beta,
+hipError_t bwd_impl(const T* dy, const T* y, const uint8_t* mbits, const T* x, const PT* gamma, const PT* beta,
                     const float* mean, const float* invstd, T* dx, T* dres, PT* dgamma, PT* dbeta,
                     float* ws, int64_t M, int C, bool relu, bool training, hipStream_t s) {
   ReducePlan rp = plan_reduce(M, C, VEC);
-  if (!relu)
-    bwd_launch<T, VEC, PT, kMaskNone>(rp, dy, y, x, gamma, beta, mean, invstd, dx, dres, dgamma,
-                                      dbeta, ws, M, C, training, s);
-  else if (dres || y == nullptr || beta == nullptr)
-    // with a residual the mask must come from y (it saw the residual)
-    bwd_launch<T, VEC, PT, kMaskY>(rp, dy, y, x, gamma, beta, mean, invstd, dx, dres, dgamma,
-                                   dbeta, ws, M, C, training, s);
-  else
-    bwd_launch<T, VEC, PT, kMaskX>(rp, dy, y, x, gamma, beta, mean, invstd, dx, dres, dgamma,
-                                   dbeta, ws, M, C, training, s);
+#define KDL_BWD(MODE)                                                                        \
+  bwd_launch<T, VEC, PT, MODE>(rp, dy, y, mbits, x, gamma, beta, mean, invstd, dx, dres, dgamma, \
+                               dbeta, ws, M, C, training, s)
+  if (!relu) KDL_BWD(kMaskNone);
+  else if (mbits != nullptr && VEC == 8) KDL_BWD(kMaskBits);
+  // with a residual the mask must come from y (it saw the residual)
+  else if (dres || y == nullptr || beta == nullptr) KDL_BWD(kMaskY);
+  else KDL_BWD(kMaskX);
+#undef KDL_BWD
   return hipGetLastError();
 }
 
@@ -539,7 +575,7 @@ int64_t bn_workspace_floats(int C) {
     }                                                                      \
   } while (0)
 
-hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* gamma,
+hipError_t bn_act_forward(const void* x, const void* res, void* y, uint8_t* mbits, const void* gamma,
                           const void* beta, float* rm, float* rv, float* save_mean,
                           float* save_invstd, float* ws, int64_t M, int C, int dtype, int pdtype,
                           bool relu, bool training, float momentum, float eps, hipStream_t s) {
@@ -547,21 +583,21 @@ hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* g
   hipError_t e = hipSuccess;
   KDL_DISPATCH_PT(pdtype, KDL_DISPATCH_T(dtype, C, {
     e = fwd_impl<T, VEC, PT>(static_cast<const T*>(x), static_cast<const T*>(res),
-                             static_cast<T*>(y), static_cast<const PT*>(gamma),
+                             static_cast<T*>(y), mbits, static_cast<const PT*>(gamma),
                              static_cast<const PT*>(beta), rm, rv, save_mean, save_invstd, ws, M,
                              C, relu, training, momentum, eps, s);
   }));
   return e;
 }
 
-hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const void* gamma,
+hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, const void* x, const void* gamma,
                            const void* beta, const float* mean, const float* invstd, void* dx,
                            void* dres, void* dgamma, void* dbeta, float* ws, int64_t M, int C,
                            int dtype, int pdtype, bool relu, bool training, hipStream_t s) {
   if (M <= 0 || C <= 0) return hipSuccess;
   hipError_t e = hipSuccess;
   KDL_DISPATCH_PT(pdtype, KDL_DISPATCH_T(dtype, C, {
-    e = bwd_impl<T, VEC, PT>(static_cast<const T*>(dy), static_cast<const T*>(y),
+    e = bwd_impl<T, VEC, PT>(static_cast<const T*>(dy), static_cast<const T*>(y), mbits,
                              static_cast<const T*>(x), static_cast<const PT*>(gamma),
                              static_cast<const PT*>(beta), mean, invstd, static_cast<T*>(dx),
                              static_cast<T*>(dres), static_cast<PT*>(dgamma),

@@ -11,11 +11,14 @@ namespace kdl {
 // ``ws`` is a per-layer fp32 workspace of bn_workspace_floats(C) elements,
 // zero when first used; the kernels leave it zero again (self-cleaning).
 int64_t bn_workspace_floats(int C);
-hipError_t bn_act_forward(const void* x, const void* res, void* y, const void* gamma,
+// ``mbits`` (optional, bf16 with C % 8 == 0, relu + residual only): uint8 [M, C/8]
+// ReLU mask written by the forward and read by the backward instead of y.
+hipError_t bn_act_forward(const void* x, const void* res, void* y, uint8_t* mbits, const void* gamma,
                           const void* beta, float* rm, float* rv, float* save_mean,
                           float* save_invstd, float* ws, int64_t M, int C, int dtype, int pdtype,
                           bool relu, bool training, float momentum, float eps, hipStream_t s);
-hipError_t bn_act_backward(const void* dy, const void* y, const void* x, const void* gamma,
+hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, const void* x,
+                           const void* gamma,
                            const void* beta, const float* mean, const float* invstd, void* dx,
                            void* dres, void* dgamma, void* dbeta, float* ws, int64_t M, int C,
                            int dtype, int pdtype, bool relu, bool training, hipStream_t s);

@@ -61,10 +61,11 @@ class _BNActFn(torch.autograd.Function):
         if residual is not None:
             residual = residual.contiguous(memory_format=torch.channels_last) if residual.dim() == 4 \
                 else residual.contiguous()
-        y, mean, invstd = ext.bn_act_fwd(x, weight, bias, running_mean, running_var,
-                                         residual, bool(relu), bool(training),
-                                         float(momentum), float(eps), ws)
-        ctx.save_for_backward(x, y, weight, bias, mean, invstd)
+        y, mean, invstd, mbits = ext.bn_act_fwd(x, weight, bias, running_mean, running_var,
+                                                residual, bool(relu), bool(training),
+                                                float(momentum), float(eps), ws, True)
+        # relu+residual layers: keep the packed 1-bit ReLU mask, not y, for the backward
+        ctx.save_for_backward(x, y if mbits is None else None, weight, bias, mean, invstd, mbits)
         ctx.ws = ws
         ctx.relu = relu
         ctx.has_residual = residual is not None
@@ -74,11 +75,11 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         ext = _ext.load()
-        x, y, weight, bias, mean, invstd = ctx.saved_tensors
+        x, y, weight, bias, mean, invstd, mbits = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
         dx, dgamma, dbeta, dres = ext.bn_act_bwd(dy, x, y, weight, bias, mean, invstd,
                                                  bool(ctx.relu), bool(ctx.has_residual),
-                                                 bool(ctx.training), ctx.ws)
+                                                 bool(ctx.training), ctx.ws, mbits)
         return dx, dgamma, dbeta, None, None, (dres if ctx.has_residual else None), \
             None, None, None, None, None
 

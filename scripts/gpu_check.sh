@@ -39,6 +39,11 @@ want benchab && run_step bench_torch 600 python bench.py --steps 20 --warmup 8 -
 want prof   && run_step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 3
 want benchfind && run_step bench_find 900 python bench.py --steps 20 --warmup 8 --conv-benchmark 1
 want launch && run_step bench_launch 600 python -m kubedl_amd.cli bench-launch --jobs 1 --gpus 1 --steps 20 --warmup 5
+if want bnsweep; then
+  for mr in ${SWEEP:-128 256 512 1024}; do
+    KDL_BN_MIN_ROWS=$mr run_step bench_minrows_$mr 600 python bench.py --steps 20 --warmup 8
+  done
+fi
 want convgemm && run_step conv_vs_gemm 600 python scripts/conv_vs_gemm.py
 want benchimm && run_step bench_immediate 600 python bench.py --steps 20 --warmup 8 --conv-benchmark 0
 # ship the MIOpen find-db / kernel cache back (merged into gpurun_out/)
