@@ -7,7 +7,10 @@ import argparse
 import json
 import os
 
+import sys
+
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, _ROOT)
 os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db", "user"))
 os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_ROOT, "miopen_db", "cache"))
 
