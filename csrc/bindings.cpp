@@ -136,6 +136,63 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
   return {dx, dgamma, dbeta, has_residual ? dres : at::Tensor()};
 }
 
+std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
+                                    const at::Tensor& running_mean, const at::Tensor& running_var,
+                                    bool training, double momentum, double eps,
+                                    const c10::optional<at::Tensor>& acc) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && is_nhwc_dense(x) && x.scalar_type() == at::kBFloat16,
+              "bn_pool_fwd: x must be a channels_last bf16 NCHW tensor");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0, "bn_pool_fwd: C % 8 == 0");
+  TORCH_CHECK(weight.numel() == C && bias.numel() == C && running_mean.numel() == C &&
+                  running_var.numel() == C && running_mean.scalar_type() == at::kFloat,
+              "bn_pool_fwd: per-channel tensors");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, PH, PW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N, PH, PW, C}, x.options().dtype(at::kByte));
+  auto fopt = x.options().dtype(at::kFloat);
+  auto save_mean = at::empty({C}, fopt);
+  auto save_invstd = at::empty({C}, fopt);
+  at::Tensor a = get_acc(acc, C, x);
+  check_hip(kdl::bn_pool_forward(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), weight.data_ptr(),
+                                 bias.data_ptr(), running_mean.data_ptr<float>(),
+                                 running_var.data_ptr<float>(), save_mean.data_ptr<float>(),
+                                 save_invstd.data_ptr<float>(), a.data_ptr<float>(), static_cast<int>(N),
+                                 static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                                 dtype_code(weight), training, static_cast<float>(momentum),
+                                 static_cast<float>(eps), cur_stream()),
+            "bn_pool_forward");
+  return {y, save_mean, save_invstd, idx};
+}
+
+std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dyp, const at::Tensor& idx, const at::Tensor& x,
+                                    const at::Tensor& weight, const at::Tensor& bias, const at::Tensor& mean,
+                                    const at::Tensor& invstd, bool training,
+                                    const c10::optional<at::Tensor>& acc) {
+  TORCH_CHECK(is_nhwc_dense(x) && is_nhwc_dense(dyp) && dyp.scalar_type() == at::kBFloat16 &&
+                  x.scalar_type() == at::kBFloat16,
+              "bn_pool_bwd: channels_last bf16 tensors");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dyp.size(0) == N && dyp.size(1) == C && dyp.size(2) == PH && dyp.size(3) == PW,
+              "bn_pool_bwd: pooled gradient shape");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.numel() == N * PH * PW * C,
+              "bn_pool_bwd: idx");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto dx = at::empty_like(x);
+  auto dgamma = at::empty_like(weight);
+  auto dbeta = at::empty_like(weight);
+  at::Tensor a = get_acc(acc, C, x);
+  check_hip(kdl::bn_pool_backward(dyp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), weight.data_ptr(),
+                                  bias.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                  dx.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), a.data_ptr<float>(),
+                                  static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
+                                  static_cast<int>(C), dtype_code(weight), training, cur_stream()),
+            "bn_pool_backward");
+  return {dx, dgamma, dbeta};
+}
+
 // ------------------------------------------------------------------ optimizers
 kdl::OptHyper make_hyper(double lr, double momentum, double dampening, double eps, double bc1,
                          double bc2, double grad_scale, bool nesterov, bool first_step, bool adam_w,
@@ -401,6 +458,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC");
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC");
+  m.def("bn_pool_fwd", &bn_pool_fwd, "stem BatchNorm + ReLU + max-pool(3,2,1) forward, NHWC bf16");
+  m.def("bn_pool_bwd", &bn_pool_bwd, "stem BatchNorm + ReLU + max-pool(3,2,1) backward, NHWC bf16");
   m.def("bn_workspace_floats", &bn_ws_floats, "per-layer BN workspace size (fp32 elements)");
   m.def("sgd_step", &sgd_step, "flat chunked fused SGD-momentum with fp32 master weights");
   m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights");

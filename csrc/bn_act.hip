@@ -427,6 +427,186 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(
   if (r < M) body(r);
 }
 
+// ---------------------------------------------------------------- stem: BN + ReLU + max-pool 3x3/s2/p1
+// The ResNet stem's BN output is only ever read by the max-pool, so it is
+// never materialised: the forward writes the pooled map plus a 1-byte
+// in-window argmax per channel (first maximum in (kh, kw) scan order, the
+// tie rule of torch's NHWC max-pool, on the bf16-rounded ReLU output); the
+// backward rebuilds d(relu output) at each input pixel from the <= 2x2
+// windows that contain it and feeds it straight into the BN reduce/apply.
+// Saves the full-resolution y write + re-read in the forward and the
+// full-resolution d(y) write + two re-reads in the backward.
+__device__ __forceinline__ float bf16_round(float v) { return bf16_to_f32(f32_to_bf16(v)); }
+
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(
+    const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
+    const float* __restrict__ coef, int64_t MP, int C, int H, int W, int PH, int PW, int TPR,
+    int RPI) {
+  const int t = threadIdx.x;
+  const int lc = t % TPR, r0 = t / TPR;
+  const int cg = blockIdx.y * TPR + lc;
+  if (r0 >= RPI || cg >= C / VEC) return;
+  const int c0 = cg * VEC;
+  float sc[VEC], sf[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { sc[i] = coef[c0 + i]; sf[i] = coef[C + c0 + i]; }
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
+  for (int64_t p = static_cast<int64_t>(blockIdx.x) * RPI + r0; p < MP; p += step) {
+    const int64_t n = p / (static_cast<int64_t>(PH) * PW);
+    const int rem = static_cast<int>(p - n * PH * PW);
+    const int ph = rem / PW, pw = rem % PW;
+    float best[VEC];
+    uint32_t bi[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { best[i] = -__builtin_inff(); bi[i] = 0; }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * ph - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * pw - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v[VEC];
+        VecIO<bf16_t, VEC>::load(x + ((n * H + ih) * W + iw) * C + c0, v);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          float z = fmaf(v[i], sc[i], sf[i]);
+          z = bf16_round(z > 0.f ? z : 0.f);
+          if (z > best[i]) { best[i] = z; bi[i] = kh * 3 + kw; }
+        }
+      }
+    }
+    VecIO<bf16_t, VEC>::store(y + p * C + c0, best);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      if (i < 4) lo |= bi[i] << (8 * i);
+      else hi |= bi[i] << (8 * (i - 4));
+    }
+    if constexpr (VEC == 8) {
+      *reinterpret_cast<uint2*>(idx + p * C + c0) = make_uint2(lo, hi);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) idx[p * C + c0 + i] = static_cast<uint8_t>(bi[i]);
+    }
+  }
+}
+
+// d(relu output) at input pixel (n, h, w), channels c0..c0+VEC: the pooled
+// gradients of the windows whose argmax is this pixel.
+template <int VEC>
+__device__ __forceinline__ void pool_grad_at(const bf16_t* __restrict__ dyp,
+                                             const uint8_t* __restrict__ idx, int64_t n, int h,
+                                             int w, int C, int c0, int PH, int PW, float (&g)[VEC]) {
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) g[i] = 0.f;
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) {
+    const int ph = (h + 1) / 2 - dh;
+    const int kh = h + 1 - 2 * ph;
+    if (ph < 0 || ph >= PH || kh > 2) continue;
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int pw = (w + 1) / 2 - dw;
+      const int kw = w + 1 - 2 * pw;
+      if (pw < 0 || pw >= PW || kw > 2) continue;
+      const uint32_t pos = kh * 3 + kw;
+      const int64_t p = (n * PH + ph) * PW + pw;
+      uint8_t ib[VEC];
+      if constexpr (VEC == 8) {
+        const uint2 u = *reinterpret_cast<const uint2*>(idx + p * C + c0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          ib[i] = static_cast<uint8_t>(u.x >> (8 * i));
+          ib[i + 4] = static_cast<uint8_t>(u.y >> (8 * i));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) ib[i] = idx[p * C + c0 + i];
+      }
+      float d[VEC];
+      VecIO<bf16_t, VEC>::load(dyp + p * C + c0, d);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) g[i] += (ib[i] == pos) ? d[i] : 0.f;
+    }
+  }
+}
+
+template <typename PT, int VEC>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dyp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ x,
+    const PT* __restrict__ gamma, const PT* __restrict__ beta, const float* __restrict__ mean,
+    const float* __restrict__ invstd, int64_t M, int C, int H, int W, int PH, int PW, int TPR,
+    int RPI, float* __restrict__ acc) {
+  __shared__ float sh[2 * kBlock * VEC];
+  const int t = threadIdx.x;
+  const int lc = t % TPR, r0 = t / TPR;
+  const int cg = blockIdx.y * TPR + lc;
+  const bool active = (r0 < RPI) && (cg < C / VEC);
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
+  const int c0 = cg * VEC;
+  float mu[VEC], sa[VEC], sb[VEC], sc[VEC], sf[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { sa[i] = 0.f; sb[i] = 0.f; mu[i] = 0.f; sc[i] = 0.f; sf[i] = 0.f; }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) mu[i] = mean[c0 + i];
+    mask_coeffs<PT, VEC>(gamma, beta, mean, invstd, c0, sc, sf);
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
+      const int64_t n = r / (static_cast<int64_t>(H) * W);
+      const int rem = static_cast<int>(r - n * H * W);
+      float g[VEC], xv[VEC];
+      VecIO<bf16_t, VEC>::load(x + r * C + c0, xv);
+      pool_grad_at<VEC>(dyp, idx, n, rem / W, rem % W, C, c0, PH, PW, g);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float gi = fmaf(xv[i], sc[i], sf[i]) > 0.f ? g[i] : 0.f;
+        sa[i] += gi;
+        sb[i] = fmaf(gi, xv[i] - mu[i], sb[i]);
+      }
+    }
+  }
+  float* rep = acc + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
+  block_fold_atomic<VEC>(sa, sb, sh, t, lc, r0, TPR, RPI, active, rep + c0, rep + C + c0);
+}
+
+template <typename PT, int VEC>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(
+    const bf16_t* __restrict__ dyp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ x,
+    const PT* __restrict__ gamma, const PT* __restrict__ beta, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ coef, bf16_t* __restrict__ dx,
+    int64_t M, int C, int H, int W, int PH, int PW, int TPR, int RPI) {
+  const int t = threadIdx.x;
+  const int lc = t % TPR, r0 = t / TPR;
+  const int cg = blockIdx.y * TPR + lc;
+  if (r0 >= RPI || cg >= C / VEC) return;
+  const int c0 = cg * VEC;
+  float k[VEC], c1[VEC], c0v[VEC], sc[VEC], sf[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    k[i] = coef[c0 + i];
+    c1[i] = coef[C + c0 + i];
+    c0v[i] = coef[2 * C + c0 + i];
+  }
+  mask_coeffs<PT, VEC>(gamma, beta, mean, invstd, c0, sc, sf);
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
+    const int64_t n = r / (static_cast<int64_t>(H) * W);
+    const int rem = static_cast<int>(r - n * H * W);
+    float g[VEC], xv[VEC];
+    VecIO<bf16_t, VEC>::load(x + r * C + c0, xv);
+    pool_grad_at<VEC>(dyp, idx, n, rem / W, rem % W, C, c0, PH, PW, g);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const float gi = fmaf(xv[i], sc[i], sf[i]) > 0.f ? g[i] : 0.f;
+      xv[i] = fmaf(k[i], gi, fmaf(c1[i], xv[i], c0v[i]));
+    }
+    VecIO<bf16_t, VEC>::store(dx + r * C + c0, xv);
+  }
+}
+
 // ---------------------------------------------------------------- host side
 struct ReducePlan {
   Tiling tl;
@@ -604,6 +784,70 @@ hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, 
                              static_cast<PT*>(dbeta), ws, M, C, relu, training, s);
   }));
   return e;
+}
+
+
+hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gamma, const void* beta,
+                           float* rm, float* rv, float* save_mean, float* save_invstd, float* ws,
+                           int N, int H, int W, int C, int pdtype, bool training, float momentum,
+                           float eps, hipStream_t s) {
+  if (N <= 0 || C <= 0 || C % 8 != 0) return hipErrorInvalidValue;
+  constexpr int VEC = 8;
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  const int PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;  // k3 s2 p1
+  const int64_t MP = static_cast<int64_t>(N) * PH * PW;
+  ReducePlan rp = plan_reduce(M, C, VEC);
+  float* acc = ws_acc_fwd(ws, C);
+  float* coef = ws_coef(ws, C);
+  const int fin_grid = (C + kBlock - 1) / kBlock;
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  KDL_DISPATCH_PT(pdtype, {
+    if (training) {
+      hipLaunchKernelGGL((bn_fwd_stats_kernel<bf16_t, VEC>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
+                         xb, M, C, rp.tl.TPR, rp.tl.RPI, acc);
+      hipLaunchKernelGGL((bn_fwd_finalize_kernel<bf16_t, PT>), dim3(fin_grid), dim3(kBlock), 0, s, xb,
+                         acc, C, static_cast<float>(M), static_cast<const PT*>(gamma),
+                         static_cast<const PT*>(beta), rm, rv, momentum, eps, save_mean, save_invstd,
+                         coef);
+    } else {
+      hipLaunchKernelGGL((bn_eval_prep_kernel<PT>), dim3(fin_grid), dim3(kBlock), 0, s, C,
+                         static_cast<const PT*>(gamma), static_cast<const PT*>(beta), rm, rv, eps,
+                         save_mean, save_invstd, coef);
+    }
+  });
+  dim3 grid(apply_gx(MP, rp.tl), rp.tl.gy);
+  hipLaunchKernelGGL((bn_pool_fwd_kernel<VEC>), grid, dim3(kBlock), 0, s, xb,
+                     static_cast<bf16_t*>(y), idx, coef, MP, C, H, W, PH, PW, rp.tl.TPR, rp.tl.RPI);
+  return hipGetLastError();
+}
+
+hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, const void* gamma,
+                            const void* beta, const float* mean, const float* invstd, void* dx,
+                            void* dgamma, void* dbeta, float* ws, int N, int H, int W, int C,
+                            int pdtype, bool training, hipStream_t s) {
+  if (N <= 0 || C <= 0 || C % 8 != 0) return hipErrorInvalidValue;
+  constexpr int VEC = 8;
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  const int PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;
+  ReducePlan rp = plan_reduce(M, C, VEC);
+  float* acc = ws_acc_bwd(ws, C);
+  float* coef = ws_coef(ws, C);
+  const bf16_t* db = static_cast<const bf16_t*>(dyp);
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  KDL_DISPATCH_PT(pdtype, {
+    const PT* g = static_cast<const PT*>(gamma);
+    const PT* b = static_cast<const PT*>(beta);
+    hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<PT, VEC>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
+                       db, idx, xb, g, b, mean, invstd, M, C, H, W, PH, PW, rp.tl.TPR, rp.tl.RPI, acc);
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       s, acc, C, static_cast<float>(M), g, mean, invstd, training,
+                       static_cast<PT*>(dgamma), static_cast<PT*>(dbeta), coef);
+    dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
+    hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<PT, VEC>), grid, dim3(kBlock), 0, s, db, idx, xb, g, b,
+                       mean, invstd, coef, static_cast<bf16_t*>(dx), M, C, H, W, PH, PW, rp.tl.TPR,
+                       rp.tl.RPI);
+  });
+  return hipGetLastError();
 }
 
 }  // namespace kdl

@@ -23,6 +23,17 @@ hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, 
                            void* dres, void* dgamma, void* dbeta, float* ws, int64_t M, int C,
                            int dtype, int pdtype, bool relu, bool training, hipStream_t s);
 
+// Stem BN + ReLU + max-pool(3, 2, 1), bf16 NHWC x [N, H, W, C], C % 8 == 0.
+// y [N, PH, PW, C]; idx uint8 [N, PH, PW, C] = in-window argmax (kh*3 + kw).
+hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gamma, const void* beta,
+                           float* rm, float* rv, float* save_mean, float* save_invstd, float* ws,
+                           int N, int H, int W, int C, int pdtype, bool training, float momentum,
+                           float eps, hipStream_t s);
+hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, const void* gamma,
+                            const void* beta, const float* mean, const float* invstd, void* dx,
+                            void* dgamma, void* dbeta, float* ws, int N, int H, int W, int C,
+                            int pdtype, bool training, hipStream_t s);
+
 // ---- optim.hip
 struct OptChunk {
   int64_t start;

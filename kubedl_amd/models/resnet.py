@@ -62,6 +62,17 @@ class BNAct(nn.Module):
             residual=residual, relu=self.relu, training=self.training,
             momentum=self.momentum, eps=self.eps, backend=self.backend, workspace=ws)
 
+    def forward_maxpool(self, x: torch.Tensor) -> torch.Tensor:
+        """maxpool(3, 2, 1)(self(x)) for the stem, fused on the HIP backend."""
+        ws = None
+        if x.is_cuda and self.backend != "torch":
+            if self._ws is None or self._ws.device != x.device:
+                self._ws = bn_ops.workspace_for(self.channels, x.device)
+            ws = self._ws
+        return bn_ops.batch_norm_relu_maxpool(
+            x, self.weight, self.bias, self.running_mean, self.running_var, training=self.training,
+            momentum=self.momentum, eps=self.eps, backend=self.backend, workspace=ws)
+
 
 class Bottleneck(nn.Module):
     expansion = 4
@@ -115,7 +126,7 @@ class ResNet(nn.Module):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.bn1.forward_maxpool(self.conv1(x))  # == self.maxpool(self.bn1(conv1(x)))
         x = self.layers(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

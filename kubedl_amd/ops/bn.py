@@ -95,3 +95,40 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, residual=None, re
                              training, momentum, eps)
     return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, relu,
                           training, momentum, eps, workspace)
+
+
+class _BNPoolFn(torch.autograd.Function):
+    """Stem BN + ReLU + max-pool(3, 2, 1): the full-resolution BN output is
+    never materialised (``bn_pool_forward`` / ``bn_pool_backward``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, ws):
+        ext = _ext.load()
+        x = x.contiguous(memory_format=torch.channels_last)
+        y, mean, invstd, idx = ext.bn_pool_fwd(x, weight, bias, running_mean, running_var, bool(training),
+                                               float(momentum), float(eps), ws)
+        ctx.save_for_backward(x, idx, weight, bias, mean, invstd)
+        ctx.ws = ws
+        ctx.training = training
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ext = _ext.load()
+        x, idx, weight, bias, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dgamma, dbeta = ext.bn_pool_bwd(dy, idx, x, weight, bias, mean, invstd, bool(ctx.training), ctx.ws)
+        return dx, dgamma, dbeta, None, None, None, None, None, None
+
+
+def batch_norm_relu_maxpool(x, weight, bias, running_mean, running_var, training=True, momentum=0.1,
+                            eps=1e-5, backend="auto", workspace=None):
+    """maxpool3x3s2p1(relu(batch_norm(x))) -- one fused op on the HIP backend."""
+    if backend == "auto":
+        backend = "hip" if (x.is_cuda and _ext.available()) else "torch"
+        if x.is_cuda and backend == "torch":
+            _ext.require_on_gpu("batch_norm_relu_maxpool")
+    if backend == "torch" or x.dtype != torch.bfloat16 or x.dim() != 4 or x.shape[1] % 8:
+        y = _torch_bn_act(x, weight, bias, running_mean, running_var, None, True, training, momentum, eps)
+        return F.max_pool2d(y, 3, 2, 1)
+    return _BNPoolFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, workspace)

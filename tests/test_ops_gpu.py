@@ -225,3 +225,45 @@ def test_resnet_hip_vs_torch_backend_step():
         res.append((y.detach(), m.conv1.weight.grad.clone(), m.layers[0].bn1.weight.grad.clone()))
     for a, b in zip(*res):
         torch.testing.assert_close(b, a, atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 16, 9, 7), (3, 8, 2, 3)])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_relu_maxpool_matches_reference(shape, training):
+    """Fused stem op vs fp32 torch: maxpool(relu(bn(x))) forward, and the
+    gradients of x, gamma, beta (argmax routing computed on the bf16 ReLU
+    output like torch's max-pool over a bf16 tensor)."""
+    from kubedl_amd.ops.bn import batch_norm_relu_maxpool, workspace_for
+    torch.manual_seed(0)
+    dev = "cuda"
+    C = shape[1]
+    x = torch.randn(shape, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (1 + 0.1 * torch.randn(C, device=dev)).requires_grad_(True)
+    b = (0.1 * torch.randn(C, device=dev)).requires_grad_(True)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm.clone(), rv.clone()
+    xh = x.clone().requires_grad_(True)
+    y = batch_norm_relu_maxpool(xh, w, b, rm, rv, training=training, backend="hip",
+                                workspace=workspace_for(C, dev))
+    # reference: bn in fp32, relu, round to bf16 (what the unfused bf16 model pools over), pool
+    xr = x.float().requires_grad_(True)
+    wr, br = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    z = torch.nn.functional.batch_norm(xr, rm2, rv2, wr, br, training=training, momentum=0.1, eps=1e-5)
+    zb = torch.relu(z)
+    zq = zb + (zb.bfloat16().float() - zb).detach()  # straight-through bf16 rounding
+    yr = torch.nn.functional.max_pool2d(zq, 3, 2, 1)
+    # a 1-ulp bf16 rounding difference between the fused fp32 expression and
+    # torch's can flip a near-tie argmax: allow a tiny fraction of mismatches
+    def frac_off(a, b, tol):
+        return (~torch.isclose(a, b, atol=tol, rtol=tol)).float().mean().item()
+    assert frac_off(y.float(), yr, 2e-2) < 1e-3
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g.bfloat16().float())
+    assert frac_off(xh.grad.float(), xr.grad, 5e-2) < 1e-3
+    torch.testing.assert_close(w.grad, wr.grad, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(b.grad, br.grad, atol=5e-2, rtol=2e-2)
+    if training:
+        torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(rv, rv2, atol=1e-4, rtol=1e-3)
