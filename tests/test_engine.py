@@ -315,9 +315,13 @@ def test_xdl_min_finish_and_zk_addr(mgr):
     uid = job["metadata"]["uid"]
     job = mgr.wait_for_condition("XDLJob", "default", "xdl", ["Succeeded", "Failed"], timeout=60)
     assert "Succeeded" in _cond_types(job), job["status"]
-    env = {e["name"]: e["value"] for e in mgr.store.get("Pod", "default", "xdl-worker-0")["spec"]["containers"][0]["env"]}
+    # cleanPodPolicy Running deletes workers still running when the success threshold is hit, so read any survivor
+    workers = [p for p in mgr.store.list("Pod") if p["metadata"]["name"].startswith("xdl-worker-")]
+    assert workers
+    p = workers[0]
+    env = {e["name"]: e["value"] for e in p["spec"]["containers"][0]["env"]}
     assert env["ZK_ADDR"] == "zk://zk-0:2181/" + uid
-    assert env["TASK_NAME"] == "worker" and env["TASK_INDEX"] == "0"
+    assert env["TASK_NAME"] == "worker" and env["TASK_INDEX"] == p["metadata"]["name"].rsplit("-", 1)[1]
     env = {e["name"]: e["value"] for e in mgr.store.get("PodGroup", "default", "xdl")["metadata"].items()} \
         if mgr.store.try_get("PodGroup", "default", "xdl") else None  # no gang without the flag
     assert env is None
