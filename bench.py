@@ -56,6 +56,8 @@ def main(argv=None) -> int:
     ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--conv-benchmark", type=int, default=0,
                     help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "autograd"],
+                    help="fused = explicit engine (fused 1x1-conv GEMMs + staged BN); autograd = module + autograd")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")
     args = ap.parse_args(argv)
@@ -70,7 +72,8 @@ def main(argv=None) -> int:
               file=sys.stderr)
 
     trainer = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
-                            bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark))
+                            bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark),
+                            engine=args.engine)
     sync(info)
     kdist.barrier(info)
     launch_delay = kdist.all_reduce_max(time.time() - T_PROC_START, info)
@@ -116,6 +119,7 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{n}",
                 "optimizer": "fused SGD-momentum (fp32 master)",
                 "bn_backend": args.bn_backend,
+                "engine": trainer.engine_kind,
                 "conv_benchmark": bool(args.conv_benchmark),
             },
             "steps_per_sec": round(args.steps / dt, 4),

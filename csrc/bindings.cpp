@@ -103,7 +103,8 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
                                    const c10::optional<at::Tensor>& mask) {
   const bool has_mask = mask.has_value() && mask->defined();
   const bool has_y = y_opt.has_value() && y_opt->defined();
-  TORCH_CHECK(has_y || has_mask || !relu, "bn_act_bwd: relu needs y or the packed mask");
+  // relu without a residual recomputes its mask from x; with a residual it needs y or the bits
+  TORCH_CHECK(has_y || has_mask || !relu || !has_residual, "bn_act_bwd: relu+residual needs y or the packed mask");
   TORCH_CHECK(is_nhwc_dense(dy) && is_nhwc_dense(x) && (!has_y || is_nhwc_dense(*y_opt)),
               "bn_act_bwd: tensors must be channels_last-dense");
   TORCH_CHECK(dy.sizes() == x.sizes() && (!has_y || y_opt->sizes() == x.sizes()),
@@ -452,6 +453,282 @@ void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at:
             "segment_adagrad");
 }
 
+
+// ------------------------------------------------------------------ engine ops: fused 1x1 convs + staged BN
+// These are the raw building blocks of kubedl_amd.models.resnet_engine (explicit
+// forward/backward of the ResNet-50 bottleneck).  Outputs are preallocated by the
+// caller; every pointer is checked for device, dtype, density and extent here
+// because the kernels trust their shape arguments.
+const void* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+float* opt_fptr(const c10::optional<at::Tensor>& t) {
+  if (!(t.has_value() && t->defined())) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "expected a contiguous fp32 tensor");
+  return t->data_ptr<float>();
+}
+void need_bf16(const at::Tensor& t, int64_t numel, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, what, ": bf16 GPU tensor expected");
+  // 4-D activations must be NHWC in memory (row = pixel, channels contiguous)
+  TORCH_CHECK(is_nhwc_dense(t), what, ": channels_last-dense (4-D) or contiguous (2-D) tensor expected");
+  TORCH_CHECK(t.numel() >= numel, what, ": too small (", t.numel(), " < ", numel, ")");
+}
+void need_opt_bf16(const c10::optional<at::Tensor>& t, int64_t numel, const char* what) {
+  if (t.has_value() && t->defined()) need_bf16(*t, numel, what);
+}
+void need_opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char* what) {
+  if (t.has_value() && t->defined())
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() >= numel, what,
+                ": fp32 contiguous GPU tensor of >= ", numel, " elements expected");
+}
+
+void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_t M, int64_t N, int64_t K,
+                  int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride,
+                  const c10::optional<at::Tensor>& pro_coef, int64_t epi, const c10::optional<at::Tensor>& shift,
+                  const c10::optional<at::Tensor>& acc, const c10::optional<at::Tensor>& ex,
+                  const c10::optional<at::Tensor>& emean, const c10::optional<at::Tensor>& ecoef,
+                  const c10::optional<at::Tensor>& eres, int64_t res_stride, int64_t res_H, int64_t res_W,
+                  const c10::optional<at::Tensor>& ebits, const c10::optional<at::Tensor>& ex2,
+                  const c10::optional<at::Tensor>& emean2, const c10::optional<at::Tensor>& acc2) {
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_gemm: need K % 64 == 0, N % 64 == 0");
+  const int64_t rows_in = stride > 1 ? (M / (Hout * Wout)) * Hin * Win : M;
+  if (stride > 1) TORCH_CHECK(M % (Hout * Wout) == 0 && (Hout - 1) * stride < Hin && (Wout - 1) * stride < Win,
+                              "conv1x1_gemm: gather geometry");
+  need_bf16(A, rows_in * K, "conv1x1_gemm A");
+  need_bf16(B, N * K, "conv1x1_gemm B");
+  need_bf16(C, M * N, "conv1x1_gemm C");
+  need_opt_f32(pro_coef, 2 * K, "pro_coef");
+  const int64_t rep = 32 * 2 * N;
+  if (epi == 1) { TORCH_CHECK(opt_ptr(shift) && opt_ptr(acc), "epi STATS needs shift, acc"); need_opt_f32(shift, N, "shift"); need_opt_f32(acc, rep, "acc"); }
+  if (epi == 2) {
+    TORCH_CHECK(opt_ptr(ex) && opt_ptr(emean) && opt_ptr(ecoef) && opt_ptr(acc), "epi MASKX needs ex, emean, ecoef, acc");
+    need_opt_bf16(ex, M * N, "ex"); need_opt_f32(emean, N, "emean"); need_opt_f32(ecoef, 2 * N, "ecoef"); need_opt_f32(acc, rep, "acc");
+  }
+  if (epi == 3 || epi == 4) {
+    TORCH_CHECK(opt_ptr(eres), "epi RES/RESBITS needs eres");
+    if (res_stride > 1) {
+      TORCH_CHECK(M % (res_H * res_W) == 0, "conv1x1_gemm: residual geometry");
+      const int64_t ho = (res_H + res_stride - 1) / res_stride, wo = (res_W + res_stride - 1) / res_stride;
+      need_opt_bf16(eres, (M / (res_H * res_W)) * ho * wo * N, "eres");
+    } else {
+      need_opt_bf16(eres, M * N, "eres");
+    }
+  }
+  if (epi == 3) {
+    TORCH_CHECK(opt_ptr(ex) && opt_ptr(emean) && opt_ptr(acc) && opt_ptr(ebits), "epi RESBITS needs ex, emean, acc, ebits");
+    need_opt_bf16(ex, M * N, "ex"); need_opt_f32(emean, N, "emean"); need_opt_f32(acc, rep, "acc");
+    TORCH_CHECK(ebits->scalar_type() == at::kByte && ebits->is_contiguous() && ebits->numel() >= M * N / 8, "ebits");
+    if (opt_ptr(ex2)) {
+      need_opt_bf16(ex2, M * N, "ex2"); need_opt_f32(emean2, N, "emean2"); need_opt_f32(acc2, rep, "acc2");
+      TORCH_CHECK(opt_ptr(emean2) && opt_ptr(acc2), "ex2 needs emean2, acc2");
+    }
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  kdl::Conv1x1Args a{};
+  a.A = A.data_ptr(); a.B = B.data_ptr(); a.C = C.data_ptr();
+  a.M = static_cast<int>(M); a.N = static_cast<int>(N); a.K = static_cast<int>(K);
+  a.Hout = static_cast<int>(Hout); a.Wout = static_cast<int>(Wout); a.Hin = static_cast<int>(Hin);
+  a.Win = static_cast<int>(Win); a.stride = static_cast<int>(stride);
+  a.pro_coef = opt_fptr(pro_coef);
+  a.epi = static_cast<int>(epi);
+  a.shift = opt_fptr(shift); a.acc = opt_fptr(acc);
+  a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
+  a.eres = opt_ptr(eres); a.res_stride = static_cast<int>(res_stride); a.res_H = static_cast<int>(res_H);
+  a.res_W = static_cast<int>(res_W);
+  a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
+  a.ex2 = opt_ptr(ex2); a.emean2 = opt_fptr(emean2); a.acc2 = opt_fptr(acc2);
+  check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");
+}
+
+int64_t conv1x1_wgrad_splits(int64_t M, int64_t N, int64_t K) {
+  return kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
+}
+
+void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
+                   at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t M, int64_t N, int64_t K,
+                   int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride) {
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_wgrad: need K % 64 == 0, N % 64 == 0");
+  const int64_t rows_in = stride > 1 ? (M / (Hout * Wout)) * Hin * Win : M;
+  need_bf16(G, M * N, "conv1x1_wgrad G");
+  need_bf16(A, rows_in * K, "conv1x1_wgrad A");
+  need_opt_f32(pro_coef, 2 * K, "pro_coef");
+  TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() && dw32.numel() == N * K,
+              "conv1x1_wgrad: dw32 fp32 contiguous [N, K]");
+  if (dW.has_value() && dW->defined())
+    TORCH_CHECK(dW->is_cuda() && dW->is_contiguous() && dW->numel() == N * K && dW->scalar_type() == at::kBFloat16,
+                "conv1x1_wgrad: dW bf16 contiguous [N, K]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(G.device());
+  check_hip(kdl::conv1x1_wgrad(G.data_ptr(), A.data_ptr(), opt_fptr(pro_coef), dw32.data_ptr<float>(),
+                               dW.has_value() && dW->defined() ? dW->data_ptr() : nullptr, static_cast<float>(scale),
+                               static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Hout),
+                               static_cast<int>(Wout), static_cast<int>(Hin), static_cast<int>(Win),
+                               static_cast<int>(stride), cur_stream()),
+            "conv1x1_wgrad");
+}
+
+int64_t pdtype_of(const at::Tensor& t) { return t.scalar_type() == at::kBFloat16 ? 1 : 0; }
+
+void need_ws(const at::Tensor& ws, int64_t C) {
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() &&
+                  ws.numel() >= kdl::bn_workspace_floats(static_cast<int>(C)),
+              "bn stage: workspace must be fp32 >= bn_workspace_floats(C)");
+}
+
+int64_t bn_coef_offset(int64_t C) { return 32 * 4 * C; }
+
+void bn_stage_fwd_stats(const at::Tensor& x, at::Tensor ws, int64_t M, int64_t C) {
+  need_bf16(x, M * C, "bn_stage_fwd_stats x");
+  need_ws(ws, C);
+  TORCH_CHECK(C % 8 == 0, "C % 8");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::bn_stage_fwd_stats(x.data_ptr(), ws.data_ptr<float>(), M, static_cast<int>(C), cur_stream()),
+            "bn_stage_fwd_stats");
+}
+
+void bn_stage_fwd_finalize(const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& shift, at::Tensor ws,
+                           int64_t M, int64_t C, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor rm,
+                           at::Tensor rv, at::Tensor save_mean, at::Tensor save_invstd, bool training,
+                           double momentum, double eps) {
+  TORCH_CHECK(opt_ptr(x) || opt_ptr(shift), "bn_stage_fwd_finalize: x or shift");
+  need_opt_bf16(x, C, "x");
+  need_opt_f32(shift, C, "shift");
+  need_ws(ws, C);
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && gamma.scalar_type() == beta.scalar_type(), "gamma/beta");
+  for (const at::Tensor* t : {&rm, &rv, &save_mean, &save_invstd})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(), "fp32 [C] stats");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(ws.device());
+  check_hip(kdl::bn_stage_fwd_finalize(opt_ptr(x), opt_fptr(shift), ws.data_ptr<float>(), M, static_cast<int>(C),
+                                       gamma.data_ptr(), beta.data_ptr(), rm.data_ptr<float>(), rv.data_ptr<float>(),
+                                       save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                                       static_cast<int>(pdtype_of(gamma)), training, static_cast<float>(momentum),
+                                       static_cast<float>(eps), cur_stream()),
+            "bn_stage_fwd_finalize");
+}
+
+void bn_stage_fwd_apply(const at::Tensor& x, const at::Tensor& ws, const c10::optional<at::Tensor>& res,
+                        const c10::optional<at::Tensor>& xd, const c10::optional<at::Tensor>& wsd, at::Tensor y,
+                        const c10::optional<at::Tensor>& mbits, int64_t M, int64_t C, bool relu) {
+  need_bf16(x, M * C, "x");
+  need_bf16(y, M * C, "y");
+  need_ws(ws, C);
+  need_opt_bf16(res, M * C, "res");
+  need_opt_bf16(xd, M * C, "xd");
+  if (opt_ptr(xd)) need_ws(*wsd, C);
+  uint8_t* mb = nullptr;
+  if (mbits.has_value() && mbits->defined()) {
+    TORCH_CHECK(mbits->scalar_type() == at::kByte && mbits->is_contiguous() && mbits->numel() >= M * C / 8, "mbits");
+    mb = mbits->data_ptr<uint8_t>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::bn_stage_fwd_apply(x.data_ptr(), ws.data_ptr<float>(), opt_ptr(res), opt_ptr(xd),
+                                    opt_ptr(xd) ? wsd->data_ptr<float>() : nullptr, y.data_ptr(), mb, M,
+                                    static_cast<int>(C), relu, cur_stream()),
+            "bn_stage_fwd_apply");
+}
+
+void bn_stage_bwd_mask_reduce(const at::Tensor& dy, int64_t dy_rows_per_img, double dy_scale, const at::Tensor& mbits,
+                              const at::Tensor& x, const at::Tensor& mean, at::Tensor gout, at::Tensor ws, int64_t M,
+                              int64_t C, const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                              const c10::optional<at::Tensor>& ws2) {
+  if (opt_ptr(x2)) {
+    need_opt_bf16(x2, M * C, "x2");
+    need_opt_f32(mean2, C, "mean2");
+    TORCH_CHECK(opt_ptr(mean2) && opt_ptr(ws2), "x2 needs mean2, ws2");
+    need_ws(*ws2, C);
+  }
+  need_bf16(dy, dy_rows_per_img > 0 ? (M / dy_rows_per_img) * C : M * C, "dy");
+  if (dy_rows_per_img > 0) TORCH_CHECK(M % dy_rows_per_img == 0, "dy rows per image");
+  need_bf16(x, M * C, "x");
+  need_bf16(gout, M * C, "gout");
+  need_ws(ws, C);
+  TORCH_CHECK(mbits.scalar_type() == at::kByte && mbits.numel() >= M * C / 8, "mbits");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == C, "mean");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::bn_stage_bwd_mask_reduce(dy.data_ptr(), static_cast<int>(dy_rows_per_img),
+                                          static_cast<float>(dy_scale), mbits.data_ptr<uint8_t>(), x.data_ptr(),
+                                          mean.data_ptr<float>(), gout.data_ptr(), ws.data_ptr<float>(), M,
+                                          static_cast<int>(C), opt_ptr(x2), opt_fptr(mean2),
+                                          opt_ptr(x2) ? ws2->data_ptr<float>() : nullptr, cur_stream()),
+            "bn_stage_bwd_mask_reduce");
+}
+
+void check_bn_params(const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& mean,
+                     const at::Tensor& invstd, int64_t C) {
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && gamma.scalar_type() == beta.scalar_type() &&
+                  gamma.is_contiguous() && beta.is_contiguous(),
+              "gamma/beta [C], same dtype");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && invstd.scalar_type() == at::kFloat && mean.numel() == C &&
+                  invstd.numel() == C,
+              "mean/invstd fp32 [C]");
+}
+
+void bn_stage_bwd_reduce(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& beta,
+                         const at::Tensor& mean, const at::Tensor& invstd, at::Tensor ws, int64_t M, int64_t C,
+                         bool relu_mask_x) {
+  need_bf16(dy, M * C, "dy");
+  need_bf16(x, M * C, "x");
+  need_ws(ws, C);
+  check_bn_params(gamma, beta, mean, invstd, C);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::bn_stage_bwd_reduce(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                     mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(), M,
+                                     static_cast<int>(C), relu_mask_x, static_cast<int>(pdtype_of(gamma)),
+                                     cur_stream()),
+            "bn_stage_bwd_reduce");
+}
+
+void bn_stage_bwd_apply_maskx(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
+                              const at::Tensor& beta, const at::Tensor& mean, const at::Tensor& invstd,
+                              const at::Tensor& ws, at::Tensor dx, int64_t M, int64_t C) {
+  need_bf16(dy, M * C, "dy");
+  need_bf16(x, M * C, "x");
+  need_bf16(dx, M * C, "dx");
+  need_ws(ws, C);
+  check_bn_params(gamma, beta, mean, invstd, C);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::bn_stage_bwd_apply_maskx(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                          mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(),
+                                          dx.data_ptr(), M, static_cast<int>(C), static_cast<int>(pdtype_of(gamma)),
+                                          cur_stream()),
+            "bn_stage_bwd_apply_maskx");
+}
+
+void bn_stage_bwd_finalize(at::Tensor ws, int64_t M, int64_t C, const at::Tensor& gamma, const at::Tensor& mean,
+                           const at::Tensor& invstd, at::Tensor dgamma, at::Tensor dbeta, bool training) {
+  need_ws(ws, C);
+  TORCH_CHECK(gamma.numel() == C && dgamma.numel() == C && dbeta.numel() == C &&
+                  dgamma.scalar_type() == gamma.scalar_type() && dbeta.scalar_type() == gamma.scalar_type() &&
+                  dgamma.is_contiguous() && dbeta.is_contiguous(),
+              "bn_stage_bwd_finalize: gamma/dgamma/dbeta [C], same dtype");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && invstd.scalar_type() == at::kFloat && mean.numel() == C &&
+                  invstd.numel() == C,
+              "mean/invstd fp32 [C]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(ws.device());
+  check_hip(kdl::bn_stage_bwd_finalize(ws.data_ptr<float>(), M, static_cast<int>(C), gamma.data_ptr(),
+                                       mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr(),
+                                       dbeta.data_ptr(), static_cast<int>(pdtype_of(gamma)), training, cur_stream()),
+            "bn_stage_bwd_finalize");
+}
+
+void bn_stage_bwd_apply(const at::Tensor& g, const at::Tensor& x, const at::Tensor& ws, at::Tensor dx,
+                        const c10::optional<at::Tensor>& xd, const c10::optional<at::Tensor>& wsd,
+                        const c10::optional<at::Tensor>& dxd, int64_t M, int64_t C) {
+  need_bf16(g, M * C, "g");
+  need_bf16(x, M * C, "x");
+  need_bf16(dx, M * C, "dx");
+  need_ws(ws, C);
+  if (opt_ptr(xd)) {
+    need_opt_bf16(xd, M * C, "xd");
+    need_opt_bf16(dxd, M * C, "dxd");
+    need_ws(*wsd, C);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::bn_stage_bwd_apply(g.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), dx.data_ptr(), opt_ptr(xd),
+                                    opt_ptr(xd) ? wsd->data_ptr<float>() : nullptr,
+                                    opt_ptr(xd) ? dxd->data_ptr() : nullptr, M, static_cast<int>(C), cur_stream()),
+            "bn_stage_bwd_apply");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -474,5 +751,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
+  m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
+  m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA, fp32 atomics, bf16 cast)");
+  m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad");
+  m.def("bn_coef_offset", &bn_coef_offset, "float offset of the coefficient block in a BN workspace");
+  m.def("bn_stage_fwd_stats", &bn_stage_fwd_stats, "BN forward statistics into the workspace replicas");
+  m.def("bn_stage_fwd_finalize", &bn_stage_fwd_finalize, "BN forward finalize (mean/invstd/coefs/running stats)");
+  m.def("bn_stage_fwd_apply", &bn_stage_fwd_apply, "BN forward apply (+residual | +second BN branch)(+ReLU)(+mask)");
+  m.def("bn_stage_bwd_mask_reduce", &bn_stage_bwd_mask_reduce, "masked gradient + BN backward sums");
+  m.def("bn_stage_bwd_reduce", &bn_stage_bwd_reduce, "BN backward sums (optional ReLU mask recomputed from x)");
+  m.def("bn_stage_bwd_apply_maskx", &bn_stage_bwd_apply_maskx, "BN backward apply with the ReLU mask from x");
+  m.def("bn_stage_bwd_finalize", &bn_stage_bwd_finalize, "BN backward finalize (dgamma, dbeta, dx coefs)");
+  m.def("bn_stage_bwd_apply", &bn_stage_bwd_apply, "BN backward apply (one or two BN branches)");
   m.attr("arch") = "gfx950";
 }

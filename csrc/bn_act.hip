@@ -172,9 +172,12 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
     const T* __restrict__ x, float* __restrict__ acc, int C, float Mf, const PT* __restrict__ gamma,
     const PT* __restrict__ beta, float* __restrict__ rm, float* __restrict__ rv, float momentum,
     float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
-    float* __restrict__ coef) {
+    float* __restrict__ coef, const float* __restrict__ ext_shift = nullptr) {
   const int ch = blockIdx.x * kBlock + threadIdx.x;
   if (ch >= C) return;
+  // sums were taken around K = ext_shift[c] (GEMM-epilogue stats; may alias rm,
+  // which is read here before this thread updates it) or x[0, c] (stats kernel)
+  const float K = ext_shift ? ext_shift[ch] : Vec1<T>::ld(x + ch);
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll 8
   for (int r = 0; r < kReplicas; ++r) {
@@ -184,7 +187,6 @@ __global__ __launch_bounds__(kBlock) void bn_fwd_finalize_kernel(
     row[ch] = 0.f;
     row[C + ch] = 0.f;
   }
-  const float K = Vec1<T>::ld(x + ch);
   const float inv_m = 1.f / Mf;
   const float m1 = s1 * inv_m;
   float var = s2 * inv_m - m1 * m1;
@@ -607,6 +609,146 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(
   }
 }
 
+// ---------------------------------------------------------------- staged entry points (engine)
+// The explicit ResNet engine (kubedl_amd/models/resnet_engine.py) splits BN into
+// stages so the 1x1-conv GEMMs (conv1x1.hip) can own the reductions: the
+// kernels below are the pieces the GEMM epilogues do not cover.
+
+// out = relu(x*sc + sf + xd*scd + sfd) (+ packed mask): bottleneck output with
+// the downsample branch's BN applied on the fly (its output never hits HBM).
+__global__ __launch_bounds__(kBlock) void bn_fwd_apply_dual_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ coef, const bf16_t* __restrict__ xd,
+    const float* __restrict__ coefd, bf16_t* __restrict__ y, uint8_t* __restrict__ mbits, int64_t M, int C,
+    int TPR, int RPI) {
+  constexpr int VEC = 8;
+  const int t = threadIdx.x;
+  const int lc = t % TPR, r0 = t / TPR;
+  const int cg = blockIdx.y * TPR + lc;
+  if (r0 >= RPI || cg >= C / VEC) return;
+  const int c0 = cg * VEC;
+  float sc[VEC], sf[VEC], sd[VEC], fd[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    sc[i] = coef[c0 + i]; sf[i] = coef[C + c0 + i];
+    sd[i] = coefd[c0 + i]; fd[i] = coefd[C + c0 + i];
+  }
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
+    float v[VEC], w[VEC];
+    VecIO<bf16_t, VEC>::load(x + r * C + c0, v);
+    VecIO<bf16_t, VEC>::load(xd + r * C + c0, w);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const float o = fmaf(v[i], sc[i], sf[i]) + fmaf(w[i], sd[i], fd[i]);
+      bits |= (o > 0.f ? 1u : 0u) << i;
+      v[i] = o > 0.f ? o : 0.f;
+    }
+    VecIO<bf16_t, VEC>::store(y + r * C + c0, v);
+    if (mbits) mbits[r * (C / VEC) + cg] = static_cast<uint8_t>(bits);
+  }
+}
+
+// dx = k g + c1 x + c0 and dxd = kd g + c1d xd + c0d: backward of the dual apply
+// (g already masked), reading g once for both BN branches.
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply_dual_kernel(
+    const bf16_t* __restrict__ g, const bf16_t* __restrict__ x, const float* __restrict__ coef,
+    bf16_t* __restrict__ dx, const bf16_t* __restrict__ xd, const float* __restrict__ coefd,
+    bf16_t* __restrict__ dxd, int64_t M, int C, int TPR, int RPI) {
+  constexpr int VEC = 8;
+  const int t = threadIdx.x;
+  const int lc = t % TPR, r0 = t / TPR;
+  const int cg = blockIdx.y * TPR + lc;
+  if (r0 >= RPI || cg >= C / VEC) return;
+  const int c0 = cg * VEC;
+  float k[VEC], c1[VEC], cz[VEC], kd[VEC], c1d[VEC], czd[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    k[i] = coef[c0 + i]; c1[i] = coef[C + c0 + i]; cz[i] = coef[2 * C + c0 + i];
+    kd[i] = coefd[c0 + i]; c1d[i] = coefd[C + c0 + i]; czd[i] = coefd[2 * C + c0 + i];
+  }
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
+    float gv[VEC], xv[VEC], wv[VEC];
+    VecIO<bf16_t, VEC>::load(g + r * C + c0, gv);
+    VecIO<bf16_t, VEC>::load(x + r * C + c0, xv);
+    VecIO<bf16_t, VEC>::load(xd + r * C + c0, wv);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      xv[i] = fmaf(k[i], gv[i], fmaf(c1[i], xv[i], cz[i]));
+      wv[i] = fmaf(kd[i], gv[i], fmaf(c1d[i], wv[i], czd[i]));
+    }
+    VecIO<bf16_t, VEC>::store(dx + r * C + c0, xv);
+    VecIO<bf16_t, VEC>::store(dxd + r * C + c0, wv);
+  }
+}
+
+// g = dy * mask-bit, written out, plus sum(g), sum(g (x - mean)) into the
+// backward replicas (standalone form of the conv1x1 RESBITS epilogue, for the
+// last bottleneck whose gradient comes from the pooling head).  dy may be a
+// per-image broadcast: dy_rows_per_img > 0 means dy is [M / rows, C] scaled by
+// dy_scale (global average pool backward folded in).
+__global__ __launch_bounds__(kBlock) void bn_bwd_mask_reduce_kernel(
+    const bf16_t* __restrict__ dy, int dy_rows_per_img, float dy_scale, const uint8_t* __restrict__ mbits,
+    const bf16_t* __restrict__ x, const float* __restrict__ mean, bf16_t* __restrict__ gout, int64_t M, int C,
+    int TPR, int RPI, float* __restrict__ acc, const bf16_t* __restrict__ x2, const float* __restrict__ mean2,
+    float* __restrict__ acc2) {
+  constexpr int VEC = 8;
+  __shared__ float sh[2 * kBlock * VEC];
+  const int t = threadIdx.x;
+  const int lc = t % TPR, r0 = t / TPR;
+  const int CG = C / VEC;
+  const int cg = blockIdx.y * TPR + lc;
+  const bool active = (r0 < RPI) && (cg < CG);
+  const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
+  const int c0 = cg * VEC;
+  float mu[VEC], sa[VEC], sb[VEC], mu2[VEC], sb2[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { sa[i] = 0.f; sb[i] = 0.f; mu[i] = 0.f; mu2[i] = 0.f; sb2[i] = 0.f; }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      mu[i] = mean[c0 + i];
+      if (x2) mu2[i] = mean2[c0 + i];
+    }
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
+      float g[VEC], xv[VEC];
+      if (dy_rows_per_img > 0) {
+        VecIO<bf16_t, VEC>::load(dy + (r / dy_rows_per_img) * C + c0, g);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) g[i] = bf16_to_f32(f32_to_bf16(g[i] * dy_scale));
+      } else {
+        VecIO<bf16_t, VEC>::load(dy + r * C + c0, g);
+      }
+      VecIO<bf16_t, VEC>::load(x + r * C + c0, xv);
+      const uint32_t m = mbits[r * CG + cg];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        g[i] = (m >> i) & 1u ? g[i] : 0.f;
+        sa[i] += g[i];
+        sb[i] = fmaf(g[i], xv[i] - mu[i], sb[i]);
+      }
+      VecIO<bf16_t, VEC>::store(gout + r * C + c0, g);
+      if (x2) {  // second BN fed by the same gradient (downsample branch)
+        float xw[VEC];
+        VecIO<bf16_t, VEC>::load(x2 + r * C + c0, xw);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) sb2[i] = fmaf(g[i], xw[i] - mu2[i], sb2[i]);
+      }
+    }
+  }
+  float* rep = acc + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
+  if (x2) {
+    float* rep2 = acc2 + static_cast<int64_t>(blockIdx.x % kReplicas) * 2 * C;
+    float sa2[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) sa2[i] = sa[i];
+    block_fold_atomic<VEC>(sa2, sb2, sh, t, lc, r0, TPR, RPI, active, rep2 + c0, rep2 + C + c0);
+    __syncthreads();
+  }
+  block_fold_atomic<VEC>(sa, sb, sh, t, lc, r0, TPR, RPI, active, rep + c0, rep + C + c0);
+}
+
 // ---------------------------------------------------------------- host side
 struct ReducePlan {
   Tiling tl;
@@ -718,9 +860,11 @@ hipError_t bwd_impl(const T* dy, const T* y, const uint8_t* mbits, const T* x, c
                                dbeta, ws, M, C, training, s)
   if (!relu) KDL_BWD(kMaskNone);
   else if (mbits != nullptr && VEC == 8) KDL_BWD(kMaskBits);
-  // with a residual the mask must come from y (it saw the residual)
-  else if (dres || y == nullptr || beta == nullptr) KDL_BWD(kMaskY);
-  else KDL_BWD(kMaskX);
+  // with a residual the mask must come from y (it saw the residual); without
+  // one it is recomputed from x (y is not read)
+  else if (dres == nullptr && beta != nullptr) KDL_BWD(kMaskX);
+  else if (y != nullptr) KDL_BWD(kMaskY);
+  else return hipErrorInvalidValue;
 #undef KDL_BWD
   return hipGetLastError();
 }
@@ -847,6 +991,143 @@ hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, 
                        mean, invstd, coef, static_cast<bf16_t*>(dx), M, C, H, W, PH, PW, rp.tl.TPR,
                        rp.tl.RPI);
   });
+  return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------- staged host entry points (bf16 NHWC, C % 8 == 0)
+hipError_t bn_stage_fwd_stats(const void* x, float* ws, int64_t M, int C, hipStream_t s) {
+  if (M <= 0 || C % 8) return hipErrorInvalidValue;
+  ReducePlan rp = plan_reduce(M, C, 8);
+  hipLaunchKernelGGL((bn_fwd_stats_kernel<bf16_t, 8>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
+                     static_cast<const bf16_t*>(x), M, C, rp.tl.TPR, rp.tl.RPI, ws_acc_fwd(ws, C));
+  return hipGetLastError();
+}
+
+hipError_t bn_stage_fwd_finalize(const void* x, const float* shift, float* ws, int64_t M, int C, const void* gamma,
+                                 const void* beta, float* rm, float* rv, float* save_mean, float* save_invstd,
+                                 int pdtype, bool training, float momentum, float eps, hipStream_t s) {
+  const int fin_grid = (C + kBlock - 1) / kBlock;
+  float* coef = ws_coef(ws, C);
+  KDL_DISPATCH_PT(pdtype, {
+    if (training)
+      hipLaunchKernelGGL((bn_fwd_finalize_kernel<bf16_t, PT>), dim3(fin_grid), dim3(kBlock), 0, s,
+                         static_cast<const bf16_t*>(x), ws_acc_fwd(ws, C), C, static_cast<float>(M),
+                         static_cast<const PT*>(gamma), static_cast<const PT*>(beta), rm, rv, momentum, eps,
+                         save_mean, save_invstd, coef, shift);
+    else
+      hipLaunchKernelGGL((bn_eval_prep_kernel<PT>), dim3(fin_grid), dim3(kBlock), 0, s, C,
+                         static_cast<const PT*>(gamma), static_cast<const PT*>(beta), rm, rv, eps, save_mean,
+                         save_invstd, coef);
+  });
+  return hipGetLastError();
+}
+
+const float* bn_stage_coef(const float* ws, int C) { return ws + static_cast<int64_t>(kReplicas) * 4 * C; }
+
+hipError_t bn_stage_fwd_apply(const void* x, const float* ws, const void* res, const void* xd, const float* wsd,
+                              void* y, uint8_t* mbits, int64_t M, int C, bool relu, hipStream_t s) {
+  if (M <= 0 || C % 8) return hipErrorInvalidValue;
+  const Tiling tl = make_tiling(C, 8);
+  dim3 grid(apply_gx(M, tl), tl.gy);
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  bf16_t* yb = static_cast<bf16_t*>(y);
+  const float* coef = ws_coef(const_cast<float*>(ws), C);
+  if (xd) {
+    if (!relu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_fwd_apply_dual_kernel, grid, dim3(kBlock), 0, s, xb, coef,
+                       static_cast<const bf16_t*>(xd), ws_coef(const_cast<float*>(wsd), C), yb, mbits, M, C,
+                       tl.TPR, tl.RPI);
+    return hipGetLastError();
+  }
+  const bf16_t* rb = static_cast<const bf16_t*>(res);
+#define KDL_APPLY(R, S, MO)                                                                              \
+  hipLaunchKernelGGL((bn_fwd_apply_kernel<bf16_t, 8, R, S, MO>), grid, dim3(kBlock), 0, s, xb, rb, yb, mbits, \
+                     coef, M, C, tl.TPR, tl.RPI)
+  if (relu && rb && mbits) KDL_APPLY(true, true, true);
+  else if (relu && rb) KDL_APPLY(true, true, false);
+  else if (relu) KDL_APPLY(true, false, false);
+  else if (rb) KDL_APPLY(false, true, false);
+  else KDL_APPLY(false, false, false);
+#undef KDL_APPLY
+  return hipGetLastError();
+}
+
+hipError_t bn_stage_bwd_mask_reduce(const void* dy, int dy_rows_per_img, float dy_scale, const uint8_t* mbits,
+                                    const void* x, const float* mean, void* gout, float* ws, int64_t M, int C,
+                                    const void* x2, const float* mean2, float* ws2, hipStream_t s) {
+  if (M <= 0 || C % 8) return hipErrorInvalidValue;
+  ReducePlan rp = plan_reduce(M, C, 8);
+  hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel, dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
+                     static_cast<const bf16_t*>(dy), dy_rows_per_img, dy_scale, mbits,
+                     static_cast<const bf16_t*>(x), mean, static_cast<bf16_t*>(gout), M, C, rp.tl.TPR, rp.tl.RPI,
+                     ws_acc_bwd(ws, C), static_cast<const bf16_t*>(x2), mean2, x2 ? ws_acc_bwd(ws2, C) : nullptr);
+  return hipGetLastError();
+}
+
+hipError_t bn_stage_bwd_reduce(const void* dy, const void* x, const void* gamma, const void* beta, const float* mean,
+                               const float* invstd, float* ws, int64_t M, int C, bool relu_mask_x, int pdtype,
+                               hipStream_t s) {
+  if (M <= 0 || C % 8) return hipErrorInvalidValue;
+  ReducePlan rp = plan_reduce(M, C, 8);
+  KDL_DISPATCH_PT(pdtype, {
+    const PT* g = static_cast<const PT*>(gamma);
+    const PT* b = static_cast<const PT*>(beta);
+    if (relu_mask_x)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16_t, PT, 8, kMaskX>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
+                         static_cast<const bf16_t*>(dy), nullptr, nullptr, static_cast<const bf16_t*>(x), g, b, mean,
+                         invstd, M, C, rp.tl.TPR, rp.tl.RPI, ws_acc_bwd(ws, C));
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16_t, PT, 8, kMaskNone>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
+                         static_cast<const bf16_t*>(dy), nullptr, nullptr, static_cast<const bf16_t*>(x), g, b, mean,
+                         invstd, M, C, rp.tl.TPR, rp.tl.RPI, ws_acc_bwd(ws, C));
+  });
+  return hipGetLastError();
+}
+
+hipError_t bn_stage_bwd_apply_maskx(const void* dy, const void* x, const void* gamma, const void* beta,
+                                    const float* mean, const float* invstd, const float* ws, void* dx, int64_t M,
+                                    int C, int pdtype, hipStream_t s) {
+  if (M <= 0 || C % 8) return hipErrorInvalidValue;
+  const Tiling tl = make_tiling(C, 8);
+  dim3 grid(apply_gx(M, tl), tl.gy);
+  const float* coef = ws_coef(const_cast<float*>(ws), C);
+  KDL_DISPATCH_PT(pdtype, {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, PT, 8, kMaskX, false>), grid, dim3(kBlock), 0, s,
+                       static_cast<const bf16_t*>(dy), nullptr, nullptr, static_cast<const bf16_t*>(x),
+                       static_cast<const PT*>(gamma), static_cast<const PT*>(beta), mean, invstd, coef,
+                       static_cast<bf16_t*>(dx), nullptr, M, C, tl.TPR, tl.RPI);
+  });
+  return hipGetLastError();
+}
+
+hipError_t bn_stage_bwd_finalize(float* ws, int64_t M, int C, const void* gamma, const float* mean,
+                                 const float* invstd, void* dgamma, void* dbeta, int pdtype, bool training,
+                                 hipStream_t s) {
+  KDL_DISPATCH_PT(pdtype, {
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                       ws_acc_bwd(ws, C), C, static_cast<float>(M), static_cast<const PT*>(gamma), mean, invstd,
+                       training, static_cast<PT*>(dgamma), static_cast<PT*>(dbeta), ws_coef(ws, C));
+  });
+  return hipGetLastError();
+}
+
+hipError_t bn_stage_bwd_apply(const void* g, const void* x, const float* ws, void* dx, const void* xd,
+                              const float* wsd, void* dxd, int64_t M, int C, hipStream_t s) {
+  if (M <= 0 || C % 8) return hipErrorInvalidValue;
+  const Tiling tl = make_tiling(C, 8);
+  dim3 grid(apply_gx(M, tl), tl.gy);
+  const float* coef = ws_coef(const_cast<float*>(ws), C);
+  if (xd) {
+    hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, grid, dim3(kBlock), 0, s, static_cast<const bf16_t*>(g),
+                       static_cast<const bf16_t*>(x), coef, static_cast<bf16_t*>(dx),
+                       static_cast<const bf16_t*>(xd), ws_coef(const_cast<float*>(wsd), C),
+                       static_cast<bf16_t*>(dxd), M, C, tl.TPR, tl.RPI);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, bf16_t, 8, kMaskNone, false>), grid, dim3(kBlock), 0, s,
+                       static_cast<const bf16_t*>(g), nullptr, nullptr, static_cast<const bf16_t*>(x), nullptr,
+                       nullptr, nullptr, nullptr, coef, static_cast<bf16_t*>(dx), nullptr, M, C, tl.TPR, tl.RPI);
+  }
   return hipGetLastError();
 }
 

@@ -1,0 +1,754 @@
+// 1x1 convolutions of the NHWC ResNet bottleneck as MFMA GEMMs with the
+// neighbouring BatchNorm work fused into their prologue / epilogue (gfx950).
+//
+// At batch 256 every 1x1 conv of ResNet-50 is HBM-bound on MI355X (K, N <=
+// 2048, M = N*H*W up to 802,816 rows: ~64-400 FLOP per byte moved), so the
+// lever is not MFMA rate but bytes: each fusion below deletes a whole pass
+// over an activation tensor that the unfused step (conv -> BN stats -> BN
+// apply -> conv ...) pays for separately.
+//
+//   gemm1x1 (forward and data-gradient):   C[M, N] = pro(A)[M, K] . B[N, K]^T
+//     forward:  A = activations (row-gathered for stride-2 1x1 convs),
+//               B = conv weight [Cout, Cin];
+//     dgrad:    A = output gradient, B = W^T [Cin, Cout] (transposed copy).
+//     prologue  PRO:      A <- relu(A * scale[k] + shift[k])  -- the BN+ReLU
+//                         of the previous layer applied while staging A, so
+//                         its output is never written to HBM;
+//     epilogue  STATS:    per-output-channel shifted sums sum(y - s),
+//                         sum((y - s)^2) of the bf16 output -> the BN
+//                         forward-stats replicas (no separate stats pass);
+//               MASKX:    dgrad of the layer after a BN+ReLU: g' = g *
+//                         [x*scale + shift > 0] (mask recomputed from the
+//                         BN input x), plus the BN backward sums sum(g'),
+//                         sum(g' (x - mean)) (no separate reduce pass);
+//               RESBITS:  dgrad of a bottleneck's first conv: g = dgrad +
+//                         d(identity) (optionally stride-gathered from the
+//                         downsample branch), masked by the previous block's
+//                         packed 1-bit ReLU mask, plus the previous block's
+//                         bn3 (and downsample BN) backward sums: this
+//                         replaces autograd's residual-gradient add kernel
+//                         AND the bn3 reduce pass;
+//               RES:      g = dgrad + d(identity), no mask (network stem).
+//   wgrad1x1:   dW[N, K] = sum_m G[m, N]^T pro(A)[m, K]   (split over M, fp32
+//               atomics from the accumulators; a cast kernel writes the bf16
+//               gradient and re-zeroes the fp32 accumulator).
+//
+// Tiling (gemm1x1): 256 threads = 4 waves, tile 128 (M) x BN (N in {64,
+// 128}) x 64 (K).  The MFMA is v_mfma_f32_32x32x16_bf16 issued as D = W . X^T
+// (weight fragment as the A operand), so a lane's accumulator registers hold
+// 4 consecutive OUTPUT CHANNELS of one output row: the epilogue packs them to
+// 8-byte LDS writes, and the tile is read back row-wise as 16-byte vectors
+// (one thread = 8 channels of one row), which is the layout both the global
+// store and the per-channel reductions want.  LDS rows are padded to 72 bf16
+// (144 B): the 32 rows a fragment read touches land on distinct 16-B slots.
+// Register-staged double buffering; the next tile's first K-step is fetched
+// while the current tile's last K-step computes.  Blocks are persistent over
+// M tiles (reduction atomics once per block, not per tile) and the block ->
+// (tile_n, M-sequence) map is XCD-aware: the tile_n siblings that re-read one
+// A panel are consecutive on the same XCD (shared L2).
+//
+// The reference has no kernels; these serve the PyTorchJob
+// ResNet-50 worker (BASELINE.json config 2).
+#include "common.h"
+#include "kdl_api.h"
+
+namespace kdl {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int kThreads = 256;
+constexpr int BM = 128, BK = 64;
+constexpr int LDK = BK + 8;  // padded LDS row (bf16)
+constexpr int kRep = 32;     // replica count of the BN workspace (== bn_act.hip kReplicas)
+
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
+
+struct GemmParams {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  int M, N, K;
+  // A row gather (stride-s 1x1 conv): out row (n, oh, ow) reads in row (n, oh*s, ow*s)
+  int Hout, Wout, Hin, Win, stride;
+  const float* pro_coef;  // [2K]: scale | shift
+  // epilogue operands
+  const float* shift;   // STATS: [N]
+  float* acc;           // STATS/MASKX/RESBITS: [kRep][2N]
+  const bf16_t* ex;     // MASKX/RESBITS: BN input x [M, N]
+  const float* emean;   // [N]
+  const float* ecoef;   // MASKX: [2N] forward scale | shift of that BN
+  const bf16_t* eres;   // RESBITS/RES: d(identity)
+  int res_stride;       // 1: eres is [M, N]; s > 1: eres is [Nb, Hin/s.., N] sampled at (h%s==0, w%s==0)
+  int res_H, res_W;     // geometry of the C rows (= input resolution) for the strided residual
+  const uint8_t* ebits; // RESBITS: [M, N/8]
+  const bf16_t* ex2;    // RESBITS: optional second BN input (downsample BN)
+  const float* emean2;
+  float* acc2;          // its replicas [kRep][2N]
+};
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ __forceinline__ void unpack8(const uint4 v, float (&o)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&o)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = static_cast<uint32_t>(f32_to_bf16(o[2 * i])) | (static_cast<uint32_t>(f32_to_bf16(o[2 * i + 1])) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void atomic_add_f32(float* p, float v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int BN, bool PRO, bool GATHER, int EPI>
+__global__ __launch_bounds__(kThreads, 2) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
+  // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
+  // [BM][BN + 8] output tile and finally as the reduction scratch.
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * LDK];
+  constexpr int kBuf = (BM + BN) * LDK;
+  constexpr int WN = BN >= 128 ? 2 : 1;  // waves along N
+  constexpr int WM = 4 / WN;             // waves along M
+  constexpr int WTM = BM / WM;           // wave tile (M)
+  constexpr int WTN = BN / WN;           // wave tile (N) = 64
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_CH = BM * 8 / kThreads;  // 16-B chunks per thread per K-step
+  constexpr int B_CH = BN * 8 / kThreads;
+  constexpr int LDC = BN + 8;
+  constexpr int CPR = BN / 8;              // 16-B chunks per output row
+  constexpr int RPP = kThreads / CPR;      // rows per epilogue pass
+  constexpr bool REDUCE = EPI == EPI_STATS || EPI == EPI_MASKX || EPI == EPI_RESBITS;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nblk = gridDim.x;
+  const int b = blockIdx.x;
+  const int q = (b & 7) * (nblk >> 3) + (b >> 3);  // nblk % 8 == 0 (host)
+  const int tile_n = q % tiles_n;
+  const int gm = q / tiles_n;
+  const int n0 = tile_n * BN;
+  const int K = p.K, M = p.M, N = p.N;
+  const int nk = K / BK;
+  const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
+
+  // staging coordinates (fixed per thread)
+  int a_row[A_CH], a_kc[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int c = t + i * kThreads;
+    a_row[i] = c >> 3;
+    a_kc[i] = (c & 7) * 8;
+  }
+  int64_t a_off[A_CH];
+  bool a_ok[A_CH];
+  uint4 ra[A_CH], rb[B_CH];
+  // all A chunks of a thread share one 8-channel k-chunk ((t + i*256) & 7 == t & 7)
+  float psc[8], psf[8];
+  (void)psc; (void)psf;
+
+  auto setup_rows = [&](int tm) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = tm * BM + a_row[i];
+      a_ok[i] = m < M;
+      int64_t src = m;
+      if constexpr (GATHER) {
+        const int hw = p.Hout * p.Wout;
+        const int nimg = m / hw, rem = m - nimg * hw;
+        const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
+        src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
+      }
+      a_off[i] = a_ok[i] ? src * K : 0;
+    }
+  };
+  auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i)
+      ra[i] = a_ok[i] ? ld16(p.A + a_off[i] + k0 + a_kc[i]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int c = t + i * kThreads;
+      rb[i] = ld16(p.B + static_cast<int64_t>(n0 + (c >> 3)) * K + k0 + (c & 7) * 8);
+    }
+    if constexpr (PRO) {
+      const float4* sp = reinterpret_cast<const float4*>(p.pro_coef + k0 + a_kc[0]);
+      const float4* fp = reinterpret_cast<const float4*>(p.pro_coef + K + k0 + a_kc[0]);
+      const float4 s0 = sp[0], s1 = sp[1], f0 = fp[0], f1 = fp[1];
+      psc[0] = s0.x; psc[1] = s0.y; psc[2] = s0.z; psc[3] = s0.w;
+      psc[4] = s1.x; psc[5] = s1.y; psc[6] = s1.z; psc[7] = s1.w;
+      psf[0] = f0.x; psf[1] = f0.y; psf[2] = f0.z; psf[3] = f0.w;
+      psf[4] = f1.x; psf[5] = f1.y; psf[6] = f1.z; psf[7] = f1.w;
+    }
+  };
+  auto swrite = [&](int buf) {
+    bf16_t* As = lds + buf * kBuf;
+    bf16_t* Bs = As + BM * LDK;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      uint4 v = ra[i];
+      if constexpr (PRO) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = fmaf(f[j], psc[j], psf[j]);
+          f[j] = o > 0.f ? o : 0.f;
+        }
+        v = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(&As[a_row[i] * LDK + a_kc[i]]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int c = t + i * kThreads;
+      *reinterpret_cast<uint4*>(&Bs[(c >> 3) * LDK + (c & 7) * 8]) = rb[i];
+    }
+  };
+
+  // per-thread reduction state: 8 channels of column chunk (t % CPR)
+  const int ec = t % CPR, er0 = t / CPR;
+  const int ch0 = n0 + ec * 8;
+  float s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; s3[j] = 0.f; }
+
+  int tm = gm;
+  if (tm < tiles_m) {
+    setup_rows(tm);
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  const int fr = lane & 31, fh = lane >> 5;
+  for (; tm < tiles_m; tm += GM) {
+    f32x16_t acc[TN][TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more_k = kt + 1 < nk;
+      const bool more = more_k || tm + GM < tiles_m;
+      if (more_k) {
+        gload(kt + 1);
+      } else if (more) {
+        setup_rows(tm + GM);
+        gload(0);
+      }
+      const bf16_t* As = lds + cur * kBuf;
+      const bf16_t* Bs = As + BM * LDK;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8_t wf[TN], xf[TM];
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          wf[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&Bs[(wn0 + i * 32 + fr) * LDK + s * 16 + fh * 8]));
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          xf[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&As[(wm0 + j * 32 + fr) * LDK + s * 16 + fh * 8]));
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) swrite(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+    // ---- epilogue.  The row-side operands (BN input x, d(identity), mask bits)
+    // of the first prefetch group are issued before the accumulators go to LDS
+    // so their HBM latency overlaps the LDS round trip; later groups are issued
+    // a group ahead of their use.
+    constexpr int NP = BM / RPP;                       // rows per thread per tile
+    constexpr int PG = EPI == EPI_RESBITS ? 4 : NP;    // prefetch group (register budget)
+    constexpr bool LX = EPI == EPI_MASKX || EPI == EPI_RESBITS;
+    constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES;
+    uint4 pxv[PG], prv[PG], px2[PG];
+    uint32_t pbv[PG];
+    bool prok[PG];
+    auto prefetch = [&](int g0) {
+#pragma unroll
+      for (int i = 0; i < PG; ++i) {
+        const int m = tm * BM + (g0 + i) * RPP + er0;
+        const bool ok = m < M;
+        const int64_t go = static_cast<int64_t>(ok ? m : 0) * N + ch0;
+        if constexpr (LX) pxv[i] = ok ? ld16(p.ex + go) : make_uint4(0, 0, 0, 0);
+        if constexpr (EPI == EPI_RESBITS) {
+          pbv[i] = ok ? p.ebits[static_cast<int64_t>(m) * (N / 8) + (ch0 >> 3)] : 0u;
+          px2[i] = (ok && p.ex2) ? ld16(p.ex2 + go) : make_uint4(0, 0, 0, 0);
+        }
+        if constexpr (LR) {
+          const bf16_t* rp = nullptr;
+          if (ok) {
+            if (p.res_stride == 1) {
+              rp = p.eres + go;
+            } else {
+              const int hw = p.res_H * p.res_W;
+              const int nimg = m / hw, rem = m - nimg * hw;
+              const int h = rem / p.res_W, w = rem - h * p.res_W;
+              if (h % p.res_stride == 0 && w % p.res_stride == 0) {
+                const int Ho = (p.res_H + p.res_stride - 1) / p.res_stride;
+                const int Wo = (p.res_W + p.res_stride - 1) / p.res_stride;
+                rp = p.eres + ((static_cast<int64_t>(nimg) * Ho + h / p.res_stride) * Wo + w / p.res_stride) * N + ch0;
+              }
+            }
+          }
+          prok[i] = rp != nullptr;
+          prv[i] = rp ? ld16(rp) : make_uint4(0, 0, 0, 0);
+        }
+      }
+    };
+    (void)pxv; (void)prv; (void)px2; (void)pbv; (void)prok;
+    if constexpr (LX || LR) prefetch(0);
+    // D[n][m] -> LDS [m][n] (buffer cur^1 is free: its last reader was the final
+    // K-step, which ended with a barrier; buffer cur may already hold the next
+    // tile's first K-step)
+    bf16_t* Cs = lds + (cur ^ 1) * kBuf;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m = wm0 + j * 32 + fr;
+          const int n = wn0 + i * 32 + 8 * g + 4 * fh;
+          const uint32_t lo = static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g])) |
+                              (static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g + 1])) << 16);
+          const uint32_t hi = static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g + 2])) |
+                              (static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g + 3])) << 16);
+          *reinterpret_cast<uint2*>(&Cs[m * LDC + n]) = make_uint2(lo, hi);
+        }
+    __syncthreads();
+    // per-channel epilogue constants, loaded here (acc is dead) to keep them
+    // out of the K loop's register budget
+    float ea[8], eb[8], em[8], em2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ea[j] = 0.f; eb[j] = 0.f; em[j] = 0.f; em2[j] = 0.f; }
+    if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) em[j] = p.shift[ch0 + j];
+    } else if constexpr (EPI == EPI_MASKX) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { em[j] = p.emean[ch0 + j]; ea[j] = p.ecoef[ch0 + j]; eb[j] = p.ecoef[N + ch0 + j]; }
+    } else if constexpr (EPI == EPI_RESBITS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        em[j] = p.emean[ch0 + j];
+        if (p.ex2) em2[j] = p.emean2[ch0 + j];
+      }
+    }
+#pragma unroll
+    for (int g0 = 0; g0 < NP; g0 += PG) {
+      uint4 cxv[PG], crv[PG], cx2[PG];
+      uint32_t cbv[PG];
+      bool crok[PG];
+#pragma unroll
+      for (int i = 0; i < PG; ++i) { cxv[i] = pxv[i]; crv[i] = prv[i]; cx2[i] = px2[i]; cbv[i] = pbv[i]; crok[i] = prok[i]; }
+      (void)cxv; (void)crv; (void)cx2; (void)cbv; (void)crok;
+      if constexpr (LX || LR) {
+        if (g0 + PG < NP) prefetch(g0 + PG);
+      }
+#pragma unroll
+      for (int i = 0; i < PG; ++i) {
+        const int row = (g0 + i) * RPP + er0;
+        const int m = tm * BM + row;
+        if (m >= M) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(&Cs[row * LDC + ec * 8]), v);
+        const int64_t go = static_cast<int64_t>(m) * N + ch0;
+        if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = v[j] - em[j];
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+        } else if constexpr (EPI == EPI_MASKX) {
+          float x[8];
+          unpack8(cxv[i], x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float g = fmaf(x[j], ea[j], eb[j]) > 0.f ? v[j] : 0.f;
+            v[j] = g;
+            s1[j] += g;
+            s2[j] = fmaf(g, x[j] - em[j], s2[j]);
+          }
+        } else if constexpr (LR) {  // RESBITS / RES: add d(identity)
+          if (crok[i]) {
+            float r[8];
+            unpack8(crv[i], r);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(f32_to_bf16(v[j] + r[j]));
+          }
+          if constexpr (EPI == EPI_RESBITS) {
+            const uint32_t bits = cbv[i];
+            float x[8];
+            unpack8(cxv[i], x);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float g = (bits >> j) & 1u ? v[j] : 0.f;
+              v[j] = g;
+              s1[j] += g;
+              s2[j] = fmaf(g, x[j] - em[j], s2[j]);
+            }
+            if (p.ex2) {
+              float x2[8];
+              unpack8(cx2[i], x2);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) s3[j] = fmaf(v[j], x2[j] - em2[j], s3[j]);
+            }
+          }
+        }
+        *reinterpret_cast<uint4*>(p.C + go) = pack8(v);
+      }
+    }
+    __syncthreads();  // Cs (buffer cur^1) is restaged by the next tile's second K-step
+  }
+
+  if constexpr (REDUCE) {
+    // fold the RPP row groups of each channel chunk in LDS, one atomic per
+    // channel per sum into this block's replica
+    float* sh = reinterpret_cast<float*>(lds);
+    constexpr int NS = 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sh[(0 * kThreads + t) * 8 + j] = s1[j];
+      sh[(1 * kThreads + t) * 8 + j] = s2[j];
+      sh[(2 * kThreads + t) * 8 + j] = s3[j];
+    }
+    __syncthreads();
+    if (gm < tiles_m && er0 == 0) {
+#pragma unroll
+      for (int si = 0; si < NS; ++si) {
+        if (si == 2 && !(EPI == EPI_RESBITS && p.ex2)) break;
+        float a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = 0.f;
+        for (int rr = 0; rr < RPP; ++rr) {
+          const int o = (si * kThreads + rr * CPR + ec) * 8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[j] += sh[o + j];
+        }
+        float* dst;
+        if (si == 0) dst = p.acc + static_cast<int64_t>(b % kRep) * 2 * N + ch0;
+        else if (si == 1) dst = p.acc + static_cast<int64_t>(b % kRep) * 2 * N + N + ch0;
+        else dst = p.acc2 + static_cast<int64_t>(b % kRep) * 2 * N + N + ch0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomic_add_f32(dst + j, a[j]);
+        if (si == 0 && EPI == EPI_RESBITS && p.ex2) {
+          // the downsample BN sees the same masked gradient: same sum(g')
+          float* d2 = p.acc2 + static_cast<int64_t>(b % kRep) * 2 * N + ch0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomic_add_f32(d2 + j, a[j]);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ wgrad
+// dW[N, K] = sum_m G[m, n] * pro(A)[m, k], A row-gathered for strided convs.
+// Tile TN_ (N) x TK_ (K) (each 64 or 128) x 64 (M-step); each block reduces
+// one contiguous M-range and adds its tile into the fp32 dW32 with atomics.  Both operands
+// arrive with the reduction index (m) strided, so staging transposes them: a
+// thread loads an 8 (m) x 8 (channel) bf16 block as eight 16-B row chunks,
+// transposes it in registers (v_perm_b32 half-word selects) and writes eight
+// 16-B channel rows of m-contiguous data -- the K-contiguous fragment layout
+// the MFMA operands want.
+constexpr int WMK = 64;   // M per step
+constexpr int LDW = WMK + 8;
+
+__device__ __forceinline__ void transpose8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
+  // in[r] = 8 bf16 of row r (elements c = 0..7); out[c] = 8 bf16 (rows 0..7) of column c
+  uint32_t w[8][4];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) { w[r][0] = in[r].x; w[r][1] = in[r].y; w[r][2] = in[r].z; w[r][3] = in[r].w; }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    uint32_t o[4];
+#pragma unroll
+    for (int rp = 0; rp < 4; ++rp) {
+      const uint32_t x0 = w[2 * rp][c >> 1], x1 = w[2 * rp + 1][c >> 1];
+      // low half of the output dword = element c of row 2rp, high half = element c of row 2rp+1
+      o[rp] = (c & 1) ? __builtin_amdgcn_perm(x1, x0, 0x07060302u) : __builtin_amdgcn_perm(x1, x0, 0x05040100u);
+    }
+    out[c] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+template <int TN_, int TK_, bool PRO, bool GATHER>
+__global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
+    const bf16_t* __restrict__ G, const bf16_t* __restrict__ A, const float* __restrict__ pro_coef,
+    float* __restrict__ dw32, int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride,
+    int rows_per_split, int tiles_k) {
+  // [2 buffers][G^T tile TN_ x LDW | A^T tile TK_ x LDW]
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (TN_ + TK_) * LDW];
+  constexpr int kBuf = (TN_ + TK_) * LDW;
+  constexpr int WTN = TN_ / 2, WTK = TK_ / 2;  // 2 x 2 waves
+  constexpr int FN = WTN / 32, FK = WTK / 32;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int tn = blockIdx.y / tiles_k, tk = blockIdx.y % tiles_k;
+  const int split = blockIdx.x;
+  const int n0 = tn * TN_, k0 = tk * TK_;
+  const int mbeg = split * rows_per_split;
+  const int mend = min(M, mbeg + rows_per_split);
+  // staging units: an 8 (m) x 8 (channel) block each; TN_ units of G, then TK_ of A
+  const bool isA = t >= TN_;
+  const bool stager = t < TN_ + TK_;
+  const int u = isA ? t - TN_ : t;
+  const int cpr = (isA ? TK_ : TN_) / 8;
+  const int mg = u / cpr;         // 0..7: rows mg*8 .. +7 of the M-step
+  const int cc = (u % cpr) * 8;   // channel chunk within the tile
+  const int col0 = (isA ? k0 : n0) + cc;
+  const int ld = isA ? K : N;
+  const bf16_t* base = isA ? A : G;
+  float psc[8], psf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { psc[j] = 1.f; psf[j] = 0.f; }
+  if (PRO && isA && stager) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { psc[j] = pro_coef[col0 + j]; psf[j] = pro_coef[K + col0 + j]; }
+  }
+  uint4 rr[8];
+  auto gload = [&](int m0) {
+    if (!stager) return;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int m = m0 + mg * 8 + r;
+      if (m < mend) {
+        int64_t src = m;
+        if (GATHER && isA) {
+          const int hw = Hout * Wout;
+          const int nimg = m / hw, rem = m - nimg * hw;
+          const int oh = rem / Wout, ow = rem - oh * Wout;
+          src = (static_cast<int64_t>(nimg) * Hin + oh * stride) * Win + ow * stride;
+        }
+        rr[r] = ld16(base + src * ld + col0);
+      } else {
+        rr[r] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto swrite = [&](int buf, int m0) {
+    if (!stager) return;
+    if (PRO && isA) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        if (m0 + mg * 8 + r >= mend) continue;  // padding rows stay zero
+        float f[8];
+        unpack8(rr[r], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = fmaf(f[j], psc[j], psf[j]);
+          f[j] = o > 0.f ? o : 0.f;
+        }
+        rr[r] = pack8(f);
+      }
+    }
+    uint4 tr[8];
+    transpose8x8(rr, tr);
+    bf16_t* S = lds + buf * kBuf + (isA ? TN_ * LDW : 0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) *reinterpret_cast<uint4*>(&S[(cc + c) * LDW + mg * 8]) = tr[c];
+  };
+  const int wn0 = (wave >> 1) * WTN, wk0 = (wave & 1) * WTK;
+  const int fr = lane & 31, fh = lane >> 5;
+  f32x16_t acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  int cur = 0;
+  if (mbeg < mend) {
+    gload(mbeg);
+    swrite(0, mbeg);
+  }
+  __syncthreads();
+  for (int m0 = mbeg; m0 < mend; m0 += WMK) {
+    const bool more = m0 + WMK < mend;
+    if (more) gload(m0 + WMK);
+    const bf16_t* Gs = lds + cur * kBuf;
+    const bf16_t* As = Gs + TN_ * LDW;
+#pragma unroll
+    for (int s = 0; s < WMK / 16; ++s) {
+      bf16x8_t gf[FN], af[FK];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        gf[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&Gs[(wn0 + i * 32 + fr) * LDW + s * 16 + fh * 8]));
+#pragma unroll
+      for (int j = 0; j < FK; ++j)
+        af[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&As[(wk0 + j * 32 + fr) * LDW + s * 16 + fh * 8]));
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[i], af[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) swrite(cur ^ 1, m0 + WMK);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // D[n][k]: col k = lane&31, rows n = (r&3) + 8(r>>2) + 4h.  No-return fp32
+  // atomics into dW32 [N][K] (zeroed by the caller): per register, each
+  // half-wave adds one 128-B row segment -- the full-rate atomic shape
+  // (MI355X_MICROARCH.md "Global float atomics").
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const int k = k0 + wk0 + j * 32 + fr;
+        atomic_add_f32(dw32 + static_cast<int64_t>(n) * K + k, acc[i][j][r]);
+      }
+}
+
+// dW (bf16) = scale * dW32, and dW32 re-zeroed for the next accumulation
+__global__ __launch_bounds__(kThreads) void wgrad_cast_kernel(float* __restrict__ dw32, int64_t nk, float scale,
+                                                              bf16_t* __restrict__ out) {
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x) * 4;
+  if (i4 >= nk) return;
+  const float4 a = *reinterpret_cast<const float4*>(dw32 + i4);
+  *reinterpret_cast<float4*>(dw32 + i4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  const uint32_t lo = static_cast<uint32_t>(f32_to_bf16(a.x * scale)) | (static_cast<uint32_t>(f32_to_bf16(a.y * scale)) << 16);
+  const uint32_t hi = static_cast<uint32_t>(f32_to_bf16(a.z * scale)) | (static_cast<uint32_t>(f32_to_bf16(a.w * scale)) << 16);
+  *reinterpret_cast<uint2*>(out + i4) = make_uint2(lo, hi);
+}
+
+template <int BN, bool PRO, bool GATHER, int EPI>
+hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = p.N / BN;
+  // ~4 waves of persistent blocks over 256 CUs x 2 blocks/CU, nblk % 8 == 0
+  int GM = (2048 + tiles_n - 1) / tiles_n;
+  if (GM > tiles_m) GM = tiles_m;
+  while ((GM * tiles_n) % 8) ++GM;
+  hipLaunchKernelGGL((gemm1x1_kernel<BN, PRO, GATHER, EPI>), dim3(GM * tiles_n), dim3(kThreads), 0, s, p, GM,
+                     tiles_m, tiles_n);
+  return hipGetLastError();
+}
+
+// forward convs (prologue / row gather) only ever use the PLAIN and STATS
+// epilogues; the dgrad epilogues run without either
+template <int BN, bool PRO, bool GATHER>
+hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
+  switch (epi) {
+    case EPI_PLAIN: return launch_gemm<BN, PRO, GATHER, EPI_PLAIN>(p, s);
+    case EPI_STATS: return launch_gemm<BN, PRO, GATHER, EPI_STATS>(p, s);
+  }
+  if constexpr (!PRO && !GATHER) {
+    switch (epi) {
+      case EPI_MASKX: return launch_gemm<BN, PRO, GATHER, EPI_MASKX>(p, s);
+      case EPI_RESBITS: return launch_gemm<BN, PRO, GATHER, EPI_RESBITS>(p, s);
+      case EPI_RES: return launch_gemm<BN, PRO, GATHER, EPI_RES>(p, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
+  if (a.K % BK || a.N % 64 || a.M <= 0) return hipErrorInvalidValue;
+  GemmParams p{};
+  p.A = static_cast<const bf16_t*>(a.A);
+  p.B = static_cast<const bf16_t*>(a.B);
+  p.C = static_cast<bf16_t*>(a.C);
+  p.M = a.M; p.N = a.N; p.K = a.K;
+  p.Hout = a.Hout; p.Wout = a.Wout; p.Hin = a.Hin; p.Win = a.Win; p.stride = a.stride;
+  p.pro_coef = a.pro_coef;
+  p.shift = a.shift; p.acc = a.acc;
+  p.ex = static_cast<const bf16_t*>(a.ex); p.emean = a.emean; p.ecoef = a.ecoef;
+  p.eres = static_cast<const bf16_t*>(a.eres); p.res_stride = a.res_stride > 0 ? a.res_stride : 1;
+  p.res_H = a.res_H; p.res_W = a.res_W;
+  p.ebits = a.ebits; p.ex2 = static_cast<const bf16_t*>(a.ex2); p.emean2 = a.emean2; p.acc2 = a.acc2;
+  const bool pro = a.pro_coef != nullptr;
+  const bool gather = a.stride > 1;
+  const int epi = a.epi;
+  if (epi == EPI_RES || epi == EPI_RESBITS) {
+    if (!p.eres) return hipErrorInvalidValue;
+  }
+  // BN = 128 whenever N allows (fewer A re-reads); 64 for the 64-channel layers
+  if (a.N % 128 == 0) {
+    if (pro) return gather ? dispatch_epi<128, true, true>(p, epi, s) : dispatch_epi<128, true, false>(p, epi, s);
+    return gather ? dispatch_epi<128, false, true>(p, epi, s) : dispatch_epi<128, false, false>(p, epi, s);
+  }
+  if (pro) return gather ? dispatch_epi<64, true, true>(p, epi, s) : dispatch_epi<64, true, false>(p, epi, s);
+  return gather ? dispatch_epi<64, false, true>(p, epi, s) : dispatch_epi<64, false, false>(p, epi, s);
+}
+
+int conv1x1_wgrad_splits(int M, int N, int K) {
+  const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
+  const int tiles = (N / tn) * (K / tk);
+  int splits = (1024 + tiles - 1) / tiles;
+  const int max_splits = (M + WMK - 1) / WMK;
+  if (splits > max_splits) splits = max_splits;
+  return splits < 1 ? 1 : splits;
+}
+
+namespace {
+template <int TN_, int TK_>
+void launch_wgrad(dim3 grid, hipStream_t s, const bf16_t* g, const bf16_t* x, const float* pro, float* dw32, int M,
+                  int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int rps, int tiles_k) {
+  const bool gather = stride > 1;
+  if (pro) {
+    if (gather)
+      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, true, true>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N,
+                         K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+    else
+      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, true, false>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N,
+                         K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  } else {
+    if (gather)
+      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, false, true>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N,
+                         K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+    else
+      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, false, false>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M,
+                         N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  }
+}
+}  // namespace
+
+hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
+                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s) {
+  if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
+  const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
+  const int splits = conv1x1_wgrad_splits(M, N, K);
+  int rps = (M + splits - 1) / splits;
+  rps = (rps + WMK - 1) / WMK * WMK;
+  const int tiles_k = K / tk;
+  dim3 grid((M + rps - 1) / rps, (N / tn) * tiles_k);
+  const bf16_t* g = static_cast<const bf16_t*>(G);
+  const bf16_t* x = static_cast<const bf16_t*>(A);
+  if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  KDL_CHECK_HIP(hipGetLastError());
+  if (dW) {
+    const int64_t nk = static_cast<int64_t>(N) * K;
+    const int rgrid = static_cast<int>((nk / 4 + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(wgrad_cast_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, scale, static_cast<bf16_t*>(dW));
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kdl

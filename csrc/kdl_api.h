@@ -34,6 +34,36 @@ hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, 
                             void* dgamma, void* dbeta, float* ws, int N, int H, int W, int C,
                             int pdtype, bool training, hipStream_t s);
 
+// Staged BN entry points for the explicit ResNet engine (bf16 NHWC, C % 8 == 0).
+// Forward: stats (or a conv1x1 STATS epilogue) -> finalize (shift = the K the sums
+// were taken around: null = x[0, c]) -> apply (optional residual, or a second
+// BN-normalised branch xd/wsd; optional packed mask).  Backward: mask_reduce (or a
+// conv1x1 MASKX/RESBITS epilogue) -> finalize -> apply (g already masked;
+// optional second branch).
+hipError_t bn_stage_fwd_stats(const void* x, float* ws, int64_t M, int C, hipStream_t s);
+hipError_t bn_stage_fwd_finalize(const void* x, const float* shift, float* ws, int64_t M, int C, const void* gamma,
+                                 const void* beta, float* rm, float* rv, float* save_mean, float* save_invstd,
+                                 int pdtype, bool training, float momentum, float eps, hipStream_t s);
+const float* bn_stage_coef(const float* ws, int C);
+hipError_t bn_stage_fwd_apply(const void* x, const float* ws, const void* res, const void* xd, const float* wsd,
+                              void* y, uint8_t* mbits, int64_t M, int C, bool relu, hipStream_t s);
+hipError_t bn_stage_bwd_mask_reduce(const void* dy, int dy_rows_per_img, float dy_scale, const uint8_t* mbits,
+                                    const void* x, const float* mean, void* gout, float* ws, int64_t M, int C,
+                                    const void* x2, const float* mean2, float* ws2, hipStream_t s);
+// BN+ReLU backward with the ReLU mask recomputed from x (relu_mask_x) or no mask:
+// reduce (sums only) -> finalize -> apply_maskx.
+hipError_t bn_stage_bwd_reduce(const void* dy, const void* x, const void* gamma, const void* beta, const float* mean,
+                               const float* invstd, float* ws, int64_t M, int C, bool relu_mask_x, int pdtype,
+                               hipStream_t s);
+hipError_t bn_stage_bwd_apply_maskx(const void* dy, const void* x, const void* gamma, const void* beta,
+                                    const float* mean, const float* invstd, const float* ws, void* dx, int64_t M,
+                                    int C, int pdtype, hipStream_t s);
+hipError_t bn_stage_bwd_finalize(float* ws, int64_t M, int C, const void* gamma, const float* mean,
+                                 const float* invstd, void* dgamma, void* dbeta, int pdtype, bool training,
+                                 hipStream_t s);
+hipError_t bn_stage_bwd_apply(const void* g, const void* x, const float* ws, void* dx, const void* xd,
+                              const float* wsd, void* dxd, int64_t M, int C, hipStream_t s);
+
 // ---- optim.hip
 struct OptChunk {
   int64_t start;
@@ -95,6 +125,37 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
                           const int64_t* seg, int U, int D, float* out, hipStream_t s);
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
                            int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s);
+
+
+// ---- conv1x1.hip (ResNet 1x1 convs as MFMA GEMMs with fused BN prologue/epilogues)
+// epi: 0 plain, 1 BN-forward stats, 2 ReLU-mask-from-x + BN-backward sums,
+//      3 residual add + packed-bit mask + BN-backward sums (+ second BN), 4 residual add.
+struct Conv1x1Args {
+  const void* A;        // bf16 [rows, K]
+  const void* B;        // bf16 [N, K]
+  void* C;              // bf16 [M, N]
+  int M, N, K;
+  int Hout, Wout, Hin, Win, stride;  // stride > 1: A rows are gathered (strided 1x1 conv)
+  const float* pro_coef;             // [2K] scale | shift -> A = relu(A*scale + shift); null = none
+  int epi;
+  const float* shift;                // epi 1: [N]
+  float* acc;                        // epi 1-3: BN workspace replicas [32][2N]
+  const void* ex;                    // epi 2-3: BN input [M, N]
+  const float* emean;                // epi 2-3: [N]
+  const float* ecoef;                // epi 2: [2N]
+  const void* eres;                  // epi 3-4: d(identity)
+  int res_stride, res_H, res_W;      // eres sampled at stride res_stride of the (res_H, res_W) grid
+  const uint8_t* ebits;              // epi 3: [M, N/8]
+  const void* ex2;                   // epi 3: optional second BN input
+  const float* emean2;
+  float* acc2;
+};
+hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
+int conv1x1_wgrad_splits(int M, int N, int K);
+// dw32 [N, K] fp32 (zero on entry) += sum_m G[m, :]^T pro(A)[m, :]; if dW (bf16) is
+// given, dW = scale * dw32 and dw32 is re-zeroed (so dw32 can be reused).
+hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
+                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s);
 
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 

@@ -1,0 +1,565 @@
+"""Explicit forward/backward engine for ResNet-50 training on MI355X.
+
+Autograd executes a network as a chain of independent ops, so every op pays
+its own passes over HBM and every activation with two consumers (the
+bottleneck input feeds conv1 AND the residual) gets an extra gradient-sum
+kernel.  This engine runs the same ``models.resnet.ResNet`` parameters
+through a hand-scheduled step instead, built around the fused 1x1-conv MFMA
+GEMMs of ``csrc/conv1x1.hip``:
+
+forward, per bottleneck (``B`` = BatchNorm, ``R`` = ReLU)::
+
+    c1 = conv1(x)                [GEMM, epilogue: B1 statistics]
+    a1 = R(B1(c1))               [apply pass]
+    c2 = conv2(a1)               [MIOpen 3x3]      ; B2 statistics pass
+    c3 = conv3(R(B2(c2)))        [GEMM, prologue: B2+R while staging A -- the
+                                  B2 output never reaches HBM; epilogue: B3 stats]
+    cd = down(x)                 [GEMM, strided row gather, epilogue: Bd stats]
+    out = R(B3(c3) + (Bd(cd) | x))  [one apply pass, 1-bit ReLU mask saved]
+
+backward, per bottleneck (``g`` = gradient at the pre-ReLU block sum, already
+masked; it and B3's reduction sums come out of the NEXT block's conv1 dgrad
+epilogue)::
+
+    dc3 (, dcd) = B3 (, Bd) apply-backward of g        [one pass for both branches]
+    g2 = conv3 dgrad (dc3), masked by R'(B2(c2)) + B2 reduction sums   [GEMM epilogue]
+    dW3 = sum dc3^T R(B2(c2))                          [GEMM, B2+R recomputed in the prologue]
+    dc2 = B2 apply-backward(g2) ; da1, dW2 = conv2 backward [MIOpen]
+    dc1 = B1 backward(da1) (mask recomputed from c1)
+    g_prev = conv1 dgrad(dc1) + d(identity) (strided gather of the downsample dgrad),
+             masked by the previous block's ReLU bits, + B3_prev (and Bd_prev)
+             reduction sums                            [GEMM epilogue]
+    dW1, dWd                                           [GEMM]
+
+which deletes, per block, the B1/B3/Bd statistics passes, the B2 apply pass
+(and its activation), the B2 and B3 reduction passes, the downsample BN
+output, and autograd's residual-gradient add kernel.
+
+Gradients are written straight into the ``FlatParamSpace`` gradient buffer
+and each parameter is announced to ``FlatDDP.ready`` as soon as it is final,
+so the bucketed RCCL all-reduce overlaps the rest of the backward exactly as
+with autograd hooks.
+
+Two kernel backends with identical semantics: ``HipKernels`` (the CDNA4
+kernels; the only GPU path) and ``TorchKernels`` (plain fp32 PyTorch with the
+same bf16 rounding points), which lets the CPU test-suite check the engine's
+data flow against autograd on ``resnet_tiny``.
+
+The reference has no model code; this is the data plane of
+BASELINE.json's "PyTorchJob ResNet-50 DDP bf16" config.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from kubedl_amd.models.resnet import BNAct, Bottleneck, ResNet
+
+REP = 32  # BN workspace replicas (csrc/bn_act.hip kReplicas)
+
+
+def _nhwc_empty(n, c, h, w, like):
+    # allocate channels_last directly (.contiguous(channels_last) on a fresh
+    # NCHW tensor would launch a full-size copy kernel)
+    return torch.empty((n, c, h, w), dtype=like.dtype, device=like.device, memory_format=torch.channels_last)
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> [N*H*W, C] view of the same memory."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _from_rows(r: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    c = r.shape[1]
+    return r.view(n, h, w, c).permute(0, 3, 1, 2)
+
+
+def _bfr(t: torch.Tensor) -> torch.Tensor:
+    """Round an fp32 tensor through bf16 (the kernels' storage precision)."""
+    return t.to(torch.bfloat16).float()
+
+
+class BNState:
+    """Per-layer BatchNorm bookkeeping of one step (module + saved statistics)."""
+
+    def __init__(self, mod: BNAct, dev):
+        self.mod = mod
+        C = mod.channels
+        self.C = C
+        self.save_mean = torch.zeros(C, device=dev)
+        self.save_invstd = torch.ones(C, device=dev)
+        self.ws = None          # HIP workspace (replicas | coefs), self-cleaning
+        # torch-backend state
+        self.fsum = None        # (s1, s2, shift) forward sums
+        self.fcoef = None       # (scale, shift)
+        self.bsum = None        # (sa, sb) backward sums
+        self.bcoef = None       # (k, c1, c0)
+
+
+# ---------------------------------------------------------------------------- kernels
+class HipKernels:
+    """The CDNA4 path: csrc/conv1x1.hip GEMMs + csrc/bn_act.hip staged BN kernels."""
+
+    name = "hip"
+
+    def __init__(self, dev):
+        from kubedl_amd.ops import _ext
+        self.ext = _ext.load()
+        self.dev = dev
+        self._dw32 = {}
+
+    def init_bn(self, st: BNState):
+        st.ws = torch.zeros(self.ext.bn_workspace_floats(st.C), device=self.dev)
+        st.coef_off = self.ext.bn_coef_offset(st.C)
+
+    def fcoef(self, st):  # [2C] scale | shift view of the workspace
+        return st.ws[st.coef_off:st.coef_off + 2 * st.C]
+
+    def _fwd_acc(self, st):
+        return st.ws[:REP * 2 * st.C]
+
+    def _bwd_acc(self, st):
+        return st.ws[REP * 2 * st.C:REP * 4 * st.C]
+
+    # -- forward
+    def conv1x1_fwd(self, x, w, stride, pro: BNState | None, out: BNState):
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+        y = _nhwc_empty(n, cout, ho, wo, x)
+        M = n * ho * wo
+        self.ext.conv1x1_gemm(x, w, y, M, cout, cin, ho, wo, h, wd, stride,
+                              self.fcoef(pro) if pro is not None else None, 1, out.mod.running_mean,
+                              self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
+        return y
+
+    def bn_stats(self, x, st):
+        self.ext.bn_stage_fwd_stats(x, st.ws, x.numel() // st.C, st.C)
+
+    def bn_finalize(self, st, M, x=None, gemm_shift=False):
+        m = st.mod
+        self.ext.bn_stage_fwd_finalize(None if gemm_shift else x, m.running_mean if gemm_shift else None, st.ws, M,
+                                       st.C, m.weight, m.bias, m.running_mean, m.running_var, st.save_mean,
+                                       st.save_invstd, True, float(m.momentum), float(m.eps))
+
+    def bn_apply(self, x, st, relu=True, res=None, other=None, want_mask=False):
+        M = x.numel() // st.C
+        y = torch.empty_like(x)
+        mb = torch.empty(M * st.C // 8, dtype=torch.uint8, device=x.device) if want_mask else None
+        xd, std_ = other if other is not None else (None, None)
+        self.ext.bn_stage_fwd_apply(x, st.ws, res, xd, std_.ws if std_ is not None else None, y, mb, M, st.C, relu)
+        return y, mb
+
+    def stem_fwd(self, c0, st):
+        m = st.mod
+        y, mean, invstd, idx = self.ext.bn_pool_fwd(c0, m.weight, m.bias, m.running_mean, m.running_var, True,
+                                                    float(m.momentum), float(m.eps), st.ws)
+        st.save_mean, st.save_invstd = mean, invstd
+        return y, idx
+
+    # -- backward
+    def head_mask_reduce(self, dfeat, hw, mbits, x, st, xd=None, std_=None):
+        M = x.numel() // st.C
+        g = torch.empty_like(x)
+        self.ext.bn_stage_bwd_mask_reduce(dfeat.to(torch.bfloat16).contiguous(), hw, 1.0 / hw, mbits, x,
+                                          st.save_mean, g, st.ws, M, st.C, xd,
+                                          std_.save_mean if std_ is not None else None,
+                                          std_.ws if std_ is not None else None)
+        return g
+
+    def bn_bwd_finalize(self, st, M, dgamma, dbeta):
+        self.ext.bn_stage_bwd_finalize(st.ws, M, st.C, st.mod.weight, st.save_mean, st.save_invstd, dgamma, dbeta,
+                                       True)
+
+    def bn_bwd_apply(self, g, x, st, xd=None, std_=None):
+        M = x.numel() // st.C
+        dx = torch.empty_like(x)
+        dxd = torch.empty_like(xd) if xd is not None else None
+        self.ext.bn_stage_bwd_apply(g, x, st.ws, dx, xd, std_.ws if std_ is not None else None, dxd, M, st.C)
+        return dx, dxd
+
+    def bn_bwd_full(self, dy, x, st, dgamma, dbeta):
+        """BN+ReLU backward with the mask recomputed from x: reduce pass, then the
+        staged finalize (dgamma/dbeta straight into the gradient buffer) + apply."""
+        m = st.mod
+        M = x.numel() // st.C
+        self.ext.bn_stage_bwd_reduce(dy, x, m.weight, m.bias, st.save_mean, st.save_invstd, st.ws, M, st.C, True)
+        self.bn_bwd_finalize(st, M, dgamma, dbeta)
+        dx = torch.empty_like(x)
+        self.ext.bn_stage_bwd_apply_maskx(dy, x, m.weight, m.bias, st.save_mean, st.save_invstd, st.ws, dx, M, st.C)
+        return dx
+
+    def dgrad_maskx(self, g, wt, x2, st2):
+        """g [.., K=cout] -> masked d(input) [.., cin] + st2 backward sums; wt = W^T [cin, cout]."""
+        n, cout, h, w = g.shape
+        cin = wt.shape[0]
+        out = _nhwc_empty(n, cin, h, w, g)
+        M = n * h * w
+        self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), x2,
+                              st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
+        return out
+
+    def dgrad_plain(self, g, wt):
+        n, cout, h, w = g.shape
+        cin = wt.shape[0]
+        out = _nhwc_empty(n, cin, h, w, g)
+        self.ext.conv1x1_gemm(g, wt, out, n * h * w, cin, cout, 0, 0, 0, 0, 1, None, 0, None, None, None, None, None,
+                              None, 1, 0, 0, None, None, None, None)
+        return out
+
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None):
+        """conv1 dgrad + d(identity); with ``prev`` = (mbits, c3, st3, cd, std) the
+        previous block's ReLU mask is applied and its BN sums accumulated."""
+        n, cout, h, w = g.shape
+        cin = wt.shape[0]
+        out = _nhwc_empty(n, cin, h, w, g)
+        M = n * h * w
+        if prev is None:
+            self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 4, None, None, None, None, None, eres,
+                                  res_stride, h, w, None, None, None, None)
+        else:
+            mbits, c3, st3, cd, std_ = prev
+            self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, self._bwd_acc(st3), c3,
+                                  st3.save_mean, None, eres, res_stride, h, w, mbits, cd,
+                                  std_.save_mean if std_ is not None else None,
+                                  self._bwd_acc(std_) if std_ is not None else None)
+        return out
+
+    def wgrad(self, g, x, stride, pro: BNState | None, dW):
+        n, cout, ho, wo = g.shape
+        _, cin, h, w = x.shape
+        key = (cout, cin)
+        dw32 = self._dw32.get(key)
+        if dw32 is None:
+            dw32 = self._dw32[key] = torch.zeros(cout, cin, device=g.device)
+        self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
+                               n * ho * wo, cout, cin, ho, wo, h, w, stride)
+
+    def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
+        m = st.mod
+        dx, dg, db = self.ext.bn_pool_bwd(dp, idx, c0, m.weight, m.bias, st.save_mean, st.save_invstd, True, st.ws)
+        dgamma.copy_(dg)
+        dbeta.copy_(db)
+        return dx
+
+
+class TorchKernels:
+    """Reference semantics of every HipKernels op in fp32 PyTorch (CPU tests)."""
+
+    name = "torch"
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def init_bn(self, st):
+        pass
+
+    @staticmethod
+    def _pro(x, st):
+        sc, sf = st.fcoef
+        return _bfr(F.relu(x.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)))
+
+    def conv1x1_fwd(self, x, w, stride, pro, out):
+        a = self._pro(x, pro) if pro is not None else x.float()
+        y = F.conv2d(a[:, :, ::stride, ::stride], w.float()[:, :, None, None])
+        y = y.to(x.dtype)
+        self._stats(y, out, out.mod.running_mean.clone())
+        return y.contiguous(memory_format=torch.channels_last)
+
+    def _stats(self, y, st, shift):
+        d = _rows(y.float()) - shift
+        st.fsum = (d.sum(0), (d * d).sum(0), shift)
+
+    def bn_stats(self, x, st):
+        self._stats(x, st, _rows(x.float())[0].clone())
+
+    def bn_finalize(self, st, M, x=None, gemm_shift=False):
+        s1, s2, K = st.fsum
+        m = st.mod
+        m1 = s1 / M
+        var = (s2 / M - m1 * m1).clamp_min(0)
+        mean = K + m1
+        invstd = torch.rsqrt(var + m.eps)
+        st.save_mean, st.save_invstd = mean, invstd
+        with torch.no_grad():
+            unb = var * M / (M - 1) if M > 1 else var
+            m.running_mean.mul_(1 - m.momentum).add_(m.momentum * mean)
+            m.running_var.mul_(1 - m.momentum).add_(m.momentum * unb)
+        sc = m.weight.float() * invstd
+        st.fcoef = (sc, m.bias.float() - mean * sc)
+
+    def bn_apply(self, x, st, relu=True, res=None, other=None, want_mask=False):
+        sc, sf = st.fcoef
+        o = x.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)
+        if other is not None:
+            xd, sd = other
+            o = o + (xd.float() * sd.fcoef[0].view(1, -1, 1, 1) + sd.fcoef[1].view(1, -1, 1, 1))
+        elif res is not None:
+            o = o + res.float()
+        mask = o > 0 if want_mask else None
+        if relu:
+            o = F.relu(o)
+        return o.to(x.dtype).contiguous(memory_format=torch.channels_last), mask
+
+    def stem_fwd(self, c0, st):
+        self.bn_stats(c0, st)
+        self.bn_finalize(st, c0.numel() // st.C)
+        a, _ = self.bn_apply(c0, st, relu=True)
+        y, idx = F.max_pool2d(a.float(), 3, 2, 1, return_indices=True)
+        return y.to(c0.dtype).contiguous(memory_format=torch.channels_last), idx
+
+    def head_mask_reduce(self, dfeat, hw, mask, x, st, xd=None, std_=None):
+        n, c, h, w = x.shape
+        dy = _bfr(_bfr(dfeat.float()) / hw).view(n, c, 1, 1).expand(n, c, h, w)
+        g = torch.where(mask, dy, torch.zeros_like(dy))
+        self._bsum(g, x, st)
+        if xd is not None:
+            self._bsum(g, xd, std_)
+        return g.to(x.dtype).contiguous(memory_format=torch.channels_last)
+
+    def _bsum(self, g, x, st):
+        gr = _rows(g.float())
+        st.bsum = (gr.sum(0), (gr * (_rows(x.float()) - st.save_mean)).sum(0))
+
+    def bn_bwd_finalize(self, st, M, dgamma, dbeta):
+        sa, sb = st.bsum
+        inv = st.save_invstd
+        db, dg = sa, sb * inv
+        dgamma.copy_(dg)
+        dbeta.copy_(db)
+        k = st.mod.weight.float() * inv
+        c1 = -k * inv * dg / M
+        c0 = -k * db / M - c1 * st.save_mean
+        st.bcoef = (k, c1, c0)
+
+    @staticmethod
+    def _bapply(g, x, st):
+        k, c1, c0 = (t.view(1, -1, 1, 1) for t in st.bcoef)
+        return (k * g.float() + c1 * x.float() + c0).to(x.dtype).contiguous(memory_format=torch.channels_last)
+
+    def bn_bwd_apply(self, g, x, st, xd=None, std_=None):
+        return self._bapply(g, x, st), (self._bapply(g, xd, std_) if xd is not None else None)
+
+    def bn_bwd_full(self, dy, x, st, dgamma, dbeta):
+        sc, sf = st.fcoef
+        mask = (x.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
+        g = torch.where(mask, dy.float(), torch.zeros_like(dy.float()))
+        self._bsum(g, x, st)
+        self.bn_bwd_finalize(st, x.numel() // st.C, dgamma, dbeta)
+        return self._bapply(g, x, st)
+
+    def dgrad_maskx(self, g, wt, x2, st2):
+        d = _bfr(F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)))
+        sc, sf = st2.fcoef
+        mask = (x2.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
+        d = torch.where(mask, d, torch.zeros_like(d))
+        self._bsum(d, x2, st2)
+        return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
+
+    def dgrad_plain(self, g, wt):
+        return F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)).to(g.dtype).contiguous(
+            memory_format=torch.channels_last)
+
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None):
+        d = _bfr(F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)))
+        r = torch.zeros_like(d)
+        r[:, :, ::res_stride, ::res_stride] = eres.float()
+        d = _bfr(d + r)
+        if prev is not None:
+            mask, c3, st3, cd, std_ = prev
+            d = torch.where(mask, d, torch.zeros_like(d))
+            self._bsum(d, c3, st3)
+            if cd is not None:
+                self._bsum(d, cd, std_)
+        return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
+
+    def wgrad(self, g, x, stride, pro, dW):
+        a = self._pro(x, pro) if pro is not None else x.float()
+        a = _rows(a[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last))
+        dW.copy_((_rows(g.float()).t() @ a).view_as(dW))
+
+    def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
+        sc, sf = st.fcoef
+        n, c, h, w = c0.shape
+        # overlapping 3x3/s2 windows: a pixel that is the max of several windows
+        # receives the sum of their gradients (scatter-add, not unpool's overwrite)
+        da = torch.zeros(n, c, h * w, dtype=torch.float32, device=c0.device)
+        da.scatter_add_(2, idx.reshape(n, c, -1), dp.float().reshape(n, c, -1))
+        da = da.view(n, c, h, w).to(c0.dtype).contiguous(memory_format=torch.channels_last)
+        return self.bn_bwd_full(da, c0, st, dgamma, dbeta)
+
+
+# ---------------------------------------------------------------------------- engine
+class ResNetEngine:
+    """Hand-scheduled training step of a ``ResNet`` built from ``Bottleneck``s.
+
+    ``grad_view(param)`` must return the tensor that receives ``param``'s
+    gradient (a view of the flat gradient buffer); ``on_ready(param)`` is
+    called once that gradient is final (DP bucket launch)."""
+
+    def __init__(self, model: ResNet, backend: str = "auto", grad_view=None, on_ready=None):
+        self.model = model
+        p = next(model.parameters())
+        self.dev = p.device
+        if backend == "auto":
+            backend = "hip" if self.dev.type == "cuda" else "torch"
+        self.K = HipKernels(self.dev) if backend == "hip" else TorchKernels(self.dev)
+        self.grad_view = grad_view or self._own_grad
+        self.on_ready = on_ready or (lambda prm: None)
+        self.bn = {}
+        for m in model.modules():
+            if isinstance(m, BNAct):
+                st = BNState(m, self.dev)
+                self.K.init_bn(st)
+                self.bn[m] = st
+        self.blocks = [b for b in model.layers if isinstance(b, Bottleneck)]
+        assert len(self.blocks) == len(model.layers), "engine supports Bottleneck stacks only"
+
+    @staticmethod
+    def _own_grad(prm):
+        if prm.grad is None:
+            prm.grad = torch.zeros_like(prm)
+        return prm.grad
+
+    def _g(self, prm):
+        return self.grad_view(prm)
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor):
+        K, m = self.K, self.model
+        st0 = self.bn[m.bn1]
+        c0 = F.conv2d(x, m.conv1.weight, stride=2, padding=3).contiguous(memory_format=torch.channels_last)
+        x1, idx = K.stem_fwd(c0, st0)
+        saved = []
+        cur = x1
+        for blk in self.blocks:
+            s = blk.conv2.stride[0]
+            st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
+            n, _, h, w = cur.shape
+            c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
+            K.bn_finalize(st1, n * h * w, gemm_shift=True)
+            a1, _ = K.bn_apply(c1, st1, relu=True)
+            c2 = F.conv2d(a1, blk.conv2.weight, stride=s, padding=1).contiguous(memory_format=torch.channels_last)
+            ho, wo = c2.shape[-2:]
+            K.bn_stats(c2, st2)
+            K.bn_finalize(st2, n * ho * wo, x=c2)
+            c3 = K.conv1x1_fwd(c2, blk.conv3.weight.view(blk.conv3.out_channels, -1), 1, st2, st3)
+            K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
+            cd = None
+            if blk.down_conv is not None:
+                std_ = self.bn[blk.down_bn]
+                cd = K.conv1x1_fwd(cur, blk.down_conv.weight.view(blk.down_conv.out_channels, -1),
+                                   blk.down_conv.stride[0], None, std_)
+                K.bn_finalize(std_, n * ho * wo, gemm_shift=True)
+                out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
+            else:
+                out, mbits = K.bn_apply(c3, st3, relu=True, res=cur, want_mask=True)
+            saved.append((cur, c1, a1, c2, c3, cd, mbits))
+            cur = out
+        self._saved = (x, c0, idx, saved, cur)
+        return cur
+
+    # ------------------------------------------------------------------ step
+    def forward_backward(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """One training forward + backward; returns the (detached) loss."""
+        m = self.model
+        feat_map = self.forward(x)
+        n, c, h, w = feat_map.shape
+        with torch.enable_grad():  # the pooling head (0.1% of the FLOPs) runs under autograd
+            feat = feat_map.mean((2, 3), dtype=torch.float32).detach().requires_grad_(True)
+            fcw = m.fc.weight.detach().requires_grad_(True)
+            fcb = m.fc.bias.detach().requires_grad_(True)
+            logits = F.linear(feat.to(fcw.dtype), fcw, fcb)
+            loss = F.cross_entropy(logits.float(), y)
+            dfeat, dfcw, dfcb = torch.autograd.grad(loss, (feat, fcw, fcb))
+        with torch.no_grad():
+            self._g(m.fc.weight).copy_(dfcw)
+            self._g(m.fc.bias).copy_(dfcb)
+        self.on_ready(m.fc.weight)
+        self.on_ready(m.fc.bias)
+        self.backward(dfeat, h * w)
+        return loss.detach()
+
+    def _wt(self, conv):
+        return conv.weight.view(conv.out_channels, -1).t().contiguous()
+
+    def _bn_grads(self, st):
+        return self._g(st.mod.weight), self._g(st.mod.bias)
+
+    def _bn_ready(self, st):
+        self.on_ready(st.mod.weight)
+        self.on_ready(st.mod.bias)
+
+    @torch.no_grad()
+    def backward(self, dfeat: torch.Tensor, hw: int) -> None:
+        K, m = self.K, self.model
+        x, c0, idx, saved, last = self._saved
+        nb = len(self.blocks)
+        # gradient at the last block's pre-ReLU sum, plus its bn3 sums
+        cur_in, c1, a1, c2, c3, cd, mbits = saved[-1]
+        lblk = self.blocks[-1]
+        g = K.head_mask_reduce(dfeat, hw, mbits, c3, self.bn[lblk.bn3], cd,
+                               self.bn[lblk.down_bn] if cd is not None else None)
+        for i in range(nb - 1, -1, -1):
+            blk = self.blocks[i]
+            cur_in, c1, a1, c2, c3, cd, mbits = saved[i]
+            st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
+            n, _, ho, wo = c3.shape
+            Mo = n * ho * wo
+            # bn3 (+ downsample BN) backward: one apply pass over g for both branches
+            K.bn_bwd_finalize(st3, Mo, *self._bn_grads(st3))
+            self._bn_ready(st3)
+            std_ = self.bn[blk.down_bn] if blk.down_bn is not None else None
+            if std_ is not None:
+                K.bn_bwd_finalize(std_, Mo, *self._bn_grads(std_))
+                self._bn_ready(std_)
+            dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)
+            # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
+            g2 = K.dgrad_maskx(dc3, self._wt(blk.conv3), c2, st2)
+            K.wgrad(dc3, c2, 1, st2, self._g(blk.conv3.weight))
+            self.on_ready(blk.conv3.weight)
+            K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
+            self._bn_ready(st2)
+            dc2, _ = K.bn_bwd_apply(g2, c2, st2)
+            # conv2 (3x3, MIOpen)
+            s = blk.conv2.stride[0]
+            da1, dw2, _ = torch.ops.aten.convolution_backward(
+                dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, True, False])
+            self._g(blk.conv2.weight).copy_(dw2)
+            self.on_ready(blk.conv2.weight)
+            dc1 = K.bn_bwd_full(da1.contiguous(memory_format=torch.channels_last), c1, st1, *self._bn_grads(st1))
+            self._bn_ready(st1)
+            # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
+            if blk.down_conv is not None:
+                ds = blk.down_conv.stride[0]
+                eres = K.dgrad_plain(dcd, self._wt(blk.down_conv))
+                res_stride = ds
+            else:
+                eres, res_stride = g, 1
+            if i > 0:
+                p_in, p_c1, p_a1, p_c2, p_c3, p_cd, p_mbits = saved[i - 1]
+                pblk = self.blocks[i - 1]
+                p_std = self.bn[pblk.down_bn] if pblk.down_bn is not None else None
+                g_prev = K.dgrad_res(dc1, self._wt(blk.conv1), eres, res_stride,
+                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std))
+            else:
+                g_prev = K.dgrad_res(dc1, self._wt(blk.conv1), eres, res_stride, None)
+            K.wgrad(dc1, cur_in, 1, None, self._g(blk.conv1.weight))
+            self.on_ready(blk.conv1.weight)
+            if blk.down_conv is not None:
+                K.wgrad(dcd, cur_in, blk.down_conv.stride[0], None, self._g(blk.down_conv.weight))
+                self.on_ready(blk.down_conv.weight)
+            g = g_prev
+        # stem: fused BN + ReLU + max-pool backward, then the 7x7 conv weight gradient
+        st0 = self.bn[m.bn1]
+        dc0 = K.stem_bwd(g, idx, c0, st0, *self._bn_grads(st0))
+        self._bn_ready(st0)
+        _, dw0, _ = torch.ops.aten.convolution_backward(
+            dc0, x, m.conv1.weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False])
+        self._g(m.conv1.weight).copy_(dw0)
+        self.on_ready(m.conv1.weight)
+        self._saved = None

@@ -163,6 +163,14 @@ class FlatParamSpace:
     def _view(flat: torch.Tensor, s: ParamSlot) -> torch.Tensor:
         return torch.as_strided(flat, s.param.shape, s.param.stride(), s.offset)
 
+    def grad_view(self, param: torch.Tensor) -> torch.Tensor:
+        """The slice of the flat gradient buffer that holds ``param``'s gradient
+        (for code that writes gradients directly, e.g. the ResNet engine)."""
+        idx = getattr(self, "_slot_of", None)
+        if idx is None:
+            idx = self._slot_of = {id(s.param): s for s in self.slots}
+        return self._view(self.grad, idx[id(param)])
+
     def _chunk_table(self) -> torch.Tensor:
         rows = []
         for s in self.slots:

@@ -41,8 +41,12 @@ class Bucket:
 class FlatDDP:
     def __init__(self, space: FlatParamSpace, world_size: int, process_group=None,
                  bucket_cap_mb: float = 12.0, first_bucket_mb: float = 2.0,
-                 broadcast_from: int | None = 0):
+                 broadcast_from: int | None = 0, direct: bool = False):
+        """``direct``: gradients are written straight into ``space.grad`` by the
+        caller (the ResNet engine), which announces each finished parameter with
+        ``ready(param)`` -- no autograd hooks, no pack kernels."""
         self.space = space
+        self.direct = direct
         self.world = world_size
         self.pg = process_group
         self.buckets: list[Bucket] = []
@@ -53,7 +57,8 @@ class FlatDDP:
                     dist.broadcast(space.param, broadcast_from, group=process_group)
                     space.sync_master_from_params()
             self._build_buckets(bucket_cap_mb, first_bucket_mb)
-            self._install_hooks()
+            if not direct:
+                self._install_hooks()
 
     def _build_buckets(self, cap_mb: float, first_mb: float) -> None:
         esz = self.space.grad.element_size()
@@ -70,7 +75,7 @@ class FlatDDP:
                 cap = cap_mb * 2 ** 20
         if cur:
             self.buckets.append(Bucket(lo, _end(self.space, cur[-1]), cur))
-        if self.space.grad_mode == "pack":
+        if self.space.grad_mode == "pack" and not self.direct:
             for b in self.buckets:
                 b.packer = self.space.packer(b.slots)
         self._slot_bucket = {}
@@ -95,6 +100,12 @@ class FlatDDP:
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
+
+    def ready(self, p: torch.Tensor) -> None:
+        """Direct mode: ``p``'s gradient slice is final (launches its bucket's
+        all-reduce when it was the bucket's last parameter)."""
+        if self.world > 1:
+            self._on_grad(p)
 
     def finish(self) -> None:
         """Wait for every bucket (launching any whose params got no gradient)."""

@@ -31,7 +31,11 @@ class ResNetTrainer:
                  num_classes: int = 1000, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 5e-5, tiny: bool = False,
                  bn_backend: str = "auto", bucket_cap_mb: float = 12.0, seed: int = 0,
-                 conv_benchmark: bool = False):
+                 conv_benchmark: bool = False, engine: str = "auto"):
+        """``engine``: "fused" runs the step through ``models.resnet_engine``
+        (fused 1x1-conv GEMMs + staged BN, explicit backward); "autograd" runs
+        the module under autograd; "auto" = fused on the GPU when the model's
+        channel counts fit the GEMM tiles (multiples of 64), else autograd."""
         self.info = info
         dev = info.device
         if dev.type == "cuda":
@@ -49,7 +53,16 @@ class ResNetTrainer:
         self.model = model
         self.dtype = dtype
         self.space = FlatParamSpace(model, dtype=dtype, device=dev)
-        self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb)
+        if engine == "auto":
+            engine = "fused" if (dev.type == "cuda" and not tiny and bn_backend != "torch") else "autograd"
+        self.engine_kind = engine
+        self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb,
+                           direct=(engine == "fused"))
+        self.engine = None
+        if engine == "fused":
+            from kubedl_amd.models.resnet_engine import ResNetEngine
+            self.engine = ResNetEngine(model, backend="hip" if dev.type == "cuda" else "torch",
+                                       grad_view=self.space.grad_view, on_ready=self.ddp.ready)
         self.opt = FusedSGD(self.space, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.opt.grad_scale = self.ddp.grad_scale
         g = torch.Generator(device="cpu").manual_seed(seed + 1000 + info.rank)
@@ -63,9 +76,13 @@ class ResNetTrainer:
 
     def step(self) -> torch.Tensor:
         self.space.zero_grad()
-        out = self.model(self.x)
-        loss = F.cross_entropy(out.float(), self.y)
-        loss.backward()
+        if self.engine is not None:
+            loss = self.engine.forward_backward(self.x, self.y)
+            self.space.mark_packed()  # gradients were written into the flat buffer
+        else:
+            out = self.model(self.x)
+            loss = F.cross_entropy(out.float(), self.y)
+            loss.backward()
         self.ddp.finish()
         self.opt.step()
         self.last_loss = loss.detach()
@@ -82,7 +99,7 @@ def run(args) -> dict:
     info = kdist.init_from_env("cpu" if args.cpu else None)
     common.signal_ready({"rank": info.rank})
     tr = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
-                       bn_backend=args.bn_backend)
+                       bn_backend=args.bn_backend, engine=args.engine)
     for i in range(args.warmup):
         tr.step()
         common.maybe_inject_fault(info.rank, i)
@@ -120,6 +137,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests)")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "autograd"])
     return ap
 
 
