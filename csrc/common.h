@@ -24,12 +24,18 @@ __device__ __forceinline__ float bf16_to_f32(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
 
-// round-to-nearest-even, NaN preserved
+typedef __attribute__((ext_vector_type(2))) float kdl_f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 kdl_bf16x2_t;
+
+// round-to-nearest-even, NaN preserved: gfx950's v_cvt_pk_bf16_f32 (one VALU
+// instruction per PAIR, vs ~5 integer ops per value for the bit-trick)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const kdl_f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, kdl_bf16x2_t));
+}
+
 __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return static_cast<bf16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
+  return static_cast<bf16_t>(pack_bf16x2(f, 0.f) & 0xffffu);
 }
 
 // Load/store VEC elements of type T as fp32.  VEC*sizeof(T) is 16 bytes on
@@ -49,9 +55,7 @@ template <> struct Vec<bf16_t, 8> {
   __device__ __forceinline__ static void store(bf16_t* p, const float (&o)[8]) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = static_cast<uint32_t>(f32_to_bf16(o[2 * i])) |
-             (static_cast<uint32_t>(f32_to_bf16(o[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(o[2 * i], o[2 * i + 1]);
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

@@ -49,6 +49,8 @@
 //
 // The reference has no kernels; these serve the PyTorchJob
 // ResNet-50 worker (BASELINE.json config 2).
+#include <cstdlib>
+
 #include "common.h"
 #include "kdl_api.h"
 
@@ -59,7 +61,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 constexpr int kThreads = 256;
-constexpr int BM = 128, BK = 64;
+constexpr int BK = 64;
 constexpr int LDK = BK + 8;  // padded LDS row (bf16)
 constexpr int kRep = 32;     // replica count of the BN workspace (== bn_act.hip kReplicas)
 
@@ -100,25 +102,23 @@ __device__ __forceinline__ void unpack8(const uint4 v, float (&o)[8]) {
 }
 
 __device__ __forceinline__ uint4 pack8(const float (&o)[8]) {
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    w[i] = static_cast<uint32_t>(f32_to_bf16(o[2 * i])) | (static_cast<uint32_t>(f32_to_bf16(o[2 * i + 1])) << 16);
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
+                    pack_bf16x2(o[6], o[7]));
 }
 
 __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BN, bool PRO, bool GATHER, int EPI>
-__global__ __launch_bounds__(kThreads, 2) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
+template <int BM, int BN, int MINB, bool PRO, bool GATHER, int EPI>
+__global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
   // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
   // [BM][BN + 8] output tile and finally as the reduction scratch.
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * LDK];
   constexpr int kBuf = (BM + BN) * LDK;
-  constexpr int WN = BN >= 128 ? 2 : 1;  // waves along N
-  constexpr int WM = 4 / WN;             // waves along M
+  constexpr int WN = (BN >= 64 && BM >= 64) ? 2 : 1;  // waves along N
+  constexpr int WM = 4 / WN;                           // waves along M
+  static_assert(BM % (WM * 32) == 0 && BN % (WN * 32) == 0, "wave tile must be whole 32x32 MFMA blocks");
   constexpr int WTM = BM / WM;           // wave tile (M)
   constexpr int WTN = BN / WN;           // wave tile (N) = 64
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm1x1_kernel(GemmParams p, int 
     // so their HBM latency overlaps the LDS round trip; later groups are issued
     // a group ahead of their use.
     constexpr int NP = BM / RPP;                       // rows per thread per tile
-    constexpr int PG = EPI == EPI_RESBITS ? 4 : NP;    // prefetch group (register budget)
+    constexpr int PG = (EPI == EPI_RESBITS && NP > 4) ? 4 : NP;  // prefetch group (register budget)
     constexpr bool LX = EPI == EPI_MASKX || EPI == EPI_RESBITS;
     constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES;
     uint4 pxv[PG], prv[PG], px2[PG];
@@ -327,10 +327,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm1x1_kernel(GemmParams p, int 
         for (int g = 0; g < 4; ++g) {
           const int m = wm0 + j * 32 + fr;
           const int n = wn0 + i * 32 + 8 * g + 4 * fh;
-          const uint32_t lo = static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g])) |
-                              (static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g + 1])) << 16);
-          const uint32_t hi = static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g + 2])) |
-                              (static_cast<uint32_t>(f32_to_bf16(acc[i][j][4 * g + 3])) << 16);
+          const uint32_t lo = pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]);
+          const uint32_t hi = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
           *reinterpret_cast<uint2*>(&Cs[m * LDC + n]) = make_uint2(lo, hi);
         }
     __syncthreads();
@@ -393,7 +391,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm1x1_kernel(GemmParams p, int 
             float r[8];
             unpack8(crv[i], r);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(f32_to_bf16(v[j] + r[j]));
+            for (int j = 0; j < 8; j += 2) {
+              const uint32_t pr = pack_bf16x2(v[j] + r[j], v[j + 1] + r[j + 1]);
+              v[j] = __uint_as_float(pr << 16);
+              v[j + 1] = __uint_as_float(pr & 0xffff0000u);
+            }
           }
           if constexpr (EPI == EPI_RESBITS) {
             const uint32_t bits = cbv[i];
@@ -429,7 +431,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm1x1_kernel(GemmParams p, int 
     for (int j = 0; j < 8; ++j) {
       sh[(0 * kThreads + t) * 8 + j] = s1[j];
       sh[(1 * kThreads + t) * 8 + j] = s2[j];
-      sh[(2 * kThreads + t) * 8 + j] = s3[j];
+      if constexpr (EPI == EPI_RESBITS) sh[(2 * kThreads + t) * 8 + j] = s3[j];
     }
     __syncthreads();
     if (gm < tiles_m && er0 == 0) {
@@ -628,40 +630,60 @@ __global__ __launch_bounds__(kThreads) void wgrad_cast_kernel(float* __restrict_
   if (i4 >= nk) return;
   const float4 a = *reinterpret_cast<const float4*>(dw32 + i4);
   *reinterpret_cast<float4*>(dw32 + i4) = make_float4(0.f, 0.f, 0.f, 0.f);
-  const uint32_t lo = static_cast<uint32_t>(f32_to_bf16(a.x * scale)) | (static_cast<uint32_t>(f32_to_bf16(a.y * scale)) << 16);
-  const uint32_t hi = static_cast<uint32_t>(f32_to_bf16(a.z * scale)) | (static_cast<uint32_t>(f32_to_bf16(a.w * scale)) << 16);
+  const uint32_t lo = pack_bf16x2(a.x * scale, a.y * scale);
+  const uint32_t hi = pack_bf16x2(a.z * scale, a.w * scale);
   *reinterpret_cast<uint2*>(out + i4) = make_uint2(lo, hi);
 }
 
-template <int BN, bool PRO, bool GATHER, int EPI>
+template <int BM, int BN, int MINB, bool PRO, bool GATHER, int EPI>
 hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = p.N / BN;
-  // ~4 waves of persistent blocks over 256 CUs x 2 blocks/CU, nblk % 8 == 0
-  int GM = (2048 + tiles_n - 1) / tiles_n;
+  // persistent blocks: ~2 rounds of the resident capacity (256 CUs x MINB), nblk % 8 == 0
+  const int target = 256 * MINB * 2;
+  int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
-  hipLaunchKernelGGL((gemm1x1_kernel<BN, PRO, GATHER, EPI>), dim3(GM * tiles_n), dim3(kThreads), 0, s, p, GM,
-                     tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm1x1_kernel<BM, BN, MINB, PRO, GATHER, EPI>), dim3(GM * tiles_n), dim3(kThreads), 0, s, p,
+                     GM, tiles_m, tiles_n);
   return hipGetLastError();
 }
 
 // forward convs (prologue / row gather) only ever use the PLAIN and STATS
 // epilogues; the dgrad epilogues run without either
-template <int BN, bool PRO, bool GATHER>
+template <int BM, int BN, int MINB, bool PRO, bool GATHER>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   switch (epi) {
-    case EPI_PLAIN: return launch_gemm<BN, PRO, GATHER, EPI_PLAIN>(p, s);
-    case EPI_STATS: return launch_gemm<BN, PRO, GATHER, EPI_STATS>(p, s);
+    case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN>(p, s);
+    case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS>(p, s);
   }
   if constexpr (!PRO && !GATHER) {
     switch (epi) {
-      case EPI_MASKX: return launch_gemm<BN, PRO, GATHER, EPI_MASKX>(p, s);
-      case EPI_RESBITS: return launch_gemm<BN, PRO, GATHER, EPI_RESBITS>(p, s);
-      case EPI_RES: return launch_gemm<BN, PRO, GATHER, EPI_RES>(p, s);
+      case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX>(p, s);
+      case EPI_RESBITS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS>(p, s);
+      case EPI_RES: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RES>(p, s);
     }
   }
   return hipErrorInvalidValue;
+}
+
+template <int BM, int BN, int MINB>
+hipError_t dispatch_pg(const GemmParams& p, int epi, bool pro, bool gather, hipStream_t s) {
+  if (pro) return gather ? dispatch_epi<BM, BN, MINB, true, true>(p, epi, s) : dispatch_epi<BM, BN, MINB, true, false>(p, epi, s);
+  return gather ? dispatch_epi<BM, BN, MINB, false, true>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, false>(p, epi, s);
+}
+
+// Tile configs: 0 = 128x128 (2 blocks/CU), 1 = 128x64, 2 = 64x128, 3 = 64x64 (4 blocks/CU).
+int pick_config(int M, int N, int K) {
+  static const int forced = [] {
+    const char* e = getenv("KDL_GEMM_CFG");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0 && forced <= 3) {
+    if ((forced == 0 || forced == 2) && N % 128) return 3;
+    return forced;
+  }
+  return N % 128 == 0 ? 0 : 1;
 }
 
 }  // namespace
@@ -686,13 +708,12 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (epi == EPI_RES || epi == EPI_RESBITS) {
     if (!p.eres) return hipErrorInvalidValue;
   }
-  // BN = 128 whenever N allows (fewer A re-reads); 64 for the 64-channel layers
-  if (a.N % 128 == 0) {
-    if (pro) return gather ? dispatch_epi<128, true, true>(p, epi, s) : dispatch_epi<128, true, false>(p, epi, s);
-    return gather ? dispatch_epi<128, false, true>(p, epi, s) : dispatch_epi<128, false, false>(p, epi, s);
+  switch (pick_config(p.M, p.N, p.K)) {
+    case 0: return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
+    case 1: return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
+    case 2: return dispatch_pg<64, 128, 3>(p, epi, pro, gather, s);
+    default: return dispatch_pg<64, 64, 4>(p, epi, pro, gather, s);
   }
-  if (pro) return gather ? dispatch_epi<64, true, true>(p, epi, s) : dispatch_epi<64, true, false>(p, epi, s);
-  return gather ? dispatch_epi<64, false, true>(p, epi, s) : dispatch_epi<64, false, false>(p, epi, s);
 }
 
 int conv1x1_wgrad_splits(int M, int N, int K) {

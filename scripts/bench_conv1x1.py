@@ -12,7 +12,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from kubedl_amd.ops import _ext  # noqa: E402
 
 # (cin, cout, hin, stride, prologue, count) -- ResNet-50 v1.5 bottleneck 1x1 convs
@@ -75,6 +75,10 @@ def main():
                 None, None, None))
             r["kdl_dgrad_maskx"] = timeit(lambda: ext.conv1x1_gemm(
                 dy, wt, dx, M, cin, cout, 0, 0, 0, 0, 1, None, 2, None, wsi, x, mean_in, coef, None, 1, 0, 0, None,
+                None, None, None))
+            bits = torch.randint(0, 256, (M * cin // 8,), device=dev, dtype=torch.uint8)
+            r["kdl_dgrad_resbits"] = timeit(lambda: ext.conv1x1_gemm(
+                dy, wt, dx, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, wsi, x, mean_in, None, x, 1, h, h, bits,
                 None, None, None))
         else:
             dxs = torch.empty(M, cin, device=dev, dtype=torch.bfloat16)
