@@ -50,6 +50,7 @@
 // The reference has no kernels; these serve the PyTorchJob
 // ResNet-50 worker (BASELINE.json config 2).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kdl_api.h"
@@ -101,6 +102,21 @@ __device__ __forceinline__ void unpack8(const uint4 v, float (&o)[8]) {
   }
 }
 
+// packed-fp32 pairs: v_pk_add_f32 / v_pk_fma_f32 halve the epilogue VALU count
+typedef __attribute__((ext_vector_type(2))) float f2_t;
+
+__device__ __forceinline__ void unpack4x2(const uint4 v, f2_t (&o)[4]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f2_t{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+}
+
+__device__ __forceinline__ uint32_t pack2(const f2_t v) { return pack_bf16x2(v.x, v.y); }
+
+__device__ __forceinline__ f2_t pfma(const f2_t a, const f2_t b, const f2_t c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+
 __device__ __forceinline__ uint4 pack8(const float (&o)[8]) {
   return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
                     pack_bf16x2(o[6], o[7]));
@@ -149,7 +165,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     a_kc[i] = (c & 7) * 8;
   }
   int64_t a_off[A_CH];
-  bool a_ok[A_CH];
   uint4 ra[A_CH], rb[B_CH];
   // all A chunks of a thread share one 8-channel k-chunk ((t + i*256) & 7 == t & 7)
   float psc[8], psf[8];
@@ -158,8 +173,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   auto setup_rows = [&](int tm) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int m = tm * BM + a_row[i];
-      a_ok[i] = m < M;
+      const int m0 = tm * BM + a_row[i];
+      const int m = m0 < M ? m0 : 0;  // tail rows re-read row 0 (never stored): no divergent loads
       int64_t src = m;
       if constexpr (GATHER) {
         const int hw = p.Hout * p.Wout;
@@ -167,14 +182,14 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
         src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
       }
-      a_off[i] = a_ok[i] ? src * K : 0;
+      a_off[i] = src * K;
     }
   };
   auto gload = [&](int kt) {
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i)
-      ra[i] = a_ok[i] ? ld16(p.A + a_off[i] + k0 + a_kc[i]) : make_uint4(0, 0, 0, 0);
+      ra[i] = ld16(p.A + a_off[i] + k0 + a_kc[i]);  // rows >= M read row 0: their outputs are never stored
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int c = t + i * kThreads;
@@ -218,9 +233,9 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // per-thread reduction state: 8 channels of column chunk (t % CPR)
   const int ec = t % CPR, er0 = t / CPR;
   const int ch0 = n0 + ec * 8;
-  float s1[8], s2[8], s3[8];
+  f2_t s1[4], s2[4], s3[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; s3[j] = 0.f; }
+  for (int q = 0; q < 4; ++q) { s1[q] = f2_t{0.f, 0.f}; s2[q] = s1[q]; s3[q] = s1[q]; }
 
   int tm = gm;
   if (tm < tiles_m) {
@@ -236,10 +251,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
-      for (int j = 0; j < TM; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
+      for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
     for (int kt = 0; kt < nk; ++kt) {
       const bool more_k = kt + 1 < nk;
       const bool more = more_k || tm + GM < tiles_m;
@@ -334,20 +346,25 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     __syncthreads();
     // per-channel epilogue constants, loaded here (acc is dead) to keep them
     // out of the K loop's register budget
-    float ea[8], eb[8], em[8], em2[8];
+    f2_t ea[4], eb[4], em[4], em2[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { ea[j] = 0.f; eb[j] = 0.f; em[j] = 0.f; em2[j] = 0.f; }
+    for (int q = 0; q < 4; ++q) { ea[q] = f2_t{0.f, 0.f}; eb[q] = ea[q]; em[q] = ea[q]; em2[q] = ea[q]; }
+    auto ld2 = [](const float* src, int c) { return *reinterpret_cast<const f2_t*>(src + c); };
     if constexpr (EPI == EPI_STATS) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) em[j] = p.shift[ch0 + j];
+      for (int q = 0; q < 4; ++q) em[q] = ld2(p.shift, ch0 + 2 * q);
     } else if constexpr (EPI == EPI_MASKX) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { em[j] = p.emean[ch0 + j]; ea[j] = p.ecoef[ch0 + j]; eb[j] = p.ecoef[N + ch0 + j]; }
+      for (int q = 0; q < 4; ++q) {
+        em[q] = ld2(p.emean, ch0 + 2 * q);
+        ea[q] = ld2(p.ecoef, ch0 + 2 * q);
+        eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
+      }
     } else if constexpr (EPI == EPI_RESBITS) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        em[j] = p.emean[ch0 + j];
-        if (p.ex2) em2[j] = p.emean2[ch0 + j];
+      for (int q = 0; q < 4; ++q) {
+        em[q] = ld2(p.emean, ch0 + 2 * q);
+        if (p.ex2) em2[q] = ld2(p.emean2, ch0 + 2 * q);
       }
     }
 #pragma unroll
@@ -366,57 +383,64 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         const int row = (g0 + i) * RPP + er0;
         const int m = tm * BM + row;
         if (m >= M) continue;
-        float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(&Cs[row * LDC + ec * 8]), v);
+        const uint4 raw = *reinterpret_cast<const uint4*>(&Cs[row * LDC + ec * 8]);
         const int64_t go = static_cast<int64_t>(m) * N + ch0;
-        if constexpr (EPI == EPI_STATS) {
+        uint4 out = raw;  // PLAIN / STATS store the tile as it is
+        if constexpr (EPI != EPI_PLAIN) {
+          f2_t v[4];
+          unpack4x2(raw, v);
+          uint32_t o[4];
+          if constexpr (EPI == EPI_STATS) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = v[j] - em[j];
-            s1[j] += d;
-            s2[j] = fmaf(d, d, s2[j]);
-          }
-        } else if constexpr (EPI == EPI_MASKX) {
-          float x[8];
-          unpack8(cxv[i], x);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float g = fmaf(x[j], ea[j], eb[j]) > 0.f ? v[j] : 0.f;
-            v[j] = g;
-            s1[j] += g;
-            s2[j] = fmaf(g, x[j] - em[j], s2[j]);
-          }
-        } else if constexpr (LR) {  // RESBITS / RES: add d(identity)
-          if (crok[i]) {
-            float r[8];
-            unpack8(crv[i], r);
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-              const uint32_t pr = pack_bf16x2(v[j] + r[j], v[j + 1] + r[j + 1]);
-              v[j] = __uint_as_float(pr << 16);
-              v[j + 1] = __uint_as_float(pr & 0xffff0000u);
+            for (int q = 0; q < 4; ++q) {
+              const f2_t d = v[q] - em[q];
+              s1[q] += d;
+              s2[q] = pfma(d, d, s2[q]);
             }
-          }
-          if constexpr (EPI == EPI_RESBITS) {
-            const uint32_t bits = cbv[i];
-            float x[8];
-            unpack8(cxv[i], x);
+          } else if constexpr (EPI == EPI_MASKX) {
+            f2_t x[4];
+            unpack4x2(cxv[i], x);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float g = (bits >> j) & 1u ? v[j] : 0.f;
-              v[j] = g;
-              s1[j] += g;
-              s2[j] = fmaf(g, x[j] - em[j], s2[j]);
+            for (int q = 0; q < 4; ++q) {
+              const f2_t z = pfma(x[q], ea[q], eb[q]);
+              const f2_t g = f2_t{z.x > 0.f ? v[q].x : 0.f, z.y > 0.f ? v[q].y : 0.f};
+              s1[q] += g;
+              s2[q] = pfma(g, x[q] - em[q], s2[q]);
+              o[q] = pack2(g);
             }
-            if (p.ex2) {
-              float x2[8];
-              unpack8(cx2[i], x2);
+            out = make_uint4(o[0], o[1], o[2], o[3]);
+          } else if constexpr (LR) {  // RESBITS / RES: add d(identity), rounded to bf16
+            if (crok[i]) {
+              f2_t r[4];
+              unpack4x2(crv[i], r);
 #pragma unroll
-              for (int j = 0; j < 8; ++j) s3[j] = fmaf(v[j], x2[j] - em2[j], s3[j]);
+              for (int q = 0; q < 4; ++q) o[q] = pack2(v[q] + r[q]);
+              out = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+            if constexpr (EPI == EPI_RESBITS) {
+              unpack4x2(out, v);
+              const uint32_t bits = cbv[i];
+              f2_t x[4];
+              unpack4x2(cxv[i], x);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const f2_t g = f2_t{(bits >> (2 * q)) & 1u ? v[q].x : 0.f, (bits >> (2 * q + 1)) & 1u ? v[q].y : 0.f};
+                v[q] = g;
+                s1[q] += g;
+                s2[q] = pfma(g, x[q] - em[q], s2[q]);
+                o[q] = pack2(g);
+              }
+              if (p.ex2) {
+                f2_t x2[4];
+                unpack4x2(cx2[i], x2);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) s3[q] = pfma(v[q], x2[q] - em2[q], s3[q]);
+              }
+              out = make_uint4(o[0], o[1], o[2], o[3]);
             }
           }
         }
-        *reinterpret_cast<uint4*>(p.C + go) = pack8(v);
+        *reinterpret_cast<uint4*>(p.C + go) = out;
       }
     }
     __syncthreads();  // Cs (buffer cur^1) is restaged by the next tile's second K-step
@@ -429,9 +453,9 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     constexpr int NS = 3;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sh[(0 * kThreads + t) * 8 + j] = s1[j];
-      sh[(1 * kThreads + t) * 8 + j] = s2[j];
-      if constexpr (EPI == EPI_RESBITS) sh[(2 * kThreads + t) * 8 + j] = s3[j];
+      sh[(0 * kThreads + t) * 8 + j] = s1[j >> 1][j & 1];
+      sh[(1 * kThreads + t) * 8 + j] = s2[j >> 1][j & 1];
+      if constexpr (EPI == EPI_RESBITS) sh[(2 * kThreads + t) * 8 + j] = s3[j >> 1][j & 1];
     }
     __syncthreads();
     if (gm < tiles_m && er0 == 0) {
@@ -527,31 +551,30 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
     for (int j = 0; j < 8; ++j) { psc[j] = pro_coef[col0 + j]; psf[j] = pro_coef[K + col0 + j]; }
   }
   uint4 rr[8];
+  // Loads are unconditional (tail rows clamp to row mbeg) so that no load sits
+  // behind an exec branch; the tail rows are zeroed when staged to LDS.
   auto gload = [&](int m0) {
     if (!stager) return;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const int m = m0 + mg * 8 + r;
-      if (m < mend) {
-        int64_t src = m;
-        if (GATHER && isA) {
-          const int hw = Hout * Wout;
-          const int nimg = m / hw, rem = m - nimg * hw;
-          const int oh = rem / Wout, ow = rem - oh * Wout;
-          src = (static_cast<int64_t>(nimg) * Hin + oh * stride) * Win + ow * stride;
-        }
-        rr[r] = ld16(base + src * ld + col0);
-      } else {
-        rr[r] = make_uint4(0, 0, 0, 0);
+      const int m1 = m0 + mg * 8 + r;
+      const int m = m1 < mend ? m1 : mbeg;
+      int64_t src = m;
+      if (GATHER && isA) {
+        const int hw = Hout * Wout;
+        const int nimg = m / hw, rem = m - nimg * hw;
+        const int oh = rem / Wout, ow = rem - oh * Wout;
+        src = (static_cast<int64_t>(nimg) * Hin + oh * stride) * Win + ow * stride;
       }
+      rr[r] = ld16(base + src * ld + col0);
     }
   };
   auto swrite = [&](int buf, int m0) {
     if (!stager) return;
-    if (PRO && isA) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        if (m0 + mg * 8 + r >= mend) continue;  // padding rows stay zero
+    for (int r = 0; r < 8; ++r) {
+      const bool ok = m0 + mg * 8 + r < mend;  // padding rows stage as zero
+      if (PRO && isA) {
         float f[8];
         unpack8(rr[r], f);
 #pragma unroll
@@ -561,6 +584,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
         }
         rr[r] = pack8(f);
       }
+      if (!ok) rr[r] = make_uint4(0, 0, 0, 0);
     }
     uint4 tr[8];
     transpose8x8(rr, tr);

@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 kernel_stats.csv into per-step ms by kernel family.
+"""Summarise a rocprofv3 kernel trace into per-step ms by kernel family.
 
-usage: prof_summary.py <kernel_stats.csv> [steps]
+usage: prof_summary.py <run_kernel_stats.csv | run_results.db> [steps]
+(the .db is rocprofv3's default rocpd output; the csv needs --output-format csv)
 """
 import csv
 import re
+import sqlite3
 import sys
 
 FAMILIES = [
+    ("conv1x1-gemm(kdl)", r"kdl::.*(gemm1x1|wgrad1x1)"),
     ("bn(kdl)", r"kdl::.*bn_"),
     ("optim(kdl)", r"kdl::.*(sgd|adam|sumsq|cast)"),
     ("kdl-other", r"kdl::"),
@@ -30,18 +33,25 @@ def family(name):
     return "other"
 
 
+def load(path):
+    """(name, calls, total ns) per kernel name."""
+    if path.endswith(".db"):
+        con = sqlite3.connect(path)
+        q = "select name, count(*), sum(end - start) from kernels group by name"
+        return [(n, int(k), float(t)) for n, k, t in con.execute(q)]
+    with open(path) as f:
+        return [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])) for r in csv.DictReader(f)]
+
+
 def main():
     path = sys.argv[1]
     steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
     fam_ns, fam_calls, rows = {}, {}, []
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            ns = float(r["TotalDurationNs"])
-            calls = int(r["Calls"])
-            fam = family(r["Name"])
-            fam_ns[fam] = fam_ns.get(fam, 0.0) + ns
-            fam_calls[fam] = fam_calls.get(fam, 0) + calls
-            rows.append((ns, calls, r["Name"][:110]))
+    for name, calls, ns in load(path):
+        fam = family(name)
+        fam_ns[fam] = fam_ns.get(fam, 0.0) + ns
+        fam_calls[fam] = fam_calls.get(fam, 0) + calls
+        rows.append((ns, calls, name[:110]))
     tot = sum(fam_ns.values())
     print(f"total GPU kernel time per step: {tot / steps / 1e6:.3f} ms  (steps={steps:g})")
     print(f"{'family':28s} {'ms/step':>9s} {'%':>6s} {'launches/step':>14s}")
