@@ -552,8 +552,10 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
   need_bf16(G, M * N, "conv1x1_wgrad G");
   need_bf16(A, rows_in * K, "conv1x1_wgrad A");
   need_opt_f32(pro_coef, 2 * K, "pro_coef");
-  TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() && dw32.numel() == N * K,
-              "conv1x1_wgrad: dw32 fp32 contiguous [N, K]");
+  const int64_t slabs = kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
+  TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
+                  dw32.numel() >= slabs * N * K,
+              "conv1x1_wgrad: dw32 must be fp32 contiguous with conv1x1_wgrad_splits(M, N, K) * N * K elements");
   if (dW.has_value() && dW->defined())
     TORCH_CHECK(dW->is_cuda() && dW->is_contiguous() && dW->numel() == N * K && dW->scalar_type() == at::kBFloat16,
                 "conv1x1_wgrad: dW bf16 contiguous [N, K]");
@@ -752,7 +754,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
-  m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA, fp32 atomics, bf16 cast)");
+  m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
   m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad");
   m.def("bn_coef_offset", &bn_coef_offset, "float offset of the coefficient block in a BN workspace");
   m.def("bn_stage_fwd_stats", &bn_stage_fwd_stats, "BN forward statistics into the workspace replicas");

@@ -60,6 +60,7 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
 constexpr int kThreads = 256;
 constexpr int BK = 64;
@@ -631,10 +632,14 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
     __syncthreads();
     cur ^= 1;
   }
-  // D[n][k]: col k = lane&31, rows n = (r&3) + 8(r>>2) + 4h.  No-return fp32
-  // atomics into dW32 [N][K] (zeroed by the caller): per register, each
-  // half-wave adds one 128-B row segment -- the full-rate atomic shape
-  // (MI355X_MICROARCH.md "Global float atomics").
+  // D[n][k]: col k = lane&31, rows n = (r&3) + 8(r>>2) + 4h.  Plain fp32 stores
+  // of this split's partial tile into its own slab dw32[split][N][K] (each
+  // half-wave writes one 128-B row segment per register); wgrad_reduce_kernel
+  // sums the slabs in a fixed order.  Plain stores stream at the HBM rate where
+  // fp32 atomics into one [N][K] buffer were capped at ~1.3 TB/s of added bytes
+  // (MI355X_MICROARCH.md "Global float atomics") -- 16 splits x 4 MiB at the
+  // 7x7 stage was half the kernel's time -- and the result is deterministic.
+  float* slab = dw32 + static_cast<int64_t>(split) * N * K;
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -643,20 +648,42 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
       for (int r = 0; r < 16; ++r) {
         const int n = n0 + wn0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
         const int k = k0 + wk0 + j * 32 + fr;
-        atomic_add_f32(dw32 + static_cast<int64_t>(n) * K + k, acc[i][j][r]);
+        __builtin_nontemporal_store(acc[i][j][r], slab + static_cast<int64_t>(n) * K + k);
       }
 }
 
-// dW (bf16) = scale * dW32, and dW32 re-zeroed for the next accumulation
-__global__ __launch_bounds__(kThreads) void wgrad_cast_kernel(float* __restrict__ dw32, int64_t nk, float scale,
-                                                              bf16_t* __restrict__ out) {
-  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x) * 4;
-  if (i4 >= nk) return;
-  const float4 a = *reinterpret_cast<const float4*>(dw32 + i4);
-  *reinterpret_cast<float4*>(dw32 + i4) = make_float4(0.f, 0.f, 0.f, 0.f);
-  const uint32_t lo = pack_bf16x2(a.x * scale, a.y * scale);
-  const uint32_t hi = pack_bf16x2(a.z * scale, a.w * scale);
-  *reinterpret_cast<uint2*>(out + i4) = make_uint2(lo, hi);
+// out = scale * sum_s dw32[s] (fixed order), bf16 into dW or fp32 into slab 0.
+// Block = 16 float4 columns x 16 split groups; the groups are folded in LDS.
+constexpr int kRedCols = 16, kRedGroups = kThreads / kRedCols;
+__global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restrict__ dw32, int64_t nk, int splits,
+                                                                float scale, bf16_t* __restrict__ out) {
+  __shared__ float4 part[kRedGroups][kRedCols];
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kRedCols + col) * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < nk) {
+#pragma unroll 4
+    for (int sp = grp; sp < splits; sp += kRedGroups) {
+      const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(dw32 + sp * nk + i4));
+      a.x += v[0]; a.y += v[1]; a.z += v[2]; a.w += v[3];
+    }
+  }
+  part[grp][col] = a;
+  __syncthreads();
+  if (grp == 0 && i4 < nk) {
+#pragma unroll
+    for (int g = 1; g < kRedGroups; ++g) {
+      const float4 v = part[g][col];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    if (out) {
+      const uint32_t lo = pack_bf16x2(a.x * scale, a.y * scale);
+      const uint32_t hi = pack_bf16x2(a.z * scale, a.w * scale);
+      *reinterpret_cast<uint2*>(out + i4) = make_uint2(lo, hi);
+    } else {
+      *reinterpret_cast<float4*>(dw32 + i4) = make_float4(a.x * scale, a.y * scale, a.z * scale, a.w * scale);
+    }
+  }
 }
 
 template <int BM, int BN, int MINB, bool PRO, bool GATHER, int EPI>
@@ -788,11 +815,10 @@ hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, fl
   else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
   else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
   KDL_CHECK_HIP(hipGetLastError());
-  if (dW) {
-    const int64_t nk = static_cast<int64_t>(N) * K;
-    const int rgrid = static_cast<int>((nk / 4 + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(wgrad_cast_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, scale, static_cast<bf16_t*>(dW));
-  }
+  const int64_t nk = static_cast<int64_t>(N) * K;
+  const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, static_cast<int>(grid.x), scale,
+                     static_cast<bf16_t*>(dW));
   return hipGetLastError();
 }
 

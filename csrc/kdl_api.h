@@ -152,8 +152,9 @@ struct Conv1x1Args {
 };
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 int conv1x1_wgrad_splits(int M, int N, int K);
-// dw32 [N, K] fp32 (zero on entry) += sum_m G[m, :]^T pro(A)[m, :]; if dW (bf16) is
-// given, dW = scale * dw32 and dw32 is re-zeroed (so dw32 can be reused).
+// dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace
+// (conv1x1_wgrad_splits(M, N, K) x [N, K] fp32, no initialisation needed); the
+// result goes to dW (bf16) if given, else as fp32 into the first [N, K] of dw32.
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s);
 

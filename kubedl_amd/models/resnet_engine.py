@@ -231,12 +231,14 @@ class HipKernels:
     def wgrad(self, g, x, stride, pro: BNState | None, dW):
         n, cout, ho, wo = g.shape
         _, cin, h, w = x.shape
-        key = (cout, cin)
+        M = n * ho * wo
+        key = (M, cout, cin)  # split-M slab workspace, shared by the layers of one shape (stream-ordered)
         dw32 = self._dw32.get(key)
         if dw32 is None:
-            dw32 = self._dw32[key] = torch.zeros(cout, cin, device=g.device)
+            slabs = self.ext.conv1x1_wgrad_splits(M, cout, cin)
+            dw32 = self._dw32[key] = torch.empty(slabs * cout * cin, device=g.device)
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
-                               n * ho * wo, cout, cin, ho, wo, h, w, stride)
+                               M, cout, cin, ho, wo, h, w, stride)
 
     def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
         m = st.mod

@@ -87,7 +87,7 @@ def main():
                 None, None, None))
         r["miopen_wgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False]))
-        dw32 = torch.zeros(cout, cin, device=dev)
+        dw32 = torch.empty(ext.conv1x1_wgrad_splits(M, cout, cin) * cout * cin, device=dev)
         dw = torch.empty(cout, cin, device=dev, dtype=torch.bfloat16)
         r["kdl_wgrad"] = timeit(lambda: ext.conv1x1_wgrad(dy, x, coef if pro else None, dw32, dw, 1.0, M, cout, cin,
                                                           ho, ho, h, h, s))

@@ -67,10 +67,15 @@ for (K, N, h, pro) in WCASES:
     M = 256 * h * h
     a = torch.randn(M, K, device="cuda").bfloat16()
     g = torch.randn(M, N, device="cuda").bfloat16()
-    dw32 = torch.zeros(N * K, device="cuda")
+    dw32 = torch.empty(ext.conv1x1_wgrad_splits(M, N, K) * N * K, device="cuda")
     dW = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
     pcoef = torch.cat([torch.ones(K, device="cuda"), torch.zeros(K, device="cuda")]) if pro else None
     f = lambda: ext.conv1x1_wgrad(g, a, pcoef, dw32, dW, 1.0, M, N, K, 0, 0, 0, 0, 1)
+    try:
+        f()
+    except RuntimeError:  # older builds: one zeroed [N, K] fp32 atomic accumulator
+        dw32 = torch.zeros(N * K, device="cuda")
+        f = lambda: ext.conv1x1_wgrad(g, a, pcoef, dw32, dW, 1.0, M, N, K, 0, 0, 0, 0, 1)
     us = t(f)
     wtotal += us
     gb = M * (K + N) * 2
