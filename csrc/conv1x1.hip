@@ -529,8 +529,16 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
   constexpr int WTN = TN_ / 2, WTK = TK_ / 2;  // 2 x 2 waves
   constexpr int FN = WTN / 32, FK = WTK / 32;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int tn = blockIdx.y / tiles_k, tk = blockIdx.y % tiles_k;
-  const int split = blockIdx.x;
+  // XCD-aware order: hardware block b runs on XCD b % 8; give each XCD a
+  // contiguous range of logical ids (bijective for any grid size), and make the
+  // tiles of one M-split consecutive, so the blocks that stream the same G/A
+  // rows share that XCD's L2 instead of re-reading them from MALL/HBM.
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xq = nblk >> 3, xr = nblk & 7, xcd = bid & 7;
+  const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (bid >> 3);
+  const int tiles = (N / TN_) * tiles_k;
+  const int split = wid / tiles, tile = wid - split * tiles;
+  const int tn = tile / tiles_k, tk = tile - tn * tiles_k;
   const int n0 = tn * TN_, k0 = tk * TK_;
   const int mbeg = split * rows_per_split;
   const int mend = min(M, mbeg + rows_per_split);
@@ -807,7 +815,8 @@ hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, fl
   int rps = (M + splits - 1) / splits;
   rps = (rps + WMK - 1) / WMK * WMK;
   const int tiles_k = K / tk;
-  dim3 grid((M + rps - 1) / rps, (N / tn) * tiles_k);
+  const int nsplit = (M + rps - 1) / rps;
+  dim3 grid(nsplit * (N / tn) * tiles_k);
   const bf16_t* g = static_cast<const bf16_t*>(G);
   const bf16_t* x = static_cast<const bf16_t*>(A);
   if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
@@ -817,7 +826,7 @@ hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, fl
   KDL_CHECK_HIP(hipGetLastError());
   const int64_t nk = static_cast<int64_t>(N) * K;
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, static_cast<int>(grid.x), scale,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, nsplit, scale,
                      static_cast<bf16_t*>(dW));
   return hipGetLastError();
 }
