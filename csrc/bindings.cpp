@@ -301,6 +301,17 @@ void pack_grads(const at::Tensor& chunks, const at::Tensor& src_ptrs, at::Tensor
             "pack_tensors");
 }
 
+void transpose_tiles(const at::Tensor& table) {
+  static_assert(sizeof(kdl::TransposeTile) == 32, "TransposeTile layout");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 4 &&
+                  table.is_contiguous(),
+              "transpose_tiles: table must be a contiguous int64 [n, 4] GPU tensor (src, dst, rows|cols<<32, r0|c0<<32)");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  check_hip(kdl::transpose_tiles(reinterpret_cast<const kdl::TransposeTile*>(table.data_ptr<int64_t>()),
+                                 static_cast<int>(table.size(0)), cur_stream()),
+            "transpose_tiles");
+}
+
 // ------------------------------------------------------------------ GBDT
 void gbdt_hist(const at::Tensor& bins, const at::Tensor& grad, const at::Tensor& hess, int64_t gh_stride,
                const at::Tensor& rows, const at::Tensor& seg, int64_t max_rows_per_node, int64_t num_bins,
@@ -744,6 +755,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights");
   m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");
   m.def("cast_copy", &cast_copy, "flat dtype-casting copy");
+  m.def("transpose_tiles", &transpose_tiles, "batched bf16 2-D transposes from a static 64x64 tile table");
   m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");

@@ -101,6 +101,14 @@ struct PackChunk {
   int64_t src_off; // element offset inside the source tensor
   int64_t dst_off; // element offset inside the flat destination
 };
+// One 64x64 tile of a batched bf16 transpose dst[cols][rows] = src[rows][cols].
+struct TransposeTile {
+  const uint16_t* src;
+  uint16_t* dst;
+  int rows, cols;
+  int r0, c0;
+};
+hipError_t transpose_tiles(const TransposeTile* tiles, int ntiles, hipStream_t s);
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
                         int dtype, float scale, hipStream_t s);
 

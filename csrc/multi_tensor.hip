@@ -68,7 +68,41 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackChunk* __restrict__
   }
 }
 
+// Batched transpose: dst[c][r] = src[r][c] for a static list of 64x64 tiles
+// (the 1x1 conv weights W[Cout][Cin] -> W^T[Cin][Cout] that the data-gradient
+// GEMMs read as their B operand).  One launch per step replaces one
+// ``.t().contiguous()`` copy kernel per conv.
+__global__ __launch_bounds__(256) void transpose_tiles_kernel(const TransposeTile* __restrict__ tiles) {
+  __shared__ bf16_t sh[64][64 + 2];
+  const TransposeTile tt = tiles[blockIdx.x];
+  const int t = threadIdx.x;
+  const int lr = t >> 2, lc = (t & 3) * 16;  // 64 rows x 4 threads x 16 elements
+  {
+    const int r = tt.r0 + lr;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = tt.c0 + lc + j;
+      sh[lr][lc + j] = (r < tt.rows && c < tt.cols) ? tt.src[static_cast<int64_t>(r) * tt.cols + c] : bf16_t(0);
+    }
+  }
+  __syncthreads();
+  const int c = tt.c0 + lr;  // destination row = source column
+  if (c < tt.cols) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = tt.r0 + lc + j;
+      if (r < tt.rows) tt.dst[static_cast<int64_t>(c) * tt.rows + r] = sh[lc + j][lr];
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t transpose_tiles(const TransposeTile* tiles, int ntiles, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(transpose_tiles_kernel, dim3(ntiles), dim3(256), 0, s, tiles);
+  return hipGetLastError();
+}
 
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
                         int dtype, float scale, hipStream_t s) {

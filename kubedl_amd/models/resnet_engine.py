@@ -419,6 +419,32 @@ class ResNetEngine:
                 self.bn[m] = st
         self.blocks = [b for b in model.layers if isinstance(b, Bottleneck)]
         assert len(self.blocks) == len(model.layers), "engine supports Bottleneck stacks only"
+        self._wt_ptrs = None
+        self._wt_buf = {}
+
+    def _refresh_wt(self) -> None:
+        """HIP path: W^T of every 1x1 conv (the data-gradient GEMMs' B operand) in
+        ONE batched-transpose launch per step (csrc/multi_tensor.hip), instead of
+        a ``.t().contiguous()`` copy kernel per conv.  The tile table is static
+        while the parameter storage is."""
+        if self.K.name != "hip":
+            return
+        convs = [c for b in self.blocks for c in (b.conv1, b.conv3, b.down_conv) if c is not None]
+        ptrs = tuple(c.weight.data_ptr() for c in convs)
+        if ptrs != self._wt_ptrs:
+            rows = []
+            self._wt_buf = {}
+            for c in convs:
+                w = c.weight.view(c.out_channels, -1)
+                co, ci = w.shape
+                wt = torch.empty(ci, co, dtype=w.dtype, device=w.device)
+                self._wt_buf[c] = wt
+                for r0 in range(0, co, 64):
+                    for c0 in range(0, ci, 64):
+                        rows.append((w.data_ptr(), wt.data_ptr(), co | (ci << 32), r0 | (c0 << 32)))
+            self._wt_table = torch.tensor(rows, dtype=torch.int64).to(self.dev)
+            self._wt_ptrs = ptrs
+        self.K.ext.transpose_tiles(self._wt_table)
 
     @staticmethod
     def _own_grad(prm):
@@ -487,6 +513,9 @@ class ResNetEngine:
         return loss.detach()
 
     def _wt(self, conv):
+        wt = self._wt_buf.get(conv)
+        if wt is not None:
+            return wt
         return conv.weight.view(conv.out_channels, -1).t().contiguous()
 
     def _bn_grads(self, st):
@@ -499,6 +528,7 @@ class ResNetEngine:
     @torch.no_grad()
     def backward(self, dfeat: torch.Tensor, hw: int) -> None:
         K, m = self.K, self.model
+        self._refresh_wt()
         x, c0, idx, saved, last = self._saved
         nb = len(self.blocks)
         # gradient at the last block's pre-ReLU sum, plus its bn3 sums
