@@ -44,7 +44,10 @@ def init_from_env(device: str | None = None, timeout_s: float = 600.0) -> DistIn
         ndev = torch.cuda.device_count()
         dev = torch.device("cuda", local_rank % max(ndev, 1))
         torch.cuda.set_device(dev)
-        backend = "nccl"
+        # KDL_DIST_BACKEND=gloo: rehearse a multi-rank job on fewer GPUs than
+        # ranks (gloo moves CUDA tensors through host memory; RCCL would
+        # refuse two ranks on one device)
+        backend = os.environ.get("KDL_DIST_BACKEND", "nccl")
     else:
         dev = torch.device("cpu")
         backend = "gloo"
