@@ -48,6 +48,8 @@ from kubedl_amd.store import NORMAL, WARNING, AlreadyExists, EventRecorder, NotF
 
 log = logging.getLogger("kubedl_amd.engine")
 
+from kubedl_amd.utils.log import logger_for_job, logger_for_replica  # noqa: E402
+
 # event reasons (pkg/job_controller/pod_control.go, service_control.go, pod.go)
 from kubedl_amd.engine.control import (FAILED_CREATE_POD, FAILED_CREATE_SERVICE, FAILED_DELETE_POD,  # noqa: F401,E402
                                        SUCCESSFUL_CREATE_POD, SUCCESSFUL_CREATE_SERVICE,
@@ -436,6 +438,7 @@ class JobController:
     def reconcile_pods(self, job: dict, job_status: dict, pods: List[dict], rtype: str, spec: dict,
                        replicas: Dict[str, dict], restart: List[bool]) -> None:
         rt = rtype.lower()
+        rlog = logger_for_replica(job, rt, log)
         pods = self.filter_for_replica_type(pods, rt)
         num = c.replicas_of(spec)
         # initializeReplicaStatuses: reset this type's counts every pass
@@ -443,7 +446,7 @@ class JobController:
         rs = job_status["replicaStatuses"][rtype]
         for index, sl in enumerate(self.get_slices(pods, num)):
             if len(sl) > 1:
-                log.warning("too many pods for %s %d", rt, index)
+                rlog.warning("too many pods for %s %d", rt, index)
             elif len(sl) == 0:
                 master = self.controller.is_master_role(replicas, rtype, index)
                 try:
@@ -466,7 +469,7 @@ class JobController:
                         break
                 if spec.get("restartPolicy") == c.RESTART_POLICY_EXIT_CODE:
                     if pod_phase(pod) == "Failed" and c.is_retryable_exit_code(exit_code):
-                        log.info("need to restart pod %s", pod["metadata"]["name"])
+                        rlog.info("need to restart pod %s", pod["metadata"]["name"])
                         self.delete_pod(job, pod)
                         restart[0] = True
                 phase = pod_phase(pod)
@@ -495,7 +498,7 @@ class JobController:
         pspec = tmpl.setdefault("spec", {})
         if pspec.get("restartPolicy"):
             msg = "Restart policy in pod template will be overwritten by restart policy in replica spec"
-            log.warning(msg)
+            logger_for_job(job, log).warning(msg)
             self.recorder.event(job, WARNING, POD_TEMPLATE_RESTART_POLICY, msg)
         # setRestartPolicy: ExitCode is implemented by the controller => pod Never
         rp = spec.get("restartPolicy", "")
