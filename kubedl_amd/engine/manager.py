@@ -27,6 +27,8 @@ from kubedl_amd.gang import interface as gang_iface
 from kubedl_amd.gang.allocator import GPUAllocator, GPUInventory, detect_gpus
 from kubedl_amd.metrics.job_metrics import MetricsRegistry
 from kubedl_amd.store import ADDED, DELETED, MODIFIED, EventRecorder, Store
+from kubedl_amd.utils.log import logger_for_key
+from kubedl_amd.utils.trace import trace_range
 
 log = logging.getLogger("kubedl_amd.manager")
 
@@ -69,14 +71,15 @@ class _KindLoop:
                 continue
             ns, name = key.split("/", 1)
             try:
-                res = self.r.reconcile(ns, name)
+                with trace_range(f"reconcile {self.r.kind} {key}"):
+                    res = self.r.reconcile(ns, name)
                 self.queue.forget(key)
                 if res.requeue_after > 0:
                     self.queue.add_after(key, res.requeue_after)
                 elif res.requeue:
                     self.queue.add_rate_limited(key)
             except Exception as e:  # reconcile error -> rate-limited retry (controller-runtime)
-                log.warning("reconcile %s %s failed: %s", self.r.kind, key, e)
+                logger_for_key(key, log).warning("reconcile %s failed: %s", self.r.kind, e)
                 self.errors.append(f"{key}: {e}")
                 self.queue.add_rate_limited(key)
             finally:

@@ -23,6 +23,8 @@ from kubedl_amd.models.resnet import resnet50, resnet_tiny
 from kubedl_amd.ops.optim import FlatParamSpace, FusedSGD
 from kubedl_amd.parallel import dist as kdist
 from kubedl_amd.parallel.ddp import FlatDDP
+from kubedl_amd.utils.checkpoint import Checkpointer
+from kubedl_amd.utils.trace import StepLog, trace_range
 from kubedl_amd.workers import common
 
 
@@ -76,17 +78,39 @@ class ResNetTrainer:
 
     def step(self) -> torch.Tensor:
         self.space.zero_grad()
-        if self.engine is not None:
-            loss = self.engine.forward_backward(self.x, self.y)
-            self.space.mark_packed()  # gradients were written into the flat buffer
-        else:
-            out = self.model(self.x)
-            loss = F.cross_entropy(out.float(), self.y)
-            loss.backward()
-        self.ddp.finish()
-        self.opt.step()
+        with trace_range("forward_backward"):
+            if self.engine is not None:
+                loss = self.engine.forward_backward(self.x, self.y)
+                self.space.mark_packed()  # gradients were written into the flat buffer
+            else:
+                out = self.model(self.x)
+                loss = F.cross_entropy(out.float(), self.y)
+                loss.backward()
+        with trace_range("allreduce_wait"):
+            self.ddp.finish()
+        with trace_range("optimizer"):
+            self.opt.step()
         self.last_loss = loss.detach()
         return self.last_loss
+
+    # ------------------------------------------------------------ checkpoint
+    def state_dict(self) -> dict:
+        """Everything a restarted rank needs to continue bit-exactly: bf16 params,
+        fp32 master weights, momentum, step count, BN running statistics."""
+        st = {"param": self.space.param, "master": self.space.master, "momentum": self.opt.mom,
+              "opt_steps": int(self.opt.step_count)}
+        for name, buf in self.model.named_buffers():
+            st["buf." + name] = buf
+        return st
+
+    @torch.no_grad()
+    def load_state_dict(self, st: dict) -> None:
+        self.space.param.copy_(st["param"])
+        self.space.master.copy_(st["master"])
+        self.opt.mom.copy_(st["momentum"])
+        self.opt.step_count = int(st["opt_steps"])
+        for name, buf in self.model.named_buffers():
+            buf.copy_(st["buf." + name])
 
 
 def sync(info: kdist.DistInfo) -> None:
@@ -100,30 +124,51 @@ def run(args) -> dict:
     common.signal_ready({"rank": info.rank})
     tr = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
                        bn_backend=args.bn_backend, engine=args.engine)
-    for i in range(args.warmup):
+    ckpt = Checkpointer.from_env(info.rank)
+    steplog = StepLog(rank=info.rank)
+    done = 0  # optimizer steps completed by this job (across restarts)
+    resumed = ckpt.load_latest(map_location=info.device)
+    if resumed is not None:
+        done, st = resumed
+        tr.load_state_dict(st)
+    total = args.warmup + args.steps
+
+    def one(i):
+        t = time.perf_counter()
         tr.step()
+        if steplog.enabled:
+            sync(info)
+            steplog.write(i + 1, (time.perf_counter() - t) * 1e3, loss=float(tr.last_loss.float().item()))
+        if ckpt.due(i + 1):
+            ckpt.save(i + 1, tr.state_dict())
         common.maybe_inject_fault(info.rank, i)
+
+    for i in range(done, args.warmup):
+        one(i)
     sync(info)
     kdist.barrier(info)
     sync(info)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        tr.step()
-        common.maybe_inject_fault(info.rank, args.warmup + i)
+    timed = range(max(done, args.warmup), total)
+    for i in timed:
+        one(i)
     sync(info)
     kdist.barrier(info)
     sync(info)
     dt = time.perf_counter() - t0
     dt = kdist.all_reduce_max(dt, info)
+    nsteps = len(timed)
     loss = float(tr.last_loss.item()) if tr.last_loss is not None else float("nan")
     res = {
-        "rank": info.rank, "world_size": info.world_size, "steps": args.steps,
-        "seconds": dt, "ms_per_step": dt / max(args.steps, 1) * 1e3,
-        "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
-        "images_per_sec": args.steps * args.batch * info.world_size / dt if dt > 0 else 0.0,
-        "loss": loss, "startup_s": t0 - t_start if False else None,
+        "rank": info.rank, "world_size": info.world_size, "steps": nsteps,
+        "seconds": dt, "ms_per_step": dt / max(nsteps, 1) * 1e3,
+        "steps_per_sec": nsteps / dt if dt > 0 else 0.0,
+        "images_per_sec": nsteps * args.batch * info.world_size / dt if dt > 0 else 0.0,
+        "loss": loss, "startup_s": t0 - t_start, "resumed_from_step": done if resumed is not None else None,
+        "total_steps": total,
     }
-    common.report_progress(args.warmup + args.steps, res["steps_per_sec"], loss=loss)
+    steplog.close()
+    common.report_progress(total, res["steps_per_sec"], loss=loss)
     kdist.shutdown(info)
     return res
 
