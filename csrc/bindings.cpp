@@ -302,10 +302,11 @@ void pack_grads(const at::Tensor& chunks, const at::Tensor& src_ptrs, at::Tensor
 }
 
 void transpose_tiles(const at::Tensor& table) {
-  static_assert(sizeof(kdl::TransposeTile) == 32, "TransposeTile layout");
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 4 &&
+  static_assert(sizeof(kdl::TransposeTile) == 40, "TransposeTile layout");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 5 &&
                   table.is_contiguous(),
-              "transpose_tiles: table must be a contiguous int64 [n, 4] GPU tensor (src, dst, rows|cols<<32, r0|c0<<32)");
+              "transpose_tiles: table must be a contiguous int64 [n, 5] GPU tensor "
+              "(src, dst, rows|cols<<32, r0|c0<<32, src_ld|dst_ld<<32)");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   check_hip(kdl::transpose_tiles(reinterpret_cast<const kdl::TransposeTile*>(table.data_ptr<int64_t>()),
                                  static_cast<int>(table.size(0)), cur_stream()),
@@ -555,6 +556,46 @@ int64_t conv1x1_wgrad_splits(int64_t M, int64_t N, int64_t K) {
   return kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
 }
 
+// 3x3 / pad 1 convolution as an implicit GEMM on the same MFMA kernel:
+// y[Nb, Ho, Wo, Cout] = conv(pro(x)[Nb, H, W, Cin], W[Cout][3][3][Cin]).
+//   epi 0 PLAIN, 1 STATS (shift = rm, acc = fwd replicas), 2 MASKX (dgrad:
+//   ex = that BN's input [M, Cout], emean, ecoef).  pro_coef [2Cin] applies
+//   relu(x*scale + shift) to in-image taps; padding taps are zero.
+void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_t Nb, int64_t H, int64_t Wd,
+                  int64_t Cin, int64_t Cout, int64_t stride, const c10::optional<at::Tensor>& pro_coef, int64_t epi,
+                  const c10::optional<at::Tensor>& shift, const c10::optional<at::Tensor>& acc,
+                  const c10::optional<at::Tensor>& ex, const c10::optional<at::Tensor>& emean,
+                  const c10::optional<at::Tensor>& ecoef) {
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && Nb > 0 && stride >= 1, "conv3x3_gemm: need Cin, Cout % 64 == 0");
+  TORCH_CHECK(epi == 0 || epi == 1 || epi == 2, "conv3x3_gemm: epilogue must be PLAIN, STATS or MASKX");
+  TORCH_CHECK(!(epi == 2 && opt_ptr(pro_coef)), "conv3x3_gemm: MASKX runs without a prologue");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (Wd - 1) / stride + 1;
+  const int64_t M = Nb * Ho * Wo, K = 9 * Cin, N = Cout;
+  need_bf16(A, Nb * H * Wd * Cin, "conv3x3_gemm A");
+  need_bf16(W, N * K, "conv3x3_gemm W");
+  need_bf16(C, M * N, "conv3x3_gemm C");
+  need_opt_f32(pro_coef, 2 * Cin, "pro_coef");
+  const int64_t rep = 32 * 2 * N;
+  if (epi == 1) { TORCH_CHECK(opt_ptr(shift) && opt_ptr(acc), "epi STATS needs shift, acc"); need_opt_f32(shift, N, "shift"); need_opt_f32(acc, rep, "acc"); }
+  if (epi == 2) {
+    TORCH_CHECK(opt_ptr(ex) && opt_ptr(emean) && opt_ptr(ecoef) && opt_ptr(acc), "epi MASKX needs ex, emean, ecoef, acc");
+    need_opt_bf16(ex, M * N, "ex"); need_opt_f32(emean, N, "emean"); need_opt_f32(ecoef, 2 * N, "ecoef"); need_opt_f32(acc, rep, "acc");
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  kdl::Conv1x1Args a{};
+  a.A = A.data_ptr(); a.B = W.data_ptr(); a.C = C.data_ptr();
+  a.M = static_cast<int>(M); a.N = static_cast<int>(N); a.K = static_cast<int>(K);
+  a.Hout = static_cast<int>(Ho); a.Wout = static_cast<int>(Wo); a.Hin = static_cast<int>(H);
+  a.Win = static_cast<int>(Wd); a.stride = static_cast<int>(stride);
+  a.ksize = 3; a.Cin = static_cast<int>(Cin);
+  a.pro_coef = opt_fptr(pro_coef);
+  a.epi = static_cast<int>(epi);
+  a.shift = opt_fptr(shift); a.acc = opt_fptr(acc);
+  a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
+  a.res_stride = 1;
+  check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv3x3_gemm");
+}
+
 void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
                    at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t M, int64_t N, int64_t K,
                    int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride) {
@@ -577,6 +618,30 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
                                static_cast<int>(Wout), static_cast<int>(Hin), static_cast<int>(Win),
                                static_cast<int>(stride), cur_stream()),
             "conv1x1_wgrad");
+}
+
+void conv3x3_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
+                   at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t Nb, int64_t H,
+                   int64_t Wd, int64_t Cin, int64_t Cout, int64_t stride) {
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && Nb > 0 && stride >= 1, "conv3x3_wgrad: need Cin, Cout % 64 == 0");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (Wd - 1) / stride + 1, M = Nb * Ho * Wo, K = 9 * Cin;
+  need_bf16(G, M * Cout, "conv3x3_wgrad G");
+  need_bf16(A, Nb * H * Wd * Cin, "conv3x3_wgrad A");
+  need_opt_f32(pro_coef, 2 * Cin, "pro_coef");
+  const int64_t slabs = kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(Cout), static_cast<int>(K));
+  TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
+                  dw32.numel() >= slabs * Cout * K,
+              "conv3x3_wgrad: dw32 must hold conv1x1_wgrad_splits(M, Cout, 9 Cin) * Cout * 9 Cin fp32");
+  if (dW.has_value() && dW->defined()) {
+    need_bf16(*dW, Cout * K, "conv3x3_wgrad dW");  // OHWI: channels_last [Cout, Cin, 3, 3] or [Cout, 9 Cin]
+    TORCH_CHECK(dW->numel() == Cout * K, "conv3x3_wgrad: dW must have Cout * 9 * Cin elements");
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(G.device());
+  check_hip(kdl::conv3x3_wgrad(G.data_ptr(), A.data_ptr(), opt_fptr(pro_coef), dw32.data_ptr<float>(),
+                               dW.has_value() && dW->defined() ? dW->data_ptr() : nullptr, static_cast<float>(scale),
+                               static_cast<int>(Nb), static_cast<int>(H), static_cast<int>(Wd), static_cast<int>(Cin),
+                               static_cast<int>(Cout), static_cast<int>(stride), cur_stream()),
+            "conv3x3_wgrad");
 }
 
 int64_t pdtype_of(const at::Tensor& t) { return t.scalar_type() == at::kBFloat16 ? 1 : 0; }
@@ -766,7 +831,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
+  m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
+  m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 pad-1 conv weight gradient (implicit GEMM, split-M slabs)");
   m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad");
   m.def("bn_coef_offset", &bn_coef_offset, "float offset of the coefficient block in a BN workspace");
   m.def("bn_stage_fwd_stats", &bn_stage_fwd_stats, "BN forward statistics into the workspace replicas");

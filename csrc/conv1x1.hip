@@ -68,6 +68,8 @@ constexpr int LDK = BK + 8;  // padded LDS row (bf16)
 constexpr int kRep = 32;     // replica count of the BN workspace (== bn_act.hip kReplicas)
 
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
+// A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s)
+enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2 };
 
 struct GemmParams {
   const bf16_t* A;
@@ -76,7 +78,8 @@ struct GemmParams {
   int M, N, K;
   // A row gather (stride-s 1x1 conv): out row (n, oh, ow) reads in row (n, oh*s, ow*s)
   int Hout, Wout, Hin, Win, stride;
-  const float* pro_coef;  // [2K]: scale | shift
+  int Cin;                // GATHER == G_CONV3: channels per tap (K = 9 * Cin, Cin % 64 == 0)
+  const float* pro_coef;  // [2K] (3x3: [2Cin]): scale | shift
   // epilogue operands
   const float* shift;   // STATS: [N]
   float* acc;           // STATS/MASKX/RESBITS: [kRep][2N]
@@ -127,7 +130,7 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BM, int BN, int MINB, bool PRO, bool GATHER, int EPI>
+template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
   // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
   // [BM][BN + 8] output tile and finally as the reduction scratch.
@@ -166,6 +169,12 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     a_kc[i] = (c & 7) * 8;
   }
   int64_t a_off[A_CH];
+  // 3x3 implicit GEMM: per A chunk the image base row and the top-left input
+  // coordinate of its output pixel; ``ra_ok`` = chunks whose tap is inside the
+  // image for the K-step held in ``ra`` (padding taps stage as zeros)
+  int a_base[A_CH], a_ih[A_CH], a_iw[A_CH];
+  uint32_t ra_ok = 0;
+  (void)a_base; (void)a_ih; (void)a_iw; (void)ra_ok;
   uint4 ra[A_CH], rb[B_CH];
   // all A chunks of a thread share one 8-channel k-chunk ((t + i*256) & 7 == t & 7)
   float psc[8], psf[8];
@@ -177,28 +186,52 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       const int m0 = tm * BM + a_row[i];
       const int m = m0 < M ? m0 : 0;  // tail rows re-read row 0 (never stored): no divergent loads
       int64_t src = m;
-      if constexpr (GATHER) {
+      if constexpr (GATHER != G_DENSE) {
         const int hw = p.Hout * p.Wout;
         const int nimg = m / hw, rem = m - nimg * hw;
         const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
-        src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
+        if constexpr (GATHER == G_STRIDED) {
+          src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
+        } else {
+          a_base[i] = nimg * p.Hin * p.Win;
+          a_ih[i] = oh * p.stride - 1;
+          a_iw[i] = ow * p.stride - 1;
+        }
       }
       a_off[i] = src * K;
     }
   };
   auto gload = [&](int kt) {
     const int k0 = kt * BK;
+    int kc0 = k0;  // channel offset of this K-step within a tap
+    if constexpr (GATHER == G_CONV3) {
+      const int tap = k0 / p.Cin;  // BK divides Cin: a K-step never straddles taps
+      kc0 = k0 - tap * p.Cin;
+      const int r = tap / 3, q = tap - 3 * (tap / 3);
+      ra_ok = 0;
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i)
-      ra[i] = ld16(p.A + a_off[i] + k0 + a_kc[i]);  // rows >= M read row 0: their outputs are never stored
+      for (int i = 0; i < A_CH; ++i) {
+        const int ih = a_ih[i] + r, iw = a_iw[i] + q;
+        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(p.Hin) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win);
+        const int row = ok ? a_base[i] + ih * p.Win + iw : 0;
+        ra_ok |= ok ? (1u << i) : 0u;
+        ra[i] = ld16(p.A + static_cast<int64_t>(row) * p.Cin + kc0 + a_kc[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i)
+        ra[i] = ld16(p.A + a_off[i] + k0 + a_kc[i]);  // rows >= M read row 0: their outputs are never stored
+    }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int c = t + i * kThreads;
       rb[i] = ld16(p.B + static_cast<int64_t>(n0 + (c >> 3)) * K + k0 + (c & 7) * 8);
     }
     if constexpr (PRO) {
-      const float4* sp = reinterpret_cast<const float4*>(p.pro_coef + k0 + a_kc[0]);
-      const float4* fp = reinterpret_cast<const float4*>(p.pro_coef + K + k0 + a_kc[0]);
+      const int kcoef = GATHER == G_CONV3 ? p.Cin : K;
+      const float4* sp = reinterpret_cast<const float4*>(p.pro_coef + kc0 + a_kc[0]);
+      const float4* fp = reinterpret_cast<const float4*>(p.pro_coef + kcoef + kc0 + a_kc[0]);
       const float4 s0 = sp[0], s1 = sp[1], f0 = fp[0], f1 = fp[1];
       psc[0] = s0.x; psc[1] = s0.y; psc[2] = s0.z; psc[3] = s0.w;
       psc[4] = s1.x; psc[5] = s1.y; psc[6] = s1.z; psc[7] = s1.w;
@@ -221,6 +254,9 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           f[j] = o > 0.f ? o : 0.f;
         }
         v = pack8(f);
+      }
+      if constexpr (GATHER == G_CONV3) {
+        if (!((ra_ok >> i) & 1u)) v = make_uint4(0, 0, 0, 0);  // zero padding (after BN+ReLU)
       }
       *reinterpret_cast<uint4*>(&As[a_row[i] * LDK + a_kc[i]]) = v;
     }
@@ -518,11 +554,11 @@ __device__ __forceinline__ void transpose8x8(const uint4 (&in)[8], uint4 (&out)[
   }
 }
 
-template <int TN_, int TK_, bool PRO, bool GATHER>
+template <int TN_, int TK_, bool PRO, int GATHER>
 __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
     const bf16_t* __restrict__ G, const bf16_t* __restrict__ A, const float* __restrict__ pro_coef,
     float* __restrict__ dw32, int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride,
-    int rows_per_split, int tiles_k) {
+    int rows_per_split, int tiles_k, int cin) {
   // [2 buffers][G^T tile TN_ x LDW | A^T tile TK_ x LDW]
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (TN_ + TK_) * LDW];
   constexpr int kBuf = (TN_ + TK_) * LDW;
@@ -549,17 +585,24 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
   const int cpr = (isA ? TK_ : TN_) / 8;
   const int mg = u / cpr;         // 0..7: rows mg*8 .. +7 of the M-step
   const int cc = (u % cpr) * 8;   // channel chunk within the tile
-  const int col0 = (isA ? k0 : n0) + cc;
-  const int ld = isA ? K : N;
+  // 3x3 weight gradient: K = 9 * cin, this tile's K range lies in one tap (TK_ | cin)
+  const int tap = GATHER == G_CONV3 ? k0 / cin : 0;
+  const int kin0 = k0 - tap * cin;
+  const int tr3 = tap / 3, tq3 = tap - 3 * (tap / 3);
+  const int col0 = (isA ? (GATHER == G_CONV3 ? kin0 : k0) : n0) + cc;
+  const int ld = isA ? (GATHER == G_CONV3 ? cin : K) : N;
+  const int kcoef = GATHER == G_CONV3 ? cin : K;
   const bf16_t* base = isA ? A : G;
   float psc[8], psf[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { psc[j] = 1.f; psf[j] = 0.f; }
   if (PRO && isA && stager) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { psc[j] = pro_coef[col0 + j]; psf[j] = pro_coef[K + col0 + j]; }
+    for (int j = 0; j < 8; ++j) { psc[j] = pro_coef[col0 + j]; psf[j] = pro_coef[kcoef + col0 + j]; }
   }
   uint4 rr[8];
+  uint32_t rok = 0xffu;  // 3x3: rows of the staged set whose tap lies inside the image
+  (void)tr3; (void)tq3;
   // Loads are unconditional (tail rows clamp to row mbeg) so that no load sits
   // behind an exec branch; the tail rows are zeroed when staged to LDS.
   auto gload = [&](int m0) {
@@ -569,11 +612,19 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
       const int m1 = m0 + mg * 8 + r;
       const int m = m1 < mend ? m1 : mbeg;
       int64_t src = m;
-      if (GATHER && isA) {
+      if (GATHER != G_DENSE && isA) {
         const int hw = Hout * Wout;
         const int nimg = m / hw, rem = m - nimg * hw;
         const int oh = rem / Wout, ow = rem - oh * Wout;
-        src = (static_cast<int64_t>(nimg) * Hin + oh * stride) * Win + ow * stride;
+        if (GATHER == G_STRIDED) {
+          src = (static_cast<int64_t>(nimg) * Hin + oh * stride) * Win + ow * stride;
+        } else {
+          const int ih = oh * stride + tr3 - 1, iw = ow * stride + tq3 - 1;
+          const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(Hin) &&
+                          static_cast<unsigned>(iw) < static_cast<unsigned>(Win);
+          src = ok ? (static_cast<int64_t>(nimg) * Hin + ih) * Win + iw : 0;
+          rok = ok ? (rok | (1u << r)) : (rok & ~(1u << r));
+        }
       }
       rr[r] = ld16(base + src * ld + col0);
     }
@@ -582,7 +633,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
     if (!stager) return;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const bool ok = m0 + mg * 8 + r < mend;  // padding rows stage as zero
+      const bool ok = m0 + mg * 8 + r < mend && ((rok >> r) & 1u);  // tail rows / padding taps stage as zero
       if (PRO && isA) {
         float f[8];
         unpack8(rr[r], f);
@@ -694,7 +745,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restric
   }
 }
 
-template <int BM, int BN, int MINB, bool PRO, bool GATHER, int EPI>
+template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI>
 hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = p.N / BN;
@@ -709,27 +760,32 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
 }
 
 // forward convs (prologue / row gather) only ever use the PLAIN and STATS
-// epilogues; the dgrad epilogues run without either
-template <int BM, int BN, int MINB, bool PRO, bool GATHER>
+// epilogues; the dgrad epilogues run without either (3x3 dgrad: MASKX)
+template <int BM, int BN, int MINB, bool PRO, int GATHER>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   switch (epi) {
     case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN>(p, s);
     case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS>(p, s);
   }
-  if constexpr (!PRO && !GATHER) {
+  if constexpr (!PRO && GATHER == G_DENSE) {
     switch (epi) {
       case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX>(p, s);
       case EPI_RESBITS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS>(p, s);
       case EPI_RES: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RES>(p, s);
     }
   }
+  if constexpr (!PRO && GATHER == G_CONV3) {
+    if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX>(p, s);
+  }
   return hipErrorInvalidValue;
 }
 
 template <int BM, int BN, int MINB>
-hipError_t dispatch_pg(const GemmParams& p, int epi, bool pro, bool gather, hipStream_t s) {
-  if (pro) return gather ? dispatch_epi<BM, BN, MINB, true, true>(p, epi, s) : dispatch_epi<BM, BN, MINB, true, false>(p, epi, s);
-  return gather ? dispatch_epi<BM, BN, MINB, false, true>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, false>(p, epi, s);
+hipError_t dispatch_pg(const GemmParams& p, int epi, bool pro, int gather, hipStream_t s) {
+  if (gather == G_CONV3)
+    return pro ? dispatch_epi<BM, BN, MINB, true, G_CONV3>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_CONV3>(p, epi, s);
+  if (pro) return gather ? dispatch_epi<BM, BN, MINB, true, G_STRIDED>(p, epi, s) : dispatch_epi<BM, BN, MINB, true, G_DENSE>(p, epi, s);
+  return gather ? dispatch_epi<BM, BN, MINB, false, G_STRIDED>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_DENSE>(p, epi, s);
 }
 
 // Tile configs: 0 = 128x128 (2 blocks/CU), 1 = 128x64, 2 = 64x128, 3 = 64x64 (4 blocks/CU).
@@ -762,7 +818,19 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.res_H = a.res_H; p.res_W = a.res_W;
   p.ebits = a.ebits; p.ex2 = static_cast<const bf16_t*>(a.ex2); p.emean2 = a.emean2; p.acc2 = a.acc2;
   const bool pro = a.pro_coef != nullptr;
-  const bool gather = a.stride > 1;
+  int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
+  p.Cin = a.K;
+  if (a.ksize == 3) {
+    // 3x3, pad 1: K = 9 * Cin, B = weight [N][3][3][Cin] (OHWI = channels_last OIHW)
+    if (a.Cin <= 0 || a.Cin % BK || a.K != 9 * a.Cin || a.stride < 1 ||
+        a.Hout != (a.Hin - 1) / a.stride + 1 || a.Wout != (a.Win - 1) / a.stride + 1 ||
+        a.M % (a.Hout * a.Wout))
+      return hipErrorInvalidValue;
+    gather = G_CONV3;
+    p.Cin = a.Cin;
+  } else if (a.ksize != 1 && a.ksize != 0) {
+    return hipErrorInvalidValue;
+  }
   const int epi = a.epi;
   if (epi == EPI_RES || epi == EPI_RESBITS) {
     if (!p.eres) return hipErrorInvalidValue;
@@ -787,28 +855,28 @@ int conv1x1_wgrad_splits(int M, int N, int K) {
 namespace {
 template <int TN_, int TK_>
 void launch_wgrad(dim3 grid, hipStream_t s, const bf16_t* g, const bf16_t* x, const float* pro, float* dw32, int M,
-                  int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int rps, int tiles_k) {
-  const bool gather = stride > 1;
+                  int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int rps, int tiles_k, int mode,
+                  int cin) {
+#define KDL_WG(P, G)                                                                                             \
+  hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, P, G>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N, K, Hout, \
+                     Wout, Hin, Win, stride, rps, tiles_k, cin)
   if (pro) {
-    if (gather)
-      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, true, true>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N,
-                         K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
-    else
-      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, true, false>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N,
-                         K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+    if (mode == G_CONV3) KDL_WG(true, G_CONV3);
+    else if (mode == G_STRIDED) KDL_WG(true, G_STRIDED);
+    else KDL_WG(true, G_DENSE);
   } else {
-    if (gather)
-      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, false, true>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N,
-                         K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
-    else
-      hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, false, false>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M,
-                         N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+    if (mode == G_CONV3) KDL_WG(false, G_CONV3);
+    else if (mode == G_STRIDED) KDL_WG(false, G_STRIDED);
+    else KDL_WG(false, G_DENSE);
   }
+#undef KDL_WG
 }
 }  // namespace
 
-hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
-                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s) {
+namespace {
+hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
+                      int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
+                      hipStream_t s) {
   if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
   const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
   const int splits = conv1x1_wgrad_splits(M, N, K);
@@ -819,16 +887,31 @@ hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, fl
   dim3 grid(nsplit * (N / tn) * tiles_k);
   const bf16_t* g = static_cast<const bf16_t*>(G);
   const bf16_t* x = static_cast<const bf16_t*>(A);
-  if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
-  else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
-  else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
-  else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k);
+  if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+  else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+  else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+  else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
   KDL_CHECK_HIP(hipGetLastError());
   const int64_t nk = static_cast<int64_t>(N) * K;
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, nsplit, scale,
                      static_cast<bf16_t*>(dW));
   return hipGetLastError();
+}
+}  // namespace
+
+hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
+                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s) {
+  return wgrad_impl(G, A, pro_coef, dw32, dW, scale, M, N, K, Hout, Wout, Hin, Win, stride,
+                    stride > 1 ? G_STRIDED : G_DENSE, K, s);
+}
+
+hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
+                         int Nb, int Hin, int Win, int Cin, int Cout, int stride, hipStream_t s) {
+  if (Cin % 64 || Cout % 64 || Nb <= 0 || stride < 1) return hipErrorInvalidValue;
+  const int Ho = (Hin - 1) / stride + 1, Wo = (Win - 1) / stride + 1;
+  return wgrad_impl(G, A, pro_coef, dw32, dW, scale, Nb * Ho * Wo, Cout, 9 * Cin, Ho, Wo, Hin, Win, stride, G_CONV3,
+                    Cin, s);
 }
 
 }  // namespace kdl

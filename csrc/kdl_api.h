@@ -101,12 +101,14 @@ struct PackChunk {
   int64_t src_off; // element offset inside the source tensor
   int64_t dst_off; // element offset inside the flat destination
 };
-// One 64x64 tile of a batched bf16 transpose dst[cols][rows] = src[rows][cols].
+// One 64x64 tile of a batched bf16 transpose dst[c * dst_ld + r] = src[r * src_ld + c]
+// (r < rows, c < cols).
 struct TransposeTile {
   const uint16_t* src;
   uint16_t* dst;
   int rows, cols;
   int r0, c0;
+  int src_ld, dst_ld;
 };
 hipError_t transpose_tiles(const TransposeTile* tiles, int ntiles, hipStream_t s);
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
@@ -157,6 +159,8 @@ struct Conv1x1Args {
   const void* ex2;                   // epi 3: optional second BN input
   const float* emean2;
   float* acc2;
+  int ksize;                         // 1 (or 0): 1x1 conv / GEMM; 3: 3x3 pad-1 implicit GEMM (K = 9 * Cin)
+  int Cin;                           // ksize 3: input channels (the A row width)
 };
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 int conv1x1_wgrad_splits(int M, int N, int K);
@@ -165,6 +169,10 @@ int conv1x1_wgrad_splits(int M, int N, int K);
 // result goes to dW (bf16) if given, else as fp32 into the first [N, K] of dw32.
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s);
+// 3x3 / pad 1: dW[Cout][3][3][Cin] = sum_m G[m, :]^T pro(A)_tap(m); slabs as conv1x1_wgrad with
+// M = Nb * Ho * Wo, N = Cout, K = 9 * Cin.
+hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
+                         int Nb, int Hin, int Win, int Cin, int Cout, int stride, hipStream_t s);
 
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 

@@ -68,10 +68,11 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackChunk* __restrict__
   }
 }
 
-// Batched transpose: dst[c][r] = src[r][c] for a static list of 64x64 tiles
-// (the 1x1 conv weights W[Cout][Cin] -> W^T[Cin][Cout] that the data-gradient
-// GEMMs read as their B operand).  One launch per step replaces one
-// ``.t().contiguous()`` copy kernel per conv.
+// Batched transpose: dst[c * dst_ld + r] = src[r * src_ld + c] for a static list
+// of 64x64 tiles: the 1x1 conv weights W[Cout][Cin] -> W^T[Cin][Cout] and the
+// per-tap slices of the 3x3 weights W[Cout][3][3][Cin] -> Wd[Cin][3][3][Cout]
+// (taps reversed) that the data-gradient GEMMs read as their B operand.  One
+// launch per step replaces one ``.t().contiguous()`` copy kernel per conv.
 __global__ __launch_bounds__(256) void transpose_tiles_kernel(const TransposeTile* __restrict__ tiles) {
   __shared__ bf16_t sh[64][64 + 2];
   const TransposeTile tt = tiles[blockIdx.x];
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256) void transpose_tiles_kernel(const TransposeTil
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int c = tt.c0 + lc + j;
-      sh[lr][lc + j] = (r < tt.rows && c < tt.cols) ? tt.src[static_cast<int64_t>(r) * tt.cols + c] : bf16_t(0);
+      sh[lr][lc + j] = (r < tt.rows && c < tt.cols) ? tt.src[static_cast<int64_t>(r) * tt.src_ld + c] : bf16_t(0);
     }
   }
   __syncthreads();
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(256) void transpose_tiles_kernel(const TransposeTil
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int r = tt.r0 + lc + j;
-      if (r < tt.rows) tt.dst[static_cast<int64_t>(c) * tt.rows + r] = sh[lc + j][lr];
+      if (r < tt.rows) tt.dst[static_cast<int64_t>(c) * tt.dst_ld + r] = sh[lc + j][lr];
     }
   }
 }

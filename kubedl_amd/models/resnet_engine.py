@@ -202,6 +202,16 @@ class HipKernels:
                               st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
         return out
 
+    def dgrad3x3_maskx(self, g, wd, x1, st1):
+        """Stride-1 3x3 dgrad (implicit GEMM, B = wd [Cin][3][3][Cout]) with the
+        previous BN+ReLU's mask and backward sums fused into the epilogue."""
+        n, cout, h, w = g.shape
+        cin = wd.shape[0]
+        out = _nhwc_empty(n, cin, h, w, g)
+        self.ext.conv3x3_gemm(g, wd, out, n, h, w, cout, cin, 1, None, 2, None, self._bwd_acc(st1), x1,
+                              st1.save_mean, self.fcoef(st1))
+        return out
+
     def dgrad_plain(self, g, wt):
         n, cout, h, w = g.shape
         cin = wt.shape[0]
@@ -361,6 +371,14 @@ class TorchKernels:
         self._bsum(d, x2, st2)
         return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
 
+    def dgrad3x3_maskx(self, g, wd, x1, st1):
+        d = _bfr(F.conv2d(g.float(), wd.float(), padding=1))
+        sc, sf = st1.fcoef
+        mask = (x1.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
+        d = torch.where(mask, d, torch.zeros_like(d))
+        self._bsum(d, x1, st1)
+        return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
+
     def dgrad_plain(self, g, wt):
         return F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)).to(g.dtype).contiguous(
             memory_format=torch.channels_last)
@@ -423,14 +441,16 @@ class ResNetEngine:
         self._wt_buf = {}
 
     def _refresh_wt(self) -> None:
-        """HIP path: W^T of every 1x1 conv (the data-gradient GEMMs' B operand) in
-        ONE batched-transpose launch per step (csrc/multi_tensor.hip), instead of
-        a ``.t().contiguous()`` copy kernel per conv.  The tile table is static
-        while the parameter storage is."""
+        """HIP path: the data-gradient GEMMs' B operands -- W^T of every 1x1 conv
+        and the tap-reversed per-tap transpose Wd[Cin][3][3][Cout] of every
+        stride-1 3x3 conv -- in ONE batched-transpose launch per step
+        (csrc/multi_tensor.hip), instead of a copy kernel per conv.  The tile
+        table is static while the parameter storage is."""
         if self.K.name != "hip":
             return
         convs = [c for b in self.blocks for c in (b.conv1, b.conv3, b.down_conv) if c is not None]
-        ptrs = tuple(c.weight.data_ptr() for c in convs)
+        c3s = [b.conv2 for b in self.blocks if b.conv2.stride[0] == 1]
+        ptrs = tuple(c.weight.data_ptr() for c in convs + c3s)
         if ptrs != self._wt_ptrs:
             rows = []
             self._wt_buf = {}
@@ -441,10 +461,30 @@ class ResNetEngine:
                 self._wt_buf[c] = wt
                 for r0 in range(0, co, 64):
                     for c0 in range(0, ci, 64):
-                        rows.append((w.data_ptr(), wt.data_ptr(), co | (ci << 32), r0 | (c0 << 32)))
+                        rows.append((w.data_ptr(), wt.data_ptr(), co | (ci << 32), r0 | (c0 << 32), ci | (co << 32)))
+            for c in c3s:
+                w = c.weight  # [Cout, Cin, 3, 3] channels_last = OHWI in memory
+                co, ci = w.shape[:2]
+                assert w.is_contiguous(memory_format=torch.channels_last)
+                wd = torch.empty(ci, co, 3, 3, dtype=w.dtype, device=w.device).contiguous(
+                    memory_format=torch.channels_last)
+                self._wt_buf[c] = wd
+                esz = w.element_size()
+                for tap in range(9):
+                    for r0 in range(0, co, 64):
+                        for c0 in range(0, ci, 64):
+                            rows.append((w.data_ptr() + tap * ci * esz, wd.data_ptr() + (8 - tap) * co * esz,
+                                         co | (ci << 32), r0 | (c0 << 32), (9 * ci) | ((9 * co) << 32)))
             self._wt_table = torch.tensor(rows, dtype=torch.int64).to(self.dev)
             self._wt_ptrs = ptrs
         self.K.ext.transpose_tiles(self._wt_table)
+
+    def _wd(self, conv):
+        """Data-gradient weight of a stride-1 3x3 conv: flip(W, taps) with Cin/Cout swapped."""
+        wd = self._wt_buf.get(conv)
+        if wd is not None:
+            return wd
+        return conv.weight.flip(2, 3).transpose(0, 1)
 
     @staticmethod
     def _own_grad(prm):
@@ -557,13 +597,24 @@ class ResNetEngine:
             K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
             self._bn_ready(st2)
             dc2, _ = K.bn_bwd_apply(g2, c2, st2)
-            # conv2 (3x3, MIOpen)
+            # conv2 (3x3): weight gradient on MIOpen; stride-1 data gradient on the
+            # implicit-GEMM kernel with bn1's ReLU mask + backward sums fused
             s = blk.conv2.stride[0]
-            da1, dw2, _ = torch.ops.aten.convolution_backward(
-                dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, True, False])
-            self._g(blk.conv2.weight).copy_(dw2)
-            self.on_ready(blk.conv2.weight)
-            dc1 = K.bn_bwd_full(da1.contiguous(memory_format=torch.channels_last), c1, st1, *self._bn_grads(st1))
+            if s == 1:
+                _, dw2, _ = torch.ops.aten.convolution_backward(
+                    dc2, a1, blk.conv2.weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
+                self._g(blk.conv2.weight).copy_(dw2)
+                self.on_ready(blk.conv2.weight)
+                g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
+                n1, _, h1, w1 = c1.shape
+                K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
+                dc1, _ = K.bn_bwd_apply(g1, c1, st1)
+            else:
+                da1, dw2, _ = torch.ops.aten.convolution_backward(
+                    dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, True, False])
+                self._g(blk.conv2.weight).copy_(dw2)
+                self.on_ready(blk.conv2.weight)
+                dc1 = K.bn_bwd_full(da1.contiguous(memory_format=torch.channels_last), c1, st1, *self._bn_grads(st1))
             self._bn_ready(st1)
             # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
             if blk.down_conv is not None:

@@ -282,7 +282,18 @@ def test_transpose_tiles_matches_torch():
         r, c = s.shape
         for r0 in range(0, r, 64):
             for c0 in range(0, c, 64):
-                rows.append((s.data_ptr(), d.data_ptr(), r | (c << 32), r0 | (c0 << 32)))
+                rows.append((s.data_ptr(), d.data_ptr(), r | (c << 32), r0 | (c0 << 32), c | (r << 32)))
+    # 3x3 weight [Cout][3][3][Cin] -> per-tap transposed, taps reversed: [Cin][3][3][Cout]
+    co, ci = 128, 64
+    w = torch.randn(co, ci, 3, 3, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    wd = torch.empty(ci, co, 3, 3, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    esz = 2
+    for tap in range(9):
+        for r0 in range(0, co, 64):
+            for c0 in range(0, ci, 64):
+                rows.append((w.data_ptr() + tap * ci * esz, wd.data_ptr() + (8 - tap) * co * esz, co | (ci << 32),
+                             r0 | (c0 << 32), (9 * ci) | ((9 * co) << 32)))
     ext.transpose_tiles(torch.tensor(rows, dtype=torch.int64).cuda())
     for s, d in zip(srcs, dsts):
         assert torch.equal(d, s.t().contiguous())
+    assert torch.equal(wd, w.flip(2, 3).transpose(0, 1))
