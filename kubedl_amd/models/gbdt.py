@@ -206,68 +206,81 @@ class HistGBDT:
 
     # ------------------------------------------------------------ one tree
     def _grow(self, bins, g, h, n_local: int) -> (Tree, torch.Tensor):
+        """Depth-wise growth.  Per level the host does O(1) device syncs (one
+        batched read of the split decisions, one of the child counts): every
+        per-node quantity is gathered/scattered with one tensor op per level,
+        and each row's node id is carried through the stable sort instead of
+        being re-expanded from the segment counts."""
         p = self.p
         F, B = bins.shape[1], p.max_bin
+        dev = self.device
         tree = Tree()
         root = tree.add()
-        rows = torch.arange(n_local, dtype=torch.int32, device=self.device)
+        rows = torch.arange(n_local, dtype=torch.int32, device=dev)
+        row_node = torch.zeros(n_local, dtype=torch.int32, device=dev)  # level-local node of each row in ``rows``
         seg = [0, n_local]
         level_nodes = [root]
-        leaf_of_row = torch.zeros(n_local, dtype=torch.int32, device=self.device)
+        leaf_of_row = torch.zeros(n_local, dtype=torch.int32, device=dev)
         hist = _allreduce_(self._hist(bins, g, h, rows, seg, F, B))
+        ncut = self.cuts.shape[1]
         for depth in range(p.max_depth + 1):
             nodes = len(level_nodes)
             tot = hist[:, 0].sum(1)  # [nodes, 2] (every feature sums to the node total)
-            G, H = tot[:, 0], tot[:, 1]
+            weight = -tot[:, 0] / (tot[:, 1] + p.reg_lambda) * p.learning_rate
             if depth < p.max_depth:
                 gain, sbin, gl, hl = self._split(hist)
                 best_gain, best_f = gain.max(1)
                 do_split = (best_gain > p.gamma) & torch.isfinite(best_gain)
+                best_b = sbin.gather(1, best_f[:, None])[:, 0].long()
+                thr = self.cuts[best_f, best_b.clamp(0, ncut - 1)]
+                thr = torch.where(best_b < ncut, thr, torch.full_like(thr, math.inf))
+                # one device->host transfer for every per-node decision of this level
+                host = torch.stack([do_split.double(), weight.double(), best_f.double(), best_b.double(),
+                                    thr.double()]).tolist()
+                ds, weights, bf, bb, th = host[0], host[1], [int(v) for v in host[2]], [int(v) for v in host[3]], \
+                    host[4]
+                ds = [v > 0.5 for v in ds]
             else:
-                do_split = torch.zeros(nodes, dtype=torch.bool, device=self.device)
-            ds = do_split.tolist()
-            weights = (-G / (H + p.reg_lambda) * p.learning_rate).tolist()
-            counts = [seg[i + 1] - seg[i] for i in range(nodes)]
-            row_node = torch.repeat_interleave(torch.arange(nodes, device=self.device, dtype=torch.int32),
-                                               torch.tensor(counts, device=self.device))
-            if not any(ds):
-                for i, nid in enumerate(level_nodes):
+                ds, weights = [False] * nodes, weight.tolist()
+            # leaves of this level: every row of a non-split node ends here
+            leaf_id = [-1 if ds[i] else level_nodes[i] for i in range(nodes)]
+            if any(v >= 0 for v in leaf_id):
+                lid = torch.tensor(leaf_id, dtype=torch.int32, device=dev)[row_node.long()]
+                m = lid >= 0
+                leaf_of_row[rows[m].long()] = lid[m]
+            for i, nid in enumerate(level_nodes):
+                if not ds[i]:
                     tree.value[nid] = weights[i]
-                    leaf_of_row[rows[seg[i]:seg[i + 1]].long()] = nid
+            if not any(ds):
                 break
-            bf = best_f.tolist()
-            bb = sbin.gather(1, best_f[:, None])[:, 0].tolist()
-            sfeat = torch.tensor([bf[i] if ds[i] else -1 for i in range(nodes)], dtype=torch.int32,
-                                 device=self.device)
-            sb = torch.tensor([bb[i] if ds[i] else -1 for i in range(nodes)], dtype=torch.int32, device=self.device)
+            sfeat = torch.tensor([bf[i] if ds[i] else -1 for i in range(nodes)], dtype=torch.int32, device=dev)
+            sb = torch.tensor([bb[i] if ds[i] else -1 for i in range(nodes)], dtype=torch.int32, device=dev)
             go_right = self._route(bins, rows, row_node, sfeat, sb)
-            next_nodes, child_of = [], {}
+            next_nodes, remap = [], []
             for i, nid in enumerate(level_nodes):
                 if ds[i]:
                     l, r = tree.add(), tree.add()
                     tree.feature[nid], tree.split_bin[nid] = bf[i], bb[i]
-                    tree.threshold[nid] = float(self.cuts[bf[i], bb[i]]) if bb[i] < self.cuts.shape[1] else math.inf
+                    tree.threshold[nid] = th[i]
                     tree.left[nid], tree.right[nid] = l, r
-                    child_of[i] = (len(next_nodes), len(next_nodes) + 1)
+                    remap.append((len(next_nodes), len(next_nodes) + 1))
                     next_nodes += [l, r]
                 else:
-                    tree.value[nid] = weights[i]
-                    leaf_of_row[rows[seg[i]:seg[i + 1]].long()] = nid
-            # new child index per row (-1 = leaf reached)
-            remap = torch.full((nodes, 2), -1, dtype=torch.int64, device=self.device)
-            for i, (a, b_) in child_of.items():
-                remap[i, 0], remap[i, 1] = a, b_
-            child = remap[row_node.long(), go_right.long()]
+                    remap.append((-1, -1))
+            # new child index per row (-1 = leaf reached); the stable sort keeps rows grouped by child
+            child = torch.tensor(remap, dtype=torch.int32, device=dev)[row_node.long(), go_right.long()]
             keep = child >= 0
             child, rows_k = child[keep], rows[keep]
-            order = torch.sort(child, stable=True).indices
+            child, order = torch.sort(child, stable=True)
             rows = rows_k[order].contiguous()
+            row_node = child.contiguous()
             ccount = torch.bincount(child, minlength=len(next_nodes))
-            seg = [0] + torch.cumsum(ccount, 0).tolist()
             # histogram subtraction: build the smaller child (by global count), derive the sibling
             glob = _allreduce_(ccount.clone().float())
-            parent_hist = hist
-            small = [2 * j + (0 if glob[2 * j] <= glob[2 * j + 1] else 1) for j in range(len(next_nodes) // 2)]
+            cc = torch.stack([torch.cumsum(ccount, 0).double(), glob.double()]).tolist()
+            seg = [0] + [int(v) for v in cc[0]]
+            gl_ = cc[1]
+            small = [2 * j + (0 if gl_[2 * j] <= gl_[2 * j + 1] else 1) for j in range(len(next_nodes) // 2)]
             sub_seg = [0]
             sub_rows = []
             for c in small:
@@ -275,13 +288,13 @@ class HistGBDT:
                 sub_seg.append(sub_seg[-1] + seg[c + 1] - seg[c])
             srows = torch.cat(sub_rows) if sub_rows else rows[:0]
             h_small = _allreduce_(self._hist(bins, g, h, srows.contiguous(), sub_seg, F, B))
-            parents = [i for i in range(nodes) if ds[i]]
-            hist = torch.empty(len(next_nodes), F, B, 2, dtype=torch.float32, device=self.device)
-            for j, c in enumerate(small):
-                sib = c ^ 1
-                hist[c] = h_small[j]
-                hist[sib] = parent_hist[parents[j]] - h_small[j]
-                self.stats["hist_subtracted"] += 1
+            parents = torch.tensor([i for i in range(nodes) if ds[i]], dtype=torch.long, device=dev)
+            small_t = torch.tensor(small, dtype=torch.long, device=dev)
+            parent_hist = hist
+            hist = torch.empty(len(next_nodes), F, B, 2, dtype=torch.float32, device=dev)
+            hist[small_t] = h_small
+            hist[small_t ^ 1] = parent_hist[parents] - h_small
+            self.stats["hist_subtracted"] += len(small)
             level_nodes = next_nodes
         return tree, leaf_of_row
 
