@@ -30,36 +30,41 @@ namespace {
 constexpr int kHistBlock = 256;
 constexpr int kFTile = 64;  // features per block = wave width
 
+// ``fp`` = features per row slot (power of two >= the tile's feature count, <= 64):
+// a wave covers 64 / fp rows per step (F = 28 -> two rows per wave, no idle
+// half-wave), and the LDS tile is [fp][B][2] (64 KiB at F <= 32 -> two blocks
+// per CU).  Blocks past their node's last row exit before touching LDS (the
+// grid is sized by the largest node of the level).
 __global__ __launch_bounds__(kHistBlock) void hist_build_kernel(
     const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
     int64_t gh_stride, const int32_t* __restrict__ rows, const int32_t* __restrict__ seg, int F, int B,
-    int rows_per_block, float* __restrict__ hist) {
-  extern __shared__ float lds[];  // [kFTile][B][2]
+    int rows_per_block, int fp, float* __restrict__ hist) {
+  extern __shared__ float lds[];  // [fp][B][2]
   const int node = blockIdx.y;
-  const int f0 = blockIdx.z * kFTile;
-  const int nf = (F - f0) < kFTile ? (F - f0) : kFTile;
-  const int t = threadIdx.x;
-  for (int i = t; i < kFTile * B * 2; i += kHistBlock) lds[i] = 0.f;
-  __syncthreads();
   const int s0 = seg[node], s1 = seg[node + 1];
   const int r0 = s0 + blockIdx.x * rows_per_block;
+  if (r0 >= s1) return;  // block-uniform
   const int r1 = (r0 + rows_per_block) < s1 ? (r0 + rows_per_block) : s1;
+  const int f0 = blockIdx.z * fp;
+  const int nf = (F - f0) < fp ? (F - f0) : fp;
+  const int t = threadIdx.x;
+  for (int i = t; i < nf * B * 2; i += kHistBlock) lds[i] = 0.f;
+  __syncthreads();
   const int lane = t & 63, wave = t >> 6;
-  if (r0 < s1) {
-    for (int r = r0 + wave; r < r1; r += kHistBlock / 64) {
-      const int row = rows[r];
-      const float g = grad[static_cast<int64_t>(row) * gh_stride];
-      const float h = hess[static_cast<int64_t>(row) * gh_stride];
-      if (lane < nf) {
-        const int b = bins[static_cast<int64_t>(row) * F + f0 + lane];
-        float* p = lds + (lane * B + b) * 2;
-        atomicAdd(p, g);
-        atomicAdd(p + 1, h);
-      }
+  const int rpw = 64 / fp;                 // rows per wave step
+  const int sub = lane / fp, fl = lane - sub * fp;
+  for (int r = r0 + wave * rpw + sub; r < r1; r += (kHistBlock / 64) * rpw) {
+    const int row = rows[r];
+    const float g = grad[static_cast<int64_t>(row) * gh_stride];
+    const float h = hess[static_cast<int64_t>(row) * gh_stride];
+    if (fl < nf) {
+      const int b = bins[static_cast<int64_t>(row) * F + f0 + fl];
+      float* p = lds + (fl * B + b) * 2;
+      atomicAdd(p, g);
+      atomicAdd(p + 1, h);
     }
   }
   __syncthreads();
-  if (r0 >= s1) return;
   float* out = hist + (static_cast<int64_t>(node) * F + f0) * B * 2;
   for (int i = t; i < nf * B * 2; i += kHistBlock) {
     const float v = lds[i];
@@ -184,8 +189,10 @@ hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* 
   const int rows_per_block = 2048;
   int chunks = (max_rows_per_node + rows_per_block - 1) / rows_per_block;
   if (chunks < 1) chunks = 1;
-  dim3 grid(chunks, num_nodes, (F + kFTile - 1) / kFTile);
-  const size_t lds = static_cast<size_t>(kFTile) * B * 2 * sizeof(float);
+  int fp = 1;
+  while (fp < F && fp < kFTile) fp <<= 1;  // features per row slot
+  dim3 grid(chunks, num_nodes, (F + fp - 1) / fp);
+  const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(float);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once
   if (!attr_set) {
     KDL_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_kernel),
@@ -194,7 +201,7 @@ hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* 
     attr_set = true;
   }
   hipLaunchKernelGGL(hist_build_kernel, grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows,
-                     seg, F, B, rows_per_block, hist);
+                     seg, F, B, rows_per_block, fp, hist);
   return hipGetLastError();
 }
 
