@@ -129,19 +129,25 @@ class BaseReconciler(WorkloadController):
     def _failed_or_restarting(self, job: dict, status: dict, rtype: str, failed: int, restart: bool,
                               prev_restarting: bool, prev_failed: bool, display: str) -> None:
         name = job["metadata"]["name"]
+        # The reference captures previousRestarting/previousFailed once per pass,
+        # so two replica types failing in the same pass count the job twice
+        # (found by tests/test_stress.py).  Here the transition is counted once:
+        # "already" also covers an earlier replica type of this pass.
         if restart:
             msg = f"{display} {name} is restarting because {failed} {rtype} replica(s) failed."
             self.recorder.event(job, "Warning", c.JOB_RESTARTING_REASON, msg)
+            already = prev_restarting or c.is_restarting(status)
             c.update_job_conditions(status, c.JOB_RESTARTING, c.JOB_RESTARTING_REASON, msg)
-            if not prev_restarting:
+            if not already:
                 self.metrics.failure_inc()
                 self.metrics.restart_inc()
         else:
             msg = f"{display} {name} is failed because {failed} {rtype} replica(s) failed."
             self.recorder.event(job, "Normal", c.JOB_FAILED_REASON, msg)
             self._set_completion(status)
+            already = prev_failed or c.is_failed(status)
             c.update_job_conditions(status, c.JOB_FAILED, c.JOB_FAILED_REASON, msg)
-            if not prev_failed:
+            if not already:
                 self.metrics.failure_inc()
 
     def _succeeded(self, job: dict, status: dict, msg: str) -> None:
