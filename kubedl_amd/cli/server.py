@@ -10,13 +10,18 @@ A small JSON REST surface over the store, mirroring what ``kubectl`` needs:
 ``GET    /api/events?namespace=&uid=``                 events
 ``GET    /api/logs/<ns>/<pod>?container=&tail=N``      container log
 ``GET    /api/node``                                   GPU inventory + gang allocations
+``GET    /api/summary``                                one row per job: state, age, replicas, launch delays
+``GET    /dashboard``                                  the same as an auto-refreshing HTML page (the
+                                                      reference's "job dashboard", README.md:100-105)
 ``GET    /metrics``                                    Prometheus exposition (kubedl_jobs_*)
 ====================================================  ==========================================
 """
 from __future__ import annotations
 
+import html
 import json
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Optional
 from urllib.parse import parse_qs, urlparse
@@ -35,6 +40,40 @@ def resolve_kind(k: str) -> str:
     if k.lower() in CORE_KINDS:
         return CORE_KINDS[k.lower()]
     return K.lookup(k).kind
+
+
+def job_summary(mgr) -> list:
+    """Dashboard rows: every job of every kind with its state and timings."""
+    from kubedl_amd.api import common as c
+    rows = []
+    now = time.time()
+    for kind in sorted(K.BY_KIND):
+        for j in mgr.store.list(kind):
+            md, st = j["metadata"], j.get("status") or {}
+            conds = [x for x in st.get("conditions") or [] if x.get("status") == "True"]
+            created = c.to_epoch(md.get("creationTimestamp")) or now
+            done = c.to_epoch(st.get("completionTime"))
+            reps = {rt: {k: int(v) for k, v in (rs or {}).items()} for rt, rs in (st.get("replicaStatuses") or {}).items()}
+            uid = md.get("uid", "")
+            obs = getattr(mgr.metrics, "observed", {"first": {}, "all": {}})
+            rows.append({"kind": kind, "namespace": md.get("namespace", ""), "name": md["name"],
+                         "state": conds[-1]["type"] if conds else "", "age_s": round(now - created, 1),
+                         "duration_s": round((done or now) - created, 1), "replicas": reps,
+                         "first_pod_launch_delay_s": obs["first"].get(uid), "all_pods_launch_delay_s": obs["all"].get(uid)})
+    return rows
+
+
+def dashboard_html(rows) -> str:
+    def cell(v):
+        return html.escape("" if v is None else (json.dumps(v) if isinstance(v, dict) else str(v)))
+    cols = ["kind", "namespace", "name", "state", "age_s", "duration_s", "replicas", "first_pod_launch_delay_s",
+            "all_pods_launch_delay_s"]
+    head = "".join(f"<th>{c}</th>" for c in cols)
+    body = "".join("<tr>" + "".join(f"<td>{cell(r.get(c))}</td>" for c in cols) + "</tr>" for r in rows)
+    return ("<!doctype html><html><head><meta charset='utf-8'><meta http-equiv='refresh' content='5'>"
+            "<title>kdl jobs</title><style>body{font-family:sans-serif}table{border-collapse:collapse}"
+            "td,th{border:1px solid #bbb;padding:3px 8px;font-size:13px}</style></head><body>"
+            f"<h3>kdl jobs ({len(rows)})</h3><table><tr>{head}</tr>{body}</table></body></html>")
 
 
 def make_handler(mgr):
@@ -91,6 +130,10 @@ def make_handler(mgr):
                     return self._send(200, {"gpus": a.inv.count if a else 0, "hbm_gb": a.inv.hbm_gb if a else 0,
                                             "free": a.free if a else [], "allocations": a.snapshot() if a else {},
                                             "running_pods": mgr.kubelet.running_pods() if mgr.kubelet else []})
+                if parts[:2] == ["api", "summary"]:
+                    return self._send(200, {"items": job_summary(mgr)})
+                if parts == ["dashboard"]:
+                    return self._send(200, dashboard_html(job_summary(mgr)), "text/html; charset=utf-8")
                 if parts == ["healthz"]:
                     return self._send(200, "ok", "text/plain")
                 return self._err(404, f"no route {u.path}")
