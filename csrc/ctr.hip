@@ -71,21 +71,31 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
   uint4 ra[4], rb[4];
   const int nk = (K + BK - 1) / BK;
 
+  // Loads are unconditional (no load behind an exec branch, which makes hipcc
+  // drain vmcnt before the next tile's MFMAs): rows past M / N re-read row 0
+  // (their outputs are never stored), and K-tail chunks re-read chunk 0 and are
+  // zeroed when staged (they would otherwise feed valid outputs).
+  uint32_t kok = 0;
   auto gload = [&](int kt) {
     const int k0 = kt * BK;
+    kok = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kk = k0 + schunk[i] * 8;
-      const int am = m0 + srow[i], bn = n0 + srow[i];
-      ra[i] = ld16_or_zero(A + static_cast<int64_t>(am) * K + kk, am < M && kk < K);
-      rb[i] = ld16_or_zero(B + static_cast<int64_t>(bn) * K + kk, bn < N && kk < K);
+      const bool kin = kk < K;
+      kok |= kin ? (1u << i) : 0u;
+      const int kc = kin ? kk : 0;
+      const int am = m0 + srow[i] < M ? m0 + srow[i] : 0, bn = n0 + srow[i] < N ? n0 + srow[i] : 0;
+      ra[i] = *reinterpret_cast<const uint4*>(A + static_cast<int64_t>(am) * K + kc);
+      rb[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(bn) * K + kc);
     }
   };
   auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(&lds[buf][0][srow[i] * LDA + schunk[i] * 8]) = ra[i];
-      *reinterpret_cast<uint4*>(&lds[buf][1][srow[i] * LDA + schunk[i] * 8]) = rb[i];
+      const bool kin = (kok >> i) & 1u;
+      *reinterpret_cast<uint4*>(&lds[buf][0][srow[i] * LDA + schunk[i] * 8]) = kin ? ra[i] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(&lds[buf][1][srow[i] * LDA + schunk[i] * 8]) = kin ? rb[i] : make_uint4(0, 0, 0, 0);
     }
   };
 
