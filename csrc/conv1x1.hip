@@ -130,10 +130,12 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI>
+template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
   // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
   // [BM][BN + 8] output tile and finally as the reduction scratch.
+  constexpr int LDK = KBK + 8;  // padded LDS row (bf16): 16-B slot stride odd -> conflict-free fragment reads
+  constexpr int CPRK = KBK / 8; // 16-B chunks per staged row
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * LDK];
   constexpr int kBuf = (BM + BN) * LDK;
   constexpr int WN = (BN >= 64 && BM >= 64) ? 2 : 1;  // waves along N
@@ -142,9 +144,13 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   constexpr int WTM = BM / WM;           // wave tile (M)
   constexpr int WTN = BN / WN;           // wave tile (N) = 64
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int A_CH = BM * 8 / kThreads;  // 16-B chunks per thread per K-step
-  constexpr int B_CH = BN * 8 / kThreads;
+  constexpr int A_CH = BM * CPRK / kThreads;  // 16-B chunks per thread per K-step
+  constexpr int B_CH = BN * CPRK / kThreads;
   constexpr int LDC = BN + 8;
+  // Small K-steps (KBK = 32): the [BM][LDC] output tile does not fit one stage
+  // buffer, so the next tile's first K-step stays in registers through the
+  // epilogue (which then owns both buffers) and is staged after it.
+  constexpr bool SPLIT_C = BM * LDC > kBuf;
   constexpr int CPR = BN / 8;              // 16-B chunks per output row
   constexpr int RPP = kThreads / CPR;      // rows per epilogue pass
   constexpr bool REDUCE = EPI == EPI_STATS || EPI == EPI_MASKX || EPI == EPI_RESBITS;
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   const int gm = q / tiles_n;
   const int n0 = tile_n * BN;
   const int K = p.K, M = p.M, N = p.N;
-  const int nk = K / BK;
+  const int nk = K / KBK;
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
 
   // staging coordinates (fixed per thread)
@@ -165,8 +171,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int c = t + i * kThreads;
-    a_row[i] = c >> 3;
-    a_kc[i] = (c & 7) * 8;
+    a_row[i] = c / CPRK;
+    a_kc[i] = (c % CPRK) * 8;
   }
   int64_t a_off[A_CH];
   // 3x3 implicit GEMM: per A chunk the image base row and the top-left input
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   };
   auto gload = [&](int kt) {
-    const int k0 = kt * BK;
+    const int k0 = kt * KBK;
     int kc0 = k0;  // channel offset of this K-step within a tap
     if constexpr (GATHER == G_CONV3) {
       const int tap = k0 / p.Cin;  // BK divides Cin: a K-step never straddles taps
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int c = t + i * kThreads;
-      rb[i] = ld16(p.B + static_cast<int64_t>(n0 + (c >> 3)) * K + k0 + (c & 7) * 8);
+      rb[i] = ld16(p.B + static_cast<int64_t>(n0 + c / CPRK) * K + k0 + (c % CPRK) * 8);
     }
     if constexpr (PRO) {
       const int kcoef = GATHER == G_CONV3 ? p.Cin : K;
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int c = t + i * kThreads;
-      *reinterpret_cast<uint4*>(&Bs[(c >> 3) * LDK + (c & 7) * 8]) = rb[i];
+      *reinterpret_cast<uint4*>(&Bs[(c / CPRK) * LDK + (c % CPRK) * 8]) = rb[i];
     }
   };
 
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       const bf16_t* As = lds + cur * kBuf;
       const bf16_t* Bs = As + BM * LDK;
 #pragma unroll
-      for (int s = 0; s < BK / 16; ++s) {
+      for (int s = 0; s < KBK / 16; ++s) {
         bf16x8_t wf[TN], xf[TM];
 #pragma unroll
         for (int i = 0; i < TN; ++i)
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           for (int j = 0; j < TM; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
       }
-      if (more) swrite(cur ^ 1);
+      if (more_k || (more && !SPLIT_C)) swrite(cur ^ 1);
       __syncthreads();
       cur ^= 1;
     }
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     // D[n][m] -> LDS [m][n] (buffer cur^1 is free: its last reader was the final
     // K-step, which ended with a barrier; buffer cur may already hold the next
     // tile's first K-step)
-    bf16_t* Cs = lds + (cur ^ 1) * kBuf;
+    bf16_t* Cs = SPLIT_C ? lds : lds + (cur ^ 1) * kBuf;
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -481,6 +487,11 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       }
     }
     __syncthreads();  // Cs (buffer cur^1) is restaged by the next tile's second K-step
+    if constexpr (SPLIT_C) {  // stage the next tile's first K-step now that the epilogue is done
+      if (tm + GM < tiles_m) swrite(0);
+      cur = 0;
+      __syncthreads();
+    }
   }
 
   if constexpr (REDUCE) {
@@ -745,7 +756,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restric
   }
 }
 
-template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI>
+template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI, int KBK>
 hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = p.N / BN;
@@ -756,50 +767,56 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
-  hipLaunchKernelGGL((gemm1x1_kernel<BM, BN, MINB, PRO, GATHER, EPI>), dim3(GM * tiles_n), dim3(kThreads), 0, s, p,
+  hipLaunchKernelGGL((gemm1x1_kernel<BM, BN, MINB, PRO, GATHER, EPI, KBK>), dim3(GM * tiles_n), dim3(kThreads), 0, s, p,
                      GM, tiles_m, tiles_n);
   return hipGetLastError();
 }
 
 // forward convs (prologue / row gather) only ever use the PLAIN and STATS
 // epilogues; the dgrad epilogues run without either (3x3 dgrad: MASKX)
-template <int BM, int BN, int MINB, bool PRO, int GATHER>
+template <int BM, int BN, int MINB, bool PRO, int GATHER, int KBK>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   switch (epi) {
-    case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN>(p, s);
-    case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS>(p, s);
+    case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
+    case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
   }
   if constexpr (!PRO && GATHER == G_DENSE) {
     switch (epi) {
-      case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX>(p, s);
-      case EPI_RESBITS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS>(p, s);
-      case EPI_RES: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RES>(p, s);
+      case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
+      case EPI_RESBITS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
+      case EPI_RES: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RES, KBK>(p, s);
     }
   }
   if constexpr (!PRO && GATHER == G_CONV3) {
-    if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX>(p, s);
+    if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
   }
   return hipErrorInvalidValue;
 }
 
-template <int BM, int BN, int MINB>
+template <int BM, int BN, int MINB, int KBK = BK>
 hipError_t dispatch_pg(const GemmParams& p, int epi, bool pro, int gather, hipStream_t s) {
   if (gather == G_CONV3)
-    return pro ? dispatch_epi<BM, BN, MINB, true, G_CONV3>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_CONV3>(p, epi, s);
-  if (pro) return gather ? dispatch_epi<BM, BN, MINB, true, G_STRIDED>(p, epi, s) : dispatch_epi<BM, BN, MINB, true, G_DENSE>(p, epi, s);
-  return gather ? dispatch_epi<BM, BN, MINB, false, G_STRIDED>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_DENSE>(p, epi, s);
+    return pro ? dispatch_epi<BM, BN, MINB, true, G_CONV3, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_CONV3, KBK>(p, epi, s);
+  if (pro) return gather ? dispatch_epi<BM, BN, MINB, true, G_STRIDED, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, true, G_DENSE, KBK>(p, epi, s);
+  return gather ? dispatch_epi<BM, BN, MINB, false, G_STRIDED, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_DENSE, KBK>(p, epi, s);
 }
 
-// Tile configs: 0 = 128x128 (2 blocks/CU), 1 = 128x64, 2 = 64x128, 3 = 64x64 (4 blocks/CU).
-int pick_config(int M, int N, int K) {
+// Tile configs: 0 = 128x128 (2 blocks/CU), 1 = 128x64, 2 = 64x128, 3 = 64x64 (4 blocks/CU),
+// 5 = 128x128 with 32-deep K-steps (40 KiB of LDS, 3 blocks/CU).
+int pick_config(int M, int N, int K, int epi) {
   static const int forced = [] {
     const char* e = getenv("KDL_GEMM_CFG");
     return e ? atoi(e) : -1;
   }();
-  if (forced >= 0 && forced <= 3) {
-    if ((forced == 0 || forced == 2) && N % 128) return 3;
+  if (forced >= 0 && forced <= 5) {
+    if ((forced == 0 || forced == 2 || forced == 5) && N % 128) return 3;
+    if (forced == 4) return N % 128 ? 1 : 0;
     return forced;
   }
+  // Short-K statistics GEMMs (the forward 1x1 convs of stages 1-2) gain from the
+  // third resident block of the 32-deep-K config (-8..14 %); dgrad epilogues do
+  // not (RESBITS spills at 168 VGPRs) and long K is neutral.
+  if (N % 128 == 0 && epi == EPI_STATS && K <= 256) return 5;
   return N % 128 == 0 ? 0 : 1;
 }
 
@@ -837,10 +854,11 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (epi == EPI_RES || epi == EPI_RESBITS) {
     if (!p.eres) return hipErrorInvalidValue;
   }
-  switch (pick_config(p.M, p.N, p.K)) {
+  switch (pick_config(p.M, p.N, p.K, epi)) {
     case 0: return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
     case 1: return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
     case 2: return dispatch_pg<64, 128, 3>(p, epi, pro, gather, s);
+    case 5: return dispatch_pg<128, 128, 3, 32>(p, epi, pro, gather, s);
     default: return dispatch_pg<64, 64, 4>(p, epi, pro, gather, s);
   }
 }
