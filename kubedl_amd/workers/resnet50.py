@@ -16,10 +16,15 @@ import json
 import os
 import time
 
-import torch
-import torch.nn.functional as F
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# shipped MIOpen find-db / kernel cache (as bench.py): no conv-kernel recompiles per job
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db", "user"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_ROOT, "miopen_db", "cache"))
 
-from kubedl_amd.models.resnet import resnet50, resnet_tiny
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from kubedl_amd.models.resnet import resnet50, resnet_tiny  # noqa: E402
 from kubedl_amd.ops.optim import FlatParamSpace, FusedSGD
 from kubedl_amd.parallel import dist as kdist
 from kubedl_amd.parallel.ddp import FlatDDP
