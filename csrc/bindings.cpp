@@ -5,6 +5,7 @@
 // the PyTorch caching allocator) and stream selection.  Every launch goes to
 // PyTorch's current HIP stream so the ops compose with autograd, RCCL and
 // hipGraph capture.
+#include <cstring>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -311,6 +312,84 @@ void transpose_tiles(const at::Tensor& table) {
   check_hip(kdl::transpose_tiles(reinterpret_cast<const kdl::TransposeTile*>(table.data_ptr<int64_t>()),
                                  static_cast<int>(table.size(0)), cur_stream()),
             "transpose_tiles");
+}
+
+// ------------------------------------------------------------------ P2P all-reduce
+// IPC plumbing is stateless here: python (kubedl_amd/parallel/p2p.py) owns the
+// exchanged handles, the mapped peer pointers and the epoch counter.
+py::tuple ipc_handle(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda(), "ipc_handle: GPU tensor required");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  check_hip(hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(t.data_ptr())),
+            "hipMemGetAddressRange");
+  hipIpcMemHandle_t h;
+  check_hip(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(base)), "hipIpcGetMemHandle");
+  const int64_t off = reinterpret_cast<const char*>(t.data_ptr()) - reinterpret_cast<const char*>(base);
+  return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)), off);
+}
+
+int64_t ipc_open(const std::string& handle, int64_t device) {
+  TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "ipc_open: bad handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data(), sizeof(h));
+  check_hip(hipSetDevice(static_cast<int>(device)), "hipSetDevice");
+  void* p = nullptr;
+  check_hip(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ipc_close(int64_t base) {
+  check_hip(hipIpcCloseMemHandle(reinterpret_cast<void*>(base)), "hipIpcCloseMemHandle");
+}
+
+at::Tensor p2p_signal_alloc(int64_t device) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, device));
+  const size_t bytes = kdl::kP2PSignalWords * sizeof(uint32_t);
+  void* p = nullptr;
+  // uncached: flags are polled across GPUs
+  check_hip(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
+  check_hip(hipMemset(p, 0, bytes), "hipMemset");
+  check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return at::from_blob(p, {static_cast<int64_t>(bytes)}, [](void* q) { (void)hipFree(q); },
+                       at::TensorOptions().dtype(at::kByte).device(c10::DeviceType::CUDA, device));
+}
+
+// host-mapped error word: returns (host pointer, device pointer)
+py::tuple p2p_error_word() {
+  void* h = nullptr;
+  check_hip(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  std::memset(h, 0, 64);
+  void* d = nullptr;
+  check_hip(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer");
+  return py::make_tuple(reinterpret_cast<int64_t>(h), reinterpret_cast<int64_t>(d));
+}
+
+void p2p_error_free(int64_t host) { (void)hipHostFree(reinterpret_cast<void*>(host)); }
+
+void p2p_allreduce(const std::vector<int64_t>& bufs, const std::vector<int64_t>& sigs, int64_t err_dev,
+                   int64_t rank, int64_t nbytes, int64_t epoch, double scale, bool bf16, double timeout_s) {
+  const int64_t world = static_cast<int64_t>(bufs.size());
+  TORCH_CHECK(world >= 1 && world <= kdl::kP2PMaxRanks && static_cast<int64_t>(sigs.size()) == world,
+              "p2p_allreduce: 1..8 ranks, one buffer and one signal pointer per rank");
+  TORCH_CHECK(rank >= 0 && rank < world, "p2p_allreduce: rank out of range");
+  TORCH_CHECK(nbytes > 0 && nbytes % 16 == 0 && nbytes / 16 < (int64_t(1) << 28),
+              "p2p_allreduce: bucket bytes must be a positive multiple of 16 below 4 GiB");
+  kdl::P2PArgs a{};
+  for (int64_t j = 0; j < world; ++j) {
+    TORCH_CHECK(bufs[j] % 16 == 0 && bufs[j] != 0 && sigs[j] != 0, "p2p_allreduce: unaligned or null pointer");
+    a.buf[j] = reinterpret_cast<void*>(bufs[j]);
+    a.sig[j] = reinterpret_cast<uint32_t*>(sigs[j]);
+  }
+  a.err = reinterpret_cast<uint32_t*>(err_dev);
+  a.timeout_ticks = static_cast<uint64_t>(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  a.units = static_cast<uint32_t>(nbytes / 16);
+  a.epoch = static_cast<uint32_t>(epoch);
+  a.scale = static_cast<float>(scale);
+  a.rank = static_cast<int>(rank);
+  a.world = static_cast<int>(world);
+  check_hip(kdl::p2p_allreduce(a, bf16, cur_stream()), "p2p_allreduce");
 }
 
 // ------------------------------------------------------------------ GBDT
@@ -821,6 +900,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");
   m.def("cast_copy", &cast_copy, "flat dtype-casting copy");
   m.def("transpose_tiles", &transpose_tiles, "batched bf16 2-D transposes from a static 64x64 tile table");
+  m.def("ipc_handle", &ipc_handle, "(IPC handle bytes, byte offset) of a GPU tensor's allocation");
+  m.def("ipc_open", &ipc_open, "map a peer process's IPC handle; returns the mapped base pointer");
+  m.def("ipc_close", &ipc_close, "unmap a pointer returned by ipc_open");
+  m.def("p2p_signal_alloc", &p2p_signal_alloc, "zeroed uncached signal buffer for p2p_allreduce");
+  m.def("p2p_error_word", &p2p_error_word, "host-mapped error word (host ptr, device ptr)");
+  m.def("p2p_error_free", &p2p_error_free, "free a p2p_error_word");
+  m.def("p2p_blocks", &kdl::p2p_blocks, "blocks per p2p_allreduce launch for (16-B units, world)");
+  m.def("p2p_allreduce", &p2p_allreduce, "in-place two-phase all-reduce over IPC-mapped peer buffers");
   m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");

@@ -114,6 +114,24 @@ hipError_t transpose_tiles(const TransposeTile* tiles, int ntiles, hipStream_t s
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
                         int dtype, float scale, hipStream_t s);
 
+// ---- p2p.hip (two-phase all-reduce over IPC-mapped peer buffers)
+constexpr int kP2PMaxRanks = 8;
+constexpr int kP2PMaxBlocks = 128;
+// Signal buffer per rank: uint32 [3 phases][kP2PMaxBlocks][kP2PMaxRanks].
+constexpr int kP2PSignalWords = 3 * kP2PMaxBlocks * kP2PMaxRanks;
+struct P2PArgs {
+  void* buf[kP2PMaxRanks];      // bucket start in every rank's buffer (buf[rank] = own, local)
+  uint32_t* sig[kP2PMaxRanks];  // every rank's signal buffer (peer-mapped)
+  uint32_t* err;                // host-mapped error word: bit p = a phase-p wait timed out
+  uint64_t timeout_ticks;       // per wait, in 100 MHz wall-clock ticks
+  uint32_t units;               // 16-byte units in the bucket
+  uint32_t epoch;               // call number (same sequence on every rank, starts at 1)
+  float scale;                  // applied to the sum (1/world for an average)
+  int rank, world;
+};
+int p2p_blocks(int64_t units, int world);
+hipError_t p2p_allreduce(const P2PArgs& a, bool bf16, hipStream_t s);
+
 // ---- gbdt.hip (histogram GBDT for the XGBoostJob worker)
 hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                            const int32_t* rows, const int32_t* seg, int num_nodes, int max_rows_per_node,

@@ -16,6 +16,11 @@ the last (smallest, first-layer) bucket with backward while staying far above
 the latency-bound regime.  The first bucket is capped smaller so the first
 collective starts early.
 
+Transport: RCCL (``dist.all_reduce``) by default; ``KDL_ALLREDUCE=p2p`` runs
+each bucket through ``kubedl_amd.parallel.p2p`` instead (one kernel reading
+all peers' IPC-mapped gradient buffers over their own xGMI links), on a side
+stream ordered after the bucket's producers.
+
 The reference has no collective code; this is the DP
 strategy a PyTorchJob's env (``MASTER_ADDR/PORT``, ``WORLD_SIZE``, ``RANK``)
 exists to enable.
@@ -26,6 +31,7 @@ import torch
 import torch.distributed as dist
 
 from kubedl_amd.ops.optim import FlatParamSpace
+from kubedl_amd.parallel import p2p
 
 
 class Bucket:
@@ -51,12 +57,15 @@ class FlatDDP:
         self.pg = process_group
         self.buckets: list[Bucket] = []
         self._hooks = []
+        self.transport = None
         if world_size > 1:
             if broadcast_from is not None:
                 with torch.no_grad():
                     dist.broadcast(space.param, broadcast_from, group=process_group)
                     space.sync_master_from_params()
             self._build_buckets(bucket_cap_mb, first_bucket_mb)
+            if p2p.wanted() and space.grad.is_cuda:
+                self.transport = p2p.P2PTransport(space.grad, process_group)
             if not direct:
                 self._install_hooks()
 
@@ -93,7 +102,10 @@ class FlatDDP:
             b.packer.pack()
             for s in b.slots:  # gradients now live in the bucket: free autograd's copies
                 s.param.grad = None
-        b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
+        if self.transport is not None:
+            b.handle = self.transport.launch(b.lo, b.hi)
+        else:
+            b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
 
     def _on_grad(self, p: torch.Tensor) -> None:
         b = self._slot_bucket[id(p)]
@@ -118,6 +130,8 @@ class FlatDDP:
             b.handle.wait()
             b.handle = None
             b.pending = len(b.slots)
+        if self.transport is not None:
+            self.transport.check()  # host-mapped timeout bits of earlier steps (no sync)
         self.space.mark_packed()
 
     @property
