@@ -369,7 +369,8 @@ py::tuple p2p_error_word() {
 void p2p_error_free(int64_t host) { (void)hipHostFree(reinterpret_cast<void*>(host)); }
 
 void p2p_allreduce(const std::vector<int64_t>& bufs, const std::vector<int64_t>& sigs, int64_t err_dev,
-                   int64_t rank, int64_t nbytes, int64_t epoch, double scale, bool bf16, double timeout_s) {
+                   int64_t rank, int64_t nbytes, int64_t epoch, double scale, bool bf16, double timeout_s,
+                   bool oneshot) {
   const int64_t world = static_cast<int64_t>(bufs.size());
   TORCH_CHECK(world >= 1 && world <= kdl::kP2PMaxRanks && static_cast<int64_t>(sigs.size()) == world,
               "p2p_allreduce: 1..8 ranks, one buffer and one signal pointer per rank");
@@ -389,7 +390,8 @@ void p2p_allreduce(const std::vector<int64_t>& bufs, const std::vector<int64_t>&
   a.scale = static_cast<float>(scale);
   a.rank = static_cast<int>(rank);
   a.world = static_cast<int>(world);
-  check_hip(kdl::p2p_allreduce(a, bf16, cur_stream()), "p2p_allreduce");
+  TORCH_CHECK(!oneshot || nbytes / 16 <= kdl::p2p_oneshot_max_units(), "p2p_allreduce: bucket too large for one-shot");
+  check_hip(kdl::p2p_allreduce(a, bf16, oneshot, cur_stream()), "p2p_allreduce");
 }
 
 // ------------------------------------------------------------------ GBDT
@@ -907,6 +909,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("p2p_error_word", &p2p_error_word, "host-mapped error word (host ptr, device ptr)");
   m.def("p2p_error_free", &p2p_error_free, "free a p2p_error_word");
   m.def("p2p_blocks", &kdl::p2p_blocks, "blocks per p2p_allreduce launch for (16-B units, world)");
+  m.def("p2p_oneshot_max_units", &kdl::p2p_oneshot_max_units, "largest bucket (16-B units) of the one-shot path");
   m.def("p2p_allreduce", &p2p_allreduce, "in-place two-phase all-reduce over IPC-mapped peer buffers");
   m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");

@@ -130,7 +130,9 @@ struct P2PArgs {
   int rank, world;
 };
 int p2p_blocks(int64_t units, int world);
-hipError_t p2p_allreduce(const P2PArgs& a, bool bf16, hipStream_t s);
+int p2p_oneshot_max_units();
+// oneshot: whole bucket summed by every rank (units <= p2p_oneshot_max_units())
+hipError_t p2p_allreduce(const P2PArgs& a, bool bf16, bool oneshot, hipStream_t s);
 
 // ---- gbdt.hip (histogram GBDT for the XGBoostJob worker)
 hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,

@@ -25,6 +25,9 @@
 // stores; peer data is always read with sc0|sc1 (system-coherent) buffer loads,
 // so no stale line of a previous call can be served from this GPU's caches.
 //
+// Small buckets take a one-shot path (each rank sums the whole bucket from all
+// peers, two barriers); the caller picks it by size, identically on every rank.
+//
 // Every wait is bounded by the wall clock (s_memrealtime, 100 MHz): a peer
 // that never arrives sets a bit in a host-mapped error word and the kernel
 // drains instead of hanging the GPU.
@@ -147,7 +150,53 @@ __global__ __launch_bounds__(kP2PThreads) void p2p_allreduce_kernel(P2PArgs a) {
   p2p_barrier(a, 2);  // nobody reads this rank's buffer any more
 }
 
+// One-shot variant for small buckets (latency-bound): every rank sums the
+// WHOLE bucket from all peers into registers (at most kOneShotUnits units per
+// thread), waits until every rank has read every buffer, then writes its sums
+// in place.  Two barriers and one round of peer reads instead of three and two.
+constexpr int kOneShotUnits = 4;
+
+template <bool BF16>
+__global__ __launch_bounds__(kP2PThreads) void p2p_allreduce_oneshot_kernel(P2PArgs a) {
+  const int W = a.world;
+  const uint32_t units = a.units;
+  const uint32_t step = gridDim.x * kP2PThreads;
+  const uint32_t first = blockIdx.x * kP2PThreads + threadIdx.x;
+  const uint32_t bytes = units * 16u;
+  __amdgpu_buffer_rsrc_t rs[kP2PMaxRanks];
+#pragma unroll
+  for (int j = 0; j < kP2PMaxRanks; ++j) rs[j] = p2p_rsrc(a.buf[j < W ? j : 0], bytes);
+  uint4* own = reinterpret_cast<uint4*>(a.buf[a.rank]);
+
+  p2p_barrier(a, 0);
+  uint4 out[kOneShotUnits];
+#pragma unroll
+  for (int i = 0; i < kOneShotUnits; ++i) {
+    const uint32_t u = first + i * step;
+    out[i] = make_uint4(0, 0, 0, 0);
+    if (u < units) {  // the buffer descriptor range-checks the rest anyway
+      uint4 v[kP2PMaxRanks];
+#pragma unroll
+      for (int j = 0; j < kP2PMaxRanks; ++j)
+        if (j < W) v[j] = p2p_load(rs[j], u * 16u);
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < kP2PMaxRanks; ++j)
+        if (j < W) acc_unit<BF16>(s, v[j]);
+      out[i] = pack_unit<BF16>(s, a.scale);
+    }
+  }
+  p2p_barrier(a, 1);  // every rank has read every buffer: overwrite in place
+#pragma unroll
+  for (int i = 0; i < kOneShotUnits; ++i) {
+    const uint32_t u = first + i * step;
+    if (u < units) own[u] = out[i];
+  }
+}
+
 }  // namespace
+
+int p2p_oneshot_max_units() { return kP2PMaxBlocks * kP2PThreads * kOneShotUnits; }
 
 int p2p_blocks(int64_t units, int world) {
   const int64_t per_rank = (units + world - 1) / world;
@@ -157,8 +206,18 @@ int p2p_blocks(int64_t units, int world) {
   return static_cast<int>(b);
 }
 
-hipError_t p2p_allreduce(const P2PArgs& a, bool bf16, hipStream_t s) {
+hipError_t p2p_allreduce(const P2PArgs& a, bool bf16, bool oneshot, hipStream_t s) {
   if (a.world < 1 || a.world > kP2PMaxRanks || a.units == 0) return hipErrorInvalidValue;
+  if (oneshot) {
+    if (a.units > static_cast<uint32_t>(p2p_oneshot_max_units())) return hipErrorInvalidValue;
+    int blocks = static_cast<int>((a.units + kP2PThreads * kOneShotUnits - 1) / (kP2PThreads * kOneShotUnits));
+    if (blocks < 1) blocks = 1;
+    if (bf16)
+      hipLaunchKernelGGL(p2p_allreduce_oneshot_kernel<true>, dim3(blocks), dim3(kP2PThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(p2p_allreduce_oneshot_kernel<false>, dim3(blocks), dim3(kP2PThreads), 0, s, a);
+    return hipGetLastError();
+  }
   const int blocks = p2p_blocks(a.units, a.world);
   if (bf16)
     hipLaunchKernelGGL(p2p_allreduce_kernel<true>, dim3(blocks), dim3(kP2PThreads), 0, s, a);

@@ -5,8 +5,10 @@ buffer of a ``FlatParamSpace``): every rank exports an IPC handle of its
 buffer and of a small uncached signal buffer, gathers everybody's handles
 through the process group (``all_gather_object``: a few hundred bytes, once)
 and maps the peers.  ``all_reduce_(lo, hi)`` then sums ``buf[lo:hi]`` over all
-ranks in place with one kernel (csrc/p2p.hip: reduce-scatter + all-gather,
-every peer read concurrently over its own xGMI link) on the current stream.
+ranks in place with one kernel on the current stream (csrc/p2p.hip:
+reduce-scatter + all-gather, every peer read concurrently over its own xGMI
+link; buckets up to ``KDL_P2P_ONESHOT_BYTES`` (256 KiB) take the one-shot
+kernel instead: every rank sums the whole bucket, two barriers).
 
 Why beside RCCL: on a fully connected 8-GPU MI355X node a ring moves each
 byte over one link per step and pays 2(W-1) latency-bound steps; reading the 7
@@ -78,21 +80,29 @@ class P2PAllReduce:
             self.buf_ptrs.append(bbase + boff)
             self.sig_ptrs.append(sbase + soff)
         self.epoch = 0
+        # buckets up to this size take the one-shot kernel (latency-bound regime)
+        self.oneshot_bytes = min(int(os.environ.get("KDL_P2P_ONESHOT_BYTES", 256 * 1024)),
+                                 ext.p2p_oneshot_max_units() * 16)
         # every rank has zeroed its signals and mapped its peers before anyone signals
         torch.cuda.synchronize(self.dev)
         dist.barrier(group=group)
 
-    def all_reduce_(self, lo: int = 0, hi: int | None = None, scale: float = 1.0) -> torch.Tensor:
-        """Sum ``buf[lo:hi]`` over ranks in place (times ``scale``), on the current stream."""
+    def all_reduce_(self, lo: int = 0, hi: int | None = None, scale: float = 1.0,
+                    oneshot: bool | None = None) -> torch.Tensor:
+        """Sum ``buf[lo:hi]`` over ranks in place (times ``scale``), on the current stream.
+        ``oneshot`` = None picks by size (must agree on every rank; it does, as the
+        threshold is the same everywhere)."""
         hi = self.buf.numel() if hi is None else hi
         nbytes = (hi - lo) * self.esz
         if (lo * self.esz) % 16 or nbytes % 16 or nbytes <= 0:
             raise ValueError("P2PAllReduce: the slice must start and end on 16-byte boundaries")
+        if oneshot is None:
+            oneshot = nbytes <= self.oneshot_bytes
         self.epoch = (self.epoch + 1) & 0xFFFFFFFF
         off = lo * self.esz
         self._ext.p2p_allreduce([p + off for p in self.buf_ptrs], self.sig_ptrs, self._err_dev, self.rank,
                                 nbytes, self.epoch, float(scale), self.buf.dtype == torch.bfloat16,
-                                float(self.timeout_s))
+                                float(self.timeout_s), bool(oneshot))
         return self.buf[lo:hi]
 
     def errors(self) -> int:

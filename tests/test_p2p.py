@@ -68,7 +68,7 @@ def test_ddp_keeps_collectives_for_cpu_buffers():
     assert all(r[1] for r in res)
 
 
-def _p2p_worker(rank, world, port, q, dtype_name, n, bounds, reps):
+def _p2p_worker(rank, world, port, q, dtype_name, n, bounds, reps, oneshot=None):
     import torch.distributed as dist
     from kubedl_amd.parallel.p2p import P2PAllReduce
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -83,7 +83,7 @@ def _p2p_worker(rank, world, port, q, dtype_name, n, bounds, reps):
         src = torch.randn(n, generator=g).to(dtype)
         buf.copy_(src.to(dev))
         for lo, hi in bounds:
-            ar.all_reduce_(lo, hi)
+            ar.all_reduce_(lo, hi, oneshot=oneshot)
         torch.cuda.synchronize()
         outs.append((src.float().numpy(), buf.float().cpu().numpy()))
     err = ar.errors()
@@ -94,14 +94,19 @@ def _p2p_worker(rank, world, port, q, dtype_name, n, bounds, reps):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype_name", ["bfloat16", "float32"])
-def test_p2p_allreduce_two_ranks_gpu(dtype_name):
+@pytest.mark.parametrize("dtype_name,oneshot", [("bfloat16", None), ("float32", None), ("bfloat16", True),
+                                                ("float32", False)])
+def test_p2p_allreduce_two_ranks_gpu(dtype_name, oneshot):
     """Buckets of several sizes (one unit per rank up to many blocks), reused over
-    repeated calls (epochs), against an fp32 sum of the ranks' inputs."""
+    repeated calls (epochs), against an fp32 sum of the ranks' inputs; size-picked
+    (one-shot below 256 KiB, two-shot above), forced one-shot, forced two-shot."""
     n = 1 << 20
-    bounds = [(0, 64), (64, 4160), (4160, 300000), (300000, n)]
+    bounds = [(0, 64), (64, 4160), (4160, 100000), (100000, 300000), (300000, n)]
+    if oneshot:  # one-shot holds at most 128 blocks x 256 threads x 4 units
+        n = 1 << 19
+        bounds = [(0, 64), (64, 4160), (4160, 100000), (100000, n)]
     world = 2
-    res = _spawn(_p2p_worker, world, dtype_name, n, bounds, 3)
+    res = _spawn(_p2p_worker, world, dtype_name, n, bounds, 3, oneshot)
     assert all(r[2] == 0 for r in res), "a p2p wait timed out"
     for it in range(3):
         ref = sum(torch.from_numpy(r[1][it][0]) for r in res)
