@@ -58,9 +58,12 @@ def main(argv=None) -> int:
                     help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "autograd"],
                     help="fused = explicit engine (fused 1x1-conv GEMMs + staged BN); autograd = module + autograd")
+    ap.add_argument("--allreduce", default=os.environ.get("KDL_ALLREDUCE", "rccl"), choices=["rccl", "p2p"],
+                    help="DP gradient transport for N > 1: RCCL, or the IPC peer-buffer kernel (csrc/p2p.hip)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")
     args = ap.parse_args(argv)
+    os.environ["KDL_ALLREDUCE"] = args.allreduce
 
     if "WORLD_SIZE" not in os.environ:
         os.environ["WORLD_SIZE"] = "1"
@@ -121,6 +124,7 @@ def main(argv=None) -> int:
                 "bn_backend": args.bn_backend,
                 "engine": trainer.engine_kind,
                 "conv_benchmark": bool(args.conv_benchmark),
+                "allreduce": args.allreduce if n > 1 else None,
             },
             "steps_per_sec": round(args.steps / dt, 4),
             "launch_delay_s": round(launch_delay, 3),
