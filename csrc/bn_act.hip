@@ -32,7 +32,7 @@
 //                        apply    -- dx = k*dz + c1*x + c0, d(residual) = dz.
 //
 // Workspace per BN layer (fp32, zero on first use, kept zero by finalize):
-//   [kReplicas][2C] forward accumulators | [kReplicas][2C] backward | [4C] coefs.
+//   [kReplicas][2C] forward accumulators | [kReplicas][2C] backward | [2C] forward coefs (scale, shift) | [3C] backward coefs (k, c1, c0).
 // History (profiles/): v0 wrote [P][C] partials and finalised them with a
 // single-block serial loop (65-73 us per launch, 7.3 ms/step); v1 put all P
 // blocks' atomics on one [2C] row (165 us per stats launch: same-address
@@ -84,6 +84,10 @@ __host__ __device__ __forceinline__ float* ws_acc_bwd(float* ws, int C) {
 __host__ __device__ __forceinline__ float* ws_coef(float* ws, int C) {
   return ws + static_cast<int64_t>(kReplicas) * 4 * C;
 }
+// backward coefficients (k, c1, c0) live beside the forward ones (scale, shift),
+// so a weight gradient that re-applies the forward BN (GEMM prologue) may run on
+// a side stream while the backward finalize of the same BN runs on the main one
+__host__ __device__ __forceinline__ float* ws_bcoef(float* ws, int C) { return ws_coef(ws, C) + 2 * C; }
 
 __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
   // no-return fp32 atomic (global_atomic_add_f32 with -munsafe-fp-atomics),
@@ -834,7 +838,7 @@ void bwd_launch(const ReducePlan& rp, const T* dy, const T* y, const uint8_t* mb
                 const PT* beta, const float* mean, const float* invstd, T* dx, T* dres, PT* dgamma,
                 PT* dbeta, float* ws, int64_t M, int C, bool training, hipStream_t s) {
   float* acc = ws_acc_bwd(ws, C);
-  float* coef = ws_coef(ws, C);
+  float* coef = ws_bcoef(ws, C);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, PT, VEC, MASK>), dim3(rp.gx, rp.tl.gy), dim3(kBlock),
                      0, s, dy, y, mbits, x, gamma, beta, mean, invstd, M, C, rp.tl.TPR, rp.tl.RPI, acc);
   hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0,
@@ -872,7 +876,7 @@ hipError_t bwd_impl(const T* dy, const T* y, const uint8_t* mbits, const T* x, c
 }  // namespace
 
 int64_t bn_workspace_floats(int C) {
-  return static_cast<int64_t>(kReplicas) * 4 * C + 4 * static_cast<int64_t>(C);
+  return static_cast<int64_t>(kReplicas) * 4 * C + 5 * static_cast<int64_t>(C);
 }
 
 #define KDL_DISPATCH_PT(pdtype, ...)              \
@@ -975,7 +979,7 @@ hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, 
   const int PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;
   ReducePlan rp = plan_reduce(M, C, VEC);
   float* acc = ws_acc_bwd(ws, C);
-  float* coef = ws_coef(ws, C);
+  float* coef = ws_bcoef(ws, C);
   const bf16_t* db = static_cast<const bf16_t*>(dyp);
   const bf16_t* xb = static_cast<const bf16_t*>(x);
   KDL_DISPATCH_PT(pdtype, {
@@ -1091,7 +1095,7 @@ hipError_t bn_stage_bwd_apply_maskx(const void* dy, const void* x, const void* g
   if (M <= 0 || C % 8) return hipErrorInvalidValue;
   const Tiling tl = make_tiling(C, 8);
   dim3 grid(apply_gx(M, tl), tl.gy);
-  const float* coef = ws_coef(const_cast<float*>(ws), C);
+  const float* coef = ws_bcoef(const_cast<float*>(ws), C);
   KDL_DISPATCH_PT(pdtype, {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, PT, 8, kMaskX, false>), grid, dim3(kBlock), 0, s,
                        static_cast<const bf16_t*>(dy), nullptr, nullptr, static_cast<const bf16_t*>(x),
@@ -1107,7 +1111,7 @@ hipError_t bn_stage_bwd_finalize(float* ws, int64_t M, int C, const void* gamma,
   KDL_DISPATCH_PT(pdtype, {
     hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                        ws_acc_bwd(ws, C), C, static_cast<float>(M), static_cast<const PT*>(gamma), mean, invstd,
-                       training, static_cast<PT*>(dgamma), static_cast<PT*>(dbeta), ws_coef(ws, C));
+                       training, static_cast<PT*>(dgamma), static_cast<PT*>(dbeta), ws_bcoef(ws, C));
   });
   return hipGetLastError();
 }
@@ -1117,11 +1121,11 @@ hipError_t bn_stage_bwd_apply(const void* g, const void* x, const float* ws, voi
   if (M <= 0 || C % 8) return hipErrorInvalidValue;
   const Tiling tl = make_tiling(C, 8);
   dim3 grid(apply_gx(M, tl), tl.gy);
-  const float* coef = ws_coef(const_cast<float*>(ws), C);
+  const float* coef = ws_bcoef(const_cast<float*>(ws), C);
   if (xd) {
     hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, grid, dim3(kBlock), 0, s, static_cast<const bf16_t*>(g),
                        static_cast<const bf16_t*>(x), coef, static_cast<bf16_t*>(dx),
-                       static_cast<const bf16_t*>(xd), ws_coef(const_cast<float*>(wsd), C),
+                       static_cast<const bf16_t*>(xd), ws_bcoef(const_cast<float*>(wsd), C),
                        static_cast<bf16_t*>(dxd), M, C, tl.TPR, tl.RPI);
   } else {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, bf16_t, 8, kMaskNone, false>), grid, dim3(kBlock), 0, s,

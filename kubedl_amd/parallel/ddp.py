@@ -58,6 +58,11 @@ class FlatDDP:
         self.buckets: list[Bucket] = []
         self._hooks = []
         self.transport = None
+        # producers on a second stream (the ResNet engine's weight-gradient
+        # stream): a bucket's collective is issued on that stream after it has
+        # joined the current one, so it waits for both without stalling the
+        # current stream's remaining backward work
+        self.join_stream = None
         if world_size > 1:
             if broadcast_from is not None:
                 with torch.no_grad():
@@ -102,6 +107,15 @@ class FlatDDP:
             b.packer.pack()
             for s in b.slots:  # gradients now live in the bucket: free autograd's copies
                 s.param.grad = None
+        js = self.join_stream
+        if js is not None:
+            js.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(js):
+                self._issue(b)
+        else:
+            self._issue(b)
+
+    def _issue(self, b: Bucket) -> None:
         if self.transport is not None:
             b.handle = self.transport.launch(b.lo, b.hi)
         else:

@@ -70,6 +70,7 @@ class ResNetTrainer:
             from kubedl_amd.models.resnet_engine import ResNetEngine
             self.engine = ResNetEngine(model, backend="hip" if dev.type == "cuda" else "torch",
                                        grad_view=self.space.grad_view, on_ready=self.ddp.ready)
+            self.ddp.join_stream = self.engine.side
         self.opt = FusedSGD(self.space, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.opt.grad_scale = self.ddp.grad_scale
         g = torch.Generator(device="cpu").manual_seed(seed + 1000 + info.rank)

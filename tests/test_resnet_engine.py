@@ -121,11 +121,21 @@ def test_engine_torch_backend_bf16_close_to_autograd():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wgrad_stream", ["0", "1"])
 @pytest.mark.parametrize("layers,image,batch", [((1, 1, 1, 1), 64, 8), ((2, 2, 2, 2), 96, 4)])
-def test_engine_hip_matches_autograd(layers, image, batch):
+def test_engine_hip_matches_autograd(layers, image, batch, wgrad_stream, monkeypatch):
+    """``wgrad_stream=1``: weight gradients on the engine's second stream,
+    concurrent with the main stream's BN-backward / data-gradient kernels (a
+    race there -- a wgrad reading a coefficient block or operand the main
+    stream rewrites -- shows up as a gradient far off the fp32 truth).  The two
+    schedules are not compared with each other: the first MIOpen call of a
+    process may pick a different solver, so runs differ at bf16-noise level."""
+    monkeypatch.setenv("KDL_WGRAD_STREAM", wgrad_stream)
     model, ref, x, y = _setup(layers, 64, "cuda", image, batch)
     truth, tloss = _truth_of(ref, x, y)
-    loss = ResNetEngine(model, backend="hip").forward_backward(x, y)
+    eng = ResNetEngine(model, backend="hip")
+    assert (eng.side is not None) == (wgrad_stream == "1")
+    loss = eng.forward_backward(x, y)
     _ref_step(ref, x, y)
     torch.cuda.synchronize()
     torch.testing.assert_close(loss, tloss, atol=2e-2, rtol=2e-2)
