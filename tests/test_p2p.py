@@ -158,6 +158,11 @@ def _engine_worker(rank, world, port, q, transport):
     from kubedl_amd.parallel.dist import DistInfo
     from kubedl_amd.workers.resnet50 import ResNetTrainer
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KDL_ALLREDUCE=transport)
+    # the two transports' runs are compared with each other: MIOpen must pick the
+    # same solvers in both (find mode times candidates, and a different split-K
+    # wgrad solver for the stem moves its bf16 gradient by several ulps)
+    torch.backends.miopen.immediate = True
+    torch.backends.cudnn.deterministic = True
     dist.init_process_group("gloo", rank=rank, world_size=world)
     info = DistInfo(rank, world, 0, torch.device("cuda", 0), "gloo")
     tr = ResNetTrainer(info, batch=4, image=64, num_classes=10, bn_backend="hip", engine="fused",
