@@ -1,138 +1,179 @@
 #!/usr/bin/env python3
-"""Headline benchmark: PyTorchJob ResNet-50 DDP bf16 training throughput on MI355X.
+"""Headline benchmark: PyTorchJob ResNet-50 DDP bf16 training on MI355X.
 
 Metric/config from BASELINE.json ("Job launch delay (s) + steps/sec, PyTorchJob
 ResNet-50 at 1/2/4/8 MI355X"; config "PyTorchJob ResNet-50 DDP bf16, 8 workers").
 The reference publishes no number, so ``vs_baseline`` is null.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-it is started by ``torch.distributed.run`` with one rank per GPU.  W untimed
-warmup steps, then exactly K steps timed between barrier+synchronize on both
-sides, MAX over ranks; rank 0 prints one JSON line.  ``value`` is whole-job
-images/s (weak scaling: fixed per-GPU batch), ``steps_per_sec`` is reported
-alongside.  Data is synthetic (random bf16 images / labels, fixed per rank),
-weights random-init; every step is a full forward + backward + all-reduce +
-fused SGD update of the full 25.6M-parameter ResNet-50.
+Driver contract: ``python bench.py --gpus N --steps K --warmup W``.  Two ways in:
 
-``launch_delay_s`` (process start -> rank ready, i.e. process group up and
-model resident) is the rank-side half of the reference's
-first/all-pods-launch-delay metric; ``python -m kubedl_amd.cli bench-launch``
-measures the full controller path (job submitted -> all ranks Ready).
+* **No ``WORLD_SIZE`` in the environment** (the default, any N >= 1): this
+  process is a kdl control plane.  It starts an in-process ``Manager`` (store,
+  PyTorchJob controller, all-or-nothing gang allocator, node scheduler,
+  kubelet with the pre-warmed rank zygote), submits ONE PyTorchJob of N ranks
+  (1 Master + N-1 Workers, ``amd.com/gpu: 1`` each), waits for it to succeed
+  and prints rank 0's result plus the controller-path launch delays
+  (``first_pod_launch_delay_s`` / ``all_pods_launch_delay_s``: job creation ->
+  first / last rank Ready, the reference's histograms,
+  ``pkg/metrics/job_metrics.go:139-194``, observed at
+  ``pkg/job_controller/job.go:242-259``).  This process never touches the GPU
+  (it does not even import torch): the ranks are forked from the zygote or
+  spawned by the kubelet before any GPU call.  Exit status is non-zero if the
+  job did not succeed with N Ready ranks or rank 0's world size is not N.
+* **``WORLD_SIZE`` set** (``torch.distributed.run``, or ``--direct``): this
+  process IS a rank (``kubedl_amd.workers.resnet_bench.run``).
+
+Either way the timed region is the ranks' own: W untimed warm-up steps, then
+exactly K steps between a barrier + ``synchronize`` on both sides, MAX over
+ranks; ``value`` is whole-job images/s (weak scaling, fixed per-GPU batch).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
-T_PROC_START = time.time()
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
 
-# MIOpen find-db / kernel cache shipped in-tree (populated on an MI355X by
-# scripts/gpu_check.sh): conv algorithm search and kernel compiles are not
-# repeated on every fresh box.
-_ROOT = os.path.dirname(os.path.abspath(__file__))
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db", "user"))
-os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_ROOT, "miopen_db", "cache"))
+from kubedl_amd.workers import resnet_bench  # noqa: E402  (no torch import at module level)
 
-import torch  # noqa: E402
+JOB_NAME = "resnet50-bench"
 
-from kubedl_amd.parallel import dist as kdist  # noqa: E402
-from kubedl_amd.workers.resnet50 import ResNetTrainer, sync  # noqa: E402
-from kubedl_amd.workers import common  # noqa: E402
 
-METRIC = "Job launch delay (s) + steps/sec, PyTorchJob ResNet-50 at 1/2/4/8 MI355X"
-BASELINE_VALUE = None  # reference publishes no number
+def _rank_args(args) -> list:
+    out = ["--gpus", str(args.gpus), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--batch", str(args.batch), "--image", str(args.image), "--bn-backend", args.bn_backend,
+           "--conv-benchmark", str(args.conv_benchmark), "--engine", args.engine,
+           "--allreduce", args.allreduce]
+    if args.cpu:
+        out.append("--cpu")
+    if args.tiny:
+        out.append("--tiny")
+    return out
+
+
+def make_job(args) -> dict:
+    """One PyTorchJob, N ranks, one GPU each (the BASELINE.json job spec)."""
+    cmd = [sys.executable, "-u", "-m", "kubedl_amd.workers.resnet_bench"] + _rank_args(args)
+    res = {"limits": {"cpu": "2"}} if args.cpu else {"limits": {"amd.com/gpu": 1}}
+    env = [{"name": "KDL_BENCH_LAUNCHER", "value": "kdl-pytorchjob"}]
+    if os.environ.get("KDL_FAULT"):  # fault-injection rehearsal (the kubelet never leaks it by itself)
+        env.append({"name": "KDL_FAULT", "value": os.environ["KDL_FAULT"]})
+
+    def tmpl():
+        return {"spec": {"containers": [{"name": "pytorch", "image": "kubedl-amd/resnet50",
+                                         "command": list(cmd), "env": list(env), "resources": res}]}}
+    specs = {"Master": {"replicas": 1, "restartPolicy": "Never", "template": tmpl()}}
+    if args.gpus > 1:
+        specs["Worker"] = {"replicas": args.gpus - 1, "restartPolicy": "Never", "template": tmpl()}
+    return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+            "metadata": {"name": JOB_NAME, "namespace": "default"},
+            "spec": {"cleanPodPolicy": "None", "pytorchReplicaSpecs": specs}}
+
+
+def _last_json(path):
+    try:
+        for line in reversed(open(path, errors="replace").read().splitlines()):
+            line = line.strip()
+            if line.startswith("{") and line.endswith("}"):
+                return json.loads(line)
+    except (OSError, TypeError, ValueError):
+        pass
+    return None
+
+
+def _tail(path, n=40) -> str:
+    try:
+        return "\n".join(open(path, errors="replace").read().splitlines()[-n:])
+    except (OSError, TypeError):
+        return "<no log>"
+
+
+def launch_job(args) -> int:
+    from kubedl_amd.api import common as c
+    from kubedl_amd.engine.manager import Manager, ManagerOptions
+    from kubedl_amd.gang.allocator import detect_gpus
+
+    if not args.cpu:
+        have = detect_gpus().count
+        if have < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but this node has {have} GPU(s)", file=sys.stderr)
+            return 2
+    home = tempfile.mkdtemp(prefix="kdl-bench-")
+    t_submit = time.time()
+    mgr = Manager(ManagerOptions(home=home, gang_scheduler_name="kdl-gang")).start()
+    rc = 1
+    try:
+        job = mgr.apply(make_job(args))
+        uid = job["metadata"]["uid"]
+        try:
+            job = mgr.wait_for_condition("PyTorchJob", "default", JOB_NAME, ["Succeeded", "Failed"],
+                                         timeout=args.timeout)
+        except TimeoutError as e:
+            print(f"[bench] {e}", file=sys.stderr)
+            job = mgr.get("PyTorchJob", "default", JOB_NAME)
+        st = job.get("status") or {}
+        state = c.last_condition_type(st)
+        pods = [p for p in mgr.store.list("Pod", "default") if p["metadata"]["name"].startswith(JOB_NAME + "-")]
+        ready = [p for p in pods if any(x.get("type") == "Ready" and x.get("status") == "True"
+                                        for x in (p.get("status") or {}).get("conditions") or [])
+                 or (p.get("status") or {}).get("phase") == "Succeeded"]
+        master_log = mgr.kubelet.log_path("default", f"{JOB_NAME}-master-0")
+        res = _last_json(master_log)
+        if state != "Succeeded" or res is None:
+            print(f"[bench] job {JOB_NAME} ended {state!r}; rank logs:", file=sys.stderr)
+            for p in sorted(pods, key=lambda p: p["metadata"]["name"]):
+                lp = mgr.kubelet.log_path("default", p["metadata"]["name"])
+                print(f"---- {p['metadata']['name']} ----\n{_tail(lp)}", file=sys.stderr)
+            return 1
+        if res.get("n_gpus") != args.gpus or len(pods) != args.gpus:
+            print(f"[bench] world size mismatch: rank 0 reports {res.get('n_gpus')}, "
+                  f"{len(pods)} pods, --gpus {args.gpus}", file=sys.stderr)
+            return 1
+        created = c.to_epoch(job["metadata"]["creationTimestamp"])
+        first = mgr.metrics.observed["first"].get(uid)
+        alld = mgr.metrics.observed["all"].get(uid)
+        res["first_pod_launch_delay_s"] = round(first, 3) if first is not None else None
+        res["all_pods_launch_delay_s"] = round(alld, 3) if alld is not None else None
+        res["job_wall_s"] = (round(c.to_epoch(st["completionTime"]) - created, 3)
+                             if st.get("completionTime") else None)
+        res["submit_to_done_s"] = round(time.time() - t_submit, 3)
+        res["ranks_ready"] = len(ready)
+        res["gpus"] = sorted({int(g) for p in pods
+                              for g in ((p["metadata"].get("annotations") or {}).get("kubedl.io/gpus") or "")
+                              .split(",") if g})
+        print(json.dumps(res), flush=True)
+        rc = 0 if len(ready) == args.gpus else 1
+        if rc:
+            print(f"[bench] only {len(ready)}/{args.gpus} ranks became Ready", file=sys.stderr)
+        return rc
+    finally:
+        mgr.stop()
+        if not os.environ.get("KDL_BENCH_KEEP"):
+            shutil.rmtree(home, ignore_errors=True)
 
 
 def main(argv=None) -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--conv-benchmark", type=int, default=0,
-                    help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
-    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "autograd"],
-                    help="fused = explicit engine (fused 1x1-conv GEMMs + staged BN); autograd = module + autograd")
-    ap.add_argument("--allreduce", default=os.environ.get("KDL_ALLREDUCE", "rccl"), choices=["rccl", "p2p"],
-                    help="DP gradient transport for N > 1: RCCL, or the IPC peer-buffer kernel (csrc/p2p.hip)")
-    ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
-    ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    resnet_bench.add_args(ap)
+    ap.add_argument("--direct", action="store_true",
+                    help="run as a single in-process rank (no control plane); WORLD_SIZE forces this too")
+    ap.add_argument("--timeout", type=float, default=1800.0, help="job-path wait limit (s)")
     args = ap.parse_args(argv)
-    os.environ["KDL_ALLREDUCE"] = args.allreduce
-
-    if "WORLD_SIZE" not in os.environ:
-        os.environ["WORLD_SIZE"] = "1"
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("LOCAL_RANK", "0")
-    info = kdist.init_from_env("cpu" if args.cpu else None)
-    if info.world_size != args.gpus and info.rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}",
-              file=sys.stderr)
-
-    trainer = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
-                            bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark),
-                            engine=args.engine)
-    sync(info)
-    kdist.barrier(info)
-    launch_delay = kdist.all_reduce_max(time.time() - T_PROC_START, info)
-    common.signal_ready({"rank": info.rank})
-
-    for _ in range(args.warmup):
-        trainer.step()
-    sync(info)
-    kdist.barrier(info)
-    sync(info)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step()
-    sync(info)
-    kdist.barrier(info)
-    sync(info)
-    dt = kdist.all_reduce_max(time.perf_counter() - t0, info)
-    loss = float(trainer.last_loss.float().item())
-
-    n = info.world_size
-    ms = dt / args.steps * 1e3
-    imgs = args.batch * n * args.steps / dt
-    if info.rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": round(imgs, 2),
-            "unit": "images/s",
-            "n_gpus": n,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": (imgs / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16",
-            "data": "synthetic (random bf16 images/labels, random-init weights)",
-            "config": {
-                "model": "resnet50" if not args.tiny else "resnet_tiny",
-                "global_batch": args.batch * n,
-                "per_gpu_batch": args.batch,
-                "image_size": args.image,
-                "seq_len": None,
-                "parallelism": f"dp{n}",
-                "optimizer": "fused SGD-momentum (fp32 master)",
-                "bn_backend": args.bn_backend,
-                "engine": trainer.engine_kind,
-                "conv_benchmark": bool(args.conv_benchmark),
-                "allreduce": args.allreduce if n > 1 else None,
-            },
-            "steps_per_sec": round(args.steps / dt, 4),
-            "launch_delay_s": round(launch_delay, 3),
-            "final_loss": round(loss, 4),
-        }
-        print(json.dumps(out), flush=True)
-    kdist.shutdown(info)
-    return 0
+    if "WORLD_SIZE" in os.environ or args.direct:
+        if "WORLD_SIZE" not in os.environ:
+            os.environ.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+        ws = int(os.environ["WORLD_SIZE"])
+        if ws != args.gpus and int(os.environ.get("RANK", "0")) == 0:
+            print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+        return resnet_bench.run(args, "direct" if args.direct else "torchrun")
+    return launch_job(args)
 
 
 if __name__ == "__main__":

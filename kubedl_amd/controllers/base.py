@@ -31,6 +31,9 @@ log = logging.getLogger("kubedl_amd.controllers")
 
 class BaseReconciler(WorkloadController):
     info: K.KindInfo
+    # [NEW] ranks share one communicator (RCCL / gloo / rabit / XDL's PS mesh):
+    # a retryable failure of one restarts the whole gang (JobController.restart_gang)
+    collective: bool = False
 
     def __init__(self, store, recorder, metrics_registry, config: Optional[JobControllerConfig] = None,
                  gang=None):
@@ -70,6 +73,9 @@ class BaseReconciler(WorkloadController):
 
     def created_msg_kind(self) -> str:
         return self.kind
+
+    def restart_whole_gang(self, replicas) -> bool:
+        return self.collective and c.total_replicas(replicas) > 1
 
     # ------------------------------------------------------------ reconcile
     def reconcile(self, namespace: str, name: str) -> ReconcileResult:

@@ -25,6 +25,7 @@ from kubedl_amd.controllers.base import BaseReconciler
 
 class PyTorchJobReconciler(BaseReconciler):
     info = K.PYTORCHJOB
+    collective = True
 
     def created_msg_kind(self) -> str:
         return "PytorchJob"  # reference message spelling (status.go:137)

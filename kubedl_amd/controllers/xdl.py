@@ -39,6 +39,7 @@ def calculate_min_finish(job: dict, workers: int) -> int:
 
 class XDLJobReconciler(BaseReconciler):
     info = K.XDLJOB
+    collective = True
 
     def created_msg_kind(self) -> str:
         return "XdlJob"

@@ -23,6 +23,7 @@ from kubedl_amd.controllers.base import BaseReconciler
 
 class XGBoostJobReconciler(BaseReconciler):
     info = K.XGBOOSTJOB
+    collective = True
 
     def created_msg_kind(self) -> str:
         return "xgboostJob"  # reference message spelling (job.go:218)

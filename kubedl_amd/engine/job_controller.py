@@ -140,6 +140,14 @@ class WorkloadController:
         """Whether ReconcileServices runs for this replica type (PyTorch: Master only)."""
         return True
 
+    def restart_whole_gang(self, replicas: Dict[str, dict]) -> bool:
+        """[NEW] Whether a retryable failure of one replica restarts EVERY pod of
+        the job.  True for collective jobs (the ranks share an RCCL/gloo
+        communicator, which cannot survive a dead peer: the survivors would
+        block in their next collective until the process-group timeout);
+        False keeps the reference's per-pod restart (``pod.go:281-307``)."""
+        return False
+
 
 class JobController:
     def __init__(self, controller: WorkloadController, store: Store, recorder: EventRecorder,
@@ -341,14 +349,17 @@ class JobController:
             return result
 
         restart = [False]
+        deleted: set = set()
         for rtype in self.controller.get_reconcile_orders():
             spec = replicas.get(rtype)
             if spec is None:
                 continue
-            self.reconcile_pods(job, job_status, pods, rtype, spec, replicas, restart)
+            self.reconcile_pods(job, job_status, pods, rtype, spec, replicas, restart, deleted)
             if not self.controller.reconcile_services_for(rtype):
                 continue
             self.reconcile_services(job, services, rtype, spec)
+        if deleted and self.controller.restart_whole_gang(replicas):
+            self.restart_gang(job, pods, deleted)
 
         self.controller.update_job_status(job, replicas, job_status, restart[0])
 
@@ -435,8 +446,31 @@ class JobController:
             self.delete_service(job, p["metadata"]["name"], p["metadata"]["namespace"])
 
     # ------------------------------------------------------------ pods
+    def restart_gang(self, job: dict, pods: List[dict], deleted: set) -> None:
+        """[NEW] Gang-wide teardown for collective jobs (failure
+        detection): a retryable failure of one rank deletes every other pod of
+        the job as well, so all ranks are recreated together and rendezvous
+        afresh (resuming from the job's checkpoint) instead of the survivors
+        hanging in a collective with a dead peer.  The kubelet starts the new
+        pods only after the old rank processes have exited and the scheduler
+        returns the old pods' GPUs only then, so the gang's re-admission is
+        all-or-nothing against exactly the GPUs it held."""
+        others = [p for p in pods if p["metadata"]["name"] not in deleted
+                  and not p["metadata"].get("deletionTimestamp")]
+        if not others:
+            return
+        msg = (f"Restarting all {len(others) + len(deleted)} ranks of {job['metadata']['name']}: "
+               f"{', '.join(sorted(deleted))} failed with a retryable exit code")
+        logger_for_job(job, log).info(msg)
+        self.recorder.event(job, NORMAL, "GangRestart", msg)
+        for p in others:
+            try:
+                self.delete_pod(job, p)
+            except NotFound:
+                pass
+
     def reconcile_pods(self, job: dict, job_status: dict, pods: List[dict], rtype: str, spec: dict,
-                       replicas: Dict[str, dict], restart: List[bool]) -> None:
+                       replicas: Dict[str, dict], restart: List[bool], deleted: Optional[set] = None) -> None:
         rt = rtype.lower()
         rlog = logger_for_replica(job, rt, log)
         pods = self.filter_for_replica_type(pods, rt)
@@ -472,6 +506,8 @@ class JobController:
                         rlog.info("need to restart pod %s", pod["metadata"]["name"])
                         self.delete_pod(job, pod)
                         restart[0] = True
+                        if deleted is not None:
+                            deleted.add(pod["metadata"]["name"])
                 phase = pod_phase(pod)
                 if phase == "Running":
                     c.rs_inc(rs, "active")
@@ -509,10 +545,13 @@ class JobController:
             if entity is None:
                 entity = self.gang.create_gang(job, replicas)
             self.gang.bind_pod_to_gang(tmpl, entity)
+        annotations = dict(tmd.get("annotations") or {})
+        # [NEW] FIFO position of the job (a restarted gang keeps its place)
+        annotations.setdefault("kubedl.io/queue-time", job["metadata"].get("creationTimestamp") or c.now())
         pod = {"apiVersion": "v1", "kind": "Pod",
                "metadata": {"name": tmd["name"], "namespace": job["metadata"]["namespace"],
                             "labels": dict(tmd.get("labels") or {}),
-                            "annotations": dict(tmd.get("annotations") or {}),
+                            "annotations": annotations,
                             "ownerReferences": [gen_owner_reference(job)]},
                "spec": pspec,
                "status": {"phase": "Pending"}}

@@ -127,6 +127,8 @@ class Manager:
             self.scheduler = NodeScheduler(self.store, self.allocator, starvation_s=self.opts.starvation_s,
                                            metrics=self.metrics)
             self.kubelet = Kubelet(self.store, os.path.join(self.opts.home, "node"))
+            self.scheduler.holder = self.kubelet.holds
+            self.kubelet.on_worker_done = self.scheduler.wake
         # persistence (controllers/persist)
         self.persist = None
         if self.opts.object_storage or self.opts.event_storage:

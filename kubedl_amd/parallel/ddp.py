@@ -69,7 +69,7 @@ class FlatDDP:
                     dist.broadcast(space.param, broadcast_from, group=process_group)
                     space.sync_master_from_params()
             self._build_buckets(bucket_cap_mb, first_bucket_mb)
-            if p2p.wanted() and space.grad.is_cuda:
+            if p2p.wanted() and space.grad.is_cuda and p2p.single_node(process_group):
                 self.transport = p2p.P2PTransport(space.grad, process_group)
             if not direct:
                 self._install_hooks()
@@ -145,7 +145,10 @@ class FlatDDP:
             b.handle = None
             b.pending = len(b.slots)
         if self.transport is not None:
-            self.transport.check()  # host-mapped timeout bits of earlier steps (no sync)
+            # bits of EARLIER steps only (no sync here); the authoritative check
+            # follows a device sync: ResNetTrainer.check_transport, run before
+            # every checkpoint and after the last step
+            self.transport.check()
         self.space.mark_packed()
 
     @property

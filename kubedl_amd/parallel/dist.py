@@ -35,7 +35,22 @@ def env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
-def init_from_env(device: str | None = None, timeout_s: float = 600.0) -> DistInfo:
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def init_from_env(device: str | None = None, timeout_s: float | None = None,
+                  world1_group: bool = False) -> DistInfo:
+    """``world1_group``: also build a (one-rank) process group at WORLD_SIZE=1,
+    so a single-GPU job still runs its collectives through RCCL (SURVEY.md
+    §7.2 step 5).  ``timeout_s`` defaults to ``KDL_PG_TIMEOUT_S`` (600 s)."""
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("KDL_PG_TIMEOUT_S", 600))
     rank = env_int("RANK", 0)
     world = env_int("WORLD_SIZE", 1)
     local_rank = env_int("LOCAL_RANK", 0)
@@ -51,8 +66,10 @@ def init_from_env(device: str | None = None, timeout_s: float = 600.0) -> DistIn
     else:
         dev = torch.device("cpu")
         backend = "gloo"
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or world1_group) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         os.environ.setdefault("MASTER_PORT", "23456")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
@@ -79,5 +96,41 @@ def all_reduce_max(value: float, info: DistInfo) -> float:
 
 
 def shutdown(info: DistInfo) -> None:
-    if info.world_size > 1 and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- failure exit
+# A rank whose collective fails because a PEER died (gloo "Connection closed by
+# peer", an RCCL/NCCL error or watchdog abort, a P2P all-reduce timeout) exits
+# with 138 -- the reference's retryable "user retry" code
+# (pkg/util/train/train_util.go:18-52) -- instead of 1 (permanent), so an
+# ExitCode job restarts its gang instead of failing on the survivor's symptom.
+COMM_FAILURE_EXIT = 138
+_COMM_MARKERS = ("connection closed by peer", "connection reset by peer", "broken pipe", "nccl", "rccl",
+                 "gloo", "watchdog", "p2p all-reduce", "process group", "timed out")
+
+
+def is_comm_failure(exc: BaseException) -> bool:
+    dist_error = getattr(dist, "DistError", None)
+    if dist_error is not None and isinstance(exc, dist_error):
+        return True
+    if type(exc).__name__ == "P2PError":
+        return True
+    return isinstance(exc, RuntimeError) and any(m in str(exc).lower() for m in _COMM_MARKERS)
+
+
+def run_rank(main, *args, **kw) -> int:
+    """Run a worker ``main``; a collective failure exits COMM_FAILURE_EXIT."""
+    try:
+        return main(*args, **kw)
+    except BaseException as e:  # noqa: BLE001
+        if not is_comm_failure(e):
+            raise
+        import sys
+        import traceback
+        traceback.print_exc()
+        print(f"[kdl] collective failure ({type(e).__name__}): a peer rank is gone; "
+              f"exiting {COMM_FAILURE_EXIT} so the job restarts its gang", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(COMM_FAILURE_EXIT)

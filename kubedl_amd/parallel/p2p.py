@@ -18,9 +18,18 @@ for the small first/last buckets of a DP step.  RCCL stays the default
 transport when every rank is a GPU process on one node.
 
 Failure model: a peer that never arrives makes the kernel time out (bounded
-waits, default 10 s) instead of hanging the GPU; the timeout sets a bit in a
-host-mapped word that ``check()`` raises on.  The job supervisor then tears
-the gang down exactly as for an RCCL failure.
+waits, ``KDL_P2P_TIMEOUT_S``, default 300 s like a process-group timeout:
+the clock starts at kernel start, so it must cover host-side skew between
+ranks such as a rank-0 checkpoint write) instead of hanging the GPU; the
+timeout sets a bit in a host-mapped word that ``check()`` raises on (callers
+check after a device sync: before it, in-flight kernels have not reported).
+The worker then exits with the retryable collective-failure code and the job
+controller restarts the whole gang.
+
+Only ranks of ONE node can map each other's memory: the transport is used
+only when every rank reports the same host (else ``FlatDDP`` keeps RCCL), and
+the one-shot/two-shot threshold is rank 0's, so every rank picks the same
+kernel and barrier slots for a bucket.
 """
 from __future__ import annotations
 
@@ -39,12 +48,36 @@ def wanted() -> bool:
     return os.environ.get("KDL_ALLREDUCE", "rccl").lower() == "p2p"
 
 
+def _host_id() -> str:
+    import socket
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
+def single_node(group=None) -> bool:
+    """Whether every rank of ``group`` runs on this host (IPC handles are node-local)."""
+    world = dist.get_world_size(group)
+    if int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
+        return False
+    ids = [None] * world
+    dist.all_gather_object(ids, _host_id(), group=group)
+    return len(set(ids)) == 1
+
+
+def default_timeout_s() -> float:
+    return float(os.environ.get("KDL_P2P_TIMEOUT_S", 300.0))
+
+
 class P2PError(RuntimeError):
     pass
 
 
 class P2PAllReduce:
-    def __init__(self, buf: torch.Tensor, group=None, timeout_s: float = 10.0):
+    def __init__(self, buf: torch.Tensor, group=None, timeout_s: float | None = None):
         if not buf.is_cuda:
             raise ValueError("P2PAllReduce needs a GPU buffer")
         if buf.dtype not in (torch.bfloat16, torch.float32):
@@ -55,20 +88,21 @@ class P2PAllReduce:
             raise ValueError(f"P2PAllReduce supports 1..{MAX_RANKS} ranks")
         self.buf = buf
         self.group = group
-        self.timeout_s = timeout_s
+        self.timeout_s = default_timeout_s() if timeout_s is None else float(timeout_s)
         self.esz = buf.element_size()
         self.dev = buf.device.index if buf.device.index is not None else torch.cuda.current_device()
         ext = _ext.load()
         self._ext = ext
         self.sig = ext.p2p_signal_alloc(self.dev)
         self._err_host, self._err_dev = ext.p2p_error_word()
-        mine = (ext.ipc_handle(buf), ext.ipc_handle(self.sig), os.getpid())
+        oneshot = min(int(os.environ.get("KDL_P2P_ONESHOT_BYTES", 256 * 1024)), ext.p2p_oneshot_max_units() * 16)
+        mine = (ext.ipc_handle(buf), ext.ipc_handle(self.sig), os.getpid(), oneshot)
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=group)
         self._mapped: list[int] = []
         self.buf_ptrs: list[int] = []
         self.sig_ptrs: list[int] = []
-        for j, ((bh, boff), (sh, soff), _pid) in enumerate(allh):
+        for j, ((bh, boff), (sh, soff), _pid, _os) in enumerate(allh):
             if j == self.rank:
                 self.buf_ptrs.append(buf.data_ptr())
                 self.sig_ptrs.append(self.sig.data_ptr())
@@ -80,9 +114,9 @@ class P2PAllReduce:
             self.buf_ptrs.append(bbase + boff)
             self.sig_ptrs.append(sbase + soff)
         self.epoch = 0
-        # buckets up to this size take the one-shot kernel (latency-bound regime)
-        self.oneshot_bytes = min(int(os.environ.get("KDL_P2P_ONESHOT_BYTES", 256 * 1024)),
-                                 ext.p2p_oneshot_max_units() * 16)
+        # buckets up to this size take the one-shot kernel (latency-bound
+        # regime); rank 0's value, so every rank picks the same kernel
+        self.oneshot_bytes = int(allh[0][3])
         # every rank has zeroed its signals and mapped its peers before anyone signals
         torch.cuda.synchronize(self.dev)
         dist.barrier(group=group)

@@ -27,7 +27,12 @@ For every pod bound to this node (``spec.nodeName``, GPUs in the
    in place with exponential back-off (``restartCount``++, pod stays Running,
    which is what ``pastBackoffLimit`` counts); Never leaves it terminated;
 6. on pod deletion sends SIGTERM to the process group, waits
-   ``terminationGracePeriodSeconds`` (default 5 s locally), then SIGKILL.
+   ``terminationGracePeriodSeconds`` (default 5 s locally), then SIGKILL;
+7. [NEW] gang teardown barrier: a new pod of a job does not start its
+   containers while another pod of the same job is still terminating (a gang
+   restart deletes every rank; the replacements must not race the old ranks
+   for the master port or the GPU), and the scheduler keeps a deleted pod's
+   GPUs reserved until its processes are gone (``holds``).
 """
 from __future__ import annotations
 
@@ -97,6 +102,7 @@ class PodWorker(threading.Thread):
         self.grace = float((pod.get("spec") or {}).get("terminationGracePeriodSeconds",
                                                       kubelet.default_grace))
         self.gpus = [g for g in ((md.get("annotations") or {}).get(GPU_ANNOTATION) or "").split(",") if g]
+        self.job_label = (md.get("labels") or {}).get(c.JOB_NAME_LABEL, "")
         self.containers: List[_Container] = []
         self.start_time = c.now()
 
@@ -338,7 +344,18 @@ class PodWorker(threading.Thread):
         finally:
             self.k._worker_done(self)
 
+    def _wait_peers_gone(self) -> None:
+        """Gang teardown barrier: wait (bounded) until no other pod of this job
+        is still terminating."""
+        t_end = time.monotonic() + self.k.default_grace + 15.0
+        while self.k.terminating_peers(self) and time.monotonic() < t_end:
+            if self.deleted.wait(self.k.poll_interval * 5):
+                return
+
     def _run(self) -> None:
+        self._wait_peers_gone()
+        if self.deleted.is_set():
+            return
         os.makedirs(os.path.join(self.sandbox, "logs"), exist_ok=True)
         os.makedirs(os.path.join(self.sandbox, "root"), exist_ok=True)
         spec = self.pod.get("spec") or {}
@@ -527,6 +544,7 @@ class Kubelet:
         self.resolver = ServiceResolver(store)
         self._workers: Dict[str, PodWorker] = {}
         self._lock = threading.Lock()
+        self.on_worker_done = None  # callback(uid) once a pod's processes are gone
         os.makedirs(os.path.join(root, "pods"), exist_ok=True)
         self._cancel = None
         if zygote is None:
@@ -588,6 +606,21 @@ class Kubelet:
             if not hasattr(self, "_done"):
                 self._done = set()
             self._done.add(w.uid)
+        cb = self.on_worker_done
+        if cb is not None:
+            cb(w.uid)
+
+    def holds(self, uid: str) -> bool:
+        """Whether the pod ``uid`` still has a worker (live or terminating processes)."""
+        with self._lock:
+            return uid in self._workers
+
+    def terminating_peers(self, w: PodWorker) -> List[str]:
+        if not w.job_label:
+            return []
+        with self._lock:
+            return [o.name for o in self._workers.values()
+                    if o is not w and o.deleted.is_set() and o.ns == w.ns and o.job_label == w.job_label]
 
     def running_pods(self) -> List[str]:
         with self._lock:

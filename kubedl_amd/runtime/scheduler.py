@@ -14,8 +14,13 @@ Replaces kube-scheduler + kube-batch for one node:
   in the currently free GPUs may start while the head waits, until the head
   has waited ``starvation_s`` -- then backfill stops so big gangs cannot starve;
 * binding writes ``spec.nodeName``, the ``kubedl.io/gpus`` annotation and the
-  ``PodScheduled`` condition; GPUs return to the pool when the pod is deleted
-  or reaches a terminal phase.
+  ``PodScheduled`` condition; GPUs return to the pool when the pod reaches a
+  terminal phase, or when it is deleted AND the kubelet no longer holds its
+  processes (``holder``): a rank being torn down keeps its GPU until it has
+  exited, so a gang restart never overlaps old and new ranks on one device;
+* a scheduling unit's queue age is the owning job's creation time
+  (``kubedl.io/queue-time``), so a gang re-admitted after a restart keeps its
+  place in the FIFO instead of queueing behind later jobs.
 """
 from __future__ import annotations
 
@@ -45,6 +50,15 @@ def pod_gpus(pod: dict) -> int:
     return c.pod_template_gpus({"spec": pod.get("spec") or {}})
 
 
+QUEUE_TIME_ANNOTATION = "kubedl.io/queue-time"
+
+
+def _queue_age(pod: dict) -> float:
+    md = pod["metadata"]
+    t = c.to_epoch((md.get("annotations") or {}).get(QUEUE_TIME_ANNOTATION))
+    return t if t is not None else (c.to_epoch(md.get("creationTimestamp")) or 0)
+
+
 def is_terminal(pod: dict) -> bool:
     return (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed")
 
@@ -63,6 +77,9 @@ class NodeScheduler:
         self._owner_of_pod: Dict[str, str] = {}
         self._unsched_marked: set = set()
         self._lock = threading.Lock()
+        # uid -> still has processes (kubelet.holds); deleted pods' GPUs wait for it
+        self.holder = None
+        self._deferred: Dict[str, dict] = {}
         self._cancel = store.watch(self._on_event)
 
     # ------------------------------------------------------------ lifecycle
@@ -81,7 +98,10 @@ class NodeScheduler:
     def _on_event(self, etype: str, obj: dict) -> None:
         kind = obj.get("kind")
         if kind == "Pod":
-            if etype == DELETED or (etype == MODIFIED and is_terminal(obj)):
+            if etype == DELETED and self.holder is not None and self.holder(obj["metadata"].get("uid", "")):
+                with self._lock:
+                    self._deferred[pod_key(obj)] = obj
+            elif etype == DELETED or (etype == MODIFIED and is_terminal(obj)):
                 self._release(obj)
             self._wake.set()
         elif kind == "PodGroup":
@@ -98,12 +118,26 @@ class NodeScheduler:
                 self.metrics.gpus_allocated.set(self.alloc.used())
             self._wake.set()
 
+    def wake(self, uid: str = "") -> None:
+        """Kubelet callback: a pod's processes are gone (its deferred GPUs can go back)."""
+        self._wake.set()
+
+    def _release_deferred(self) -> None:
+        with self._lock:
+            items = list(self._deferred.items())
+        for k, pod in items:
+            if self.holder is None or not self.holder(pod["metadata"].get("uid", "")):
+                with self._lock:
+                    self._deferred.pop(k, None)
+                self._release(pod)
+
     def _loop(self) -> None:
         while not self._stop.is_set():
             self._wake.wait(timeout=1.0)
             self._wake.clear()
             if self._stop.is_set():
                 break
+            self._release_deferred()
             try:
                 self.schedule_once()
             except Exception:
@@ -132,10 +166,10 @@ class NodeScheduler:
             ns, name = gkey.split("/", 1)
             pg = self.store.try_get("PodGroup", ns, name)
             min_member = int(((pg or {}).get("spec") or {}).get("minMember", len(members)))
-            age = min(c.to_epoch(p["metadata"].get("creationTimestamp")) or 0 for p in members)
+            age = min(_queue_age(p) for p in members)
             units.append((age, "gang:" + gkey, unbound, min_member if len(members) < min_member else 0))
         for p in singles:
-            age = c.to_epoch(p["metadata"].get("creationTimestamp")) or 0
+            age = _queue_age(p)
             units.append((age, "pod:" + pod_key(p), [p], 0))
         units.sort(key=lambda u: u[0])
         return units

@@ -31,7 +31,7 @@ from typing import List, Optional
 
 PRELOAD = ("torch", "torch.distributed", "torch.nn.functional", "kubedl_amd.workers.common",
            "kubedl_amd.parallel.dist", "kubedl_amd.ops.optim", "kubedl_amd.models.resnet",
-           "kubedl_amd.workers.resnet50", "kubedl_amd.workers.pytorch_dist", "kubedl_amd.workers.xdl_ctr",
+           "kubedl_amd.workers.resnet50", "kubedl_amd.workers.resnet_bench", "kubedl_amd.workers.pytorch_dist", "kubedl_amd.workers.xdl_ctr",
            "kubedl_amd.workers.xgboost_dist", "kubedl_amd.workers.tf_stub")
 
 

@@ -22,6 +22,7 @@ os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db", "u
 os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_ROOT, "miopen_db", "cache"))
 
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 from kubedl_amd.models.resnet import resnet50, resnet_tiny  # noqa: E402
@@ -81,6 +82,7 @@ class ResNetTrainer:
         self.y = torch.randint(0, num_classes, (batch,), generator=g).to(dev)
         self.batch = batch
         self.last_loss = None
+        self._loss_work = None
 
     def step(self) -> torch.Tensor:
         self.space.zero_grad()
@@ -96,8 +98,28 @@ class ResNetTrainer:
             self.ddp.finish()
         with trace_range("optimizer"):
             self.opt.step()
-        self.last_loss = loss.detach()
+        loss = loss.detach().float().reshape(1)
+        if dist.is_initialized():
+            # the step's loss summed over ranks (reporting); at world 1 this is
+            # the collective that keeps the RCCL path exercised in every step
+            loss = loss.clone()
+            self._loss_work = dist.all_reduce(loss, async_op=True)
+        self.last_loss = loss
+        return loss
+
+    def loss(self) -> torch.Tensor:
+        """The last step's loss summed over ranks (waits for its all-reduce)."""
+        if self._loss_work is not None:
+            self._loss_work.wait()
+            self._loss_work = None
         return self.last_loss
+
+    def check_transport(self) -> None:
+        """Raise if a P2P all-reduce of any step so far timed out.  Call after
+        a device synchronisation: the kernels report through host-mapped
+        memory, so before a sync the bits of in-flight steps are not there yet."""
+        if self.ddp.transport is not None:
+            self.ddp.transport.check()
 
     # ------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
@@ -126,7 +148,7 @@ def sync(info: kdist.DistInfo) -> None:
 
 def run(args) -> dict:
     t_start = time.time()
-    info = kdist.init_from_env("cpu" if args.cpu else None)
+    info = kdist.init_from_env("cpu" if args.cpu else None, world1_group=True)
     common.signal_ready({"rank": info.rank})
     tr = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
                        bn_backend=args.bn_backend, engine=args.engine)
@@ -144,9 +166,12 @@ def run(args) -> dict:
         tr.step()
         if steplog.enabled:
             sync(info)
-            steplog.write(i + 1, (time.perf_counter() - t) * 1e3, loss=float(tr.last_loss.float().item()))
+            steplog.write(i + 1, (time.perf_counter() - t) * 1e3, loss=float(tr.loss().item()) / info.world_size)
         if ckpt.due(i + 1):
+            sync(info)
+            tr.check_transport()  # never persist weights of a timed-out all-reduce
             ckpt.save(i + 1, tr.state_dict())
+            kdist.barrier(info)  # peers wait for the save instead of racing ahead into timeouts
         common.maybe_inject_fault(info.rank, i)
 
     for i in range(done, args.warmup):
@@ -162,9 +187,10 @@ def run(args) -> dict:
     kdist.barrier(info)
     sync(info)
     dt = time.perf_counter() - t0
+    tr.check_transport()
     dt = kdist.all_reduce_max(dt, info)
     nsteps = len(timed)
-    loss = float(tr.last_loss.item()) if tr.last_loss is not None else float("nan")
+    loss = float(tr.loss().item()) / info.world_size if tr.last_loss is not None else float("nan")
     res = {
         "rank": info.rank, "world_size": info.world_size, "steps": nsteps,
         "seconds": dt, "ms_per_step": dt / max(nsteps, 1) * 1e3,
@@ -201,4 +227,4 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    raise SystemExit(main())
+    raise SystemExit(kdist.run_rank(main))

@@ -1,0 +1,144 @@
+"""Rank side of the headline benchmark (BASELINE.json: "Job launch delay (s) +
+steps/sec, PyTorchJob ResNet-50 at 1/2/4/8 MI355X").
+
+One process per GPU, started either by the kdl control plane (``bench.py``
+with no ``WORLD_SIZE`` in its environment submits a PyTorchJob whose ranks run
+``python -m kubedl_amd.workers.resnet_bench``; the controller injects
+``MASTER_ADDR/MASTER_PORT/WORLD_SIZE/RANK`` exactly as the reference's
+``controllers/pytorch/pytorchjob_controller.go:180-233`` does) or by an
+external ``torch.distributed.run`` (``bench.py`` calls :func:`run` in-process).
+
+W untimed warm-up steps, then exactly K steps timed between a barrier and a
+``synchronize`` on both sides, MAX over ranks.  Rank 0 prints one JSON line
+(the driver contract): ``value`` = whole-job images/s (weak scaling: fixed
+per-GPU batch).  Every step is a full forward + backward + gradient
+all-reduce + fused SGD update of the full 25.6M-parameter ResNet-50 on
+synthetic bf16 images and random-init weights; the step's loss is summed over
+ranks with RCCL (so the collective path runs even at world 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+T_PROC_START = time.time()
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# MIOpen find-db / kernel cache shipped in-tree: no conv algorithm search or
+# kernel compile on a fresh box
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db", "user"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_ROOT, "miopen_db", "cache"))
+
+METRIC = "Job launch delay (s) + steps/sec, PyTorchJob ResNet-50 at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def add_args(ap: argparse.ArgumentParser) -> None:
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--bn-backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--conv-benchmark", type=int, default=0,
+                    help="1 = MIOpen find mode (torch.backends.cudnn.benchmark)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "autograd"],
+                    help="fused = explicit engine (fused conv GEMMs + staged BN); autograd = module + autograd")
+    ap.add_argument("--allreduce", default=os.environ.get("KDL_ALLREDUCE", "rccl"), choices=["rccl", "p2p"],
+                    help="DP gradient transport for N > 1: RCCL, or the IPC peer-buffer kernel (csrc/p2p.hip)")
+    ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
+    ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="ResNet-50 DDP bf16 benchmark rank")
+    add_args(ap)
+    return ap
+
+
+def run(args, launcher: str) -> int:
+    os.environ["KDL_ALLREDUCE"] = args.allreduce
+    import torch  # noqa: F401  (first GPU-touching import happens in the rank only)
+    from kubedl_amd.parallel import dist as kdist
+    from kubedl_amd.workers import common
+    from kubedl_amd.workers.resnet50 import ResNetTrainer, sync
+
+    info = kdist.init_from_env("cpu" if args.cpu else None,
+                               world1_group=os.environ.get("KDL_WORLD1_PG", "1") != "0")
+    trainer = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
+                            bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark),
+                            engine=args.engine)
+    sync(info)
+    kdist.barrier(info)
+    rank_ready_s = kdist.all_reduce_max(time.time() - T_PROC_START, info)
+    common.signal_ready({"rank": info.rank})
+
+    fault = bool(os.environ.get("KDL_FAULT"))
+    for i in range(args.warmup):
+        trainer.step()
+        if fault:
+            common.maybe_inject_fault(info.rank, i)
+    sync(info)
+    kdist.barrier(info)
+    sync(info)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step()
+    sync(info)
+    kdist.barrier(info)
+    sync(info)
+    dt = kdist.all_reduce_max(time.perf_counter() - t0, info)
+    trainer.check_transport()  # a timed-out P2P all-reduce must fail the run, not report a number
+    loss = float(trainer.loss().float().item())
+
+    n = info.world_size
+    ms = dt / args.steps * 1e3
+    imgs = args.batch * n * args.steps / dt
+    if info.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(imgs, 2),
+            "unit": "images/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (imgs / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (random bf16 images/labels, random-init weights)",
+            "config": {
+                "model": "resnet50" if not args.tiny else "resnet_tiny",
+                "global_batch": args.batch * n,
+                "per_gpu_batch": args.batch,
+                "image_size": args.image,
+                "seq_len": None,
+                "parallelism": f"dp{n}",
+                "optimizer": "fused SGD-momentum (fp32 master)",
+                "bn_backend": args.bn_backend,
+                "engine": trainer.engine_kind,
+                "conv_benchmark": bool(args.conv_benchmark),
+                "allreduce": args.allreduce if n > 1 else None,
+                "launcher": launcher,
+            },
+            "steps_per_sec": round(args.steps / dt, 4),
+            "rank_ready_s": round(rank_ready_s, 3),
+            "final_loss": round(loss / n, 4),
+        }
+        print(json.dumps(out), flush=True)
+    kdist.shutdown(info)
+    return 0
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    return run(args, os.environ.get("KDL_BENCH_LAUNCHER", "kdl-pytorchjob"))
+
+
+if __name__ == "__main__":
+    from kubedl_amd.parallel.dist import run_rank
+    sys.exit(run_rank(main))

@@ -109,4 +109,5 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from kubedl_amd.parallel.dist import run_rank
+    sys.exit(run_rank(main))

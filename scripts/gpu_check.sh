@@ -33,11 +33,13 @@ want() { [ "$STEPS" = "all" ] || [[ ",$STEPS," == *",$1,"* ]]; }
 python -c "import kubedl_amd._C" 2>/dev/null || python -m kubedl_amd.ops.build > gpurun_out/build.log 2>&1
 
 want smoke  && run_step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-want pytest && run_step pytest 900 python -m pytest tests -m gpu -q
-want bench  && run_step bench_hip 600 python bench.py --steps 20 --warmup 8
-want benchab && run_step bench_torch 600 python bench.py --steps 20 --warmup 8 --bn-backend torch
-want prof   && run_step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 3
-want benchfind && run_step bench_find 900 python bench.py --steps 20 --warmup 8 --conv-benchmark 1
+want pytest && run_step pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+want bench  && run_step bench_job 600 python bench.py --gpus 1 --steps 20 --warmup 5
+want benchdirect && run_step bench_direct 600 python bench.py --direct --gpus 1 --steps 20 --warmup 5
+want bench2 && run_step bench_job2 600 python bench.py --gpus 1 --steps 20 --warmup 5
+want benchab && run_step bench_torch 600 python bench.py --direct --steps 20 --warmup 8 --bn-backend torch
+want prof   && run_step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --direct --steps 5 --warmup 3
+want benchfind && run_step bench_find 900 python bench.py --direct --steps 20 --warmup 8 --conv-benchmark 1
 want launch && run_step bench_launch 600 python -m kubedl_amd.cli bench-launch --jobs 1 --gpus 1 --steps 20 --warmup 5
 if want bnsweep; then
   for mr in ${SWEEP:-128 256 512 1024}; do

@@ -342,8 +342,13 @@ def test_gang_all_or_nothing(tmp_path):
         assert m.allocator.used() == 8
         pods3 = [p for p in m.store.list("Pod") if p["metadata"]["name"].startswith("g3-")]
         assert len(pods3) == 4 and all(not p["spec"].get("nodeName") for p in pods3)
-        unsched = [x for p in pods3 for x in p["status"].get("conditions", []) if x.get("reason") == "Unschedulable"]
-        assert unsched
+        def unsched():
+            return [x for p in m.store.list("Pod") if p["metadata"]["name"].startswith("g3-")
+                    for x in p["status"].get("conditions", []) if x.get("reason") == "Unschedulable"]
+        t_end = time.time() + 10
+        while not unsched() and time.time() < t_end:  # the scheduler marks them on its next pass
+            time.sleep(0.02)
+        assert unsched()
         pg = m.store.get("PodGroup", "default", "g1")
         assert pg["spec"]["minMember"] == 4
         # each running gang sits inside one NUMA half
