@@ -890,7 +890,25 @@ void bn_stage_bwd_apply(const at::Tensor& g, const at::Tensor& x, const at::Tens
 
 }  // namespace
 
+// ------------------------------------------------------------------ streams
+int64_t make_stream_py(bool dedicated, int64_t priority) {
+  hipStream_t s = nullptr;
+  check_hip(kdl::make_stream(dedicated, static_cast<int>(priority), &s), "make_stream");
+  return reinterpret_cast<int64_t>(s);
+}
+
+void destroy_stream_py(int64_t handle) {
+  if (handle) check_hip(hipStreamDestroy(reinterpret_cast<hipStream_t>(handle)), "hipStreamDestroy");
+}
+
+void spin_py(double microseconds) { check_hip(kdl::spin(cur_stream(), microseconds), "spin"); }
+
+
 PYBIND11_MODULE(_C, m) {
+  m.def("make_stream", &make_stream_py, "new HIP stream (dedicated=True: own hardware queue via a full CU mask)",
+        py::arg("dedicated"), py::arg("priority") = 0);
+  m.def("destroy_stream", &destroy_stream_py, "destroy a stream from make_stream");
+  m.def("spin", &spin_py, "one wave busy-waiting N microseconds on the current stream");
   m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC");
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC");

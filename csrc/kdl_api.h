@@ -196,4 +196,10 @@ hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, fl
 
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 
+// ---- streams.hip
+// dedicated = the stream gets a hardware queue of its own (full CU mask).
+hipError_t make_stream(bool dedicated, int priority, hipStream_t* out);
+// one wave busy-waiting ``microseconds`` (queue-concurrency probe)
+hipError_t spin(hipStream_t s, double microseconds);
+
 }  // namespace kdl

@@ -451,7 +451,8 @@ class ResNetEngine:
         # main stream's backward finalize of the same BN.
         self.side = None
         if self.K.name == "hip" and os.environ.get("KDL_WGRAD_STREAM", "1") == "1":
-            self.side = torch.cuda.Stream(self.dev)
+            from kubedl_amd.ops.streams import side_stream
+            self.side = side_stream(self.dev)  # (ops/streams.py)
 
     def _refresh_wt(self) -> None:
         """HIP path: the data-gradient GEMMs' B operands -- W^T of every 1x1 conv

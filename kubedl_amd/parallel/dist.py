@@ -73,7 +73,7 @@ def init_from_env(device: str | None = None, timeout_s: float | None = None,
         os.environ.setdefault("MASTER_PORT", "23456")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        if backend == "nccl":
+        if backend == "nccl" and os.environ.get("KDL_PG_EAGER", "1") != "0":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
     return DistInfo(rank, world, local_rank, dev, backend)

@@ -34,6 +34,9 @@ from kubedl_amd.utils.trace import StepLog, trace_range
 from kubedl_amd.workers import common
 
 
+_LOSS_ALLREDUCE = os.environ.get("KDL_LOSS_ALLREDUCE", "1") != "0"
+
+
 class ResNetTrainer:
     def __init__(self, info: kdist.DistInfo, batch: int = 256, image: int = 224,
                  num_classes: int = 1000, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
@@ -83,8 +86,24 @@ class ResNetTrainer:
         self.batch = batch
         self.last_loss = None
         self._loss_work = None
+        # the step runs on a non-blocking stream of its own, never the null
+        # stream: with an RCCL process group present the null stream loses the
+        # engine's side-stream overlap (-9 %, ops/streams.py); the caller's
+        # stream waits for it after each step
+        from kubedl_amd.ops.streams import compute_stream
+        self.stream = compute_stream(dev)
 
     def step(self) -> torch.Tensor:
+        if self.stream is None:
+            return self._step()
+        caller = torch.cuda.current_stream(self.info.device)
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            loss = self._step()
+        caller.wait_stream(self.stream)
+        return loss
+
+    def _step(self) -> torch.Tensor:
         self.space.zero_grad()
         with trace_range("forward_backward"):
             if self.engine is not None:
@@ -99,7 +118,7 @@ class ResNetTrainer:
         with trace_range("optimizer"):
             self.opt.step()
         loss = loss.detach().float().reshape(1)
-        if dist.is_initialized():
+        if dist.is_initialized() and _LOSS_ALLREDUCE:
             # the step's loss summed over ranks (reporting); at world 1 this is
             # the collective that keeps the RCCL path exercised in every step
             loss = loss.clone()
