@@ -53,7 +53,12 @@ class ResNetTrainer:
             # MIOpen find (benchmark) vs immediate-mode heuristics: A/B'd in profiles/
             torch.backends.cudnn.benchmark = bool(conv_benchmark)
         torch.manual_seed(seed)
-        model = resnet_tiny(num_classes) if tiny else resnet50(num_classes)
+        if dev.type == "cuda":
+            torch.cuda.manual_seed(seed)
+        # built directly on the rank's device: the weight init runs on the GPU
+        # instead of ~0.5 s of CPU RNG + a host->device copy (launch delay)
+        with torch.device(dev):
+            model = resnet_tiny(num_classes) if tiny else resnet50(num_classes)
         model.set_bn_backend(bn_backend)
         model = model.to(dev)
         if dev.type == "cuda":
@@ -77,15 +82,18 @@ class ResNetTrainer:
             self.ddp.join_stream = self.engine.side
         self.opt = FusedSGD(self.space, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.opt.grad_scale = self.ddp.grad_scale
-        g = torch.Generator(device="cpu").manual_seed(seed + 1000 + info.rank)
-        x = torch.randn(batch, 3, image, image, generator=g).to(dev, dtype)
+        # synthetic batch, generated where it is used (no 77 MB host->device copy)
+        g = torch.Generator(device=dev).manual_seed(seed + 1000 + info.rank)
         if dev.type == "cuda":
-            x = x.contiguous(memory_format=torch.channels_last)
+            x = torch.randn(batch, image, image, 3, generator=g, device=dev, dtype=dtype).permute(0, 3, 1, 2)
+        else:
+            x = torch.randn(batch, 3, image, image, generator=g).to(dtype)
         self.x = x
-        self.y = torch.randint(0, num_classes, (batch,), generator=g).to(dev)
+        self.y = torch.randint(0, num_classes, (batch,), generator=g, device=dev)
         self.batch = batch
         self.last_loss = None
         self._loss_work = None
+        self._loss_sum = None
         # the step runs on a non-blocking stream of its own, never the null
         # stream: with an RCCL process group present the null stream loses the
         # engine's side-stream overlap (-9 %, ops/streams.py); the caller's
@@ -118,20 +126,22 @@ class ResNetTrainer:
         with trace_range("optimizer"):
             self.opt.step()
         loss = loss.detach().float().reshape(1)
+        self.last_loss = loss  # this rank's loss (returned)
+        self._loss_sum = loss
         if dist.is_initialized() and _LOSS_ALLREDUCE:
             # the step's loss summed over ranks (reporting); at world 1 this is
             # the collective that keeps the RCCL path exercised in every step
-            loss = loss.clone()
-            self._loss_work = dist.all_reduce(loss, async_op=True)
-        self.last_loss = loss
+            self._loss_sum = loss.clone()
+            self._loss_work = dist.all_reduce(self._loss_sum, async_op=True)
         return loss
 
     def loss(self) -> torch.Tensor:
-        """The last step's loss summed over ranks (waits for its all-reduce)."""
+        """The last step's loss summed over ranks (waits for its all-reduce;
+        at world 1 or without a process group: this rank's loss)."""
         if self._loss_work is not None:
             self._loss_work.wait()
             self._loss_work = None
-        return self.last_loss
+        return self._loss_sum
 
     def check_transport(self) -> None:
         """Raise if a P2P all-reduce of any step so far timed out.  Call after

@@ -66,15 +66,23 @@ def run(args, launcher: str) -> int:
     from kubedl_amd.workers import common
     from kubedl_amd.workers.resnet50 import ResNetTrainer, sync
 
+    t_import = time.time()
     info = kdist.init_from_env("cpu" if args.cpu else None,
                                world1_group=os.environ.get("KDL_WORLD1_PG", "1") != "0")
+    t_pg = time.time()
+    # Ready (the rank has started and its process group is up) --
+    # the timestamp of the controller's launch-delay histograms
+    common.signal_ready({"rank": info.rank})
     trainer = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
                             bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark),
                             engine=args.engine)
     sync(info)
+    t_model = time.time()
     kdist.barrier(info)
+    # process start -> model resident on every rank
     rank_ready_s = kdist.all_reduce_max(time.time() - T_PROC_START, info)
-    common.signal_ready({"rank": info.rank})
+    print(f"[bench] rank {info.rank} start: imports {t_import - T_PROC_START:.3f}s, process group "
+          f"{t_pg - t_import:.3f}s, model+data {t_model - t_pg:.3f}s", file=sys.stderr, flush=True)
 
     fault = bool(os.environ.get("KDL_FAULT"))
     for i in range(args.warmup):
