@@ -908,6 +908,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("make_stream", &make_stream_py, "new HIP stream (dedicated=True: own hardware queue via a full CU mask)",
         py::arg("dedicated"), py::arg("priority") = 0);
   m.def("destroy_stream", &destroy_stream_py, "destroy a stream from make_stream");
+  m.def("set_gemm_core", &kdl::set_gemm_core_mode, "conv GEMM main loop: -1 by shape, 0 register-staged, 1 LDS-DMA");
+  m.def("set_igemm_cfg", &kdl::set_igemm_cfg, "force an LDS-DMA tile config (-1 = by shape)");
+  m.def("get_gemm_core", &kdl::gemm_core_mode, "current conv GEMM main-loop mode");
   m.def("spin", &spin_py, "one wave busy-waiting N microseconds on the current stream");
   m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC");

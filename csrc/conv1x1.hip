@@ -53,82 +53,16 @@
 #include <type_traits>
 
 #include "common.h"
+#include "gemm_epi.h"
 #include "kdl_api.h"
 
 namespace kdl {
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-typedef __attribute__((ext_vector_type(16))) float f32x16_t;
-typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+using namespace gemm;  // GemmParams, EPI_*, G_*, fragment types, epilogue (csrc/gemm_epi.h)
 
 constexpr int kThreads = 256;
 constexpr int BK = 64;
-constexpr int LDK = BK + 8;  // padded LDS row (bf16)
-constexpr int kRep = 32;     // replica count of the BN workspace (== bn_act.hip kReplicas)
-
-enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
-// A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s)
-enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2 };
-
-struct GemmParams {
-  const bf16_t* A;
-  const bf16_t* B;
-  bf16_t* C;
-  int M, N, K;
-  // A row gather (stride-s 1x1 conv): out row (n, oh, ow) reads in row (n, oh*s, ow*s)
-  int Hout, Wout, Hin, Win, stride;
-  int Cin;                // GATHER == G_CONV3: channels per tap (K = 9 * Cin, Cin % 64 == 0)
-  const float* pro_coef;  // [2K] (3x3: [2Cin]): scale | shift
-  // epilogue operands
-  const float* shift;   // STATS: [N]
-  float* acc;           // STATS/MASKX/RESBITS: [kRep][2N]
-  const bf16_t* ex;     // MASKX/RESBITS: BN input x [M, N]
-  const float* emean;   // [N]
-  const float* ecoef;   // MASKX: [2N] forward scale | shift of that BN
-  const bf16_t* eres;   // RESBITS/RES: d(identity)
-  int res_stride;       // 1: eres is [M, N]; s > 1: eres is [Nb, Hin/s.., N] sampled at (h%s==0, w%s==0)
-  int res_H, res_W;     // geometry of the C rows (= input resolution) for the strided residual
-  const uint8_t* ebits; // RESBITS: [M, N/8]
-  const bf16_t* ex2;    // RESBITS: optional second BN input (downsample BN)
-  const float* emean2;
-  float* acc2;          // its replicas [kRep][2N]
-};
-
-__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
-
-__device__ __forceinline__ void unpack8(const uint4 v, float (&o)[8]) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    o[2 * i] = __uint_as_float(w[i] << 16);
-    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
-// packed-fp32 pairs: v_pk_add_f32 / v_pk_fma_f32 halve the epilogue VALU count
-typedef __attribute__((ext_vector_type(2))) float f2_t;
-
-__device__ __forceinline__ void unpack4x2(const uint4 v, f2_t (&o)[4]) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f2_t{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
-}
-
-__device__ __forceinline__ uint32_t pack2(const f2_t v) { return pack_bf16x2(v.x, v.y); }
-
-__device__ __forceinline__ f2_t pfma(const f2_t a, const f2_t b, const f2_t c) {
-  return __builtin_elementwise_fma(a, b, c);
-}
-
-__device__ __forceinline__ uint4 pack8(const float (&o)[8]) {
-  return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
-                    pack_bf16x2(o[6], o[7]));
-}
-
-__device__ __forceinline__ void atomic_add_f32(float* p, float v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
@@ -151,9 +85,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // buffer, so the next tile's first K-step stays in registers through the
   // epilogue (which then owns both buffers) and is staged after it.
   constexpr bool SPLIT_C = BM * LDC > kBuf;
-  constexpr int CPR = BN / 8;              // 16-B chunks per output row
-  constexpr int RPP = kThreads / CPR;      // rows per epilogue pass
-  constexpr bool REDUCE = EPI == EPI_STATS || EPI == EPI_MASKX || EPI == EPI_RESBITS;
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int nblk = gridDim.x;
@@ -273,12 +204,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   };
 
-  // per-thread reduction state: 8 channels of column chunk (t % CPR)
-  const int ec = t % CPR, er0 = t / CPR;
-  const int ch0 = n0 + ec * 8;
-  f2_t s1[4], s2[4], s3[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) { s1[q] = f2_t{0.f, 0.f}; s2[q] = s1[q]; s3[q] = s1[q]; }
+  Epilogue<BM, BN, kThreads, EPI> epi;
+  epi.init(t, n0);
 
   int tm = gm;
   if (tm < tiles_m) {
@@ -325,167 +252,16 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       __syncthreads();
       cur ^= 1;
     }
-    // ---- epilogue.  The row-side operands (BN input x, d(identity), mask bits)
-    // of the first prefetch group are issued before the accumulators go to LDS
-    // so their HBM latency overlaps the LDS round trip; later groups are issued
-    // a group ahead of their use.
-    constexpr int NP = BM / RPP;                       // rows per thread per tile
-    constexpr int PG = (EPI == EPI_RESBITS && NP > 4) ? 4 : NP;  // prefetch group (register budget)
-    constexpr bool LX = EPI == EPI_MASKX || EPI == EPI_RESBITS;
-    constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES;
-    uint4 pxv[PG], prv[PG], px2[PG];
-    uint32_t pbv[PG];
-    bool prok[PG];
-    auto prefetch = [&](int g0) {
-#pragma unroll
-      for (int i = 0; i < PG; ++i) {
-        const int m = tm * BM + (g0 + i) * RPP + er0;
-        const bool ok = m < M;
-        const int64_t go = static_cast<int64_t>(ok ? m : 0) * N + ch0;
-        if constexpr (LX) pxv[i] = ok ? ld16(p.ex + go) : make_uint4(0, 0, 0, 0);
-        if constexpr (EPI == EPI_RESBITS) {
-          pbv[i] = ok ? p.ebits[static_cast<int64_t>(m) * (N / 8) + (ch0 >> 3)] : 0u;
-          px2[i] = (ok && p.ex2) ? ld16(p.ex2 + go) : make_uint4(0, 0, 0, 0);
-        }
-        if constexpr (LR) {
-          const bf16_t* rp = nullptr;
-          if (ok) {
-            if (p.res_stride == 1) {
-              rp = p.eres + go;
-            } else {
-              const int hw = p.res_H * p.res_W;
-              const int nimg = m / hw, rem = m - nimg * hw;
-              const int h = rem / p.res_W, w = rem - h * p.res_W;
-              if (h % p.res_stride == 0 && w % p.res_stride == 0) {
-                const int Ho = (p.res_H + p.res_stride - 1) / p.res_stride;
-                const int Wo = (p.res_W + p.res_stride - 1) / p.res_stride;
-                rp = p.eres + ((static_cast<int64_t>(nimg) * Ho + h / p.res_stride) * Wo + w / p.res_stride) * N + ch0;
-              }
-            }
-          }
-          prok[i] = rp != nullptr;
-          prv[i] = rp ? ld16(rp) : make_uint4(0, 0, 0, 0);
-        }
-      }
-    };
-    (void)pxv; (void)prv; (void)px2; (void)pbv; (void)prok;
-    if constexpr (LX || LR) prefetch(0);
+    // ---- epilogue (csrc/gemm_epi.h): row-side operands of the first
+    // prefetch group are issued before the accumulators go to LDS.
+    epi.begin(p, tm);
     // D[n][m] -> LDS [m][n] (buffer cur^1 is free: its last reader was the final
     // K-step, which ended with a barrier; buffer cur may already hold the next
     // tile's first K-step)
     bf16_t* Cs = SPLIT_C ? lds : lds + (cur ^ 1) * kBuf;
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int m = wm0 + j * 32 + fr;
-          const int n = wn0 + i * 32 + 8 * g + 4 * fh;
-          const uint32_t lo = pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]);
-          const uint32_t hi = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
-          *reinterpret_cast<uint2*>(&Cs[m * LDC + n]) = make_uint2(lo, hi);
-        }
+    acc_to_lds<TN, TM>(acc, Cs, LDC, wm0, wn0, lane);
     __syncthreads();
-    // per-channel epilogue constants, loaded here (acc is dead) to keep them
-    // out of the K loop's register budget
-    f2_t ea[4], eb[4], em[4], em2[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { ea[q] = f2_t{0.f, 0.f}; eb[q] = ea[q]; em[q] = ea[q]; em2[q] = ea[q]; }
-    auto ld2 = [](const float* src, int c) { return *reinterpret_cast<const f2_t*>(src + c); };
-    if constexpr (EPI == EPI_STATS) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) em[q] = ld2(p.shift, ch0 + 2 * q);
-    } else if constexpr (EPI == EPI_MASKX) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        em[q] = ld2(p.emean, ch0 + 2 * q);
-        ea[q] = ld2(p.ecoef, ch0 + 2 * q);
-        eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
-      }
-    } else if constexpr (EPI == EPI_RESBITS) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        em[q] = ld2(p.emean, ch0 + 2 * q);
-        if (p.ex2) em2[q] = ld2(p.emean2, ch0 + 2 * q);
-      }
-    }
-#pragma unroll
-    for (int g0 = 0; g0 < NP; g0 += PG) {
-      uint4 cxv[PG], crv[PG], cx2[PG];
-      uint32_t cbv[PG];
-      bool crok[PG];
-#pragma unroll
-      for (int i = 0; i < PG; ++i) { cxv[i] = pxv[i]; crv[i] = prv[i]; cx2[i] = px2[i]; cbv[i] = pbv[i]; crok[i] = prok[i]; }
-      (void)cxv; (void)crv; (void)cx2; (void)cbv; (void)crok;
-      if constexpr (LX || LR) {
-        if (g0 + PG < NP) prefetch(g0 + PG);
-      }
-#pragma unroll
-      for (int i = 0; i < PG; ++i) {
-        const int row = (g0 + i) * RPP + er0;
-        const int m = tm * BM + row;
-        if (m >= M) continue;
-        const uint4 raw = *reinterpret_cast<const uint4*>(&Cs[row * LDC + ec * 8]);
-        const int64_t go = static_cast<int64_t>(m) * N + ch0;
-        uint4 out = raw;  // PLAIN / STATS store the tile as it is
-        if constexpr (EPI != EPI_PLAIN) {
-          f2_t v[4];
-          unpack4x2(raw, v);
-          uint32_t o[4];
-          if constexpr (EPI == EPI_STATS) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const f2_t d = v[q] - em[q];
-              s1[q] += d;
-              s2[q] = pfma(d, d, s2[q]);
-            }
-          } else if constexpr (EPI == EPI_MASKX) {
-            f2_t x[4];
-            unpack4x2(cxv[i], x);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const f2_t z = pfma(x[q], ea[q], eb[q]);
-              const f2_t g = f2_t{z.x > 0.f ? v[q].x : 0.f, z.y > 0.f ? v[q].y : 0.f};
-              s1[q] += g;
-              s2[q] = pfma(g, x[q] - em[q], s2[q]);
-              o[q] = pack2(g);
-            }
-            out = make_uint4(o[0], o[1], o[2], o[3]);
-          } else if constexpr (LR) {  // RESBITS / RES: add d(identity), rounded to bf16
-            if (crok[i]) {
-              f2_t r[4];
-              unpack4x2(crv[i], r);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) o[q] = pack2(v[q] + r[q]);
-              out = make_uint4(o[0], o[1], o[2], o[3]);
-            }
-            if constexpr (EPI == EPI_RESBITS) {
-              unpack4x2(out, v);
-              const uint32_t bits = cbv[i];
-              f2_t x[4];
-              unpack4x2(cxv[i], x);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const f2_t g = f2_t{(bits >> (2 * q)) & 1u ? v[q].x : 0.f, (bits >> (2 * q + 1)) & 1u ? v[q].y : 0.f};
-                v[q] = g;
-                s1[q] += g;
-                s2[q] = pfma(g, x[q] - em[q], s2[q]);
-                o[q] = pack2(g);
-              }
-              if (p.ex2) {
-                f2_t x2[4];
-                unpack4x2(cx2[i], x2);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) s3[q] = pfma(v[q], x2[q] - em2[q], s3[q]);
-              }
-              out = make_uint4(o[0], o[1], o[2], o[3]);
-            }
-          }
-        }
-        *reinterpret_cast<uint4*>(p.C + go) = out;
-      }
-    }
+    epi.rows(p, Cs, tm);
     __syncthreads();  // Cs (buffer cur^1) is restaged by the next tile's second K-step
     if constexpr (SPLIT_C) {  // stage the next tile's first K-step now that the epilogue is done
       if (tm + GM < tiles_m) swrite(0);
@@ -494,45 +270,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   }
 
-  if constexpr (REDUCE) {
-    // fold the RPP row groups of each channel chunk in LDS, one atomic per
-    // channel per sum into this block's replica
-    float* sh = reinterpret_cast<float*>(lds);
-    constexpr int NS = 3;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sh[(0 * kThreads + t) * 8 + j] = s1[j >> 1][j & 1];
-      sh[(1 * kThreads + t) * 8 + j] = s2[j >> 1][j & 1];
-      if constexpr (EPI == EPI_RESBITS) sh[(2 * kThreads + t) * 8 + j] = s3[j >> 1][j & 1];
-    }
-    __syncthreads();
-    if (gm < tiles_m && er0 == 0) {
-#pragma unroll
-      for (int si = 0; si < NS; ++si) {
-        if (si == 2 && !(EPI == EPI_RESBITS && p.ex2)) break;
-        float a[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = 0.f;
-        for (int rr = 0; rr < RPP; ++rr) {
-          const int o = (si * kThreads + rr * CPR + ec) * 8;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) a[j] += sh[o + j];
-        }
-        float* dst;
-        if (si == 0) dst = p.acc + static_cast<int64_t>(b % kRep) * 2 * N + ch0;
-        else if (si == 1) dst = p.acc + static_cast<int64_t>(b % kRep) * 2 * N + N + ch0;
-        else dst = p.acc2 + static_cast<int64_t>(b % kRep) * 2 * N + N + ch0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) atomic_add_f32(dst + j, a[j]);
-        if (si == 0 && EPI == EPI_RESBITS && p.ex2) {
-          // the downsample BN sees the same masked gradient: same sum(g')
-          float* d2 = p.acc2 + static_cast<int64_t>(b % kRep) * 2 * N + ch0;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) atomic_add_f32(d2 + j, a[j]);
-        }
-      }
-    }
-  }
+  epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -822,6 +560,18 @@ int pick_config(int M, int N, int K, int epi) {
 
 }  // namespace
 
+namespace {
+// KDL_GEMM_CORE: "reg" = register-staged loop only, "dma" = LDS-DMA loop
+// wherever it applies, unset = by shape (long K / 3x3 without prologue -> DMA)
+int g_core = [] {
+  const char* e = getenv("KDL_GEMM_CORE");
+  return e ? (e[0] == 'r' ? 0 : 1) : -1;
+}();
+}  // namespace
+
+int gemm_core_mode() { return g_core; }
+void set_gemm_core_mode(int m) { g_core = m; }
+
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (a.K % BK || a.N % 64 || a.M <= 0) return hipErrorInvalidValue;
   GemmParams p{};
@@ -853,6 +603,16 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   const int epi = a.epi;
   if (epi == EPI_RES || epi == EPI_RESBITS) {
     if (!p.eres) return hipErrorInvalidValue;
+  }
+  // long K without an A prologue: the LDS-DMA main loop (csrc/igemm.hip)
+  const int core = gemm_core_mode();
+  const int min_k = gather == G_CONV3 ? 0 : 512;
+  if (!pro && core != 0 && (core == 1 || p.K >= min_k) && p.K % 64 == 0) {
+    p.a_rows = gather == G_CONV3 ? static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win
+               : gather == G_STRIDED ? static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win
+                                     : p.M;
+    const hipError_t e = igemm(p, epi, gather, igemm_pick(p.M, p.N, p.K), s);
+    if (e != hipErrorInvalidValue) return e;
   }
   switch (pick_config(p.M, p.N, p.K, epi)) {
     case 0: return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);

@@ -1,0 +1,310 @@
+// Long-K conv GEMMs on an LDS-DMA operand pipeline (gfx950).
+//
+//   C[M, N] = A[M, K] . B[N, K]^T, bf16 in, fp32 MFMA accumulation, bf16 out,
+//   with the fused ResNet epilogues of csrc/gemm_epi.h.
+//   A rows: dense | stride-s 1x1 gather | 3x3 pad-1 implicit GEMM (K = 9 Cin,
+//   one tap per 64-deep K-step; padding taps are buffer-OOB loads, which the
+//   hardware returns as zeros).
+//
+// Why a second main loop (csrc/conv1x1.hip keeps the register-staged one for
+// short K and for the BN+ReLU prologue): the register-staged loop spends
+// ~49 % of its wave time waiting on operands and its ds_write pass adds ~40 %
+// LDS traffic on top of the fragment reads (profiles/r01_gemm_longk_pmc.txt).
+// Here every operand byte goes HBM/L2 -> LDS by `buffer_load_dwordx4 ... lds`
+// (no VGPRs, no ds_write), 1 KiB per wave instruction, issued one full K-step
+// ahead so each 64-deep stage lands while the previous one is multiplied:
+//
+//   issue(stage 0)
+//   for k-step t:  barrier (t landed everywhere; stage t+1 free) ;
+//                  issue(t+1 -> other stage) ; fragments + MFMAs of stage t
+//
+// LDS image: each operand row is 64 bf16 = 128 B = 8 chunks of 16 B, chunk c
+// of row r stored at chunk position c ^ ((r >> 1) & 7).  The DMA writes
+// lane-linear (base + 16 * lane), so the swizzle is applied to the SOURCE
+// address (guide §5.4 rule 21), and a fragment read of 32 consecutive rows at
+// one logical chunk is conflict-free for every 16-lane group of
+// ds_read_b128.  MFMA v_mfma_f32_32x32x16_bf16 with the weight fragment as
+// the A operand (lanes index output pixels, registers 4 channel runs: the
+// epilogue's LDS transpose).  Blocks are persistent over M tiles with the
+// XCD-aware (tile_n, M-sequence) order of conv1x1.hip.
+//
+// The reference has no kernels; this serves the PyTorchJob
+// ResNet-50 worker (BASELINE.json config 2).
+#include "common.h"
+#include "gemm_epi.h"
+#include "kdl_api.h"
+
+namespace kdl {
+namespace {
+
+using namespace gemm;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int IBK = 64;                 // K per stage (one 128-B LDS row per operand row)
+constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load returns zeros
+
+template <int A, int B> struct cmax { static constexpr int v = A > B ? A : B; };
+
+// One 16-byte-per-lane LDS-DMA load (1 KiB per wave at dst + 16 * lane).  The
+// builtin exists only for the device pass; referenced in the host pass it
+// makes clang drop the kernel's host stub, hence the pass guard.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+#endif
+}
+
+template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int NW = WM * WN;
+  constexpr int SA = BM * 128, SB = BN * 128, STAGE = SA + SB;  // bytes per stage
+  static_assert((BM + BN) % (8 * NW) == 0 && BM % 16 == 0 && BN % 16 == 0, "DMA row groups");
+  constexpr int IPW = (BM + BN) / 8 / NW;  // 1-KiB DMA instructions per wave per stage
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile = whole 32x32 MFMA blocks");
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  using Epi = Epilogue<BM, BN, NT, EPI>;
+  constexpr int LDC = Epi::LDC;
+  constexpr int LDS_BYTES = cmax<cmax<2 * STAGE, BM * LDC * 2>::v, Epi::kScratchBytes>::v;
+  // ONE __shared__ object (a second one makes hipcc drain vmcnt before ds_reads)
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nblk = gridDim.x, b = blockIdx.x;
+  const int q = (b & 7) * (nblk >> 3) + (b >> 3);  // nblk % 8 == 0 (host)
+  const int tile_n = q % tiles_n;
+  const int gm = q / tiles_n;
+  const int n0 = tile_n * BN;
+  const int K = p.K, M = p.M;
+  const int nk = K / IBK;
+  const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
+  const int fr = lane & 31, fh = lane >> 5;
+
+  // buffer resources (wave-uniform: built from kernel arguments only)
+  const int lda = GATHER == G_CONV3 ? p.Cin : K;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.A), (short)0, static_cast<int>(p.a_rows * lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.B), (short)0, static_cast<int>(static_cast<int64_t>(p.N) * K * 2), 0x00020000);
+
+  // per DMA instruction i of this wave: operand row (within its A or B region)
+  // and the logical 16-B chunk this lane fetches (source-side swizzle)
+  const int lrow = lane >> 3;
+  uint32_t voff[IPW];
+  int crow[IPW];    // conv3: image base row (n * Hin * Win) or -1 for rows >= M
+  int cih[IPW], ciw[IPW];
+  (void)crow; (void)cih; (void)ciw;
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int g = wave * IPW + i;
+    if (g >= BM / 8) {  // B (weights): row n0 + r, chunk c
+      const int r = 8 * (g - BM / 8) + lrow;
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      voff[i] = static_cast<uint32_t>(((n0 + r) * K + 8 * c) * 2);
+    }
+  }
+
+  auto setup_rows = [&](int tm) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int g = wave * IPW + i;
+      if (g < BM / 8) {
+        const int r = 8 * g + lrow;
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int m = tm * BM + r;
+        if constexpr (GATHER == G_CONV3) {
+          if (m < M) {
+            const int hw = p.Hout * p.Wout;
+            const int nimg = m / hw, rem = m - nimg * hw;
+            const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
+            crow[i] = nimg * p.Hin * p.Win;
+            cih[i] = oh * p.stride - 1;
+            ciw[i] = ow * p.stride - 1;
+          } else {
+            crow[i] = -1;
+            cih[i] = 0;
+            ciw[i] = 0;
+          }
+          voff[i] = static_cast<uint32_t>(8 * c * 2);  // chunk byte offset; the row part is per tap
+        } else {
+          int64_t src = m;
+          if constexpr (GATHER == G_STRIDED) {
+            const int hw = p.Hout * p.Wout;
+            const int nimg = m / hw, rem = m - nimg * hw;
+            const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
+            src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
+          }
+          voff[i] = m < M ? static_cast<uint32_t>((src * K + 8 * c) * 2) : kOOB;
+        }
+      }
+    }
+  };
+
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * IBK;
+    char* base = lds + stage * STAGE;
+    int tap = 0, kc0 = k0, r3 = 0, q3 = 0;
+    (void)tap; (void)r3; (void)q3;
+    if constexpr (GATHER == G_CONV3) {
+      tap = k0 / p.Cin;  // a 64-deep K-step never straddles taps (Cin % 64 == 0)
+      kc0 = k0 - tap * p.Cin;
+      r3 = tap / 3;
+      q3 = tap - 3 * r3;
+    }
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int g = wave * IPW + i;
+      lds_void_t* dst = (lds_void_t*)(base + g * 1024);
+      if (g < BM / 8) {
+        if constexpr (GATHER == G_CONV3) {
+          const int ih = cih[i] + r3, iw = ciw[i] + q3;
+          const bool ok = crow[i] >= 0 && static_cast<unsigned>(ih) < static_cast<unsigned>(p.Hin) &&
+                          static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win);
+          const uint32_t off = ok ? static_cast<uint32_t>(((crow[i] + ih * p.Win + iw) * p.Cin + kc0) * 2) + voff[i]
+                                  : kOOB;
+          dma16(rA, dst, off, 0);
+        } else {
+          dma16(rA, dst, voff[i], k0 * 2);
+        }
+      } else {
+        dma16(rB, dst, voff[i], k0 * 2);
+      }
+    }
+  };
+
+  // fragment byte offsets within a row: logical chunk 2s + fh, swizzled by the
+  // row's (r >> 1) & 7 == (fr >> 1) & 7 (fragment rows start at multiples of 16)
+  uint32_t xo[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) xo[s] = static_cast<uint32_t>((((2 * s + fh) ^ ((fr >> 1) & 7))) * 16);
+
+  Epi epi;
+  epi.init(t, n0);
+
+  for (int tm = gm; tm < tiles_m; tm += GM) {
+    setup_rows(tm);
+    f32x16_t acc[TN][TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
+    issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();  // stage kt landed (every wave's vmcnt(0) + barrier); stage kt+1 free
+      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+      const char* As = lds + (kt & 1) * STAGE;
+      const char* Bs = As + SA;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8_t wf[TN], xf[TM];
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          wf[i] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + i * 32 + fr) * 128 + xo[s]);
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          xf[j] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + j * 32 + fr) * 128 + xo[s]);
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave's last fragment reads are done: the stages become the C tile
+    epi.begin(p, tm);
+    bf16_t* Cs = reinterpret_cast<bf16_t*>(lds);
+    acc_to_lds<TN, TM>(acc, Cs, LDC, wm0, wn0, lane);
+    __syncthreads();
+    epi.rows(p, Cs, tm);
+    __syncthreads();  // the next tile's DMA overwrites Cs
+  }
+  epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
+}
+
+template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB>
+hipError_t launch(const GemmParams& p, hipStream_t s) {
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = p.N / BN;
+  const int target = 256 * MINB;  // one round of resident blocks
+  int GM = (target + tiles_n - 1) / tiles_n;
+  if (GM > tiles_m) GM = tiles_m;
+  while ((GM * tiles_n) % 8) ++GM;
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB>), dim3(GM * tiles_n), dim3(64 * WM * WN), 0, s,
+                     p, GM, tiles_m, tiles_n);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN, int GATHER, int MINB>
+hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
+  switch (epi) {
+    case EPI_PLAIN: return launch<BM, BN, WM, WN, GATHER, EPI_PLAIN, MINB>(p, s);
+    case EPI_STATS: return launch<BM, BN, WM, WN, GATHER, EPI_STATS, MINB>(p, s);
+    case EPI_MASKX: return launch<BM, BN, WM, WN, GATHER, EPI_MASKX, MINB>(p, s);
+  }
+  if constexpr (GATHER == G_DENSE) {
+    switch (epi) {
+      case EPI_RESBITS: return launch<BM, BN, WM, WN, GATHER, EPI_RESBITS, MINB>(p, s);
+      case EPI_RES: return launch<BM, BN, WM, WN, GATHER, EPI_RES, MINB>(p, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int BM, int BN, int WM, int WN, int MINB>
+hipError_t dispatch_gather(const GemmParams& p, int epi, int gather, hipStream_t s) {
+  switch (gather) {
+    case G_DENSE: return dispatch_epi<BM, BN, WM, WN, G_DENSE, MINB>(p, epi, s);
+    case G_STRIDED: return dispatch_epi<BM, BN, WM, WN, G_STRIDED, MINB>(p, epi, s);
+    case G_CONV3: return dispatch_epi<BM, BN, WM, WN, G_CONV3, MINB>(p, epi, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// Tile configs: 0 = 256x256 (8 waves, 128x64 wave tiles, 1 block/CU);
+// 1 = 256x128 (8 waves, 64x64); 2 = 128x128 (4 waves, 64x64, 2 blocks/CU);
+// 3 = 256x64 (4 waves, 64x64, 2 blocks/CU).
+namespace {
+int g_forced_cfg = [] { const char* e = getenv("KDL_IGEMM_CFG"); return e ? atoi(e) : -1; }();
+}  // namespace
+
+void set_igemm_cfg(int cfg) { g_forced_cfg = cfg; }
+
+namespace gemm {
+int igemm_pick(int M, int N, int K) {
+  const int forced = g_forced_cfg;
+  if (forced >= 0 && forced <= 3) {
+    const int bn = forced == 0 ? 256 : forced == 3 ? 64 : 128;
+    if (N % bn == 0) return forced;
+  }
+  // measured on the ResNet-50 b256 shapes (profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl):
+  // 256x256 wins at N = 256 (fewest operand bytes per MFMA), 128x128 at two
+  // blocks per CU elsewhere (more resident waves, more tiles to fill 256 CUs)
+  (void)M; (void)K;
+  if (N == 256) return 0;
+  if (N % 128 == 0) return 2;
+  return 3;
+}
+}  // namespace gemm
+
+namespace gemm {
+hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t s) {
+  if (p.K % IBK || p.M <= 0) return hipErrorInvalidValue;
+  const int lda = gather == G_CONV3 ? p.Cin : p.K;
+  if (p.a_rows * lda * 2 >= (int64_t(1) << 31) || static_cast<int64_t>(p.N) * p.K * 2 >= (int64_t(1) << 31))
+    return hipErrorInvalidValue;  // 32-bit buffer offsets
+  switch (cfg) {
+    case 0: if (p.N % 256) break; return dispatch_gather<256, 256, 2, 4, 1>(p, epi, gather, s);
+    case 1: if (p.N % 128) break; return dispatch_gather<256, 128, 4, 2, 1>(p, epi, gather, s);
+    case 2: if (p.N % 128) break; return dispatch_gather<128, 128, 2, 2, 2>(p, epi, gather, s);
+    case 3: if (p.N % 64) break; return dispatch_gather<256, 64, 4, 1, 2>(p, epi, gather, s);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace gemm
+
+}  // namespace kdl

@@ -202,4 +202,10 @@ hipError_t make_stream(bool dedicated, int priority, hipStream_t* out);
 // one wave busy-waiting ``microseconds`` (queue-concurrency probe)
 hipError_t spin(hipStream_t s, double microseconds);
 
+// conv GEMM main-loop selection (-1 by shape, 0 register-staged, 1 LDS-DMA)
+int gemm_core_mode();
+void set_gemm_core_mode(int m);
+// force an LDS-DMA tile config (-1 = by shape; csrc/igemm.hip igemm_pick)
+void set_igemm_cfg(int cfg);
+
 }  // namespace kdl

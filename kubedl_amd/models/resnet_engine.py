@@ -138,6 +138,17 @@ class HipKernels:
                               self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
         return y
 
+    def conv3x3_fwd(self, x, w, stride, out: BNState):
+        """3x3 pad-1 conv as an implicit GEMM (LDS-DMA main loop, csrc/igemm.hip)
+        with ``out``'s BN statistics in the epilogue (no separate stats pass)."""
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+        y = _nhwc_empty(n, cout, ho, wo, x)
+        self.ext.conv3x3_gemm(x, w, y, n, h, wd, cin, cout, stride, None, 1, out.mod.running_mean,
+                              self._fwd_acc(out), None, None, None)
+        return y
+
     def bn_stats(self, x, st):
         self.ext.bn_stage_fwd_stats(x, st.ws, x.numel() // st.C, st.C)
 
@@ -280,6 +291,11 @@ class TorchKernels:
         a = self._pro(x, pro) if pro is not None else x.float()
         y = F.conv2d(a[:, :, ::stride, ::stride], w.float()[:, :, None, None])
         y = y.to(x.dtype)
+        self._stats(y, out, out.mod.running_mean.clone())
+        return y.contiguous(memory_format=torch.channels_last)
+
+    def conv3x3_fwd(self, x, w, stride, out):
+        y = F.conv2d(x.float(), w.float(), stride=stride, padding=1).to(x.dtype)
         self._stats(y, out, out.mod.running_mean.clone())
         return y.contiguous(memory_format=torch.channels_last)
 
@@ -441,6 +457,10 @@ class ResNetEngine:
         assert len(self.blocks) == len(model.layers), "engine supports Bottleneck stacks only"
         self._wt_ptrs = None
         self._wt_buf = {}
+        # 3x3 forward convs on the implicit-GEMM kernel (KDL_CONV3_FWD=miopen: MIOpen
+        # + a separate statistics pass; A/B in profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl)
+        self.conv3_native = os.environ.get("KDL_CONV3_FWD", "kdl") != "miopen" and all(
+            b.conv2.in_channels % 64 == 0 and b.conv2.out_channels % 64 == 0 for b in self.blocks)
         # Weight gradients on a second HIP stream (default; KDL_WGRAD_STREAM=0 turns
         # it off -- 10.7k -> 11.3k img/s at batch 256, profiles/): a wgrad
         # depends only on its layer's output gradient and saved input, and nothing
@@ -538,10 +558,16 @@ class ResNetEngine:
             c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
             a1, _ = K.bn_apply(c1, st1, relu=True)
-            c2 = F.conv2d(a1, blk.conv2.weight, stride=s, padding=1).contiguous(memory_format=torch.channels_last)
-            ho, wo = c2.shape[-2:]
-            K.bn_stats(c2, st2)
-            K.bn_finalize(st2, n * ho * wo, x=c2)
+            if self.conv3_native:
+                # implicit GEMM + B2 statistics in the epilogue (shift = running mean)
+                c2 = K.conv3x3_fwd(a1, blk.conv2.weight, s, st2)
+                ho, wo = c2.shape[-2:]
+                K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
+            else:
+                c2 = F.conv2d(a1, blk.conv2.weight, stride=s, padding=1).contiguous(memory_format=torch.channels_last)
+                ho, wo = c2.shape[-2:]
+                K.bn_stats(c2, st2)
+                K.bn_finalize(st2, n * ho * wo, x=c2)
             c3 = K.conv1x1_fwd(c2, blk.conv3.weight.view(blk.conv3.out_channels, -1), 1, st2, st3)
             K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
             cd = None
