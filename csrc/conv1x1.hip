@@ -626,9 +626,11 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
 int conv1x1_wgrad_splits(int M, int N, int K) {
   const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
   const int tiles = (N / tn) * (K / tk);
-  // ~2 blocks per CU (one round): halves the slab bytes of 4 blocks/CU, measured +1.5% per step
+  // ~2 blocks per CU (one round): halves the slab bytes of 4 blocks/CU, measured +1.5% per step.
+  // Rounded DOWN so the grid never spills a partial second round onto the CUs
+  // (3x3 stage-4: 576 blocks = 1.125 rounds took 1.7x the time of 432).
   const int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 512; }();
-  int splits = (target + tiles - 1) / tiles;
+  int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;
   if (splits > max_splits) splits = max_splits;
   return splits < 1 ? 1 : splits;
@@ -669,11 +671,28 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
   dim3 grid(nsplit * (N / tn) * tiles_k);
   const bf16_t* g = static_cast<const bf16_t*>(G);
   const bf16_t* x = static_cast<const bf16_t*>(A);
-  if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
-  else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
-  else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
-  else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
-  KDL_CHECK_HIP(hipGetLastError());
+  bool done = false;
+  if (gemm_core_mode() != 0) {  // LDS-DMA pipeline (csrc/wgrad_dma.hip) unless forced off
+    WgParams wp{};
+    wp.G = g; wp.A = x; wp.pro = pro_coef; wp.dw32 = dw32;
+    wp.M = M; wp.N = N; wp.K = K; wp.Hout = Hout; wp.Wout = Wout; wp.Hin = Hin; wp.Win = Win;
+    wp.stride = stride; wp.cin = cin; wp.rps = rps; wp.tiles_k = tiles_k; wp.mode = mode;
+    wp.a_rows = mode == G_DENSE ? M : static_cast<int64_t>(M / (Hout * Wout)) * Hin * Win;
+    if (mode != G_DENSE) {
+      wp.mg_hw = static_cast<uint32_t>(((uint64_t(1) << 32) + Hout * Wout - 1) / (Hout * Wout));
+      wp.mg_w = static_cast<uint32_t>(((uint64_t(1) << 32) + Wout - 1) / Wout);
+    }
+    const hipError_t e = wgrad_dma(wp, nsplit, tn, tk, s);
+    if (e != hipSuccess && e != hipErrorInvalidValue) return e;
+    done = e == hipSuccess;
+  }
+  if (!done) {
+    if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+    else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+    else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+    else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
+    KDL_CHECK_HIP(hipGetLastError());
+  }
   const int64_t nk = static_cast<int64_t>(N) * K;
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, nsplit, scale,

@@ -61,6 +61,23 @@ struct GemmParams {
   float* acc2;          // its replicas [kRep][2N]
 };
 
+// csrc/wgrad_dma.hip: weight gradient on the LDS-DMA pipeline into fp32
+// slabs dw32[split][N][K] (rps % 64 == 0; tn, tk in {64, 128}).
+struct WgParams {
+  const bf16_t* G;        // [M][N] output gradient
+  const bf16_t* A;        // layer input rows (gathered per mode)
+  const float* pro;       // optional BN+ReLU prologue of A: [2 * lda] scale | shift
+  float* dw32;
+  int M, N, K;            // K = 9 * cin for 3x3
+  int Hout, Wout, Hin, Win, stride, cin;
+  int rps, tiles_k, mode; // rows per split, K tiles, G_DENSE | G_STRIDED | G_CONV3
+  int64_t a_rows;         // rows of the A tensor (buffer bounds)
+  // n / d == umulhi(n, ceil(2^32 / d)) for n * d < 2^32 (host-checked): the
+  // per-row image coordinates without integer division in the main loop
+  uint32_t mg_hw, mg_w;   // magic multipliers of Hout * Wout and Wout
+};
+hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t s);
+
 // csrc/igemm.hip: LDS-DMA main loop (no A prologue); cfg from igemm_pick.
 // Requires K % 64 == 0 (3x3: Cin % 64 == 0) and 32-bit operand byte offsets.
 int igemm_pick(int M, int N, int K);

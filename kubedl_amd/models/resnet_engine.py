@@ -11,7 +11,7 @@ forward, per bottleneck (``B`` = BatchNorm, ``R`` = ReLU)::
 
     c1 = conv1(x)                [GEMM, epilogue: B1 statistics]
     a1 = R(B1(c1))               [apply pass]
-    c2 = conv2(a1)               [MIOpen 3x3]      ; B2 statistics pass
+    c2 = conv2(a1)               [3x3 implicit GEMM (csrc/igemm.hip), epilogue: B2 stats]
     c3 = conv3(R(B2(c2)))        [GEMM, prologue: B2+R while staging A -- the
                                   B2 output never reaches HBM; epilogue: B3 stats]
     cd = down(x)                 [GEMM, strided row gather, epilogue: Bd stats]
@@ -24,7 +24,8 @@ epilogue)::
     dc3 (, dcd) = B3 (, Bd) apply-backward of g        [one pass for both branches]
     g2 = conv3 dgrad (dc3), masked by R'(B2(c2)) + B2 reduction sums   [GEMM epilogue]
     dW3 = sum dc3^T R(B2(c2))                          [GEMM, B2+R recomputed in the prologue]
-    dc2 = B2 apply-backward(g2) ; da1, dW2 = conv2 backward [MIOpen]
+    dc2 = B2 apply-backward(g2) ; dW2 [3x3 implicit GEMM, csrc/wgrad_dma.hip] ;
+          da1 [stride 1: implicit GEMM with bn1's mask + sums fused; stride 2: MIOpen]
     dc1 = B1 backward(da1) (mask recomputed from c1)
     g_prev = conv1 dgrad(dc1) + d(identity) (strided gather of the downsample dgrad),
              masked by the previous block's ReLU bits, + B3_prev (and Bd_prev)
@@ -263,6 +264,19 @@ class HipKernels:
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
                                M, cout, cin, ho, wo, h, w, stride)
 
+    def wgrad3x3(self, g, x, stride, dW):
+        """3x3 pad-1 weight gradient straight into ``dW`` (channels_last = OHWI):
+        LDS-DMA implicit GEMM (csrc/wgrad_dma.hip) into split-M slabs + reduce."""
+        n, cout, ho, wo = g.shape
+        _, cin, h, w = x.shape
+        M = n * ho * wo
+        key = (M, cout, 9 * cin)
+        dw32 = self._dw32.get(key)
+        if dw32 is None:
+            slabs = self.ext.conv1x1_wgrad_splits(M, cout, 9 * cin)
+            dw32 = self._dw32[key] = torch.empty(slabs * cout * 9 * cin, device=g.device)
+        self.ext.conv3x3_wgrad(g, x, None, dw32, dW, 1.0, n, h, w, cin, cout, stride)
+
     def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
         m = st.mod
         dx, dg, db = self.ext.bn_pool_bwd(dp, idx, c0, m.weight, m.bias, st.save_mean, st.save_invstd, True, st.ws)
@@ -419,6 +433,9 @@ class TorchKernels:
         a = _rows(a[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last))
         dW.copy_((_rows(g.float()).t() @ a).view_as(dW))
 
+    def wgrad3x3(self, g, x, stride, dW):
+        dW.copy_(torch.nn.grad.conv2d_weight(x.float(), tuple(dW.shape), g.float(), stride=stride, padding=1))
+
     def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
         sc, sf = st.fcoef
         n, c, h, w = c0.shape
@@ -457,9 +474,10 @@ class ResNetEngine:
         assert len(self.blocks) == len(model.layers), "engine supports Bottleneck stacks only"
         self._wt_ptrs = None
         self._wt_buf = {}
-        # 3x3 forward convs on the implicit-GEMM kernel (KDL_CONV3_FWD=miopen: MIOpen
-        # + a separate statistics pass; A/B in profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl)
-        self.conv3_native = os.environ.get("KDL_CONV3_FWD", "kdl") != "miopen" and all(
+        # 3x3 forward convs and weight gradients on the LDS-DMA implicit-GEMM kernels
+        # (KDL_CONV3=miopen: MIOpen + a separate statistics pass + gradient copies;
+        # per-layer A/B: profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl, r02_wgrad_dma_vs_reg_vs_miopen.jsonl)
+        self.conv3_native = os.environ.get("KDL_CONV3", "kdl") != "miopen" and all(
             b.conv2.in_channels % 64 == 0 and b.conv2.out_channels % 64 == 0 for b in self.blocks)
         # Weight gradients on a second HIP stream (default; KDL_WGRAD_STREAM=0 turns
         # it off -- 10.7k -> 11.3k img/s at batch 256, profiles/): a wgrad
@@ -611,6 +629,16 @@ class ResNetEngine:
             return wt
         return conv.weight.view(conv.out_channels, -1).t().contiguous()
 
+    def _wgrad3x3(self, g, a, stride, weight):
+        """conv2's weight gradient: the implicit-GEMM kernel writing straight into
+        the gradient buffer, or (KDL_CONV3=miopen) MIOpen + a copy."""
+        if self.conv3_native:
+            self.K.wgrad3x3(g, a, stride, self._g(weight))
+        else:
+            _, dw, _ = torch.ops.aten.convolution_backward(
+                g, a, weight, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
+            self._g(weight).copy_(dw)
+
     def _bn_grads(self, st):
         return self._g(st.mod.weight), self._g(st.mod.bias)
 
@@ -656,10 +684,7 @@ class ResNetEngine:
             s = blk.conv2.stride[0]
             if s == 1:
                 with self._on_side(dc2):
-                    _, dw2, _ = torch.ops.aten.convolution_backward(
-                        dc2, a1, blk.conv2.weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                        [False, True, False])
-                    self._g(blk.conv2.weight).copy_(dw2)
+                    self._wgrad3x3(dc2, a1, 1, blk.conv2.weight)
                 self.on_ready(blk.conv2.weight)
                 g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
@@ -673,10 +698,7 @@ class ResNetEngine:
                     self._g(blk.conv2.weight).copy_(dw2)
                 else:  # weight gradient on the side stream, data gradient on the main one
                     with self._on_side(dc2):
-                        _, dw2, _ = torch.ops.aten.convolution_backward(
-                            dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                            [False, True, False])
-                        self._g(blk.conv2.weight).copy_(dw2)
+                        self._wgrad3x3(dc2, a1, s, blk.conv2.weight)
                     da1, _, _ = torch.ops.aten.convolution_backward(
                         dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
                         [True, False, False])

@@ -10,7 +10,7 @@ import sqlite3
 import sys
 
 FAMILIES = [
-    ("conv1x1-gemm(kdl)", r"kdl::.*(gemm1x1|wgrad1x1)"),
+    ("conv-gemm(kdl)", r"kdl::.*(gemm1x1|wgrad1x1|igemm)"),
     ("bn(kdl)", r"kdl::.*bn_"),
     ("optim(kdl)", r"kdl::.*(sgd|adam|sumsq|cast)"),
     ("kdl-other", r"kdl::"),

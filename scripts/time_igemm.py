@@ -106,3 +106,56 @@ if __name__ == "__main__":
                                     (256, 7, 512, 512, 1), (256, 56, 128, 128, 2), (256, 28, 256, 256, 2),
                                     (256, 14, 512, 512, 2)]:
             run_3x3(nb, H, Cin, Cout, s)
+
+
+def run_wgrad_1x1(M, N, K, rounds=3):
+    A = torch.randn(M, K, device=dev).bfloat16()
+    G = torch.randn(M, N, device=dev).bfloat16()
+    ws = torch.empty(ext.conv1x1_wgrad_splits(M, N, K) * N * K, device=dev)
+    dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+    res = {}
+    for _ in range(rounds):
+        for name, core in (("reg", 0), ("dma", 1)):
+            ext.set_gemm_core(core)
+            res.setdefault(name, []).append(timed(
+                lambda: ext.conv1x1_wgrad(G, A, None, ws, dW, 1.0, M, N, K, 0, 0, 0, 0, 1)))
+    ext.set_gemm_core(-1)
+    fl = 2.0 * M * N * K
+    for name, ts in res.items():
+        us = min(ts)
+        print(json.dumps({"op": "wgrad1x1", "M": M, "N": N, "K": K, "variant": name, "us": round(us, 1),
+                          "tflops": round(fl / us / 1e6, 1)}), flush=True)
+
+
+def run_wgrad_3x3(nb, H, Cin, Cout, stride, rounds=3):
+    x = torch.randn(nb, H, H, Cin, device=dev).bfloat16().permute(0, 3, 1, 2)
+    w = (torch.randn(Cout, 3, 3, Cin, device=dev) / (3 * Cin ** 0.5)).bfloat16().permute(0, 3, 1, 2)
+    Ho = (H - 1) // stride + 1
+    dy = torch.randn(nb, Ho, Ho, Cout, device=dev).bfloat16().permute(0, 3, 1, 2)
+    M = nb * Ho * Ho
+    ws = torch.empty(ext.conv1x1_wgrad_splits(M, Cout, 9 * Cin) * Cout * 9 * Cin, device=dev)
+    dW = torch.empty(Cout, 3, 3, Cin, device=dev, dtype=torch.bfloat16).permute(0, 3, 1, 2)
+    res = {}
+    for _ in range(rounds):
+        res.setdefault("miopen", []).append(timed(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])))
+        for name, core in (("reg", 0), ("dma", 1)):
+            ext.set_gemm_core(core)
+            res.setdefault(name, []).append(timed(
+                lambda: ext.conv3x3_wgrad(dy, x, None, ws, dW, 1.0, nb, H, H, Cin, Cout, stride)))
+    ext.set_gemm_core(-1)
+    fl = 2.0 * M * Cout * 9 * Cin
+    for name, ts in res.items():
+        us = min(ts)
+        print(json.dumps({"op": "wgrad3x3", "nb": nb, "H": H, "Cin": Cin, "Cout": Cout, "stride": stride,
+                          "variant": name, "us": round(us, 1), "tflops": round(fl / us / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__" and (len(sys.argv) > 1 and sys.argv[1] in ("all", "wgrad")):
+    for M, N, K in [(50176, 256, 1024), (12544, 512, 2048), (200704, 128, 512), (802816, 256, 64),
+                    (802816, 64, 256), (50176, 1024, 256)]:
+        run_wgrad_1x1(M, N, K)
+    for nb, H, Cin, Cout, s in [(256, 56, 64, 64, 1), (256, 28, 128, 128, 1), (256, 14, 256, 256, 1),
+                                (256, 7, 512, 512, 1), (256, 56, 128, 128, 2), (256, 28, 256, 256, 2),
+                                (256, 14, 512, 512, 2)]:
+        run_wgrad_3x3(nb, H, Cin, Cout, s)
