@@ -27,6 +27,8 @@ exists to enable.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -35,13 +37,21 @@ from kubedl_amd.parallel import p2p
 
 
 class Bucket:
-    __slots__ = ("lo", "hi", "slots", "pending", "handle", "packer")
+    __slots__ = ("lo", "hi", "slots", "pending", "handle", "packer", "wide")
 
     def __init__(self, lo: int, hi: int, slots):
         self.lo, self.hi, self.slots = lo, hi, slots
         self.pending = len(slots)
         self.handle = None
         self.packer = None
+        self.wide = None  # fp32 copy of a bf16 bucket being reduced (reduce_fp32)
+
+
+def reduce_fp32_wanted() -> bool:
+    """``KDL_DDP_REDUCE=fp32``: RCCL buckets of a bf16 gradient buffer are summed in
+    fp32 (2x the bytes on the links, one bf16 rounding at the end instead of one
+    per ring step; tests/test_multigpu.py bounds the bf16 error at world 8)."""
+    return os.environ.get("KDL_DDP_REDUCE", "bf16").lower() == "fp32"
 
 
 class FlatDDP:
@@ -58,6 +68,7 @@ class FlatDDP:
         self.buckets: list[Bucket] = []
         self._hooks = []
         self.transport = None
+        self.reduce_fp32 = reduce_fp32_wanted()
         # producers on a second stream (the ResNet engine's weight-gradient
         # stream): a bucket's collective is issued on that stream after it has
         # joined the current one, so it waits for both without stalling the
@@ -118,6 +129,9 @@ class FlatDDP:
     def _issue(self, b: Bucket) -> None:
         if self.transport is not None:
             b.handle = self.transport.launch(b.lo, b.hi)
+        elif self.reduce_fp32 and self.space.grad.dtype != torch.float32:
+            b.wide = self.space.grad[b.lo:b.hi].float()
+            b.handle = dist.all_reduce(b.wide, group=self.pg, async_op=True)
         else:
             b.handle = dist.all_reduce(self.space.grad[b.lo:b.hi], group=self.pg, async_op=True)
 
@@ -144,6 +158,11 @@ class FlatDDP:
             b.handle.wait()
             b.handle = None
             b.pending = len(b.slots)
+            if b.wide is not None:
+                self.space.grad[b.lo:b.hi].copy_(b.wide)
+                if b.wide.is_cuda:  # allocated on the join stream, last read here
+                    b.wide.record_stream(torch.cuda.current_stream())
+                b.wide = None
         if self.transport is not None:
             # bits of EARLIER steps only (no sync here); the authoritative check
             # follows a device sync: ResNetTrainer.check_transport, run before

@@ -16,6 +16,8 @@ os.environ.setdefault("KDL_ZYGOTE", "0")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "multigpu: ranks on distinct GPUs; skips itself below its world size "
+                                       "(tests/test_multigpu.py)")
 
 
 def _has_gpu():

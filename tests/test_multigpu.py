@@ -1,0 +1,272 @@
+"""Cross-device tier of the data-parallel path.
+
+Every rank is its own process on its OWN GPU (``cuda:<rank>``), so these tests
+exercise what the one-GPU suite cannot: RCCL rings over xGMI, P2P all-reduce
+kernels reading peer HBM through IPC mappings across device boundaries
+(system-scope release/acquire between GPUs), and a DDP training step whose
+ranks must end bit-identical.  Marked ``gpu`` + ``multigpu``; each case skips
+itself unless ``torch.cuda.device_count()`` covers its world size, so the
+1-GPU box reports skips and an 8-GPU node runs all of them unchanged.
+
+The last test is the CPU (gloo, 8 ranks) bound on bf16 gradient sums that
+motivates ``KDL_DDP_REDUCE=fp32``.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ndev() -> int:
+    try:
+        return torch.cuda.device_count() if torch.cuda.is_available() else 0
+    except Exception:
+        return 0
+
+
+def _need(world):
+    if _ndev() < world:
+        pytest.skip(f"needs {world} GPUs, have {_ndev()}")
+
+
+def _spawn(target, world, *args, timeout=300):
+    import torch.multiprocessing as mp
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=timeout) for _ in range(world)), key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+def _init(rank, world, port, backend="nccl"):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    torch.cuda.set_device(rank)
+    kw = dict(backend=backend, rank=rank, world_size=world)
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", rank)
+    dist.init_process_group(**kw)
+
+
+def _inputs(rank, n, dtype):
+    g = torch.Generator().manual_seed(1234 + rank)
+    return torch.randn(n, generator=g).to(dtype)
+
+
+# ------------------------------------------------------------------ RCCL
+def _rccl_worker(rank, world, port, q, n):
+    import torch.distributed as dist
+    _init(rank, world, port)
+    xs = [_inputs(r, n, torch.bfloat16) for r in range(world)]
+    truth = torch.stack([x.double() for x in xs]).sum(0)
+    out = {}
+    for name, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        t = xs[rank].to(dt).cuda()
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        out[name] = ((t.double().cpu() - truth).abs().max().item(), truth.abs().max().item())
+    q.put((rank, out))
+    dist.barrier(device_ids=[rank])
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.multigpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_rccl_allreduce_vs_fp64_truth(world):
+    _need(world)
+    res = _spawn(_rccl_worker, world, 1 << 20)
+    for _, out in res:
+        err32, scale = out["fp32"]
+        err16, _ = out["bf16"]
+        assert err32 <= 1e-5 * scale * world
+        # bf16 ring: a rounding per step; stays within ~world bf16 ulps of the largest sum
+        assert err16 <= world * 2 ** -8 * scale
+    assert len({round(o["bf16"][0], 6) for _, o in res}) == 1  # every rank holds the same result
+
+
+# ------------------------------------------------------------------ P2P (IPC peer buffers)
+def _p2p_worker(rank, world, port, q, dtype_name, n):
+    import torch.distributed as dist
+    from kubedl_amd.parallel.p2p import P2PAllReduce
+    _init(rank, world, port)
+    dt = getattr(torch, dtype_name)
+    xs = [_inputs(r, n, dt) for r in range(world)]
+    truth = torch.stack([x.double() for x in xs]).sum(0)
+    buf = xs[rank].cuda()
+    ar = P2PAllReduce(buf, timeout_s=60.0)
+    res = {}
+    for mode, (lo, hi) in (("oneshot", (0, 32768 // buf.element_size())), ("twoshot", (0, n))):
+        buf.copy_(xs[rank].cuda())
+        torch.cuda.synchronize()
+        dist.barrier(device_ids=[rank])
+        ar.all_reduce_(lo, hi, oneshot=(mode == "oneshot"))
+        torch.cuda.synchronize()
+        ar.check()
+        got = buf[lo:hi].double().cpu()
+        res[mode] = ((got - truth[lo:hi]).abs().max().item(), truth[lo:hi].abs().max().item())
+        # RCCL on the same data for comparison
+        t = xs[rank][lo:hi].cuda()
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        res[mode + "_rccl"] = (t.double().cpu() - truth[lo:hi]).abs().max().item()
+    ar.close()
+    q.put((rank, res))
+    dist.barrier(device_ids=[rank])
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.multigpu
+@pytest.mark.parametrize("dtype_name", ["bfloat16", "float32"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_p2p_allreduce_cross_device(world, dtype_name):
+    """One-shot and two-shot kernels across distinct GPUs vs fp64 truth and RCCL.
+    P2P accumulates in fp32 and rounds once, so in bf16 it must not be worse
+    than RCCL's per-step bf16 ring."""
+    _need(world)
+    res = _spawn(_p2p_worker, world, dtype_name, 3 << 20)
+    for _, r in res:
+        for mode in ("oneshot", "twoshot"):
+            err, scale = r[mode]
+            if dtype_name == "float32":
+                assert err <= 1e-5 * scale * world, (mode, err)
+            else:
+                assert err <= 2 ** -8 * scale, (mode, err)  # one rounding of the fp32 sum
+                assert err <= r[mode + "_rccl"] + 1e-6, (mode, err, r[mode + "_rccl"])
+
+
+# ------------------------------------------------------------------ DDP training step
+def _ddp_step_worker(rank, world, port, q, transport):
+    import torch.distributed as dist
+    from kubedl_amd.parallel.dist import DistInfo
+    from kubedl_amd.workers.resnet50 import ResNetTrainer
+    os.environ["KDL_ALLREDUCE"] = transport
+    _init(rank, world, port)
+    info = DistInfo(rank, world, rank, torch.device("cuda", rank), "nccl")
+    tr = ResNetTrainer(info, batch=16, image=64, num_classes=10, bn_backend="hip", seed=0)
+    losses = [float(tr.step()) for _ in range(2)]
+    torch.cuda.synchronize()
+    tr.check_transport()
+    q.put((rank, losses, tr.space.master.cpu(), tr.space.param.float().cpu(), tr.engine_kind))
+    dist.barrier(device_ids=[rank])
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.multigpu
+@pytest.mark.parametrize("transport", ["rccl", "p2p"])
+@pytest.mark.parametrize("world", [2, 8])
+def test_engine_ddp_step_identical_weights(world, transport):
+    """Two fused-engine DDP steps (ResNet-50 widths, 64 px) on distinct GPUs: the
+    ranks' losses differ (different data) but their master and bf16 weights are
+    bit-identical afterwards."""
+    _need(world)
+    res = _spawn(_ddp_step_worker, world, transport)
+    assert res[0][4] == "fused"
+    m0, p0 = res[0][2], res[0][3]
+    for r in res[1:]:
+        assert torch.equal(r[2], m0) and torch.equal(r[3], p0)
+    assert len({round(r[1][0], 5) for r in res}) > 1  # the ranks did see different data
+
+
+# ------------------------------------------------------------------ CPU: bf16 sum bound at world 8
+def _bf16_sum_worker(rank, world, port, q, n):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    xs = [_inputs(r, n, torch.bfloat16) for r in range(world)]
+    truth = torch.stack([x.double() for x in xs]).sum(0)
+    t16 = xs[rank].clone()
+    dist.all_reduce(t16)
+    t32 = xs[rank].float()
+    dist.all_reduce(t32)
+    e16 = (t16.double() - truth).abs()
+    e32 = (t32.to(torch.bfloat16).double() - truth).abs()  # fp32 sum, one bf16 rounding
+    q.put((rank, e16.max().item(), e32.max().item(), e16.mean().item(), e32.mean().item(), truth.abs().max().item()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bf16_gradient_sum_error_bound_world8_cpu():
+    """Summing bf16 gradients in bf16 across 8 ranks rounds at every step: the
+    error is bounded by world * ulp(max |sum|) and is measurably larger on
+    average than an fp32 sum rounded once -- the case for KDL_DDP_REDUCE=fp32."""
+    world = 8
+    res = _spawn_cpu(_bf16_sum_worker, world, 1 << 16)
+    for _, m16, m32, a16, a32, scale in res:
+        assert m16 <= world * 2 ** -8 * scale
+        assert m32 <= 2 ** -8 * scale
+        assert a16 > a32
+
+
+def _spawn_cpu(target, world, *args, timeout=240):
+    import torch.multiprocessing as mp
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=timeout) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_ddp_fp32_reduce_option_cpu(monkeypatch):
+    from kubedl_amd.parallel import ddp
+    monkeypatch.delenv("KDL_DDP_REDUCE", raising=False)
+    assert not ddp.reduce_fp32_wanted()
+    monkeypatch.setenv("KDL_DDP_REDUCE", "fp32")
+    assert ddp.reduce_fp32_wanted()
+
+
+def _ddp_fp32_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from kubedl_amd.ops.optim import FlatParamSpace
+    from kubedl_amd.parallel.ddp import FlatDDP
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KDL_DDP_REDUCE="fp32")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 32), torch.nn.Linear(32, 8))
+    sp = FlatParamSpace(m, dtype=torch.bfloat16, device=torch.device("cpu"))
+    ddp = FlatDDP(sp, world, bucket_cap_mb=1e-5, first_bucket_mb=1e-5, direct=True)  # a bucket per tensor
+    assert ddp.reduce_fp32 and len(ddp.buckets) > 1
+    g = torch.Generator().manual_seed(10 + rank)
+    local = torch.randn(sp.grad.numel(), generator=g).to(torch.bfloat16)
+    sp.grad.copy_(local)
+    for s in sp.slots:
+        ddp.ready(s.param)
+    ddp.finish()
+    q.put((rank, local, sp.grad.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_fp32_reduce_matches_fp32_sum_cpu():
+    world = 4
+    res = _spawn_cpu(_ddp_fp32_worker, world)
+    total = torch.stack([r[1].float() for r in res]).sum(0).to(torch.bfloat16)
+    for r in res:
+        assert torch.equal(r[2], total)  # fp32 sum, rounded to bf16 once

@@ -142,6 +142,25 @@ def test_engine_hip_matches_autograd(layers, image, batch, wgrad_stream, monkeyp
     _vs_truth(model, ref, truth)
 
 
+@pytest.mark.gpu
+def test_engine_hip_full_resnet50_224_matches_fp32_truth():
+    """The shape the bench times: the full (3, 4, 6, 3) ResNet-50 at 224 px
+    (56 -> 28 -> 14 -> 7 geometry, stride-2 3x3 convs and strided downsample
+    GEMMs), batch 32, every GEMM on the kdl kernels (LDS-DMA implicit GEMMs for
+    the 3x3 forward / weight gradients and the long-K 1x1s), weight gradients
+    on the side stream -- against fp32 autograd truth, with the same error
+    budget as the bf16 autograd model."""
+    model, ref, x, y = _setup((3, 4, 6, 3), 64, "cuda", 224, 32, classes=1000)
+    truth, tloss = _truth_of(ref, x, y)
+    eng = ResNetEngine(model, backend="hip")
+    assert eng.conv3_native and eng.side is not None
+    loss = eng.forward_backward(x, y)
+    _ref_step(ref, x, y)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss, tloss, atol=2e-2, rtol=2e-2)
+    _vs_truth(model, ref, truth)
+
+
 def _ddp_worker(rank, world, port, q):
     import os
     import torch.distributed as dist
