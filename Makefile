@@ -3,7 +3,7 @@
 PY ?= python
 GPURUN ?= /usr/local/graft/bin/gpurun
 
-.PHONY: all build native test test-gpu bench manifests docker-build clean
+.PHONY: all build native native-asan test test-gpu bench manifests docker-build clean
 
 all: build
 
@@ -12,6 +12,14 @@ build:            ## compile every HIP kernel for gfx950 + the native runtime, i
 
 native:           ## only the C++ runtime (spawner, GPU best-fit) -> kubedl_amd/_native.so
 	$(PY) -m kubedl_amd.ops.build --native-only
+
+native-asan:      ## C++ runtime with -fsanitize=address,undefined + its stress run (host only)
+	$(PY) -m kubedl_amd.ops.build --native-asan
+	KDL_NATIVE_SO=build/kdl_ext/asan/_native.so KDL_ZYGOTE=0 \
+	LD_PRELOAD=$$(gcc -print-file-name=libasan.so) \
+	ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:halt_on_error=1 \
+	UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+	$(PY) scripts/native_stress.py
 
 test:             ## CPU suite (what CI runs)
 	$(PY) -m pytest tests -q -m "not gpu" --timeout=300

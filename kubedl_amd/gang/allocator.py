@@ -70,11 +70,8 @@ def detect_gpus() -> GPUInventory:
 
 
 def _native():
-    try:
-        from kubedl_amd import _native as nat
-        return nat
-    except ImportError:
-        return None
+    from kubedl_amd.runtime import native
+    return native.load()
 
 
 @dataclass

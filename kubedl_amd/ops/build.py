@@ -112,33 +112,44 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
 NATIVE_OUT = ROOT / "kubedl_amd" / "_native.so"
 
 
-def build_native(force: bool = False, verbose: bool = True) -> Path:
+NATIVE_ASAN_OUT = BUILD / "asan" / "_native.so"
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=undefined"]
+
+
+def build_native(force: bool = False, verbose: bool = True, sanitize: bool = False) -> Path:
     """Host-only C++ runtime module (process supervisor + gang placement core).
 
     Plain CPython C API, no torch/HIP dependency, so the controller process
-    never needs to import torch or touch the GPU."""
+    never needs to import torch or touch the GPU.  ``sanitize=True`` builds the
+    AddressSanitizer + UBSan variant into build/asan/_native.so (host code only;
+    loaded with ``KDL_NATIVE_SO`` under an LD_PRELOADed libasan)."""
     srcs = sorted((CSRC / "runtime").glob("*.cpp"))
     py_inc = sysconfig.get_paths()["include"]
     h = hashlib.sha256()
     for p in srcs:
         h.update(p.read_bytes())
+    opt = SANITIZE_FLAGS if sanitize else ["-O2"]
+    h.update(" ".join(opt).encode())
     key = h.hexdigest()[:16]
-    stamp = BUILD / "native.stamp"
+    out = NATIVE_ASAN_OUT if sanitize else NATIVE_OUT
+    stamp = BUILD / ("native_asan.stamp" if sanitize else "native.stamp")
+    out.parent.mkdir(parents=True, exist_ok=True)
     BUILD.mkdir(parents=True, exist_ok=True)
-    if NATIVE_OUT.exists() and stamp.exists() and stamp.read_text() == key and not force:
-        return NATIVE_OUT
+    if out.exists() and stamp.exists() and stamp.read_text() == key and not force:
+        return out
     cxx = os.environ.get("CXX", "g++")
-    tmp = NATIVE_OUT.with_suffix(".so.tmp")
-    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{py_inc}", "-o", str(tmp)] + \
+    tmp = out.with_suffix(".so.tmp")
+    cmd = [cxx] + opt + ["-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{py_inc}", "-o", str(tmp)] + \
         [str(p) for p in srcs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"native build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, NATIVE_OUT)
+    os.replace(tmp, out)
     stamp.write_text(key)
     if verbose:
-        print(f"[kdl-build] linked {NATIVE_OUT}", flush=True)
-    return NATIVE_OUT
+        print(f"[kdl-build] linked {out}", flush=True)
+    return out
 
 
 def main(argv=None):
@@ -146,7 +157,11 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--native-only", action="store_true")
+    ap.add_argument("--native-asan", action="store_true", help="only the ASan+UBSan host-runtime variant")
     a = ap.parse_args(argv)
+    if a.native_asan:
+        build_native(force=a.force, sanitize=True)
+        return
     build_native(force=a.force)
     if not a.native_only:
         build(force=a.force, jobs=a.jobs)

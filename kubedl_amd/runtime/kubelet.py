@@ -64,11 +64,8 @@ _ENV_DENY = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADD
 
 
 def _spawner():
-    try:
-        from kubedl_amd import _native
-        return _native
-    except ImportError:  # pragma: no cover - the native module is part of build()
-        return None
+    from kubedl_amd.runtime import native  # KDL_NATIVE_SO: e.g. the sanitizer build
+    return native.load()
 
 
 class _Container:
