@@ -17,8 +17,9 @@ MI355X-first re-design:
   (``segment_reduce``) so only one row per unique id crosses xGMI.
 * **Dense tower on MFMA.**  ``FusedLinear`` runs forward as the hand-written
   ``gemm_bias_act`` kernel (v_mfma_f32_32x32x16_bf16, bias + ReLU fused in the
-  epilogue); backward fuses ReLU-mask + bias-gradient (``relu_bwd_dbias``) and
-  uses hipBLASLt for the two plain GEMMs.
+  epilogue); backward fuses ReLU-mask + bias-gradient (``relu_bwd_dbias``),
+  runs dx on ``gemm_bias_act`` and dW on the LDS-DMA weight-gradient kernel
+  (csrc/wgrad_dma.hip) -- no vendor GEMM in the step.
 
 On CPU (tests) every op has a torch composition with the same semantics.
 """
@@ -51,9 +52,31 @@ class _FusedLinearFn(torch.autograd.Function):
         ext = _ext.load()
         dy = dy.contiguous()
         dz, db = ext.relu_bwd_dbias(dy, y if ctx.relu else None)
-        dx = dz @ w
-        dw = dz.t() @ x
+        fout, fin = w.shape
+        # dx = dz . W on the same MFMA kernel as the forward (B operand = W^T rows)
+        dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
+        if fout % 64 == 0 and fin % 64 == 0:
+            # dW = dz^T x: the reduction over the batch is the weight-gradient
+            # form of csrc/wgrad_dma.hip (both operands row-major, LDS-DMA +
+            # transposed LDS reads; split-batch fp32 slabs, fixed-order reduce)
+            B = x.shape[0]
+            ws = _wgrad_workspace(ext, B, fout, fin, x.device)
+            dw = torch.empty(fout, fin, dtype=w.dtype, device=w.device)
+            ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1)
+        else:
+            dw = (dz.t() @ x).to(w.dtype)
         return dx, dw, (db.to(w.dtype) if ctx.has_b else None), None
+
+
+_WS = {}
+
+
+def _wgrad_workspace(ext, M, N, K, device):
+    key = (M, N, K, str(device))
+    ws = _WS.get(key)
+    if ws is None:
+        ws = _WS[key] = torch.empty(ext.conv1x1_wgrad_splits(M, N, K) * N * K, device=device)
+    return ws
 
 
 def fused_linear(x, w, b=None, relu=False):
@@ -203,7 +226,9 @@ class CTRModel:
                  device, dtype=torch.bfloat16):
         self.F, self.V, self.D, self.nd = n_fields, vocab_per_field, dim, n_dense
         self.k_in = n_fields * dim + n_dense
-        self.k_pad = (self.k_in + 7) // 8 * 8
+        # padded to 64 columns: every tower layer's weight gradient then fits the
+        # MFMA weight-gradient kernel's 64-wide tiles (no hipBLASLt in the step)
+        self.k_pad = (self.k_in + 63) // 64 * 64
         self.emb = emb
         self.device = torch.device(device)
         self.dtype = dtype

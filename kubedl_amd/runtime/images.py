@@ -41,6 +41,7 @@ REGISTRY: Dict[str, ImageEntry] = {
     "kubedl/tf-mnist-with-summaries": ImageEntry(_py("kubedl_amd.workers.tf_stub")),
     "merlintang/xgboost-dist-iris": ImageEntry(_py("kubedl_amd.workers.xgboost_dist")),
     "kubedl/xdl": ImageEntry(_py("kubedl_amd.workers.xdl_ctr")),
+    "kubedl/xdl-mnist-example": ImageEntry(_py("kubedl_amd.workers.xdl_ctr")),
     "xdl": ImageEntry(_py("kubedl_amd.workers.xdl_ctr")),
     "kubedl/git-sync": ImageEntry(_py("kubedl_amd.code_sync.git_sync"), readiness="start"),
     # bundled MI355X workloads
@@ -80,11 +81,46 @@ def _runnable(cmd0: str, cwd: Optional[str], path: str) -> bool:
 
 
 def _script_exists(argv: List[str], cwd: Optional[str]) -> bool:
-    """``python /var/tf_mnist/x.py``: the interpreter exists but its script may not."""
+    """``python /var/tf_mnist/x.py``: the interpreter exists but its script may
+    not.  Shell wrappers (``bash -c "exec python mnist.py ..."``, the XDL
+    example) are looked through: the check applies to the wrapped command."""
+    if len(argv) >= 3 and os.path.basename(argv[0]) in ("bash", "sh") and argv[1] == "-c":
+        import shlex
+        try:
+            inner = shlex.split(argv[2])
+        except ValueError:
+            return True
+        while inner and inner[0] == "exec":
+            inner = inner[1:]
+        return _script_exists(inner, cwd)
     if len(argv) >= 2 and os.path.basename(argv[0]).startswith("python") and not argv[1].startswith("-"):
         p = argv[1] if os.path.isabs(argv[1]) else os.path.join(cwd or ".", argv[1])
         return os.path.exists(p)
     return True
+
+
+def expand_env_refs(s: str, env: Dict[str, str]) -> str:
+    """Kubernetes dependent-variable expansion of a command/arg string:
+    ``$(NAME)`` becomes the container's ``NAME`` when it is defined (else it is
+    left as written), ``$$(NAME)`` is the escaped literal ``$(NAME)``."""
+    out, i, n = [], 0, len(s)
+    while i < n:
+        if s.startswith("$$", i):
+            out.append("$")
+            i += 2
+        elif s.startswith("$(", i):
+            j = s.find(")", i + 2)
+            name = s[i + 2:j] if j > 0 else ""
+            if j > 0 and name in env:
+                out.append(env[name])
+                i = j + 1
+            else:
+                out.append(s[i:j + 1] if j > 0 else s[i:])
+                i = j + 1 if j > 0 else n
+        else:
+            out.append(s[i])
+            i += 1
+    return "".join(out)
 
 
 def resolve_argv(container: dict, cwd: Optional[str], path: str) -> (List[str], str):

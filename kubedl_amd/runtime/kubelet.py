@@ -227,6 +227,8 @@ class PodWorker(threading.Thread):
         nat = self.k.native
         try:
             argv, cs.readiness = images.resolve_argv(ctr, cwd, env.get("PATH", ""))
+            # $(VAR) references in command/args (k8s dependent-variable expansion)
+            argv = [images.expand_env_refs(a, env) for a in argv]
             with open(cs.log_path, "a") as f:
                 f.write(f"[kdl-kubelet] {c.now()} start {cs.name} (restart {cs.restart_count}): "
                         f"{' '.join(argv)}\n")

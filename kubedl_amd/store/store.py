@@ -29,6 +29,7 @@ import os
 import socket
 import sqlite3
 import threading
+import time
 import uuid
 from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
 
@@ -71,7 +72,10 @@ class Store:
         self._watchers: List[Tuple[Optional[str], Callable[[str, Dict[str, Any]], None]]] = []
         self._ports: Dict[str, int] = {}
         self._port_range = port_range
-        self._next_port = port_range[0]
+        # start the scan at a per-store offset: two control planes on one host
+        # (parallel test workers, two `kdl` homes) would otherwise hand out the
+        # same first port between its free-check and the rank's bind
+        self._next_port = port_range[0] + (os.getpid() * 7919 + time.monotonic_ns()) % (port_range[1] - port_range[0])
         self._db: Optional[sqlite3.Connection] = None
         if db_path:
             self._open_db(db_path)
