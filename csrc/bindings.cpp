@@ -495,6 +495,51 @@ std::vector<at::Tensor> relu_bwd_dbias(const at::Tensor& dy, const c10::optional
   return {dz, db};
 }
 
+static void check_head(const at::Tensor& x, const at::Tensor& w, const char* who) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
+              who, ": x bf16 [M,K] contiguous");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == x.size(1), who, ": w bf16 [K]");
+  TORCH_CHECK(x.size(1) % 8 == 0, who, ": K % 8 == 0");
+}
+
+std::vector<at::Tensor> head_bce_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                     const at::Tensor& y) {
+  check_head(x, w, "head_bce_fwd");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(b.scalar_type() == at::kFloat && b.numel() == 1 && b.is_cuda(), "head_bce_fwd: bias f32 [1]");
+  TORCH_CHECK(y.scalar_type() == at::kFloat && y.numel() == M && y.is_contiguous(), "head_bce_fwd: labels f32 [M]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto opt = x.options().dtype(at::kFloat);
+  auto logit = at::empty({M}, opt), dlogit = at::empty({M}, opt), part = at::empty({(M + 3) / 4}, opt);
+  check_hip(kdl::head_bce_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), y.data_ptr<float>(),
+                              static_cast<int>(M), static_cast<int>(K), logit.data_ptr<float>(),
+                              dlogit.data_ptr<float>(), part.data_ptr<float>(), cur_stream()),
+            "head_bce_fwd");
+  return {logit, dlogit, part};
+}
+
+std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dlogit,
+                                     double scale, const c10::optional<at::Tensor>& gscale) {
+  check_head(x, w, "head_bce_bwd");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(dlogit.scalar_type() == at::kFloat && dlogit.numel() == M && dlogit.is_contiguous(),
+              "head_bce_bwd: dlogit f32 [M]");
+  const bool has_g = gscale.has_value() && gscale->defined();
+  if (has_g)
+    TORCH_CHECK(gscale->scalar_type() == at::kFloat && gscale->numel() == 1 && gscale->is_cuda(),
+                "head_bce_bwd: gscale f32 [1]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int nb = kdl::head_bce_bwd_blocks(static_cast<int>(M));
+  auto opt = x.options().dtype(at::kFloat);
+  auto dx = at::empty_like(x), dw = at::empty({nb, K}, opt), db = at::empty({nb}, opt);
+  check_hip(kdl::head_bce_bwd(x.data_ptr(), w.data_ptr(), dlogit.data_ptr<float>(), static_cast<float>(scale),
+                              has_g ? gscale->data_ptr<float>() : nullptr, static_cast<int>(M), static_cast<int>(K),
+                              dx.data_ptr(), dw.data_ptr<float>(),
+                              db.data_ptr<float>(), cur_stream()),
+            "head_bce_bwd");
+  return {dx, dw, db};
+}
+
 void embed_gather(const at::Tensor& table, const at::Tensor& idx, int64_t F, at::Tensor out, int64_t col0) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous(), "embed_gather: table [V, D]");
   TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous(), "embed_gather: int64 idx");
@@ -938,6 +983,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
   m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b)");
   m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient");
+  m.def("head_bce_fwd", &head_bce_fwd, "1-wide logit layer + sigmoid BCE: (logit, dlogit, per-block loss sums)");
+  m.def("head_bce_bwd", &head_bce_bwd, "logit layer backward: (dx, per-block dw partials, per-block db partials)");
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");

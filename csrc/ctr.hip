@@ -20,6 +20,12 @@
 // segment_reduce / segment_adagrad: rows sorted by key; one wave per unique
 //   key sums its segment (fixed order -> bitwise reproducible) and either
 //   writes the sum or applies Adagrad to the owned table row in place.
+// head_bce_fwd / head_bce_bwd: the tower's 1-wide logit layer fused with the
+//   sigmoid-BCE loss.  A [K] -> 1 projection is a GEMV (no MFMA shape), so it
+//   runs as one wave per row (dot product in registers + DPP reduction), the
+//   loss and dlogit computed in the same pass; the backward writes
+//   dx = dlogit * w and per-block fp32 partials of dw / db (reduced in fixed
+//   order by the caller) -- no vendor GEMM for the N=1 layer.
 #include "common.h"
 #include "kdl_api.h"
 
@@ -275,7 +281,129 @@ __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __res
   }
 }
 
+// ---------------------------------------------------------------- logit head + BCE
+// one wave per row: logit = x[m,:] . w + b; loss_m = softplus(l) - y l;
+// dlogit_m = sigmoid(l) - y.  Each block writes the sum of its rows' losses.
+__global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ w, const float* __restrict__ b,
+                                                           const float* __restrict__ y, int M, int K,
+                                                           float* __restrict__ logit, float* __restrict__ dlogit,
+                                                           float* __restrict__ loss_part) {
+  __shared__ float wave_loss[4];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + wv;
+  float l = 0.f;
+  if (m < M) {
+    const bf16_t* xr = x + static_cast<int64_t>(m) * K;
+    float acc = 0.f;
+    for (int k = lane * 8; k < K; k += 512) {
+      float xv[8], wv8[8];
+      Vec<bf16_t, 8>::load(xr + k, xv);
+      Vec<bf16_t, 8>::load(w + k, wv8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += xv[i] * wv8[i];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    const float z = acc + b[0];
+    const float t = y[m];
+    // softplus(z) - t z, stable for both signs
+    l = fmaxf(z, 0.f) - t * z + log1pf(__expf(-fabsf(z)));
+    if (lane == 0) {
+      logit[m] = z;
+      dlogit[m] = 1.f / (1.f + __expf(-z)) - t;
+    }
+  }
+  if (lane == 0) wave_loss[wv] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) loss_part[blockIdx.x] = (wave_loss[0] + wave_loss[1]) + (wave_loss[2] + wave_loss[3]);
+}
+
+// block = 256 threads = 8 row lanes x 32 column groups of 8 (K <= 256 per
+// pass, looped for wider K); rows [blockIdx.x*rpb, +rpb).  dx = g*w (bf16),
+// dw partial[block, k] = sum g*x, db partial[block] = sum g; g = dlogit*scale.
+__global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ w,
+                                                           const float* __restrict__ dlogit, float scale,
+                                                           const float* __restrict__ gscale, int M,
+                                                           int K, int rpb, bf16_t* __restrict__ dx,
+                                                           float* __restrict__ dw_part, float* __restrict__ db_part) {
+  __shared__ float red[8][257];
+  if (gscale != nullptr) scale *= gscale[0];  // upstream gradient of the loss, read on the device
+  const int rl = threadIdx.x >> 5, cg = threadIdx.x & 31;
+  const int m0 = blockIdx.x * rpb;
+  const int m1 = (m0 + rpb) < M ? (m0 + rpb) : M;
+  float gsum = 0.f;
+  for (int kb = 0; kb < K; kb += 256) {
+    const int k = kb + cg * 8;
+    const bool on = k < K;
+    float wv8[8], s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    if (on) Vec<bf16_t, 8>::load(w + k, wv8);
+    for (int m = m0 + rl; m < m1; m += 8) {
+      const float g = dlogit[m] * scale;
+      if (kb == 0 && cg == 0) gsum += g;
+      if (!on) continue;
+      float xv[8], d[8];
+      const int64_t o = static_cast<int64_t>(m) * K + k;
+      Vec<bf16_t, 8>::load(x + o, xv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s[i] += g * xv[i];
+        d[i] = g * wv8[i];
+      }
+      Vec<bf16_t, 8>::store(dx + o, d);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[rl][cg * 8 + i] = s[i];
+    if (kb == 0 && cg == 0) red[rl][256] = gsum;
+    __syncthreads();
+    // fixed-order sum over the 8 row lanes
+    const int c = threadIdx.x;  // 0..255 -> column kb + c
+    if (kb + c < K) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += red[r][c];
+      dw_part[static_cast<int64_t>(blockIdx.x) * K + kb + c] = t;
+    }
+    if (kb == 0 && threadIdx.x == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += red[r][256];
+      db_part[blockIdx.x] = t;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+hipError_t head_bce_fwd(const void* x, const void* w, const float* b, const float* y, int M, int K, float* logit,
+                        float* dlogit, float* loss_part, hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  hipLaunchKernelGGL(head_bce_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                     static_cast<const bf16_t*>(w), b, y, M, K, logit, dlogit, loss_part);
+  return hipGetLastError();
+}
+
+int head_bce_bwd_blocks(int M) {
+  // >= 2 resident rounds over 256 CUs at 64 rows per block, at most 1024 partials
+  const int rpb = 64;
+  int nb = (M + rpb - 1) / rpb;
+  return nb < 1024 ? nb : 1024;
+}
+
+hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
+                        int K, void* dx, float* dw_part, float* db_part, hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  const int nb = head_bce_bwd_blocks(M);
+  const int rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(head_bce_bwd_kernel, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                     static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx), dw_part,
+                     db_part);
+  return hipGetLastError();
+}
 
 hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, bool relu,
                          hipStream_t s) {

@@ -149,6 +149,11 @@ hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32
 hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, bool relu,
                          hipStream_t s);
 hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* dbias, int M, int N, hipStream_t s);
+hipError_t head_bce_fwd(const void* x, const void* w, const float* b, const float* y, int M, int K, float* logit,
+                        float* dlogit, float* loss_part, hipStream_t s);
+int head_bce_bwd_blocks(int M);
+hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
+                        int K, void* dx, float* dw_part, float* db_part, hipStream_t s);
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s);
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,

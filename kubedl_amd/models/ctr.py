@@ -19,7 +19,9 @@ MI355X-first re-design:
   ``gemm_bias_act`` kernel (v_mfma_f32_32x32x16_bf16, bias + ReLU fused in the
   epilogue); backward fuses ReLU-mask + bias-gradient (``relu_bwd_dbias``),
   runs dx on ``gemm_bias_act`` and dW on the LDS-DMA weight-gradient kernel
-  (csrc/wgrad_dma.hip) -- no vendor GEMM in the step.
+  (csrc/wgrad_dma.hip); the 1-wide logit layer is fused with the sigmoid-BCE
+  loss (``head_bce_fwd/bwd``: a GEMV per row + loss + dlogit in one pass,
+  dx / dw / db in one backward pass) -- no vendor GEMM in the step.
 
 On CPU (tests) every op has a torch composition with the same semantics.
 """
@@ -88,6 +90,42 @@ def fused_linear(x, w, b=None, relu=False):
     return torch.relu(y) if relu else y
 
 
+class _HeadBCEFn(torch.autograd.Function):
+    """mean_m BCEWithLogits(x[m] . w + b, y[m]) for a [K] -> 1 head."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, y):
+        ext = _ext.load()
+        x = x.contiguous()
+        logit, dlogit, part = ext.head_bce_fwd(x, w.reshape(-1).contiguous(), b.float().reshape(1),
+                                               y.float().contiguous())
+        ctx.save_for_backward(x, w, dlogit)
+        ctx.b_dtype = b.dtype
+        ctx.mark_non_differentiable(logit)
+        return part.sum() / x.shape[0], logit
+
+    @staticmethod
+    def backward(ctx, gloss, _glogit):
+        x, w, dlogit = ctx.saved_tensors
+        ext = _ext.load()
+        dx, dw_part, db_part = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0],
+                                                gloss.float().reshape(1).contiguous())
+        # per-block partials summed in a fixed order (deterministic)
+        dw = dw_part.sum(0).to(w.dtype).reshape(w.shape)
+        db = db_part.sum().to(ctx.b_dtype).reshape(1)
+        return dx, dw, db, None
+
+
+def head_bce(x, w, b, y):
+    """(loss, logits) of the logit layer + mean sigmoid BCE."""
+    if x.is_cuda and _ext.available() and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+        return _HeadBCEFn.apply(x, w, b, y)
+    if x.is_cuda and not _ext.available():
+        _ext.require_on_gpu("head_bce")
+    logit = torch.nn.functional.linear(x, w, b).float().squeeze(-1)
+    return torch.nn.functional.binary_cross_entropy_with_logits(logit, y.float()), logit.detach()
+
+
 class FusedLinear(nn.Module):
     def __init__(self, fin: int, fout: int, relu: bool):
         super().__init__()
@@ -111,6 +149,13 @@ class DenseTower(nn.Module):
         for l in self.layers:
             x = l(x)
         return self.head(x).float().squeeze(-1)
+
+    def loss(self, x, y):
+        """Training step forward: (mean BCE loss, logits); the head runs fused
+        with the loss (``head_bce``)."""
+        for l in self.layers:
+            x = l(x)
+        return head_bce(x, self.head.weight, self.head.bias, y)
 
 
 # ---------------------------------------------------------------- sparse embedding
@@ -152,15 +197,23 @@ class ShardedEmbedding:
             return out
         return self.table[local_rows]
 
-    def _apply_updates(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:
-        """Sum duplicate rows and apply Adagrad on the owned shard."""
-        if ids_local.numel() == 0:
+    def _apply_updates(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float,
+                       distinct: bool = False) -> None:
+        """Sum duplicate rows and apply Adagrad on the owned shard.  ``distinct``:
+        the caller's ids are already unique (a world-1 push of the pull's
+        de-duplicated ids) -- every segment is one row, no sort needed."""
+        n = ids_local.numel()
+        if n == 0:
             return
-        uniq, inv = torch.unique(ids_local, return_inverse=True)
-        order = torch.argsort(inv, stable=True)
-        counts = torch.bincount(inv, minlength=uniq.numel())
-        seg = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=self.device)
-        seg[1:] = torch.cumsum(counts, 0)
+        if distinct:
+            uniq, inv = ids_local, torch.arange(n, device=self.device)
+            order, seg = inv, torch.arange(n + 1, device=self.device)
+        else:
+            uniq, inv = torch.unique(ids_local, return_inverse=True)
+            order = torch.argsort(inv, stable=True)
+            counts = torch.bincount(inv, minlength=uniq.numel())
+            seg = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=self.device)
+            seg[1:] = torch.cumsum(counts, 0)
         if self.use_hip:
             _ext.load().segment_adagrad(grads.contiguous().float(), order, seg, uniq, self.table, self.accum,
                                         self.lr, self.eps, scale)
@@ -204,7 +257,7 @@ class ShardedEmbedding:
         uniq_sorted, order = ctx[0], ctx[1]
         g_sorted = grad_unique[order]
         if ctx[2] is None:
-            self._apply_updates(uniq_sorted // self.n_own, g_sorted, scale)
+            self._apply_updates(uniq_sorted // self.n_own, g_sorted, scale, distinct=True)
             return
         send_l, recv_l, req = ctx[2], ctx[3], ctx[4]
         g_recv = _a2a(recv_l, send_l, g_sorted.float(), self.group)

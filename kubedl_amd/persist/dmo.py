@@ -29,6 +29,7 @@ from typing import Dict, Optional
 
 from kubedl_amd.api import common as c
 from kubedl_amd.api import kinds as K
+from kubedl_amd.utils import k8sutil
 
 # ---------------------------------------------------------------- quantities
 _SUFFIX = {"": 1, "m": Fraction(1, 1000), "k": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12,
@@ -78,9 +79,11 @@ def _res_max(a: Dict[str, Fraction], b: Dict[str, Fraction]):
 
 
 def compute_pod_resources(pod_spec: dict) -> dict:
-    """max(max over init containers, sum over containers), requests and limits."""
+    """max(max over init containers, sum over containers), requests and limits.
+    Key order is the serialised ``ResourceRequirements`` (limits, requests;
+    resource names sorted) so ``go_json`` reproduces the reference's column."""
     res = {}
-    for sect in ("requests", "limits"):
+    for sect in ("limits", "requests"):
         init_max: Dict[str, Fraction] = {}
         for ic in pod_spec.get("initContainers") or []:
             cur = {k: parse_quantity(v) for k, v in ((ic.get("resources") or {}).get(sect) or {}).items()}
@@ -90,6 +93,11 @@ def compute_pod_resources(pod_spec: dict) -> dict:
         if tot:
             res[sect] = {k: format_quantity(v, _is_binary(k)) for k, v in sorted(tot.items())}
     return res
+
+
+def go_json(obj) -> str:
+    """``encoding/json`` shape: compact separators, dict order as built."""
+    return json.dumps(obj, separators=(",", ":"))
 
 
 # ---------------------------------------------------------------- tenancy
@@ -124,11 +132,11 @@ def job_to_dmo(job: dict, region: str = "") -> dict:
     if st.get("completionTime"):
         row["gmt_finished"] = st["completionTime"]
     res = {}
-    for rt, spec in specs.items():
-        rr = {"resources": compute_pod_resources((spec.get("template") or {}).get("spec") or {}),
-              "replicas": int(spec["replicas"]) if spec.get("replicas") is not None else 0}
-        res[rt] = rr
-    row["resources"] = json.dumps(res, sort_keys=True)
+    for rt in sorted(specs):  # Go marshals map keys sorted; struct fields in declaration order
+        spec = specs[rt]
+        res[rt] = {"resources": compute_pod_resources((spec.get("template") or {}).get("spec") or {}),
+                   "replicas": int(spec["replicas"]) if spec.get("replicas") is not None else 0}
+    row["resources"] = go_json(res)
     return row
 
 
@@ -136,16 +144,9 @@ class ConvertError(ValueError):
     pass
 
 
-def resolve_dependent_owner(obj: dict) -> str:
-    for r in (obj.get("metadata") or {}).get("ownerReferences") or []:
-        if r.get("controller") and r.get("kind") in K.BY_KIND:
-            return r.get("uid", "")
-    return ""
-
-
 def pod_to_dmo(pod: dict, default_container: str, region: str = "") -> dict:
     md = pod["metadata"]
-    job_id = resolve_dependent_owner(pod)
+    job_id, _ = k8sutil.resolve_dependent_owner(pod)
     if not job_id:
         raise ConvertError("object has no dependent owner")
     rtype = (md.get("labels") or {}).get(c.REPLICA_TYPE_LABEL)
@@ -156,9 +157,9 @@ def pod_to_dmo(pod: dict, default_container: str, region: str = "") -> dict:
     row = {"name": md["name"], "namespace": md["namespace"], "pod_id": md.get("uid", ""),
            "version": md.get("resourceVersion", ""), "gmt_created": md.get("creationTimestamp"),
            "deploy_region": region or None, "job_id": job_id, "replica_type": rtype,
-           "resources": json.dumps(compute_pod_resources(spec), sort_keys=True),
+           "resources": go_json(compute_pod_resources(spec)),
            "deleted": 0, "is_in_etcd": 1, "pod_ip": st.get("podIP") or None,
-           "host_ip": st.get("hostIP") or None, "image": "", "status": "Unknown",
+           "host_ip": st.get("hostIP") or None, "image": "", "status": "",
            "gmt_started": None, "gmt_finished": None, "remark": None}
     ctrs = spec.get("containers") or []
     if not ctrs:
@@ -169,6 +170,7 @@ def pod_to_dmo(pod: dict, default_container: str, region: str = "") -> dict:
             image = ct.get("image", "")
             break
     row["image"] = image
+    row["status"] = "Unknown"  # defaulted once the pod has containers (converters/pod.go:97)
     css = st.get("containerStatuses") or []
     if not css:
         return row
@@ -177,7 +179,7 @@ def pod_to_dmo(pod: dict, default_container: str, region: str = "") -> dict:
         if x.get("name") == default_container:
             cs = x
             break
-    phase = st.get("phase", "Unknown")
+    phase = st.get("phase", "")
     row["status"] = phase
     state = cs.get("state") or {}
     if phase == "Running":
@@ -200,5 +202,5 @@ def event_to_dmo(ev: dict, region: str = "") -> dict:
     return {"name": ev["metadata"]["name"], "kind": io.get("kind", ""), "type": ev.get("type", ""),
             "obj_namespace": io.get("namespace", ""), "obj_name": io.get("name", ""),
             "obj_uid": io.get("uid", ""), "reason": ev.get("reason", ""), "message": ev.get("message", ""),
-            "count": int(ev.get("count", 1)), "region": region or None,
+            "count": int(ev.get("count") or 0), "region": region or None,
             "first_timestamp": ev.get("firstTimestamp"), "last_timestamp": ev.get("lastTimestamp")}

@@ -47,6 +47,10 @@ if want bnsweep; then
   done
 fi
 want convgemm && run_step conv_vs_gemm 600 python scripts/conv_vs_gemm.py
+want ctr && run_step ctr 300 python -u -m kubedl_amd.workers.xdl_ctr
+want ctrprof && run_step ctr_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ctr_prof -o run -- python -u -m kubedl_amd.workers.xdl_ctr --steps 10 --warmup 3
+want gbdt && run_step gbdt 300 python -u -m kubedl_amd.workers.xgboost_dist
+want gbdtprof && run_step gbdt_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gbdt_prof -o run -- python -u -m kubedl_amd.workers.xgboost_dist
 want benchimm && run_step bench_immediate 600 python bench.py --steps 20 --warmup 8 --conv-benchmark 0
 # ship the MIOpen find-db / kernel cache back (merged into gpurun_out/)
 if [ -d miopen_db ]; then mkdir -p gpurun_out/miopen_db && cp -r miopen_db/. gpurun_out/miopen_db/; du -sh gpurun_out/miopen_db; fi

@@ -117,6 +117,30 @@ def test_fused_linear_backward_matches_autograd():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,K", [(4096, 256), (1000, 128), (77, 520)])
+def test_head_bce_matches_fp32(M, K):
+    """Fused logit layer + sigmoid BCE (csrc/ctr.hip head_bce_*) vs fp32 autograd,
+    including a non-unit upstream gradient and K > 256 (looped column passes)."""
+    from kubedl_amd.models.ctr import head_bce
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").relu().bfloat16().requires_grad_(True)
+    w = (torch.randn(1, K, device="cuda") / K ** 0.5).bfloat16().requires_grad_(True)
+    b = torch.tensor([0.3], device="cuda").bfloat16().requires_grad_(True)
+    y = (torch.rand(M, device="cuda") < 0.4).float()
+    loss, logit = head_bce(x, w, b, y)
+    (loss * 2.5).backward()
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    lr_ = (xr @ wr.t() + br).squeeze(-1)
+    ref = torch.nn.functional.binary_cross_entropy_with_logits(lr_, y)
+    (ref * 2.5).backward()
+    torch.testing.assert_close(logit, lr_.detach(), atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(loss.float(), ref.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-4, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=2e-3, rtol=2e-2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=2e-3, rtol=2e-2)
+
+
+@pytest.mark.gpu
 def test_embedding_kernels_match_torch():
     from kubedl_amd.ops import _ext
     ext = _ext.load()

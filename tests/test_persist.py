@@ -78,8 +78,13 @@ def test_pod_to_dmo():
                                                         "finishedAt": "F", "message": "m"}}), "tensorflow")
     assert row["remark"] == "Reason: OOMKilled\nExitCode: 137\nMessage: m"
     assert row["gmt_started"] == "S" and row["gmt_finished"] == "F"
+    # any controller reference is the dependent owner (k8sutil.ResolveDependentOwner);
+    # the persist controller only feeds pods owned by a job kind
+    assert dmo.pod_to_dmo(_pod("Running", owner_kind="ReplicaSet"), "tensorflow")["job_id"] == "uid-1"
+    p = _pod("Running")
+    p["metadata"]["ownerReferences"] = []
     with pytest.raises(dmo.ConvertError):
-        dmo.pod_to_dmo(_pod("Running", owner_kind="ReplicaSet"), "tensorflow")
+        dmo.pod_to_dmo(p, "tensorflow")
 
 
 def test_sqlite_object_backend(tmp_path):
