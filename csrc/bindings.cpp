@@ -435,7 +435,8 @@ std::vector<at::Tensor> gbdt_split(const at::Tensor& hist, double lambda, double
   check_hip(kdl::gbdt_split_find(hist.data_ptr<float>(), static_cast<int>(nodes), static_cast<int>(F),
                                  static_cast<int>(B), static_cast<float>(lambda),
                                  static_cast<float>(min_child_weight), gain.data_ptr<float>(),
-                                 bin.data_ptr<int32_t>(), gl.data_ptr<float>(), hl.data_ptr<float>(), cur_stream()),
+                                 bin.data_ptr<int32_t>(), gl.data_ptr<float>(), hl.data_ptr<float>(), nullptr,
+                                 cur_stream()),
             "gbdt_split_find");
   return {gain, bin, gl, hl};
 }
@@ -949,7 +950,10 @@ void destroy_stream_py(int64_t handle) {
 void spin_py(double microseconds) { check_hip(kdl::spin(cur_stream(), microseconds), "spin"); }
 
 
+void register_gbdt(pybind11::module& m);  // gbdt_grower.cpp
+
 PYBIND11_MODULE(_C, m) {
+  register_gbdt(m);
   m.def("make_stream", &make_stream_py, "new HIP stream (dedicated=True: own hardware queue via a full CU mask)",
         py::arg("dedicated"), py::arg("priority") = 0);
   m.def("destroy_stream", &destroy_stream_py, "destroy a stream from make_stream");

@@ -19,6 +19,24 @@
 //     GL^2/(HL+l) + GR^2/(HR+l) - G^2/(H+l)
 //   subject to min_child_weight on both sides, block argmax -> best split.
 //
+// Device-resident tree growth (no host round trip inside a tree; the host only
+// enqueues a fixed kernel sequence per level):
+//   nodes live in heap order (level d = heap ids [2^d-1, 2^(d+1)-1)); each row
+//   carries its heap node id (``node_of_row``) and ``rows`` keeps rows grouped by
+//   node, node i of the level owning rows[lo[i] .. hi[i]).  Per level:
+//   split_find -> gbdt_decide (argmax over features, leaf weight, tree arrays)
+//   -> gbdt_route_flags (1 = goes right) -> inclusive scan of the flags
+//   -> gbdt_partition (stable in-segment partition: left rows keep their
+//   order, then right rows; node ids advanced to 2h+1 / 2h+2)
+//   -> gbdt_children (child segments; the smaller child by row count is the
+//   one whose histogram gets built) -> gbdt_hist_plan (chunks per built node,
+//   exclusive prefix) -> hist_build_wq (work-queue grid: block -> (node,
+//   chunk) by binary search over the prefix) -> gbdt_subtract (sibling =
+//   parent - built).  With > 1 rank the child counts and the built histograms
+//   are all-reduced between these kernels (RCCL), nothing else.
+// gbdt_quantise: bins = number of cuts < x (torch.bucketize right=False), one
+//   thread per element, binary search over the feature's cut row.
+//
 // The reference runs XGBoost/rabit inside a user image; the
 // distributed part here is an RCCL all-reduce of the level's histograms.
 #include "common.h"
@@ -86,7 +104,7 @@ __device__ __forceinline__ float wave_incl_scan(float v) {
 __global__ __launch_bounds__(256) void split_find_kernel(
     const float* __restrict__ hist, int F, int B, float lambda, float min_child_weight,
     float* __restrict__ best_gain, int32_t* __restrict__ best_bin, float* __restrict__ best_gl,
-    float* __restrict__ best_hl) {
+    float* __restrict__ best_hl, float* __restrict__ node_tot) {
   __shared__ float carry_g[4], carry_h[4];
   __shared__ float red_gain[4];
   __shared__ int red_bin[4];
@@ -113,6 +131,10 @@ __global__ __launch_bounds__(256) void split_find_kernel(
     }
     tot_g += carry_g[w];
     tot_h += carry_h[w];
+  }
+  if (node_tot != nullptr && f == 0 && t == 0) {
+    node_tot[2 * node] = tot_g;
+    node_tot[2 * node + 1] = tot_h;
   }
   const float gl = sg + pre_g, hl = sh + pre_h;  // rows with bin <= t go left
   const float gr = tot_g - gl, hr = tot_h - hl;
@@ -180,6 +202,255 @@ __global__ __launch_bounds__(256) void route_rows_kernel(
   go_right[i] = r;
 }
 
+// ---------------------------------------------------------------- device-resident growth
+// Work-queue histogram build: block c of the grid works on chunk c of the
+// concatenated chunk lists of the ``nb`` built nodes (chunk_off = exclusive
+// prefix of ceil(size / rpb), chunk_off[nb] = total).  Each wave keeps UNROLL
+// row slots in flight (row ids, g/h and bin codes loaded before any LDS
+// atomic) so the dependent global loads overlap.
+template <int UNROLL>
+__global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
+    const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
+    int64_t gh_stride, const int32_t* __restrict__ rows, const int32_t* __restrict__ blo,
+    const int32_t* __restrict__ bhi, const int32_t* __restrict__ chunk_off, int nb, int F, int B, int rpb, int fp,
+    float* __restrict__ hist) {
+  extern __shared__ float lds[];  // [fp][B][2]
+  const int c = blockIdx.x;
+  if (c >= chunk_off[nb]) return;  // block-uniform
+  int a = 0, z = nb;               // last j with chunk_off[j] <= c
+  while (z - a > 1) {
+    const int m = (a + z) >> 1;
+    if (chunk_off[m] <= c) a = m; else z = m;
+  }
+  const int j = a;
+  const int r0 = blo[j] + (c - chunk_off[j]) * rpb;
+  const int r1 = (r0 + rpb) < bhi[j] ? (r0 + rpb) : bhi[j];
+  const int f0 = blockIdx.y * fp;
+  const int nf = (F - f0) < fp ? (F - f0) : fp;
+  const int t = threadIdx.x;
+  for (int i = t; i < nf * B * 2; i += kHistBlock) lds[i] = 0.f;
+  __syncthreads();
+  const int lane = t & 63, wave = t >> 6;
+  const int rpw = 64 / fp;
+  const int sub = lane / fp, fl = lane - sub * fp;
+  const int step = (kHistBlock / 64) * rpw;  // rows per block-wide slot
+  for (int base = r0 + wave * rpw + sub; base < r1; base += step * UNROLL) {
+    int row[UNROLL];
+    float g[UNROLL], h[UNROLL];
+    int b[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int r = base + u * step;
+      row[u] = r < r1 ? rows[r] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (row[u] >= 0) {
+        g[u] = grad[static_cast<int64_t>(row[u]) * gh_stride];
+        h[u] = hess[static_cast<int64_t>(row[u]) * gh_stride];
+        b[u] = fl < nf ? bins[static_cast<int64_t>(row[u]) * F + f0 + fl] : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (row[u] >= 0 && fl < nf) {
+        float* p = lds + (fl * B + b[u]) * 2;
+        atomicAdd(p, g[u]);
+        atomicAdd(p + 1, h[u]);
+      }
+    }
+  }
+  __syncthreads();
+  float* out = hist + (static_cast<int64_t>(j) * F + f0) * B * 2;
+  for (int i = t; i < nf * B * 2; i += kHistBlock) {
+    const float v = lds[i];
+    if (v != 0.f) __hip_atomic_fetch_add(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// one thread: chunk_off[j+1] = chunk_off[j] + ceil((bhi[j] - blo[j]) / rpb)
+__global__ void hist_plan_kernel(const int32_t* __restrict__ blo, const int32_t* __restrict__ bhi, int nb, int rpb,
+                                 int32_t* __restrict__ chunk_off) {
+  if (threadIdx.x != 0) return;
+  int acc = 0;
+  chunk_off[0] = 0;
+  for (int j = 0; j < nb; ++j) {
+    const int n = bhi[j] - blo[j];
+    acc += n > 0 ? (n + rpb - 1) / rpb : 0;
+    chunk_off[j + 1] = acc;
+  }
+}
+
+// thread per level node i (heap id h0 + i): best feature (ties -> lower id),
+// split decision, leaf weight, tree arrays; split[i] and the children's
+// existence for the next level.
+__global__ __launch_bounds__(256) void decide_kernel(
+    const float* __restrict__ gain, const int32_t* __restrict__ sbin, const float* __restrict__ tot,
+    const float* __restrict__ cuts, const int32_t* __restrict__ exists, int L, int F, int ncut, int h0,
+    int can_split, float lambda, float gamma, float lr, int32_t* __restrict__ t_feat,
+    int32_t* __restrict__ t_bin, float* __restrict__ t_thr, float* __restrict__ t_val, int32_t* __restrict__ split,
+    int32_t* __restrict__ exists_next) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  const int h = h0 + i;
+  const bool ex = exists[i] != 0;
+  float bg = -INFINITY;
+  int bf = -1;
+  for (int f = 0; f < F; ++f) {
+    const float v = gain[static_cast<int64_t>(i) * F + f];
+    if (v > bg) {
+      bg = v;
+      bf = f;
+    }
+  }
+  const bool sp = ex && can_split && bf >= 0 && bg > gamma && bg < INFINITY;
+  const int bb = sp ? sbin[static_cast<int64_t>(i) * F + bf] : -1;
+  t_feat[h] = sp ? bf : -1;
+  t_bin[h] = bb;
+  t_thr[h] = sp ? (bb < ncut ? cuts[static_cast<int64_t>(bf) * ncut + bb] : INFINITY) : 0.f;
+  t_val[h] = ex ? -tot[2 * i] / (tot[2 * i + 1] + lambda) * lr : 0.f;
+  split[i] = sp ? 1 : 0;
+  if (exists_next != nullptr) {
+    exists_next[2 * i] = sp ? 1 : 0;
+    exists_next[2 * i + 1] = sp ? 1 : 0;
+  }
+}
+
+// flag[p] = 1 when the row at position p belongs to a splitting node of the
+// level and goes right.
+__global__ __launch_bounds__(256) void route_flags_kernel(
+    const uint8_t* __restrict__ bins, const int32_t* __restrict__ rows, const int32_t* __restrict__ node_of_row,
+    const int32_t* __restrict__ split, const int32_t* __restrict__ t_feat, const int32_t* __restrict__ t_bin,
+    int F, int n, int h0, int L, int32_t* __restrict__ flag) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const int row = rows[p];
+  const int i = node_of_row[row] - h0;
+  int r = 0;
+  if (i >= 0 && i < L && split[i]) {
+    const int h = h0 + i;
+    r = bins[static_cast<int64_t>(row) * F + t_feat[h]] > t_bin[h] ? 1 : 0;
+  }
+  flag[p] = r;
+}
+
+// stable in-segment partition by flag (sc = inclusive scan of flag over all
+// positions): left rows first, then right rows, each in their old order.
+__global__ __launch_bounds__(256) void partition_kernel(
+    const int32_t* __restrict__ rows, int32_t* __restrict__ node_of_row, const int32_t* __restrict__ split,
+    const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, const int32_t* __restrict__ flag,
+    const int32_t* __restrict__ sc, int n, int h0, int L, int32_t* __restrict__ rows_next) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const int row = rows[p];
+  const int hn = node_of_row[row];
+  const int i = hn - h0;
+  if (i >= 0 && i < L && split[i]) {
+    const int s0 = lo[i], s1 = hi[i];
+    const int base = s0 > 0 ? sc[s0 - 1] : 0;
+    const int rb = sc[p] - flag[p] - base;  // right rows before p in the segment
+    const int rt = sc[s1 - 1] - base;
+    const int nl = (s1 - s0) - rt;
+    int np, child;
+    if (flag[p]) {
+      np = s0 + nl + rb;
+      child = 2 * hn + 2;
+    } else {
+      np = s0 + (p - s0 - rb);
+      child = 2 * hn + 1;
+    }
+    rows_next[np] = row;
+    node_of_row[row] = child;
+  } else {
+    rows_next[p] = row;
+  }
+}
+
+// thread per parent i: child segments and counts; when ``pick`` (counts are
+// already global) also the built (smaller) child and its segment.
+__global__ __launch_bounds__(256) void children_kernel(
+    const int32_t* __restrict__ split, const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
+    const int32_t* __restrict__ sc, int L, int32_t* __restrict__ lo_next, int32_t* __restrict__ hi_next,
+    float* __restrict__ cnt, int pick, int32_t* __restrict__ build_child, int32_t* __restrict__ blo,
+    int32_t* __restrict__ bhi) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  int a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  // a node split on the global histogram may own no rows on this rank
+  if (split[i] && hi[i] > lo[i]) {
+    const int s0 = lo[i], s1 = hi[i];
+    const int base = s0 > 0 ? sc[s0 - 1] : 0;
+    const int nl = (s1 - s0) - (sc[s1 - 1] - base);
+    a0 = s0;
+    a1 = s0 + nl;
+    b0 = s0 + nl;
+    b1 = s1;
+  }
+  lo_next[2 * i] = a0;
+  hi_next[2 * i] = a1;
+  lo_next[2 * i + 1] = b0;
+  hi_next[2 * i + 1] = b1;
+  cnt[2 * i] = static_cast<float>(a1 - a0);
+  cnt[2 * i + 1] = static_cast<float>(b1 - b0);
+  if (pick) {
+    const int c = (a1 - a0) <= (b1 - b0) ? 0 : 1;
+    build_child[i] = 2 * i + c;
+    blo[i] = c ? b0 : a0;
+    bhi[i] = c ? b1 : a1;
+  }
+}
+
+__global__ __launch_bounds__(256) void pick_small_kernel(const float* __restrict__ cnt,
+                                                         const int32_t* __restrict__ lo_next,
+                                                         const int32_t* __restrict__ hi_next, int L,
+                                                         int32_t* __restrict__ build_child, int32_t* __restrict__ blo,
+                                                         int32_t* __restrict__ bhi) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  const int c = 2 * i + (cnt[2 * i] <= cnt[2 * i + 1] ? 0 : 1);
+  build_child[i] = c;
+  blo[i] = lo_next[c];
+  bhi[i] = hi_next[c];
+}
+
+// hist_next[build_child[i]] = built[i]; hist_next[sibling] = parent[i] - built[i]
+// (zero below a non-split parent).  float4 per thread over [L][F*B*2].
+__global__ __launch_bounds__(256) void subtract_kernel(const float4* __restrict__ parent,
+                                                       const float4* __restrict__ built,
+                                                       const int32_t* __restrict__ split,
+                                                       const int32_t* __restrict__ build_child, int L, int per_node4,
+                                                       float4* __restrict__ next) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= static_cast<int64_t>(L) * per_node4) return;
+  const int i = static_cast<int>(e / per_node4);
+  const int64_t k = e - static_cast<int64_t>(i) * per_node4;
+  const int c = build_child[i];
+  const float4 b = built[e];
+  float4 sib = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (split[i]) {
+    const float4 pa = parent[e];
+    sib = make_float4(pa.x - b.x, pa.y - b.y, pa.z - b.z, pa.w - b.w);
+  }
+  next[static_cast<int64_t>(c) * per_node4 + k] = b;
+  next[static_cast<int64_t>(c ^ 1) * per_node4 + k] = sib;
+}
+
+__global__ __launch_bounds__(256) void quantise_kernel(const float* __restrict__ X, const float* __restrict__ cuts,
+                                                       int64_t n, int F, int ncut, int max_code,
+                                                       uint8_t* __restrict__ out) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= n * F) return;
+  const int f = static_cast<int>(e % F);
+  const float x = X[e];
+  const float* c = cuts + static_cast<int64_t>(f) * ncut;
+  int a = 0, z = ncut;  // first index with c[idx] >= x
+  while (a < z) {
+    const int m = (a + z) >> 1;
+    if (c[m] < x) a = m + 1; else z = m;
+  }
+  out[e] = static_cast<uint8_t>(a < max_code ? a : max_code);
+}
+
 }  // namespace
 
 hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
@@ -207,10 +478,106 @@ hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* 
 
 hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float lambda,
                            float min_child_weight, float* best_gain, int32_t* best_bin, float* best_gl,
-                           float* best_hl, hipStream_t s) {
+                           float* best_hl, float* node_tot, hipStream_t s) {
   if (num_nodes <= 0 || F <= 0) return hipSuccess;
   hipLaunchKernelGGL(split_find_kernel, dim3(F, num_nodes), dim3(256), 0, s, hist, F, B, lambda,
-                     min_child_weight, best_gain, best_bin, best_gl, best_hl);
+                     min_child_weight, best_gain, best_bin, best_gl, best_hl, node_tot);
+  return hipGetLastError();
+}
+
+static int hist_fp(int F) {
+  int fp = 1;
+  while (fp < F && fp < kFTile) fp <<= 1;
+  return fp;
+}
+
+static hipError_t hist_lds_attr() {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const int bytes = static_cast<int>(kFTile * 256 * 2 * sizeof(float));
+    KDL_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<4>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    attr_set = true;
+  }
+  return hipSuccess;
+}
+
+hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
+                        const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
+                        int max_chunks, int rpb, int F, int B, float* hist, hipStream_t s) {
+  if (nb <= 0 || F <= 0 || max_chunks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hist_plan_kernel, dim3(1), dim3(64), 0, s, blo, bhi, nb, rpb, chunk_off);
+  const int fp = hist_fp(F);
+  KDL_CHECK_HIP(hist_lds_attr());
+  dim3 grid(max_chunks, (F + fp - 1) / fp);
+  const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(float);
+  hipLaunchKernelGGL((hist_build_wq_kernel<4>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows,
+                     blo, bhi, chunk_off, nb, F, B, rpb, fp, hist);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot, const float* cuts,
+                       const int32_t* exists, int L, int F, int ncut, int h0, int can_split, float lambda,
+                       float gamma, float lr, int32_t* t_feat, int32_t* t_bin, float* t_thr, float* t_val,
+                       int32_t* split, int32_t* exists_next, hipStream_t s) {
+  if (L <= 0) return hipSuccess;
+  hipLaunchKernelGGL(decide_kernel, dim3((L + 255) / 256), dim3(256), 0, s, gain, sbin, tot, cuts, exists, L, F,
+                     ncut, h0, can_split, lambda, gamma, lr, t_feat, t_bin, t_thr, t_val, split, exists_next);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_of_row,
+                            const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
+                            int L, int32_t* flag, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(route_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bins, rows, node_of_row, split,
+                     t_feat, t_bin, F, n, h0, L, flag);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_partition(const int32_t* rows, int32_t* node_of_row, const int32_t* split, const int32_t* lo,
+                          const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
+                          int32_t* rows_next, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(partition_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, node_of_row, split, lo, hi,
+                     flag, sc, n, h0, L, rows_next);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_children(const int32_t* split, const int32_t* lo, const int32_t* hi, const int32_t* sc, int L,
+                         int32_t* lo_next, int32_t* hi_next, float* cnt, int pick, int32_t* build_child,
+                         int32_t* blo, int32_t* bhi, hipStream_t s) {
+  if (L <= 0) return hipSuccess;
+  hipLaunchKernelGGL(children_kernel, dim3((L + 255) / 256), dim3(256), 0, s, split, lo, hi, sc, L, lo_next,
+                     hi_next, cnt, pick, build_child, blo, bhi);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_pick_small(const float* cnt, const int32_t* lo_next, const int32_t* hi_next, int L,
+                           int32_t* build_child, int32_t* blo, int32_t* bhi, hipStream_t s) {
+  if (L <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pick_small_kernel, dim3((L + 255) / 256), dim3(256), 0, s, cnt, lo_next, hi_next, L,
+                     build_child, blo, bhi);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_subtract(const float* parent, const float* built, const int32_t* split, const int32_t* build_child,
+                         int L, int per_node, float* next, hipStream_t s) {
+  if (L <= 0) return hipSuccess;
+  const int per4 = per_node / 4;
+  const int64_t n = static_cast<int64_t>(L) * per4;
+  hipLaunchKernelGGL(subtract_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(parent), reinterpret_cast<const float4*>(built), split,
+                     build_child, L, per4, reinterpret_cast<float4*>(next));
+  return hipGetLastError();
+}
+
+hipError_t gbdt_quantise(const float* X, const float* cuts, int64_t n, int F, int ncut, int max_code, uint8_t* out,
+                         hipStream_t s) {
+  if (n <= 0 || F <= 0) return hipSuccess;
+  const int64_t tot = n * F;
+  hipLaunchKernelGGL(quantise_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, s, X, cuts, n,
+                     F, ncut, max_code, out);
   return hipGetLastError();
 }
 

@@ -1,0 +1,246 @@
+// Native driver of the device-resident GBDT level pipeline (csrc/gbdt.hip).
+//
+// ``GbdtGrower`` owns every per-tree workspace of one training job (row order,
+// per-row heap node, per-level segments, histograms, the tree's heap arrays)
+// and enqueues the fixed kernel sequence of each level on the current HIP
+// stream.  Nothing in a tree reads device memory from the host: split
+// decisions, child segments and the smaller-child choice stay on the GPU, so a
+// whole tree is a stream of ~10 launches per level.
+//
+// Single rank: ``grow_local`` runs the whole tree in C++.  Several ranks: the
+// Python caller interleaves the two collectives of each level (child counts,
+// built histograms) between ``level_a`` / ``level_b`` / ``level_c``, which is
+// exactly where the reference's rabit all-reduce sits in XGBoost's hist
+// updater.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kdl_api.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void ck(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "kubedl_amd: ", what, " failed: ", hipGetErrorString(e));
+}
+
+int32_t* ip(const at::Tensor& t) { return t.data_ptr<int32_t>(); }
+float* fp(const at::Tensor& t) { return t.data_ptr<float>(); }
+
+class GbdtGrower {
+ public:
+  GbdtGrower(const at::Tensor& bins, const at::Tensor& cuts, int64_t num_bins, int64_t max_depth, double lambda,
+             double gamma, double lr, double min_child_weight)
+      : bins_(bins), cuts_(cuts.to(at::kFloat).contiguous()) {
+    TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.dim() == 2 && bins.is_contiguous(),
+                "GbdtGrower: bins must be a contiguous uint8 [N, F] GPU tensor");
+    TORCH_CHECK(num_bins >= 2 && num_bins <= 256, "GbdtGrower: 2 <= num_bins <= 256");
+    TORCH_CHECK(max_depth >= 0 && max_depth <= 10, "GbdtGrower: max_depth <= 10");
+    N_ = static_cast<int>(bins.size(0));
+    F_ = static_cast<int>(bins.size(1));
+    B_ = static_cast<int>(num_bins);
+    D_ = static_cast<int>(max_depth);
+    TORCH_CHECK(cuts_.dim() == 2 && cuts_.size(0) == F_ && cuts_.device() == bins.device(),
+                "GbdtGrower: cuts [F, ncut] on the bins' device");
+    TORCH_CHECK((static_cast<int64_t>(F_) * B_) % 2 == 0, "GbdtGrower: F * num_bins must be even (float4 hist)");
+    TORCH_CHECK(static_cast<int64_t>(N_) * F_ < (1LL << 31), "GbdtGrower: N * F must fit in int32");
+    ncut_ = static_cast<int>(cuts_.size(1));
+    lam_ = static_cast<float>(lambda);
+    gamma_ = static_cast<float>(gamma);
+    lr_ = static_cast<float>(lr);
+    mcw_ = static_cast<float>(min_child_weight);
+    // rows per histogram chunk: ~1000 chunks over the root level, 256..2048
+    rpb_ = 256;
+    while (rpb_ < 2048 && static_cast<int64_t>(rpb_) * 2 * 1024 <= N_) rpb_ *= 2;
+
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
+    auto io = bins.options().dtype(at::kInt);
+    auto fo = bins.options().dtype(at::kFloat);
+    const int64_t maxL = 1LL << D_, heap = (1LL << (D_ + 1)) - 1;
+    iota_ = at::arange(N_, io);
+    rows_ = at::empty({N_}, io);
+    rows_next_ = at::empty({N_}, io);
+    node_of_row_ = at::empty({N_}, io);
+    flag_ = at::empty({N_}, io);
+    sc_ = at::empty({N_}, io);
+    for (int d = 0; d <= D_; ++d) {
+      lo_.push_back(at::zeros({1LL << d}, io));
+      hi_.push_back(at::zeros({1LL << d}, io));
+      exists_.push_back(at::zeros({1LL << d}, io));
+    }
+    split_ = at::zeros({maxL}, io);
+    gain_ = at::empty({maxL, F_}, fo);
+    sbin_ = at::empty({maxL, F_}, io);
+    gl_ = at::empty({maxL, F_}, fo);
+    hl_ = at::empty({maxL, F_}, fo);
+    tot_ = at::empty({maxL, 2}, fo);
+    feat_ = at::empty({heap}, io);
+    tbin_ = at::empty({heap}, io);
+    thr_ = at::empty({heap}, fo);
+    val_ = at::empty({heap}, fo);
+    per_node_ = static_cast<int64_t>(F_) * B_ * 2;
+    hist_cur_ = at::empty({maxL, F_, B_, 2}, fo);
+    hist_next_ = at::empty({maxL, F_, B_, 2}, fo);
+    built_ = at::empty({std::max<int64_t>(maxL / 2, 1), F_, B_, 2}, fo);
+    cnt_ = at::zeros({maxL}, fo);
+    build_child_ = at::zeros({std::max<int64_t>(maxL / 2, 1)}, io);
+    blo_ = at::zeros({std::max<int64_t>(maxL / 2, 1)}, io);
+    bhi_ = at::zeros({std::max<int64_t>(maxL / 2, 1)}, io);
+    chunk_off_ = at::zeros({std::max<int64_t>(maxL / 2, 1) + 1}, io);
+    root_lo_hi_ = at::tensor({0, N_}, io.device(at::kCPU)).to(bins.device());
+  }
+
+  // Reset the per-tree state and build the root histogram (returned: the
+  // caller all-reduces it in place when there are several ranks).
+  at::Tensor begin_tree(const at::Tensor& grad, const at::Tensor& hess) {
+    TORCH_CHECK(grad.is_cuda() && grad.scalar_type() == at::kFloat && grad.is_contiguous() && grad.numel() == N_,
+                "GbdtGrower: grad must be contiguous fp32 [N]");
+    TORCH_CHECK(hess.is_cuda() && hess.scalar_type() == at::kFloat && hess.is_contiguous() && hess.numel() == N_,
+                "GbdtGrower: hess must be contiguous fp32 [N]");
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
+    grad_ = grad;
+    hess_ = hess;
+    rows_.copy_(iota_);
+    node_of_row_.zero_();
+    feat_.fill_(-1);
+    tbin_.fill_(-1);
+    thr_.zero_();
+    val_.zero_();
+    exists_[0].fill_(1);
+    lo_[0].zero_();
+    hi_[0].fill_(N_);
+    auto root = hist_cur_.narrow(0, 0, 1);
+    root.zero_();
+    const int max_chunks = (N_ + rpb_ - 1) / rpb_ + 1;
+    ck(kdl::gbdt_hist_wq(bins_.data_ptr<uint8_t>(), fp(grad_), fp(hess_), 1, ip(rows_), ip(root_lo_hi_),
+                         ip(root_lo_hi_) + 1, ip(chunk_off_), 1, max_chunks, rpb_, F_, B_, fp(root), stream()),
+       "gbdt_hist_wq(root)");
+    builds_ += 1;
+    return root;
+  }
+
+  // Level d: split search + decisions; below max depth also route, partition
+  // and child segments.  Returns the child row counts [2L] (all-reduce them
+  // and call ``level_b(d, true)`` when ranks > 1), or an empty tensor at the
+  // last level.
+  at::Tensor level_a(int64_t d, bool pick) {
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
+    const int L = 1 << d, h0 = L - 1;
+    const bool last = d >= D_;
+    ck(kdl::gbdt_split_find(fp(hist_cur_), L, F_, B_, lam_, mcw_, fp(gain_), ip(sbin_), fp(gl_), fp(hl_), fp(tot_),
+                            stream()),
+       "gbdt_split_find");
+    ck(kdl::gbdt_decide(fp(gain_), ip(sbin_), fp(tot_), fp(cuts_), ip(exists_[d]), L, F_, ncut_, h0, last ? 0 : 1,
+                        lam_, gamma_, lr_, ip(feat_), ip(tbin_), fp(thr_), fp(val_), ip(split_),
+                        last ? nullptr : ip(exists_[d + 1]), stream()),
+       "gbdt_decide");
+    if (last) return at::Tensor();
+    ck(kdl::gbdt_route_flags(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_of_row_), ip(split_), ip(feat_),
+                             ip(tbin_), F_, N_, h0, L, ip(flag_), stream()),
+       "gbdt_route_flags");
+    at::cumsum_out(sc_, flag_, 0, at::kInt);
+    ck(kdl::gbdt_partition(ip(rows_), ip(node_of_row_), ip(split_), ip(lo_[d]), ip(hi_[d]), ip(flag_), ip(sc_), N_,
+                           h0, L, ip(rows_next_), stream()),
+       "gbdt_partition");
+    std::swap(rows_, rows_next_);
+    ck(kdl::gbdt_children(ip(split_), ip(lo_[d]), ip(hi_[d]), ip(sc_), L, ip(lo_[d + 1]), ip(hi_[d + 1]), fp(cnt_),
+                          pick ? 1 : 0, ip(build_child_), ip(blo_), ip(bhi_), stream()),
+       "gbdt_children");
+    return cnt_.narrow(0, 0, 2 * L);
+  }
+
+  // Build the histogram of each split node's smaller child (returned [L, F,
+  // B, 2]: all-reduce it when ranks > 1).  ``pick``: choose the smaller child
+  // from the (all-reduced) counts now.
+  at::Tensor level_b(int64_t d, bool pick) {
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
+    const int L = 1 << d;
+    if (pick)
+      ck(kdl::gbdt_pick_small(fp(cnt_), ip(lo_[d + 1]), ip(hi_[d + 1]), L, ip(build_child_), ip(blo_), ip(bhi_),
+                              stream()),
+         "gbdt_pick_small");
+    auto built = built_.narrow(0, 0, L);
+    built.zero_();
+    const int max_chunks = (N_ + rpb_ - 1) / rpb_ + L;
+    ck(kdl::gbdt_hist_wq(bins_.data_ptr<uint8_t>(), fp(grad_), fp(hess_), 1, ip(rows_), ip(blo_), ip(bhi_),
+                         ip(chunk_off_), L, max_chunks, rpb_, F_, B_, fp(built), stream()),
+       "gbdt_hist_wq");
+    builds_ += L;
+    return built;
+  }
+
+  // Children's histograms: built one copied, sibling = parent - built.
+  void level_c(int64_t d) {
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
+    const int L = 1 << d;
+    ck(kdl::gbdt_subtract(fp(hist_cur_), fp(built_), ip(split_), ip(build_child_), L, static_cast<int>(per_node_),
+                          fp(hist_next_), stream()),
+       "gbdt_subtract");
+    std::swap(hist_cur_, hist_next_);
+    subtracted_ += L;
+  }
+
+  // Whole tree on one rank.
+  void grow_local(const at::Tensor& grad, const at::Tensor& hess) {
+    begin_tree(grad, hess);
+    for (int d = 0; d <= D_; ++d) {
+      level_a(d, true);
+      if (d < D_) {
+        level_b(d, false);
+        level_c(d);
+      }
+    }
+  }
+
+  at::Tensor node_of_row() const { return node_of_row_; }
+  // (feature, split_bin, threshold, value) heap arrays of the current tree
+  std::vector<at::Tensor> tree() const { return {feat_, tbin_, thr_, val_}; }
+  std::vector<int64_t> stats() const { return {builds_, subtracted_}; }
+  int64_t rows_per_chunk() const { return rpb_; }
+
+ private:
+  at::Tensor bins_, cuts_, grad_, hess_;
+  int N_ = 0, F_ = 0, B_ = 0, D_ = 0, ncut_ = 0, rpb_ = 256;
+  float lam_ = 1.f, gamma_ = 0.f, lr_ = 0.3f, mcw_ = 1.f;
+  int64_t per_node_ = 0, builds_ = 0, subtracted_ = 0;
+  at::Tensor iota_, rows_, rows_next_, node_of_row_, flag_, sc_, root_lo_hi_;
+  std::vector<at::Tensor> lo_, hi_, exists_;
+  at::Tensor split_, gain_, sbin_, gl_, hl_, tot_, feat_, tbin_, thr_, val_;
+  at::Tensor hist_cur_, hist_next_, built_, cnt_, build_child_, blo_, bhi_, chunk_off_;
+};
+
+at::Tensor gbdt_quantise(const at::Tensor& X, const at::Tensor& cuts, int64_t num_bins) {
+  TORCH_CHECK(X.is_cuda() && X.dim() == 2, "gbdt_quantise: X [N, F] on the GPU");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  auto x = X.to(at::kFloat).contiguous();
+  auto c = cuts.to(at::kFloat).contiguous();
+  TORCH_CHECK(c.dim() == 2 && c.size(0) == x.size(1), "gbdt_quantise: cuts [F, ncut]");
+  TORCH_CHECK(num_bins >= 2 && num_bins <= 256, "gbdt_quantise: 2 <= num_bins <= 256");
+  auto out = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  ck(kdl::gbdt_quantise(fp(x), fp(c), x.size(0), static_cast<int>(x.size(1)), static_cast<int>(c.size(1)),
+                        static_cast<int>(num_bins - 1), out.data_ptr<uint8_t>(), stream()),
+     "gbdt_quantise");
+  return out;
+}
+
+}  // namespace
+
+void register_gbdt(pybind11::module& m) {
+  namespace py = pybind11;
+  py::class_<GbdtGrower>(m, "GbdtGrower")
+      .def(py::init<const at::Tensor&, const at::Tensor&, int64_t, int64_t, double, double, double, double>(),
+           py::arg("bins"), py::arg("cuts"), py::arg("num_bins"), py::arg("max_depth"), py::arg("reg_lambda"),
+           py::arg("gamma"), py::arg("learning_rate"), py::arg("min_child_weight"))
+      .def("begin_tree", &GbdtGrower::begin_tree)
+      .def("level_a", &GbdtGrower::level_a)
+      .def("level_b", &GbdtGrower::level_b)
+      .def("level_c", &GbdtGrower::level_c)
+      .def("grow_local", &GbdtGrower::grow_local)
+      .def("node_of_row", &GbdtGrower::node_of_row)
+      .def("tree", &GbdtGrower::tree)
+      .def("stats", &GbdtGrower::stats)
+      .def("rows_per_chunk", &GbdtGrower::rows_per_chunk);
+  m.def("gbdt_quantise", &gbdt_quantise, "GBDT feature quantisation (bins = #cuts < x, clamped)");
+}

@@ -140,7 +140,30 @@ hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* 
                            int F, int B, float* hist, hipStream_t s);
 hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float lambda,
                            float min_child_weight, float* best_gain, int32_t* best_bin, float* best_gl,
-                           float* best_hl, hipStream_t s);
+                           float* best_hl, float* node_tot, hipStream_t s);
+// device-resident growth (see gbdt.hip header)
+hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
+                        const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
+                        int max_chunks, int rpb, int F, int B, float* hist, hipStream_t s);
+hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot, const float* cuts,
+                       const int32_t* exists, int L, int F, int ncut, int h0, int can_split, float lambda,
+                       float gamma, float lr, int32_t* t_feat, int32_t* t_bin, float* t_thr, float* t_val,
+                       int32_t* split, int32_t* exists_next, hipStream_t s);
+hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_of_row,
+                            const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
+                            int L, int32_t* flag, hipStream_t s);
+hipError_t gbdt_partition(const int32_t* rows, int32_t* node_of_row, const int32_t* split, const int32_t* lo,
+                          const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
+                          int32_t* rows_next, hipStream_t s);
+hipError_t gbdt_children(const int32_t* split, const int32_t* lo, const int32_t* hi, const int32_t* sc, int L,
+                         int32_t* lo_next, int32_t* hi_next, float* cnt, int pick, int32_t* build_child,
+                         int32_t* blo, int32_t* bhi, hipStream_t s);
+hipError_t gbdt_pick_small(const float* cnt, const int32_t* lo_next, const int32_t* hi_next, int L,
+                           int32_t* build_child, int32_t* blo, int32_t* bhi, hipStream_t s);
+hipError_t gbdt_subtract(const float* parent, const float* built, const int32_t* split, const int32_t* build_child,
+                         int L, int per_node, float* next, hipStream_t s);
+hipError_t gbdt_quantise(const float* X, const float* cuts, int64_t n, int F, int ncut, int max_code, uint8_t* out,
+                         hipStream_t s);
 hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32_t* row_node,
                            const int32_t* split_feat, const int32_t* split_bin, int F, int n,
                            int32_t* go_right, hipStream_t s);

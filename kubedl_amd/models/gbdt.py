@@ -16,6 +16,14 @@ XGBoost's ``hist`` algorithm, depth-wise, re-designed for one GPU per rank:
 * objectives ``reg:squarederror``, ``binary:logistic``, ``multi:softprob``
   (one tree per class per round, as XGBoost).
 
+On the GPU a tree never leaves the device while it grows: the native
+``GbdtGrower`` (csrc/gbdt_grower.cpp over csrc/gbdt.hip) keeps nodes in heap
+order, rows grouped per node by a stable in-segment partition, and the split
+decisions, child segments and smaller-child choice in device arrays; the host
+only enqueues a fixed kernel sequence per level (plus the two all-reduces per
+level with several ranks).  The trees' heap arrays are copied to the host once,
+at the end of ``fit``.  Quantisation is one kernel (``gbdt_quantise``).
+
 Every rank holds a row shard; all ranks grow identical trees because they
 see identical all-reduced histograms.  On CPU (or without the extension)
 the same algorithm runs on torch ops -- that path is the numerics reference
@@ -127,6 +135,8 @@ class HistGBDT:
         self.cuts = cuts.float().contiguous()
 
     def quantise(self, X: torch.Tensor) -> torch.Tensor:
+        if self.use_hip and X.is_cuda:
+            return _ext.load().gbdt_quantise(X, self.cuts, self.p.max_bin)
         F = X.shape[1]
         out = torch.empty(X.shape, dtype=torch.uint8, device=X.device)
         for f in range(F):
@@ -298,6 +308,42 @@ class HistGBDT:
             level_nodes = next_nodes
         return tree, leaf_of_row
 
+    # ------------------------------------------------------------ device-resident tree
+    def _device_grower(self, bins):
+        p = self.p
+        if not self.use_hip or p.max_depth > 10 or (bins.shape[1] * p.max_bin) % 2:
+            return None
+        return _ext.load().GbdtGrower(bins, self.cuts, p.max_bin, p.max_depth, p.reg_lambda, p.gamma,
+                                      p.learning_rate, p.min_child_weight)
+
+    def _grow_device(self, gr, g, h):
+        """One tree on the GPU; returns (heap arrays, per-row leaf value)."""
+        D = self.p.max_depth
+        if _world() == 1:
+            gr.grow_local(g, h)
+        else:
+            _allreduce_(gr.begin_tree(g, h))
+            for d in range(D + 1):
+                cnt = gr.level_a(d, False)
+                if d < D:
+                    _allreduce_(cnt)                    # global child counts -> same smaller child on all ranks
+                    _allreduce_(gr.level_b(d, True))    # the built children's histograms
+                    gr.level_c(d)
+        feat, tbin, thr, val = gr.tree()
+        return torch.stack([feat.float(), tbin.float(), thr, val]), val[gr.node_of_row().long()]
+
+    @staticmethod
+    def _heap_tree(arr) -> Tree:
+        feat, tbin, thr, val = arr
+        t = Tree()
+        t.feature = [int(v) for v in feat]
+        t.split_bin = [int(v) for v in tbin]
+        t.threshold = [float(v) for v in thr]
+        t.value = [float(v) for v in val]
+        t.left = [2 * i + 1 if f >= 0 else -1 for i, f in enumerate(t.feature)]
+        t.right = [2 * i + 2 if f >= 0 else -1 for i, f in enumerate(t.feature)]
+        return t
+
     # ------------------------------------------------------------ training
     def fit(self, X: torch.Tensor, y: torch.Tensor, log_every: int = 0, callback=None):
         X = X.to(self.device)
@@ -308,19 +354,37 @@ class HistGBDT:
         n = X.shape[0]
         pred = self._base(n)
         K = pred.shape[1]
+        grower = self._device_grower(bins)
+        dev_trees = []
         for it in range(self.p.n_estimators):
             g_all, h_all = self._grad_hess(pred, y)
             round_trees = []
             for k in range(K):
                 g = g_all[:, k].contiguous()
                 h = h_all[:, k].contiguous()
+                if grower is not None:
+                    arr, leaf_val = self._grow_device(grower, g, h)
+                    pred[:, k] += leaf_val
+                    round_trees.append(arr)
+                    continue
                 tree, leaf = self._grow(bins, g, h, n)
                 vals = torch.tensor(tree.value, dtype=torch.float32, device=self.device)
                 pred[:, k] += vals[leaf.long()]
                 round_trees.append(tree)
-            self.trees.append(round_trees)
+            if grower is not None:
+                dev_trees.append(round_trees)
+            else:
+                self.trees.append(round_trees)
             if callback is not None:
                 callback(it, pred)
+        if grower is not None:
+            # the only device->host copy of training: every tree's heap arrays at once
+            if dev_trees:
+                host = torch.stack([torch.stack(r) for r in dev_trees]).cpu()
+                self.trees += [[self._heap_tree(host[i, k]) for k in range(K)] for i in range(len(dev_trees))]
+            b, s = grower.stats()
+            self.stats["hist_builds"] += b
+            self.stats["hist_subtracted"] += s
         return pred
 
     def predict_margin(self, X: torch.Tensor) -> torch.Tensor:

@@ -34,6 +34,7 @@ python -c "import kubedl_amd._C" 2>/dev/null || python -m kubedl_amd.ops.build >
 
 want smoke  && run_step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want pytest && run_step pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+want pytestsub && run_step pytest_sub 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread
 want bench  && run_step bench_job 600 python bench.py --gpus 1 --steps 20 --warmup 5
 want benchdirect && run_step bench_direct 600 python bench.py --direct --gpus 1 --steps 20 --warmup 5
 want bench2 && run_step bench_job2 600 python bench.py --gpus 1 --steps 20 --warmup 5
@@ -50,6 +51,7 @@ want convgemm && run_step conv_vs_gemm 600 python scripts/conv_vs_gemm.py
 want ctr && run_step ctr 300 python -u -m kubedl_amd.workers.xdl_ctr
 want ctrprof && run_step ctr_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ctr_prof -o run -- python -u -m kubedl_amd.workers.xdl_ctr --steps 10 --warmup 3
 want gbdt && run_step gbdt 300 python -u -m kubedl_amd.workers.xgboost_dist
+want gbdt2m && run_step gbdt_2m 300 python -u -m kubedl_amd.workers.xgboost_dist --rows 2000000 --n_estimators 100
 want gbdtprof && run_step gbdt_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gbdt_prof -o run -- python -u -m kubedl_amd.workers.xgboost_dist
 want benchimm && run_step bench_immediate 600 python bench.py --steps 20 --warmup 8 --conv-benchmark 0
 # ship the MIOpen find-db / kernel cache back (merged into gpurun_out/)
