@@ -460,19 +460,28 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
       }
 }
 
-// out = scale * sum_s dw32[s] (fixed order), bf16 into dW or fp32 into slab 0.
-// Block = 16 float4 columns x 16 split groups; the groups are folded in LDS.
+// Block (x, y) sums the slabs (y * chunk + j) * stride, j < min(chunk, count -
+// y * chunk), over 64 columns, in a fixed order: into bf16 dW (scaled) when
+// ``out`` is given, else as fp32 into the block's first slab (an in-place
+// partial: only this block touches those columns of that slab).  Block = 16
+// float4 columns x 16 split groups folded in LDS.  Many splits over few
+// columns (early layers: 256 slabs of a 64x256 weight) go through two passes:
+// partial sums over y-chunks of splits, then the chunk partials.
 constexpr int kRedCols = 16, kRedGroups = kThreads / kRedCols;
-__global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restrict__ dw32, int64_t nk, int splits,
-                                                                float scale, bf16_t* __restrict__ out) {
+__global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restrict__ dw32, int64_t nk, int count,
+                                                                int chunk, int stride, float scale,
+                                                                bf16_t* __restrict__ out) {
   __shared__ float4 part[kRedGroups][kRedCols];
   const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
   const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kRedCols + col) * 4;
+  const int base = blockIdx.y * chunk;
+  const int cnt = (count - base) < chunk ? (count - base) : chunk;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i4 < nk) {
 #pragma unroll 4
-    for (int sp = grp; sp < splits; sp += kRedGroups) {
-      const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(dw32 + sp * nk + i4));
+    for (int sp = grp; sp < cnt; sp += kRedGroups) {
+      const f32x4_t v = __builtin_nontemporal_load(
+          reinterpret_cast<const f32x4_t*>(dw32 + static_cast<int64_t>(base + sp) * stride * nk + i4));
       a.x += v[0]; a.y += v[1]; a.z += v[2]; a.w += v[3];
     }
   }
@@ -489,7 +498,8 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restric
       const uint32_t hi = pack_bf16x2(a.z * scale, a.w * scale);
       *reinterpret_cast<uint2*>(out + i4) = make_uint2(lo, hi);
     } else {
-      *reinterpret_cast<float4*>(dw32 + i4) = make_float4(a.x * scale, a.y * scale, a.z * scale, a.w * scale);
+      *reinterpret_cast<float4*>(dw32 + static_cast<int64_t>(base) * stride * nk + i4) =
+          make_float4(a.x * scale, a.y * scale, a.z * scale, a.w * scale);
     }
   }
 }
@@ -658,6 +668,27 @@ void launch_wgrad(dim3 grid, hipStream_t s, const bf16_t* g, const bf16_t* x, co
 }  // namespace
 
 namespace {
+// Fixed-order sum of ``nsplit`` fp32 slabs into bf16 dW: one pass, or two when
+// the columns alone would leave the chip idle (chunk partials first).
+hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t* dW, hipStream_t s) {
+  const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
+  int groups = (2048 + rgrid - 1) / rgrid;            // y-blocks to reach ~2048 blocks
+  const int by_work = (nsplit + 31) / 32;             // >= 2 slabs per thread in pass 1
+  if (groups > by_work) groups = by_work;
+  if (groups <= 1) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, nsplit, nsplit, 1, scale,
+                       dW);
+    return hipGetLastError();
+  }
+  const int chunk = (nsplit + groups - 1) / groups;
+  groups = (nsplit + chunk - 1) / chunk;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid, groups), dim3(kThreads), 0, s, dw32, nk, nsplit, chunk, 1,
+                     1.0f, static_cast<bf16_t*>(nullptr));
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, groups, groups, chunk, scale,
+                     dW);
+  return hipGetLastError();
+}
+
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
                       hipStream_t s) {
@@ -693,11 +724,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
     KDL_CHECK_HIP(hipGetLastError());
   }
-  const int64_t nk = static_cast<int64_t>(N) * K;
-  const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, nsplit, scale,
-                     static_cast<bf16_t*>(dW));
-  return hipGetLastError();
+  return wgrad_reduce(dw32, static_cast<int64_t>(N) * K, nsplit, scale, static_cast<bf16_t*>(dW), s);
 }
 }  // namespace
 

@@ -46,6 +46,36 @@ constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load r
 
 template <int A, int B> struct cmax { static constexpr int v = A > B ? A : B; };
 
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+// Raw buffer resource words (what __builtin_amdgcn_make_buffer_rsrc builds):
+// 48-bit base, stride 0, num_records bytes, raw-buffer flags.
+__device__ __forceinline__ i32x4_t rsrc_words(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane(static_cast<int>(a & 0xffffffffu));
+  r.y = __builtin_amdgcn_readfirstlane(static_cast<int>((a >> 32) & 0xffffu));
+  r.z = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+  r.w = 0x00020000;
+  return r;
+}
+
+// The same 16-B-per-lane LDS-DMA as dma16, issued from inline asm so the
+// compiler does not see an LDS write: hipcc otherwise inserts its own
+// vmcnt wait before the first ds_read of a step, retiring the NEWER stage a
+// step early (guide: "three .s-level traps", item b).  The caller's counted
+// s_waitcnt vmcnt + barrier is then the only ordering, by construction.
+__device__ __forceinline__ void dma16_asm(i32x4_t r, lds_void_t* dst, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst)));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(r), "s"(soff)
+               : "memory", "m0");
+#endif
+}
+
 // One 16-byte-per-lane LDS-DMA load (1 KiB per wave at dst + 16 * lane).  The
 // builtin exists only for the device pass; referenced in the host pass it
 // makes clang drop the kernel's host stub, hence the pass guard.
@@ -55,8 +85,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst,
 #endif
 }
 
-template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB>
+template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
+  static_assert(STAGES == 2 || STAGES == 3, "2 or 3 LDS stages");
   constexpr int NT = 64 * WM * WN;
   constexpr int NW = WM * WN;
   constexpr int SA = BM * 128, SB = BN * 128, STAGE = SA + SB;  // bytes per stage
@@ -67,7 +98,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   constexpr int TM = WTM / 32, TN = WTN / 32;
   using Epi = Epilogue<BM, BN, NT, EPI>;
   constexpr int LDC = Epi::LDC;
-  constexpr int LDS_BYTES = cmax<cmax<2 * STAGE, BM * LDC * 2>::v, Epi::kScratchBytes>::v;
+  constexpr int LDS_BYTES = cmax<cmax<STAGES * STAGE, BM * LDC * 2>::v, Epi::kScratchBytes>::v;
   // ONE __shared__ object (a second one makes hipcc drain vmcnt before ds_reads)
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
 
@@ -89,6 +120,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
       const_cast<bf16_t*>(p.A), (short)0, static_cast<int>(p.a_rows * lda * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(p.B), (short)0, static_cast<int>(static_cast<int64_t>(p.N) * K * 2), 0x00020000);
+  i32x4_t wA{}, wB{};
+  if constexpr (STAGES == 3) {
+    wA = rsrc_words(p.A, static_cast<uint32_t>(p.a_rows * lda * 2));
+    wB = rsrc_words(p.B, static_cast<uint32_t>(static_cast<int64_t>(p.N) * K * 2));
+  }
+  auto dma = [&](bool is_a, lds_void_t* dst, uint32_t voff, uint32_t soff) {
+    if constexpr (STAGES == 3) dma16_asm(is_a ? wA : wB, dst, voff, soff);
+    else dma16(is_a ? rA : rB, dst, voff, soff);
+  };
 
   // per DMA instruction i of this wave: operand row (within its A or B region)
   // and the logical 16-B chunk this lane fetches (source-side swizzle)
@@ -165,12 +205,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
                           static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win);
           const uint32_t off = ok ? static_cast<uint32_t>(((crow[i] + ih * p.Win + iw) * p.Cin + kc0) * 2) + voff[i]
                                   : kOOB;
-          dma16(rA, dst, off, 0);
+          dma(true, dst, off, 0);
         } else {
-          dma16(rA, dst, voff[i], k0 * 2);
+          dma(true, dst, voff[i], k0 * 2);
         }
       } else {
-        dma16(rB, dst, voff[i], k0 * 2);
+        dma(false, dst, voff[i], k0 * 2);
       }
     }
   };
@@ -191,11 +231,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-    issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      __syncthreads();  // stage kt landed (every wave's vmcnt(0) + barrier); stage kt+1 free
-      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-      const char* As = lds + (kt & 1) * STAGE;
+    auto compute = [&](const char* As) {
       const char* Bs = As + SA;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -212,6 +248,36 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
           for (int j = 0; j < TM; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
       }
+    };
+    if constexpr (STAGES == 2) {
+      issue(0, 0);
+      for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();  // stage kt landed (every wave's vmcnt(0) + barrier); stage kt+1 free
+        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+        compute(lds + (kt & 1) * STAGE);
+      }
+    } else {
+      // three stages, two K-steps of DMA in flight across each barrier: a
+      // counted vmcnt retires stage kt only (the IPW loads of stage kt+1 stay
+      // in flight), a raw s_barrier publishes it (no __syncthreads: its fence
+      // would drain vmcnt to 0), then stage kt+2 is issued into the buffer
+      // every wave finished reading in step kt-1 (its ds_reads retired by the
+      // lgkmcnt(0) before this barrier).
+      issue(0, 0);
+      if (nk > 1) issue(1, 1);
+      int cur = 0;
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 2 < nk) issue(kt + 2, cur == 0 ? 2 : cur - 1);
+        compute(lds + cur * STAGE);
+        cur = cur == 2 ? 0 : cur + 1;
+      }
     }
     __syncthreads();  // every wave's last fragment reads are done: the stages become the C tile
     epi.begin(p, tm);
@@ -224,41 +290,43 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
 }
 
-template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB>
+template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES, int BPC>
 hipError_t launch(const GemmParams& p, hipStream_t s) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = p.N / BN;
-  const int target = 256 * MINB;  // one round of resident blocks
+  const int target = 256 * BPC;  // one round of resident blocks
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB>), dim3(GM * tiles_n), dim3(64 * WM * WN), 0, s,
-                     p, GM, tiles_m, tiles_n);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB, STAGES>), dim3(GM * tiles_n), dim3(64 * WM * WN),
+                     0, s, p, GM, tiles_m, tiles_n);
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int GATHER, int MINB>
+// MINB: the launch bound's minimum waves per SIMD (register budget); BPC:
+// resident blocks per CU the persistent grid is sized for.
+template <int BM, int BN, int WM, int WN, int GATHER, int MINB, int STAGES, int BPC>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   switch (epi) {
-    case EPI_PLAIN: return launch<BM, BN, WM, WN, GATHER, EPI_PLAIN, MINB>(p, s);
-    case EPI_STATS: return launch<BM, BN, WM, WN, GATHER, EPI_STATS, MINB>(p, s);
-    case EPI_MASKX: return launch<BM, BN, WM, WN, GATHER, EPI_MASKX, MINB>(p, s);
+    case EPI_PLAIN: return launch<BM, BN, WM, WN, GATHER, EPI_PLAIN, MINB, STAGES, BPC>(p, s);
+    case EPI_STATS: return launch<BM, BN, WM, WN, GATHER, EPI_STATS, MINB, STAGES, BPC>(p, s);
+    case EPI_MASKX: return launch<BM, BN, WM, WN, GATHER, EPI_MASKX, MINB, STAGES, BPC>(p, s);
   }
   if constexpr (GATHER == G_DENSE) {
     switch (epi) {
-      case EPI_RESBITS: return launch<BM, BN, WM, WN, GATHER, EPI_RESBITS, MINB>(p, s);
-      case EPI_RES: return launch<BM, BN, WM, WN, GATHER, EPI_RES, MINB>(p, s);
+      case EPI_RESBITS: return launch<BM, BN, WM, WN, GATHER, EPI_RESBITS, MINB, STAGES, BPC>(p, s);
+      case EPI_RES: return launch<BM, BN, WM, WN, GATHER, EPI_RES, MINB, STAGES, BPC>(p, s);
     }
   }
   return hipErrorInvalidValue;
 }
 
-template <int BM, int BN, int WM, int WN, int MINB>
+template <int BM, int BN, int WM, int WN, int MINB, int STAGES = 2, int BPC = MINB>
 hipError_t dispatch_gather(const GemmParams& p, int epi, int gather, hipStream_t s) {
   switch (gather) {
-    case G_DENSE: return dispatch_epi<BM, BN, WM, WN, G_DENSE, MINB>(p, epi, s);
-    case G_STRIDED: return dispatch_epi<BM, BN, WM, WN, G_STRIDED, MINB>(p, epi, s);
-    case G_CONV3: return dispatch_epi<BM, BN, WM, WN, G_CONV3, MINB>(p, epi, s);
+    case G_DENSE: return dispatch_epi<BM, BN, WM, WN, G_DENSE, MINB, STAGES, BPC>(p, epi, s);
+    case G_STRIDED: return dispatch_epi<BM, BN, WM, WN, G_STRIDED, MINB, STAGES, BPC>(p, epi, s);
+    case G_CONV3: return dispatch_epi<BM, BN, WM, WN, G_CONV3, MINB, STAGES, BPC>(p, epi, s);
   }
   return hipErrorInvalidValue;
 }
@@ -267,7 +335,14 @@ hipError_t dispatch_gather(const GemmParams& p, int epi, int gather, hipStream_t
 
 // Tile configs: 0 = 256x256 (8 waves, 128x64 wave tiles, 1 block/CU);
 // 1 = 256x128 (8 waves, 64x64); 2 = 128x128 (4 waves, 64x64, 2 blocks/CU);
-// 3 = 256x64 (4 waves, 64x64, 2 blocks/CU).
+// 3 = 256x64 (4 waves, 64x64, 2 blocks/CU); 4 = 256x128 with three stages
+// (two K-steps of DMA in flight, counted vmcnt + raw barrier, 144 KiB).
+// Measured on the ResNet-50 shapes (profiles/r02_igemm_small_blocks_ab.jsonl,
+// docs/perf_notes.md): three stages tie two at one block per CU (4 vs 1) and
+// lose badly where they cost the second resident block (128x128 / 256x64 at
+// 96-120 KiB: 1.6-1.7x slower); smaller independent blocks (128x64, 64x64,
+// 64x128 at 3-4 blocks/CU) lose 15-60 %.  Operand delivery into LDS, not
+// latency, bounds these kernels (~7-10 TB/s of L2->LDS traffic chip-wide).
 namespace {
 int g_forced_cfg = [] { const char* e = getenv("KDL_IGEMM_CFG"); return e ? atoi(e) : -1; }();
 }  // namespace
@@ -277,7 +352,7 @@ void set_igemm_cfg(int cfg) { g_forced_cfg = cfg; }
 namespace gemm {
 int igemm_pick(int M, int N, int K) {
   const int forced = g_forced_cfg;
-  if (forced >= 0 && forced <= 3) {
+  if (forced >= 0 && forced <= 4) {
     const int bn = forced == 0 ? 256 : forced == 3 ? 64 : 128;
     if (N % bn == 0) return forced;
   }
@@ -302,6 +377,7 @@ hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t 
     case 1: if (p.N % 128) break; return dispatch_gather<256, 128, 4, 2, 1>(p, epi, gather, s);
     case 2: if (p.N % 128) break; return dispatch_gather<128, 128, 2, 2, 2>(p, epi, gather, s);
     case 3: if (p.N % 64) break; return dispatch_gather<256, 64, 4, 1, 2>(p, epi, gather, s);
+    case 4: if (p.N % 128) break; return dispatch_gather<256, 128, 4, 2, 1, 3>(p, epi, gather, s);
   }
   return hipErrorInvalidValue;
 }

@@ -304,6 +304,23 @@ def pod_template_gpus(template: Dict[str, Any]) -> int:
     return sum(gpus_requested(c) for c in ((template or {}).get("spec") or {}).get("containers") or [])
 
 
+HBM_RESOURCE = "kubedl.io/hbm-gb"
+
+
+def hbm_requested(container: Dict[str, Any]) -> float:
+    """``kubedl.io/hbm-gb`` of a container (limits, else requests), in GB."""
+    res = container.get("resources") or {}
+    for section in ("limits", "requests"):
+        d = res.get(section) or {}
+        if HBM_RESOURCE in d:
+            return float(str(d[HBM_RESOURCE]))
+    return 0.0
+
+
+def pod_template_hbm(template: Dict[str, Any]) -> float:
+    return sum(hbm_requested(c) for c in ((template or {}).get("spec") or {}).get("containers") or [])
+
+
 def gen_general_name(job_name: str, rtype: str, index) -> str:
     """GenGeneralName (util.go:29-32): ``<job>-<rtype>-<index>`` with '/' -> '-'."""
     return f"{job_name}-{rtype}-{index}".replace("/", "-")

@@ -372,8 +372,11 @@ class JobController:
         # for all-pods, as in the reference).
         uid = job["metadata"].get("uid")
         marks = self._launch_marks.setdefault(uid, set())
-        if "first" not in marks and c.is_created(job_status) and c.is_running(job_status):
-            if self.metrics.first_pod_launch_delay(active_pods, job, job_status) is not None:
+        if "first" not in marks and c.is_created(job_status) and (
+                c.is_running(job_status) or c.is_succeeded(job_status)):
+            # every pod of the job, not only active ones: a short rank may already
+            # have finished (its readyTime survives) when the job first reads Running
+            if self.metrics.first_pod_launch_delay(pods, job, job_status) is not None:
                 marks.add("first")
         if "all" not in marks and not c.is_restarting(old_status) and not c.is_restarting(job_status):
             if c.total_active(job_status.get("replicaStatuses")) == total_replicas:

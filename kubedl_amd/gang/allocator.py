@@ -16,9 +16,17 @@ Placement policy (MI355X-first):
   kept there, choosing the half with the FEWEST free GPUs that still fits
   (best fit -> two 4-GPU jobs land on opposite halves, leaving whole halves
   free for later 4-GPU jobs).
-* HBM: each GPU advertises 288 GB; a pod may additionally request
-  ``kubedl.io/hbm-gb`` per GPU, checked against the per-GPU capacity (no
-  over-commit: one pod per GPU).
+* HBM: each GPU advertises 288 GB.  A pod asking for whole GPUs
+  (``amd.com/gpu: N``) owns them; ``kubedl.io/hbm-gb`` on such a pod is its
+  per-process cap and must fit one GPU.  A pod asking for ``kubedl.io/hbm-gb:
+  X`` and NO whole GPU gets an HBM *slice*: it shares a GPU with other slices
+  as long as their sum stays <= 288 GB (best fit: the fullest shared GPU that
+  still has X GB left, a fresh GPU only when none has -- so whole GPUs stay
+  available for exclusive gangs).  Exclusive and shared use never mix on one
+  GPU.  The kubelet exports the slice as ``KDL_HBM_LIMIT_GB`` and the rank
+  caps its caching allocator to it (``parallel.dist.apply_hbm_limit``), which
+  is what makes the accounting real: many small jobs (CTR towers, GBDT, tests)
+  pack onto one 288 GB device instead of idling seven eighths of it.
 
 The inventory is discovered from the KFD topology (no GPU initialisation,
 so the controller never touches the device), or forced with
@@ -78,10 +86,12 @@ def _native():
 class Allocation:
     owner: str
     pods: Dict[str, List[int]]  # pod key -> gpu ids
+    slices: Dict[str, float] = field(default_factory=dict)  # pod key -> HBM GB of a shared-GPU slice
 
     @property
     def gpus(self) -> List[int]:
-        return sorted(g for v in self.pods.values() for g in v)
+        """GPUs owned exclusively."""
+        return sorted(g for k, v in self.pods.items() if k not in self.slices for g in v)
 
 
 class GPUAllocator:
@@ -90,11 +100,27 @@ class GPUAllocator:
         self._lock = threading.Lock()
         self._owner_of: Dict[int, str] = {}
         self._allocs: Dict[str, Allocation] = {}
+        self._shared: Dict[int, Dict[tuple, float]] = {}  # gpu -> {(owner, pod key): GB} of HBM slices
+
+    def _is_free(self, g: int) -> bool:
+        return g not in self._owner_of and not self._shared.get(g)
 
     @property
     def free(self) -> List[int]:
+        """GPUs with neither an owner nor a slice."""
         with self._lock:
-            return [g for g in range(self.inv.count) if g not in self._owner_of]
+            return [g for g in range(self.inv.count) if self._is_free(g)]
+
+    def hbm_free(self) -> Dict[int, float]:
+        """Unreserved HBM GB per GPU (0 on exclusively owned GPUs)."""
+        with self._lock:
+            return {g: (0.0 if g in self._owner_of else self.inv.hbm_gb - sum(self._shared.get(g, {}).values()))
+                    for g in range(self.inv.count)}
+
+    def hbm_used(self) -> float:
+        with self._lock:
+            return (len(self._owner_of) * self.inv.hbm_gb
+                    + sum(v for d in self._shared.values() for v in d.values()))
 
     def allocation(self, owner: str) -> Optional[Allocation]:
         with self._lock:
@@ -107,31 +133,65 @@ class GPUAllocator:
         Idempotent per owner: pods already placed keep their GPUs; only the
         missing ones are placed, still all-or-nothing across the missing set.
         """
+        hbm_gb = hbm_gb or {}
         with self._lock:
             cur = self._allocs.get(owner)
             placed = dict(cur.pods) if cur else {}
+            slices = dict(cur.slices) if cur else {}
             todo = {k: n for k, n in requests.items() if k not in placed}
             for k, n in todo.items():
                 if n < 0:
                     raise ValueError("negative GPU request")
-                need = (hbm_gb or {}).get(k, 0.0)
-                if n > 0 and need > self.inv.hbm_gb:
+                need = float(hbm_gb.get(k, 0.0) or 0.0)
+                if need < 0:
+                    raise ValueError("negative HBM request")
+                if need > self.inv.hbm_gb:
                     return None  # can never fit on this node
-            need_total = sum(todo.values())
-            free = [g for g in range(self.inv.count) if g not in self._owner_of]
+            whole = {k: n for k, n in todo.items() if n > 0}
+            sliced = {k: float(hbm_gb[k]) for k, n in todo.items() if n == 0 and float(hbm_gb.get(k, 0) or 0) > 0}
+            need_total = sum(whole.values())
+            free = [g for g in range(self.inv.count) if self._is_free(g)]
             if need_total > len(free):
                 return None
             chosen = self._choose(free, need_total)
             if chosen is None:
                 return None
+            # slices go on GPUs not taken by this gang's whole-GPU members
+            slice_gpu = self._place_slices(sliced, set(chosen))
+            if slice_gpu is None:
+                return None
             it = iter(chosen)
-            for k, n in sorted(todo.items()):
+            for k, n in sorted(whole.items()):
                 placed[k] = [next(it) for _ in range(n)]
-            alloc = Allocation(owner, placed)
+            for k in todo:
+                if k not in placed:
+                    placed[k] = [slice_gpu[k]] if k in slice_gpu else []
+            for k, g in slice_gpu.items():
+                slices[k] = sliced[k]
+                self._shared.setdefault(g, {})[(owner, k)] = sliced[k]
+            alloc = Allocation(owner, placed, slices)
             self._allocs[owner] = alloc
             for g in alloc.gpus:
                 self._owner_of[g] = owner
             return alloc
+
+    def _place_slices(self, sliced: Dict[str, float], taken: set) -> Optional[Dict[str, int]]:
+        """Best-fit packing of HBM slices (largest first) onto shared or free
+        GPUs; all-or-nothing (nothing is recorded here)."""
+        room = {g: self.inv.hbm_gb - sum(self._shared.get(g, {}).values())
+                for g in range(self.inv.count) if g not in self._owner_of and g not in taken}
+        shared_now = {g for g, d in self._shared.items() if d}
+        out: Dict[str, int] = {}
+        for k, gb in sorted(sliced.items(), key=lambda kv: (-kv[1], kv[0])):
+            cands = [g for g, r in room.items() if r + 1e-9 >= gb]
+            if not cands:
+                return None
+            # a GPU that already carries slices first (the fullest that fits), a fresh one last
+            used = shared_now | set(out.values())
+            g = min(cands, key=lambda g: (g not in used, room[g], g))
+            room[g] -= gb
+            out[k] = g
+        return out
 
     def _choose(self, free: Sequence[int], n: int) -> Optional[List[int]]:
         if n == 0:
@@ -164,7 +224,16 @@ class GPUAllocator:
             keys = [pod_key] if pod_key is not None else list(alloc.pods)
             freed = []
             for k in keys:
-                for g in alloc.pods.pop(k, []):
+                gpus = alloc.pods.pop(k, [])
+                if alloc.slices.pop(k, None) is not None:
+                    for g in gpus:
+                        d = self._shared.get(g, {})
+                        d.pop((owner, k), None)
+                        if not d:
+                            self._shared.pop(g, None)
+                            freed.append(g)
+                    continue
+                for g in gpus:
                     self._owner_of.pop(g, None)
                     freed.append(g)
             if not alloc.pods:
@@ -172,8 +241,9 @@ class GPUAllocator:
             return freed
 
     def used(self) -> int:
+        """GPUs in use (owned, or carrying at least one slice)."""
         with self._lock:
-            return len(self._owner_of)
+            return len(self._owner_of) + sum(1 for g, d in self._shared.items() if d)
 
     def snapshot(self) -> Dict[str, Dict[str, List[int]]]:
         with self._lock:

@@ -129,11 +129,12 @@ class JobMetrics:
         self._restart.inc()
 
     def first_pod_launch_delay(self, active_pods: List[dict], job: dict, status: dict) -> Optional[float]:
-        if not c.is_running(status):
+        # Running, or Succeeded in the same reconcile that first saw a ready rank
+        if not (c.is_running(status) or c.is_succeeded(status)):
             return None
         earliest = None
         for pod in active_pods:
-            if (pod.get("status") or {}).get("phase") != "Running":
+            if (pod.get("status") or {}).get("phase") not in ("Running", "Succeeded"):
                 continue
             t = _ready_time(pod)
             if t is None:
@@ -172,10 +173,15 @@ class JobMetrics:
 
 def _ready_time(pod: dict) -> Optional[float]:
     """lastTransitionTime of a TRUE Ready condition (a False one means the rank
-    has not signalled readiness yet and is not a launch-complete time)."""
-    for cond in (pod.get("status") or {}).get("conditions") or []:
+    has not signalled readiness yet and is not a launch-complete time); for a
+    pod that already ran to completion, the time it first became Ready
+    (``status.readyTime``, kept by the kubelet after Ready turns False)."""
+    st = pod.get("status") or {}
+    for cond in st.get("conditions") or []:
         if cond.get("type") == "Ready" and cond.get("status") == "True":
             return c.to_epoch(cond.get("lastTransitionTime"))
+    if st.get("phase") == "Succeeded" and st.get("readyTime"):
+        return c.to_epoch(st["readyTime"])
     return None
 
 

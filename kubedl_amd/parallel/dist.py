@@ -44,6 +44,23 @@ def _free_port() -> int:
     return port
 
 
+MI355X_HBM_GB = 288.0
+
+
+def apply_hbm_limit(dev: torch.device) -> float | None:
+    """Cap this process's caching allocator to ``KDL_HBM_LIMIT_GB`` (the HBM
+    slice the scheduler granted on a shared GPU, or a per-process cap).  An
+    allocation beyond it raises OOM in THIS rank instead of starving the other
+    tenants of the device.  Returns the fraction applied."""
+    gb = os.environ.get("KDL_HBM_LIMIT_GB")
+    if not gb or dev.type != "cuda":
+        return None
+    total = torch.cuda.get_device_properties(dev).total_memory / 1e9 or MI355X_HBM_GB
+    frac = max(0.0, min(1.0, float(gb) / total))
+    torch.cuda.set_per_process_memory_fraction(frac, dev)
+    return frac
+
+
 def init_from_env(device: str | None = None, timeout_s: float | None = None,
                   world1_group: bool = False) -> DistInfo:
     """``world1_group``: also build a (one-rank) process group at WORLD_SIZE=1,
@@ -59,6 +76,7 @@ def init_from_env(device: str | None = None, timeout_s: float | None = None,
         ndev = torch.cuda.device_count()
         dev = torch.device("cuda", local_rank % max(ndev, 1))
         torch.cuda.set_device(dev)
+        apply_hbm_limit(dev)
         # KDL_DIST_BACKEND=gloo: rehearse a multi-rank job on fewer GPUs than
         # ranks (gloo moves CUDA tensors through host memory; RCCL would
         # refuse two ranks on one device)

@@ -49,7 +49,7 @@ from typing import Dict, List, Optional, Tuple
 from kubedl_amd.api import common as c
 from kubedl_amd.runtime import images
 from kubedl_amd.runtime import zygote as zygote_mod
-from kubedl_amd.runtime.scheduler import GPU_ANNOTATION
+from kubedl_amd.runtime.scheduler import GPU_ANNOTATION, HBM_ANNOTATION
 from kubedl_amd.store import ADDED, DELETED, MODIFIED, NotFound, Store
 
 log = logging.getLogger("kubedl_amd.kubelet")
@@ -203,6 +203,11 @@ class PodWorker(threading.Thread):
         env["KDL_REPLICA_INDEX"] = labels.get(c.REPLICA_INDEX_LABEL, "")
         env["KDL_SANDBOX"] = self.sandbox
         env["KDL_NUM_GPUS"] = str(len(self.gpus))
+        # HBM slice of a shared GPU (scheduler annotation) or a per-process cap
+        # asked on an exclusive GPU: the rank caps its caching allocator to it
+        hbm = (md.get("annotations") or {}).get(HBM_ANNOTATION) or c.hbm_requested(ctr) or ""
+        if hbm:
+            env["KDL_HBM_LIMIT_GB"] = str(hbm)
         ready = os.path.join(self.sandbox, f"ready.{cidx}")
         env["KDL_READY_FILE"] = ready
         env["KDL_PROGRESS_FILE"] = os.path.join(self.sandbox, f"progress.{cidx}")
@@ -330,6 +335,10 @@ class PodWorker(threading.Thread):
             setc("Initialized", init_done)
             setc("ContainersReady", all_ready, ready_ts)
             setc("Ready", all_ready, ready_ts)
+            if all_ready and ready_ts:
+                # first time every container was Ready: kept after the pod ends, so a
+                # rank that finishes before the controller looks still has a launch time
+                st.setdefault("readyTime", ready_ts)
             order = ["PodScheduled", "Initialized", "ContainersReady", "Ready"]
             st["conditions"] = [conds[t] for t in order if t in conds]
         self._patch_status(fn)

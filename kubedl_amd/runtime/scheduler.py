@@ -13,6 +13,9 @@ Replaces kube-scheduler + kube-batch for one node:
 * queue order is FIFO by creation time with backfill: a later gang that fits
   in the currently free GPUs may start while the head waits, until the head
   has waited ``starvation_s`` -- then backfill stops so big gangs cannot starve;
+* a pod asking for ``kubedl.io/hbm-gb`` and no whole GPU gets an HBM slice
+  of a shared GPU (``GPUAllocator``); its binding also carries
+  ``kubedl.io/hbm-gb``;
 * binding writes ``spec.nodeName``, the ``kubedl.io/gpus`` annotation and the
   ``PodScheduled`` condition; GPUs return to the pool when the pod reaches a
   terminal phase, or when it is deleted AND the kubelet no longer holds its
@@ -38,6 +41,7 @@ from kubedl_amd.store import ADDED, DELETED, MODIFIED, NotFound, Store
 log = logging.getLogger("kubedl_amd.scheduler")
 
 GPU_ANNOTATION = "kubedl.io/gpus"
+HBM_ANNOTATION = "kubedl.io/hbm-gb"
 NODE_NAME = "localhost"
 
 
@@ -48,6 +52,10 @@ def pod_key(pod: dict) -> str:
 
 def pod_gpus(pod: dict) -> int:
     return c.pod_template_gpus({"spec": pod.get("spec") or {}})
+
+
+def pod_hbm(pod: dict) -> float:
+    return c.pod_template_hbm({"spec": pod.get("spec") or {}})
 
 
 QUEUE_TIME_ANNOTATION = "kubedl.io/queue-time"
@@ -188,18 +196,23 @@ class NodeScheduler:
                 self._mark_unschedulable(pods, "waiting behind an older gang (FIFO after starvation)")
                 continue
             req = {pod_key(p): pod_gpus(p) for p in pods}
-            alloc = self.alloc.allocate(owner, req)
+            hbm = {pod_key(p): pod_hbm(p) for p in pods}
+            alloc = self.alloc.allocate(owner, req, hbm)
             if alloc is None:
                 free = len(self.alloc.free)
+                want_hbm = sum(v for k, v in hbm.items() if not req[k])
                 self._mark_unschedulable(
                     pods, f"0/1 nodes available: insufficient amd.com/gpu (need {sum(req.values())}, "
-                          f"{free}/{self.alloc.inv.count} free)")
+                          f"{free}/{self.alloc.inv.count} free)"
+                          + (f" or kubedl.io/hbm-gb (need {want_hbm:g} GB in slices, "
+                             f"max free on a GPU {max(self.alloc.hbm_free().values(), default=0):g} GB)"
+                             if want_hbm else ""))
                 if head_blocked_since is None:
                     head_blocked_since = age
                 continue
             for p in pods:
                 k = pod_key(p)
-                if self._bind(p, alloc.pods.get(k, [])):
+                if self._bind(p, alloc.pods.get(k, []), alloc.slices.get(k)):
                     with self._lock:
                         self._owner_of_pod[k] = owner
                         self._unsched_marked.discard(k)
@@ -213,7 +226,7 @@ class NodeScheduler:
             self.metrics.gpus_allocated.set(self.alloc.used())
         return bound
 
-    def _bind(self, pod: dict, gpus: List[int]) -> bool:
+    def _bind(self, pod: dict, gpus: List[int], hbm_slice: Optional[float] = None) -> bool:
         md = pod["metadata"]
         ts = c.now()
 
@@ -221,7 +234,10 @@ class NodeScheduler:
             if o["metadata"].get("uid") != md.get("uid"):
                 raise NotFound("pod replaced")
             o.setdefault("spec", {})["nodeName"] = self.node
-            o["metadata"].setdefault("annotations", {})[GPU_ANNOTATION] = ",".join(map(str, gpus))
+            ann = o["metadata"].setdefault("annotations", {})
+            ann[GPU_ANNOTATION] = ",".join(map(str, gpus))
+            if hbm_slice is not None:
+                ann[HBM_ANNOTATION] = f"{hbm_slice:g}"
             st = o.setdefault("status", {})
             conds = [x for x in st.get("conditions") or [] if x.get("type") != "PodScheduled"]
             conds.append({"type": "PodScheduled", "status": "True", "lastTransitionTime": ts})

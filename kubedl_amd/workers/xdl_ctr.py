@@ -91,6 +91,8 @@ def main(argv=None) -> int:
     device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
+        from kubedl_amd.parallel.dist import apply_hbm_limit
+        apply_hbm_limit(device)
     backend = "nccl" if use_gpu else "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -40,7 +40,7 @@ def gemm1x1(A, W, C, M, N, K, epi, shift, ws):
 
 def variants():
     out = [("reg", 0, -1)]
-    for cfg in (0, 1, 2, 3):
+    for cfg in (0, 1, 2, 3, 4):
         out.append((f"dma{cfg}", 1, cfg))
     return out
 
@@ -54,7 +54,7 @@ def run_1x1(M, N, K, rounds=3):
     res = {}
     for _ in range(rounds):
         for name, core, cfg in variants():
-            if cfg in (0,) and N % 256 or cfg in (1, 2) and N % 128:
+            if cfg in (0,) and N % 256 or cfg in (1, 2, 4, 5, 9) and N % 128:
                 continue
             ext.set_gemm_core(core)
             ext.set_igemm_cfg(cfg)
@@ -79,7 +79,7 @@ def run_3x3(nb, H, Cin, Cout, stride, rounds=3):
     for _ in range(rounds):
         res.setdefault("miopen", []).append(timed(lambda: F.conv2d(x, w, stride=stride, padding=1)))
         for name, core, cfg in variants():
-            if cfg in (0,) and Cout % 256 or cfg in (1, 2) and Cout % 128:
+            if cfg in (0,) and Cout % 256 or cfg in (1, 2, 4, 5, 9) and Cout % 128:
                 continue
             ext.set_gemm_core(core)
             ext.set_igemm_cfg(cfg)

@@ -1,0 +1,83 @@
+"""HBM-sliced GPU sharing: the allocator packs ``kubedl.io/hbm-gb`` slices onto
+shared GPUs within 288 GB, keeps exclusive and shared use apart, and the
+scheduler/kubelet carry the slice to the rank as ``KDL_HBM_LIMIT_GB``."""
+import time
+
+import pytest
+
+from kubedl_amd.api import common as c
+from kubedl_amd.engine.manager import Manager, ManagerOptions
+from kubedl_amd.gang.allocator import GPUAllocator, GPUInventory
+
+
+def test_slices_pack_best_fit_and_release():
+    a = GPUAllocator(GPUInventory(4))
+    # four 64 GB slices share one GPU (256 <= 288), the fifth does not fit there
+    for i in range(4):
+        al = a.allocate(f"j{i}", {"p": 0}, {"p": 64})
+        assert al.pods["p"] == [0] and al.slices == {"p": 64}
+    al = a.allocate("j4", {"p": 0}, {"p": 64})
+    assert al.pods["p"] == [1]
+    assert a.hbm_free()[0] == pytest.approx(288 - 256) and a.hbm_free()[1] == pytest.approx(224)
+    # a 32 GB slice fills GPU 0's remaining room (best fit: the fullest that still fits)
+    assert a.allocate("j5", {"p": 0}, {"p": 32}).pods["p"] == [0]
+    assert a.used() == 2 and a.free == [2, 3]
+    assert a.hbm_used() == pytest.approx(64 * 5 + 32)
+    # releasing every slice of GPU 1 frees the GPU
+    assert a.release("j4") == [1]
+    assert a.free == [1, 2, 3]
+
+
+def test_exclusive_and_shared_never_mix():
+    a = GPUAllocator(GPUInventory(2))
+    assert a.allocate("s", {"p": 0}, {"p": 10}).pods["p"] == [0]
+    # two whole GPUs are not available any more (GPU 0 carries a slice)
+    assert a.allocate("x", {"a": 1, "b": 1}) is None
+    x = a.allocate("x", {"a": 1})
+    assert x.pods["a"] == [1] and x.gpus == [1]
+    # no room for a slice on an exclusively owned GPU, and GPU 0 has only 278 GB left
+    assert a.allocate("big", {"p": 0}, {"p": 280}) is None
+    assert a.allocate("fits", {"p": 0}, {"p": 278}).pods["p"] == [0]
+
+
+def test_gang_with_slices_is_all_or_nothing():
+    a = GPUAllocator(GPUInventory(1))
+    # a three-member gang of 100 GB slices cannot fit one 288 GB GPU: nothing is placed
+    assert a.allocate("g", {"m": 0, "w0": 0, "w1": 0}, {"m": 100, "w0": 100, "w1": 100}) is None
+    assert a.hbm_free()[0] == pytest.approx(288) and a.used() == 0
+    al = a.allocate("g", {"m": 0, "w0": 0}, {"m": 100, "w0": 100})
+    assert al.pods == {"m": [0], "w0": [0]}
+    with pytest.raises(ValueError):
+        a.allocate("bad", {"p": 0}, {"p": -1})
+    assert a.allocate("huge", {"p": 0}, {"p": 300}) is None
+
+
+def test_scheduler_binds_slice_and_kubelet_exports_limit(tmp_path, monkeypatch):
+    """Two single-pod jobs with 100 GB slices land on the same GPU; each rank sees
+    KDL_HBM_LIMIT_GB=100 and HIP_VISIBLE_DEVICES of that GPU."""
+    monkeypatch.setenv("KDL_ZYGOTE", "0")
+    m = Manager(ManagerOptions(home=str(tmp_path), gpus=2)).start()
+    try:
+        out = tmp_path / "env"
+        out.mkdir()
+        for name in ("s1", "s2"):
+            job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                   "metadata": {"name": name, "namespace": "default"},
+                   "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "restartPolicy": "Never", "template": {
+                       "spec": {"containers": [{
+                           "name": "pytorch", "image": "kubedl-amd/sleep",
+                           "command": ["bash", "-c",
+                                       f"echo $HIP_VISIBLE_DEVICES $KDL_HBM_LIMIT_GB > {out}/{name}; sleep 2"],
+                           "resources": {"limits": {c.HBM_RESOURCE: 100}}}]}}}}}}
+            m.apply(job)
+        for name in ("s1", "s2"):
+            st = m.wait_for_condition("PyTorchJob", "default", name, ["Succeeded", "Failed"], timeout=60)
+            assert c.last_condition_type(st["status"]) == "Succeeded"
+        got = {name: (out / name).read_text().split() for name in ("s1", "s2")}
+        assert got["s1"] == got["s2"] == ["0", "100"], got
+        deadline = time.time() + 10
+        while m.allocator.used() and time.time() < deadline:
+            time.sleep(0.1)
+        assert m.allocator.used() == 0
+    finally:
+        m.stop()

@@ -19,7 +19,7 @@ def _ext():
     return _ext.load()
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2, 3])
+@pytest.fixture(autouse=True, params=[0, 1, 2, 3, 4])
 def dma_core(request):
     ext = _ext()
     old = ext.get_gemm_core()

@@ -167,7 +167,8 @@ def _ddp_step_worker(rank, world, port, q, transport):
     losses = [float(tr.step()) for _ in range(2)]
     torch.cuda.synchronize()
     tr.check_transport()
-    q.put((rank, losses, tr.space.master.cpu(), tr.space.param.float().cpu(), tr.engine_kind))
+    # numpy, not tensors: a tensor in a Queue is shared through an fd that dies with this process
+    q.put((rank, losses, tr.space.master.cpu().numpy(), tr.space.param.float().cpu().numpy(), tr.engine_kind))
     dist.barrier(device_ids=[rank])
     dist.destroy_process_group()
 
@@ -185,7 +186,7 @@ def test_engine_ddp_step_identical_weights(world, transport):
     assert res[0][4] == "fused"
     m0, p0 = res[0][2], res[0][3]
     for r in res[1:]:
-        assert torch.equal(r[2], m0) and torch.equal(r[3], p0)
+        assert (r[2] == m0).all() and (r[3] == p0).all()
     assert len({round(r[1][0], 5) for r in res}) > 1  # the ranks did see different data
 
 
@@ -259,7 +260,7 @@ def _ddp_fp32_worker(rank, world, port, q):
     for s in sp.slots:
         ddp.ready(s.param)
     ddp.finish()
-    q.put((rank, local, sp.grad.clone()))
+    q.put((rank, local.float().numpy(), sp.grad.float().numpy()))  # numpy: see _ddp_step_worker
     dist.barrier()
     dist.destroy_process_group()
 
@@ -267,6 +268,6 @@ def _ddp_fp32_worker(rank, world, port, q):
 def test_ddp_fp32_reduce_matches_fp32_sum_cpu():
     world = 4
     res = _spawn_cpu(_ddp_fp32_worker, world)
-    total = torch.stack([r[1].float() for r in res]).sum(0).to(torch.bfloat16)
+    total = torch.stack([torch.as_tensor(r[1]) for r in res]).sum(0).to(torch.bfloat16)
     for r in res:
-        assert torch.equal(r[2], total)  # fp32 sum, rounded to bf16 once
+        assert torch.equal(torch.as_tensor(r[2]), total.float())  # fp32 sum, rounded to bf16 once

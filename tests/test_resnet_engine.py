@@ -173,7 +173,8 @@ def _ddp_worker(rank, world, port, q):
     tr = ResNetTrainer(info, batch=2, image=32, num_classes=10, tiny=True, engine="fused",
                        bucket_cap_mb=0.05, seed=0)
     losses = [float(tr.step()) for _ in range(2)]
-    q.put((rank, losses, tr.space.master.clone(), tr.space.grad.float().clone()))
+    # numpy, not tensors: a tensor in a Queue is shared through an fd that dies with this process
+    q.put((rank, losses, tr.space.master.numpy().copy(), tr.space.grad.float().numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -197,6 +198,7 @@ def test_engine_ddp_gloo_two_ranks():
         p.join(60)
         assert p.exitcode == 0
     (_, l0, m0, g0), (_, l1, m1, g1) = res
+    m0, m1, g0, g1 = (torch.as_tensor(a) for a in (m0, m1, g0, g1))
     assert l0 != l1  # different data per rank
     torch.testing.assert_close(m0, m1, atol=0, rtol=0)
     torch.testing.assert_close(g0, g1, atol=0, rtol=0)  # all-reduced
