@@ -458,3 +458,75 @@ def test_xgboost_cluster_spec_table(workers, rtype, index, want):
     XGB.set_cluster_spec(XGB.__new__(XGB), job, tmpl, rtype.lower(), index)
     env = {e["name"]: e["value"] for e in tmpl["spec"]["containers"][0]["env"]}
     assert {k: env[k] for k in want} == want
+
+
+# =================================================================== job_controller/pod_test.go, status_test.go, util_test.go
+@pytest.mark.parametrize("replica_policy,pod_policy", [
+    ("ExitCode", "Never"), ("Never", "Never"), ("Always", "Always"), ("OnFailure", "OnFailure")])
+def test_set_restart_policy_table(replica_policy, pod_policy):
+    """TestSetRestartPolicy: ExitCode is implemented by the controller, so the pod gets Never."""
+    jc, pods, _ = new_job_controller()
+    job = new_test_job(workers=2, restart_policy=replica_policy)
+    specs = job["spec"]["testReplicaSpecs"]
+    jc.create_new_pod(job, "worker", "0", specs["Worker"], False, specs)
+    assert pods.templates[-1]["spec"]["restartPolicy"] == pod_policy
+
+
+def test_update_job_replica_statuses():
+    """TestUpdateJobReplicaStatuses: 2 failed, 3 succeeded, 1 running -> counts per phase."""
+    jc, _, _ = new_job_controller()
+    job = new_test_job(workers=6, master=False)
+    spec = job["spec"]["testReplicaSpecs"]["Worker"]
+    phases = ["Failed"] * 2 + ["Succeeded"] * 3 + ["Running"]
+    pods = [{"metadata": {"name": f"test-job-worker-{i}", "namespace": "default",
+                          "labels": {c.REPLICA_TYPE_LABEL: "worker", c.REPLICA_INDEX_LABEL: str(i)}},
+             "status": {"phase": ph}} for i, ph in enumerate(phases)]
+    status = {"conditions": [], "replicaStatuses": {}}
+    jc.reconcile_pods(job, status, pods, "Worker", spec, {"Worker": spec}, [False])
+    assert status["replicaStatuses"]["Worker"] == {"failed": 2, "succeeded": 3, "active": 1}
+
+
+def test_gen_general_name():
+    """TestGenGeneralName: '/' in the job key becomes '-'."""
+    assert c.gen_general_name("1/2/3/4/5", "worker", "1") == "1-2-3-4-5-worker-1"
+
+
+# =================================================================== metrics/status_counter_test.go
+@pytest.mark.parametrize("conds,running,pending", [(["Created"], 0, 1), (["Created", "Running"], 1, 0)])
+def test_job_status_counter(conds, running, pending):
+    """JobStatusCounter: pending = only the Created condition; running = last condition Running."""
+    from kubedl_amd.metrics.job_metrics import MetricsRegistry
+    reg = MetricsRegistry()
+    reg.job_metrics("TFJob")
+    status = {"conditions": [], "replicaStatuses": {}}
+    for t in conds:
+        c.update_job_conditions(status, t, "", "")
+    reg.lister = lambda kind: [{"kind": "TFJob", "status": status}] if kind == "TFJob" else []
+    got = {m.name: m.samples[0].value for m in reg.registry.collect() if m.name in ("kubedl_jobs_running",
+                                                                                        "kubedl_jobs_pending")}
+    assert got == {"kubedl_jobs_running": running, "kubedl_jobs_pending": pending}
+
+
+# =================================================================== service_control_test.go, pod_control_test.go
+@pytest.mark.parametrize("with_ref", [False, True], ids=["plain", "controllerRef"])
+@pytest.mark.parametrize("kind", ["Service", "Pod"])
+def test_object_control_create(kind, with_ref):
+    """ServiceControl/PodControl create: the stored object keeps labels, name,
+    namespace and spec (ports / containers); with a controller reference it is owned."""
+    from kubedl_amd.engine.control import PodControl
+    store = Store()
+    job = new_test_job(name="test-job")
+    labels = {"group-name": "test.kubedl.io", "test-job-name": "test-job"}
+    md = {"name": f"{kind.lower()}-name", "namespace": "default", "labels": dict(labels), "ownerReferences": []}
+    if with_ref:
+        md["ownerReferences"] = [gen_owner_reference(job)]
+    spec = ({"ports": [{"name": "test-port", "protocol": "TCP", "port": 8888, "targetPort": 8888}]}
+            if kind == "Service" else {"containers": [{"name": "c", "image": "img"}]})
+    ctl = (ServiceControl if kind == "Service" else PodControl)(store, EventRecorder(store))
+    ctl.create(job, {"apiVersion": "v1", "kind": kind, "metadata": md, "spec": spec})
+    got = store.get(kind, "default", f"{kind.lower()}-name")
+    assert got["metadata"]["labels"] == labels and got["spec"] == spec
+    refs = got["metadata"].get("ownerReferences") or []
+    assert (refs == [gen_owner_reference(job)]) if with_ref else refs == []
+    reasons = {e["reason"] for e in store.list("Event")}
+    assert ("SuccessfulCreateService" if kind == "Service" else "SuccessfulCreatePod") in reasons
