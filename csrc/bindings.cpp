@@ -959,6 +959,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("destroy_stream", &destroy_stream_py, "destroy a stream from make_stream");
   m.def("set_gemm_core", &kdl::set_gemm_core_mode, "conv GEMM main loop: -1 by shape, 0 register-staged, 1 LDS-DMA");
   m.def("set_igemm_cfg", &kdl::set_igemm_cfg, "force an LDS-DMA tile config (-1 = by shape)");
+  m.def("set_halo3x3", &kdl::set_halo3x3, "1: stride-1 3x3 convs of the early stages on the halo kernel");
   m.def("get_gemm_core", &kdl::gemm_core_mode, "current conv GEMM main-loop mode");
   m.def("spin", &spin_py, "one wave busy-waiting N microseconds on the current stream");
   m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";

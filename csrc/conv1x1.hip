@@ -621,6 +621,10 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
     p.a_rows = gather == G_CONV3 ? static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win
                : gather == G_STRIDED ? static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win
                                      : p.M;
+    if (gather == G_CONV3) {  // early stages: input halo staged once per tile (csrc/halo3x3.hip)
+      const hipError_t h = halo3x3(p, epi, s);
+      if (h != hipErrorInvalidValue) return h;
+    }
     const hipError_t e = igemm(p, epi, gather, igemm_pick(p.M, p.N, p.K), s);
     if (e != hipErrorInvalidValue) return e;
   }

@@ -59,6 +59,7 @@ struct GemmParams {
   const bf16_t* ex2;    // RESBITS: optional second BN input (downsample BN)
   const float* emean2;
   float* acc2;          // its replicas [kRep][2N]
+  int price_drop;       // timing-only builds (KDL_IGEMM_PRICE): bit 0 drops A's loads, bit 1 B's
 };
 
 // csrc/wgrad_dma.hip: weight gradient on the LDS-DMA pipeline into fp32
@@ -82,6 +83,9 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
 // Requires K % 64 == 0 (3x3: Cin % 64 == 0) and 32-bit operand byte offsets.
 int igemm_pick(int M, int N, int K);
 hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t s);
+// csrc/halo3x3.hip: 3x3 stride-1 conv with an LDS-resident input halo (Cin 64 @ 56x56);
+// hipErrorInvalidValue when the geometry is not one it serves
+hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s);
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 

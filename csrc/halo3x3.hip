@@ -1,0 +1,276 @@
+// 3x3 stride-1 pad-1 convolution with the input tile staged ONCE per tile as
+// a halo in LDS (gfx950), for the operand-stream-bound early ResNet stages.
+//
+// Why: the LDS-DMA implicit GEMM of csrc/igemm.hip fetches every output row's
+// input pixel once per tap, so its A stream is 9x the input, and LDS-DMA into
+// LDS runs at ~7-10 TB/s chip-wide (docs/perf_notes.md) -- the N = 64 / 128
+// layers sit on that stream, not on the MFMAs.  Here a tile is TH full output
+// rows of one image (BM = TH * W = 224 pixels); its (TH + 2) x (W + 2) input
+// halo (zero padding = buffer-OOB loads) lands in LDS once and the nine taps
+// read shifted 32-pixel fragments from it.  The weights of the block's BN
+// output channels for all nine taps (9 * Cin * BN bf16 = 72 KiB) stay
+// resident in LDS for the block's lifetime (persistent blocks, one N tile per
+// block), so per tile the only DMA is the halo:
+//
+//   Cin = 64  (56x56): BN = 64, TH = 4, halo 348 px x 128 B, double-buffered:
+//                      the next tile's halo streams in under this tile's MFMAs.
+//                      118.7 -> 80.6 us per layer (stage-1 forward and data
+//                      gradient; profiles/r02_halo3x3_vs_igemm.jsonl)
+//   Cin = 128 (28x28): the template's single-buffered form (BN = 32, TH = 8,
+//                      300 px x 256 B) measured equal to the implicit GEMM
+//                      (90.0 vs 90.2 us) and is not dispatched: with one
+//                      7-wave block per CU the epilogue is not overlapped and
+//                      the halo is fetched once per 32-channel N tile.
+//
+// LDS image: rows of 128 B (one 64-channel chunk of one pixel; a Cin = 128
+// pixel is two consecutive rows), 16-B chunk c of row R at chunk position
+// c ^ ((R >> 1) & 7) -- swizzled on the SOURCE address because the DMA writes
+// lane-linear (the igemm.hip scheme).  Seven waves, one 32-pixel MFMA row
+// block each (v_mfma_f32_32x32x16_bf16, weight fragment as the A operand), and
+// the fused epilogues of gemm_epi.h (BN statistics for the forward conv, ReLU
+// mask + BN backward sums for the stride-1 data gradient).  The DMA is issued
+// from inline asm and retired by counted vmcnt + raw barriers (csrc/igemm.hip
+// three-stage path) so the next halo stays in flight across the barriers.
+#include <cstdlib>
+
+#include "common.h"
+#include "gemm_epi.h"
+#include "kdl_api.h"
+
+namespace kdl {
+namespace {
+
+using namespace gemm;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: zeros
+constexpr int kWaves = 7, kNT = 64 * kWaves, kBM = 32 * kWaves;  // 224-pixel tiles
+constexpr int kBRows = 576;            // resident weight rows: 9 taps x Cin/64 chunks x BN
+
+__device__ __forceinline__ i32x4_t rsrc_words(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane(static_cast<int>(a & 0xffffffffu));
+  r.y = __builtin_amdgcn_readfirstlane(static_cast<int>((a >> 32) & 0xffffu));
+  r.z = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+  r.w = 0x00020000;
+  return r;
+}
+
+// 16 B per lane LDS-DMA (1 KiB per wave instruction at dst + 16 * lane), from
+// inline asm: the compiler sees no LDS write, so it adds no waits of its own.
+__device__ __forceinline__ void dma16(i32x4_t r, lds_void_t* dst, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst)));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(r)
+               : "memory", "m0");
+#endif
+}
+
+template <int CIN, int BN, int TH, bool DOUBLE, int EPI>
+__global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, int W, int tiles_m, int tiles_n) {
+  constexpr int RP = CIN / 64;             // 128-B LDS rows per pixel
+  constexpr int TN = BN / 32;              // 32-wide MFMA column blocks per wave
+  static_assert(9 * RP * BN == kBRows, "weights fill the resident block");
+  constexpr int B_BYTES = kBRows * 128;
+  using Epi = Epilogue<kBM, BN, kNT, EPI>;
+  constexpr int LDC = Epi::LDC;
+  // halo rows (per buffer) for the largest geometry this instantiation serves
+  constexpr int HW_MAX = TH == 4 ? 58 : 30;                    // W + 2
+  constexpr int HROWS = ((TH + 2) * HW_MAX * RP + 7) / 8 * 8;  // whole 1-KiB DMA groups
+  constexpr int HALO_BYTES = HROWS * 128;
+  constexpr int NBUF = DOUBLE ? 2 : 1;
+  static_assert(HALO_BYTES >= kBM * LDC * 2 && HALO_BYTES >= Epi::kScratchBytes, "epilogue fits a halo buffer");
+  static_assert(B_BYTES + NBUF * HALO_BYTES <= 160 * 1024, "LDS budget");
+  constexpr int HI = HROWS / 8;                                // DMA instructions per halo
+  constexpr int HIPW = (HI + kWaves - 1) / kWaves;             // per wave (upper bound)
+  constexpr int HIPW_MIN = HI / kWaves;                        // per wave (lower bound: counted waits)
+  constexpr int BIPW = (kBRows / 8 + kWaves - 1) / kWaves;
+  __shared__ __attribute__((aligned(1024))) char lds[B_BYTES + NBUF * HALO_BYTES];
+  char* Bs = lds;
+  char* Hs = lds + B_BYTES;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
+  const int tile_n = blockIdx.x % tiles_n;
+  const int gm0 = blockIdx.x / tiles_n, gstride = gridDim.x / tiles_n;
+  const int n0 = tile_n * BN;
+  const int WP = W + 2;
+  const int nh = (TH + 2) * WP * RP;  // halo rows actually used
+
+  const i32x4_t rA = rsrc_words(p.A, static_cast<uint32_t>(p.a_rows * CIN * 2));
+  const i32x4_t rB = rsrc_words(p.B, static_cast<uint32_t>(static_cast<int64_t>(p.N) * 9 * CIN * 2));
+
+  // ---- resident weights: row b = (tap * RP + kc) * BN + n -> W[n0 + n][tap * CIN + kc * 64 ..]
+#pragma unroll
+  for (int i = 0; i < BIPW; ++i) {
+    const int g = wave + i * kWaves;
+    if (g < kBRows / 8) {
+      const int b = 8 * g + (lane >> 3);
+      const int c = (lane & 7) ^ ((b >> 1) & 7);
+      const int tk = b / BN, n = b - tk * BN;  // tk = tap * RP + kc
+      const int tap = tk / RP, kc = tk - tap * RP;
+      const uint32_t off = static_cast<uint32_t>(
+          (static_cast<int64_t>(n0 + n) * 9 * CIN + tap * CIN + kc * 64 + 8 * c) * 2);
+      dma16(rB, (lds_void_t*)(Bs + g * 1024), off);
+    }
+  }
+
+  // ---- halo geometry per DMA slot (tile-invariant): LDS row R = hp * RP + kc
+  int hrow[HIPW], hcol[HIPW], hsub[HIPW];  // input row/col relative to the tile, chunk offset (bytes)
+#pragma unroll
+  for (int i = 0; i < HIPW; ++i) {
+    const int g = wave + i * kWaves;
+    const int R = 8 * g + (lane >> 3);
+    const int hp = R / RP, kc = R - hp * RP;
+    const int c = (lane & 7) ^ ((R >> 1) & 7);
+    const int hr = hp / WP;
+    hrow[i] = (g < HI && R < nh) ? hr - 1 : -0x4000;  // -0x4000: never inside an image
+    hcol[i] = hp - hr * WP - 1;
+    hsub[i] = (kc * 64 + 8 * c) * 2;
+  }
+  auto issue_halo = [&](int tm, int buf) {
+    const int tpi = H / TH;
+    const int img = tm / tpi, r0 = (tm - img * tpi) * TH;
+    char* base = Hs + buf * HALO_BYTES;
+#pragma unroll
+    for (int i = 0; i < HIPW; ++i) {
+      const int g = wave + i * kWaves;
+      if (g < HI) {
+        const int ih = r0 + hrow[i], iw = hcol[i];
+        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+        const uint32_t off =
+            ok ? static_cast<uint32_t>(((static_cast<int64_t>(img) * H + ih) * W + iw) * (CIN * 2) + hsub[i]) : kOOB;
+        dma16(rA, (lds_void_t*)(base + g * 1024), off);
+      }
+    }
+  };
+
+  // ---- fragment geometry: this lane's output pixel m = wave * 32 + fr of the
+  // tile -> (i, j); tap (r, s) reads halo pixel (i + r) * WP + j + s
+  const int m = wave * 32 + fr;
+  const int pi = m / W, pj = m - pi * W;
+  const int hbase = pi * WP + pj;
+
+  Epi epi;
+  epi.init(t, n0);
+
+  int buf = 0;
+  int tm = gm0;
+  if (tm < tiles_m) issue_halo(tm, 0);
+  for (; tm < tiles_m; tm += gstride) {
+    const int next = tm + gstride;
+    if constexpr (DOUBLE) {
+      if (next < tiles_m) {
+        issue_halo(next, buf ^ 1);
+        // retire everything older than the halo just issued (this tile's halo, the weights)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HIPW_MIN) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    const char* Hb = Hs + buf * HALO_BYTES;
+    f32x16_t acc[TN][1];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) acc[i][0] = f32x16_t{};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int hp = hbase + (tap / 3) * WP + (tap % 3);
+#pragma unroll
+      for (int kc = 0; kc < RP; ++kc) {
+        const int R = hp * RP + kc;
+        const int xr = (R >> 1) & 7;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8_t xf = *reinterpret_cast<const bf16x8_t*>(Hb + R * 128 + (((2 * s + fh) ^ xr) * 16));
+#pragma unroll
+          for (int i = 0; i < TN; ++i) {
+            const int b = (tap * RP + kc) * BN + i * 32 + fr;
+            const bf16x8_t wf =
+                *reinterpret_cast<const bf16x8_t*>(Bs + b * 128 + (((2 * s + fh) ^ ((b >> 1) & 7)) * 16));
+            acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf, acc[i][0], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // every wave's fragment reads of this halo are done before it becomes the C tile
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    epi.begin(p, tm);
+    bf16_t* Cs = reinterpret_cast<bf16_t*>(Hs + buf * HALO_BYTES);
+    acc_to_lds<TN, 1>(acc, Cs, LDC, wave * 32, 0, lane);
+    __syncthreads();
+    epi.rows(p, Cs, tm);
+    __syncthreads();  // the C tile is read out before the buffer takes a halo again
+    if constexpr (DOUBLE) {
+      buf ^= 1;
+    } else {
+      if (next < tiles_m) issue_halo(next, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  epi.finish(p, reinterpret_cast<float*>(Hs), blockIdx.x, gm0 < tiles_m);
+}
+
+template <int CIN, int BN, int TH, bool DOUBLE>
+hipError_t launch(const GemmParams& p, int epi, int H, int W, hipStream_t s) {
+  const int tiles_m = p.M / kBM;
+  const int tiles_n = p.N / BN;
+  int per_n = 256 / tiles_n;  // one resident block per CU, each pinned to one N tile
+  if (per_n > tiles_m) per_n = tiles_m;
+  if (per_n < 1) per_n = 1;
+  const dim3 grid(per_n * tiles_n), block(kNT);
+  switch (epi) {
+    case EPI_PLAIN:
+      hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_PLAIN>), grid, block, 0, s, p, H, W, tiles_m, tiles_n);
+      break;
+    case EPI_STATS:
+      hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_STATS>), grid, block, 0, s, p, H, W, tiles_m, tiles_n);
+      break;
+    case EPI_MASKX:
+      hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_MASKX>), grid, block, 0, s, p, H, W, tiles_m, tiles_n);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+int g_halo = [] {  // KDL_HALO=0 keeps every 3x3 on the implicit GEMM
+  const char* e = getenv("KDL_HALO");
+  return e ? atoi(e) : 1;
+}();
+
+}  // namespace
+
+void set_halo3x3(int on) { g_halo = on; }
+
+namespace gemm {
+// 3x3 / stride 1 / pad 1 / dense A (no prologue) on the halo kernel when the
+// geometry is one it serves (56x56, Cin 64); hipErrorInvalidValue = "not
+// here, use igemm".
+hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s) {
+  if (!g_halo || p.stride != 1 || p.pro_coef != nullptr) return hipErrorInvalidValue;
+  const int H = p.Hin, W = p.Win;
+  if (p.Hout != H || p.Wout != W || p.M % (H * W) || p.K != 9 * p.Cin) return hipErrorInvalidValue;
+  if (static_cast<int64_t>(p.a_rows) * p.Cin * 2 >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  if (p.Cin == 64 && W == 56 && H % 4 == 0 && p.N % 64 == 0) return launch<64, 64, 4, true>(p, epi, H, W, s);
+  return hipErrorInvalidValue;
+}
+}  // namespace gemm
+
+}  // namespace kdl

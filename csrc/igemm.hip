@@ -30,6 +30,9 @@
 //
 // The reference has no kernels; this serves the PyTorchJob
 // ResNet-50 worker (BASELINE.json config 2).
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 #include "gemm_epi.h"
 #include "kdl_api.h"
@@ -116,14 +119,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
 
   // buffer resources (wave-uniform: built from kernel arguments only)
   const int lda = GATHER == G_CONV3 ? p.Cin : K;
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(p.A), (short)0, static_cast<int>(p.a_rows * lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(p.B), (short)0, static_cast<int>(static_cast<int64_t>(p.N) * K * 2), 0x00020000);
+  // (a zero-record descriptor drops that operand's loads: KDL_IGEMM_PRICE timing builds)
+  const int bytesA = (p.price_drop & 1) ? 0 : static_cast<int>(p.a_rows * lda * 2);
+  const int bytesB = (p.price_drop & 2) ? 0 : static_cast<int>(static_cast<int64_t>(p.N) * K * 2);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), (short)0, bytesA,
+                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.B), (short)0, bytesB,
+                                                                      0x00020000);
   i32x4_t wA{}, wB{};
   if constexpr (STAGES == 3) {
-    wA = rsrc_words(p.A, static_cast<uint32_t>(p.a_rows * lda * 2));
-    wB = rsrc_words(p.B, static_cast<uint32_t>(static_cast<int64_t>(p.N) * K * 2));
+    wA = rsrc_words(p.A, static_cast<uint32_t>(bytesA));
+    wB = rsrc_words(p.B, static_cast<uint32_t>(bytesB));
   }
   auto dma = [&](bool is_a, lds_void_t* dst, uint32_t voff, uint32_t soff) {
     if constexpr (STAGES == 3) dma16_asm(is_a ? wA : wB, dst, voff, soff);
@@ -367,7 +373,14 @@ int igemm_pick(int M, int N, int K) {
 }  // namespace gemm
 
 namespace gemm {
-hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t s) {
+hipError_t igemm(const GemmParams& p_in, int epi, int gather, int cfg, hipStream_t s) {
+  static const int price = [] {  // timing-only: price one operand's traffic (outputs are wrong)
+    const char* e = getenv("KDL_IGEMM_PRICE");
+    if (!e) return 0;
+    return (strchr(e, 'A') ? 1 : 0) | (strchr(e, 'B') ? 2 : 0);
+  }();
+  GemmParams p = p_in;
+  p.price_drop = price;
   if (p.K % IBK || p.M <= 0) return hipErrorInvalidValue;
   const int lda = gather == G_CONV3 ? p.Cin : p.K;
   if (p.a_rows * lda * 2 >= (int64_t(1) << 31) || static_cast<int64_t>(p.N) * p.K * 2 >= (int64_t(1) << 31))

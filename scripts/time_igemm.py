@@ -78,15 +78,17 @@ def run_3x3(nb, H, Cin, Cout, stride, rounds=3):
     res = {}
     for _ in range(rounds):
         res.setdefault("miopen", []).append(timed(lambda: F.conv2d(x, w, stride=stride, padding=1)))
-        for name, core, cfg in variants():
+        for name, core, cfg in variants() + [("halo", 1, -1)]:
             if cfg in (0,) and Cout % 256 or cfg in (1, 2, 4, 5, 9) and Cout % 128:
                 continue
+            ext.set_halo3x3(1 if name == "halo" else 0)
             ext.set_gemm_core(core)
             ext.set_igemm_cfg(cfg)
             res.setdefault(name, []).append(timed(
                 lambda: ext.conv3x3_gemm(x, w, y, nb, H, H, Cin, Cout, stride, None, 1, shift, acc, None, None, None)))
     ext.set_gemm_core(-1)
     ext.set_igemm_cfg(-1)
+    ext.set_halo3x3(1)
     fl = 2.0 * nb * Ho * Ho * Cout * 9 * Cin
     for name, ts in res.items():
         us = min(ts)
