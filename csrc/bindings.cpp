@@ -723,6 +723,37 @@ void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv3x3_gemm");
 }
 
+// dx of a 3x3 / pad 1 / stride 2 conv: dy [Nb, Hd, Wd, Cd] (channels_last),
+// ball = the weights regrouped class-major [N][9 Cd] (kubedl_amd.ops.conv.s2_dgrad_weights),
+// dx [Nb, 2 Hd, 2 Wd, N]; epi 0 PLAIN, 2 MASKX (ex = that BN's input [Nb, 2Hd, 2Wd, N]).
+void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor dx, int64_t Nb, int64_t Hd,
+                      int64_t Wd, int64_t Cd, int64_t N, int64_t epi, const c10::optional<at::Tensor>& acc,
+                      const c10::optional<at::Tensor>& ex, const c10::optional<at::Tensor>& emean,
+                      const c10::optional<at::Tensor>& ecoef) {
+  TORCH_CHECK(Cd % 64 == 0 && N % 64 == 0 && Nb > 0 && Hd > 0 && Wd > 0, "conv3x3_s2_dgrad: need Cd, N % 64 == 0");
+  TORCH_CHECK(epi == 0 || epi == 2, "conv3x3_s2_dgrad: epilogue must be PLAIN or MASKX");
+  const int64_t Mdx = Nb * 4 * Hd * Wd;
+  need_bf16(dy, Nb * Hd * Wd * Cd, "conv3x3_s2_dgrad dy");
+  need_bf16(ball, N * 9 * Cd, "conv3x3_s2_dgrad ball");
+  need_bf16(dx, Mdx * N, "conv3x3_s2_dgrad dx");
+  if (epi == 2) {
+    TORCH_CHECK(opt_ptr(ex) && opt_ptr(emean) && opt_ptr(ecoef) && opt_ptr(acc), "epi MASKX needs ex, emean, ecoef, acc");
+    need_opt_bf16(ex, Mdx * N, "ex"); need_opt_f32(emean, N, "emean"); need_opt_f32(ecoef, 2 * N, "ecoef");
+    need_opt_f32(acc, 32 * 2 * N, "acc");
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  kdl::Conv1x1Args a{};
+  a.A = dy.data_ptr(); a.B = ball.data_ptr(); a.C = dx.data_ptr();
+  a.M = static_cast<int>(Nb * Hd * Wd); a.N = static_cast<int>(N); a.K = static_cast<int>(9 * Cd);
+  a.Hin = static_cast<int>(Hd); a.Win = static_cast<int>(Wd);
+  a.Hout = static_cast<int>(2 * Hd); a.Wout = static_cast<int>(2 * Wd); a.stride = 2;
+  a.ksize = 3; a.Cin = static_cast<int>(Cd);
+  a.epi = static_cast<int>(epi);
+  a.acc = opt_fptr(acc);
+  a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
+  check_hip(kdl::conv3x3_dgrad_s2(a, cur_stream()), "conv3x3_s2_dgrad");
+}
+
 void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
                    at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t M, int64_t N, int64_t K,
                    int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride) {
@@ -994,6 +1025,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
+  m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 pad-1 conv weight gradient (implicit GEMM, split-M slabs)");

@@ -637,6 +637,26 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   }
 }
 
+hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
+  if (a.Cin <= 0 || a.Cin % 64 || a.N % 64 || a.K != 9 * a.Cin || a.Hout != 2 * a.Hin || a.Wout != 2 * a.Win ||
+      a.M <= 0 || a.M % (a.Hin * a.Win) || (a.epi != EPI_PLAIN && a.epi != EPI_MASKX) || a.pro_coef)
+    return hipErrorInvalidValue;
+  GemmParams p{};
+  p.A = static_cast<const bf16_t*>(a.A);
+  p.B = static_cast<const bf16_t*>(a.B);
+  p.C = static_cast<bf16_t*>(a.C);
+  p.N = a.N; p.K = a.K; p.Cin = a.Cin;
+  p.Hin = a.Hin; p.Win = a.Win; p.Hout = a.Hout; p.Wout = a.Wout; p.stride = 2;
+  p.mc = a.M;
+  p.M = 4 * a.M;  // the launcher pads each class to whole tiles
+  p.a_rows = a.M;
+  p.acc = a.acc;
+  p.ex = static_cast<const bf16_t*>(a.ex); p.emean = a.emean; p.ecoef = a.ecoef;
+  int cfg = igemm_pick(4 * a.M, a.N, a.K);
+  if (cfg == 4) cfg = 1;  // the three-stage loop has no G_DGRAD2 variant
+  return igemm(p, a.epi, G_DGRAD2, cfg, s);
+}
+
 int conv1x1_wgrad_splits(int M, int N, int K) {
   const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
   const int tiles = (N / tn) * (K / tk);

@@ -33,8 +33,9 @@ typedef __attribute__((ext_vector_type(2))) float f2_t;
 constexpr int kRep = 32;  // replica count of the BN workspace (== bn_act.hip kReplicas)
 
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
-// A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s)
-enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2 };
+// A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s) |
+// data gradient of a stride-2 3x3 pad-1 conv as four sub-pixel class GEMMs (csrc/igemm.hip)
+enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2, G_DGRAD2 = 3 };
 
 struct GemmParams {
   const bf16_t* A;
@@ -60,6 +61,11 @@ struct GemmParams {
   const float* emean2;
   float* acc2;          // its replicas [kRep][2N]
   int price_drop;       // timing-only builds (KDL_IGEMM_PRICE): bit 0 drops A's loads, bit 1 B's
+  // G_DGRAD2: A = dy [Nb, Hin, Win, Cin] (Hin x Win = each class's pixel grid),
+  // C = dx [Nb, Hout = 2 Hin, Wout = 2 Win, N]; class c = 2 py + px owns the
+  // dx pixels (2i + py, 2j + px).  mc = Nb Hin Win rows per class, padded to
+  // mc_pad (a multiple of BM, set by the launcher); M = 4 mc_pad.
+  int mc, mc_pad;
 };
 
 // csrc/wgrad_dma.hip: weight gradient on the LDS-DMA pipeline into fp32
@@ -141,7 +147,7 @@ __device__ __forceinline__ void acc_to_lds(const f32x16_t (&acc)[TN][TM], bf16_t
       }
 }
 
-template <int BM, int BN, int NT, int EPI>
+template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE>
 struct Epilogue {
   static constexpr int LDC = BN + 8;
   static constexpr int CPR = BN / 8;           // 16-B chunks per output row
@@ -170,12 +176,26 @@ struct Epilogue {
     for (int q = 0; q < 4; ++q) { s1[q] = f2_t{0.f, 0.f}; s2[q] = s1[q]; s3[q] = s1[q]; }
   }
 
+  // output row of GEMM row m (-1: padding row past M / past a class's rows)
+  __device__ __forceinline__ int row_of(const GemmParams& p, int m) const {
+    if constexpr (GATHER == G_DGRAD2) {
+      const int cls = m / p.mc_pad, r = m - cls * p.mc_pad;
+      if (r >= p.mc) return -1;
+      const int hw = p.Hin * p.Win;
+      const int nimg = r / hw, rem = r - nimg * hw;
+      const int i = rem / p.Win, j = rem - i * p.Win;
+      return (nimg * p.Hout + 2 * i + (cls >> 1)) * p.Wout + 2 * j + (cls & 1);
+    } else {
+      return m < p.M ? m : -1;
+    }
+  }
+
   // row-side operands (BN input x, d(identity), mask bits) of rows g0.. of tile tm
   __device__ __forceinline__ void prefetch(const GemmParams& p, int tm, int g0) {
 #pragma unroll
     for (int i = 0; i < PG; ++i) {
-      const int m = tm * BM + (g0 + i) * RPP + er0;
-      const bool ok = m < p.M;
+      const int m = row_of(p, tm * BM + (g0 + i) * RPP + er0);
+      const bool ok = m >= 0;
       const int64_t go = static_cast<int64_t>(ok ? m : 0) * p.N + ch0;
       if constexpr (LX) pxv[i] = ok ? ld16(p.ex + go) : make_uint4(0, 0, 0, 0);
       if constexpr (EPI == EPI_RESBITS) {
@@ -248,8 +268,8 @@ struct Epilogue {
 #pragma unroll
       for (int i = 0; i < PG; ++i) {
         const int row = (g0 + i) * RPP + er0;
-        const int m = tm * BM + row;
-        if (m >= p.M) continue;
+        const int m = row_of(p, tm * BM + row);
+        if (m < 0) continue;
         const uint4 raw = *reinterpret_cast<const uint4*>(&Cs[row * LDC + ec * 8]);
         const int64_t go = static_cast<int64_t>(m) * N + ch0;
         uint4 out = raw;  // PLAIN / STATS store the tile as it is

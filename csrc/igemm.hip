@@ -4,7 +4,13 @@
 //   with the fused ResNet epilogues of csrc/gemm_epi.h.
 //   A rows: dense | stride-s 1x1 gather | 3x3 pad-1 implicit GEMM (K = 9 Cin,
 //   one tap per 64-deep K-step; padding taps are buffer-OOB loads, which the
-//   hardware returns as zeros).
+//   hardware returns as zeros) | stride-2 3x3 data gradient (G_DGRAD2): dx
+//   pixel (2i + py, 2j + px) only sees the taps with r = py ? {0, 2} : {1}
+//   and s = px ? {0, 2} : {1}, reading dy at (i + [r == 0], j + [s == 0]);
+//   the four (py, px) classes are four GEMMs of 1, 2, 2, 4 taps over the
+//   dy-sized pixel grid, run as consecutive M-tile ranges of one launch with
+//   the weights regrouped class-major (no zero taps, no zero-filled output;
+//   the epilogue scatters rows to their dx pixels).
 //
 // Why a second main loop (csrc/conv1x1.hip keeps the register-staged one for
 // short K and for the BN+ReLU prologue): the register-staged loop spends
@@ -99,7 +105,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   constexpr int WTM = BM / WM, WTN = BN / WN;
   static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile = whole 32x32 MFMA blocks");
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  using Epi = Epilogue<BM, BN, NT, EPI>;
+  using Epi = Epilogue<BM, BN, NT, EPI, GATHER>;
+  constexpr bool TAPS = GATHER == G_CONV3 || GATHER == G_DGRAD2;
   constexpr int LDC = Epi::LDC;
   constexpr int LDS_BYTES = cmax<cmax<STAGES * STAGE, BM * LDC * 2>::v, Epi::kScratchBytes>::v;
   // ONE __shared__ object (a second one makes hipcc drain vmcnt before ds_reads)
@@ -113,12 +120,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   const int gm = q / tiles_n;
   const int n0 = tile_n * BN;
   const int K = p.K, M = p.M;
-  const int nk = K / IBK;
+  int nk = K / IBK;
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
   const int fr = lane & 31, fh = lane >> 5;
 
   // buffer resources (wave-uniform: built from kernel arguments only)
-  const int lda = GATHER == G_CONV3 ? p.Cin : K;
+  const int lda = TAPS ? p.Cin : K;
   // (a zero-record descriptor drops that operand's loads: KDL_IGEMM_PRICE timing builds)
   const int bytesA = (p.price_drop & 1) ? 0 : static_cast<int>(p.a_rows * lda * 2);
   const int bytesB = (p.price_drop & 2) ? 0 : static_cast<int>(static_cast<int64_t>(p.N) * K * 2);
@@ -140,7 +147,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   // and the logical 16-B chunk this lane fetches (source-side swizzle)
   const int lrow = lane >> 3;
   uint32_t voff[IPW];
-  int crow[IPW];    // conv3: image base row (n * Hin * Win) or -1 for rows >= M
+  int crow[IPW];    // conv3 / dgrad2: image base row (n * Hin * Win) or -1 for rows >= M
+  // G_DGRAD2 (per tile, wave-uniform): sub-pixel class (py, px), its taps per
+  // row-of-taps (ns) and its first K column in the class-major weight matrix
+  int py = 0, px = 0, ns = 1, koff = 0;
+  (void)py; (void)px; (void)ns; (void)koff;
   int cih[IPW], ciw[IPW];
   (void)crow; (void)cih; (void)ciw;
 #pragma unroll
@@ -161,7 +172,23 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
         const int r = 8 * g + lrow;
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         const int m = tm * BM + r;
-        if constexpr (GATHER == G_CONV3) {
+        if constexpr (GATHER == G_DGRAD2) {
+          const int cls = tm / (p.mc_pad / BM);
+          const int mc = m - cls * p.mc_pad;  // row within the class
+          if (mc < p.mc) {
+            const int hw = p.Hin * p.Win;
+            const int nimg = mc / hw, rem = mc - nimg * hw;
+            const int oi = rem / p.Win;
+            crow[i] = nimg * hw;
+            cih[i] = oi;
+            ciw[i] = rem - oi * p.Win;
+          } else {
+            crow[i] = -1;
+            cih[i] = 0;
+            ciw[i] = 0;
+          }
+          voff[i] = static_cast<uint32_t>(8 * c * 2);
+        } else if constexpr (GATHER == G_CONV3) {
           if (m < M) {
             const int hw = p.Hout * p.Wout;
             const int nimg = m / hw, rem = m - nimg * hw;
@@ -194,7 +221,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     char* base = lds + stage * STAGE;
     int tap = 0, kc0 = k0, r3 = 0, q3 = 0;
     (void)tap; (void)r3; (void)q3;
-    if constexpr (GATHER == G_CONV3) {
+    if constexpr (GATHER == G_DGRAD2) {
+      // class tap (ri, si): dy pixel offset (di, dj) = (py && ri == 0, px && si == 0)
+      tap = k0 / p.Cin;
+      kc0 = k0 - tap * p.Cin;
+      const int ri = tap / ns, si = tap - ri * ns;
+      r3 = (py && ri == 0) ? 1 : 0;
+      q3 = (px && si == 0) ? 1 : 0;
+    } else if constexpr (GATHER == G_CONV3) {
       tap = k0 / p.Cin;  // a 64-deep K-step never straddles taps (Cin % 64 == 0)
       kc0 = k0 - tap * p.Cin;
       r3 = tap / 3;
@@ -205,7 +239,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
       const int g = wave * IPW + i;
       lds_void_t* dst = (lds_void_t*)(base + g * 1024);
       if (g < BM / 8) {
-        if constexpr (GATHER == G_CONV3) {
+        if constexpr (TAPS) {
           const int ih = cih[i] + r3, iw = ciw[i] + q3;
           const bool ok = crow[i] >= 0 && static_cast<unsigned>(ih) < static_cast<unsigned>(p.Hin) &&
                           static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win);
@@ -216,7 +250,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
           dma(true, dst, voff[i], k0 * 2);
         }
       } else {
-        dma(false, dst, voff[i], k0 * 2);
+        dma(false, dst, voff[i], (koff + k0) * 2);
       }
     }
   };
@@ -231,6 +265,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   epi.init(t, n0);
 
   for (int tm = gm; tm < tiles_m; tm += GM) {
+    if constexpr (GATHER == G_DGRAD2) {
+      // class 0 (py, px) = (0, 0): 1 tap; 1 = (0, 1): 2; 2 = (1, 0): 2; 3 = (1, 1): 4
+      const int cls = tm / (p.mc_pad / BM);
+      py = cls >> 1;
+      px = cls & 1;
+      ns = px ? 2 : 1;
+      koff = (cls == 0 ? 0 : cls == 1 ? 1 : cls == 2 ? 3 : 5) * p.Cin;
+      nk = (py ? 2 : 1) * ns * (p.Cin / IBK);
+    }
     setup_rows(tm);
     f32x16_t acc[TN][TM];
 #pragma unroll
@@ -298,14 +341,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
 
 template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES, int BPC>
 hipError_t launch(const GemmParams& p, hipStream_t s) {
-  const int tiles_m = (p.M + BM - 1) / BM;
-  const int tiles_n = p.N / BN;
+  GemmParams q = p;
+  if constexpr (GATHER == G_DGRAD2) {  // four classes of ceil(mc / BM) tiles each
+    q.mc_pad = (p.mc + BM - 1) / BM * BM;
+    q.M = 4 * q.mc_pad;
+  }
+  const int tiles_m = (q.M + BM - 1) / BM;
+  const int tiles_n = q.N / BN;
   const int target = 256 * BPC;  // one round of resident blocks
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB, STAGES>), dim3(GM * tiles_n), dim3(64 * WM * WN),
-                     0, s, p, GM, tiles_m, tiles_n);
+                     0, s, q, GM, tiles_m, tiles_n);
   return hipGetLastError();
 }
 
@@ -333,6 +381,9 @@ hipError_t dispatch_gather(const GemmParams& p, int epi, int gather, hipStream_t
     case G_DENSE: return dispatch_epi<BM, BN, WM, WN, G_DENSE, MINB, STAGES, BPC>(p, epi, s);
     case G_STRIDED: return dispatch_epi<BM, BN, WM, WN, G_STRIDED, MINB, STAGES, BPC>(p, epi, s);
     case G_CONV3: return dispatch_epi<BM, BN, WM, WN, G_CONV3, MINB, STAGES, BPC>(p, epi, s);
+    case G_DGRAD2:
+      if constexpr (STAGES == 2) return dispatch_epi<BM, BN, WM, WN, G_DGRAD2, MINB, STAGES, BPC>(p, epi, s);
+      break;
   }
   return hipErrorInvalidValue;
 }
@@ -382,7 +433,7 @@ hipError_t igemm(const GemmParams& p_in, int epi, int gather, int cfg, hipStream
   GemmParams p = p_in;
   p.price_drop = price;
   if (p.K % IBK || p.M <= 0) return hipErrorInvalidValue;
-  const int lda = gather == G_CONV3 ? p.Cin : p.K;
+  const int lda = (gather == G_CONV3 || gather == G_DGRAD2) ? p.Cin : p.K;
   if (p.a_rows * lda * 2 >= (int64_t(1) << 31) || static_cast<int64_t>(p.N) * p.K * 2 >= (int64_t(1) << 31))
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   switch (cfg) {

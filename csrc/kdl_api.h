@@ -211,6 +211,12 @@ struct Conv1x1Args {
   int Cin;                           // ksize 3: input channels (the A row width)
 };
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
+// Data gradient of a 3x3 / pad 1 / stride 2 conv as four sub-pixel class GEMMs
+// on the LDS-DMA core (one launch): A = dy [Nb, Hin, Win, Cin], B = the weights
+// regrouped class-major [N][9 Cin] (conv3x3_s2_dgrad_weights), C = dx
+// [Nb, Hout = 2 Hin, Wout = 2 Win, N]; M = Nb * Hin * Win; epi PLAIN or MASKX
+// (ex / emean / ecoef / acc as conv1x1_gemm, indexed by dx rows).
+hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s);
 int conv1x1_wgrad_splits(int M, int N, int K);
 // dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace
 // (conv1x1_wgrad_splits(M, N, K) x [N, K] fp32, no initialisation needed); the

@@ -25,8 +25,9 @@ epilogue)::
     g2 = conv3 dgrad (dc3), masked by R'(B2(c2)) + B2 reduction sums   [GEMM epilogue]
     dW3 = sum dc3^T R(B2(c2))                          [GEMM, B2+R recomputed in the prologue]
     dc2 = B2 apply-backward(g2) ; dW2 [3x3 implicit GEMM, csrc/wgrad_dma.hip] ;
-          da1 [stride 1: implicit GEMM with bn1's mask + sums fused; stride 2: MIOpen]
-    dc1 = B1 backward(da1) (mask recomputed from c1)
+          da1 [implicit GEMM with bn1's mask + sums fused; stride 2: four sub-pixel
+          class GEMMs in one launch, kubedl_amd/ops/conv.py]
+    dc1 = B1 apply-backward(da1)
     g_prev = conv1 dgrad(dc1) + d(identity) (strided gather of the downsample dgrad),
              masked by the previous block's ReLU bits, + B3_prev (and Bd_prev)
              reduction sums                            [GEMM epilogue]
@@ -59,6 +60,7 @@ import torch
 import torch.nn.functional as F
 
 from kubedl_amd.models.resnet import BNAct, Bottleneck, ResNet
+from kubedl_amd.ops.conv import S2_TAPS, s2_dgrad_weights
 
 REP = 32  # BN workspace replicas (csrc/bn_act.hip kReplicas)
 
@@ -224,6 +226,17 @@ class HipKernels:
         out = _nhwc_empty(n, cin, h, w, g)
         self.ext.conv3x3_gemm(g, wd, out, n, h, w, cout, cin, 1, None, 2, None, self._bwd_acc(st1), x1,
                               st1.save_mean, self.fcoef(st1))
+        return out
+
+    def dgrad3x3s2_maskx(self, g, ball, x1, st1):
+        """Stride-2 3x3 dgrad as four sub-pixel class GEMMs in one launch
+        (csrc/igemm.hip G_DGRAD2; ball = class-major weights [Cin][9 Cout],
+        kubedl_amd/ops/conv.py) with bn1's mask and backward sums fused."""
+        n, cout, h, w = g.shape
+        cin = ball.shape[0]
+        out = _nhwc_empty(n, cin, 2 * h, 2 * w, g)
+        self.ext.conv3x3_s2_dgrad(g, ball, out, n, h, w, cout, cin, 2, self._bwd_acc(st1), x1, st1.save_mean,
+                                  self.fcoef(st1))
         return out
 
     def dgrad_plain(self, g, wt):
@@ -411,6 +424,14 @@ class TorchKernels:
         self._bsum(d, x1, st1)
         return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
 
+    def dgrad3x3s2_maskx(self, g, w, x1, st1):
+        d = _bfr(torch.nn.grad.conv2d_input(x1.shape, w.float(), g.float(), stride=2, padding=1))
+        sc, sf = st1.fcoef
+        mask = (x1.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
+        d = torch.where(mask, d, torch.zeros_like(d))
+        self._bsum(d, x1, st1)
+        return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
+
     def dgrad_plain(self, g, wt):
         return F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)).to(g.dtype).contiguous(
             memory_format=torch.channels_last)
@@ -479,6 +500,8 @@ class ResNetEngine:
         # per-layer A/B: profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl, r02_wgrad_dma_vs_reg_vs_miopen.jsonl)
         self.conv3_native = os.environ.get("KDL_CONV3", "kdl") != "miopen" and all(
             b.conv2.in_channels % 64 == 0 and b.conv2.out_channels % 64 == 0 for b in self.blocks)
+        # stride-2 3x3 data gradients as sub-pixel class GEMMs (KDL_DGRAD_S2=0: MIOpen)
+        self.dgrad_s2 = self.conv3_native and os.environ.get("KDL_DGRAD_S2", "1") == "1"
         # Weight gradients on a second HIP stream (default; KDL_WGRAD_STREAM=0 turns
         # it off -- 10.7k -> 11.3k img/s at batch 256, profiles/): a wgrad
         # depends only on its layer's output gradient and saved input, and nothing
@@ -502,7 +525,8 @@ class ResNetEngine:
             return
         convs = [c for b in self.blocks for c in (b.conv1, b.conv3, b.down_conv) if c is not None]
         c3s = [b.conv2 for b in self.blocks if b.conv2.stride[0] == 1]
-        ptrs = tuple(c.weight.data_ptr() for c in convs + c3s)
+        c3s2 = [b.conv2 for b in self.blocks if b.conv2.stride[0] == 2] if self.dgrad_s2 else []
+        ptrs = tuple(c.weight.data_ptr() for c in convs + c3s + c3s2)
         if ptrs != self._wt_ptrs:
             rows = []
             self._wt_buf = {}
@@ -527,9 +551,29 @@ class ResNetEngine:
                         for c0 in range(0, ci, 64):
                             rows.append((w.data_ptr() + tap * ci * esz, wd.data_ptr() + (8 - tap) * co * esz,
                                          co | (ci << 32), r0 | (c0 << 32), (9 * ci) | ((9 * co) << 32)))
+            for c in c3s2:  # class-major [Cin][9 Cout] of the stride-2 dgrad (ops/conv.py CLASS_TAPS)
+                w = c.weight
+                co, ci = w.shape[:2]
+                assert w.is_contiguous(memory_format=torch.channels_last)
+                ball = torch.empty(ci, 9 * co, dtype=w.dtype, device=w.device)
+                self._wt_buf[c] = ball
+                esz = w.element_size()
+                for pos, (r, s) in enumerate(S2_TAPS):
+                    for r0 in range(0, co, 64):
+                        for c0 in range(0, ci, 64):
+                            rows.append((w.data_ptr() + (3 * r + s) * ci * esz, ball.data_ptr() + pos * co * esz,
+                                         co | (ci << 32), r0 | (c0 << 32), (9 * ci) | ((9 * co) << 32)))
             self._wt_table = torch.tensor(rows, dtype=torch.int64).to(self.dev)
             self._wt_ptrs = ptrs
         self.K.ext.transpose_tiles(self._wt_table)
+
+    def _ball(self, conv):
+        """B operand of the stride-2 3x3 data gradient: the class-major
+        [Cin][9 Cout] regrouping (HIP path) or the weight itself (torch path)."""
+        if self.K.name != "hip":
+            return conv.weight
+        ball = self._wt_buf.get(conv)
+        return ball if ball is not None else s2_dgrad_weights(conv.weight)
 
     def _wd(self, conv):
         """Data-gradient weight of a stride-1 3x3 conv: flip(W, taps) with Cin/Cout swapped."""
@@ -687,6 +731,16 @@ class ResNetEngine:
                     self._wgrad3x3(dc2, a1, 1, blk.conv2.weight)
                 self.on_ready(blk.conv2.weight)
                 g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
+                n1, _, h1, w1 = c1.shape
+                K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
+                dc1, _ = K.bn_bwd_apply(g1, c1, st1)
+            elif self.dgrad_s2 and c1.shape[-2:] == (2 * dc2.shape[-2], 2 * dc2.shape[-1]):
+                # stride 2: four sub-pixel class GEMMs with bn1's mask + sums fused
+                # (no MIOpen, no zero-filled dx, no separate BN-backward reduce pass)
+                with self._on_side(dc2):
+                    self._wgrad3x3(dc2, a1, s, blk.conv2.weight)
+                self.on_ready(blk.conv2.weight)
+                g1 = K.dgrad3x3s2_maskx(dc2, self._ball(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
                 dc1, _ = K.bn_bwd_apply(g1, c1, st1)

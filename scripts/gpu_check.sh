@@ -50,6 +50,14 @@ if want bnsweep; then
     KDL_BN_MIN_ROWS=$mr run_step bench_minrows_$mr 600 python bench.py --steps 20 --warmup 8
   done
 fi
+if want envsweep; then  # SWEEPVAR=<env var> SWEEP="<values>": direct bench per value
+  for v in ${SWEEP}; do
+    export "${SWEEPVAR}=$v"
+    run_step "bench_${SWEEPVAR}_$v" 600 python bench.py --direct --gpus 1 --steps 20 --warmup 5
+    unset "${SWEEPVAR}"
+  done
+fi
+want dgrads2 && run_step time_dgrad_s2 300 python -u scripts/time_dgrad_s2.py
 want convgemm && run_step conv_vs_gemm 600 python scripts/conv_vs_gemm.py
 want ctr && run_step ctr 300 python -u -m kubedl_amd.workers.xdl_ctr
 want ctrprof && run_step ctr_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ctr_prof -o run -- python -u -m kubedl_amd.workers.xdl_ctr --steps 10 --warmup 3

@@ -60,13 +60,15 @@ def _compare(model, ref, loss, rloss, gtol, stat_tol=2e-2, cos_min=0.99):
     return worst
 
 
-@pytest.mark.parametrize("layers", [(1, 1, 1, 1), (2, 1, 1, 2)])
-def test_engine_torch_backend_matches_autograd_fp32(layers, monkeypatch):
-    """Exact data-flow check: fp32 storage, no bf16 rounding points."""
+@pytest.mark.parametrize("layers,width", [((1, 1, 1, 1), 8), ((2, 1, 1, 2), 8), ((1, 1, 1, 1), 64)])
+def test_engine_torch_backend_matches_autograd_fp32(layers, width, monkeypatch):
+    """Exact data-flow check: fp32 storage, no bf16 rounding points.  Width 64
+    puts every 3x3 on the native branches (stride-2 data gradient with the
+    mask + sums fused, as the HIP sub-pixel class GEMMs)."""
     import kubedl_amd.models.resnet_engine as RE
     monkeypatch.setattr(RE, "_bfr", lambda t: t.float())
     torch.manual_seed(0)
-    model = ResNet(layers, num_classes=10, width=8)
+    model = ResNet(layers, num_classes=10, width=width)
     with torch.no_grad():
         for m in model.modules():
             if hasattr(m, "running_mean"):
