@@ -141,9 +141,10 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
 std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
                                     const at::Tensor& running_mean, const at::Tensor& running_var,
                                     bool training, double momentum, double eps,
-                                    const c10::optional<at::Tensor>& acc) {
+                                    const c10::optional<at::Tensor>& acc, bool gemm_stats) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && is_nhwc_dense(x) && x.scalar_type() == at::kBFloat16,
               "bn_pool_fwd: x must be a channels_last bf16 NCHW tensor");
+  TORCH_CHECK(!gemm_stats || (acc.has_value() && acc->defined()), "bn_pool_fwd: gemm_stats reads the statistics from acc");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   TORCH_CHECK(C % 8 == 0, "bn_pool_fwd: C % 8 == 0");
   TORCH_CHECK(weight.numel() == C && bias.numel() == C && running_mean.numel() == C &&
@@ -163,7 +164,7 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
                                  save_invstd.data_ptr<float>(), a.data_ptr<float>(), static_cast<int>(N),
                                  static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                  dtype_code(weight), training, static_cast<float>(momentum),
-                                 static_cast<float>(eps), cur_stream()),
+                                 static_cast<float>(eps), cur_stream(), gemm_stats),
             "bn_pool_forward");
   return {y, save_mean, save_invstd, idx};
 }
@@ -723,6 +724,24 @@ void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv3x3_gemm");
 }
 
+// ResNet stem 7x7 / stride 2 / pad 3 conv, 224x224x3 -> 112x112x64 (csrc/stem.hip).
+void stem7x7_fwd(const at::Tensor& x, const at::Tensor& wp, at::Tensor y, const c10::optional<at::Tensor>& shift,
+                 const c10::optional<at::Tensor>& acc) {
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && x.size(2) == 224 && x.size(3) == 224 && is_nhwc_dense(x),
+              "stem7x7_fwd: x must be [Nb, 3, 224, 224] channels_last");
+  const int64_t Nb = x.size(0);
+  need_bf16(x, Nb * 224 * 224 * 3, "stem7x7_fwd x");
+  need_bf16(wp, 64 * 224, "stem7x7_fwd wp");
+  need_bf16(y, Nb * 112 * 112 * 64, "stem7x7_fwd y");
+  TORCH_CHECK(!opt_ptr(acc) || opt_ptr(shift), "stem7x7_fwd: statistics need a shift");
+  need_opt_f32(shift, 64, "shift");
+  need_opt_f32(acc, 32 * 2 * 64, "acc");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::stem7x7_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), static_cast<int>(Nb), opt_fptr(shift),
+                             opt_fptr(acc), cur_stream()),
+            "stem7x7_fwd");
+}
+
 // dx of a 3x3 / pad 1 / stride 2 conv: dy [Nb, Hd, Wd, Cd] (channels_last),
 // ball = the weights regrouped class-major [N][9 Cd] (kubedl_amd.ops.conv.s2_dgrad_weights),
 // dx [Nb, 2 Hd, 2 Wd, N]; epi 0 PLAIN, 2 MASKX (ex = that BN's input [Nb, 2Hd, 2Wd, N]).
@@ -1025,6 +1044,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
+  m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
+  m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");
   m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");

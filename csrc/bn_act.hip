@@ -954,7 +954,7 @@ hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, 
 hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gamma, const void* beta,
                            float* rm, float* rv, float* save_mean, float* save_invstd, float* ws,
                            int N, int H, int W, int C, int pdtype, bool training, float momentum,
-                           float eps, hipStream_t s) {
+                           float eps, hipStream_t s, bool gemm_stats) {
   if (N <= 0 || C <= 0 || C % 8 != 0) return hipErrorInvalidValue;
   constexpr int VEC = 8;
   const int64_t M = static_cast<int64_t>(N) * H * W;
@@ -966,7 +966,12 @@ hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gam
   const int fin_grid = (C + kBlock - 1) / kBlock;
   const bf16_t* xb = static_cast<const bf16_t*>(x);
   KDL_DISPATCH_PT(pdtype, {
-    if (training) {
+    if (training && gemm_stats) {  // sums around rm already in acc (conv epilogue, csrc/stem.hip)
+      hipLaunchKernelGGL((bn_fwd_finalize_kernel<bf16_t, PT>), dim3(fin_grid), dim3(kBlock), 0, s,
+                         static_cast<const bf16_t*>(nullptr), acc, C, static_cast<float>(M),
+                         static_cast<const PT*>(gamma), static_cast<const PT*>(beta), rm, rv, momentum, eps,
+                         save_mean, save_invstd, coef, rm);
+    } else if (training) {
       hipLaunchKernelGGL((bn_fwd_stats_kernel<bf16_t, VEC>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
                          xb, M, C, rp.tl.TPR, rp.tl.RPI, acc);
       hipLaunchKernelGGL((bn_fwd_finalize_kernel<bf16_t, PT>), dim3(fin_grid), dim3(kBlock), 0, s, xb,

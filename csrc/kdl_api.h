@@ -28,7 +28,8 @@ hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, 
 hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gamma, const void* beta,
                            float* rm, float* rv, float* save_mean, float* save_invstd, float* ws,
                            int N, int H, int W, int C, int pdtype, bool training, float momentum,
-                           float eps, hipStream_t s);
+                           float eps, hipStream_t s,
+                           bool gemm_stats = false);
 hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, const void* gamma,
                             const void* beta, const float* mean, const float* invstd, void* dx,
                             void* dgamma, void* dbeta, float* ws, int N, int H, int W, int C,
@@ -217,6 +218,13 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 // [Nb, Hout = 2 Hin, Wout = 2 Win, N]; M = Nb * Hin * Win; epi PLAIN or MASKX
 // (ex / emean / ecoef / acc as conv1x1_gemm, indexed by dx rows).
 hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s);
+// ResNet stem conv (csrc/stem.hip): x [Nb, 224, 224, 3] NHWC bf16, wp = the
+// weights as [64][224] bf16 (k = r * 32 + s * 4 + c, zero for s = 7 / c = 3),
+// y [Nb, 112, 112, 64] NHWC; acc != null: BN statistics around shift into the
+// forward replicas (STATS epilogue), else a plain store.
+hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const float* shift, float* acc,
+                       hipStream_t s);
+void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)
 int conv1x1_wgrad_splits(int M, int N, int K);
 // dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace
 // (conv1x1_wgrad_splits(M, N, K) x [N, K] fp32, no initialisation needed); the

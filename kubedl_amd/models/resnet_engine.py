@@ -60,7 +60,7 @@ import torch
 import torch.nn.functional as F
 
 from kubedl_amd.models.resnet import BNAct, Bottleneck, ResNet
-from kubedl_amd.ops.conv import S2_TAPS, s2_dgrad_weights
+from kubedl_amd.ops.conv import S2_TAPS, s2_dgrad_weights, stem_weights
 
 REP = 32  # BN workspace replicas (csrc/bn_act.hip kReplicas)
 
@@ -115,6 +115,7 @@ class HipKernels:
         self.ext = _ext.load()
         self.dev = dev
         self._dw32 = {}
+        self.stem_native = os.environ.get("KDL_STEM", "kdl") != "miopen"  # KDL_STEM=miopen: vendor stem conv
 
     def init_bn(self, st: BNState):
         st.ws = torch.zeros(self.ext.bn_workspace_floats(st.C), device=self.dev)
@@ -169,10 +170,21 @@ class HipKernels:
         self.ext.bn_stage_fwd_apply(x, st.ws, res, xd, std_.ws if std_ is not None else None, y, mb, M, st.C, relu)
         return y, mb
 
-    def stem_fwd(self, c0, st):
+    def stem_conv(self, x, w, st):
+        """7x7 / stride 2 stem conv: csrc/stem.hip (MFMA, the stem BN's statistics
+        in the epilogue) at the 224-px geometry it serves, else MIOpen.  Returns
+        (c0, statistics already in st's workspace)."""
+        if (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(w.shape) == (64, 3, 7, 7)
+                and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
+            c0 = _nhwc_empty(x.shape[0], 64, 112, 112, x)
+            self.ext.stem7x7_fwd(x, stem_weights(w), c0, st.mod.running_mean, self._fwd_acc(st))
+            return c0, True
+        return F.conv2d(x, w, stride=2, padding=3).contiguous(memory_format=torch.channels_last), False
+
+    def stem_fwd(self, c0, st, gemm_stats=False):
         m = st.mod
         y, mean, invstd, idx = self.ext.bn_pool_fwd(c0, m.weight, m.bias, m.running_mean, m.running_var, True,
-                                                    float(m.momentum), float(m.eps), st.ws)
+                                                    float(m.momentum), float(m.eps), st.ws, gemm_stats)
         st.save_mean, st.save_invstd = mean, invstd
         return y, idx
 
@@ -361,7 +373,11 @@ class TorchKernels:
             o = F.relu(o)
         return o.to(x.dtype).contiguous(memory_format=torch.channels_last), mask
 
-    def stem_fwd(self, c0, st):
+    @staticmethod
+    def stem_conv(x, w, st):
+        return F.conv2d(x, w, stride=2, padding=3).contiguous(memory_format=torch.channels_last), False
+
+    def stem_fwd(self, c0, st, gemm_stats=False):
         self.bn_stats(c0, st)
         self.bn_finalize(st, c0.numel() // st.C)
         a, _ = self.bn_apply(c0, st, relu=True)
@@ -609,8 +625,8 @@ class ResNetEngine:
     def forward(self, x: torch.Tensor):
         K, m = self.K, self.model
         st0 = self.bn[m.bn1]
-        c0 = F.conv2d(x, m.conv1.weight, stride=2, padding=3).contiguous(memory_format=torch.channels_last)
-        x1, idx = K.stem_fwd(c0, st0)
+        c0, gemm_stats = K.stem_conv(x, m.conv1.weight, st0)
+        x1, idx = K.stem_fwd(c0, st0, gemm_stats)
         saved = []
         cur = x1
         for blk in self.blocks:

@@ -106,7 +106,7 @@ class _BNPoolFn(torch.autograd.Function):
         ext = _ext.load()
         x = x.contiguous(memory_format=torch.channels_last)
         y, mean, invstd, idx = ext.bn_pool_fwd(x, weight, bias, running_mean, running_var, bool(training),
-                                               float(momentum), float(eps), ws)
+                                               float(momentum), float(eps), ws, False)
         ctx.save_for_backward(x, idx, weight, bias, mean, invstd)
         ctx.ws = ws
         ctx.training = training

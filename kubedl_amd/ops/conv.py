@@ -1,4 +1,6 @@
-"""Stride-2 3x3 data gradient as four sub-pixel class GEMMs.
+"""Weight layouts of the ResNet conv kernels that are not plain GEMMs.
+
+Stride-2 3x3 data gradient as four sub-pixel class GEMMs.
 
 For a 3x3 / pad 1 / stride 2 conv y = conv(x, w), dx pixel (2i + py, 2j + px)
 receives dy(oh, ow) * w[:, :, r, s] only where 2 oh - 1 + r = 2i + py, i.e.
@@ -60,3 +62,31 @@ def s2_dgrad_reference(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             acc = acc + torch.einsum("nohw,oi->nihw", src, w[:, :, r, s])
         dx[:, :, py::2, px::2] = acc
     return dx
+
+
+# ---------------------------------------------------------------------------- stem
+STEM_K = 224  # 7 r x 8 s x 4 c (s = 7 and c = 3 are zero padding)
+
+
+def stem_weights(w: torch.Tensor) -> torch.Tensor:
+    """[64, 3, 7, 7] stem weight -> [64, 224] bf16 in csrc/stem.hip's K order
+    k = r * 32 + s * 4 + c (so an 8-deep MFMA fragment is two horizontally
+    adjacent input pixels of 4 channels)."""
+    cout = w.shape[0]
+    wt = F.pad(w.permute(0, 2, 3, 1), (0, 1, 0, 1))  # [Cout, 7 r, 8 s, 4 c]
+    return wt.reshape(cout, STEM_K).to(torch.bfloat16).contiguous()
+
+
+def stem_reference(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """The stem kernel's GEMM in plain PyTorch: patches of the NHWC input in
+    the same K order times ``stem_weights`` (fp32) -> NCHW output."""
+    nb, _, h, wd = x.shape
+    oh, ow = (h + 6 - 7) // 2 + 1, (wd + 6 - 7) // 2 + 1
+    xp = F.pad(x.float().permute(0, 2, 3, 1), (0, 1, 3, 4, 3, 3))  # [Nb, H+6, W+7, 4]
+    cols = []
+    for r in range(7):
+        for s in range(8):
+            cols.append(xp[:, r:r + 2 * oh:2, s:s + 2 * ow:2, :])  # [Nb, oh, ow, 4]
+    patches = torch.stack(cols, dim=3).reshape(nb, oh, ow, STEM_K)
+    wt = F.pad(w.float().permute(0, 2, 3, 1), (0, 1, 0, 1)).reshape(w.shape[0], STEM_K)
+    return (patches @ wt.t()).permute(0, 3, 1, 2)

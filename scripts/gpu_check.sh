@@ -57,6 +57,7 @@ if want envsweep; then  # SWEEPVAR=<env var> SWEEP="<values>": direct bench per 
     unset "${SWEEPVAR}"
   done
 fi
+want stem && run_step time_stem 300 python -u scripts/time_stem.py
 want dgrads2 && run_step time_dgrad_s2 300 python -u scripts/time_dgrad_s2.py
 want convgemm && run_step conv_vs_gemm 600 python scripts/conv_vs_gemm.py
 want ctr && run_step ctr 300 python -u -m kubedl_amd.workers.xdl_ctr

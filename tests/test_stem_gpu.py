@@ -1,0 +1,65 @@
+"""ResNet stem conv on MFMA (csrc/stem.hip, 7x7 / stride 2 / pad 3, 224 -> 112,
+3 -> 64 channels) vs plain PyTorch fp32 conv2d: plain store, the BN-statistics
+epilogue, and the stem BN + ReLU + max-pool forward fed by those statistics
+(``bn_pool_fwd(gemm_stats=True)``) vs the same op computing its own."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from kubedl_amd.ops.conv import stem_weights
+
+pytestmark = pytest.mark.gpu
+
+REP = 32
+
+
+def _ext():
+    from kubedl_amd.ops import _ext
+    return _ext.load()
+
+
+def _inputs(nb, seed):
+    torch.manual_seed(seed)
+    x = torch.randn(nb, 224, 224, 3, device="cuda").bfloat16().permute(0, 3, 1, 2)  # NHWC storage
+    w = (torch.randn(64, 3, 7, 7, device="cuda") / 12).bfloat16().contiguous(memory_format=torch.channels_last)
+    return x, w
+
+
+@pytest.mark.parametrize("nb", [1, 3])
+def test_stem_plain_matches_fp32(nb):
+    ext = _ext()
+    x, w = _inputs(nb, 31)
+    y = torch.full((nb, 64, 112, 112), float("nan"), device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ext.stem7x7_fwd(x, stem_weights(w), y, None, None)
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=3)
+    assert torch.isfinite(y.float()).all()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_stem_stats_and_bn_pool():
+    ext = _ext()
+    nb = 2
+    x, w = _inputs(nb, 32)
+    y = torch.empty(nb, 64, 112, 112, device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    rm = torch.randn(64, device="cuda") * 0.1
+    rv = torch.rand(64, device="cuda") + 0.5
+    ws = torch.zeros(ext.bn_workspace_floats(64), device="cuda")
+    ext.stem7x7_fwd(x, stem_weights(w), y, rm, ws[:REP * 2 * 64])
+    yr = y.float().permute(0, 2, 3, 1).reshape(-1, 64) - rm
+    s = ws[:REP * 2 * 64].view(REP, 2, 64).sum(0)
+    torch.testing.assert_close(s[0], yr.sum(0), atol=0.5, rtol=1e-3)
+    torch.testing.assert_close(s[1], (yr * yr).sum(0), atol=0.5, rtol=1e-3)
+    # the BN + ReLU + max-pool forward from the epilogue's sums == computing its own
+    gamma = (torch.rand(64, device="cuda") + 0.5).bfloat16()
+    beta = (torch.randn(64, device="cuda") * 0.1).bfloat16()
+    rm2, rv2 = rm.clone(), rv.clone()
+    ws2 = torch.zeros_like(ws)
+    out = ext.bn_pool_fwd(y, gamma, beta, rm, rv, True, 0.1, 1e-5, ws, True)
+    ref = ext.bn_pool_fwd(y, gamma, beta, rm2, rv2, True, 0.1, 1e-5, ws2, False)
+    torch.testing.assert_close(out[1], ref[1], atol=1e-4, rtol=1e-4)  # mean
+    torch.testing.assert_close(out[2], ref[2], atol=1e-3, rtol=1e-3)  # invstd
+    torch.testing.assert_close(out[0].float(), ref[0].float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(rv, rv2, atol=1e-3, rtol=1e-3)
