@@ -742,6 +742,27 @@ void stem7x7_fwd(const at::Tensor& x, const at::Tensor& wp, at::Tensor y, const 
             "stem7x7_fwd");
 }
 
+// stem weight gradient -> dW [64][224] bf16 (kubedl_amd.ops.conv.stem_weights K order)
+void stem7x7_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor dw32, at::Tensor dW) {
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && x.size(2) == 224 && x.size(3) == 224 && is_nhwc_dense(x),
+              "stem7x7_wgrad: x must be [Nb, 3, 224, 224] channels_last");
+  const int64_t Nb = x.size(0);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == Nb && dy.size(1) == 64 && dy.size(2) == 112 && dy.size(3) == 112 &&
+                  is_nhwc_dense(dy),
+              "stem7x7_wgrad: dy must be [Nb, 64, 112, 112] channels_last");
+  need_bf16(x, Nb * 224 * 224 * 3, "stem7x7_wgrad x");
+  need_bf16(dy, Nb * 112 * 112 * 64, "stem7x7_wgrad dy");
+  need_bf16(dW, 64 * 224, "stem7x7_wgrad dW");
+  const int64_t slabs = kdl::stem7x7_wgrad_slabs(static_cast<int>(Nb));
+  TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
+                  dw32.numel() >= slabs * 64 * 224,
+              "stem7x7_wgrad: dw32 must hold stem7x7_wgrad_slabs(Nb) x 64 x 224 fp32");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::stem7x7_wgrad(dy.data_ptr(), x.data_ptr(), dw32.data_ptr<float>(), dW.data_ptr(),
+                               static_cast<int>(Nb), cur_stream()),
+            "stem7x7_wgrad");
+}
+
 // dx of a 3x3 / pad 1 / stride 2 conv: dy [Nb, Hd, Wd, Cd] (channels_last),
 // ball = the weights regrouped class-major [N][9 Cd] (kubedl_amd.ops.conv.s2_dgrad_weights),
 // dx [Nb, 2 Hd, 2 Wd, N]; epi 0 PLAIN, 2 MASKX (ex = that BN's input [Nb, 2Hd, 2Wd, N]).
@@ -1045,6 +1066,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
+  m.def("stem7x7_wgrad", &stem7x7_wgrad, "ResNet stem 7x7/s2/p3 conv weight gradient -> [64][224] bf16 (stem K order)");
+  m.def("stem7x7_wgrad_slabs", [](int64_t nb) { return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb)); },
+        "fp32 slab count of stem7x7_wgrad's workspace");
   m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");
   m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");

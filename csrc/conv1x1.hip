@@ -713,6 +713,13 @@ hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t
   return hipGetLastError();
 }
 
+}  // namespace
+
+hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s) {
+  return wgrad_reduce(dw32, nk, nsplit, scale, static_cast<bf16_t*>(dW), s);
+}
+
+namespace {
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
                       hipStream_t s) {

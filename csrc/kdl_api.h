@@ -224,6 +224,13 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s);
 // forward replicas (STATS epilogue), else a plain store.
 hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const float* shift, float* acc,
                        hipStream_t s);
+// stem weight gradient: dy [Nb, 112, 112, 64], x [Nb, 224, 224, 3] (NHWC bf16)
+// -> dW [64][224] bf16 in stem_weights' K order; dw32 = stem7x7_wgrad_slabs(Nb)
+// x [64][224] fp32 slabs (no initialisation needed)
+int stem7x7_wgrad_slabs(int Nb);
+hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s);
+// fixed-order sum of nsplit fp32 [nk] slabs into bf16 (scaled), csrc/conv1x1.hip
+hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s);
 void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)
 int conv1x1_wgrad_splits(int M, int N, int K);
 // dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace

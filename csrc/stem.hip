@@ -18,7 +18,8 @@
 //
 // Seven waves own one 32-pixel row block each (both 32-channel halves); the
 // weights [64][224] stay resident in LDS; the next tile's input is loaded into
-// registers under this tile's MFMAs and written to the halo after them.
+// registers under this tile's MFMAs and written to the halo after them
+// (HaloStager).
 // Epilogue: gemm_epi.h STATS (per-channel shifted sums into the BN workspace
 // replicas) -- the stem BN needs no statistics pass of its own.
 #include "common.h"
@@ -36,9 +37,41 @@ constexpr int kHR = 9;                   // input rows per tile (2 output rows, 
 constexpr int kHC = 232;                 // halo pixels per row: iw = -3 .. 228 (+3 offset)
 constexpr int kK = 224;                  // 7 r x 8 s x 4 c
 constexpr int kLDB = kK + 8;             // weight row stride (bf16): conflict-free fragment reads
-constexpr int kRowDw = kW * 3 / 2;       // dwords per input row (336)
-constexpr int kSlots = kHR * kRowDw;     // dwords per tile (3024)
-constexpr int kPf = (kSlots + kNT - 1) / kNT;  // per thread (7)
+
+// The 9 input rows of a tile -> LDS halo [9][kHC][4] bf16 (channel 3 and the
+// column padding stay zero): thread-pairs of pixels, 12 B per global load
+// (one dwordx3), two 8-B LDS writes; rows outside the image are written as
+// zeros.  load() runs under the previous tile's MFMAs, store() after them.
+struct HaloStager {
+  static constexpr int kPairs = kHR * (kW / 2);           // 1008 pixel pairs per tile
+  static constexpr int kIt = (kPairs + kNT - 1) / kNT;    // 3 per thread
+  uint3 v[kIt];
+
+  __device__ __forceinline__ void load(const bf16_t* x, int tm, int t) {
+    const int img = tm / (kOH / 2), ih0 = (tm - img * (kOH / 2)) * 4 - 3;
+#pragma unroll
+    for (int q = 0; q < kIt; ++q) {
+      const int j = t + q * kNT;
+      const int hr = j / (kW / 2), pr = j - hr * (kW / 2);
+      const int ih = ih0 + hr;
+      v[q] = make_uint3(0u, 0u, 0u);
+      if (j < kPairs && static_cast<unsigned>(ih) < static_cast<unsigned>(kH))
+        v[q] = *reinterpret_cast<const uint3*>(x + ((static_cast<int64_t>(img) * kH + ih) * kW + 2 * pr) * 3);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* Hs, int t) const {
+#pragma unroll
+    for (int q = 0; q < kIt; ++q) {
+      const int j = t + q * kNT;
+      if (j < kPairs) {
+        const int hr = j / (kW / 2), pr = j - hr * (kW / 2);
+        uint2* d = reinterpret_cast<uint2*>(Hs + (hr * kHC + 2 * pr + 3) * 4);
+        d[0] = make_uint2(v[q].x, v[q].y & 0xffffu);
+        d[1] = make_uint2((v[q].y >> 16) | (v[q].z << 16), v[q].z >> 16);
+      }
+    }
+  }
+};
 
 template <int EPI>
 __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tiles) {
@@ -56,7 +89,6 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int fr = lane & 31, fh = lane >> 5;
-  const uint16_t* X = reinterpret_cast<const uint16_t*>(p.A);
 
   // weights (row n: 224 bf16 = 28 uint4) and a zeroed halo (the column and
   // channel padding is never written again)
@@ -66,34 +98,7 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
   }
   for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
 
-  // input dwords of tile tm (rows outside the image read as zero)
-  uint32_t pf[kPf];
-  auto load = [&](int tm) {
-    const int img = tm / (kOH / 2), ih0 = (tm - img * (kOH / 2)) * 4 - 3;
-#pragma unroll
-    for (int q = 0; q < kPf; ++q) {
-      const int j = t + q * kNT;
-      const int hr = j / kRowDw, wd = j - hr * kRowDw;
-      const int ih = ih0 + hr;
-      pf[q] = 0u;
-      if (j < kSlots && static_cast<unsigned>(ih) < static_cast<unsigned>(kH))
-        pf[q] = *reinterpret_cast<const uint32_t*>(X + (static_cast<int64_t>(img) * kH + ih) * (kW * 3) + 2 * wd);
-    }
-  };
-  auto store = [&]() {
-    uint16_t* H16 = reinterpret_cast<uint16_t*>(Hs);
-#pragma unroll
-    for (int q = 0; q < kPf; ++q) {
-      const int j = t + q * kNT;
-      if (j < kSlots) {
-        const int hr = j / kRowDw, wd = j - hr * kRowDw;
-        const int e0 = 2 * wd, e1 = e0 + 1;  // element = 3 * pixel + channel
-        const int p0 = e0 / 3, p1 = e1 / 3;
-        H16[(hr * kHC + p0 + 3) * 4 + (e0 - 3 * p0)] = static_cast<uint16_t>(pf[q] & 0xffffu);
-        H16[(hr * kHC + p1 + 3) * 4 + (e1 - 3 * p1)] = static_cast<uint16_t>(pf[q] >> 16);
-      }
-    }
-  };
+  HaloStager hs;
 
   // this lane's output pixel of the tile: m = wave * 32 + fr -> (row ohl, col ow);
   // K-step ks reads halo row 2 ohl + ks / 2, pixels 2 ow + s0, +1 (s0 = 4 (ks & 1) + 2 fh)
@@ -107,14 +112,14 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
 
   int tm = blockIdx.x;
   if (tm < tiles) {
-    load(tm);
-    store();
+    hs.load(p.A, tm, t);
+    hs.store(Hs, t);
   }
   __syncthreads();
   for (; tm < tiles; tm += gridDim.x) {
     const int next = tm + gridDim.x;
     const int drop = p.price_drop;  // timing-only breakdown (set_stem_drop): 1 MFMA, 2 epilogue, 4 input
-    if (next < tiles && !(drop & 4)) load(next);  // lands under the MFMAs
+    if (next < tiles && !(drop & 4)) hs.load(p.A, next, t);  // lands under the MFMAs
     f32x16_t acc[2][1];
     acc[0][0] = f32x16_t{};
     acc[1][0] = f32x16_t{};
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
       }
     }
     __syncthreads();  // every wave is done with this halo
-    if (next < tiles && !(drop & 4)) store();
+    if (next < tiles && !(drop & 4)) hs.store(Hs, t);
     epi.begin(p, tm);
     acc_to_lds<2, 1>(acc, Cs, LDC, wave * 32, 0, lane);
     __syncthreads();  // C tile and the next halo are complete
@@ -141,6 +146,131 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
 }
 
 int g_stem_drop = 0;
+
+// ---------------------------------------------------------------- weight gradient
+// dW[co][k] = sum_px dY[px][co] * P[px][k] over all 3.2 M output pixels, in
+// the forward's K order (k = r * 32 + s * 4 + c; the s = 7 / c = 3 columns are
+// computed and dropped).  Per 224-pixel tile: dY's 224 x 64 rows arrive by
+// LDS-DMA (double-buffered, the csrc/wgrad_dma.hip panel swizzle) and the
+// input rows by the forward's register-staged halo; both MFMA operands are
+// read pixel-major with ds_read_b64_tr_b16 (the reduction index is the pixel):
+// dY from its panel, P straight from the halo -- lane (row px, columns C..C+3)
+// reads halo pixel (2 ohl + r, 2 ow + s), one 8-B pixel of 4 channels, so no
+// patch matrix is ever built.  Wave w owns kernel row r = w (32 k) for both
+// 32-channel halves; the block's fp32 partial goes to its own slab, summed in
+// a fixed order by wgrad_slab_reduce (deterministic).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, 0, 0, 0);
+#endif
+}
+
+__device__ __forceinline__ v4s_t tr_read(const char* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(p));
+#else
+  return v4s_t{};
+#endif
+}
+
+__device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
+  const uint2 a = __builtin_bit_cast(uint2, lo), b = __builtin_bit_cast(uint2, hi);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+__global__ __launch_bounds__(kNT, 2) void stem_wgrad_kernel(const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ x, float* __restrict__ dw32,
+                                                             int tiles, int64_t dy_bytes) {
+  constexpr int G_BYTES = kBM * 128;  // 224 pixel rows x 64 channels
+  constexpr int H_BYTES = kHR * kHC * 8;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * G_BYTES + H_BYTES];
+  char* Gs = lds;
+  bf16_t* Hs = reinterpret_cast<bf16_t*>(lds + 2 * G_BYTES);
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
+
+  const __amdgpu_buffer_rsrc_t rG =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dy), (short)0, static_cast<int>(dy_bytes), 0x00020000);
+  // dY DMA: 28 1-KiB groups of 8 rows, 4 per wave; chunk c of row r lands at c ^ (((r >> 1) & 1) * 4)
+  auto issue_g = [&](int tm, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int g = wave * 4 + i;
+      const int r = 8 * g + (lane >> 3);
+      const int c = (lane & 7) ^ (((r >> 1) & 1) * 4);
+      dma16(rG, (lds_void_t*)(Gs + buf * G_BYTES + g * 1024),
+            static_cast<uint32_t>((static_cast<int64_t>(tm) * kBM + r) * 128 + 16 * c));
+    }
+  };
+
+  HaloStager hs;
+
+  // transposed-read lane roles (csrc/wgrad_dma.hip): rows lrow (+4) of each
+  // 16-row step, columns 16 (grp & 1) + 4 pp of a 32-column fragment
+  const int grp = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int lrow = 8 * (grp >> 1) + q;
+  const int swz = ((q >> 1) & 1) * 4;
+  int goff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int chunk = (32 * i + 16 * (grp & 1) + 4 * pp) >> 3;
+    goff[i] = lrow * 128 + 16 * (chunk ^ swz) + 8 * (pp & 1);
+  }
+  // P[px][32 w + 16 (grp & 1) + 4 pp ..] = halo pixel (2 ohl + w, 2 ow + 4 (grp & 1) + pp)
+  const char* pbase = reinterpret_cast<const char*>(Hs) + (wave * kHC + 4 * (grp & 1) + pp + 2 * lrow) * 8;
+
+  f32x16_t acc[2];
+  acc[0] = f32x16_t{};
+  acc[1] = f32x16_t{};
+
+  int tm = blockIdx.x, buf = 0;
+  if (tm < tiles) {
+    issue_g(tm, 0);
+    hs.load(x, tm, t);
+    hs.store(Hs, t);
+  }
+  for (; tm < tiles; tm += gridDim.x) {
+    const int next = tm + gridDim.x;
+    __syncthreads();  // dY tile landed (vmcnt 0), halo written, the other dY buffer is free
+    if (next < tiles) {
+      issue_g(next, buf ^ 1);
+      hs.load(x, next, t);
+    }
+    const char* G = Gs + buf * G_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < kBM / 16; ++ks) {
+      const int hi = ks >= 7 ? 1 : 0;  // second output row of the tile
+      const int poff = (2 * hi * kHC + 2 * (16 * ks - 112 * hi)) * 8;
+      const bf16x8_t pf8 = frag8(tr_read(pbase + poff), tr_read(pbase + poff + 64));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* b = G + goff[i] + ks * 16 * 128;
+        const bf16x8_t gf = frag8(tr_read(b), tr_read(b + 4 * 128));
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf, pf8, acc[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with this halo
+    if (next < tiles) hs.store(Hs, t);
+    buf ^= 1;
+  }
+  // D[co][k]: column k = 32 w + (lane & 31), rows co = 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  float* slab = dw32 + static_cast<int64_t>(blockIdx.x) * 64 * kK;
+  const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * fh;
+      __builtin_nontemporal_store(acc[i][r], slab + co * kK + 32 * wave + fr);
+    }
+}
 
 }  // namespace
 
@@ -167,6 +297,24 @@ hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const flo
     hipLaunchKernelGGL(stem_fwd_kernel<EPI_PLAIN>, dim3(grid), dim3(kNT), 0, s, p, tiles);
   }
   return hipGetLastError();
+}
+
+int stem7x7_wgrad_slabs(int Nb) {
+  const int tiles = Nb * (kOH / 2);
+  return tiles < 512 ? tiles : 512;
+}
+
+hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s) {
+  if (Nb <= 0) return hipErrorInvalidValue;
+  const int64_t dy_bytes = static_cast<int64_t>(Nb) * kOH * kOW * 64 * 2;
+  if (dy_bytes >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit buffer offsets
+  const int tiles = Nb * (kOH / 2);
+  const int grid = stem7x7_wgrad_slabs(Nb);
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(dy),
+                     static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s);
 }
 
 }  // namespace kdl

@@ -60,7 +60,7 @@ import torch
 import torch.nn.functional as F
 
 from kubedl_amd.models.resnet import BNAct, Bottleneck, ResNet
-from kubedl_amd.ops.conv import S2_TAPS, s2_dgrad_weights, stem_weights
+from kubedl_amd.ops.conv import S2_TAPS, s2_dgrad_weights, stem_grad_from_k, stem_weights
 
 REP = 32  # BN workspace replicas (csrc/bn_act.hip kReplicas)
 
@@ -302,6 +302,27 @@ class HipKernels:
             dw32 = self._dw32[key] = torch.empty(slabs * cout * 9 * cin, device=g.device)
         self.ext.conv3x3_wgrad(g, x, None, dw32, dW, 1.0, n, h, w, cin, cout, stride)
 
+    def stem_wgrad(self, dc0, x, dw):
+        """Stem conv weight gradient into ``dw`` ([64, 3, 7, 7]): csrc/stem.hip
+        (both operands read pixel-major from LDS, no patch matrix) where the
+        forward ran on it, else MIOpen."""
+        if (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(dw.shape) == (64, 3, 7, 7)
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and dc0.is_contiguous(memory_format=torch.channels_last)):
+            nb = x.shape[0]
+            key = ("stem", nb)
+            ws = self._dw32.get(key)
+            if ws is None:
+                ws = (torch.empty(self.ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device=x.device),
+                      torch.empty(64, 224, device=x.device, dtype=torch.bfloat16))
+                self._dw32[key] = ws
+            self.ext.stem7x7_wgrad(dc0, x, ws[0], ws[1])
+            dw.copy_(stem_grad_from_k(ws[1]))
+            return
+        _, dw0, _ = torch.ops.aten.convolution_backward(
+            dc0, x, dw, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False])
+        dw.copy_(dw0)
+
     def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
         m = st.mod
         dx, dg, db = self.ext.bn_pool_bwd(dp, idx, c0, m.weight, m.bias, st.save_mean, st.save_invstd, True, st.ws)
@@ -472,6 +493,10 @@ class TorchKernels:
 
     def wgrad3x3(self, g, x, stride, dW):
         dW.copy_(torch.nn.grad.conv2d_weight(x.float(), tuple(dW.shape), g.float(), stride=stride, padding=1))
+
+    @staticmethod
+    def stem_wgrad(dc0, x, dw):
+        dw.copy_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dc0.float(), stride=2, padding=3))
 
     def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
         sc, sf = st.fcoef
@@ -802,9 +827,7 @@ class ResNetEngine:
         st0 = self.bn[m.bn1]
         dc0 = K.stem_bwd(g, idx, c0, st0, *self._bn_grads(st0))
         self._bn_ready(st0)
-        _, dw0, _ = torch.ops.aten.convolution_backward(
-            dc0, x, m.conv1.weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False])
-        self._g(m.conv1.weight).copy_(dw0)
+        K.stem_wgrad(dc0, x, self._g(m.conv1.weight))
         if self.side is not None:  # the optimizer (and the next forward) read every weight gradient
             torch.cuda.current_stream(self.dev).wait_stream(self.side)
         self.on_ready(m.conv1.weight)

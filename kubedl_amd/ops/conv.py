@@ -90,3 +90,8 @@ def stem_reference(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     patches = torch.stack(cols, dim=3).reshape(nb, oh, ow, STEM_K)
     wt = F.pad(w.float().permute(0, 2, 3, 1), (0, 1, 0, 1)).reshape(w.shape[0], STEM_K)
     return (patches @ wt.t()).permute(0, 3, 1, 2)
+
+
+def stem_grad_from_k(dwk: torch.Tensor) -> torch.Tensor:
+    """[64, 224] (stem K order) -> [64, 3, 7, 7] (the s = 7 / c = 3 padding columns dropped)."""
+    return dwk.view(dwk.shape[0], 7, 8, 4)[:, :, :7, :3].permute(0, 3, 1, 2)

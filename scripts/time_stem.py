@@ -47,6 +47,12 @@ def main():
         "bn_pool_own_stats": timed(lambda: ext.bn_pool_fwd(y, g, b, rm, rv, True, 0.1, 1e-5, ws, False)),
         "bn_pool_gemm_stats": timed(lambda: ext.bn_pool_fwd(y, g, b, rm, rv, True, 0.1, 1e-5, ws, True)),
     }
+    dy = torch.randn(nb, 112, 112, 64, device=dev).bfloat16().permute(0, 3, 1, 2)
+    wsw = torch.empty(ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device=dev)
+    dwk = torch.empty(64, 224, device=dev, dtype=torch.bfloat16)
+    res["kdl_stem_wgrad"] = timed(lambda: ext.stem7x7_wgrad(dy, x, wsw, dwk))
+    res["miopen_stem_wgrad"] = timed(lambda: torch.ops.aten.convolution_backward(
+        dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]))
     for bits, name in ((1, "no_mfma"), (2, "no_epilogue"), (4, "no_input"), (3, "no_mfma_no_epi"),
                        (6, "mfma_only"), (5, "epilogue_only")):
         ext.set_stem_drop(bits)

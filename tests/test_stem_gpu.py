@@ -63,3 +63,24 @@ def test_stem_stats_and_bn_pool():
     torch.testing.assert_close(out[0].float(), ref[0].float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(rv, rv2, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("nb", [1, 3, 10])
+def test_stem_wgrad_matches_fp32(nb):
+    """Weight gradient (both operands read pixel-major from LDS, fp32 slabs,
+    fixed-order reduce) vs torch.nn.grad.conv2d_weight in fp32; nb = 3 and 10
+    leave a partial last round of tiles for some blocks."""
+    from kubedl_amd.ops.conv import stem_grad_from_k
+    ext = _ext()
+    x, _ = _inputs(nb, 33)
+    dy = torch.randn(nb, 112, 112, 64, device="cuda").bfloat16().permute(0, 3, 1, 2)
+    ws = torch.empty(ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device="cuda")
+    dwk = torch.empty(64, 224, device="cuda", dtype=torch.bfloat16)
+    ext.stem7x7_wgrad(dy, x, ws, dwk)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (64, 3, 7, 7), dy.float(), stride=2, padding=3)
+    got = stem_grad_from_k(dwk).float()
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(got, ref, atol=1e-2 * scale, rtol=1e-2)
+    again = torch.empty_like(dwk)
+    ext.stem7x7_wgrad(dy, x, ws, again)
+    assert torch.equal(again, dwk), "stem weight gradient must be deterministic"
