@@ -224,15 +224,20 @@ struct Epilogue {
     }
   }
 
-  // issue the first prefetch group before the accumulators go to LDS, so its
-  // HBM latency overlaps the LDS round trip
-  __device__ __forceinline__ void begin(const GemmParams& p, int tm) {
+  // issue the first prefetch group and this thread's per-channel epilogue
+  // coefficients before the accumulators go to LDS, so their latency overlaps
+  // the LDS round trip (a coefficient load issued in rows() stalls the whole
+  // epilogue on one dependent global load per tile)
+  // (reload = false: the caller loaded them once with coefs() and keeps them
+  // live across tiles)
+  __device__ __forceinline__ void begin(const GemmParams& p, int tm, bool reload = true) {
     if constexpr (LX || LR) prefetch(p, tm, 0);
+    if (reload) coefs(p);
   }
 
-  // the tile's rows, from Cs[BM][LDC] (after a barrier that follows acc_to_lds)
-  __device__ __forceinline__ void rows(const GemmParams& p, const bf16_t* Cs, int tm) {
-    f2_t ea[4], eb[4], em[4], em2[4];
+  f2_t ea[4], eb[4], em[4], em2[4];  // per-channel coefficients of this thread's 8 channels
+
+  __device__ __forceinline__ void coefs(const GemmParams& p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) { ea[q] = f2_t{0.f, 0.f}; eb[q] = ea[q]; em[q] = ea[q]; em2[q] = ea[q]; }
     auto ld2 = [](const float* src, int c) { return *reinterpret_cast<const f2_t*>(src + c); };
@@ -254,6 +259,11 @@ struct Epilogue {
         if (p.ex2) em2[q] = ld2(p.emean2, ch0 + 2 * q);
       }
     }
+  }
+
+  // the tile's rows, from Cs[BM][LDC] (after a barrier that follows acc_to_lds)
+  __device__ __forceinline__ void rows(const GemmParams& p, const bf16_t* Cs, int tm) {
+    const int N = p.N;
 #pragma unroll
     for (int g0 = 0; g0 < NP; g0 += PG) {
       uint4 cxv[PG], crv[PG], cx2[PG];

@@ -109,6 +109,7 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
 
   Epi epi;
   epi.init(t, 0);
+  epi.coefs(p);  // 8 channels per thread, the same for every tile
 
   int tm = blockIdx.x;
   if (tm < tiles) {
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tile
     }
     __syncthreads();  // every wave is done with this halo
     if (next < tiles && !(drop & 4)) hs.store(Hs, t);
-    epi.begin(p, tm);
+    epi.begin(p, tm, false);
     acc_to_lds<2, 1>(acc, Cs, LDC, wave * 32, 0, lane);
     __syncthreads();  // C tile and the next halo are complete
     if (!(drop & 2)) epi.rows(p, Cs, tm);
