@@ -141,7 +141,7 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& dy, const at::Tensor& x,
 std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
                                     const at::Tensor& running_mean, const at::Tensor& running_var,
                                     bool training, double momentum, double eps,
-                                    const c10::optional<at::Tensor>& acc, bool gemm_stats) {
+                                    const c10::optional<at::Tensor>& acc, bool gemm_stats, bool want_xam) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && is_nhwc_dense(x) && x.scalar_type() == at::kBFloat16,
               "bn_pool_fwd: x must be a channels_last bf16 NCHW tensor");
   TORCH_CHECK(!gemm_stats || (acc.has_value() && acc->defined()), "bn_pool_fwd: gemm_stats reads the statistics from acc");
@@ -158,21 +158,23 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& weigh
   auto save_mean = at::empty({C}, fopt);
   auto save_invstd = at::empty({C}, fopt);
   at::Tensor a = get_acc(acc, C, x);
+  auto xam = want_xam ? at::empty_like(y) : at::Tensor();
   check_hip(kdl::bn_pool_forward(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), weight.data_ptr(),
                                  bias.data_ptr(), running_mean.data_ptr<float>(),
                                  running_var.data_ptr<float>(), save_mean.data_ptr<float>(),
                                  save_invstd.data_ptr<float>(), a.data_ptr<float>(), static_cast<int>(N),
                                  static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                                  dtype_code(weight), training, static_cast<float>(momentum),
-                                 static_cast<float>(eps), cur_stream(), gemm_stats),
+                                 static_cast<float>(eps), cur_stream(), gemm_stats,
+                                 want_xam ? xam.data_ptr() : nullptr),
             "bn_pool_forward");
-  return {y, save_mean, save_invstd, idx};
+  return {y, save_mean, save_invstd, idx, xam};
 }
 
 std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dyp, const at::Tensor& idx, const at::Tensor& x,
                                     const at::Tensor& weight, const at::Tensor& bias, const at::Tensor& mean,
                                     const at::Tensor& invstd, bool training,
-                                    const c10::optional<at::Tensor>& acc) {
+                                    const c10::optional<at::Tensor>& acc, bool with_dx) {
   TORCH_CHECK(is_nhwc_dense(x) && is_nhwc_dense(dyp) && dyp.scalar_type() == at::kBFloat16 &&
                   x.scalar_type() == at::kBFloat16,
               "bn_pool_bwd: channels_last bf16 tensors");
@@ -183,15 +185,15 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& dyp, const at::Tensor& idx
   TORCH_CHECK(idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.numel() == N * PH * PW * C,
               "bn_pool_bwd: idx");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  auto dx = at::empty_like(x);
+  auto dx = with_dx ? at::empty_like(x) : at::Tensor();
   auto dgamma = at::empty_like(weight);
   auto dbeta = at::empty_like(weight);
   at::Tensor a = get_acc(acc, C, x);
   check_hip(kdl::bn_pool_backward(dyp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), weight.data_ptr(),
                                   bias.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                                  dx.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), a.data_ptr<float>(),
-                                  static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
-                                  static_cast<int>(C), dtype_code(weight), training, cur_stream()),
+                                  with_dx ? dx.data_ptr() : nullptr, dgamma.data_ptr(), dbeta.data_ptr(),
+                                  a.data_ptr<float>(), static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
+                                  static_cast<int>(C), dtype_code(weight), training, cur_stream(), with_dx),
             "bn_pool_backward");
   return {dx, dgamma, dbeta};
 }
@@ -763,6 +765,39 @@ void stem7x7_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor dw32, a
             "stem7x7_wgrad");
 }
 
+// stem weight gradient with the stem BN + ReLU + max-pool backward folded in
+// (after bn_pool_bwd(..., with_dx = false) filled the workspace's coefficients)
+void stem7x7_wgrad_bn(const at::Tensor& c0, const at::Tensor& dp, const at::Tensor& idx, const at::Tensor& ws,
+                      const at::Tensor& x, at::Tensor dw32, at::Tensor dW) {
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && x.size(2) == 224 && x.size(3) == 224 && is_nhwc_dense(x),
+              "stem7x7_wgrad_bn: x must be [Nb, 3, 224, 224] channels_last");
+  const int64_t Nb = x.size(0);
+  TORCH_CHECK(c0.dim() == 4 && c0.size(0) == Nb && c0.size(1) == 64 && c0.size(2) == 112 && c0.size(3) == 112 &&
+                  is_nhwc_dense(c0),
+              "stem7x7_wgrad_bn: c0 must be [Nb, 64, 112, 112] channels_last");
+  TORCH_CHECK(dp.dim() == 4 && dp.size(0) == Nb && dp.size(1) == 64 && dp.size(2) == 56 && dp.size(3) == 56 &&
+                  is_nhwc_dense(dp),
+              "stem7x7_wgrad_bn: dp must be [Nb, 64, 56, 56] channels_last");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.numel() == Nb * 56 * 56 * 64,
+              "stem7x7_wgrad_bn: idx");
+  need_bf16(x, Nb * 224 * 224 * 3, "x");
+  need_bf16(c0, Nb * 112 * 112 * 64, "c0");
+  need_bf16(dp, Nb * 56 * 56 * 64, "dp");
+  need_bf16(dW, 64 * 224, "dW");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() &&
+                  ws.numel() >= kdl::bn_workspace_floats(64),
+              "stem7x7_wgrad_bn: ws must be the stem BN workspace");
+  const int64_t slabs = kdl::stem7x7_wgrad_slabs(static_cast<int>(Nb));
+  TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
+                  dw32.numel() >= slabs * 64 * 224,
+              "stem7x7_wgrad_bn: dw32 must hold stem7x7_wgrad_slabs(Nb) x 64 x 224 fp32");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::stem7x7_wgrad_bn(c0.data_ptr(), dp.data_ptr(), idx.data_ptr<uint8_t>(),
+                                  ws.data_ptr<float>() + 32 * 4 * 64 /* bn_coef_offset(64) */, x.data_ptr(), dw32.data_ptr<float>(),
+                                  dW.data_ptr(), static_cast<int>(Nb), cur_stream()),
+            "stem7x7_wgrad_bn");
+}
+
 // dx of a 3x3 / pad 1 / stride 2 conv: dy [Nb, Hd, Wd, Cd] (channels_last),
 // ball = the weights regrouped class-major [N][9 Cd] (kubedl_amd.ops.conv.s2_dgrad_weights),
 // dx [Nb, 2 Hd, 2 Wd, N]; epi 0 PLAIN, 2 MASKX (ex = that BN's input [Nb, 2Hd, 2Wd, N]).
@@ -1066,6 +1101,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
+  m.def("stem7x7_wgrad_bn", &stem7x7_wgrad_bn, "stem weight gradient with the stem BN+ReLU+max-pool backward folded in");
   m.def("stem7x7_wgrad", &stem7x7_wgrad, "ResNet stem 7x7/s2/p3 conv weight gradient -> [64][224] bf16 (stem K order)");
   m.def("stem7x7_wgrad_slabs", [](int64_t nb) { return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb)); },
         "fp32 slab count of stem7x7_wgrad's workspace");

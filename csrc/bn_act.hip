@@ -461,10 +461,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(
 __device__ __forceinline__ float bf16_round(float v) { return bf16_to_f32(f32_to_bf16(v)); }
 
 template <int VEC>
+// xam (optional): the BN input x at each window's argmax -- the backward's
+// BN sums then run over the pooled cells (dp * mask(xam), dp * mask * (xam -
+// mean)) instead of gathering every full-resolution pixel's windows.
 __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(
     const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
     const float* __restrict__ coef, int64_t MP, int C, int H, int W, int PH, int PW, int TPR,
-    int RPI) {
+    int RPI, bf16_t* __restrict__ xam) {
   const int t = threadIdx.x;
   const int lc = t % TPR, r0 = t / TPR;
   const int cg = blockIdx.y * TPR + lc;
@@ -475,13 +478,16 @@ __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(
   for (int i = 0; i < VEC; ++i) { sc[i] = coef[c0 + i]; sf[i] = coef[C + c0 + i]; }
   const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
   for (int64_t p = static_cast<int64_t>(blockIdx.x) * RPI + r0; p < MP; p += step) {
-    const int64_t n = p / (static_cast<int64_t>(PH) * PW);
-    const int rem = static_cast<int>(p - n * PH * PW);
-    const int ph = rem / PW, pw = rem % PW;
-    float best[VEC];
+    // 32-bit index math (host guarantees MP < 2^31): a 64-bit division per
+    // element made these passes VALU-bound
+    const uint32_t pu = static_cast<uint32_t>(p), phw = static_cast<uint32_t>(PH * PW);
+    const int n = static_cast<int>(pu / phw);
+    const int rem = static_cast<int>(pu - static_cast<uint32_t>(n) * phw);
+    const int ph = rem / PW, pw = rem - (rem / PW) * PW;
+    float best[VEC], bx[VEC];
     uint32_t bi[VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) { best[i] = -__builtin_inff(); bi[i] = 0; }
+    for (int i = 0; i < VEC; ++i) { best[i] = -__builtin_inff(); bi[i] = 0; bx[i] = 0.f; }
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int ih = 2 * ph - 1 + kh;
@@ -491,16 +497,17 @@ __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(
         const int iw = 2 * pw - 1 + kw;
         if (iw < 0 || iw >= W) continue;
         float v[VEC];
-        VecIO<bf16_t, VEC>::load(x + ((n * H + ih) * W + iw) * C + c0, v);
+        VecIO<bf16_t, VEC>::load(x + static_cast<int64_t>((n * H + ih) * W + iw) * C + c0, v);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           float z = fmaf(v[i], sc[i], sf[i]);
           z = bf16_round(z > 0.f ? z : 0.f);
-          if (z > best[i]) { best[i] = z; bi[i] = kh * 3 + kw; }
+          if (z > best[i]) { best[i] = z; bi[i] = kh * 3 + kw; bx[i] = v[i]; }
         }
       }
     }
     VecIO<bf16_t, VEC>::store(y + p * C + c0, best);
+    if (xam) VecIO<bf16_t, VEC>::store(xam + p * C + c0, bx);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -520,7 +527,7 @@ __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(
 // gradients of the windows whose argmax is this pixel.
 template <int VEC>
 __device__ __forceinline__ void pool_grad_at(const bf16_t* __restrict__ dyp,
-                                             const uint8_t* __restrict__ idx, int64_t n, int h,
+                                             const uint8_t* __restrict__ idx, int n, int h,
                                              int w, int C, int c0, int PH, int PW, float (&g)[VEC]) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) g[i] = 0.f;
@@ -535,7 +542,7 @@ __device__ __forceinline__ void pool_grad_at(const bf16_t* __restrict__ dyp,
       const int kw = w + 1 - 2 * pw;
       if (pw < 0 || pw >= PW || kw > 2) continue;
       const uint32_t pos = kh * 3 + kw;
-      const int64_t p = (n * PH + ph) * PW + pw;
+      const int64_t p = static_cast<int64_t>((n * PH + ph) * PW + pw);
       uint8_t ib[VEC];
       if constexpr (VEC == 8) {
         const uint2 u = *reinterpret_cast<const uint2*>(idx + p * C + c0);
@@ -577,11 +584,13 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce_kernel(
     for (int i = 0; i < VEC; ++i) mu[i] = mean[c0 + i];
     mask_coeffs<PT, VEC>(gamma, beta, mean, invstd, c0, sc, sf);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
-      const int64_t n = r / (static_cast<int64_t>(H) * W);
-      const int rem = static_cast<int>(r - n * H * W);
+      const uint32_t ru = static_cast<uint32_t>(r), hw = static_cast<uint32_t>(H * W);
+      const int n = static_cast<int>(ru / hw);
+      const int rem = static_cast<int>(ru - static_cast<uint32_t>(n) * hw);
+      const int h = rem / W;
       float g[VEC], xv[VEC];
       VecIO<bf16_t, VEC>::load(x + r * C + c0, xv);
-      pool_grad_at<VEC>(dyp, idx, n, rem / W, rem % W, C, c0, PH, PW, g);
+      pool_grad_at<VEC>(dyp, idx, n, h, rem - h * W, C, c0, PH, PW, g);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         const float gi = fmaf(xv[i], sc[i], sf[i]) > 0.f ? g[i] : 0.f;
@@ -615,11 +624,13 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(
   mask_coeffs<PT, VEC>(gamma, beta, mean, invstd, c0, sc, sf);
   const int64_t step = static_cast<int64_t>(gridDim.x) * RPI;
   for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPI + r0; r < M; r += step) {
-    const int64_t n = r / (static_cast<int64_t>(H) * W);
-    const int rem = static_cast<int>(r - n * H * W);
+    const uint32_t ru = static_cast<uint32_t>(r), hw = static_cast<uint32_t>(H * W);
+    const int n = static_cast<int>(ru / hw);
+    const int rem = static_cast<int>(ru - static_cast<uint32_t>(n) * hw);
+    const int h = rem / W;
     float g[VEC], xv[VEC];
     VecIO<bf16_t, VEC>::load(x + r * C + c0, xv);
-    pool_grad_at<VEC>(dyp, idx, n, rem / W, rem % W, C, c0, PH, PW, g);
+    pool_grad_at<VEC>(dyp, idx, n, h, rem - h * W, C, c0, PH, PW, g);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       const float gi = fmaf(xv[i], sc[i], sf[i]) > 0.f ? g[i] : 0.f;
@@ -954,10 +965,11 @@ hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, 
 hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gamma, const void* beta,
                            float* rm, float* rv, float* save_mean, float* save_invstd, float* ws,
                            int N, int H, int W, int C, int pdtype, bool training, float momentum,
-                           float eps, hipStream_t s, bool gemm_stats) {
+                           float eps, hipStream_t s, bool gemm_stats, void* xam) {
   if (N <= 0 || C <= 0 || C % 8 != 0) return hipErrorInvalidValue;
   constexpr int VEC = 8;
   const int64_t M = static_cast<int64_t>(N) * H * W;
+  if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit pixel index math
   const int PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;  // k3 s2 p1
   const int64_t MP = static_cast<int64_t>(N) * PH * PW;
   ReducePlan rp = plan_reduce(M, C, VEC);
@@ -986,17 +998,19 @@ hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gam
   });
   dim3 grid(apply_gx(MP, rp.tl), rp.tl.gy);
   hipLaunchKernelGGL((bn_pool_fwd_kernel<VEC>), grid, dim3(kBlock), 0, s, xb,
-                     static_cast<bf16_t*>(y), idx, coef, MP, C, H, W, PH, PW, rp.tl.TPR, rp.tl.RPI);
+                     static_cast<bf16_t*>(y), idx, coef, MP, C, H, W, PH, PW, rp.tl.TPR, rp.tl.RPI,
+                     static_cast<bf16_t*>(xam));
   return hipGetLastError();
 }
 
 hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, const void* gamma,
                             const void* beta, const float* mean, const float* invstd, void* dx,
                             void* dgamma, void* dbeta, float* ws, int N, int H, int W, int C,
-                            int pdtype, bool training, hipStream_t s) {
+                            int pdtype, bool training, hipStream_t s, bool with_dx) {
   if (N <= 0 || C <= 0 || C % 8 != 0) return hipErrorInvalidValue;
   constexpr int VEC = 8;
   const int64_t M = static_cast<int64_t>(N) * H * W;
+  if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit pixel index math
   const int PH = (H - 1) / 2 + 1, PW = (W - 1) / 2 + 1;
   ReducePlan rp = plan_reduce(M, C, VEC);
   float* acc = ws_acc_bwd(ws, C);
@@ -1011,10 +1025,12 @@ hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, 
     hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0,
                        s, acc, C, static_cast<float>(M), g, mean, invstd, training,
                        static_cast<PT*>(dgamma), static_cast<PT*>(dbeta), coef);
-    dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
-    hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<PT, VEC>), grid, dim3(kBlock), 0, s, db, idx, xb, g, b,
-                       mean, invstd, coef, static_cast<bf16_t*>(dx), M, C, H, W, PH, PW, rp.tl.TPR,
-                       rp.tl.RPI);
+    if (with_dx) {  // else the consumer applies the coefficients itself (csrc/stem.hip)
+      dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
+      hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<PT, VEC>), grid, dim3(kBlock), 0, s, db, idx, xb, g, b,
+                         mean, invstd, coef, static_cast<bf16_t*>(dx), M, C, H, W, PH, PW, rp.tl.TPR,
+                         rp.tl.RPI);
+    }
   });
   return hipGetLastError();
 }

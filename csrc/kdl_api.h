@@ -29,11 +29,12 @@ hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gam
                            float* rm, float* rv, float* save_mean, float* save_invstd, float* ws,
                            int N, int H, int W, int C, int pdtype, bool training, float momentum,
                            float eps, hipStream_t s,
-                           bool gemm_stats = false);
+                           bool gemm_stats = false, void* xam = nullptr);
 hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, const void* gamma,
                             const void* beta, const float* mean, const float* invstd, void* dx,
                             void* dgamma, void* dbeta, float* ws, int N, int H, int W, int C,
-                            int pdtype, bool training, hipStream_t s);
+                            int pdtype, bool training, hipStream_t s,
+                            bool with_dx = true);
 
 // Staged BN entry points for the explicit ResNet engine (bf16 NHWC, C % 8 == 0).
 // Forward: stats (or a conv1x1 STATS epilogue) -> finalize (shift = the K the sums
@@ -229,6 +230,12 @@ hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const flo
 // x [64][224] fp32 slabs (no initialisation needed)
 int stem7x7_wgrad_slabs(int Nb);
 hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s);
+// the same with the stem BN + ReLU + max-pool backward folded in: dy is built
+// per tile from c0 [Nb, 112, 112, 64], the pooled gradient dp [Nb, 56, 56, 64],
+// its argmax bytes idx and coef5 = [5][64] (forward scale | shift, backward
+// k | c1 | c0 of the BN workspace, after bn_pool_backward(with_dx = false))
+hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, const float* coef5, const void* x,
+                            float* dw32, void* dW, int Nb, hipStream_t s);
 // fixed-order sum of nsplit fp32 [nk] slabs into bf16 (scaled), csrc/conv1x1.hip
 hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s);
 void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)

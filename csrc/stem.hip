@@ -74,7 +74,7 @@ struct HaloStager {
 };
 
 template <int EPI>
-__global__ __launch_bounds__(kNT, 2) void stem_fwd_kernel(GemmParams p, int tiles) {
+__global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tiles) {
   using Epi = Epilogue<kBM, 64, kNT, EPI>;
   constexpr int LDC = Epi::LDC;
   constexpr int B_BYTES = 64 * kLDB * 2;
@@ -184,21 +184,46 @@ __device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
   return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
 }
 
-__global__ __launch_bounds__(kNT, 2) void stem_wgrad_kernel(const bf16_t* __restrict__ dy,
+// FUSE: dY is not in memory -- each tile's 224 x 64 gradient rows are built
+// in LDS from the stem conv output c0, the pooled gradient and its argmax
+// bytes (max-pool backward as a gather over the <= 4 windows holding the
+// pixel), the ReLU mask recomputed from c0 and the BN backward coefficients:
+//   dY = k * [c0 * sc + sf > 0] * g + c1 * c0 + c0'
+// which deletes the stem's full-resolution BN-backward apply pass (read c0 +
+// write dY) and this kernel's re-read of dY.
+struct StemBnBwd {
+  const bf16_t* c0;       // [M][64] stem conv output
+  const bf16_t* dp;       // [Nb][56][56][64] pooled gradient
+  const uint8_t* idx;     // its argmax (kh * 3 + kw) per channel
+  const float* coef;      // [5][64]: forward scale | shift, backward k | c1 | c0
+};
+
+// (second launch bound = min waves per SIMD: 2 blocks of 7 waves need 4 -> <= 128 VGPRs)
+template <bool FUSE>
+__global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ x, float* __restrict__ dw32,
-                                                             int tiles, int64_t dy_bytes) {
+                                                             int tiles, int64_t dy_bytes, StemBnBwd bn) {
   constexpr int G_BYTES = kBM * 128;  // 224 pixel rows x 64 channels
   constexpr int H_BYTES = kHR * kHC * 8;
-  __shared__ __attribute__((aligned(1024))) char lds[2 * G_BYTES + H_BYTES];
+  constexpr int NG = FUSE ? 1 : 2;    // the fused tile is built in place, not DMA'd ahead
+  constexpr int P_BYTES = 2 * (kOW / 2) * 64 * 3;  // staged pooled rows: bf16 gradient + u8 argmax
+  __shared__ __attribute__((aligned(1024))) char lds[NG * G_BYTES + H_BYTES + (FUSE ? 5 * 64 * 4 + P_BYTES : 0)];
   char* Gs = lds;
-  bf16_t* Hs = reinterpret_cast<bf16_t*>(lds + 2 * G_BYTES);
+  bf16_t* Hs = reinterpret_cast<bf16_t*>(lds + NG * G_BYTES);
+  float* cf = reinterpret_cast<float*>(lds + NG * G_BYTES + H_BYTES);
+  (void)cf;
+  if constexpr (FUSE) {
+    for (int i = threadIdx.x; i < 5 * 64; i += kNT) cf[i] = bn.coef[i];
+  }
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
 
-  const __amdgpu_buffer_rsrc_t rG =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dy), (short)0, static_cast<int>(dy_bytes), 0x00020000);
+  // dY rows by LDS-DMA; fused: the c0 rows the tile's dY is built from (in place)
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(FUSE ? bn.c0 : dy), (short)0,
+      static_cast<int>(FUSE ? static_cast<int64_t>(tiles) * G_BYTES : dy_bytes), 0x00020000);
   // dY DMA: 28 1-KiB groups of 8 rows, 4 per wave; chunk c of row r lands at c ^ (((r >> 1) & 1) * 4)
   auto issue_g = [&](int tm, int buf) {
 #pragma unroll
@@ -212,6 +237,91 @@ __global__ __launch_bounds__(kNT, 2) void stem_wgrad_kernel(const bf16_t* __rest
   };
 
   HaloStager hs;
+
+  // FUSE: tile tm (output rows 2k, 2k + 1) only sees pooled rows k and k + 1
+  // (row 2k: window k; row 2k + 1: windows k and k + 1).  Their gradient and
+  // argmax bytes (2 x 56 x 64) are loaded coalesced under the previous tile's
+  // MFMAs and staged in LDS, so the per-pixel window gather reads LDS; the c0
+  // rows arrive by LDS-DMA into the dY tile itself and are overwritten in place.
+  constexpr int kPW = kOW / 2, kPH = kOH / 2;
+  constexpr int DP_CH = 2 * kPW * 8, IX_CH = 2 * kPW * 4;  // 16-B chunks: dp rows, idx rows
+  constexpr int PCH = (DP_CH + IX_CH + kNT - 1) / kNT;     // per thread (3)
+  char* Ps = lds + NG * G_BYTES + H_BYTES + 5 * 64 * 4;    // [2][56][64] bf16 dp | [2][56][64] u8 idx
+  uint4 ppf[FUSE ? PCH : 1];
+  (void)ppf; (void)Ps;
+  auto load_pool = [&](int tm) {
+    const int img = tm / kPH, k = tm - img * kPH;
+#pragma unroll
+    for (int q = 0; q < PCH; ++q) {
+      const int j = t + q * kNT;
+      ppf[q] = make_uint4(0u, 0u, 0u, 0u);
+      if (j < DP_CH) {
+        const int r = j / (kPW * 8), rem = j - r * (kPW * 8);
+        if (k + r < kPH)
+          ppf[q] = *reinterpret_cast<const uint4*>(bn.dp + ((static_cast<int64_t>(img) * kPH + k + r) * kPW) * 64 + 8 * rem);
+      } else if (j < DP_CH + IX_CH) {
+        const int jj = j - DP_CH;
+        const int r = jj / (kPW * 4), rem = jj - r * (kPW * 4);
+        if (k + r < kPH)
+          ppf[q] = *reinterpret_cast<const uint4*>(bn.idx + ((static_cast<int64_t>(img) * kPH + k + r) * kPW) * 64 + 16 * rem);
+      }
+    }
+  };
+  auto store_pool = [&]() {
+#pragma unroll
+    for (int q = 0; q < PCH; ++q) {
+      const int j = t + q * kNT;
+      if (j < DP_CH + IX_CH) reinterpret_cast<uint4*>(Ps)[j] = ppf[q];  // dp chunks, then idx chunks
+    }
+  };
+  auto build_g = [&](int tm) {
+    const int cgp = t & 7;
+    const int k = tm - (tm / kPH) * kPH;
+    const bf16_t* pdp = reinterpret_cast<const bf16_t*>(Ps);
+    const uint8_t* pix = reinterpret_cast<const uint8_t*>(Ps + DP_CH * 16);
+#pragma unroll 1
+    for (int q = 0; q < kBM * 8 / kNT; ++q) {
+      const int px = (t + q * kNT) >> 3;
+      const int ohl = px >= kOW ? 1 : 0;
+      const int ow = px - kOW * ohl;
+      uint4* slot = reinterpret_cast<uint4*>(Gs + px * 128 + 16 * (cgp ^ (((px >> 1) & 1) * 4)));
+      float xv[8], g[8];
+      unpack8(*slot, xv);  // the DMA'd c0 row chunk, replaced by dY below
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = 0.f;
+      // output row 2k + ohl: windows (staged row r, kh) = (0, 1) for ohl = 0;
+      // (1, 0) and (0, 2) for ohl = 1
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const int r = ohl ? 1 - dh : 0, kh = ohl ? (dh ? 2 : 0) : 1;
+        if ((!ohl && dh) || k + r >= kPH) continue;
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const int pw = (ow + 1) / 2 - dw, kw = ow + 1 - 2 * pw;
+          if (pw < 0 || pw >= kPW || kw > 2) continue;
+          const int cell = (r * kPW + pw) * 64 + 8 * cgp;
+          const uint2 ib = *reinterpret_cast<const uint2*>(pix + cell);
+          float d[8];
+          unpack8(*reinterpret_cast<const uint4*>(pdp + cell), d);
+          const uint32_t pos = kh * 3 + kw;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t b = ((i < 4 ? ib.x : ib.y) >> (8 * (i & 3))) & 0xffu;
+            g[i] += b == pos ? d[i] : 0.f;
+          }
+        }
+      }
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = 8 * cgp + i;
+        const bool on = fmaf(xv[i], cf[c], cf[64 + c]) > 0.f;
+        o[i] = fmaf(cf[128 + c], on ? g[i] : 0.f, fmaf(cf[192 + c], xv[i], cf[256 + c]));
+      }
+      *slot = pack8(o);
+    }
+  };
+  (void)build_g; (void)load_pool; (void)store_pool;
 
   // transposed-read lane roles (csrc/wgrad_dma.hip): rows lrow (+4) of each
   // 16-row step, columns 16 (grp & 1) + 4 pp of a 32-column fragment
@@ -232,16 +342,26 @@ __global__ __launch_bounds__(kNT, 2) void stem_wgrad_kernel(const bf16_t* __rest
   acc[1] = f32x16_t{};
 
   int tm = blockIdx.x, buf = 0;
+  if constexpr (FUSE) __syncthreads();  // coefficients in LDS
   if (tm < tiles) {
-    issue_g(tm, 0);
+    if constexpr (FUSE) {
+      issue_g(tm, 0);
+      load_pool(tm);
+      store_pool();
+      __syncthreads();  // c0 rows (vmcnt 0) and pooled rows in LDS
+      build_g(tm);
+    } else {
+      issue_g(tm, 0);
+    }
     hs.load(x, tm, t);
     hs.store(Hs, t);
   }
   for (; tm < tiles; tm += gridDim.x) {
     const int next = tm + gridDim.x;
-    __syncthreads();  // dY tile landed (vmcnt 0), halo written, the other dY buffer is free
+    __syncthreads();  // dY tile landed (vmcnt 0) / built, halo written, the other dY buffer is free
     if (next < tiles) {
-      issue_g(next, buf ^ 1);
+      if constexpr (FUSE) load_pool(next);
+      else issue_g(next, buf ^ 1);
       hs.load(x, next, t);
     }
     const char* G = Gs + buf * G_BYTES;
@@ -257,9 +377,17 @@ __global__ __launch_bounds__(kNT, 2) void stem_wgrad_kernel(const bf16_t* __rest
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf, pf8, acc[i], 0, 0, 0);
       }
     }
-    __syncthreads();  // every wave is done with this halo
-    if (next < tiles) hs.store(Hs, t);
-    buf ^= 1;
+    __syncthreads();  // every wave is done with this halo (and, fused, this dY tile)
+    if (next < tiles) {
+      if constexpr (FUSE) issue_g(next, 0);  // this tile's dY has been consumed
+      hs.store(Hs, t);
+      if constexpr (FUSE) store_pool();
+    }
+    if constexpr (FUSE) {
+      __syncthreads();  // c0 rows landed (vmcnt 0), staged pooled rows visible
+      if (next < tiles) build_g(next);
+    }
+    if constexpr (!FUSE) buf ^= 1;
   }
   // D[co][k]: column k = 32 w + (lane & 31), rows co = 32 i + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   float* slab = dw32 + static_cast<int64_t>(blockIdx.x) * 64 * kK;
@@ -311,8 +439,21 @@ hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, i
   if (dy_bytes >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit buffer offsets
   const int tiles = Nb * (kOH / 2);
   const int grid = stem7x7_wgrad_slabs(Nb);
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(dy),
-                     static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes);
+  hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(dy),
+                     static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes, StemBnBwd{});
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s);
+}
+
+hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, const float* coef5, const void* x,
+                            float* dw32, void* dW, int Nb, hipStream_t s) {
+  if (Nb <= 0) return hipErrorInvalidValue;
+  const int tiles = Nb * (kOH / 2);
+  const int grid = stem7x7_wgrad_slabs(Nb);
+  StemBnBwd bn{static_cast<const bf16_t*>(c0), static_cast<const bf16_t*>(dp), idx, coef5};
+  hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(nullptr),
+                     static_cast<const bf16_t*>(x), dw32, tiles, int64_t(0), bn);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s);

@@ -97,6 +97,7 @@ class BNState:
         self.save_mean = torch.zeros(C, device=dev)
         self.save_invstd = torch.ones(C, device=dev)
         self.ws = None          # HIP workspace (replicas | coefs), self-cleaning
+        self.xam = None         # stem: BN input at each max-pool window's argmax (native path)
         # torch-backend state
         self.fsum = None        # (s1, s2, shift) forward sums
         self.fcoef = None       # (scale, shift)
@@ -183,9 +184,13 @@ class HipKernels:
 
     def stem_fwd(self, c0, st, gemm_stats=False):
         m = st.mod
-        y, mean, invstd, idx = self.ext.bn_pool_fwd(c0, m.weight, m.bias, m.running_mean, m.running_var, True,
-                                                    float(m.momentum), float(m.eps), st.ws, gemm_stats)
+        # native stem: also keep x at each window's argmax, so the backward's BN
+        # sums run over the pooled cells (csrc/bn_act.hip bn_pool_fwd_kernel)
+        y, mean, invstd, idx, xam = self.ext.bn_pool_fwd(c0, m.weight, m.bias, m.running_mean, m.running_var, True,
+                                                         float(m.momentum), float(m.eps), st.ws, gemm_stats,
+                                                         gemm_stats)
         st.save_mean, st.save_invstd = mean, invstd
+        st.xam = xam if gemm_stats else None
         return y, idx
 
     # -- backward
@@ -306,16 +311,8 @@ class HipKernels:
         """Stem conv weight gradient into ``dw`` ([64, 3, 7, 7]): csrc/stem.hip
         (both operands read pixel-major from LDS, no patch matrix) where the
         forward ran on it, else MIOpen."""
-        if (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(dw.shape) == (64, 3, 7, 7)
-                and x.is_contiguous(memory_format=torch.channels_last)
-                and dc0.is_contiguous(memory_format=torch.channels_last)):
-            nb = x.shape[0]
-            key = ("stem", nb)
-            ws = self._dw32.get(key)
-            if ws is None:
-                ws = (torch.empty(self.ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device=x.device),
-                      torch.empty(64, 224, device=x.device, dtype=torch.bfloat16))
-                self._dw32[key] = ws
+        if self._stem_native_bwd(x, dc0, dw):
+            ws = self._stem_ws(x.shape[0], x.device)
             self.ext.stem7x7_wgrad(dc0, x, ws[0], ws[1])
             dw.copy_(stem_grad_from_k(ws[1]))
             return
@@ -323,12 +320,49 @@ class HipKernels:
             dc0, x, dw, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False])
         dw.copy_(dw0)
 
-    def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta):
+    def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta, with_dx=True):
         m = st.mod
-        dx, dg, db = self.ext.bn_pool_bwd(dp, idx, c0, m.weight, m.bias, st.save_mean, st.save_invstd, True, st.ws)
+        dx, dg, db = self.ext.bn_pool_bwd(dp, idx, c0, m.weight, m.bias, st.save_mean, st.save_invstd, True, st.ws,
+                                          with_dx)
         dgamma.copy_(dg)
         dbeta.copy_(db)
         return dx
+
+    def _stem_native_bwd(self, x, c0, dw):
+        return (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(dw.shape) == (64, 3, 7, 7)
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and c0.is_contiguous(memory_format=torch.channels_last))
+
+    def stem_backward(self, dp, idx, c0, x, st, dgamma, dbeta, dw):
+        """Stem BN + ReLU + max-pool backward and the 7x7 weight gradient.  Native
+        path: the BN sums pass only (no full-resolution apply), then
+        csrc/stem.hip builds each tile's conv-output gradient in LDS from c0,
+        the pooled gradient and the BN coefficients while it reduces dW."""
+        xam = getattr(st, "xam", None)
+        if xam is None or not self._stem_native_bwd(x, c0, dw):
+            self.stem_wgrad(self.stem_bwd(dp, idx, c0, st, dgamma, dbeta), x, dw)
+            return
+        # BN sums over the pooled cells: sum(dp * mask(xam)), sum(dp * mask * (xam - mean))
+        # == the per-pixel sums of the max-pool backward (each cell's gradient
+        # lands on its argmax pixel); M of the finalize stays the pixel count
+        m = st.mod
+        self.ext.bn_stage_bwd_reduce(dp, xam, m.weight, m.bias, st.save_mean, st.save_invstd, st.ws,
+                                     dp.numel() // st.C, st.C, True)
+        self.bn_bwd_finalize(st, c0.numel() // st.C, dgamma, dbeta)
+        st.xam = None
+        nb = x.shape[0]
+        ws = self._stem_ws(nb, x.device)
+        self.ext.stem7x7_wgrad_bn(c0, dp, idx, st.ws, x, ws[0], ws[1])
+        dw.copy_(stem_grad_from_k(ws[1]))
+
+    def _stem_ws(self, nb, device):
+        key = ("stem", nb)
+        ws = self._dw32.get(key)
+        if ws is None:
+            ws = (torch.empty(self.ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device=device),
+                  torch.empty(64, 224, device=device, dtype=torch.bfloat16))
+            self._dw32[key] = ws
+        return ws
 
 
 class TorchKernels:
@@ -493,6 +527,9 @@ class TorchKernels:
 
     def wgrad3x3(self, g, x, stride, dW):
         dW.copy_(torch.nn.grad.conv2d_weight(x.float(), tuple(dW.shape), g.float(), stride=stride, padding=1))
+
+    def stem_backward(self, dp, idx, c0, x, st, dgamma, dbeta, dw):
+        self.stem_wgrad(self.stem_bwd(dp, idx, c0, st, dgamma, dbeta), x, dw)
 
     @staticmethod
     def stem_wgrad(dc0, x, dw):
@@ -825,9 +862,8 @@ class ResNetEngine:
             g = g_prev
         # stem: fused BN + ReLU + max-pool backward, then the 7x7 conv weight gradient
         st0 = self.bn[m.bn1]
-        dc0 = K.stem_bwd(g, idx, c0, st0, *self._bn_grads(st0))
+        K.stem_backward(g, idx, c0, x, st0, *self._bn_grads(st0), self._g(m.conv1.weight))
         self._bn_ready(st0)
-        K.stem_wgrad(dc0, x, self._g(m.conv1.weight))
         if self.side is not None:  # the optimizer (and the next forward) read every weight gradient
             torch.cuda.current_stream(self.dev).wait_stream(self.side)
         self.on_ready(m.conv1.weight)

@@ -105,8 +105,8 @@ class _BNPoolFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, ws):
         ext = _ext.load()
         x = x.contiguous(memory_format=torch.channels_last)
-        y, mean, invstd, idx = ext.bn_pool_fwd(x, weight, bias, running_mean, running_var, bool(training),
-                                               float(momentum), float(eps), ws, False)
+        y, mean, invstd, idx, _ = ext.bn_pool_fwd(x, weight, bias, running_mean, running_var, bool(training),
+                                                  float(momentum), float(eps), ws, False, False)
         ctx.save_for_backward(x, idx, weight, bias, mean, invstd)
         ctx.ws = ws
         ctx.training = training
@@ -117,7 +117,8 @@ class _BNPoolFn(torch.autograd.Function):
         ext = _ext.load()
         x, idx, weight, bias, mean, invstd = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dgamma, dbeta = ext.bn_pool_bwd(dy, idx, x, weight, bias, mean, invstd, bool(ctx.training), ctx.ws)
+        dx, dgamma, dbeta = ext.bn_pool_bwd(dy, idx, x, weight, bias, mean, invstd, bool(ctx.training), ctx.ws,
+                                            True)
         return dx, dgamma, dbeta, None, None, None, None, None, None
 
 

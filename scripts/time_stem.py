@@ -44,8 +44,8 @@ def main():
         "kdl_stem_stats": timed(lambda: ext.stem7x7_fwd(x, wp, y, rm, ws[:32 * 128])),
         "stem_weights": timed(lambda: stem_weights(w)),
         "miopen_conv": timed(lambda: F.conv2d(x, w, stride=2, padding=3)),
-        "bn_pool_own_stats": timed(lambda: ext.bn_pool_fwd(y, g, b, rm, rv, True, 0.1, 1e-5, ws, False)),
-        "bn_pool_gemm_stats": timed(lambda: ext.bn_pool_fwd(y, g, b, rm, rv, True, 0.1, 1e-5, ws, True)),
+        "bn_pool_own_stats": timed(lambda: ext.bn_pool_fwd(y, g, b, rm, rv, True, 0.1, 1e-5, ws, False, False)),
+        "bn_pool_gemm_stats": timed(lambda: ext.bn_pool_fwd(y, g, b, rm, rv, True, 0.1, 1e-5, ws, True, True)),
     }
     dy = torch.randn(nb, 112, 112, 64, device=dev).bfloat16().permute(0, 3, 1, 2)
     wsw = torch.empty(ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device=dev)
@@ -53,6 +53,27 @@ def main():
     res["kdl_stem_wgrad"] = timed(lambda: ext.stem7x7_wgrad(dy, x, wsw, dwk))
     res["miopen_stem_wgrad"] = timed(lambda: torch.ops.aten.convolution_backward(
         dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]))
+    c0 = y
+    _, _, _, idx, xam = ext.bn_pool_fwd(c0, g, b, rm, rv, True, 0.1, 1e-5, ws, False, True)
+    dp = torch.randn(nb, 56, 56, 64, device=dev).bfloat16().permute(0, 3, 1, 2)
+    mean, inv = torch.zeros(64, device=dev), torch.ones(64, device=dev)
+
+    def unfused():
+        dx = ext.bn_pool_bwd(dp, idx, c0, g, b, mean, inv, True, ws, True)[0]
+        ext.stem7x7_wgrad(dx, x, wsw, dwk)
+
+    dg, db = torch.empty_like(g), torch.empty_like(b)
+
+    def fused():
+        ext.bn_stage_bwd_reduce(dp, xam, g, b, mean, inv, ws, dp.numel() // 64, 64, True)
+        ext.bn_stage_bwd_finalize(ws, c0.numel() // 64, 64, g, mean, inv, dg, db, True)
+        ext.stem7x7_wgrad_bn(c0, dp, idx, ws, x, wsw, dwk)
+    res["bn_sums_over_cells"] = timed(lambda: ext.bn_stage_bwd_reduce(dp, xam, g, b, mean, inv, ws,
+                                                                      dp.numel() // 64, 64, True))
+    res["stem_bwd_unfused"] = timed(unfused)
+    res["stem_bwd_fused"] = timed(fused)
+    res["bn_pool_bwd_sums_only"] = timed(lambda: ext.bn_pool_bwd(dp, idx, c0, g, b, mean, inv, True, ws, False))
+    res["kdl_stem_wgrad_bn"] = timed(lambda: ext.stem7x7_wgrad_bn(c0, dp, idx, ws, x, wsw, dwk))
     for bits, name in ((1, "no_mfma"), (2, "no_epilogue"), (4, "no_input"), (3, "no_mfma_no_epi"),
                        (6, "mfma_only"), (5, "epilogue_only")):
         ext.set_stem_drop(bits)

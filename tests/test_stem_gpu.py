@@ -56,8 +56,8 @@ def test_stem_stats_and_bn_pool():
     beta = (torch.randn(64, device="cuda") * 0.1).bfloat16()
     rm2, rv2 = rm.clone(), rv.clone()
     ws2 = torch.zeros_like(ws)
-    out = ext.bn_pool_fwd(y, gamma, beta, rm, rv, True, 0.1, 1e-5, ws, True)
-    ref = ext.bn_pool_fwd(y, gamma, beta, rm2, rv2, True, 0.1, 1e-5, ws2, False)
+    out = ext.bn_pool_fwd(y, gamma, beta, rm, rv, True, 0.1, 1e-5, ws, True, False)
+    ref = ext.bn_pool_fwd(y, gamma, beta, rm2, rv2, True, 0.1, 1e-5, ws2, False, False)
     torch.testing.assert_close(out[1], ref[1], atol=1e-4, rtol=1e-4)  # mean
     torch.testing.assert_close(out[2], ref[2], atol=1e-3, rtol=1e-3)  # invstd
     torch.testing.assert_close(out[0].float(), ref[0].float(), atol=2e-2, rtol=2e-2)
@@ -84,3 +84,46 @@ def test_stem_wgrad_matches_fp32(nb):
     again = torch.empty_like(dwk)
     ext.stem7x7_wgrad(dy, x, ws, again)
     assert torch.equal(again, dwk), "stem weight gradient must be deterministic"
+
+
+def _pool_setup(nb, seed):
+    ext = _ext()
+    x, w = _inputs(nb, seed)
+    c0 = torch.empty(nb, 64, 112, 112, device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ext.stem7x7_fwd(x, stem_weights(w), c0, None, None)
+    gamma = (torch.rand(64, device="cuda") + 0.5).bfloat16()
+    beta = (torch.randn(64, device="cuda") * 0.3).bfloat16()
+    rm, rv = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+    ws = torch.zeros(ext.bn_workspace_floats(64), device="cuda")
+    y, mean, invstd, idx, xam = ext.bn_pool_fwd(c0, gamma, beta, rm, rv, True, 0.1, 1e-5, ws, False, True)
+    dp = torch.randn_like(y.float()).bfloat16().contiguous(memory_format=torch.channels_last)
+    return ext, x, c0, gamma, beta, mean, invstd, idx, dp, ws, xam
+
+
+@pytest.mark.parametrize("nb", [2, 5])
+def test_stem_wgrad_bn_fused_matches_unfused(nb):
+    """BN + ReLU + max-pool backward folded into the weight gradient == the
+    separate apply pass followed by the plain stem weight gradient."""
+    ext, x, c0, gamma, beta, mean, invstd, idx, dp, ws, xam = _pool_setup(nb, 34)
+    slabs = torch.empty(ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device="cuda")
+    dx, dg, db = ext.bn_pool_bwd(dp, idx, c0, gamma, beta, mean, invstd, True, ws, True)
+    ref = torch.empty(64, 224, device="cuda", dtype=torch.bfloat16)
+    ext.stem7x7_wgrad(dx, x, slabs, ref)
+    ws2 = ws.clone()
+    nodx, dg2, db2 = ext.bn_pool_bwd(dp, idx, c0, gamma, beta, mean, invstd, True, ws2, False)
+    assert nodx is None
+    torch.testing.assert_close(dg2.float(), dg.float(), atol=0, rtol=0)
+    torch.testing.assert_close(db2.float(), db.float(), atol=0, rtol=0)
+    # the engine's sums over pooled cells (x at the argmax) == the per-pixel gather sums
+    ws3 = ws.clone()
+    dg3 = torch.empty_like(dg)
+    db3 = torch.empty_like(db)
+    ext.bn_stage_bwd_reduce(dp, xam, gamma, beta, mean, invstd, ws3, dp.numel() // 64, 64, True)
+    ext.bn_stage_bwd_finalize(ws3, c0.numel() // 64, 64, gamma, mean, invstd, dg3, db3, True)
+    torch.testing.assert_close(dg3.float(), dg.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(db3.float(), db.float(), atol=2e-2, rtol=2e-2)
+    got = torch.empty_like(ref)
+    ext.stem7x7_wgrad_bn(c0, dp, idx, ws2, x, slabs, got)
+    scale = ref.float().abs().max().item()
+    torch.testing.assert_close(got.float(), ref.float(), atol=2e-3 * scale, rtol=1e-2)
