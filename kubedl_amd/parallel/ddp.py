@@ -64,6 +64,10 @@ class FlatDDP:
         self.space = space
         self.direct = direct
         self.world = world_size
+        # KDL_DDP_WORLD1=1: a world-1 job still buckets and all-reduces (RCCL's
+        # one-rank all-reduce) -- exercises the collective path the N-GPU job
+        # takes; off by default (it is an identity)
+        self.active = world_size > 1 or (os.environ.get("KDL_DDP_WORLD1", "0") == "1" and dist.is_initialized())
         self.pg = process_group
         self.buckets: list[Bucket] = []
         self._hooks = []
@@ -74,8 +78,8 @@ class FlatDDP:
         # joined the current one, so it waits for both without stalling the
         # current stream's remaining backward work
         self.join_stream = None
-        if world_size > 1:
-            if broadcast_from is not None:
+        if self.active:
+            if broadcast_from is not None and world_size > 1:
                 with torch.no_grad():
                     dist.broadcast(space.param, broadcast_from, group=process_group)
                     space.sync_master_from_params()
@@ -144,12 +148,12 @@ class FlatDDP:
     def ready(self, p: torch.Tensor) -> None:
         """Direct mode: ``p``'s gradient slice is final (launches its bucket's
         all-reduce when it was the bucket's last parameter)."""
-        if self.world > 1:
+        if self.active:
             self._on_grad(p)
 
     def finish(self) -> None:
         """Wait for every bucket (launching any whose params got no gradient)."""
-        if self.world == 1:
+        if not self.active:
             return  # the optimizer packs (FlatParamSpace.pack_grads)
         for b in self.buckets:
             if b.handle is None:
