@@ -11,6 +11,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include "bn_fin.h"
 #include "kdl_api.h"
 
 namespace {
@@ -624,6 +625,93 @@ void need_opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char*
                 ": fp32 contiguous GPU tensor of >= ", numel, " elements expected");
 }
 
+// BN finalize folded into the next conv GEMM launch (csrc/bn_fin.h): bn_fin_arm
+// names the workspace(s) whose BN the next conv1x1_gemm / conv3x3_gemm /
+// conv3x3_s2_dgrad call on this thread finalizes in its epilogue's last
+// arriving blocks; the launch consumes (clears) the arming.
+struct FinArm {
+  float* ws = nullptr;
+  float* ws2 = nullptr;
+  float M = 0.f;
+  int64_t C = 0;
+};
+thread_local FinArm g_fin_arm;
+
+void bn_fin_arm(const at::Tensor& ws, const c10::optional<at::Tensor>& ws2, int64_t C, int64_t M) {
+  TORCH_CHECK(C > 0 && C <= 2048 && C % 64 == 0, "bn_fin_arm: C in 64..2048, C % 64 == 0");
+  auto chk = [&](const at::Tensor& w) {
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.is_contiguous() &&
+                    w.numel() >= kdl::bn_workspace_floats(static_cast<int>(C)),
+                "bn_fin_arm: workspace must be fp32 >= bn_workspace_floats(C)");
+  };
+  chk(ws);
+  g_fin_arm.ws = ws.data_ptr<float>();
+  g_fin_arm.ws2 = nullptr;
+  if (ws2.has_value() && ws2->defined()) {
+    chk(*ws2);
+    g_fin_arm.ws2 = ws2->data_ptr<float>();
+  }
+  g_fin_arm.M = static_cast<float>(M);
+  g_fin_arm.C = C;
+}
+
+// consumed at the top of every GEMM binding, so a launch that throws still
+// disarms; applied to the launch arguments once they are built
+FinArm take_fin_arm() {
+  const FinArm f = g_fin_arm;
+  g_fin_arm = FinArm{};
+  return f;
+}
+
+void apply_fin_arm(const FinArm& f, kdl::Conv1x1Args& a, int64_t N, int64_t epi) {
+  if (!f.ws) return;
+  TORCH_CHECK(f.C == N, "bn_fin_arm: armed for C = ", f.C, ", the GEMM has N = ", N);
+  TORCH_CHECK(epi == 1 || epi == 2 || epi == 3, "bn_fin_arm: the GEMM's epilogue produces no BN sums");
+  a.fin_ws = f.ws;
+  a.fin_ws2 = f.ws2;
+  a.fin_M = f.M;
+}
+
+// the layer's finalize descriptor into the workspace tail (once; the pointers are stable)
+void bn_fin_desc(at::Tensor ws, const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                 at::Tensor rm, at::Tensor rv, at::Tensor save_mean, at::Tensor save_invstd,
+                 const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, double momentum,
+                 double eps) {
+  const int64_t C = rm.numel();
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() &&
+                  ws.numel() >= kdl::bn_workspace_floats(static_cast<int>(C)),
+              "bn_fin_desc: workspace");
+  for (const at::Tensor* t : {&rm, &rv, &save_mean, &save_invstd})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C,
+                "bn_fin_desc: fp32 per-channel tensors");
+  kdl::BnFinDesc d{};
+  int pt = -1;
+  for (const c10::optional<at::Tensor>* t : {&gamma, &beta, &dgamma, &dbeta}) {
+    if (!t->has_value() || !(*t)->defined()) continue;
+    TORCH_CHECK((*t)->is_cuda() && (*t)->is_contiguous() && (*t)->numel() == C, "bn_fin_desc: affine tensors");
+    const int this_pt = (*t)->scalar_type() == at::kBFloat16 ? 1 : 0;
+    TORCH_CHECK((*t)->scalar_type() == at::kBFloat16 || (*t)->scalar_type() == at::kFloat, "bn_fin_desc: dtype");
+    TORCH_CHECK(pt < 0 || pt == this_pt, "bn_fin_desc: affine tensors of one dtype");
+    pt = this_pt;
+  }
+  d.gamma = opt_ptr(gamma);
+  d.beta = opt_ptr(beta);
+  d.rm = rm.data_ptr<float>();
+  d.rv = rv.data_ptr<float>();
+  d.save_mean = save_mean.data_ptr<float>();
+  d.save_invstd = save_invstd.data_ptr<float>();
+  d.dgamma = const_cast<void*>(opt_ptr(dgamma));
+  d.dbeta = const_cast<void*>(opt_ptr(dbeta));
+  d.momentum = static_cast<float>(momentum);
+  d.eps = static_cast<float>(eps);
+  d.C = static_cast<int>(C);
+  d.pt_bf16 = pt == 1 ? 1 : 0;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(ws.device());
+  check_hip(hipMemcpy(ws.data_ptr<float>() + kdl::fin_desc_off(static_cast<int>(C)), &d, sizeof(d),
+                      hipMemcpyHostToDevice),
+            "bn_fin_desc");
+}
+
 void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_t M, int64_t N, int64_t K,
                   int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride,
                   const c10::optional<at::Tensor>& pro_coef, int64_t epi, const c10::optional<at::Tensor>& shift,
@@ -632,6 +720,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
                   const c10::optional<at::Tensor>& eres, int64_t res_stride, int64_t res_H, int64_t res_W,
                   const c10::optional<at::Tensor>& ebits, const c10::optional<at::Tensor>& ex2,
                   const c10::optional<at::Tensor>& emean2, const c10::optional<at::Tensor>& acc2) {
+  const FinArm fin = take_fin_arm();
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_gemm: need K % 64 == 0, N % 64 == 0");
   const int64_t rows_in = stride > 1 ? (M / (Hout * Wout)) * Hin * Win : M;
   if (stride > 1) TORCH_CHECK(M % (Hout * Wout) == 0 && (Hout - 1) * stride < Hin && (Wout - 1) * stride < Win,
@@ -679,6 +768,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   a.res_W = static_cast<int>(res_W);
   a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
   a.ex2 = opt_ptr(ex2); a.emean2 = opt_fptr(emean2); a.acc2 = opt_fptr(acc2);
+  apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");
 }
 
@@ -696,6 +786,7 @@ void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_
                   const c10::optional<at::Tensor>& shift, const c10::optional<at::Tensor>& acc,
                   const c10::optional<at::Tensor>& ex, const c10::optional<at::Tensor>& emean,
                   const c10::optional<at::Tensor>& ecoef) {
+  const FinArm fin = take_fin_arm();
   TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && Nb > 0 && stride >= 1, "conv3x3_gemm: need Cin, Cout % 64 == 0");
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 2, "conv3x3_gemm: epilogue must be PLAIN, STATS or MASKX");
   TORCH_CHECK(!(epi == 2 && opt_ptr(pro_coef)), "conv3x3_gemm: MASKX runs without a prologue");
@@ -723,6 +814,7 @@ void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_
   a.shift = opt_fptr(shift); a.acc = opt_fptr(acc);
   a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
   a.res_stride = 1;
+  apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv3x3_gemm");
 }
 
@@ -805,6 +897,7 @@ void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor d
                       int64_t Wd, int64_t Cd, int64_t N, int64_t epi, const c10::optional<at::Tensor>& acc,
                       const c10::optional<at::Tensor>& ex, const c10::optional<at::Tensor>& emean,
                       const c10::optional<at::Tensor>& ecoef) {
+  const FinArm fin = take_fin_arm();
   TORCH_CHECK(Cd % 64 == 0 && N % 64 == 0 && Nb > 0 && Hd > 0 && Wd > 0, "conv3x3_s2_dgrad: need Cd, N % 64 == 0");
   TORCH_CHECK(epi == 0 || epi == 2, "conv3x3_s2_dgrad: epilogue must be PLAIN or MASKX");
   const int64_t Mdx = Nb * 4 * Hd * Wd;
@@ -826,6 +919,7 @@ void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor d
   a.epi = static_cast<int>(epi);
   a.acc = opt_fptr(acc);
   a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
+  apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv3x3_dgrad_s2(a, cur_stream()), "conv3x3_s2_dgrad");
 }
 
@@ -1101,6 +1195,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
+  m.def("bn_fin_arm", &bn_fin_arm, "fold the BN finalize of this workspace (C channels, M elements) into the next conv GEMM launch");
+  m.def("bn_fin_desc", &bn_fin_desc, "write a BN layer's finalize descriptor into its workspace tail");
   m.def("stem7x7_wgrad_bn", &stem7x7_wgrad_bn, "stem weight gradient with the stem BN+ReLU+max-pool backward folded in");
   m.def("stem7x7_wgrad", &stem7x7_wgrad, "ResNet stem 7x7/s2/p3 conv weight gradient -> [64][224] bf16 (stem K order)");
   m.def("stem7x7_wgrad_slabs", [](int64_t nb) { return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb)); },

@@ -42,6 +42,7 @@
 // the PyTorchJob ResNet-50 worker spends most of its non-conv time in.
 #include <cstdlib>
 
+#include "bn_fin.h"
 #include "common.h"
 #include "kdl_api.h"
 
@@ -902,8 +903,8 @@ hipError_t bwd_impl(const T* dy, const T* y, const uint8_t* mbits, const T* x, c
 
 }  // namespace
 
-int64_t bn_workspace_floats(int C) {
-  return static_cast<int64_t>(kReplicas) * 4 * C + 5 * static_cast<int64_t>(C);
+int64_t bn_workspace_floats(int C) {  // + the folded-finalize descriptor and tile counters (bn_fin.h)
+  return static_cast<int64_t>(kReplicas) * 4 * C + 5 * static_cast<int64_t>(C) + kFinDescFloats + kFinCounters;
 }
 
 #define KDL_DISPATCH_PT(pdtype, ...)              \

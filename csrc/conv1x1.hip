@@ -596,6 +596,7 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.eres = static_cast<const bf16_t*>(a.eres); p.res_stride = a.res_stride > 0 ? a.res_stride : 1;
   p.res_H = a.res_H; p.res_W = a.res_W;
   p.ebits = a.ebits; p.ex2 = static_cast<const bf16_t*>(a.ex2); p.emean2 = a.emean2; p.acc2 = a.acc2;
+  p.fin_ws = a.fin_ws; p.fin_ws2 = a.fin_ws2; p.fin_M = a.fin_M;
   const bool pro = a.pro_coef != nullptr;
   int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
   p.Cin = a.K;
@@ -652,6 +653,7 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
   p.a_rows = a.M;
   p.acc = a.acc;
   p.ex = static_cast<const bf16_t*>(a.ex); p.emean = a.emean; p.ecoef = a.ecoef;
+  p.fin_ws = a.fin_ws; p.fin_M = a.fin_M;
   int cfg = igemm_pick(4 * a.M, a.N, a.K);
   if (cfg == 4) cfg = 1;  // the three-stage loop has no G_DGRAD2 variant
   return igemm(p, a.epi, G_DGRAD2, cfg, s);

@@ -20,6 +20,7 @@
 // the BN workspace replica of the block (one atomic per channel per block).
 #pragma once
 
+#include "bn_fin.h"
 #include "common.h"
 
 namespace kdl {
@@ -66,6 +67,12 @@ struct GemmParams {
   // dx pixels (2i + py, 2j + px).  mc = Nb Hin Win rows per class, padded to
   // mc_pad (a multiple of BM, set by the launcher); M = 4 mc_pad.
   int mc, mc_pad;
+  // BN finalize folded into this GEMM (csrc/bn_fin.h): the workspace of the BN
+  // whose sums the epilogue produces (second one: RESBITS' downsample BN), and
+  // that BN's element count; null = the host launches the finalize
+  float* fin_ws;
+  float* fin_ws2;
+  float fin_M;
 };
 
 // csrc/wgrad_dma.hip: weight gradient on the LDS-DMA pipeline into fp32
@@ -161,14 +168,15 @@ struct Epilogue {
   static constexpr int kScratchBytes = REDUCE ? 3 * NT * 8 * 4 : 0;
   static_assert(NT % CPR == 0 && BM % RPP == 0 && NP % PG == 0, "epilogue geometry");
 
-  int t, ec, er0, ch0;
+  int t, ec, er0, ch0, n0;
   f2_t s1[4], s2[4], s3[4];
   uint4 pxv[PG], prv[PG], px2[PG];
   uint32_t pbv[PG];
   bool prok[PG];
 
-  __device__ __forceinline__ void init(int t_, int n0) {
+  __device__ __forceinline__ void init(int t_, int n0_) {
     t = t_;
+    n0 = n0_;
     ec = t % CPR;
     er0 = t / CPR;
     ch0 = n0 + ec * 8;
@@ -382,6 +390,40 @@ struct Epilogue {
           }
         }
       }
+      if (p.fin_ws) finalize_last(p, sh);
+    }
+  }
+
+  // the last block of this output-channel tile to get here finalizes the
+  // tile's channels (csrc/bn_fin.h); every block of the grid calls finish()
+  __device__ __forceinline__ void finalize_last(const GemmParams& p, float* sh) {
+    const int N = p.N;
+    __threadfence();   // this thread's replica atomics before the arrival
+    __syncthreads();   // every thread's (and the fold's reads of sh)
+    const int tiles_n = N / BN;
+    const unsigned arrivals = gridDim.x / tiles_n;
+    constexpr bool FWD = EPI == EPI_STATS;
+    unsigned* cnt = reinterpret_cast<unsigned*>(p.fin_ws + fin_desc_off(N) + kFinDescFloats) + (FWD ? 0 : 32) +
+                    n0 / BN;
+    int* flag = reinterpret_cast<int*>(sh);
+    if (t == 0)
+      flag[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1;
+    __syncthreads();
+    if (flag[0]) {
+      __threadfence();  // acquire: every other block's replica adds
+      const BnFinDesc d = *reinterpret_cast<const BnFinDesc*>(p.fin_ws + fin_desc_off(N));
+      for (int c = n0 + t; c < n0 + BN; c += NT) {
+        if constexpr (FWD) {
+          fin_fwd_channel(d, p.fin_ws, c, p.fin_M);
+        } else {
+          fin_bwd_channel(d, p.fin_ws, c, p.fin_M);
+          if (EPI == EPI_RESBITS && p.fin_ws2) {
+            const BnFinDesc d2 = *reinterpret_cast<const BnFinDesc*>(p.fin_ws2 + fin_desc_off(N));
+            fin_bwd_channel(d2, p.fin_ws2, c, p.fin_M);
+          }
+        }
+      }
+      if (t == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 };

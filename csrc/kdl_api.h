@@ -211,6 +211,9 @@ struct Conv1x1Args {
   float* acc2;
   int ksize;                         // 1 (or 0): 1x1 conv / GEMM; 3: 3x3 pad-1 implicit GEMM (K = 9 * Cin)
   int Cin;                           // ksize 3: input channels (the A row width)
+  float* fin_ws;                     // epi 1-3: finalize the BN of this workspace in the GEMM (bn_fin.h)
+  float* fin_ws2;                    // epi 3: and the downsample BN's
+  float fin_M;                       // their element count
 };
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 // Data gradient of a 3x3 / pad 1 / stride 2 conv as four sub-pixel class GEMMs

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
   constexpr int G_BYTES = kBM * 128;  // 224 pixel rows x 64 channels
   constexpr int H_BYTES = kHR * kHC * 8;
   constexpr int NG = FUSE ? 1 : 2;    // the fused tile is built in place, not DMA'd ahead
-  constexpr int P_BYTES = 2 * (kOW / 2) * 64 * 3;  // staged pooled rows: bf16 gradient + u8 argmax
+  constexpr int P_BYTES = 2 * (kOW / 2) * 64 * 3;  // staged pooled rows: bf16 gradient + u8 argmax (21 KiB)
   __shared__ __attribute__((aligned(1024))) char lds[NG * G_BYTES + H_BYTES + (FUSE ? 5 * 64 * 4 + P_BYTES : 0)];
   char* Gs = lds;
   bf16_t* Hs = reinterpret_cast<bf16_t*>(lds + NG * G_BYTES);
@@ -240,45 +240,41 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
 
   // FUSE: tile tm (output rows 2k, 2k + 1) only sees pooled rows k and k + 1
   // (row 2k: window k; row 2k + 1: windows k and k + 1).  Their gradient and
-  // argmax bytes (2 x 56 x 64) are loaded coalesced under the previous tile's
-  // MFMAs and staged in LDS, so the per-pixel window gather reads LDS; the c0
-  // rows arrive by LDS-DMA into the dY tile itself and are overwritten in place.
+  // argmax bytes (2 x 56 x 64) arrive by LDS-DMA under the previous tile's
+  // MFMAs, so the per-pixel window gather reads LDS; the c0 rows arrive by
+  // LDS-DMA into the dY tile itself and are overwritten in place (no staging
+  // registers: the kernel sits at the 128-VGPR bound of two blocks per CU).
   constexpr int kPW = kOW / 2, kPH = kOH / 2;
-  constexpr int DP_CH = 2 * kPW * 8, IX_CH = 2 * kPW * 4;  // 16-B chunks: dp rows, idx rows
-  constexpr int PCH = (DP_CH + IX_CH + kNT - 1) / kNT;     // per thread (3)
-  char* Ps = lds + NG * G_BYTES + H_BYTES + 5 * 64 * 4;    // [2][56][64] bf16 dp | [2][56][64] u8 idx
-  uint4 ppf[FUSE ? PCH : 1];
-  (void)ppf; (void)Ps;
-  auto load_pool = [&](int tm) {
+  constexpr int DP_BYTES = 2 * kPW * 128, IX_BYTES = 2 * kPW * 64;  // two pooled rows of dp | idx
+  char* Ps = lds + NG * G_BYTES + H_BYTES + 5 * 64 * 4;            // [2][56][64] bf16 dp | [2][56][64] u8 idx
+  (void)Ps;
+  // pooled rows k, k + 1 of the image are contiguous: 21 1-KiB LDS-DMA groups
+  // (rows past the last image read as zeros; past the image's last row they
+  // are never used)
+  const int64_t pool_cells = static_cast<int64_t>(tiles / kPH) * kPH * kPW;
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(FUSE ? bn.dp : x), (short)0, static_cast<int>(FUSE ? pool_cells * 128 : 0), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rI = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(FUSE ? bn.idx : nullptr), (short)0, static_cast<int>(FUSE ? pool_cells * 64 : 0),
+      0x00020000);
+  auto issue_pool = [&](int tm) {
     const int img = tm / kPH, k = tm - img * kPH;
+    const uint32_t cell0 = static_cast<uint32_t>((img * kPH + k) * kPW);
 #pragma unroll
-    for (int q = 0; q < PCH; ++q) {
-      const int j = t + q * kNT;
-      ppf[q] = make_uint4(0u, 0u, 0u, 0u);
-      if (j < DP_CH) {
-        const int r = j / (kPW * 8), rem = j - r * (kPW * 8);
-        if (k + r < kPH)
-          ppf[q] = *reinterpret_cast<const uint4*>(bn.dp + ((static_cast<int64_t>(img) * kPH + k + r) * kPW) * 64 + 8 * rem);
-      } else if (j < DP_CH + IX_CH) {
-        const int jj = j - DP_CH;
-        const int r = jj / (kPW * 4), rem = jj - r * (kPW * 4);
-        if (k + r < kPH)
-          ppf[q] = *reinterpret_cast<const uint4*>(bn.idx + ((static_cast<int64_t>(img) * kPH + k + r) * kPW) * 64 + 16 * rem);
-      }
-    }
-  };
-  auto store_pool = [&]() {
-#pragma unroll
-    for (int q = 0; q < PCH; ++q) {
-      const int j = t + q * kNT;
-      if (j < DP_CH + IX_CH) reinterpret_cast<uint4*>(Ps)[j] = ppf[q];  // dp chunks, then idx chunks
+    for (int i = 0; i < 3; ++i) {
+      const int g = wave * 3 + i;  // 0..20
+      if (g < DP_BYTES / 1024)
+        dma16(rD, (lds_void_t*)(Ps + g * 1024), cell0 * 128 + g * 1024 + 16 * lane);
+      else
+        dma16(rI, (lds_void_t*)(Ps + DP_BYTES + (g - DP_BYTES / 1024) * 1024),
+              cell0 * 64 + (g - DP_BYTES / 1024) * 1024 + 16 * lane);
     }
   };
   auto build_g = [&](int tm) {
     const int cgp = t & 7;
     const int k = tm - (tm / kPH) * kPH;
     const bf16_t* pdp = reinterpret_cast<const bf16_t*>(Ps);
-    const uint8_t* pix = reinterpret_cast<const uint8_t*>(Ps + DP_CH * 16);
+    const uint8_t* pix = reinterpret_cast<const uint8_t*>(Ps + DP_BYTES);
 #pragma unroll 1
     for (int q = 0; q < kBM * 8 / kNT; ++q) {
       const int px = (t + q * kNT) >> 3;
@@ -321,7 +317,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
       *slot = pack8(o);
     }
   };
-  (void)build_g; (void)load_pool; (void)store_pool;
+  (void)build_g; (void)issue_pool;
 
   // transposed-read lane roles (csrc/wgrad_dma.hip): rows lrow (+4) of each
   // 16-row step, columns 16 (grp & 1) + 4 pp of a 32-column fragment
@@ -346,9 +342,8 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
   if (tm < tiles) {
     if constexpr (FUSE) {
       issue_g(tm, 0);
-      load_pool(tm);
-      store_pool();
-      __syncthreads();  // c0 rows (vmcnt 0) and pooled rows in LDS
+      issue_pool(tm);
+      __syncthreads();  // c0 rows and pooled rows landed (vmcnt 0)
       build_g(tm);
     } else {
       issue_g(tm, 0);
@@ -360,7 +355,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
     const int next = tm + gridDim.x;
     __syncthreads();  // dY tile landed (vmcnt 0) / built, halo written, the other dY buffer is free
     if (next < tiles) {
-      if constexpr (FUSE) load_pool(next);
+      if constexpr (FUSE) issue_pool(next);  // this tile's pooled rows were consumed by its build
       else issue_g(next, buf ^ 1);
       hs.load(x, next, t);
     }
@@ -381,10 +376,9 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
     if (next < tiles) {
       if constexpr (FUSE) issue_g(next, 0);  // this tile's dY has been consumed
       hs.store(Hs, t);
-      if constexpr (FUSE) store_pool();
     }
     if constexpr (FUSE) {
-      __syncthreads();  // c0 rows landed (vmcnt 0), staged pooled rows visible
+      __syncthreads();  // c0 and pooled rows landed (vmcnt 0)
       if (next < tiles) build_g(next);
     }
     if constexpr (!FUSE) buf ^= 1;

@@ -98,6 +98,8 @@ class BNState:
         self.save_invstd = torch.ones(C, device=dev)
         self.ws = None          # HIP workspace (replicas | coefs), self-cleaning
         self.xam = None         # stem: BN input at each max-pool window's argmax (native path)
+        self.fin_done = False   # forward finalize already done by the producing GEMM (csrc/bn_fin.h)
+        self.bfin_done = False  # backward finalize likewise
         # torch-backend state
         self.fsum = None        # (s1, s2, shift) forward sums
         self.fcoef = None       # (scale, shift)
@@ -117,6 +119,35 @@ class HipKernels:
         self.dev = dev
         self._dw32 = {}
         self.stem_native = os.environ.get("KDL_STEM", "kdl") != "miopen"  # KDL_STEM=miopen: vendor stem conv
+        # BN finalize folded into the producing conv GEMM's last arriving blocks
+        # (csrc/bn_fin.h); KDL_BN_FIN=kernel keeps the separate finalize launches
+        self.fuse_fin = os.environ.get("KDL_BN_FIN", "kernel") != "kernel"
+        self._fin_ptrs = {}
+
+    def fin_desc(self, st, dgamma, dbeta):
+        """(Re)write st's finalize descriptor when a pointer it holds changed."""
+        if not self.fuse_fin:
+            return
+        m = st.mod
+        ptrs = (st.ws.data_ptr(), m.weight.data_ptr() if m.weight is not None else 0,
+                m.running_mean.data_ptr(), st.save_mean.data_ptr(), st.save_invstd.data_ptr(),
+                dgamma.data_ptr() if dgamma is not None else 0, dbeta.data_ptr() if dbeta is not None else 0)
+        if self._fin_ptrs.get(id(st)) != ptrs:
+            self.ext.bn_fin_desc(st.ws, m.weight, m.bias, m.running_mean, m.running_var, st.save_mean,
+                                 st.save_invstd, dgamma, dbeta, float(m.momentum), float(m.eps))
+            self._fin_ptrs[id(st)] = ptrs
+
+    def _arm(self, st, M, st2=None, fwd=True):
+        """The next conv GEMM finalizes st (and st2) itself."""
+        if not self.fuse_fin or st.C > 2048 or st.C % 64:
+            return
+        self.ext.bn_fin_arm(st.ws, st2.ws if st2 is not None else None, st.C, M)
+        for x in (st, st2):
+            if x is not None:
+                if fwd:
+                    x.fin_done = True
+                else:
+                    x.bfin_done = True
 
     def init_bn(self, st: BNState):
         st.ws = torch.zeros(self.ext.bn_workspace_floats(st.C), device=self.dev)
@@ -138,6 +169,7 @@ class HipKernels:
         ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
         y = _nhwc_empty(n, cout, ho, wo, x)
         M = n * ho * wo
+        self._arm(out, M)
         self.ext.conv1x1_gemm(x, w, y, M, cout, cin, ho, wo, h, wd, stride,
                               self.fcoef(pro) if pro is not None else None, 1, out.mod.running_mean,
                               self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
@@ -150,6 +182,7 @@ class HipKernels:
         cout = w.shape[0]
         ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
         y = _nhwc_empty(n, cout, ho, wo, x)
+        self._arm(out, n * ho * wo)
         self.ext.conv3x3_gemm(x, w, y, n, h, wd, cin, cout, stride, None, 1, out.mod.running_mean,
                               self._fwd_acc(out), None, None, None)
         return y
@@ -158,6 +191,9 @@ class HipKernels:
         self.ext.bn_stage_fwd_stats(x, st.ws, x.numel() // st.C, st.C)
 
     def bn_finalize(self, st, M, x=None, gemm_shift=False):
+        if st.fin_done:  # the producing GEMM did it
+            st.fin_done = False
+            return
         m = st.mod
         self.ext.bn_stage_fwd_finalize(None if gemm_shift else x, m.running_mean if gemm_shift else None, st.ws, M,
                                        st.C, m.weight, m.bias, m.running_mean, m.running_var, st.save_mean,
@@ -204,6 +240,9 @@ class HipKernels:
         return g
 
     def bn_bwd_finalize(self, st, M, dgamma, dbeta):
+        if st.bfin_done:  # the producing GEMM did it
+            st.bfin_done = False
+            return
         self.ext.bn_stage_bwd_finalize(st.ws, M, st.C, st.mod.weight, st.save_mean, st.save_invstd, dgamma, dbeta,
                                        True)
 
@@ -231,6 +270,7 @@ class HipKernels:
         cin = wt.shape[0]
         out = _nhwc_empty(n, cin, h, w, g)
         M = n * h * w
+        self._arm(st2, M, fwd=False)
         self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), x2,
                               st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
         return out
@@ -241,6 +281,7 @@ class HipKernels:
         n, cout, h, w = g.shape
         cin = wd.shape[0]
         out = _nhwc_empty(n, cin, h, w, g)
+        self._arm(st1, n * h * w, fwd=False)
         self.ext.conv3x3_gemm(g, wd, out, n, h, w, cout, cin, 1, None, 2, None, self._bwd_acc(st1), x1,
                               st1.save_mean, self.fcoef(st1))
         return out
@@ -252,6 +293,7 @@ class HipKernels:
         n, cout, h, w = g.shape
         cin = ball.shape[0]
         out = _nhwc_empty(n, cin, 2 * h, 2 * w, g)
+        self._arm(st1, n * 4 * h * w, fwd=False)
         self.ext.conv3x3_s2_dgrad(g, ball, out, n, h, w, cout, cin, 2, self._bwd_acc(st1), x1, st1.save_mean,
                                   self.fcoef(st1))
         return out
@@ -276,6 +318,7 @@ class HipKernels:
                                   res_stride, h, w, None, None, None, None)
         else:
             mbits, c3, st3, cd, std_ = prev
+            self._arm(st3, M, std_, fwd=False)
             self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, self._bwd_acc(st3), c3,
                                   st3.save_mean, None, eres, res_stride, h, w, mbits, cd,
                                   std_.save_mean if std_ is not None else None,
@@ -591,7 +634,7 @@ class ResNetEngine:
         self.side = None
         if self.K.name == "hip" and os.environ.get("KDL_WGRAD_STREAM", "1") == "1":
             from kubedl_amd.ops.streams import side_stream
-            self.side = side_stream(self.dev)  # (ops/streams.py)
+            self.side = side_stream(self.dev, int(os.environ.get("KDL_SIDE_PRIO", "0")))  # (ops/streams.py)
 
     def _refresh_wt(self) -> None:
         """HIP path: the data-gradient GEMMs' B operands -- W^T of every 1x1 conv
@@ -682,10 +725,23 @@ class ResNetEngine:
             t.record_stream(self.side)
         return torch.cuda.stream(self.side)
 
+    def _fin_descs(self) -> None:
+        """HIP path: every conv BN's finalize descriptor (csrc/bn_fin.h) -- written
+        once, and again only if the gradient buffer moved."""
+        if self.K.name != "hip" or not self.K.fuse_fin:
+            return
+        sts = [st for mod, st in self.bn.items() if mod is not self.model.bn1]
+        sig = tuple(t.data_ptr() for t in self._bn_grads(sts[0])) + (sts[0].ws.data_ptr(),)
+        if sig != getattr(self, "_fin_sig", None):
+            for st in sts:
+                self.K.fin_desc(st, *self._bn_grads(st))
+            self._fin_sig = sig
+
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     def forward(self, x: torch.Tensor):
         K, m = self.K, self.model
+        self._fin_descs()
         st0 = self.bn[m.bn1]
         c0, gemm_stats = K.stem_conv(x, m.conv1.weight, st0)
         x1, idx = K.stem_fwd(c0, st0, gemm_stats)

@@ -38,7 +38,10 @@ def compute_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     m = mode()
     if device.type != "cuda" or m == "null":
         return None
-    return side_stream(device)
+    # KDL_MAIN_PRIO=-1: the step's stream at high priority, so the dispatcher
+    # hands CUs to its (critical-path) kernels before the weight-gradient
+    # side stream's (torch: lower number = higher priority)
+    return side_stream(device, int(os.environ.get("KDL_MAIN_PRIO", "0")))
 
 
 def side_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:

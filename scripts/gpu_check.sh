@@ -51,9 +51,11 @@ if want bnsweep; then
   done
 fi
 if want envsweep; then  # SWEEPVAR=<env var> SWEEP="<values>": direct bench per value
+  i=0
   for v in ${SWEEP}; do
+    i=$((i+1))
     export "${SWEEPVAR}=$v"
-    run_step "bench_${SWEEPVAR}_$v" 600 python bench.py --direct --gpus 1 --steps 20 --warmup 5
+    run_step "bench_${SWEEPVAR}_${v}_r$i" 600 python bench.py --direct --gpus 1 --steps 20 --warmup 5
     unset "${SWEEPVAR}"
   done
 fi

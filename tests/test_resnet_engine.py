@@ -253,3 +253,27 @@ def test_engine_ddp_two_ranks_hip_gpu():
     torch.testing.assert_close(m0, m1, atol=0, rtol=0)
     torch.testing.assert_close(g0, g1, atol=0, rtol=0)
     assert g0.abs().sum() > 0
+
+
+@pytest.mark.gpu
+def test_engine_bn_finalize_in_gemm_matches_kernel_finalize(monkeypatch):
+    """BN finalize folded into the producing GEMMs' last arriving blocks
+    (csrc/bn_fin.h, default) == the separate finalize launches
+    (KDL_BN_FIN=kernel): gradients, BN affine gradients, running statistics."""
+    results = []
+    for mode in ("kernel", "gemm"):
+        monkeypatch.setenv("KDL_BN_FIN", mode)
+        model, ref, x, y = _setup((2, 2, 2, 2), 64, "cuda", 112, 16, classes=10, seed=3)
+        eng = ResNetEngine(model, backend="hip")
+        assert eng.K.fuse_fin == (mode == "gemm")
+        loss = eng.forward_backward(x, y)
+        torch.cuda.synchronize()
+        results.append((float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()},
+                        {n: b.float().clone() for n, b in model.named_buffers()}))
+    (l0, g0, b0), (l1, g1, b1) = results
+    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0))
+    for n in g0:
+        scale = g0[n].abs().max().item() + 1e-6
+        torch.testing.assert_close(g1[n], g0[n], atol=2e-2 * scale, rtol=2e-2, msg=n)
+    for n in b0:
+        torch.testing.assert_close(b1[n], b0[n], atol=1e-3, rtol=1e-3, msg=n)
