@@ -396,21 +396,32 @@ struct Epilogue {
 
   // the last block of this output-channel tile to get here finalizes the
   // tile's channels (csrc/bn_fin.h); every block of the grid calls finish()
+  // Hand-off (cdna_hip_programming.md, in-launch split-K recipe): the replica
+  // adds are device-scope atomics (performed at the coherence point, visible
+  // across XCDs), so a writer only waits for them (vmcnt) before lane 0 draws
+  // its ticket -- no per-thread __threadfence (an L2 write-back per thread:
+  // that version ran the ResNet step 27 % slower); the last arriver's lane 0
+  // takes one agent-scope acquire and the sums are read with agent-scope loads.
   __device__ __forceinline__ void finalize_last(const GemmParams& p, float* sh) {
     const int N = p.N;
-    __threadfence();   // this thread's replica atomics before the arrival
-    __syncthreads();   // every thread's (and the fold's reads of sh)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's replica atomics acknowledged
+    __syncthreads();                                   // every wave's (and the fold's reads of sh)
     const int tiles_n = N / BN;
     const unsigned arrivals = gridDim.x / tiles_n;
     constexpr bool FWD = EPI == EPI_STATS;
     unsigned* cnt = reinterpret_cast<unsigned*>(p.fin_ws + fin_desc_off(N) + kFinDescFloats) + (FWD ? 0 : 32) +
                     n0 / BN;
     int* flag = reinterpret_cast<int*>(sh);
-    if (t == 0)
-      flag[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1;
+    if (t == 0) {
+      const bool last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
     __syncthreads();
     if (flag[0]) {
-      __threadfence();  // acquire: every other block's replica adds
       const BnFinDesc d = *reinterpret_cast<const BnFinDesc*>(p.fin_ws + fin_desc_off(N));
       for (int c = n0 + t; c < n0 + BN; c += NT) {
         if constexpr (FWD) {

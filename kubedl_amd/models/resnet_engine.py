@@ -119,8 +119,11 @@ class HipKernels:
         self.dev = dev
         self._dw32 = {}
         self.stem_native = os.environ.get("KDL_STEM", "kdl") != "miopen"  # KDL_STEM=miopen: vendor stem conv
-        # BN finalize folded into the producing conv GEMM's last arriving blocks
-        # (csrc/bn_fin.h); KDL_BN_FIN=kernel keeps the separate finalize launches
+        # KDL_BN_FIN=gemm: BN finalize folded into the producing conv GEMM's last
+        # arriving blocks (csrc/bn_fin.h).  Measured neutral (12,612 / 12,617 vs
+        # 12,629 / 12,598 img/s, profiles/r02_bn_fin_ab.txt): the last arriver's
+        # acquire + replica reads cost what the ~106 separate launches did, so
+        # the default keeps the separate finalize kernels
         self.fuse_fin = os.environ.get("KDL_BN_FIN", "kernel") != "kernel"
         self._fin_ptrs = {}
 

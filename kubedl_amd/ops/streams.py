@@ -38,10 +38,11 @@ def compute_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     m = mode()
     if device.type != "cuda" or m == "null":
         return None
-    # KDL_MAIN_PRIO=-1: the step's stream at high priority, so the dispatcher
-    # hands CUs to its (critical-path) kernels before the weight-gradient
-    # side stream's (torch: lower number = higher priority)
-    return side_stream(device, int(os.environ.get("KDL_MAIN_PRIO", "0")))
+    # the step's stream at high priority (KDL_MAIN_PRIO, default -1): the
+    # dispatcher hands CUs to its critical-path kernels before the
+    # weight-gradient side stream's (torch: lower number = higher priority);
+    # measured 12,574-12,661 -> 12,740-12,751 img/s (profiles/r02_stream_priority_ab.txt)
+    return side_stream(device, int(os.environ.get("KDL_MAIN_PRIO", "-1")))
 
 
 def side_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:

@@ -258,10 +258,11 @@ def test_engine_ddp_two_ranks_hip_gpu():
 @pytest.mark.gpu
 def test_engine_bn_finalize_in_gemm_matches_kernel_finalize(monkeypatch):
     """BN finalize folded into the producing GEMMs' last arriving blocks
-    (csrc/bn_fin.h, default) == the separate finalize launches
-    (KDL_BN_FIN=kernel): gradients, BN affine gradients, running statistics."""
+    (csrc/bn_fin.h, KDL_BN_FIN=gemm) vs the separate finalize launches
+    (KDL_BN_FIN=kernel): the difference must be at the level of two runs of the
+    same mode (replica atomics make BN sums order-nondeterministic)."""
     results = []
-    for mode in ("kernel", "gemm"):
+    for mode in ("kernel", "kernel", "gemm"):
         monkeypatch.setenv("KDL_BN_FIN", mode)
         model, ref, x, y = _setup((2, 2, 2, 2), 64, "cuda", 112, 16, classes=10, seed=3)
         eng = ResNetEngine(model, backend="hip")
@@ -270,10 +271,17 @@ def test_engine_bn_finalize_in_gemm_matches_kernel_finalize(monkeypatch):
         torch.cuda.synchronize()
         results.append((float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()},
                         {n: b.float().clone() for n, b in model.named_buffers()}))
-    (l0, g0, b0), (l1, g1, b1) = results
-    assert abs(l0 - l1) < 1e-3 * max(1.0, abs(l0))
-    for n in g0:
-        scale = g0[n].abs().max().item() + 1e-6
-        torch.testing.assert_close(g1[n], g0[n], atol=2e-2 * scale, rtol=2e-2, msg=n)
-    for n in b0:
-        torch.testing.assert_close(b1[n], b0[n], atol=1e-3, rtol=1e-3, msg=n)
+
+    def rel(a, b):
+        return {n: ((a[n] - b[n]).norm() / (b[n].norm() + 1e-12)).item() for n in b}
+    noise = rel(results[1][1], results[0][1])
+    fused = rel(results[2][1], results[0][1])
+    worst = sorted(fused, key=lambda n: -fused[n])[:8]
+    report = "; ".join(f"{n}: fused {fused[n]:.2e} noise {noise[n]:.2e}" for n in worst)
+    assert abs(results[2][0] - results[0][0]) < 1e-3 * max(1.0, abs(results[0][0])), report
+    for n in fused:
+        assert fused[n] <= 3 * noise[n] + 2e-3, report
+    bnoise = rel(results[1][2], results[0][2])
+    bfused = rel(results[2][2], results[0][2])
+    for n in bfused:
+        assert bfused[n] <= 3 * bnoise[n] + 1e-4, (n, bfused[n], bnoise[n])
