@@ -772,6 +772,11 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");
 }
 
+int64_t conv3x3_wgrad_slabs(int64_t Nb, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int64_t stride) {
+  return kdl::conv3x3_wgrad_slabs(static_cast<int>(Nb), static_cast<int>(H), static_cast<int>(W),
+                                  static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(stride));
+}
+
 int64_t conv1x1_wgrad_splits(int64_t M, int64_t N, int64_t K) {
   return kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
 }
@@ -964,7 +969,7 @@ void conv3x3_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
     TORCH_CHECK(dW->numel() == Cout * K, "conv3x3_wgrad: dW must have Cout * 9 * Cin elements");
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(G.device());
-  check_hip(kdl::conv3x3_wgrad(G.data_ptr(), A.data_ptr(), opt_fptr(pro_coef), dw32.data_ptr<float>(),
+  check_hip(kdl::conv3x3_wgrad(G.data_ptr(), A.data_ptr(), opt_fptr(pro_coef), dw32.data_ptr<float>(), dw32.numel(),
                                dW.has_value() && dW->defined() ? dW->data_ptr() : nullptr, static_cast<float>(scale),
                                static_cast<int>(Nb), static_cast<int>(H), static_cast<int>(Wd), static_cast<int>(Cin),
                                static_cast<int>(Cout), static_cast<int>(stride), cur_stream()),
@@ -1206,6 +1211,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 pad-1 conv weight gradient (implicit GEMM, split-M slabs)");
+  m.def("conv3x3_wgrad_slabs", &conv3x3_wgrad_slabs, "fp32 [Cout, 9 Cin] slabs conv3x3_wgrad may write (its fastest path)");
   m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad");
   m.def("bn_coef_offset", &bn_coef_offset, "float offset of the coefficient block in a BN workspace");
   m.def("bn_stage_fwd_stats", &bn_stage_fwd_stats, "BN forward statistics into the workspace replicas");

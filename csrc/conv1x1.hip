@@ -767,9 +767,24 @@ hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, fl
                     stride > 1 ? G_STRIDED : G_DENSE, K, s);
 }
 
-hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
-                         int Nb, int Hin, int Win, int Cin, int Cout, int stride, hipStream_t s) {
+int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {
+  const int Ho = (Hin - 1) / stride + 1, Wo = (Win - 1) / stride + 1;
+  const int dflt = conv1x1_wgrad_splits(Nb * Ho * Wo, Cout, 9 * Cin);
+  const int halo = halo3x3_wgrad_slabs(Nb, Hin, Win, Cin, Cout, stride);
+  return halo > dflt ? halo : dflt;
+}
+
+hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, int64_t dw32_floats,
+                         void* dW, float scale, int Nb, int Hin, int Win, int Cin, int Cout, int stride,
+                         hipStream_t s) {
   if (Cin % 64 || Cout % 64 || Nb <= 0 || stride < 1) return hipErrorInvalidValue;
+  if (!pro_coef && gemm_core_mode() != 0) {  // 56x56 stage: input halo staged once per tile (csrc/halo3x3.hip)
+    int nslabs = 0;
+    const hipError_t e = halo3x3_wgrad(G, A, dw32, dw32_floats, Nb, Hin, Win, Cin, Cout, stride, &nslabs, s);
+    if (e == hipSuccess)
+      return wgrad_reduce(dw32, static_cast<int64_t>(Cout) * 9 * Cin, nslabs, scale, static_cast<bf16_t*>(dW), s);
+    if (e != hipErrorInvalidValue) return e;
+  }
   const int Ho = (Hin - 1) / stride + 1, Wo = (Win - 1) / stride + 1;
   return wgrad_impl(G, A, pro_coef, dw32, dW, scale, Nb * Ho * Wo, Cout, 9 * Cin, Ho, Wo, Hin, Win, stride, G_CONV3,
                     Cin, s);

@@ -255,6 +255,167 @@ int g_halo = [] {  // KDL_HALO=0 keeps every 3x3 on the implicit GEMM
   return e ? atoi(e) : 1;
 }();
 
+// ---------------------------------------------------------------- weight gradient
+// dW[co][tap][ci] = sum_p dy[p][co] * a[p + tap][ci] for the 56x56, Cin = Cout =
+// 64 layers.  The LDS-DMA wgrad (csrc/wgrad_dma.hip) re-fetches the input once
+// per tap (9x the tensor through LDS, 205 us per layer); here a block walks a
+// contiguous run of 4-row tiles (one image per block at batch 256), stages each
+// tile's dy rows [224][64] and its input halo [6 x 58][64] ONCE, double-buffered,
+// and all nine taps read shifted windows of the halo.  The reduction index is
+// the pixel, so both operands are read TRANSPOSED (ds_read_b64_tr_b16: 4
+// consecutive pixel rows of one channel per lane, two reads = the 8-pixel K run
+// of v_mfma_f32_32x32x16_bf16).  An 8-pixel run never crosses an image row (56 =
+// 7 x 8), so tap (r, s) of pixel k is halo row k + 2 (k / 56) + 58 r + s and the
+// run stays 8 consecutive LDS rows.  Eight waves: (co half, ci half, K parity),
+// each holding all nine taps of its 32 x 32 block (144 accumulator registers);
+// the two K-parity halves are summed through LDS at the end and every block
+// writes one fp32 slab (fixed-order reduce: wgrad_slab_reduce).
+// LDS rows are 128 B (64 channels), 16-B chunk c of row R at c ^ (((R >> 1) & 1) * 4):
+// any 4 consecutive rows of a transposed read hit distinct banks.
+constexpr int kWgWaves = 8, kWgNT = 64 * kWgWaves;
+constexpr int kWgDyRows = kBM;                      // 224 tile pixels
+constexpr int kWgHRows = 352;                       // 6 x 58 = 348 halo pixels, whole 1-KiB groups
+constexpr int kWgStage = (kWgDyRows + kWgHRows) * 128;  // 73,728 B
+constexpr int kWgIPW = (kWgDyRows + kWgHRows) / 8 / kWgWaves;
+static_assert((kWgDyRows + kWgHRows) % (8 * kWgWaves) == 0, "every wave issues the same DMA count");
+static_assert(4 * 9 * 16 * 64 * 4 <= 2 * kWgStage, "K-parity combine fits the stage buffers");
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+__device__ __forceinline__ v4s_t tr_read(const char* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(p));
+#else
+  return v4s_t{};
+#endif
+}
+
+__device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
+  const uint2 a = __builtin_bit_cast(uint2, lo), b = __builtin_bit_cast(uint2, hi);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+__device__ __forceinline__ int trswz(int R) { return ((R >> 1) & 1) * 4; }
+
+__global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G, const bf16_t* A, float* dw32,
+                                                                  int nimg, int tiles, int per) {
+  constexpr int H = 56, W = 56, WP = 58, TPI = H / 4;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * kWgStage];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int tb = blockIdx.x * per;
+  const int te = min(tiles, tb + per);
+  const i32x4_t rG = rsrc_words(G, static_cast<uint32_t>(tiles) * kWgDyRows * 128u);
+  const i32x4_t rA = rsrc_words(A, static_cast<uint32_t>(nimg) * H * W * 128u);
+
+  // ---- DMA slot i of this wave: stage row R8 < 224 = dy pixel, else halo row R8 - 224
+  // (geometry recomputed per issue: registers go to the 144 accumulators)
+  auto issue = [&](int tile, int buf) {
+    const int img = tile / TPI, r0 = (tile - img * TPI) * 4;
+    char* base = lds + buf * kWgStage;
+#pragma unroll
+    for (int i = 0; i < kWgIPW; ++i) {
+      const int g = wave + i * kWgWaves;
+      lds_void_t* dst = (lds_void_t*)(base + g * 1024);
+      if (8 * g < kWgDyRows) {
+        const int R = 8 * g + (lane >> 3);
+        const int c = (lane & 7) ^ trswz(R);
+        dma16(rG, dst, static_cast<uint32_t>(tile) * (kWgDyRows * 128u) + static_cast<uint32_t>(R * 128 + c * 16));
+      } else {
+        const int R = 8 * g - kWgDyRows + (lane >> 3);
+        const int c = (lane & 7) ^ trswz(R);
+        const int hr = R / WP;
+        const int ih = r0 + hr - 1, iw = R - hr * WP - 1;
+        const bool ok = R < 6 * WP && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+        dma16(rA, dst, ok ? static_cast<uint32_t>(((img * H + ih) * W + iw) * 128 + c * 16) : kOOB);
+      }
+    }
+  };
+
+  // ---- transposed fragment geometry (csrc/wgrad_dma.hip): lane (grp, q, pp)
+  // reads pixel rows k0 + q and k0 + q + 4 (k0 = 16 ks + 8 (lane >> 5)) at the
+  // 8-B column piece 16 (grp & 1) + 4 pp of its 32-channel fragment
+  const int grp = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int cob = wave & 1, cib = (wave >> 1) & 1, kpar = wave >> 2;
+  const int cdy = (32 * cob + 16 * (grp & 1) + 4 * pp) >> 3;
+  const int cin_ = (32 * cib + 16 * (grp & 1) + 4 * pp) >> 3;
+  const int dcol0 = 16 * cdy + 8 * (pp & 1), dcol1 = 16 * (cdy ^ 4) + 8 * (pp & 1);
+  const int acol0 = 16 * cin_ + 8 * (pp & 1), acol1 = 16 * (cin_ ^ 4) + 8 * (pp & 1);
+
+  f32x16_t acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] = f32x16_t{};
+
+  int buf = 0;
+  if (tb < te) issue(tb, 0);
+  for (int tile = tb; tile < te; ++tile) {
+    // every wave is done reading the other buffer (last tile) before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (tile + 1 < te) {
+      issue(tile + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWgIPW) : "memory");  // this tile's DMA retired
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... on every wave
+    asm volatile("" ::: "memory");
+    const char* Dy = lds + buf * kWgStage;
+    const char* Hs = Dy + kWgDyRows * 128;
+#pragma unroll 1
+    for (int j = 0; j < 7; ++j) {
+      const int k0 = 16 * (2 * j + kpar) + 8 * (lane >> 5);
+      const int Rd = k0 + q;
+      const char* pd = Dy + Rd * 128 + (trswz(Rd) ? dcol1 : dcol0);
+      const bf16x8_t gf = frag8(tr_read(pd), tr_read(pd + 512));
+      const int B = k0 + 2 * (k0 / W) + q;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int R = B + (tap / 3) * WP + (tap % 3);
+        const char* pa = Hs + R * 128 + (trswz(R) ? acol1 : acol0);
+        const bf16x8_t af = frag8(tr_read(pa), tr_read(pa + 512));
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf, af, acc[tap], 0, 0, 0);
+      }
+    }
+    buf ^= 1;
+  }
+
+  // ---- K-parity halves summed through LDS, then one fp32 slab per block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* X = reinterpret_cast<float*>(lds);
+  const int pw = wave & 3;  // (cob, cib) index shared by the two K-parity partners
+  if (kpar) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) X[((pw * 9 + tap) * 16 + r) * 64 + lane] = acc[tap][r];
+  }
+  __syncthreads();
+  if (!kpar) {
+    float* slab = dw32 + static_cast<int64_t>(blockIdx.x) * 64 * 576;
+    const int fh = lane >> 5, fr = lane & 31;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[tap][r] + X[((pw * 9 + tap) * 16 + r) * 64 + lane];
+        const int co = 32 * cob + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        __builtin_nontemporal_store(v, slab + co * 576 + tap * 64 + 32 * cib + fr);
+      }
+  }
+}
+
+int wg_blocks(int tiles, int* per) {
+  const int p = (tiles + 255) / 256;
+  *per = p;
+  return (tiles + p - 1) / p;
+}
+
 }  // namespace
 
 void set_halo3x3(int on) { g_halo = on; }
@@ -270,6 +431,28 @@ hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s) {
   if (static_cast<int64_t>(p.a_rows) * p.Cin * 2 >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   if (p.Cin == 64 && W == 56 && H % 4 == 0 && p.N % 64 == 0) return launch<64, 64, 4, true>(p, epi, H, W, s);
   return hipErrorInvalidValue;
+}
+
+// fp32 slabs the halo weight gradient writes (0 = shape not served here)
+int halo3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {
+  if (!g_halo || stride != 1 || Hin != 56 || Win != 56 || Cin != 64 || Cout != 64 || Nb <= 0) return 0;
+  int per;
+  return wg_blocks(Nb * 14, &per);
+}
+
+// dw32: >= halo3x3_wgrad_slabs(...) x 64 x 576 fp32; hipErrorInvalidValue = "not here"
+hipError_t halo3x3_wgrad(const void* G, const void* A, float* dw32, int64_t dw32_floats, int Nb, int Hin, int Win,
+                         int Cin, int Cout, int stride, int* nslabs, hipStream_t s) {
+  const int n = halo3x3_wgrad_slabs(Nb, Hin, Win, Cin, Cout, stride);
+  if (n == 0 || dw32_floats < static_cast<int64_t>(n) * 64 * 576) return hipErrorInvalidValue;
+  if (static_cast<int64_t>(Nb) * 56 * 56 * 128 >= (int64_t(1) << 32)) return hipErrorInvalidValue;
+  const int tiles = Nb * 14;
+  int per;
+  const int grid = wg_blocks(tiles, &per);
+  hipLaunchKernelGGL(halo3x3_wgrad_kernel, dim3(grid), dim3(kWgNT), 0, s, static_cast<const bf16_t*>(G),
+                     static_cast<const bf16_t*>(A), dw32, Nb, tiles, per);
+  *nslabs = grid;
+  return hipGetLastError();
 }
 }  // namespace gemm
 

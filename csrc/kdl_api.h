@@ -248,10 +248,13 @@ int conv1x1_wgrad_splits(int M, int N, int K);
 // result goes to dW (bf16) if given, else as fp32 into the first [N, K] of dw32.
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s);
-// 3x3 / pad 1: dW[Cout][3][3][Cin] = sum_m G[m, :]^T pro(A)_tap(m); slabs as conv1x1_wgrad with
-// M = Nb * Ho * Wo, N = Cout, K = 9 * Cin.
-hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
-                         int Nb, int Hin, int Win, int Cin, int Cout, int stride, hipStream_t s);
+// 3x3 / pad 1: dW[Cout][3][3][Cin] = sum_m G[m, :]^T pro(A)_tap(m); dw32 holds
+// conv3x3_wgrad_slabs(...) x [Cout, 9 Cin] fp32 (dw32_floats: its size; a smaller
+// workspace of conv1x1_wgrad_splits(M, Cout, 9 Cin) slabs keeps the implicit GEMM).
+int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride);
+hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, int64_t dw32_floats,
+                         void* dW, float scale, int Nb, int Hin, int Win, int Cin, int Cout, int stride,
+                         hipStream_t s);
 
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 

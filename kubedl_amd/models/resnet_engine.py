@@ -342,14 +342,15 @@ class HipKernels:
 
     def wgrad3x3(self, g, x, stride, dW):
         """3x3 pad-1 weight gradient straight into ``dW`` (channels_last = OHWI):
-        LDS-DMA implicit GEMM (csrc/wgrad_dma.hip) into split-M slabs + reduce."""
+        the 56x56 stage's input halo kernel (csrc/halo3x3.hip) or the LDS-DMA
+        implicit GEMM (csrc/wgrad_dma.hip), into fp32 slabs + fixed-order reduce."""
         n, cout, ho, wo = g.shape
         _, cin, h, w = x.shape
         M = n * ho * wo
-        key = (M, cout, 9 * cin)
+        key = (M, cout, 9 * cin, h, stride)
         dw32 = self._dw32.get(key)
         if dw32 is None:
-            slabs = self.ext.conv1x1_wgrad_splits(M, cout, 9 * cin)
+            slabs = self.ext.conv3x3_wgrad_slabs(n, h, w, cin, cout, stride)
             dw32 = self._dw32[key] = torch.empty(slabs * cout * 9 * cin, device=g.device)
         self.ext.conv3x3_wgrad(g, x, None, dw32, dW, 1.0, n, h, w, cin, cout, stride)
 

@@ -208,7 +208,10 @@ def test_bn_workspace_is_self_cleaning():
             outs.append((y.detach(), xi.grad, wi.grad, bi.grad))
         for p_, q_ in zip(*outs):
             torch.testing.assert_close(p_, q_, atol=0, rtol=0)
-    assert torch.count_nonzero(ws[: ws.numel() - 5 * C]) == 0
+    # layout (csrc/bn_fin.h): [32][2C] fwd replicas | [32][2C] bwd | [5C] coefficients |
+    # [32] folded-finalize descriptor | [64] tile counters -- accumulators and counters return to 0
+    assert torch.count_nonzero(ws[: 32 * 4 * C]) == 0
+    assert torch.count_nonzero(ws[-64:]) == 0
 
 
 def test_resnet_hip_vs_torch_backend_step():

@@ -102,3 +102,29 @@ def test_dma_wgrad_3x3(Cin, Cout, H, W, stride):
     ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, Cin, 3, 3), dy.float(), stride=stride, padding=1)
     scale = ref.abs().max().item()
     torch.testing.assert_close(dW.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("nb", [1, 3, 20])
+def test_halo_wgrad_3x3_stage1(nb):
+    """The 56x56 / 64-channel weight gradient on the input-halo kernel (csrc/halo3x3.hip:
+    dy and the input halo staged once per 4-row tile, nine shifted transposed reads)
+    against fp32 truth; bitwise equal to itself on a rerun (fixed-order slabs), and the
+    small conv1x1_wgrad_splits workspace still takes the implicit-GEMM path."""
+    torch.manual_seed(5)
+    ext = _ext()
+    Cin = Cout = 64
+    H = W = 56
+    x = _nhwc(torch.randn(nb, Cin, H, W, device="cuda").bfloat16())
+    dy = _nhwc(torch.randn(nb, Cout, H, W, device="cuda").bfloat16())
+    slabs = ext.conv3x3_wgrad_slabs(nb, H, W, Cin, Cout, 1)
+    assert slabs >= min(nb * 14, 128)  # one slab per halo block (<= 256 blocks)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, Cin, 3, 3), dy.float(), stride=1, padding=1)
+    scale = ref.abs().max().item()
+    outs = []
+    for n_slabs in (slabs, slabs, ext.conv1x1_wgrad_splits(nb * H * W, Cout, 9 * Cin)):
+        ws = torch.full((n_slabs * Cout * 9 * Cin,), float("nan"), device="cuda")
+        dW = _nhwc(torch.empty(Cout, Cin, 3, 3, device="cuda", dtype=torch.bfloat16))
+        ext.conv3x3_wgrad(dy, x, None, ws, dW, 1.0, nb, H, W, Cin, Cout, 1)
+        torch.testing.assert_close(dW.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+        outs.append(dW)
+    assert torch.equal(outs[0], outs[1])
