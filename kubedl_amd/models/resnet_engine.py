@@ -746,6 +746,16 @@ class ResNetEngine:
     def forward(self, x: torch.Tensor):
         K, m = self.K, self.model
         self._fin_descs()
+        self._wt_evt = None
+        if self.side is not None and K.name == "hip":
+            # the data-gradient weight transposes (~0.1 ms, one launch) run on the
+            # side stream under the forward pass instead of heading the backward;
+            # ordered after everything issued so far (last step's optimizer update)
+            self.side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self.side):
+                self._refresh_wt()
+                self._wt_evt = torch.cuda.Event()
+                self._wt_evt.record(self.side)
         st0 = self.bn[m.bn1]
         c0, gemm_stats = K.stem_conv(x, m.conv1.weight, st0)
         x1, idx = K.stem_fwd(c0, st0, gemm_stats)
@@ -831,7 +841,11 @@ class ResNetEngine:
     @torch.no_grad()
     def backward(self, dfeat: torch.Tensor, hw: int) -> None:
         K, m = self.K, self.model
-        self._refresh_wt()
+        if getattr(self, "_wt_evt", None) is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._wt_evt)
+            self._wt_evt = None
+        else:
+            self._refresh_wt()
         x, c0, idx, saved, last = self._saved
         nb = len(self.blocks)
         # gradient at the last block's pre-ReLU sum, plus its bn3 sums
