@@ -32,6 +32,7 @@ for the kernels in tests.
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -345,7 +346,16 @@ class HistGBDT:
         return t
 
     # ------------------------------------------------------------ training
+    def _sync_time(self) -> float:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return time.perf_counter()
+
     def fit(self, X: torch.Tensor, y: torch.Tensor, log_every: int = 0, callback=None):
+        """``stats['setup_s']``: host->device copy, cut fitting, quantisation and the
+        grower's workspaces; ``stats['boost_s']``: the boosting rounds alone (one
+        synchronisation at each end, none inside)."""
+        t0 = self._sync_time()
         X = X.to(self.device)
         y = y.to(self.device)
         if self.cuts is None:
@@ -355,6 +365,7 @@ class HistGBDT:
         pred = self._base(n)
         K = pred.shape[1]
         grower = self._device_grower(bins)
+        t1 = self._sync_time()
         dev_trees = []
         for it in range(self.p.n_estimators):
             g_all, h_all = self._grad_hess(pred, y)
@@ -377,6 +388,9 @@ class HistGBDT:
                 self.trees.append(round_trees)
             if callback is not None:
                 callback(it, pred)
+        t2 = self._sync_time()
+        self.stats["setup_s"] = self.stats.get("setup_s", 0.0) + (t1 - t0)
+        self.stats["boost_s"] = self.stats.get("boost_s", 0.0) + (t2 - t1)
         if grower is not None:
             # the only device->host copy of training: every tree's heap arrays at once
             if dev_trees:
