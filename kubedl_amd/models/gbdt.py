@@ -417,7 +417,10 @@ class HistGBDT:
         per-level split search, partition, histograms; every decision stays on the
         device), so on one rank it is captured once as a HIP graph and replayed:
         the round then costs its kernel time, not the host's launch rate.
-        ``KDL_GBDT_GRAPH=0`` keeps eager launches."""
+        Off by default (``KDL_GBDT_GRAPH=1`` turns it on): on a box that issues
+        launches fast enough the rounds are already kernel-bound -- 2M x 28,
+        depth 6: 349-351 rounds/s replayed vs 363 eager
+        (profiles/r02_gbdt_hist_sweep.txt)."""
         return (grower is not None and self.device.type == "cuda" and _world() == 1
                 and self.p.n_estimators >= 3 and os.environ.get("KDL_GBDT_GRAPH", "0") == "1")
 

@@ -40,7 +40,7 @@ def gemm1x1(A, W, C, M, N, K, epi, shift, ws):
 
 def variants():
     out = [("reg", 0, -1)]
-    for cfg in (0, 1, 2, 3, 4):
+    for cfg in [int(c) for c in os.environ.get("CFGS", "0,1,2,3,4").split(",")]:
         out.append((f"dma{cfg}", 1, cfg))
     return out
 
@@ -103,6 +103,10 @@ if __name__ == "__main__":
         for M, N, K in [(50176, 256, 1024), (12544, 512, 2048), (200704, 128, 512), (50176, 1024, 256),
                         (12544, 2048, 512), (802816, 64, 256)]:
             run_1x1(M, N, K)
+    if which == "n128":
+        run_1x1(200704, 128, 512)
+        for nb, H, Cin, Cout, s in [(256, 28, 128, 128, 1), (256, 56, 128, 128, 2)]:
+            run_3x3(nb, H, Cin, Cout, s)
     if which in ("all", "3x3"):
         for nb, H, Cin, Cout, s in [(256, 56, 64, 64, 1), (256, 28, 128, 128, 1), (256, 14, 256, 256, 1),
                                     (256, 7, 512, 512, 1), (256, 56, 128, 128, 2), (256, 28, 256, 256, 2),
