@@ -1,0 +1,33 @@
+"""Host-side (no GPU) checks of the HIP extension's launch planning: the
+extension imports on a CPU host, and the workspace sizing functions the engine
+allocates by agree with the kernels' dispatch rules."""
+import pytest
+
+
+def _ext():
+    try:
+        from kubedl_amd.ops import _ext
+        return _ext.load()
+    except Exception as e:  # not built in this checkout
+        pytest.skip(f"extension not built: {e}")
+
+
+def test_conv3x3_wgrad_slabs_cover_the_halo_path():
+    ext = _ext()
+    # 56x56 / 64 -> 64 / stride 1: one slab per halo block (one image's 14 tiles per block at batch 256)
+    assert ext.conv3x3_wgrad_slabs(256, 56, 56, 64, 64, 1) == 256
+    assert ext.conv3x3_wgrad_slabs(20, 56, 56, 64, 64, 1) == 140  # 280 tiles, 2 per block
+    assert ext.conv3x3_wgrad_slabs(1, 56, 56, 64, 64, 1) >= 14
+    # every other geometry keeps the implicit GEMM's split-M slab count
+    for nb, h, cin, cout, s in [(256, 28, 128, 128, 1), (256, 56, 128, 128, 2), (256, 7, 512, 512, 1),
+                                (4, 56, 64, 128, 1), (4, 55, 64, 64, 1)]:
+        ho = (h - 1) // s + 1
+        assert ext.conv3x3_wgrad_slabs(nb, h, h, cin, cout, s) == \
+            ext.conv1x1_wgrad_splits(nb * ho * ho, cout, 9 * cin)
+
+
+def test_bn_workspace_layout_size():
+    ext = _ext()
+    # [32][2C] fwd replicas | [32][2C] bwd | [5C] coefficients | [32] finalize descriptor | [64] tile counters
+    for c in (64, 256, 2048):
+        assert ext.bn_workspace_floats(c) == 32 * 4 * c + 5 * c + 32 + 64
