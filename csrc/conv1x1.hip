@@ -626,7 +626,11 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
       const hipError_t h = halo3x3(p, epi, s);
       if (h != hipErrorInvalidValue) return h;
     }
-    const hipError_t e = igemm(p, epi, gather, igemm_pick(p.M, p.N, p.K), s);
+    int cfg = igemm_pick(p.M, p.N, p.K);
+    // 3x3 at N = 512 (7x7 stage): 256x128 tiles (1 block/CU) beat 128x128 by 2-3 %
+    // (86.5-88.5 vs 89-90.6 us, profiles/r02_halo3x3_vs_igemm.jsonl dma1 vs dma2)
+    if (gather == G_CONV3 && p.N == 512 && g_forced_cfg_unset()) cfg = 1;
+    const hipError_t e = igemm(p, epi, gather, cfg, s);
     if (e != hipErrorInvalidValue) return e;
   }
   switch (pick_config(p.M, p.N, p.K, epi)) {

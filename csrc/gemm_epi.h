@@ -95,6 +95,7 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
 // csrc/igemm.hip: LDS-DMA main loop (no A prologue); cfg from igemm_pick.
 // Requires K % 64 == 0 (3x3: Cin % 64 == 0) and 32-bit operand byte offsets.
 int igemm_pick(int M, int N, int K);
+bool g_forced_cfg_unset();  // no KDL_IGEMM_CFG / set_igemm_cfg override in force
 hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t s);
 // csrc/halo3x3.hip: 3x3 stride-1 conv with an LDS-resident input halo (Cin 64 @ 56x56);
 // hipErrorInvalidValue when the geometry is not one it serves

@@ -407,6 +407,10 @@ int g_forced_cfg = [] { const char* e = getenv("KDL_IGEMM_CFG"); return e ? atoi
 void set_igemm_cfg(int cfg) { g_forced_cfg = cfg; }
 
 namespace gemm {
+bool g_forced_cfg_unset() { return g_forced_cfg < 0; }
+}  // namespace gemm
+
+namespace gemm {
 int igemm_pick(int M, int N, int K) {
   const int forced = g_forced_cfg;
   if (forced >= 0 && forced <= 4) {
