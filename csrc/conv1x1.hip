@@ -663,18 +663,41 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
   return igemm(p, a.epi, G_DGRAD2, cfg, s);
 }
 
-int conv1x1_wgrad_splits(int M, int N, int K) {
-  const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
+// Weight-gradient tile (tn x tk): 256 x 256 on the LDS-DMA core where both
+// dimensions allow it (8 waves, 1 block/CU: half the operand bytes per MFMA of
+// 128 x 128).  Standalone the 3x3 stage-3/4 gradients drop 108 -> 84 us and
+// 137 -> 94 us while the 1x1 ones rise 43 -> 55 us, yet in the two-stream step
+// the 1x1 ones gain too (fewer, heavier side-stream blocks): same box, job
+// steps off / 3x3 only / 3x3 + 1x1 = 12,640 / 12,738-12,755 / 12,780-12,794
+// img/s (profiles/r02_wgrad_big_tiles_ab.txt).  KDL_WGRAD_BIG: 0 off, 1 3x3
+// only, 2 (default) both; else 128 or 64 per dimension.
+void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk) {
+  static const int big = [] { const char* e = getenv("KDL_WGRAD_BIG"); return e ? atoi(e) : 2; }();
+  if ((conv3 ? big >= 1 : big >= 2) && gemm_core_mode() != 0 && N % 256 == 0 && K % 256 == 0) {
+    *tn = *tk = 256;
+    return;
+  }
+  *tn = N % 128 == 0 ? 128 : 64;
+  *tk = K % 128 == 0 ? 128 : 64;
+}
+
+int wgrad_splits(int M, int N, int K, bool conv3) {
+  int tn, tk;
+  wgrad_tiles(N, K, conv3, &tn, &tk);
   const int tiles = (N / tn) * (K / tk);
   // ~2 blocks per CU (one round): halves the slab bytes of 4 blocks/CU, measured +1.5% per step.
   // Rounded DOWN so the grid never spills a partial second round onto the CUs
   // (3x3 stage-4: 576 blocks = 1.125 rounds took 1.7x the time of 432).
-  const int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 512; }();
+  // 256 x 256 tiles hold one block per CU: half the blocks per round.
+  int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 512; }();
+  if (tn == 256) target /= 2;
   int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;
   if (splits > max_splits) splits = max_splits;
   return splits < 1 ? 1 : splits;
 }
+
+int conv1x1_wgrad_splits(int M, int N, int K) { return wgrad_splits(M, N, K, false); }
 
 namespace {
 template <int TN_, int TK_>
@@ -726,15 +749,17 @@ hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, v
 }
 
 namespace {
+// big: the workspace holds wgrad_splits(M, N, K, true) slabs (3x3 256-tile configs)
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
-                      hipStream_t s) {
+                      hipStream_t s, bool big = false) {
   if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
-  const int tn = N % 128 == 0 ? 128 : 64, tk = K % 128 == 0 ? 128 : 64;
-  const int splits = conv1x1_wgrad_splits(M, N, K);
+  int tn, tk;
+  wgrad_tiles(N, K, big, &tn, &tk);
+  const int splits = wgrad_splits(M, N, K, big);
   int rps = (M + splits - 1) / splits;
   rps = (rps + WMK - 1) / WMK * WMK;
-  const int tiles_k = K / tk;
+  int tiles_k = K / tk;
   const int nsplit = (M + rps - 1) / rps;
   dim3 grid(nsplit * (N / tn) * tiles_k);
   const bf16_t* g = static_cast<const bf16_t*>(G);
@@ -755,6 +780,11 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     done = e == hipSuccess;
   }
   if (!done) {
+    if (tn > 128 || tk > 128) {  // the register-staged kernel has no 256 tiles: same splits, 128 tiles
+      tn = tk = 128;
+      tiles_k = K / tk;
+      grid = dim3(nsplit * (N / tn) * tiles_k);
+    }
     if (tn == 128 && tk == 128) launch_wgrad<128, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
     else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
     else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
@@ -773,7 +803,9 @@ hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, fl
 
 int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {
   const int Ho = (Hin - 1) / stride + 1, Wo = (Win - 1) / stride + 1;
-  const int dflt = conv1x1_wgrad_splits(Nb * Ho * Wo, Cout, 9 * Cin);
+  const int M = Nb * Ho * Wo;
+  const int a = conv1x1_wgrad_splits(M, Cout, 9 * Cin), b = wgrad_splits(M, Cout, 9 * Cin, true);
+  const int dflt = a > b ? a : b;
   const int halo = halo3x3_wgrad_slabs(Nb, Hin, Win, Cin, Cout, stride);
   return halo > dflt ? halo : dflt;
 }
@@ -790,8 +822,12 @@ hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, fl
     if (e != hipErrorInvalidValue) return e;
   }
   const int Ho = (Hin - 1) / stride + 1, Wo = (Win - 1) / stride + 1;
-  return wgrad_impl(G, A, pro_coef, dw32, dW, scale, Nb * Ho * Wo, Cout, 9 * Cin, Ho, Wo, Hin, Win, stride, G_CONV3,
-                    Cin, s);
+  const int M = Nb * Ho * Wo;
+  // 256 x 256 tiles only when the caller's workspace holds their slab count
+  // (conv3x3_wgrad_slabs); a conv1x1_wgrad_splits-sized one keeps 128 tiles
+  const bool big = dw32_floats >= static_cast<int64_t>(wgrad_splits(M, Cout, 9 * Cin, true)) * Cout * 9 * Cin;
+  return wgrad_impl(G, A, pro_coef, dw32, dW, scale, M, Cout, 9 * Cin, Ho, Wo, Hin, Win, stride, G_CONV3, Cin, s,
+                    big);
 }
 
 }  // namespace kdl

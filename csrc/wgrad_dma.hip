@@ -63,13 +63,19 @@ __device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
   return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
 }
 
-template <int TN_, int TK_, int GATHER, bool PRO>
-__global__ __launch_bounds__(256, 2) void wgrad_dma_kernel(WgParams p) {
+// WN x WK waves: 2 x 2 (4 waves, 2 blocks/CU) for tiles up to 128 x 128; 2 x 4
+// (8 waves of 128 x 64, 1 block/CU, 128 KiB) for 256 x 256 -- half the LDS-DMA
+// bytes per MFMA of a 128 x 128 tile (the operand stream bounds these kernels).
+template <int TN_, int TK_, int GATHER, bool PRO, int WN = 2, int WK = 2>
+__global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dma_kernel(WgParams p) {
+  constexpr int NW = WN * WK;
   constexpr int PN = TN_ / 64, PK = TK_ / 64;  // 64-column panels per operand
   constexpr int PANEL = MK * 128;              // bytes per panel per stage
   constexpr int STAGE = (PN + PK) * PANEL;
-  constexpr int IPW = (PN + PK) * (MK / 8) / 4;  // 1-KiB DMA instructions per wave per stage
-  constexpr int TN = TN_ / 64, TK = TK_ / 64;    // 32x32 MFMA blocks per wave (2 x 2 waves)
+  static_assert((PN + PK) * (MK / 8) % NW == 0, "every wave issues the same DMA count");
+  constexpr int IPW = (PN + PK) * (MK / 8) / NW;  // 1-KiB DMA instructions per wave per stage
+  constexpr int TN = TN_ / WN / 32, TK = TK_ / WK / 32;  // 32x32 MFMA blocks per wave
+  static_assert(TN >= 1 && TK >= 1, "wave tile = whole 32x32 MFMA blocks");
   __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
 
   const int t = threadIdx.x, lane = t & 63;
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_dma_kernel(WgParams p) {
     const int chunk = (col32 + 16 * (grp & 1) + 4 * pp) >> 3;
     return rowb + 16 * (chunk ^ swz) + 8 * (pp & 1);
   };
-  const int wn0 = (wave >> 1) * (TN_ / 2), wk0 = (wave & 1) * (TK_ / 2);
+  const int wn0 = (wave / WK) * (TN_ / WN), wk0 = (wave % WK) * (TK_ / WK);
   int goff[TN], aoff[TK];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
@@ -242,9 +248,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_dma_kernel(WgParams p) {
       }
 }
 
-template <int TN_, int TK_>
+template <int TN_, int TK_, int WN = 2, int WK = 2>
 void launch(const WgParams& p, int grid, hipStream_t s) {
-#define KDL_WGD(G, P) hipLaunchKernelGGL((wgrad_dma_kernel<TN_, TK_, G, P>), dim3(grid), dim3(256), 0, s, p)
+#define KDL_WGD(G, P) \
+  hipLaunchKernelGGL((wgrad_dma_kernel<TN_, TK_, G, P, WN, WK>), dim3(grid), dim3(64 * WN * WK), 0, s, p)
   if (p.pro) {
     if (p.mode == G_CONV3) KDL_WGD(G_CONV3, true);
     else if (p.mode == G_STRIDED) KDL_WGD(G_STRIDED, true);
@@ -270,7 +277,8 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
       static_cast<uint64_t>(p.M) * static_cast<uint64_t>(p.Hout * p.Wout) >= (uint64_t(1) << 32))
     return hipErrorInvalidValue;  // magic-number division range
   const int grid = nsplit * (p.N / tn) * (p.K / tk);
-  if (tn == 128 && tk == 128) launch<128, 128>(p, grid, s);
+  if (tn == 256 && tk == 256) launch<256, 256, 2, 4>(p, grid, s);
+  else if (tn == 128 && tk == 128) launch<128, 128>(p, grid, s);
   else if (tn == 128) launch<128, 64>(p, grid, s);
   else if (tk == 128) launch<64, 128>(p, grid, s);
   else launch<64, 64>(p, grid, s);

@@ -139,7 +139,7 @@ def run_wgrad_3x3(nb, H, Cin, Cout, stride, rounds=3):
     Ho = (H - 1) // stride + 1
     dy = torch.randn(nb, Ho, Ho, Cout, device=dev).bfloat16().permute(0, 3, 1, 2)
     M = nb * Ho * Ho
-    ws = torch.empty(ext.conv1x1_wgrad_splits(M, Cout, 9 * Cin) * Cout * 9 * Cin, device=dev)
+    ws = torch.empty(ext.conv3x3_wgrad_slabs(nb, H, H, Cin, Cout, stride) * Cout * 9 * Cin, device=dev)
     dW = torch.empty(Cout, 3, 3, Cin, device=dev, dtype=torch.bfloat16).permute(0, 3, 1, 2)
     res = {}
     for _ in range(rounds):

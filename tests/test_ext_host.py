@@ -18,12 +18,17 @@ def test_conv3x3_wgrad_slabs_cover_the_halo_path():
     assert ext.conv3x3_wgrad_slabs(256, 56, 56, 64, 64, 1) == 256
     assert ext.conv3x3_wgrad_slabs(20, 56, 56, 64, 64, 1) == 140  # 280 tiles, 2 per block
     assert ext.conv3x3_wgrad_slabs(1, 56, 56, 64, 64, 1) >= 14
-    # every other geometry keeps the implicit GEMM's split-M slab count
-    for nb, h, cin, cout, s in [(256, 28, 128, 128, 1), (256, 56, 128, 128, 2), (256, 7, 512, 512, 1),
-                                (4, 56, 64, 128, 1), (4, 55, 64, 64, 1)]:
+    # every other geometry: the implicit GEMM's split-M slab count -- at 128 x 128 tiles the
+    # 1x1 rule's, at 256 x 256 tiles (Cin, Cout % 256 == 0) one round of one block per CU
+    for nb, h, cin, cout, s in [(256, 28, 128, 128, 1), (256, 56, 128, 128, 2), (4, 56, 64, 128, 1),
+                                (4, 55, 64, 64, 1)]:
         ho = (h - 1) // s + 1
         assert ext.conv3x3_wgrad_slabs(nb, h, h, cin, cout, s) == \
             ext.conv1x1_wgrad_splits(nb * ho * ho, cout, 9 * cin)
+    for nb, h, c, s, tiles in [(256, 14, 256, 1, 9), (256, 7, 512, 1, 36), (256, 14, 512, 2, 36)]:
+        ho = (h - 1) // s + 1
+        assert ext.conv3x3_wgrad_slabs(nb, h, h, c, c, s) == 256 // tiles
+        assert ext.conv3x3_wgrad_slabs(nb, h, h, c, c, s) >= ext.conv1x1_wgrad_splits(nb * ho * ho, c, 9 * c)
 
 
 def test_bn_workspace_layout_size():

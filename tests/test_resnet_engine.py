@@ -278,7 +278,10 @@ def test_engine_bn_finalize_in_gemm_matches_kernel_finalize(monkeypatch):
     fused = rel(results[2][1], results[0][1])
     worst = sorted(fused, key=lambda n: -fused[n])[:8]
     report = "; ".join(f"{n}: fused {fused[n]:.2e} noise {noise[n]:.2e}" for n in worst)
-    assert abs(results[2][0] - results[0][0]) < 1e-3 * max(1.0, abs(results[0][0])), report
+    # forward BN statistics are replica-atomic sums in both modes: the loss moves by
+    # ~1e-3 relative between two runs of one mode at this tiny batch (16 x 112 px)
+    loss_noise = abs(results[1][0] - results[0][0])
+    assert abs(results[2][0] - results[0][0]) < max(3e-3 * max(1.0, abs(results[0][0])), 3 * loss_noise), report
     for n in fused:
         assert fused[n] <= 3 * noise[n] + 2e-3, report
     bnoise = rel(results[1][2], results[0][2])

@@ -44,7 +44,7 @@ def _wgrad1x1(g, x, coef, N, K, Ho, Wo, H, Wd, stride, scale=1.0):
     return dwb
 
 
-@pytest.mark.parametrize("N,K", [(64, 64), (128, 256), (256, 64), (64, 128), (512, 2048)])
+@pytest.mark.parametrize("N,K", [(64, 64), (128, 256), (256, 64), (64, 128), (512, 2048), (256, 256), (1024, 512)])
 @pytest.mark.parametrize("stride,pro", [(1, False), (2, True), (1, True), (2, False)])
 def test_dma_wgrad_1x1(N, K, stride, pro):
     torch.manual_seed(4)
@@ -65,7 +65,7 @@ def test_dma_wgrad_1x1(N, K, stride, pro):
     assert torch.equal(dw, _wgrad1x1(g, x, coef, N, K, Ho, Wo, H, Wd, stride))  # deterministic
 
 
-@pytest.mark.parametrize("N,K", [(64, 64), (256, 128)])
+@pytest.mark.parametrize("N,K", [(64, 64), (256, 128), (256, 512)])
 def test_dma_wgrad_many_splits_matches_register_kernel(N, K):
     torch.manual_seed(5)
     ext = _ext()
@@ -87,7 +87,8 @@ def test_dma_wgrad_many_splits_matches_register_kernel(N, K):
 
 
 @pytest.mark.parametrize("Cin,Cout,H,W,stride", [(64, 64, 12, 10, 1), (128, 64, 9, 9, 2), (64, 128, 28, 27, 1),
-                                                 (256, 128, 7, 7, 1), (128, 256, 14, 14, 2)])
+                                                 (256, 128, 7, 7, 1), (128, 256, 14, 14, 2),
+                                                 (256, 256, 14, 14, 1), (256, 512, 13, 13, 2), (512, 512, 7, 7, 1)])
 def test_dma_wgrad_3x3(Cin, Cout, H, W, stride):
     torch.manual_seed(2)
     ext = _ext()
@@ -96,12 +97,15 @@ def test_dma_wgrad_3x3(Cin, Cout, H, W, stride):
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     dy = _nhwc(torch.randn(nb, Cout, Ho, Wo, device="cuda").bfloat16())
     M = nb * Ho * Wo
-    ws = torch.empty(ext.conv1x1_wgrad_splits(M, Cout, 9 * Cin) * Cout * 9 * Cin, device="cuda")
-    dW = _nhwc(torch.empty(Cout, Cin, 3, 3, device="cuda", dtype=torch.bfloat16))
-    ext.conv3x3_wgrad(dy, x, None, ws, dW, 1.0, nb, H, W, Cin, Cout, stride)
     ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, Cin, 3, 3), dy.float(), stride=stride, padding=1)
     scale = ref.abs().max().item()
-    torch.testing.assert_close(dW.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
+    # a conv1x1_wgrad_splits-sized workspace (128 x 128 tiles) and the engine's
+    # conv3x3_wgrad_slabs-sized one (256 x 256 tiles where Cin, Cout % 256 == 0)
+    for slabs in (ext.conv1x1_wgrad_splits(M, Cout, 9 * Cin), ext.conv3x3_wgrad_slabs(nb, H, W, Cin, Cout, stride)):
+        ws = torch.full((slabs * Cout * 9 * Cin,), float("nan"), device="cuda")
+        dW = _nhwc(torch.empty(Cout, Cin, 3, 3, device="cuda", dtype=torch.bfloat16))
+        ext.conv3x3_wgrad(dy, x, None, ws, dW, 1.0, nb, H, W, Cin, Cout, stride)
+        torch.testing.assert_close(dW.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("nb", [1, 3, 20])
