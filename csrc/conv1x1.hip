@@ -689,7 +689,11 @@ int wgrad_splits(int M, int N, int K, bool conv3) {
   // Rounded DOWN so the grid never spills a partial second round onto the CUs
   // (3x3 stage-4: 576 blocks = 1.125 rounds took 1.7x the time of 432).
   // 256 x 256 tiles hold one block per CU: half the blocks per round.
-  int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 512; }();
+  // With the side stream's gradients overlapping the main stream, FEWER blocks
+  // win: they leave CUs to the critical path (job step, same box, 256x256 tiles
+  // at half the target: 1024 -> 12,460, 512 -> 12,830, 384 -> 13,047, 320 ->
+  // 13,078, 256 -> 12,933, 192 -> 12,715 img/s; profiles/r02_wgrad_blocks_sweep.txt)
+  int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 320; }();
   if (tn == 256) target /= 2;
   int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;

@@ -1,6 +1,8 @@
 """Host-side (no GPU) checks of the HIP extension's launch planning: the
 extension imports on a CPU host, and the workspace sizing functions the engine
 allocates by agree with the kernels' dispatch rules."""
+import os
+
 import pytest
 
 
@@ -25,9 +27,10 @@ def test_conv3x3_wgrad_slabs_cover_the_halo_path():
         ho = (h - 1) // s + 1
         assert ext.conv3x3_wgrad_slabs(nb, h, h, cin, cout, s) == \
             ext.conv1x1_wgrad_splits(nb * ho * ho, cout, 9 * cin)
+    target = int(os.environ.get("KDL_WGRAD_BLOCKS", "320")) // 2  # 256x256 tiles: one block per CU
     for nb, h, c, s, tiles in [(256, 14, 256, 1, 9), (256, 7, 512, 1, 36), (256, 14, 512, 2, 36)]:
         ho = (h - 1) // s + 1
-        assert ext.conv3x3_wgrad_slabs(nb, h, h, c, c, s) == 256 // tiles
+        assert ext.conv3x3_wgrad_slabs(nb, h, h, c, c, s) == max(1, target // tiles)
         assert ext.conv3x3_wgrad_slabs(nb, h, h, c, c, s) >= ext.conv1x1_wgrad_splits(nb * ho * ho, c, 9 * c)
 
 
