@@ -410,8 +410,15 @@ __global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G
   }
 }
 
+// blocks of the halo weight gradient: at most KDL_HALO_WG_BLOCKS (default 256 =
+// one per CU); it runs on the side stream beside the main stream's kernels
 int wg_blocks(int tiles, int* per) {
-  const int p = (tiles + 255) / 256;
+  static const int cap = [] {
+    const char* e = getenv("KDL_HALO_WG_BLOCKS");
+    const int v = e ? atoi(e) : 256;
+    return v < 8 ? 8 : v;
+  }();
+  const int p = (tiles + cap - 1) / cap;
   *per = p;
   return (tiles + p - 1) / p;
 }
