@@ -729,7 +729,9 @@ namespace {
 // the columns alone would leave the chip idle (chunk partials first).
 hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t* dW, hipStream_t s) {
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
-  int groups = (2048 + rgrid - 1) / rgrid;            // y-blocks to reach ~2048 blocks
+  // y-blocks to reach ~KDL_WGRAD_RED_BLOCKS (2048) blocks in the first pass
+  static const int red_target = [] { const char* e = getenv("KDL_WGRAD_RED_BLOCKS"); return e ? atoi(e) : 2048; }();
+  int groups = (red_target + rgrid - 1) / rgrid;
   const int by_work = (nsplit + 31) / 32;             // >= 2 slabs per thread in pass 1
   if (groups > by_work) groups = by_work;
   if (groups <= 1) {
