@@ -73,6 +73,11 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackChunk* __restrict__
 // per-tap slices of the 3x3 weights W[Cout][3][3][Cin] -> Wd[Cin][3][3][Cout]
 // (taps reversed) that the data-gradient GEMMs read as their B operand.  One
 // launch per step replaces one ``.t().contiguous()`` copy kernel per conv.
+// One 64 x 64 bf16 tile per block: each thread moves a 16-element run of one
+// row in (two 16-B loads) and a 16-element run of one column out (two 16-B
+// stores) when the run is in bounds and 16-B aligned, element-wise otherwise.
+// (Element-wise everywhere moved the step's 51 MB at ~1 TB/s; the launch runs on
+// the side stream under the forward's memory-bound stem kernels.)
 __global__ __launch_bounds__(256) void transpose_tiles_kernel(const TransposeTile* __restrict__ tiles) {
   __shared__ bf16_t sh[64][64 + 2];
   const TransposeTile tt = tiles[blockIdx.x];
@@ -80,19 +85,45 @@ __global__ __launch_bounds__(256) void transpose_tiles_kernel(const TransposeTil
   const int lr = t >> 2, lc = (t & 3) * 16;  // 64 rows x 4 threads x 16 elements
   {
     const int r = tt.r0 + lr;
+    const bf16_t* src = tt.src + static_cast<int64_t>(r) * tt.src_ld + tt.c0 + lc;
+    if (r < tt.rows && tt.c0 + lc + 16 <= tt.cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      const uint4 a = reinterpret_cast<const uint4*>(src)[0], b = reinterpret_cast<const uint4*>(src)[1];
+      const bf16_t* pa = reinterpret_cast<const bf16_t*>(&a);
+      const bf16_t* pb = reinterpret_cast<const bf16_t*>(&b);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int c = tt.c0 + lc + j;
-      sh[lr][lc + j] = (r < tt.rows && c < tt.cols) ? tt.src[static_cast<int64_t>(r) * tt.src_ld + c] : bf16_t(0);
+      for (int j = 0; j < 8; ++j) {
+        sh[lr][lc + j] = pa[j];
+        sh[lr][lc + 8 + j] = pb[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int c = tt.c0 + lc + j;
+        sh[lr][lc + j] = (r < tt.rows && c < tt.cols) ? tt.src[static_cast<int64_t>(r) * tt.src_ld + c] : bf16_t(0);
+      }
     }
   }
   __syncthreads();
   const int c = tt.c0 + lr;  // destination row = source column
   if (c < tt.cols) {
+    bf16_t* dst = tt.dst + static_cast<int64_t>(c) * tt.dst_ld + tt.r0 + lc;
+    if (tt.r0 + lc + 16 <= tt.rows && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      uint4 a, b;
+      bf16_t* pa = reinterpret_cast<bf16_t*>(&a);
+      bf16_t* pb = reinterpret_cast<bf16_t*>(&b);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int r = tt.r0 + lc + j;
-      if (r < tt.rows) tt.dst[static_cast<int64_t>(c) * tt.dst_ld + r] = sh[lc + j][lr];
+      for (int j = 0; j < 8; ++j) {
+        pa[j] = sh[lc + j][lr];
+        pb[j] = sh[lc + 8 + j][lr];
+      }
+      reinterpret_cast<uint4*>(dst)[0] = a;
+      reinterpret_cast<uint4*>(dst)[1] = b;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int r = tt.r0 + lc + j;
+        if (r < tt.rows) tt.dst[static_cast<int64_t>(c) * tt.dst_ld + r] = sh[lc + j][lr];
+      }
     }
   }
 }
