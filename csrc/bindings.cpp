@@ -1212,6 +1212,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 pad-1 conv weight gradient (implicit GEMM, split-M slabs)");
   m.def("conv3x3_wgrad_slabs", &conv3x3_wgrad_slabs, "fp32 [Cout, 9 Cin] slabs conv3x3_wgrad may write (its fastest path)");
+  m.def("set_wgrad_big", &kdl::set_wgrad_big, "256x256 weight-gradient tiles: 0 off, 1 3x3 only, 2 3x3 + 1x1");
   m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad");
   m.def("bn_coef_offset", &bn_coef_offset, "float offset of the coefficient block in a BN workspace");
   m.def("bn_stage_fwd_stats", &bn_stage_fwd_stats, "BN forward statistics into the workspace replicas");

@@ -669,10 +669,14 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
 // 137 -> 94 us while the 1x1 ones rise 43 -> 55 us, yet in the two-stream step
 // the 1x1 ones gain too (fewer, heavier side-stream blocks): same box, job
 // steps off / 3x3 only / 3x3 + 1x1 = 12,640 / 12,738-12,755 / 12,780-12,794
-// img/s (profiles/r02_wgrad_big_tiles_ab.txt).  KDL_WGRAD_BIG: 0 off, 1 3x3
-// only, 2 (default) both; else 128 or 64 per dimension.
+// img/s (profiles/r02_wgrad_big_tiles_ab.txt).  Without that overlap (the CTR
+// tower's weight gradients) the 1x1 ones stay on 128 tiles (783 vs 802 steps/s).
+// KDL_WGRAD_BIG: 0 off, 1 3x3 only (default), 2 both -- the ResNet engine selects
+// 2 when its weight-gradient stream is on (set_wgrad_big, before its workspaces
+// are sized); else 128 or 64 per dimension.
+int g_wgrad_big = [] { const char* e = getenv("KDL_WGRAD_BIG"); return e ? atoi(e) : -1; }();
 void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk) {
-  static const int big = [] { const char* e = getenv("KDL_WGRAD_BIG"); return e ? atoi(e) : 2; }();
+  const int big = g_wgrad_big < 0 ? 1 : g_wgrad_big;
   if ((conv3 ? big >= 1 : big >= 2) && gemm_core_mode() != 0 && N % 256 == 0 && K % 256 == 0) {
     *tn = *tk = 256;
     return;
@@ -702,6 +706,12 @@ int wgrad_splits(int M, int N, int K, bool conv3) {
 }
 
 int conv1x1_wgrad_splits(int M, int N, int K) { return wgrad_splits(M, N, K, false); }
+
+// the caller's preference (an explicit KDL_WGRAD_BIG wins)
+void set_wgrad_big(int mode) {
+  static const bool env = getenv("KDL_WGRAD_BIG") != nullptr;
+  if (!env) g_wgrad_big = mode;
+}
 
 namespace {
 template <int TN_, int TK_>

@@ -75,9 +75,10 @@ _WS = {}
 
 def _wgrad_workspace(ext, M, N, K, device):
     key = (M, N, K, str(device))
+    need = ext.conv1x1_wgrad_splits(M, N, K) * N * K  # (the tile mode may change: set_wgrad_big)
     ws = _WS.get(key)
-    if ws is None:
-        ws = _WS[key] = torch.empty(ext.conv1x1_wgrad_splits(M, N, K) * N * K, device=device)
+    if ws is None or ws.numel() < need:
+        ws = _WS[key] = torch.empty(need, device=device)
     return ws
 
 

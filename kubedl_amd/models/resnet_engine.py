@@ -333,10 +333,10 @@ class HipKernels:
         _, cin, h, w = x.shape
         M = n * ho * wo
         key = (M, cout, cin)  # split-M slab workspace, shared by the layers of one shape (stream-ordered)
+        need = self.ext.conv1x1_wgrad_splits(M, cout, cin) * cout * cin  # (tile mode may change: set_wgrad_big)
         dw32 = self._dw32.get(key)
-        if dw32 is None:
-            slabs = self.ext.conv1x1_wgrad_splits(M, cout, cin)
-            dw32 = self._dw32[key] = torch.empty(slabs * cout * cin, device=g.device)
+        if dw32 is None or dw32.numel() < need:
+            dw32 = self._dw32[key] = torch.empty(need, device=g.device)
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
                                M, cout, cin, ho, wo, h, w, stride)
 
@@ -348,10 +348,10 @@ class HipKernels:
         _, cin, h, w = x.shape
         M = n * ho * wo
         key = (M, cout, 9 * cin, h, stride)
+        need = self.ext.conv3x3_wgrad_slabs(n, h, w, cin, cout, stride) * cout * 9 * cin
         dw32 = self._dw32.get(key)
-        if dw32 is None:
-            slabs = self.ext.conv3x3_wgrad_slabs(n, h, w, cin, cout, stride)
-            dw32 = self._dw32[key] = torch.empty(slabs * cout * 9 * cin, device=g.device)
+        if dw32 is None or dw32.numel() < need:
+            dw32 = self._dw32[key] = torch.empty(need, device=g.device)
         self.ext.conv3x3_wgrad(g, x, None, dw32, dW, 1.0, n, h, w, cin, cout, stride)
 
     def stem_wgrad(self, dc0, x, dw):
@@ -639,6 +639,9 @@ class ResNetEngine:
         if self.K.name == "hip" and os.environ.get("KDL_WGRAD_STREAM", "1") == "1":
             from kubedl_amd.ops.streams import side_stream
             self.side = side_stream(self.dev, int(os.environ.get("KDL_SIDE_PRIO", "0")))  # (ops/streams.py)
+            # overlapped with the main stream, the 1x1 weight gradients gain from 256x256
+            # tiles too (fewer, heavier side-stream blocks; csrc/conv1x1.hip wgrad_tiles)
+            self.K.ext.set_wgrad_big(2)
 
     def _refresh_wt(self) -> None:
         """HIP path: the data-gradient GEMMs' B operands -- W^T of every 1x1 conv
