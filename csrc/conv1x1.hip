@@ -670,7 +670,8 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
 // the 1x1 ones gain too (fewer, heavier side-stream blocks): same box, job
 // steps off / 3x3 only / 3x3 + 1x1 = 12,640 / 12,738-12,755 / 12,780-12,794
 // img/s (profiles/r02_wgrad_big_tiles_ab.txt).  Without that overlap (the CTR
-// tower's weight gradients) the 1x1 ones stay on 128 tiles (783 vs 802 steps/s).
+// tower's weight gradients) the 1x1 ones stay on 128 tiles (CTR samples/s equal
+// within run-to-run noise either way: 3.19-3.33 M vs 3.12-3.31 M).
 // KDL_WGRAD_BIG: 0 off, 1 3x3 only (default), 2 both -- the ResNet engine selects
 // 2 when its weight-gradient stream is on (set_wgrad_big, before its workspaces
 // are sized); else 128 or 64 per dimension.
