@@ -7,7 +7,9 @@
 // layers sit on that stream, not on the MFMAs.  Here a tile is TH full output
 // rows of one image (BM = TH * W = 224 pixels); its (TH + 2) x (W + 2) input
 // halo (zero padding = buffer-OOB loads) lands in LDS once and the nine taps
-// read shifted 32-pixel fragments from it.  The weights of the block's BN
+// read shifted 32-pixel fragments from it (the weight gradient of the same
+// layers, halo3x3_wgrad_kernel below, stages dy rows and the halo the same way
+// and reads both transposed).  The weights of the block's BN
 // output channels for all nine taps (9 * Cin * BN bf16 = 72 KiB) stay
 // resident in LDS for the block's lifetime (persistent blocks, one N tile per
 // block), so per tile the only DMA is the halo:

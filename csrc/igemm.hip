@@ -348,7 +348,10 @@ hipError_t launch(const GemmParams& p, hipStream_t s) {
   }
   const int tiles_m = (q.M + BM - 1) / BM;
   const int tiles_n = q.N / BN;
-  const int target = 256 * BPC;  // one round of resident blocks
+  // one round of resident blocks (KDL_IGEMM_ROUNDS > 1: that many rounds -- shorter
+  // per-block tile lists, for the two-stream step's contention; A/B knob)
+  static const int rounds = [] { const char* e = getenv("KDL_IGEMM_ROUNDS"); const int v = e ? atoi(e) : 1; return v < 1 ? 1 : v; }();
+  const int target = 256 * BPC * rounds;
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
