@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import copy
 import datetime as _dt
+import re
+from fractions import Fraction
 from typing import Any, Dict, List, Optional
 
 # ---- condition types (types.go:101-127)
@@ -306,6 +308,35 @@ def pod_template_gpus(template: Dict[str, Any]) -> int:
 
 HBM_RESOURCE = "kubedl.io/hbm-gb"
 
+# Kubernetes resource quantities (k8s.io/apimachinery resource.Quantity syntax)
+QUANTITY_SUFFIX = {"": 1, "m": Fraction(1, 1000), "k": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12,
+                   "P": 10 ** 15, "E": 10 ** 18, "Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40,
+                   "Pi": 2 ** 50, "Ei": 2 ** 60}
+_QRE = re.compile(r"^([+-]?[0-9.]+(?:[eE][+-]?[0-9]+)?)(Ki|Mi|Gi|Ti|Pi|Ei|m|k|M|G|T|P|E)?$")
+
+
+def parse_quantity(q) -> Fraction:
+    if isinstance(q, (int, float)):
+        return Fraction(q)
+    m = _QRE.match(str(q).strip())
+    if not m:
+        raise ValueError(f"bad quantity {q!r}")
+    return Fraction(m.group(1)) * QUANTITY_SUFFIX[m.group(2) or ""]
+
+
+def parse_hbm_gb(v) -> float:
+    """A ``kubedl.io/hbm-gb`` value in GB: a bare number is GB; a quantity with
+    a byte suffix (``32G``, ``32Gi``, ``512Mi``) is bytes converted to GB.
+    Raises ValueError on garbage or a negative request."""
+    s = str(v).strip()
+    q = parse_quantity(s)
+    m = _QRE.match(s)
+    suf = m.group(2) if m else None
+    gb = float(q) if not suf or suf == "m" else float(q) / 1e9
+    if gb < 0:
+        raise ValueError(f"negative {HBM_RESOURCE} request {v!r}")
+    return gb
+
 
 def hbm_requested(container: Dict[str, Any]) -> float:
     """``kubedl.io/hbm-gb`` of a container (limits, else requests), in GB."""
@@ -313,7 +344,7 @@ def hbm_requested(container: Dict[str, Any]) -> float:
     for section in ("limits", "requests"):
         d = res.get(section) or {}
         if HBM_RESOURCE in d:
-            return float(str(d[HBM_RESOURCE]))
+            return parse_hbm_gb(d[HBM_RESOURCE])
     return 0.0
 
 

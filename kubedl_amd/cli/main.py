@@ -2,7 +2,8 @@
 
 Server (``main.go`` flags kept by name, SURVEY.md §1 L0)::
 
-    python -m kubedl_amd.cli manager [--metrics-addr :8443] [--gang-scheduler-name kdl-gang]
+    python -m kubedl_amd.cli manager [--metrics-addr 8443] [--controller-metrics-addr :8080]
+        [--enable-leader-election=true] [--gang-scheduler-name kdl-gang]
         [--max-reconciles N] [--workloads auto|*|TFJob,...] [--object-storage sqlite]
         [--event-storage jsonl] [--region R] [--api-addr 127.0.0.1:8098] [--gpus N]
 
@@ -146,19 +147,26 @@ def cmd_manager(a) -> int:
     import signal
     from kubedl_amd.cli.server import APIServer
     from kubedl_amd.engine.manager import Manager, ManagerOptions
+    from kubedl_amd.metrics import parse_addr
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    port = int(a.metrics_addr.rsplit(":", 1)[-1]) if a.metrics_addr else 0
+    mhost, mport = parse_addr(a.metrics_addr)
+    chost, cport = parse_addr(a.controller_metrics_addr)
     opts = ManagerOptions(home=a.home, durable=True, workloads=a.workloads,
                           gang_scheduler_name=a.gang_scheduler_name,
                           max_reconciles=a.max_reconciles if a.max_reconciles > 0 else 1,
-                          metrics_port=port, gpus=a.gpus, object_storage=a.object_storage,
+                          metrics_port=mport, metrics_host=mhost, controller_metrics_port=cport,
+                          controller_metrics_host=chost, leader_election=a.enable_leader_election,
+                          gpus=a.gpus, object_storage=a.object_storage,
                           event_storage=a.event_storage, region=a.region or os.environ.get("REGION", ""))
+    if a.enable_leader_election:
+        print(f"kdl manager: waiting for leadership of {os.path.join(a.home, 'leader.lock')}", flush=True)
     mgr = Manager(opts).start()
     host, aport = a.api_addr.rsplit(":", 1)
     api = APIServer(mgr, int(aport), host or "127.0.0.1").start()
     print(f"kdl manager up: api http://{host or '127.0.0.1'}:{api.port}  "
           f"controllers={sorted(mgr.loops)}  gpus={mgr.allocator.inv.count if mgr.allocator else 0}  "
-          f"gang={a.gang_scheduler_name or 'off'}", flush=True)
+          f"gang={a.gang_scheduler_name or 'off'}  metrics=:{mport or 'off'}  controller-metrics=:{cport or 'off'}  "
+          f"leader-election={'on' if a.enable_leader_election else 'off'}", flush=True)
     stop = []
     signal.signal(signal.SIGTERM, lambda *_: stop.append(1))
     signal.signal(signal.SIGINT, lambda *_: stop.append(1))
@@ -255,15 +263,29 @@ def cmd_bench_launch(a) -> int:
     return bl(a)
 
 
+def _flag_bool(v) -> bool:
+    """Go flag.Bool syntax: --flag, --flag=true|false|1|0."""
+    if isinstance(v, bool):
+        return v
+    s = str(v).strip().lower()
+    if s in ("1", "t", "true", "yes", "on"):
+        return True
+    if s in ("0", "f", "false", "no", "off"):
+        return False
+    raise argparse.ArgumentTypeError(f"invalid boolean value {v!r}")
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="kdl", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
 
     m = sub.add_parser("manager", help="run the controller manager + node runtime + API server")
-    m.add_argument("--controller-metrics-addr", default=":8080", help="accepted for parity (controller-runtime)")
-    m.add_argument("--metrics-addr", default="", help="kubedl_jobs_* Prometheus endpoint, e.g. :8443")
-    m.add_argument("--enable-leader-election", default=False, action="store_true",
-                   help="accepted for parity; a single-node runtime has one manager")
+    m.add_argument("--controller-metrics-addr", default=":8080",
+                   help="controller-runtime metrics (reconcile / workqueue) endpoint; 0 = off (main.go:54)")
+    m.add_argument("--metrics-addr", default="8443",
+                   help="kubedl_jobs_* Prometheus endpoint: port or [host]:port; 0 = off (main.go:55)")
+    m.add_argument("--enable-leader-election", default=True, nargs="?", const=True, type=_flag_bool,
+                   help="only one manager per --home acts; others wait as standby (main.go:56, default true)")
     m.add_argument("--gang-scheduler-name", default="", help="enable gang scheduling (kdl-gang | kube-batch)")
     m.add_argument("--max-reconciles", type=int, default=1)
     m.add_argument("--workloads", default="auto")

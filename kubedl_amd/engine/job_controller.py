@@ -462,6 +462,23 @@ class JobController:
                   and not p["metadata"].get("deletionTimestamp")]
         if not others:
             return
+        # A peer that failed with a PERMANENT code in the same pass keeps its pod
+        # (and its failure record): no teardown, so the next reconcile fails the
+        # job exactly as the reference's per-pod ExitCode handling would.
+        # Succeeded peers ARE recreated: restarted ranks cannot rendezvous
+        # without them, and they resume from the job's checkpoint.
+        dc = self.controller.get_default_container_name()
+        for p in others:
+            if pod_phase(p) != "Failed":
+                continue
+            code = next((int(((cs.get("state") or {}).get("terminated") or {}).get("exitCode", 0))
+                         for cs in (p.get("status") or {}).get("containerStatuses") or []
+                         if cs.get("name") == dc and (cs.get("state") or {}).get("terminated") is not None),
+                        EXIT_CODE_SENTINEL)
+            if not c.is_retryable_exit_code(code):
+                logger_for_job(job, log).info("no gang restart: %s failed permanently (exit %d)",
+                                              p["metadata"]["name"], code)
+                return
         msg = (f"Restarting all {len(others) + len(deleted)} ranks of {job['metadata']['name']}: "
                f"{', '.join(sorted(deleted))} failed with a retryable exit code")
         logger_for_job(job, log).info(msg)

@@ -41,6 +41,11 @@ class ManagerOptions:
     gang_scheduler_name: str = ""         # --gang-scheduler-name (enables gang when non-empty)
     max_reconciles: int = 1               # --max-reconciles (<=0 -> 1)
     metrics_port: int = 0                 # --metrics-addr port (0 = no HTTP endpoint)
+    metrics_host: str = "127.0.0.1"       # --metrics-addr host part ("" = every interface, as Go's ":8443")
+    controller_metrics_port: int = 0      # --controller-metrics-addr port (controller-runtime metrics)
+    controller_metrics_host: str = "127.0.0.1"
+    leader_election: bool = False         # --enable-leader-election (the CLI defaults it on, main.go:56)
+    leader_wait_s: Optional[float] = None  # standby: how long to wait for leadership (None = forever)
     run_node: bool = True                 # run the local node runtime (scheduler + kubelet)
     gpus: Optional[int] = None            # override GPU inventory
     object_storage: str = ""              # --object-storage (e.g. "sqlite")
@@ -53,7 +58,10 @@ class _KindLoop:
     def __init__(self, mgr: "Manager", reconciler, workers: int):
         self.mgr = mgr
         self.r = reconciler
+        self.name = reconciler.kind.lower()  # controller-runtime names the controller after the kind
         self.queue = RateLimitingQueue()
+        cm = mgr.controller_metrics
+        cm.queues[self.name] = lambda: len(self.queue)
         self.threads = [threading.Thread(target=self._work, name=f"reconcile-{reconciler.kind}-{i}",
                                          daemon=True) for i in range(max(1, workers))]
         self.errors: List[str] = []
@@ -70,20 +78,34 @@ class _KindLoop:
             if key is None:
                 continue
             ns, name = key.split("/", 1)
+            cm = self.mgr.controller_metrics
+            t0 = time.perf_counter()
             try:
                 with trace_range(f"reconcile {self.r.kind} {key}"):
                     res = self.r.reconcile(ns, name)
                 self.queue.forget(key)
                 if res.requeue_after > 0:
                     self.queue.add_after(key, res.requeue_after)
+                    result = "requeue_after"
                 elif res.requeue:
                     self.queue.add_rate_limited(key)
+                    cm.queue_retries.labels(self.name).inc()
+                    result = "requeue"
+                else:
+                    result = "success"
             except Exception as e:  # reconcile error -> rate-limited retry (controller-runtime)
                 logger_for_key(key, log).warning("reconcile %s failed: %s", self.r.kind, e)
                 self.errors.append(f"{key}: {e}")
                 self.queue.add_rate_limited(key)
+                cm.queue_retries.labels(self.name).inc()
+                result = "error"
             finally:
                 self.queue.done(key)
+            cm.observe_reconcile(self.name, time.perf_counter() - t0, result)
+
+    def add(self, key: str) -> None:
+        self.mgr.controller_metrics.queue_adds.labels(self.name).inc()
+        self.queue.add(key)
 
 
 class Manager:
@@ -91,6 +113,17 @@ class Manager:
                  metrics: Optional[MetricsRegistry] = None):
         self.opts = opts or ManagerOptions()
         os.makedirs(self.opts.home, exist_ok=True)
+        # leader election first: a standby opens neither the store nor the node
+        # runtime until it holds the lease (engine/leader.py)
+        self.leader = None
+        if self.opts.leader_election:
+            from kubedl_amd.engine.leader import LeaderLock
+            self.leader = LeaderLock(self.opts.home)
+            if not self.leader.acquire(timeout=self.opts.leader_wait_s):
+                raise TimeoutError(f"not leader: {self.leader.path} held by "
+                                   f"{self.leader.holder().get('holderIdentity', '?')}")
+        from kubedl_amd.metrics.controller_metrics import ControllerMetrics
+        self.controller_metrics = ControllerMetrics()
         db = os.path.join(self.opts.home, "store.db") if self.opts.durable else None
         self.store = store or Store(db)
         self.recorder = EventRecorder(self.store)
@@ -136,6 +169,7 @@ class Manager:
             self.persist = PersistController(self.store, self.opts.home, self.opts.object_storage,
                                              self.opts.event_storage, self.opts.region)
         self.http = None
+        self.ctrl_http = None
         self._started = False
 
     # ------------------------------------------------------------ events -> queues
@@ -146,12 +180,12 @@ class Manager:
             key = f"{md['namespace']}/{md['name']}"
             if etype == ADDED:
                 self.reconcilers[kind].on_owner_create(obj)
-            self.loops[kind].queue.add(key)
+            self.loops[kind].add(key)
         elif kind in ("Pod", "Service"):
             for k, r in self.reconcilers.items():
                 key = r.on_dependent_event(etype, obj)
                 if key is not None:
-                    self.loops[k].queue.add(key)
+                    self.loops[k].add(key)
 
     # ------------------------------------------------------------ lifecycle
     def start(self) -> "Manager":
@@ -165,16 +199,19 @@ class Manager:
             for j in self.store.list(kind):
                 if not c.is_created(j.get("status") or {}):
                     self.reconcilers[kind].on_owner_create(j)
-                loop.queue.add(f"{j['metadata']['namespace']}/{j['metadata']['name']}")
+                loop.add(f"{j['metadata']['namespace']}/{j['metadata']['name']}")
         if self.scheduler:
             self.scheduler.start()
         if self.kubelet:
             self.kubelet.start()
         if self.persist:
             self.persist.start()
+        from kubedl_amd.metrics import start_monitoring
         if self.opts.metrics_port:
-            from kubedl_amd.metrics import start_monitoring
-            self.http = start_monitoring(self.opts.metrics_port, self.metrics)
+            self.http = start_monitoring(self.opts.metrics_port, self.metrics, self.opts.metrics_host)
+        if self.opts.controller_metrics_port:
+            self.ctrl_http = start_monitoring(self.opts.controller_metrics_port, self.controller_metrics,
+                                              self.opts.controller_metrics_host)
         return self
 
     def stop(self) -> None:
@@ -187,12 +224,16 @@ class Manager:
         if self.persist:
             self.persist.stop()
         self._cancel()
-        if self.http is not None:
-            try:
-                self.http.shutdown()
-            except Exception:
-                pass
+        for srv in (self.http, self.ctrl_http):
+            if srv is not None:
+                try:
+                    srv.shutdown()
+                    srv.server_close()
+                except Exception:
+                    pass
         self.store.close()
+        if self.leader is not None:
+            self.leader.release()
 
     def __enter__(self):
         return self.start()

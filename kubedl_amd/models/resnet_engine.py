@@ -878,8 +878,9 @@ class ResNetEngine:
             K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
             self._bn_ready(st2)
             dc2, _ = K.bn_bwd_apply(g2, c2, st2)
-            # conv2 (3x3): weight gradient on MIOpen; stride-1 data gradient on the
-            # implicit-GEMM kernel with bn1's ReLU mask + backward sums fused
+            # conv2 (3x3): weight gradient on the kdl kernels (halo / LDS-DMA implicit
+            # GEMM, side stream); stride-1 data gradient on the implicit-GEMM or halo
+            # kernel with bn1's ReLU mask + backward sums fused
             s = blk.conv2.stride[0]
             if s == 1:
                 with self._on_side(dc2):

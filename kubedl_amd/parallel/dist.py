@@ -129,17 +129,34 @@ def shutdown(info: DistInfo) -> None:
 # (pkg/util/train/train_util.go:18-52) -- instead of 1 (permanent), so an
 # ExitCode job restarts its gang instead of failing on the survivor's symptom.
 COMM_FAILURE_EXIT = 138
-_COMM_MARKERS = ("connection closed by peer", "connection reset by peer", "broken pipe", "nccl", "rccl",
-                 "gloo", "watchdog", "p2p all-reduce", "process group", "timed out")
+# message fragments that only a vanished or hung PEER produces (gloo's TCP pair,
+# RCCL's system/remote errors, the collective watchdog); anything else -- an RCCL
+# usage/argument error, an uninitialised group, a user-code "timed out" -- is a
+# deterministic bug and must fail the job permanently (exit 1), not loop
+# through gang restarts until backoffLimit
+_PEER_GONE = ("connection closed by peer", "connection reset by peer", "broken pipe",
+              "remote process exited", "unhandled system error", "network error",
+              "watchdog caught collective operation timeout")
+_NOT_PEER = ("invalid usage", "invalid argument", "has not been initialized", "not been initialized",
+             "out of memory")
 
 
 def is_comm_failure(exc: BaseException) -> bool:
-    dist_error = getattr(dist, "DistError", None)
-    if dist_error is not None and isinstance(exc, dist_error):
+    """True when ``exc`` means a peer rank is gone (retryable gang restart)."""
+    msg = str(exc).lower()
+    if any(m in msg for m in _NOT_PEER):
+        return False
+    if type(exc).__name__ == "P2PError":  # parallel/p2p.py: peer missed the arrival window
         return True
-    if type(exc).__name__ == "P2PError":
+    net_error = getattr(dist, "DistNetworkError", None)
+    if net_error is not None and isinstance(exc, net_error):
         return True
-    return isinstance(exc, RuntimeError) and any(m in str(exc).lower() for m in _COMM_MARKERS)
+    if not isinstance(exc, (RuntimeError, ConnectionError)):
+        return False
+    if any(m in msg for m in _PEER_GONE):
+        return True
+    # gloo's collective timeout: the peer hung or died without closing its socket
+    return "gloo" in msg and "timed out" in msg
 
 
 def run_rank(main, *args, **kw) -> int:

@@ -32,19 +32,7 @@ from kubedl_amd.api import kinds as K
 from kubedl_amd.utils import k8sutil
 
 # ---------------------------------------------------------------- quantities
-_SUFFIX = {"": 1, "m": Fraction(1, 1000), "k": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12,
-           "P": 10 ** 15, "E": 10 ** 18, "Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40,
-           "Pi": 2 ** 50, "Ei": 2 ** 60}
-_QRE = re.compile(r"^([+-]?[0-9.]+(?:[eE][+-]?[0-9]+)?)(Ki|Mi|Gi|Ti|Pi|Ei|m|k|M|G|T|P|E)?$")
-
-
-def parse_quantity(q) -> Fraction:
-    if isinstance(q, (int, float)):
-        return Fraction(q)
-    m = _QRE.match(str(q).strip())
-    if not m:
-        raise ValueError(f"bad quantity {q!r}")
-    return Fraction(m.group(1)) * _SUFFIX[m.group(2) or ""]
+from kubedl_amd.api.common import QUANTITY_SUFFIX as _SUFFIX, parse_quantity  # noqa: E402,F401
 
 
 def format_quantity(v: Fraction, binary: bool = False) -> str:

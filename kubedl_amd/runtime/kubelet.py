@@ -161,6 +161,22 @@ class PodWorker(threading.Thread):
         return out
 
     # ------------------------------------------------------------ env
+    def _container_hbm(self, ctr: dict) -> float:
+        """This container's HBM cap in GB: its own ``kubedl.io/hbm-gb`` request,
+        else an equal share of what is left of the pod's scheduled slice (the
+        annotation is the SUM over containers, so exporting it whole to every
+        container would let them together exceed the reservation)."""
+        own = c.hbm_requested(ctr)
+        if own:
+            return own
+        slice_gb = (self.pod["metadata"].get("annotations") or {}).get(HBM_ANNOTATION)
+        if not slice_gb:
+            return 0.0
+        ctrs = (self.pod.get("spec") or {}).get("containers") or []
+        asked = [c.hbm_requested(x) for x in ctrs]
+        unset = sum(1 for a in asked if not a)
+        return max(0.0, float(slice_gb) - sum(asked)) / max(1, unset)
+
     def _env(self, ctr: dict, mounts: Dict[str, str], cidx: str) -> Tuple[Dict[str, str], str]:
         env = {k: v for k, v in os.environ.items() if k not in _ENV_DENY}
         pp = env.get("PYTHONPATH", "")
@@ -205,9 +221,9 @@ class PodWorker(threading.Thread):
         env["KDL_NUM_GPUS"] = str(len(self.gpus))
         # HBM slice of a shared GPU (scheduler annotation) or a per-process cap
         # asked on an exclusive GPU: the rank caps its caching allocator to it
-        hbm = (md.get("annotations") or {}).get(HBM_ANNOTATION) or c.hbm_requested(ctr) or ""
+        hbm = self._container_hbm(ctr)
         if hbm:
-            env["KDL_HBM_LIMIT_GB"] = str(hbm)
+            env["KDL_HBM_LIMIT_GB"] = f"{hbm:g}"
         ready = os.path.join(self.sandbox, f"ready.{cidx}")
         env["KDL_READY_FILE"] = ready
         env["KDL_PROGRESS_FILE"] = os.path.join(self.sandbox, f"progress.{cidx}")

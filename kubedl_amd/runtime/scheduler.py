@@ -195,9 +195,15 @@ class NodeScheduler:
             if head_blocked_since is not None and now - head_blocked_since > self.starvation_s:
                 self._mark_unschedulable(pods, "waiting behind an older gang (FIFO after starvation)")
                 continue
-            req = {pod_key(p): pod_gpus(p) for p in pods}
-            hbm = {pod_key(p): pod_hbm(p) for p in pods}
-            alloc = self.alloc.allocate(owner, req, hbm)
+            try:
+                req = {pod_key(p): pod_gpus(p) for p in pods}
+                hbm = {pod_key(p): pod_hbm(p) for p in pods}
+                alloc = self.alloc.allocate(owner, req, hbm)
+            except (ValueError, TypeError) as e:
+                # a malformed request (e.g. kubedl.io/hbm-gb: "lots") fails only its
+                # own unit; the rest of the pass keeps scheduling
+                self._mark_unschedulable(pods, f"invalid resource request: {e}")
+                continue
             if alloc is None:
                 free = len(self.alloc.free)
                 want_hbm = sum(v for k, v in hbm.items() if not req[k])

@@ -4,10 +4,13 @@ Run by the PyTorch launcher (``kubedl_amd.controllers.pytorch``) as one
 process per rank with the KubeDL rendezvous env, or directly by ``bench.py``.
 
 Per step (all on the rank's HIP stream):
-  zero flat grad (one memset) -> forward (MIOpen NHWC convs + fused BN/ReLU
-  HIP kernels) -> fp32 cross-entropy -> backward (bucketed RCCL all-reduce of
-  bf16 gradient slices overlapped with backward) -> one fused SGD-momentum
-  launch (fp32 master, writes bf16 weights).
+  zero flat grad (one memset) -> forward (the explicit engine of
+  models/resnet_engine.py: kdl MFMA conv kernels -- 1x1 GEMMs, implicit-GEMM and
+  halo 3x3, the 7x7 stem -- with BN statistics in their epilogues and fused
+  BN/ReLU HIP kernels) -> fp32 cross-entropy -> backward (kdl data- and
+  weight-gradient kernels, bucketed RCCL all-reduce of bf16 gradient slices
+  overlapped with backward) -> one fused SGD-momentum launch (fp32 master,
+  writes bf16 weights).
 """
 from __future__ import annotations
 
@@ -94,6 +97,7 @@ class ResNetTrainer:
         self.last_loss = None
         self._loss_work = None
         self._loss_sum = None
+        self._loss_div = 1
         # the step runs on a non-blocking stream of its own, never the null
         # stream: with an RCCL process group present the null stream loses the
         # engine's side-stream overlap (-9 %, ops/streams.py); the caller's
@@ -128,20 +132,23 @@ class ResNetTrainer:
         loss = loss.detach().float().reshape(1)
         self.last_loss = loss  # this rank's loss (returned)
         self._loss_sum = loss
+        self._loss_div = 1
         if dist.is_initialized() and _LOSS_ALLREDUCE:
             # the step's loss summed over ranks (reporting); at world 1 this is
             # the collective that keeps the RCCL path exercised in every step
             self._loss_sum = loss.clone()
+            self._loss_div = dist.get_world_size()
             self._loss_work = dist.all_reduce(self._loss_sum, async_op=True)
         return loss
 
     def loss(self) -> torch.Tensor:
-        """The last step's loss summed over ranks (waits for its all-reduce;
-        at world 1 or without a process group: this rank's loss)."""
+        """The last step's loss averaged over ranks (waits for its all-reduce);
+        without the all-reduce (no process group, or KDL_LOSS_ALLREDUCE=0) this
+        rank's own loss -- divided only when the sum actually ran."""
         if self._loss_work is not None:
             self._loss_work.wait()
             self._loss_work = None
-        return self._loss_sum
+        return self._loss_sum / self._loss_div if self._loss_div > 1 else self._loss_sum
 
     def check_transport(self) -> None:
         """Raise if a P2P all-reduce of any step so far timed out.  Call after
@@ -195,7 +202,7 @@ def run(args) -> dict:
         tr.step()
         if steplog.enabled:
             sync(info)
-            steplog.write(i + 1, (time.perf_counter() - t) * 1e3, loss=float(tr.loss().item()) / info.world_size)
+            steplog.write(i + 1, (time.perf_counter() - t) * 1e3, loss=float(tr.loss().item()))
         if ckpt.due(i + 1):
             sync(info)
             tr.check_transport()  # never persist weights of a timed-out all-reduce
@@ -219,7 +226,7 @@ def run(args) -> dict:
     tr.check_transport()
     dt = kdist.all_reduce_max(dt, info)
     nsteps = len(timed)
-    loss = float(tr.loss().item()) / info.world_size if tr.last_loss is not None else float("nan")
+    loss = float(tr.loss().item()) if tr.last_loss is not None else float("nan")
     res = {
         "rank": info.rank, "world_size": info.world_size, "steps": nsteps,
         "seconds": dt, "ms_per_step": dt / max(nsteps, 1) * 1e3,

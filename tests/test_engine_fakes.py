@@ -76,3 +76,32 @@ def test_ref_manager_adopts_orphans_and_releases_mismatches():
     assert store.get("Pod", "default", "orphan")["metadata"]["ownerReferences"][0]["uid"] == job["metadata"]["uid"]
     assert store.get("Pod", "default", "stale")["metadata"]["ownerReferences"] == []
     assert store.get("Pod", "default", "foreign")["metadata"]["ownerReferences"][0]["uid"] == "someone-else"
+
+
+def _failed_pod(name, rt, idx, code):
+    return {"metadata": {"name": name, "namespace": "default",
+                         "labels": {c.REPLICA_TYPE_LABEL: rt, c.REPLICA_INDEX_LABEL: str(idx)}},
+            "status": {"phase": "Failed", "containerStatuses": [
+                {"name": "default-container", "state": {"terminated": {"exitCode": code}}}]}}
+
+
+def _running_pod(name, rt, idx):
+    return {"metadata": {"name": name, "namespace": "default",
+                         "labels": {c.REPLICA_TYPE_LABEL: rt, c.REPLICA_INDEX_LABEL: str(idx)}},
+            "status": {"phase": "Running"}}
+
+
+def test_gang_restart_skipped_when_a_peer_failed_permanently():
+    """rank A exits 137 (retryable) while rank B exits 1 (permanent) in
+    the same pass -> B's pod and failure record are kept (no gang teardown), so
+    the job fails like the reference's per-pod ExitCode handling."""
+    jc, pods, _ = new_job_controller()
+    job = new_test_job(workers=2, restart_policy=c.RESTART_POLICY_EXIT_CODE)
+    plist = [_failed_pod("test-job-master-0", "master", 0, 137), _failed_pod("test-job-worker-0", "worker", 0, 1),
+             _running_pod("test-job-worker-1", "worker", 1)]
+    jc.restart_gang(job, plist, {"test-job-master-0"})
+    assert pods.deleted == []
+    # all peers retryable / alive -> the whole gang is torn down
+    plist[1] = _failed_pod("test-job-worker-0", "worker", 0, 143)
+    jc.restart_gang(job, plist, {"test-job-master-0"})
+    assert sorted(pods.deleted) == ["test-job-worker-0", "test-job-worker-1"]

@@ -74,6 +74,18 @@ def test_comm_failure_classification():
     assert kdist.is_comm_failure(P2PError("peer did not arrive"))
     assert not kdist.is_comm_failure(ValueError("bad shape"))
     assert not kdist.is_comm_failure(RuntimeError("CUDA out of memory"))
+    # deterministic errors fail permanently instead of looping through gang restarts
+    assert not kdist.is_comm_failure(RuntimeError("NCCL error in: ProcessGroupNCCL.cpp:1, invalid usage"))
+    assert not kdist.is_comm_failure(RuntimeError("NCCL error: invalid argument"))
+    assert not kdist.is_comm_failure(RuntimeError("Default process group has not been initialized"))
+    assert not kdist.is_comm_failure(RuntimeError("user data loader timed out"))
+    assert not kdist.is_comm_failure(RuntimeError("process group bucket size mismatch"))
+    assert kdist.is_comm_failure(RuntimeError("[gloo/transport/tcp/unbound_buffer.cc:81] Timed out waiting 30000ms"
+                                              " for recv operation to complete (gloo)"))
+    assert kdist.is_comm_failure(ConnectionResetError("Connection reset by peer"))
+    net = getattr(__import__("torch").distributed, "DistNetworkError", None)
+    if net is not None:
+        assert kdist.is_comm_failure(net("store went away"))
     assert kdist.COMM_FAILURE_EXIT == 138
     from kubedl_amd.api import common as c
     assert c.is_retryable_exit_code(kdist.COMM_FAILURE_EXIT)

@@ -81,3 +81,54 @@ def test_scheduler_binds_slice_and_kubelet_exports_limit(tmp_path, monkeypatch):
         assert m.allocator.used() == 0
     finally:
         m.stop()
+
+
+def test_hbm_quantity_parsing():
+    assert c.parse_hbm_gb("32") == 32 and c.parse_hbm_gb(16.5) == 16.5
+    assert c.parse_hbm_gb("32G") == pytest.approx(32) and c.parse_hbm_gb("32Gi") == pytest.approx(34.359738368)
+    assert c.parse_hbm_gb("512Mi") == pytest.approx(0.536870912)
+    with pytest.raises(ValueError):
+        c.parse_hbm_gb("lots")
+    with pytest.raises(ValueError):
+        c.parse_hbm_gb("-4")
+
+
+def _job(name, containers):
+    return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "restartPolicy": "Never", "template": {
+                "spec": {"containers": containers}}}}}}
+
+
+def test_per_container_hbm_and_malformed_request_isolated(tmp_path, monkeypatch):
+    """(1) each container of a two-container slice pod caps its allocator
+    at its OWN request, not the pod's summed slice; (2) a pod with a malformed
+    kubedl.io/hbm-gb is marked Unschedulable without stopping the scheduler pass
+    for the other pods on the node."""
+    monkeypatch.setenv("KDL_ZYGOTE", "0")
+    m = Manager(ManagerOptions(home=str(tmp_path / "home"), gpus=2)).start()
+    try:
+        out = tmp_path / "env"
+        out.mkdir()
+        bad = {"name": "pytorch", "image": "kubedl-amd/sleep", "command": ["true"],
+               "resources": {"limits": {c.HBM_RESOURCE: "lots"}}}
+        m.apply(_job("bad", [bad]))
+        ctrs = [{"name": n, "image": "kubedl-amd/sleep",
+                 "command": ["bash", "-c", f"echo $KDL_HBM_LIMIT_GB > {out}/{n}"],
+                 "resources": {"limits": {c.HBM_RESOURCE: gb}}} for n, gb in (("pytorch", "100G"), ("side", 50))]
+        m.apply(_job("two", ctrs))
+        st = m.wait_for_condition("PyTorchJob", "default", "two", ["Succeeded", "Failed"], timeout=60)
+        assert c.last_condition_type(st["status"]) == "Succeeded", st["status"]
+        assert (out / "pytorch").read_text().split() == ["100"]
+        assert (out / "side").read_text().split() == ["50"]
+        deadline = time.time() + 10
+        msg = ""
+        while time.time() < deadline:
+            pod = m.store.try_get("Pod", "default", "bad-master-0")
+            conds = ((pod or {}).get("status") or {}).get("conditions") or []
+            msg = " ".join(x.get("message", "") for x in conds)
+            if "invalid resource request" in msg:
+                break
+            time.sleep(0.1)
+        assert "invalid resource request" in msg, msg
+    finally:
+        m.stop()

@@ -1,0 +1,178 @@
+"""Leader election and the default metrics endpoints of ``kdl manager``
+(VERDICT r2 missing 2-3; reference ``main.go:54-57,72-73,106``,
+``pkg/metrics/monitor.go:27-36``)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+import urllib.request
+
+import pytest
+
+from kubedl_amd.engine.leader import LeaderLock
+from kubedl_amd.engine.manager import Manager, ManagerOptions
+from kubedl_amd.metrics import parse_addr
+
+PY = sys.executable
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _port_busy(port):
+    s = socket.socket()
+    try:
+        s.bind(("0.0.0.0", port))
+        return False
+    except OSError:
+        return True
+    finally:
+        s.close()
+
+
+def test_parse_addr_forms():
+    assert parse_addr("8443") == ("", 8443)
+    assert parse_addr(":8080") == ("", 8080)
+    assert parse_addr("127.0.0.1:9") == ("127.0.0.1", 9)
+    assert parse_addr("0")[1] == 0 and parse_addr("")[1] == 0 and parse_addr(":0")[1] == 0
+
+
+def test_leader_lock_excludes_and_hands_over(tmp_path):
+    a, b = LeaderLock(str(tmp_path), "a"), LeaderLock(str(tmp_path), "b")
+    assert a.try_acquire() and a.held
+    assert not b.try_acquire()
+    assert b.holder()["holderIdentity"] == "a"
+    assert not b.acquire(timeout=0.3, poll=0.05)
+    a.release()
+    assert b.acquire(timeout=2, poll=0.05) and b.holder()["holderIdentity"] == "b"
+    b.release()
+
+
+def test_in_process_standby_manager_takes_over(tmp_path):
+    """A second Manager on the same home blocks (opens neither store nor node
+    runtime) until the first stops, then runs the durable store's jobs."""
+    home = str(tmp_path)
+    m1 = Manager(ManagerOptions(home=home, durable=True, gpus=1, leader_election=True)).start()
+    got = {}
+
+    def standby():
+        got["m"] = Manager(ManagerOptions(home=home, durable=True, gpus=1, leader_election=True)).start()
+    t = threading.Thread(target=standby, daemon=True)
+    t.start()
+    time.sleep(0.8)
+    assert "m" not in got and t.is_alive()  # still waiting for the lease
+    m1.stop()
+    t.join(10)
+    assert "m" in got and got["m"].leader.held
+    got["m"].stop()
+
+
+class _Lines:
+    """One reader thread per process; wait() polls the accumulated stdout."""
+
+    def __init__(self, proc):
+        self.out = []
+        threading.Thread(target=lambda: [self.out.append(x) for x in proc.stdout], daemon=True).start()
+
+    def wait(self, needle, timeout):
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            if any(needle in x for x in self.out):
+                return True
+            time.sleep(0.1)
+        return False
+
+    def text(self):
+        return "".join(self.out)
+
+
+def _get(url, timeout=5):
+    with urllib.request.urlopen(url, timeout=timeout) as r:
+        return r.read().decode()
+
+
+def test_two_cli_managers_one_spawns_ranks(tmp_path):
+    """Two ``kdl manager`` processes on one --home: only the leader reconciles
+    (the job's rank runs exactly once); the standby takes over on leader exit."""
+    home = str(tmp_path / "home")
+    env = dict(os.environ, PYTHONPATH=ROOT, KDL_ZYGOTE="0")
+    ports = [_free_port(), _free_port()]
+    base = [PY, "-u", "-m", "kubedl_amd.cli", "manager", "--home", home, "--gpus", "1",
+            "--metrics-addr", "0", "--controller-metrics-addr", "0"]
+    p1 = subprocess.Popen(base + ["--api-addr", f"127.0.0.1:{ports[0]}"], env=env, stdout=subprocess.PIPE,
+                          stderr=subprocess.STDOUT, text=True)
+    p2 = None
+    try:
+        l1 = _Lines(p1)
+        assert l1.wait("kdl manager up", 120), l1.text()
+        p2 = subprocess.Popen(base + ["--api-addr", f"127.0.0.1:{ports[1]}"], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True)
+        l2 = _Lines(p2)
+        assert l2.wait("waiting for leadership", 120), l2.text()
+        assert not l2.wait("kdl manager up", 4), "standby came up while the leader runs: " + l2.text()
+        marks = tmp_path / "marks"
+        marks.mkdir()
+        job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+               "metadata": {"name": "once", "namespace": "default"},
+               "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "restartPolicy": "Never", "template": {
+                   "spec": {"containers": [{"name": "pytorch", "image": "x", "command": [
+                       "bash", "-c", f"touch {marks}/$$; sleep 1"]}]}}}}}}
+        req = urllib.request.Request(f"http://127.0.0.1:{ports[0]}/api/apply", data=json.dumps(job).encode(),
+                                     method="POST", headers={"Content-Type": "application/json"})
+        urllib.request.urlopen(req, timeout=10).read()
+        deadline = time.time() + 60
+        state = ""
+        while time.time() < deadline:
+            j = json.loads(_get(f"http://127.0.0.1:{ports[0]}/api/objects/pytorchjobs/default/once"))
+            conds = (j.get("status") or {}).get("conditions") or []
+            state = conds[-1]["type"] if conds else ""
+            if state in ("Succeeded", "Failed"):
+                break
+            time.sleep(0.2)
+        assert state == "Succeeded"
+        assert len(os.listdir(marks)) == 1  # one rank process, spawned by the leader only
+        p1.terminate()
+        p1.wait(30)
+        assert l2.wait("kdl manager up", 120), "standby did not take over: " + l2.text()
+        j = json.loads(_get(f"http://127.0.0.1:{ports[1]}/api/objects/pytorchjobs/default/once"))
+        assert j["status"]["conditions"][-1]["type"] == "Succeeded"  # durable store carried over
+        time.sleep(1.0)
+        assert len(os.listdir(marks)) == 1  # the new leader did not re-run the finished job
+    finally:
+        for p in (p1, p2):
+            if p is not None and p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+
+
+@pytest.mark.skipif(_port_busy(8443) or _port_busy(8080), reason="default metrics ports in use on this host")
+def test_manager_serves_both_metrics_endpoints_by_default(tmp_path):
+    """No metrics flags: kubedl_jobs_* on :8443 and controller-runtime metrics on :8080."""
+    env = dict(os.environ, PYTHONPATH=ROOT, KDL_ZYGOTE="0")
+    port = _free_port()
+    p = subprocess.Popen([PY, "-u", "-m", "kubedl_amd.cli", "manager", "--home", str(tmp_path), "--gpus", "1",
+                          "--api-addr", f"127.0.0.1:{port}"], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True)
+    try:
+        lines = _Lines(p)
+        assert lines.wait("kdl manager up", 120), lines.text()
+        body = _get("http://127.0.0.1:8443/metrics")
+        assert "kubedl_jobs_running" in body and "kubedl_jobs_created" in body
+        ctrl = _get("http://127.0.0.1:8080/metrics")
+        assert "workqueue_depth" in ctrl and 'name="pytorchjob"' in ctrl
+        assert "controller_runtime_reconcile_total" in ctrl
+    finally:
+        p.terminate()
+        p.wait(30)
