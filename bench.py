@@ -14,7 +14,10 @@ Driver contract: ``python bench.py --gpus N --steps K --warmup W``.  Two ways in
   (1 Master + N-1 Workers, ``amd.com/gpu: 1`` each), waits for it to succeed
   and prints rank 0's result plus the controller-path launch delays
   (``first_pod_launch_delay_s`` / ``all_pods_launch_delay_s``: job creation ->
-  first / last rank Ready, the reference's histograms,
+  first / last rank Ready, the reference's histograms; measured warm -- ranks
+  forked from the running node's pre-imported zygote -- with ``cold_*`` from a
+  ready-only probe job submitted before the zygote is up; ``comm_init_s`` =
+  the first collective, where the lazy RCCL communicator bootstraps;
   ``pkg/metrics/job_metrics.go:139-194``, observed at
   ``pkg/job_controller/job.go:242-259``).  This process never touches the GPU
   (it does not even import torch): the ranks are forked from the zygote or
@@ -58,9 +61,13 @@ def _rank_args(args) -> list:
     return out
 
 
-def make_job(args) -> dict:
-    """One PyTorchJob, N ranks, one GPU each (the BASELINE.json job spec)."""
+def make_job(args, name: str = JOB_NAME, ready_only: bool = False) -> dict:
+    """One PyTorchJob, N ranks, one GPU each (the BASELINE.json job spec);
+    ``ready_only``: the same ranks exit right after signalling Ready (the cold
+    launch-delay probe)."""
     cmd = [sys.executable, "-u", "-m", "kubedl_amd.workers.resnet_bench"] + _rank_args(args)
+    if ready_only:
+        cmd.append("--ready-only")
     res = {"limits": {"cpu": "2"}} if args.cpu else {"limits": {"amd.com/gpu": 1}}
     env = [{"name": "KDL_BENCH_LAUNCHER", "value": "kdl-pytorchjob"}]
     if os.environ.get("KDL_FAULT"):  # fault-injection rehearsal (the kubelet never leaks it by itself)
@@ -73,7 +80,7 @@ def make_job(args) -> dict:
     if args.gpus > 1:
         specs["Worker"] = {"replicas": args.gpus - 1, "restartPolicy": "Never", "template": tmpl()}
     return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
-            "metadata": {"name": JOB_NAME, "namespace": "default"},
+            "metadata": {"name": name, "namespace": "default"},
             "spec": {"cleanPodPolicy": "None", "pytorchReplicaSpecs": specs}}
 
 
@@ -106,10 +113,30 @@ def launch_job(args) -> int:
             print(f"[bench] --gpus {args.gpus} but this node has {have} GPU(s)", file=sys.stderr)
             return 2
     home = tempfile.mkdtemp(prefix="kdl-bench-")
-    t_submit = time.time()
     mgr = Manager(ManagerOptions(home=home, gang_scheduler_name="kdl-gang")).start()
     rc = 1
+    cold = {}
     try:
+        # 1. cold launch delay: a ready-only job of the same N ranks submitted the
+        #    moment the node runtime is up, before the rank zygote can serve it
+        #    (every rank is a fresh interpreter importing torch) -- a node's first job
+        if not args.no_cold_probe:
+            probe = mgr.apply(make_job(args, JOB_NAME + "-cold", ready_only=True))
+            try:
+                pj = mgr.wait_for_condition("PyTorchJob", "default", JOB_NAME + "-cold", ["Succeeded", "Failed"],
+                                            timeout=min(args.timeout, 600))
+                if c.last_condition_type(pj.get("status") or {}) == "Succeeded":
+                    puid = probe["metadata"]["uid"]
+                    for k, key in (("first", "cold_first_pod_launch_delay_s"), ("all", "cold_all_pods_launch_delay_s")):
+                        v = mgr.metrics.observed[k].get(puid)
+                        cold[key] = round(v, 3) if v is not None else None
+            except TimeoutError as e:
+                print(f"[bench] cold probe: {e}", file=sys.stderr)
+        # 2. warm: a running node's steady state (the reference's long-lived
+        #    operator) -- ranks forked from the pre-imported zygote
+        z = mgr.kubelet.zygote if mgr.kubelet is not None else None
+        zygote_ready = bool(z is not None and z.ready.wait(timeout=min(args.timeout, 300)))
+        t_submit = time.time()
         job = mgr.apply(make_job(args))
         uid = job["metadata"]["uid"]
         try:
@@ -120,7 +147,8 @@ def launch_job(args) -> int:
             job = mgr.get("PyTorchJob", "default", JOB_NAME)
         st = job.get("status") or {}
         state = c.last_condition_type(st)
-        pods = [p for p in mgr.store.list("Pod", "default") if p["metadata"]["name"].startswith(JOB_NAME + "-")]
+        pods = [p for p in mgr.store.list("Pod", "default")
+                if (p["metadata"].get("labels") or {}).get(c.JOB_NAME_LABEL) == JOB_NAME]
         ready = [p for p in pods if any(x.get("type") == "Ready" and x.get("status") == "True"
                                         for x in (p.get("status") or {}).get("conditions") or [])
                  or (p.get("status") or {}).get("phase") == "Succeeded"]
@@ -145,6 +173,10 @@ def launch_job(args) -> int:
                              if st.get("completionTime") else None)
         res["submit_to_done_s"] = round(time.time() - t_submit, 3)
         res["ranks_ready"] = len(ready)
+        res["launch"] = "warm (zygote)" if zygote_ready else "cold (no zygote)"
+        res.update(cold)
+        if os.environ.get("KDL_BENCH_KEEP"):
+            res["home"] = home
         res["gpus"] = sorted({int(g) for p in pods
                               for g in ((p["metadata"].get("annotations") or {}).get("kubedl.io/gpus") or "")
                               .split(",") if g})
@@ -165,6 +197,8 @@ def main(argv=None) -> int:
     ap.add_argument("--direct", action="store_true",
                     help="run as a single in-process rank (no control plane); WORLD_SIZE forces this too")
     ap.add_argument("--timeout", type=float, default=1800.0, help="job-path wait limit (s)")
+    ap.add_argument("--no-cold-probe", action="store_true",
+                    help="job path: skip the cold (pre-zygote) ready-only probe job")
     args = ap.parse_args(argv)
     if "WORLD_SIZE" in os.environ or args.direct:
         if "WORLD_SIZE" not in os.environ:

@@ -663,6 +663,43 @@ FinArm take_fin_arm() {
   return f;
 }
 
+// BN-backward-apply prologue armed for the next conv1x1_gemm (on its A operand:
+// A' = k A + c1 x + c0, the output of bn_stage_bwd_apply) or conv1x1_wgrad (on
+// its G operand) call on this thread, so the consumer GEMM computes that
+// tensor while staging it instead of a separate apply pass writing it to HBM
+// and the consumers reading it back; ``out`` (optional) receives it, for a
+// consumer that still reads it materialised.  Consumed (cleared) by the launch.
+struct BwdArm {
+  const void* x = nullptr;
+  const float* coef = nullptr;
+  void* out = nullptr;
+  int64_t C = 0, rows = 0;
+};
+thread_local BwdArm g_bwd_arm;
+
+void bn_bwd_pro_arm(const at::Tensor& x, const at::Tensor& ws, int64_t C, const c10::optional<at::Tensor>& out) {
+  TORCH_CHECK(C > 0 && C % 64 == 0 && x.numel() % C == 0, "bn_bwd_pro_arm: C % 64 == 0 dividing x");
+  need_bf16(x, x.numel(), "bn_bwd_pro_arm x");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() &&
+                  ws.numel() >= kdl::bn_workspace_floats(static_cast<int>(C)),
+              "bn_bwd_pro_arm: workspace must be fp32 >= bn_workspace_floats(C)");
+  g_bwd_arm.x = x.data_ptr();
+  g_bwd_arm.coef = ws.data_ptr<float>() + 32 * 4 * C + 2 * C;  // ws_bcoef (csrc/bn_act.hip)
+  g_bwd_arm.out = nullptr;
+  if (out.has_value() && out->defined()) {
+    need_bf16(*out, x.numel(), "bn_bwd_pro_arm out");
+    g_bwd_arm.out = out->data_ptr();
+  }
+  g_bwd_arm.C = C;
+  g_bwd_arm.rows = x.numel() / C;
+}
+
+BwdArm take_bwd_arm() {
+  const BwdArm b = g_bwd_arm;
+  g_bwd_arm = BwdArm{};
+  return b;
+}
+
 void apply_fin_arm(const FinArm& f, kdl::Conv1x1Args& a, int64_t N, int64_t epi) {
   if (!f.ws) return;
   TORCH_CHECK(f.C == N, "bn_fin_arm: armed for C = ", f.C, ", the GEMM has N = ", N);
@@ -721,7 +758,14 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
                   const c10::optional<at::Tensor>& ebits, const c10::optional<at::Tensor>& ex2,
                   const c10::optional<at::Tensor>& emean2, const c10::optional<at::Tensor>& acc2) {
   const FinArm fin = take_fin_arm();
+  const BwdArm bw = take_bwd_arm();
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_gemm: need K % 64 == 0, N % 64 == 0");
+  if (bw.x) {
+    TORCH_CHECK(bw.C == K && bw.rows == M, "bn_bwd_pro_arm: armed for [", bw.rows, ", ", bw.C,
+                "], the GEMM's A is [", M, ", ", K, "]");
+    TORCH_CHECK(stride == 1 && !opt_ptr(pro_coef) && epi != 1,
+                "conv1x1_gemm: the backward-apply prologue serves dense data-gradient GEMMs");
+  }
   const int64_t rows_in = stride > 1 ? (M / (Hout * Wout)) * Hin * Win : M;
   if (stride > 1) TORCH_CHECK(M % (Hout * Wout) == 0 && (Hout - 1) * stride < Hin && (Wout - 1) * stride < Win,
                               "conv1x1_gemm: gather geometry");
@@ -768,6 +812,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   a.res_W = static_cast<int>(res_W);
   a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
   a.ex2 = opt_ptr(ex2); a.emean2 = opt_fptr(emean2); a.acc2 = opt_fptr(acc2);
+  a.bx = bw.x; a.bcoef = bw.coef; a.aout = bw.out;
   apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");
 }
@@ -931,7 +976,14 @@ void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor d
 void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
                    at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t M, int64_t N, int64_t K,
                    int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride) {
+  const BwdArm bw = take_bwd_arm();
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_wgrad: need K % 64 == 0, N % 64 == 0");
+  if (bw.x) {
+    TORCH_CHECK(bw.C == N && bw.rows == M, "bn_bwd_pro_arm: armed for [", bw.rows, ", ", bw.C,
+                "], the weight gradient's G is [", M, ", ", N, "]");
+    TORCH_CHECK(!bw.out, "conv1x1_wgrad: the G prologue has no write-through");
+    TORCH_CHECK(stride == 1 || !opt_ptr(pro_coef), "conv1x1_wgrad: G prologue + A prologue need dense A rows");
+  }
   const int64_t rows_in = stride > 1 ? (M / (Hout * Wout)) * Hin * Win : M;
   need_bf16(G, M * N, "conv1x1_wgrad G");
   need_bf16(A, rows_in * K, "conv1x1_wgrad A");
@@ -948,7 +1000,7 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
                                dW.has_value() && dW->defined() ? dW->data_ptr() : nullptr, static_cast<float>(scale),
                                static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Hout),
                                static_cast<int>(Wout), static_cast<int>(Hin), static_cast<int>(Win),
-                               static_cast<int>(stride), cur_stream()),
+                               static_cast<int>(stride), cur_stream(), bw.x, bw.coef),
             "conv1x1_wgrad");
 }
 
@@ -1200,6 +1252,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
+  m.def("bn_bwd_pro_arm", &bn_bwd_pro_arm, "fuse this BN's backward apply (input x, workspace ws) into the next conv1x1_gemm's A (or conv1x1_wgrad's G) staging; optional write-through tensor");
   m.def("bn_fin_arm", &bn_fin_arm, "fold the BN finalize of this workspace (C channels, M elements) into the next conv GEMM launch");
   m.def("bn_fin_desc", &bn_fin_desc, "write a BN layer's finalize descriptor into its workspace tail");
   m.def("stem7x7_wgrad_bn", &stem7x7_wgrad_bn, "stem weight gradient with the stem BN+ReLU+max-pool backward folded in");

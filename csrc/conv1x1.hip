@@ -63,15 +63,30 @@ using namespace gemm;  // GemmParams, EPI_*, G_*, fragment types, epilogue (csrc
 
 constexpr int kThreads = 256;
 constexpr int BK = 64;
+// PRO_BWD coefficient table capacity (channels of K) per tile width: 128-wide
+// tiles stay within 80 KiB of LDS (two blocks per CU) up to K = 512, 64-wide
+// tiles up to K = 2048 (the widest ResNet-50 data-gradient K)
+__host__ __device__ constexpr int bwd_kmax(int bn) { return bn >= 128 ? 512 : 2048; }
 
-template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI, int KBK = BK>
+// PRO: 0 none, PRO_FWD = BN+ReLU of the previous layer, PRO_BWD = BN-backward
+// apply (GemmParams::bx / bcoef; dense rows only)
+enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2 };
+
+template <int BM, int BN, int MINB, int PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
+  static_assert(PRO != PRO_BWD || GATHER == G_DENSE, "the backward-apply prologue reads dense rows");
   // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
   // [BM][BN + 8] output tile and finally as the reduction scratch.
   constexpr int LDK = KBK + 8;  // padded LDS row (bf16): 16-B slot stride odd -> conflict-free fragment reads
   constexpr int CPRK = KBK / 8; // 16-B chunks per staged row
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * LDK];
   constexpr int kBuf = (BM + BN) * LDK;
+  // PRO_BWD: the backward coefficients k | c1 | c0 of every K channel, staged
+  // once per block behind the operand buffers (one __shared__ array: a second
+  // one can make hipcc drain the pipeline, cdna_hip_programming.md §5 item 4a)
+  constexpr int KT = PRO == PRO_BWD ? bwd_kmax(BN) : 0;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kBuf + 6 * KT];
+  float* coef_lds = reinterpret_cast<float*>(lds + 2 * kBuf);
+  (void)coef_lds;
   constexpr int WN = (BN >= 64 && BM >= 64) ? 2 : 1;  // waves along N
   constexpr int WM = 4 / WN;                           // waves along M
   static_assert(BM % (WM * 32) == 0 && BN % (WN * 32) == 0, "wave tile must be whole 32x32 MFMA blocks");
@@ -116,11 +131,25 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // all A chunks of a thread share one 8-channel k-chunk ((t + i*256) & 7 == t & 7)
   float psc[8], psf[8];
   (void)psc; (void)psf;
+  // PRO_BWD: the BN input rows beside A, the staged K-step's k0 and the
+  // chunks whose row is < M (write-through of A')
+  uint4 rx[PRO == PRO_BWD ? A_CH : 1];
+  int st_k0 = 0;
+  uint32_t a_valid = 0;
+  const bool wthru = PRO == PRO_BWD && p.aout != nullptr && tile_n == 0;
+  (void)rx; (void)st_k0; (void)a_valid; (void)wthru;
+  if constexpr (PRO == PRO_BWD) {
+    for (int i = t; i < 3 * K / 4; i += kThreads)
+      reinterpret_cast<float4*>(coef_lds)[i] = reinterpret_cast<const float4*>(p.bcoef)[i];
+    __syncthreads();
+  }
 
   auto setup_rows = [&](int tm) {
+    a_valid = 0;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int m0 = tm * BM + a_row[i];
+      a_valid |= m0 < M ? (1u << i) : 0u;
       const int m = m0 < M ? m0 : 0;  // tail rows re-read row 0 (never stored): no divergent loads
       int64_t src = m;
       if constexpr (GATHER != G_DENSE) {
@@ -159,13 +188,18 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 #pragma unroll
       for (int i = 0; i < A_CH; ++i)
         ra[i] = ld16(p.A + a_off[i] + k0 + a_kc[i]);  // rows >= M read row 0: their outputs are never stored
+      if constexpr (PRO == PRO_BWD) {
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) rx[i] = ld16(p.bx + a_off[i] + k0 + a_kc[i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int c = t + i * kThreads;
       rb[i] = ld16(p.B + static_cast<int64_t>(n0 + c / CPRK) * K + k0 + (c % CPRK) * 8);
     }
-    if constexpr (PRO) {
+    if constexpr (PRO == PRO_BWD) st_k0 = k0;
+    if constexpr (PRO == PRO_FWD) {
       const int kcoef = GATHER == G_CONV3 ? p.Cin : K;
       const float4* sp = reinterpret_cast<const float4*>(p.pro_coef + kc0 + a_kc[0]);
       const float4* fp = reinterpret_cast<const float4*>(p.pro_coef + kcoef + kc0 + a_kc[0]);
@@ -179,10 +213,24 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   auto swrite = [&](int buf) {
     bf16_t* As = lds + buf * kBuf;
     bf16_t* Bs = As + BM * LDK;
+    float bk[8], bc1[8], bc0[8];  // PRO_BWD: this thread's 8 channels of the staged K-step
+    (void)bk; (void)bc1; (void)bc0;
+    if constexpr (PRO == PRO_BWD) {
+      const int c = st_k0 + a_kc[0];
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(coef_lds + c + j);
+        const float4 b = *reinterpret_cast<const float4*>(coef_lds + K + c + j);
+        const float4 z = *reinterpret_cast<const float4*>(coef_lds + 2 * K + c + j);
+        bk[j] = a.x; bk[j + 1] = a.y; bk[j + 2] = a.z; bk[j + 3] = a.w;
+        bc1[j] = b.x; bc1[j + 1] = b.y; bc1[j + 2] = b.z; bc1[j + 3] = b.w;
+        bc0[j] = z.x; bc0[j + 1] = z.y; bc0[j + 2] = z.z; bc0[j + 3] = z.w;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint4 v = ra[i];
-      if constexpr (PRO) {
+      if constexpr (PRO == PRO_FWD) {
         float f[8];
         unpack8(v, f);
 #pragma unroll
@@ -191,6 +239,15 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           f[j] = o > 0.f ? o : 0.f;
         }
         v = pack8(f);
+      } else if constexpr (PRO == PRO_BWD) {
+        float f[8], x[8];
+        unpack8(v, f);
+        unpack8(rx[i], x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaf(bk[j], f[j], fmaf(bc1[j], x[j], bc0[j]));
+        v = pack8(f);
+        if (wthru && ((a_valid >> i) & 1u))
+          *reinterpret_cast<uint4*>(p.aout + a_off[i] + st_k0 + a_kc[i]) = v;
       }
       if constexpr (GATHER == G_CONV3) {
         if (!((ra_ok >> i) & 1u)) v = make_uint4(0, 0, 0, 0);  // zero padding (after BN+ReLU)
@@ -504,7 +561,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restric
   }
 }
 
-template <int BM, int BN, int MINB, bool PRO, int GATHER, int EPI, int KBK>
+template <int BM, int BN, int MINB, int PRO, int GATHER, int EPI, int KBK>
 hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = p.N / BN;
@@ -521,32 +578,48 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
 }
 
 // forward convs (prologue / row gather) only ever use the PLAIN and STATS
-// epilogues; the dgrad epilogues run without either (3x3 dgrad: MASKX)
-template <int BM, int BN, int MINB, bool PRO, int GATHER, int KBK>
+// epilogues; the dgrad epilogues run without either (3x3 dgrad: MASKX); the
+// backward-apply prologue feeds only the dense dgrad epilogues
+template <int BM, int BN, int MINB, int PRO, int GATHER, int KBK>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
-  switch (epi) {
-    case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
-    case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
-  }
-  if constexpr (!PRO && GATHER == G_DENSE) {
+  if constexpr (PRO == PRO_BWD) {
     switch (epi) {
+      case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
       case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
       case EPI_RESBITS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
       case EPI_RES: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RES, KBK>(p, s);
     }
+    return hipErrorInvalidValue;
+  } else {
+    switch (epi) {
+      case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
+      case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
+    }
+    if constexpr (PRO == PRO_NONE && GATHER == G_DENSE) {
+      switch (epi) {
+        case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
+        case EPI_RESBITS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
+        case EPI_RES: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RES, KBK>(p, s);
+      }
+    }
+    if constexpr (PRO == PRO_NONE && GATHER == G_CONV3) {
+      if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
+    }
+    return hipErrorInvalidValue;
   }
-  if constexpr (!PRO && GATHER == G_CONV3) {
-    if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
-  }
-  return hipErrorInvalidValue;
 }
 
 template <int BM, int BN, int MINB, int KBK = BK>
-hipError_t dispatch_pg(const GemmParams& p, int epi, bool pro, int gather, hipStream_t s) {
+hipError_t dispatch_pg(const GemmParams& p, int epi, int pro, int gather, hipStream_t s) {
+  if (pro == PRO_BWD) {
+    if constexpr (BM == 128 && MINB == 2 && KBK == BK)  // the two configs conv1x1_gemm routes it to
+      return gather == G_DENSE ? dispatch_epi<BM, BN, MINB, PRO_BWD, G_DENSE, KBK>(p, epi, s) : hipErrorInvalidValue;
+    return hipErrorInvalidValue;
+  }
   if (gather == G_CONV3)
-    return pro ? dispatch_epi<BM, BN, MINB, true, G_CONV3, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_CONV3, KBK>(p, epi, s);
-  if (pro) return gather ? dispatch_epi<BM, BN, MINB, true, G_STRIDED, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, true, G_DENSE, KBK>(p, epi, s);
-  return gather ? dispatch_epi<BM, BN, MINB, false, G_STRIDED, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, false, G_DENSE, KBK>(p, epi, s);
+    return pro ? dispatch_epi<BM, BN, MINB, PRO_FWD, G_CONV3, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, PRO_NONE, G_CONV3, KBK>(p, epi, s);
+  if (pro) return gather ? dispatch_epi<BM, BN, MINB, PRO_FWD, G_STRIDED, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, PRO_FWD, G_DENSE, KBK>(p, epi, s);
+  return gather ? dispatch_epi<BM, BN, MINB, PRO_NONE, G_STRIDED, KBK>(p, epi, s) : dispatch_epi<BM, BN, MINB, PRO_NONE, G_DENSE, KBK>(p, epi, s);
 }
 
 // Tile configs: 0 = 128x128 (2 blocks/CU), 1 = 128x64, 2 = 64x128, 3 = 64x64 (4 blocks/CU),
@@ -597,7 +670,11 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.res_H = a.res_H; p.res_W = a.res_W;
   p.ebits = a.ebits; p.ex2 = static_cast<const bf16_t*>(a.ex2); p.emean2 = a.emean2; p.acc2 = a.acc2;
   p.fin_ws = a.fin_ws; p.fin_ws2 = a.fin_ws2; p.fin_M = a.fin_M;
-  const bool pro = a.pro_coef != nullptr;
+  p.bx = static_cast<const bf16_t*>(a.bx); p.bcoef = a.bcoef; p.aout = static_cast<bf16_t*>(a.aout);
+  const bool bpro = a.bx != nullptr;
+  if (bpro && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS))
+    return hipErrorInvalidValue;
+  const int pro = bpro ? PRO_BWD : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
   int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
   p.Cin = a.K;
   if (a.ksize == 3) {
@@ -618,6 +695,7 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   // long K without an A prologue: the LDS-DMA main loop (csrc/igemm.hip)
   const int core = gemm_core_mode();
   const int min_k = gather == G_CONV3 ? 0 : 512;
+  // (the backward-apply prologue transforms A in registers: register-staged loop)
   if (!pro && core != 0 && (core == 1 || p.K >= min_k) && p.K % 64 == 0) {
     p.a_rows = gather == G_CONV3 ? static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win
                : gather == G_STRIDED ? static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win
@@ -632,6 +710,11 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
     if (gather == G_CONV3 && p.N == 512 && g_forced_cfg_unset()) cfg = 1;
     const hipError_t e = igemm(p, epi, gather, cfg, s);
     if (e != hipErrorInvalidValue) return e;
+  }
+  if (pro == PRO_BWD) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
+    if (p.N % 128 == 0 && p.K <= bwd_kmax(128)) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
+    if (p.K <= bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
+    return hipErrorInvalidValue;
   }
   switch (pick_config(p.M, p.N, p.K, epi)) {
     case 0: return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
@@ -676,7 +759,14 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
 // 2 when its weight-gradient stream is on (set_wgrad_big, before its workspaces
 // are sized); else 128 or 64 per dimension.
 int g_wgrad_big = [] { const char* e = getenv("KDL_WGRAD_BIG"); return e ? atoi(e) : -1; }();
-void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk) {
+// bwd (a BN-backward-apply G prologue, csrc/wgrad_dma.hip BWDG): its gx panels
+// double G's LDS share, so N tiles of at most 128 with K tiles up to 256 (8 waves)
+void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk, bool bwd = false) {
+  if (bwd) {
+    *tn = N % 128 == 0 ? 128 : 64;
+    *tk = K % 256 == 0 ? 256 : K % 128 == 0 ? 128 : 64;
+    return;
+  }
   const int big = g_wgrad_big < 0 ? 1 : g_wgrad_big;
   if ((conv3 ? big >= 1 : big >= 2) && gemm_core_mode() != 0 && N % 256 == 0 && K % 256 == 0) {
     *tn = *tk = 256;
@@ -686,9 +776,9 @@ void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk) {
   *tk = K % 128 == 0 ? 128 : 64;
 }
 
-int wgrad_splits(int M, int N, int K, bool conv3) {
+int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false) {
   int tn, tk;
-  wgrad_tiles(N, K, conv3, &tn, &tk);
+  wgrad_tiles(N, K, conv3, &tn, &tk, bwd);
   const int tiles = (N / tn) * (K / tk);
   // ~2 blocks per CU (one round): halves the slab bytes of 4 blocks/CU, measured +1.5% per step.
   // Rounded DOWN so the grid never spills a partial second round onto the CUs
@@ -699,14 +789,18 @@ int wgrad_splits(int M, int N, int K, bool conv3) {
   // at half the target: 1024 -> 12,460, 512 -> 12,830, 384 -> 13,047, 320 ->
   // 13,078, 256 -> 12,933, 192 -> 12,715 img/s; profiles/r02_wgrad_blocks_sweep.txt)
   int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 320; }();
-  if (tn == 256) target /= 2;
+  if (tn == 256 || (bwd && !(tn == 64 && tk == 64))) target /= 2;  // one (8-wave) block per CU
   int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;
   if (splits > max_splits) splits = max_splits;
   return splits < 1 ? 1 : splits;
 }
 
-int conv1x1_wgrad_splits(int M, int N, int K) { return wgrad_splits(M, N, K, false); }
+// slab capacity for either G mode (plain / BN-backward prologue)
+int conv1x1_wgrad_splits(int M, int N, int K) {
+  const int a = wgrad_splits(M, N, K, false), b = wgrad_splits(M, N, K, false, true);
+  return a > b ? a : b;
+}
 
 // the caller's preference (an explicit KDL_WGRAD_BIG wins)
 void set_wgrad_big(int mode) {
@@ -769,11 +863,15 @@ namespace {
 // big: the workspace holds wgrad_splits(M, N, K, true) slabs (3x3 256-tile configs)
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
-                      hipStream_t s, bool big = false) {
+                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr) {
   if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
+  const bool bwd = gx != nullptr;
+  // the G prologue exists on the LDS-DMA kernel only
+  if (bwd && (gemm_core_mode() == 0 || !gcoef || mode == G_CONV3 || (pro_coef && mode != G_DENSE)))
+    return hipErrorInvalidValue;
   int tn, tk;
-  wgrad_tiles(N, K, big, &tn, &tk);
-  const int splits = wgrad_splits(M, N, K, big);
+  wgrad_tiles(N, K, big, &tn, &tk, bwd);
+  const int splits = wgrad_splits(M, N, K, big, bwd);
   int rps = (M + splits - 1) / splits;
   rps = (rps + WMK - 1) / WMK * WMK;
   int tiles_k = K / tk;
@@ -785,6 +883,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
   if (gemm_core_mode() != 0) {  // LDS-DMA pipeline (csrc/wgrad_dma.hip) unless forced off
     WgParams wp{};
     wp.G = g; wp.A = x; wp.pro = pro_coef; wp.dw32 = dw32;
+    wp.gx = static_cast<const bf16_t*>(gx); wp.gcoef = gcoef;
     wp.M = M; wp.N = N; wp.K = K; wp.Hout = Hout; wp.Wout = Wout; wp.Hin = Hin; wp.Win = Win;
     wp.stride = stride; wp.cin = cin; wp.rps = rps; wp.tiles_k = tiles_k; wp.mode = mode;
     wp.a_rows = mode == G_DENSE ? M : static_cast<int64_t>(M / (Hout * Wout)) * Hin * Win;
@@ -796,6 +895,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     if (e != hipSuccess && e != hipErrorInvalidValue) return e;
     done = e == hipSuccess;
   }
+  if (!done && bwd) return hipErrorInvalidValue;
   if (!done) {
     if (tn > 128 || tk > 128) {  // the register-staged kernel has no 256 tiles: same splits, 128 tiles
       tn = tk = 128;
@@ -813,9 +913,10 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
 }  // namespace
 
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
-                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s) {
+                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
+                         const void* gx, const float* gcoef) {
   return wgrad_impl(G, A, pro_coef, dw32, dW, scale, M, N, K, Hout, Wout, Hin, Win, stride,
-                    stride > 1 ? G_STRIDED : G_DENSE, K, s);
+                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef);
 }
 
 int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {

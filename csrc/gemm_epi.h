@@ -48,6 +48,13 @@ struct GemmParams {
   int Cin;                // GATHER == G_CONV3: channels per tap (K = 9 * Cin, Cin % 64 == 0)
   int64_t a_rows;         // rows of the A tensor (buffer bounds of the LDS-DMA loads)
   const float* pro_coef;  // [2K] (3x3: [2Cin]): scale | shift
+  // BN-backward-apply prologue of A (register-staged dense GEMM only):
+  //   A' = bf16(k[c] A + c1[c] bx + c0[c])  -- the same fmaf nesting and rounding
+  // as the standalone apply pass (csrc/bn_act.hip bn_bwd_apply_kernel), so A'
+  // is bit-identical to the tensor that pass would have written.
+  const bf16_t* bx;       // that BN's input x [M, K]
+  const float* bcoef;     // [3K] k | c1 | c0 (the BN workspace's backward coefficients)
+  bf16_t* aout;           // optional write-through of A' [M, K] (the blocks of output tile 0)
   // epilogue operands
   const float* shift;   // STATS: [N]
   float* acc;           // STATS/MASKX/RESBITS: [kRep][2N]
@@ -81,6 +88,10 @@ struct WgParams {
   const bf16_t* G;        // [M][N] output gradient
   const bf16_t* A;        // layer input rows (gathered per mode)
   const float* pro;       // optional BN+ReLU prologue of A: [2 * lda] scale | shift
+  // optional BN-backward-apply prologue of G: G' = k[n] G + c1[n] gx + c0[n]
+  // (GemmParams::bx / bcoef semantics, per output channel n)
+  const bf16_t* gx;       // [M][N]
+  const float* gcoef;     // [3N]
   float* dw32;
   int M, N, K;            // K = 9 * cin for 3x3
   int Hout, Wout, Hin, Win, stride, cin;

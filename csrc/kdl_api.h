@@ -214,6 +214,11 @@ struct Conv1x1Args {
   float* fin_ws;                     // epi 1-3: finalize the BN of this workspace in the GEMM (bn_fin.h)
   float* fin_ws2;                    // epi 3: and the downsample BN's
   float fin_M;                       // their element count
+  // BN-backward-apply prologue of A (dense 1x1 dgrad): A' = k A + c1 bx + c0,
+  // bit-identical to bn_stage_bwd_apply's output; aout (optional) receives A'
+  const void* bx;                    // that BN's input [M, K]
+  const float* bcoef;                // [3K] its backward coefficients (ws_bcoef)
+  void* aout;                        // [M, K]
 };
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 // Data gradient of a 3x3 / pad 1 / stride 2 conv as four sub-pixel class GEMMs
@@ -248,8 +253,11 @@ void set_wgrad_big(int mode);
 // dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace
 // (conv1x1_wgrad_splits(M, N, K) x [N, K] fp32, no initialisation needed); the
 // result goes to dW (bf16) if given, else as fp32 into the first [N, K] of dw32.
+// gx / gcoef (optional): G is replaced by the BN-backward apply k G + c1 gx + c0
+// (gcoef = [3N] k | c1 | c0), computed while staging it (LDS-DMA kernel only).
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
-                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s);
+                         int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
+                         const void* gx = nullptr, const float* gcoef = nullptr);
 // 3x3 / pad 1: dW[Cout][3][3][Cin] = sum_m G[m, :]^T pro(A)_tap(m); dw32 holds
 // conv3x3_wgrad_slabs(...) x [Cout, 9 Cin] fp32 (dw32_floats: its size; a smaller
 // workspace of conv1x1_wgrad_splits(M, Cout, 9 Cin) slabs keeps the implicit GEMM).

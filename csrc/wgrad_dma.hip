@@ -66,14 +66,21 @@ __device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
 // WN x WK waves: 2 x 2 (4 waves, 2 blocks/CU) for tiles up to 128 x 128; 2 x 4
 // (8 waves of 128 x 64, 1 block/CU, 128 KiB) for 256 x 256 -- half the LDS-DMA
 // bytes per MFMA of a 128 x 128 tile (the operand stream bounds these kernels).
-template <int TN_, int TK_, int GATHER, bool PRO, int WN = 2, int WK = 2>
+//
+// BWDG: G is the output of a BN-backward apply that was never written, G' =
+// k[n] G + c1[n] gx + c0[n] (WgParams::gx / gcoef): gx is staged by the same
+// DMA as G into PN panels of its own, read with G's transposed reads, and
+// combined per fragment -- each lane's G fragment is ONE output channel n, so
+// (k, c1, c0) are per-lane constants, exactly as the A prologue's (scale, shift).
+template <int TN_, int TK_, int GATHER, bool PRO, int WN = 2, int WK = 2, bool BWDG = false>
 __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dma_kernel(WgParams p) {
   constexpr int NW = WN * WK;
   constexpr int PN = TN_ / 64, PK = TK_ / 64;  // 64-column panels per operand
+  constexpr int PX = BWDG ? PN : 0;            // gx panels (BWDG)
   constexpr int PANEL = MK * 128;              // bytes per panel per stage
-  constexpr int STAGE = (PN + PK) * PANEL;
-  static_assert((PN + PK) * (MK / 8) % NW == 0, "every wave issues the same DMA count");
-  constexpr int IPW = (PN + PK) * (MK / 8) / NW;  // 1-KiB DMA instructions per wave per stage
+  constexpr int STAGE = (PN + PK + PX) * PANEL;
+  static_assert((PN + PK + PX) * (MK / 8) % NW == 0, "every wave issues the same DMA count");
+  constexpr int IPW = (PN + PK + PX) * (MK / 8) / NW;  // 1-KiB DMA instructions per wave per stage
   constexpr int TN = TN_ / WN / 32, TK = TK_ / WK / 32;  // 32x32 MFMA blocks per wave
   static_assert(TN >= 1 && TK >= 1, "wave tile = whole 32x32 MFMA blocks");
   __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
@@ -101,6 +108,9 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
       const_cast<bf16_t*>(p.G), (short)0, static_cast<int>(static_cast<int64_t>(p.M) * p.N * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(p.A), (short)0, static_cast<int>(p.a_rows * lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(BWDG ? p.gx : p.G), (short)0, static_cast<int>(static_cast<int64_t>(p.M) * p.N * 2),
+      0x00020000);
 
   // DMA instruction i of this wave: panel (G panels first, then A), 8-row group
   const int lrow = lane >> 3;
@@ -110,8 +120,9 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
     const int g = wave * IPW + i;
     const int panel = g / (MK / 8), r = 8 * (g % (MK / 8)) + lrow;
     const int c = (lane & 7) ^ (((r >> 1) & 1) * 4);
-    gcol[i] = panel < PN ? static_cast<uint32_t>((n0 + 64 * panel + 8 * c) * 2)
-                         : static_cast<uint32_t>((acol0 + 64 * (panel - PN) + 8 * c) * 2);
+    gcol[i] = panel < PN        ? static_cast<uint32_t>((n0 + 64 * panel + 8 * c) * 2)
+              : panel < PN + PK ? static_cast<uint32_t>((acol0 + 64 * (panel - PN) + 8 * c) * 2)
+                                : static_cast<uint32_t>((n0 + 64 * (panel - PN - PK) + 8 * c) * 2);
   }
 
   auto issue = [&](int m0, int stage) {
@@ -126,6 +137,8 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
       // the VGPR offset; soffset stays 0)
       if (panel < PN) {
         dma16(rG, dst, m < p.M ? static_cast<uint32_t>(m * p.N * 2) + gcol[i] : kOOB, 0);
+      } else if (BWDG && panel >= PN + PK) {
+        dma16(rX, dst, m < p.M ? static_cast<uint32_t>(m * p.N * 2) + gcol[i] : kOOB, 0);
       } else if constexpr (GATHER == G_DENSE) {
         dma16(rA, dst, m < p.M ? static_cast<uint32_t>(m * p.K * 2) + gcol[i] : kOOB, 0);
       } else {
@@ -185,6 +198,21 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
     }
   }
   (void)psc; (void)psf;
+  // BWDG coefficients: this lane's G row is channel n0 + wn0 + 32i + (lane & 31)
+  float gk[TN], gc1[TN], gc0[TN];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    gk[i] = 1.f;
+    gc1[i] = 0.f;
+    gc0[i] = 0.f;
+    if constexpr (BWDG) {
+      const int n = n0 + wn0 + 32 * i + (lane & 31);
+      gk[i] = p.gcoef[n];
+      gc1[i] = p.gcoef[p.N + n];
+      gc0[i] = p.gcoef[2 * p.N + n];
+    }
+  }
+  (void)gk; (void)gc1; (void)gc0;
 
   f32x16_t acc[TN][TK];
 #pragma unroll
@@ -198,7 +226,7 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
     __syncthreads();  // stage st landed everywhere; the other stage is free
     if (m0 + MK < mend) issue(m0 + MK, st ^ 1);
     const char* S = lds + st * STAGE;
-    const bool tail = PRO && m0 + MK > mend;  // rows past the range: zero after the prologue
+    const bool tail = (PRO || BWDG) && m0 + MK > mend;  // rows past the range: zero after the prologue
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8_t gf[TN], af[TK];
@@ -206,6 +234,20 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
       for (int i = 0; i < TN; ++i) {
         const char* b = S + goff[i] + s * 16 * 128;
         gf[i] = frag8(tr_read(b), tr_read(b + 4 * 128));
+        if constexpr (BWDG) {
+          const char* bx = b + (PN + PK) * PANEL;
+          const bf16x8_t xf = frag8(tr_read(bx), tr_read(bx + 4 * 128));
+          float f[8], x[8];
+          unpack8(__builtin_bit_cast(uint4, gf[i]), f);
+          unpack8(__builtin_bit_cast(uint4, xf), x);
+          const int mrow = m0 + 16 * s + 8 * (lane >> 5);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float o = fmaf(gk[i], f[e], fmaf(gc1[i], x[e], gc0[i]));  // bn_bwd_apply_kernel's nesting
+            f[e] = (!tail || mrow + e < mend) ? o : 0.f;
+          }
+          gf[i] = __builtin_bit_cast(bf16x8_t, pack8(f));
+        }
       }
 #pragma unroll
       for (int j = 0; j < TK; ++j) {
@@ -264,6 +306,17 @@ void launch(const WgParams& p, int grid, hipStream_t s) {
 #undef KDL_WGD
 }
 
+// G prologue (BWDG): 1x1 weight gradients only (dense or strided A rows)
+template <int TN_, int TK_, int WN, int WK>
+void launch_bwdg(const WgParams& p, int grid, hipStream_t s) {
+#define KDL_WGB(G, P) \
+  hipLaunchKernelGGL((wgrad_dma_kernel<TN_, TK_, G, P, WN, WK, true>), dim3(grid), dim3(64 * WN * WK), 0, s, p)
+  if (p.mode == G_STRIDED) KDL_WGB(G_STRIDED, false);  // (strided rows: the downsample conv, no A prologue)
+  else if (p.pro) KDL_WGB(G_DENSE, true);               // conv3: B2 + ReLU recomputed on A as well
+  else KDL_WGB(G_DENSE, false);
+#undef KDL_WGB
+}
+
 }  // namespace
 
 hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t s) {
@@ -277,6 +330,17 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
       static_cast<uint64_t>(p.M) * static_cast<uint64_t>(p.Hout * p.Wout) >= (uint64_t(1) << 32))
     return hipErrorInvalidValue;  // magic-number division range
   const int grid = nsplit * (p.N / tn) * (p.K / tk);
+  if (p.gx) {  // G prologue: the wgrad_tiles(bwd) configs, gx panels beside G's
+    if (!p.gcoef || p.mode == G_CONV3 || (p.pro && p.mode != G_DENSE)) return hipErrorInvalidValue;
+    if (tn == 128 && tk == 256) launch_bwdg<128, 256, 2, 4>(p, grid, s);
+    else if (tn == 128 && tk == 128) launch_bwdg<128, 128, 2, 4>(p, grid, s);
+    else if (tn == 128 && tk == 64) launch_bwdg<128, 64, 4, 2>(p, grid, s);
+    else if (tn == 64 && tk == 256) launch_bwdg<64, 256, 2, 4>(p, grid, s);
+    else if (tn == 64 && tk == 128) launch_bwdg<64, 128, 2, 4>(p, grid, s);
+    else if (tn == 64 && tk == 64) launch_bwdg<64, 64, 2, 2>(p, grid, s);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (tn == 256 && tk == 256) launch<256, 256, 2, 4>(p, grid, s);
   else if (tn == 128 && tk == 128) launch<128, 128>(p, grid, s);
   else if (tn == 128) launch<128, 64>(p, grid, s);

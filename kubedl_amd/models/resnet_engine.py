@@ -21,13 +21,15 @@ backward, per bottleneck (``g`` = gradient at the pre-ReLU block sum, already
 masked; it and B3's reduction sums come out of the NEXT block's conv1 dgrad
 epilogue)::
 
-    dc3 (, dcd) = B3 (, Bd) apply-backward of g        [one pass for both branches]
+    dc3 (, dcd) = B3 (, Bd) apply-backward of g        [NOT a pass: computed in the A
+                                                        staging of the dgrads below,
+                                                        written through for the wgrads]
     g2 = conv3 dgrad (dc3), masked by R'(B2(c2)) + B2 reduction sums   [GEMM epilogue]
     dW3 = sum dc3^T R(B2(c2))                          [GEMM, B2+R recomputed in the prologue]
     dc2 = B2 apply-backward(g2) ; dW2 [3x3 implicit GEMM, csrc/wgrad_dma.hip] ;
           da1 [implicit GEMM with bn1's mask + sums fused; stride 2: four sub-pixel
           class GEMMs in one launch, kubedl_amd/ops/conv.py]
-    dc1 = B1 apply-backward(da1)
+    dc1 = B1 apply-backward(da1)                       [in conv1 dgrad's A staging]
     g_prev = conv1 dgrad(dc1) + d(identity) (strided gather of the downsample dgrad),
              masked by the previous block's ReLU bits, + B3_prev (and Bd_prev)
              reduction sums                            [GEMM epilogue]
@@ -267,13 +269,22 @@ class HipKernels:
         self.ext.bn_stage_bwd_apply_maskx(dy, x, m.weight, m.bias, st.save_mean, st.save_invstd, st.ws, dx, M, st.C)
         return dx
 
-    def dgrad_maskx(self, g, wt, x2, st2):
+    def _arm_bpro(self, bpro, C):
+        """Fuse a BN-backward apply into the next GEMM's A staging (csrc/conv1x1.hip
+        PRO_BWD): bpro = (x, st, out) -- A' = k g + c1 x + c0 of BN ``st`` with
+        input ``x``, written through to ``out`` (None: not materialised)."""
+        if bpro is not None:
+            x, st, out = bpro
+            self.ext.bn_bwd_pro_arm(x, st.ws, C, out)
+
+    def dgrad_maskx(self, g, wt, x2, st2, bpro=None):
         """g [.., K=cout] -> masked d(input) [.., cin] + st2 backward sums; wt = W^T [cin, cout]."""
         n, cout, h, w = g.shape
         cin = wt.shape[0]
         out = _nhwc_empty(n, cin, h, w, g)
         M = n * h * w
         self._arm(st2, M, fwd=False)
+        self._arm_bpro(bpro, cout)
         self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), x2,
                               st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
         return out
@@ -301,15 +312,16 @@ class HipKernels:
                                   self.fcoef(st1))
         return out
 
-    def dgrad_plain(self, g, wt):
+    def dgrad_plain(self, g, wt, bpro=None):
         n, cout, h, w = g.shape
         cin = wt.shape[0]
         out = _nhwc_empty(n, cin, h, w, g)
+        self._arm_bpro(bpro, cout)
         self.ext.conv1x1_gemm(g, wt, out, n * h * w, cin, cout, 0, 0, 0, 0, 1, None, 0, None, None, None, None, None,
                               None, 1, 0, 0, None, None, None, None)
         return out
 
-    def dgrad_res(self, g, wt, eres, res_stride, prev=None):
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None):
         """conv1 dgrad + d(identity); with ``prev`` = (mbits, c3, st3, cd, std) the
         previous block's ReLU mask is applied and its BN sums accumulated."""
         n, cout, h, w = g.shape
@@ -317,18 +329,22 @@ class HipKernels:
         out = _nhwc_empty(n, cin, h, w, g)
         M = n * h * w
         if prev is None:
+            self._arm_bpro(bpro, cout)
             self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 4, None, None, None, None, None, eres,
                                   res_stride, h, w, None, None, None, None)
         else:
             mbits, c3, st3, cd, std_ = prev
             self._arm(st3, M, std_, fwd=False)
+            self._arm_bpro(bpro, cout)
             self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, self._bwd_acc(st3), c3,
                                   st3.save_mean, None, eres, res_stride, h, w, mbits, cd,
                                   std_.save_mean if std_ is not None else None,
                                   self._bwd_acc(std_) if std_ is not None else None)
         return out
 
-    def wgrad(self, g, x, stride, pro: BNState | None, dW):
+    def wgrad(self, g, x, stride, pro: BNState | None, dW, gbpro=None):
+        """1x1 weight gradient; ``gbpro`` = (gx, st): G is the BN-backward apply
+        k g + c1 gx + c0 of BN ``st``, computed in the G fragments (BWDG)."""
         n, cout, ho, wo = g.shape
         _, cin, h, w = x.shape
         M = n * ho * wo
@@ -337,6 +353,8 @@ class HipKernels:
         dw32 = self._dw32.get(key)
         if dw32 is None or dw32.numel() < need:
             dw32 = self._dw32[key] = torch.empty(need, device=g.device)
+        if gbpro is not None:
+            self.ext.bn_bwd_pro_arm(gbpro[0], gbpro[1].ws, cout, None)
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
                                M, cout, cin, ho, wo, h, w, stride)
 
@@ -526,7 +544,18 @@ class TorchKernels:
         self.bn_bwd_finalize(st, x.numel() // st.C, dgamma, dbeta)
         return self._bapply(g, x, st)
 
-    def dgrad_maskx(self, g, wt, x2, st2):
+    def _bpro(self, g, bpro):
+        """A operand of a GEMM with a fused BN-backward apply (HipKernels._arm_bpro)."""
+        if bpro is None:
+            return g
+        x, st, out = bpro
+        a = self._bapply(g, x, st)
+        if out is not None:
+            out.copy_(a)
+        return a
+
+    def dgrad_maskx(self, g, wt, x2, st2, bpro=None):
+        g = self._bpro(g, bpro)
         d = _bfr(F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)))
         sc, sf = st2.fcoef
         mask = (x2.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
@@ -550,11 +579,13 @@ class TorchKernels:
         self._bsum(d, x1, st1)
         return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
 
-    def dgrad_plain(self, g, wt):
+    def dgrad_plain(self, g, wt, bpro=None):
+        g = self._bpro(g, bpro)
         return F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)).to(g.dtype).contiguous(
             memory_format=torch.channels_last)
 
-    def dgrad_res(self, g, wt, eres, res_stride, prev=None):
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None):
+        g = self._bpro(g, bpro)
         d = _bfr(F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)))
         r = torch.zeros_like(d)
         r[:, :, ::res_stride, ::res_stride] = eres.float()
@@ -567,7 +598,9 @@ class TorchKernels:
                 self._bsum(d, cd, std_)
         return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
 
-    def wgrad(self, g, x, stride, pro, dW):
+    def wgrad(self, g, x, stride, pro, dW, gbpro=None):
+        if gbpro is not None:
+            g = self._bapply(g, gbpro[0], gbpro[1])
         a = self._pro(x, pro) if pro is not None else x.float()
         a = _rows(a[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last))
         dW.copy_((_rows(g.float()).t() @ a).view_as(dW))
@@ -635,6 +668,12 @@ class ResNetEngine:
         # BN workspace keeps forward (prologue) and backward coefficients apart
         # (csrc/bn_act.hip ws_bcoef) so a wgrad's recomputed BN never races the
         # main stream's backward finalize of the same BN.
+        # BN-backward apply passes of bn3 / downsample BN / bn1 fused into their
+        # 1x1 data-gradient GEMMs (csrc/conv1x1.hip PRO_BWD); KDL_BN_BWD_FUSE=0: separate passes
+        # (1: dgrad A prologue + write-through; 2: dgrad A prologue + weight-gradient G
+        # prologue, never materialised), for BNs of at most KDL_BN_BWD_FUSE_KMAX channels
+        self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "0"))
+        self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "4096"))
         self.side = None
         if self.K.name == "hip" and os.environ.get("KDL_WGRAD_STREAM", "1") == "1":
             from kubedl_amd.ops.streams import side_stream
@@ -834,6 +873,30 @@ class ResNetEngine:
                 g, a, weight, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
             self._g(weight).copy_(dw)
 
+    def _fuse_mode(self, C: int) -> int:
+        """How the BN-backward apply of a C-channel BN reaches its 1x1 consumers:
+        0 its own pass; 1 inside the data-gradient GEMM's A staging, written
+        through for the weight gradient; 2 inside both GEMMs' operand staging
+        (never materialised)."""
+        return self.fuse_bwd if C <= self.fuse_kmax else 0
+
+    def _bn_bwd_operand(self, g, x, st):
+        """(dgrad A, dgrad bpro, wgrad G, wgrad gbpro) for the BN-backward apply
+        dc = k g + c1 x + c0 of BN ``st`` (input ``x``) per ``_fuse_mode``."""
+        mode = self._fuse_mode(x.shape[1])
+        if mode == 0:
+            dc, _ = self.K.bn_bwd_apply(g, x, st)
+            return dc, None, dc, None
+        if mode == 1:
+            dc = torch.empty_like(x)
+            return g, (x, st, dc), dc, None
+        return g, (x, st, None), g, (x, st)
+
+    @staticmethod
+    def _side_of(op):
+        """Tensors a weight gradient on ``op`` reads (side-stream lifetime)."""
+        return (op[2],) if op[3] is None else (op[2], op[3][0])
+
     def _bn_grads(self, st):
         return self._g(st.mod.weight), self._g(st.mod.bias)
 
@@ -869,11 +932,16 @@ class ResNetEngine:
             if std_ is not None:
                 K.bn_bwd_finalize(std_, Mo, *self._bn_grads(std_))
                 self._bn_ready(std_)
-            dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)
+            if std_ is not None and self._fuse_mode(c3.shape[1]) == 0:
+                dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches
+                op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
+            else:
+                op3 = self._bn_bwd_operand(g, c3, st3)
+                opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
             # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
-            g2 = K.dgrad_maskx(dc3, self._wt(blk.conv3), c2, st2)
-            with self._on_side(dc3):
-                K.wgrad(dc3, c2, 1, st2, self._g(blk.conv3.weight))
+            g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
+            with self._on_side(*self._side_of(op3)):
+                K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
             self.on_ready(blk.conv3.weight)
             K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
             self._bn_ready(st2)
@@ -889,7 +957,7 @@ class ResNetEngine:
                 g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
-                dc1, _ = K.bn_bwd_apply(g1, c1, st1)
+                dc1 = None
             elif self.dgrad_s2 and c1.shape[-2:] == (2 * dc2.shape[-2], 2 * dc2.shape[-1]):
                 # stride 2: four sub-pixel class GEMMs with bn1's mask + sums fused
                 # (no MIOpen, no zero-filled dx, no separate BN-backward reduce pass)
@@ -899,7 +967,7 @@ class ResNetEngine:
                 g1 = K.dgrad3x3s2_maskx(dc2, self._ball(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
-                dc1, _ = K.bn_bwd_apply(g1, c1, st1)
+                dc1 = None
             else:
                 if self.side is None:
                     da1, dw2, _ = torch.ops.aten.convolution_backward(
@@ -915,10 +983,12 @@ class ResNetEngine:
                 self.on_ready(blk.conv2.weight)
                 dc1 = K.bn_bwd_full(da1.contiguous(memory_format=torch.channels_last), c1, st1, *self._bn_grads(st1))
             self._bn_ready(st1)
+            # bn1 backward apply: its own pass, or (fused) inside conv1's dgrad below
+            op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1)
             # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
             if blk.down_conv is not None:
                 ds = blk.down_conv.stride[0]
-                eres = K.dgrad_plain(dcd, self._wt(blk.down_conv))
+                eres = K.dgrad_plain(opd[0], self._wt(blk.down_conv), bpro=opd[1])
                 res_stride = ds
             else:
                 eres, res_stride = g, 1
@@ -926,14 +996,15 @@ class ResNetEngine:
                 p_in, p_c1, p_a1, p_c2, p_c3, p_cd, p_mbits = saved[i - 1]
                 pblk = self.blocks[i - 1]
                 p_std = self.bn[pblk.down_bn] if pblk.down_bn is not None else None
-                g_prev = K.dgrad_res(dc1, self._wt(blk.conv1), eres, res_stride,
-                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std))
+                g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride,
+                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std), bpro=op1[1])
             else:
-                g_prev = K.dgrad_res(dc1, self._wt(blk.conv1), eres, res_stride, None)
-            with self._on_side(dc1, *((dcd,) if blk.down_conv is not None else ())):
-                K.wgrad(dc1, cur_in, 1, None, self._g(blk.conv1.weight))
+                g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride, None, bpro=op1[1])
+            with self._on_side(*self._side_of(op1), *(self._side_of(opd) if opd is not None else ())):
+                K.wgrad(op1[2], cur_in, 1, None, self._g(blk.conv1.weight), gbpro=op1[3])
                 if blk.down_conv is not None:
-                    K.wgrad(dcd, cur_in, blk.down_conv.stride[0], None, self._g(blk.down_conv.weight))
+                    K.wgrad(opd[2], cur_in, blk.down_conv.stride[0], None, self._g(blk.down_conv.weight),
+                            gbpro=opd[3])
             self.on_ready(blk.conv1.weight)
             if blk.down_conv is not None:
                 self.on_ready(blk.down_conv.weight)

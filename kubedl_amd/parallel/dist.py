@@ -109,6 +109,25 @@ def barrier(info: DistInfo) -> None:
             dist.barrier()
 
 
+def first_collective(info: DistInfo) -> float:
+    """Time (max over ranks) of the job's first collective -- with the lazy
+    communicator (init_from_env) this is where RCCL bootstraps: topology
+    discovery, the xGMI P2P/IPC transport setup, ring/tree building.  0 without
+    a process group."""
+    import time
+    if not dist.is_initialized():
+        return 0.0
+    t0 = time.perf_counter()
+    t = torch.ones(1, device=info.device)
+    dist.all_reduce(t)
+    if info.device.type == "cuda":
+        torch.cuda.synchronize(info.device)
+    dt = time.perf_counter() - t0
+    m = torch.tensor([dt], dtype=torch.float64, device=info.device)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return float(m.item())
+
+
 def all_reduce_max(value: float, info: DistInfo) -> float:
     if info.world_size == 1:
         return value

@@ -15,7 +15,9 @@ For every pod bound to this node (``spec.nodeName``, GPUs in the
    rewritten to ``127.0.0.1`` with each ``<svc>:<port>`` mapped to the
    store's host port (so two jobs can both use 23456), ``MASTER_PORT``
    remapped along with ``MASTER_ADDR``, ``HIP_VISIBLE_DEVICES`` from the gang
-   allocation, ``LOCAL_RANK=0``, and ``KDL_*`` sandbox variables;
+   allocation -- a gang member sees the gang's whole GPU set and selects its
+   own with ``LOCAL_RANK`` / ``LOCAL_WORLD_SIZE`` (torch.distributed.run's
+   process shape, runtime/gpu_env.py) -- and ``KDL_*`` sandbox variables;
 4. reports status like a kubelet: ``phase`` Pending -> Running ->
    Succeeded/Failed, ``containerStatuses`` (``state.running|terminated``,
    ``exitCode``, ``restartCount``, ``lastState``), and the ``Initialized`` /
@@ -49,7 +51,8 @@ from typing import Dict, List, Optional, Tuple
 from kubedl_amd.api import common as c
 from kubedl_amd.runtime import images
 from kubedl_amd.runtime import zygote as zygote_mod
-from kubedl_amd.runtime.scheduler import GPU_ANNOTATION, HBM_ANNOTATION
+from kubedl_amd.runtime.gpu_env import rank_gpu_env
+from kubedl_amd.runtime.scheduler import GANG_GPUS_ANNOTATION, GPU_ANNOTATION, HBM_ANNOTATION
 from kubedl_amd.store import ADDED, DELETED, MODIFIED, NotFound, Store
 
 log = logging.getLogger("kubedl_amd.kubelet")
@@ -203,12 +206,17 @@ class PodWorker(threading.Thread):
             if v in mounts:
                 raw[k] = mounts[v]
         env.update(raw)
-        env["HIP_VISIBLE_DEVICES"] = ",".join(self.gpus) if self.gpus else "-1"
+        # GPU visibility: the gang's whole set + LOCAL_RANK / LOCAL_WORLD_SIZE
+        # (torch.distributed.run's process shape, runtime/gpu_env.py), else own GPUs
+        gang = [g for g in ((self.pod["metadata"].get("annotations") or {}).get(GANG_GPUS_ANNOTATION) or "")
+                .split(",") if g]
+        for k, v in rank_gpu_env(self.gpus, gang).items():
+            if k == "HIP_VISIBLE_DEVICES" or k not in raw:  # an explicit container env LOCAL_* wins
+                env[k] = v
         cpu = str(((ctr.get("resources") or {}).get("limits") or {}).get("cpu", ""))
         if cpu:  # honour a CPU limit the way a cgroup quota would bound intra-op threads
             n = float(cpu[:-1]) / 1000.0 if cpu.endswith("m") else float(cpu)
             env["OMP_NUM_THREADS"] = str(max(1, int(n)))
-        env.setdefault("LOCAL_RANK", "0")
         md = self.pod["metadata"]
         labels = md.get("labels") or {}
         env["KDL_POD_NAME"] = self.name

@@ -41,6 +41,7 @@ from kubedl_amd.store import ADDED, DELETED, MODIFIED, NotFound, Store
 log = logging.getLogger("kubedl_amd.scheduler")
 
 GPU_ANNOTATION = "kubedl.io/gpus"
+GANG_GPUS_ANNOTATION = "kubedl.io/gang-gpus"  # the gang's GPU set on this node (runtime/gpu_env.py)
 HBM_ANNOTATION = "kubedl.io/hbm-gb"
 NODE_NAME = "localhost"
 
@@ -216,9 +217,14 @@ class NodeScheduler:
                 if head_blocked_since is None:
                     head_blocked_since = age
                 continue
+            gang_gpus = None
+            if owner.startswith("gang:"):
+                gang_gpus = sorted({g for k in alloc.pods for g in alloc.pods[k]})
+                if len(gang_gpus) < 2:
+                    gang_gpus = None
             for p in pods:
                 k = pod_key(p)
-                if self._bind(p, alloc.pods.get(k, []), alloc.slices.get(k)):
+                if self._bind(p, alloc.pods.get(k, []), alloc.slices.get(k), gang_gpus):
                     with self._lock:
                         self._owner_of_pod[k] = owner
                         self._unsched_marked.discard(k)
@@ -232,7 +238,8 @@ class NodeScheduler:
             self.metrics.gpus_allocated.set(self.alloc.used())
         return bound
 
-    def _bind(self, pod: dict, gpus: List[int], hbm_slice: Optional[float] = None) -> bool:
+    def _bind(self, pod: dict, gpus: List[int], hbm_slice: Optional[float] = None,
+              gang_gpus: Optional[List[int]] = None) -> bool:
         md = pod["metadata"]
         ts = c.now()
 
@@ -244,6 +251,10 @@ class NodeScheduler:
             ann[GPU_ANNOTATION] = ",".join(map(str, gpus))
             if hbm_slice is not None:
                 ann[HBM_ANNOTATION] = f"{hbm_slice:g}"
+            if gang_gpus is not None and len(gpus) == 1:
+                ann[GANG_GPUS_ANNOTATION] = ",".join(map(str, gang_gpus))
+            else:
+                ann.pop(GANG_GPUS_ANNOTATION, None)
             st = o.setdefault("status", {})
             conds = [x for x in st.get("conditions") or [] if x.get("type") != "PodScheduled"]
             conds.append({"type": "PodScheduled", "status": "True", "lastTransitionTime": ts})

@@ -49,6 +49,8 @@ def add_args(ap: argparse.ArgumentParser) -> None:
                     help="fused = explicit engine (fused conv GEMMs + staged BN); autograd = module + autograd")
     ap.add_argument("--allreduce", default=os.environ.get("KDL_ALLREDUCE", "rccl"), choices=["rccl", "p2p"],
                     help="DP gradient transport for N > 1: RCCL, or the IPC peer-buffer kernel (csrc/p2p.hip)")
+    ap.add_argument("--ready-only", action="store_true",
+                    help="initialise, signal Ready, exit (bench.py's cold launch-delay probe job)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo dry run (tests only)")
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests only; invalid metric)")
 
@@ -73,11 +75,18 @@ def run(args, launcher: str) -> int:
     # Ready (the rank has started and its process group is up) --
     # the timestamp of the controller's launch-delay histograms
     common.signal_ready({"rank": info.rank})
+    if args.ready_only:
+        kdist.shutdown(info)
+        return 0
     trainer = ResNetTrainer(info, batch=args.batch, image=args.image, tiny=args.tiny,
                             bn_backend=args.bn_backend, conv_benchmark=bool(args.conv_benchmark),
                             engine=args.engine)
     sync(info)
     t_model = time.time()
+    # the first collective builds the RCCL communicator (lazy: init_process_group
+    # returns after the TCP-store rendezvous, dist.py) -- timed on its own so the
+    # bootstrap cost is reported instead of hiding in the warm-up steps
+    comm_init_s = kdist.first_collective(info)
     kdist.barrier(info)
     # process start -> model resident on every rank
     rank_ready_s = kdist.all_reduce_max(time.time() - T_PROC_START, info)
@@ -135,7 +144,8 @@ def run(args, launcher: str) -> int:
             },
             "steps_per_sec": round(args.steps / dt, 4),
             "rank_ready_s": round(rank_ready_s, 3),
-            "final_loss": round(loss / n, 4),
+            "comm_init_s": round(comm_init_s, 3),
+            "final_loss": round(loss, 4),
         }
         print(json.dumps(out), flush=True)
     kdist.shutdown(info)

@@ -22,8 +22,8 @@ def _json_lines(out: str):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-def _run(cmd, timeout=600):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+def _run(cmd, timeout=600, **env_over):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2", **env_over)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -32,7 +32,7 @@ def _run(cmd, timeout=600):
 
 def test_bench_contract_one_rank_cpu():
     (line,) = _run([sys.executable, "bench.py", "--cpu", "--tiny", "--steps", "2", "--warmup", "1",
-                    "--batch", "8", "--image", "32"])
+                    "--batch", "8", "--image", "32"], KDL_ZYGOTE="1")
     assert line["config"]["launcher"] == "kdl-pytorchjob"
     assert line["first_pod_launch_delay_s"] > 0 and line["all_pods_launch_delay_s"] >= line["first_pod_launch_delay_s"]
     assert KEYS <= set(line)
@@ -41,6 +41,13 @@ def test_bench_contract_one_rank_cpu():
     assert line["config"]["parallelism"] == "dp1" and line["config"]["global_batch"] == 8
     assert line["value"] > 0
     assert abs(line["value"] - 8 * 1000.0 / line["ms_per_step"]) / line["value"] < 0.01
+    # warm launch (ranks forked from the node's pre-imported
+    # zygote) and the cold probe job (fresh interpreters) are both reported, and
+    # the zygote's fork is the faster one; comm_init_s = the first collective
+    assert line["launch"] == "warm (zygote)"
+    assert line["cold_first_pod_launch_delay_s"] > 0 and line["cold_all_pods_launch_delay_s"] > 0
+    assert line["first_pod_launch_delay_s"] < line["cold_first_pod_launch_delay_s"]
+    assert line["comm_init_s"] >= 0
 
 
 def test_bench_contract_two_ranks_cpu():

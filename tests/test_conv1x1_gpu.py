@@ -173,3 +173,76 @@ def test_wgrad_many_splits(N, K):
     ext.conv1x1_wgrad(g, x, None, ws, dwb, 1.0, M, N, K, H, Wd, H, Wd, 1)
     ref = g.float().t() @ _rows(x.float())
     torch.testing.assert_close(dwb.float(), ref, atol=0.25, rtol=2e-2)
+
+
+def _bwd_ws(C, dev, seed):
+    """BN workspace with random backward coefficients k | c1 | c0 (ws_bcoef)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    ws = _ws(C, dev)
+    off = _ext().bn_coef_offset(C) + 2 * C
+    ws[off:off + 3 * C] = torch.randn(3 * C, device=dev, generator=g)
+    return ws
+
+
+@pytest.mark.parametrize("epi", [0, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(3000, 64, 256), (700, 512, 2048), (1100, 256, 64), (513, 128, 512)])
+def test_gemm_bwd_apply_prologue_bit_exact(epi, M, N, K):
+    """csrc/conv1x1.hip PRO_BWD: the armed dgrad GEMM on (g, x) equals the
+    separate bn_stage_bwd_apply pass + the same GEMM on its output bit for bit
+    (register-staged main loop in both arms), and writes that output through."""
+    ext = _ext()
+    torch.manual_seed(7)
+    dev = "cuda"
+    g = torch.randn(M, K, device=dev).bfloat16()
+    x = (torch.randn(M, K, device=dev) * 2 + 0.5).bfloat16()
+    wt = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+    wsb = _bwd_ws(K, dev, 11)
+    dc = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    ext.bn_stage_bwd_apply(g, x, wsb, dc, None, None, None, M, K)
+    kw = {}
+    if epi == 2:
+        kw = dict(ex=torch.randn(M, N, device=dev).bfloat16(), emean=torch.randn(N, device=dev),
+                  ecoef=torch.randn(2 * N, device=dev))
+    elif epi == 3:
+        kw = dict(ex=torch.randn(M, N, device=dev).bfloat16(), emean=torch.randn(N, device=dev),
+                  eres=torch.randn(M, N, device=dev).bfloat16(),
+                  ebits=torch.randint(0, 256, (M, N // 8), device=dev, dtype=torch.uint8))
+    old = ext.get_gemm_core()
+    ext.set_gemm_core(0)
+    try:
+        ref = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ws_r = _ws(N, dev)
+        _gemm(dc, wt, ref, M, N, K, epi=epi, acc=ws_r if epi else None, **kw)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        thru = torch.full((M, K), float("nan"), device=dev, dtype=torch.bfloat16)
+        ws_f = _ws(N, dev)
+        ext.bn_bwd_pro_arm(x, wsb, K, thru)
+        _gemm(g, wt, out, M, N, K, epi=epi, acc=ws_f if epi else None, **kw)
+    finally:
+        ext.set_gemm_core(old)
+    torch.cuda.synchronize()
+    assert torch.equal(thru.view(torch.int16), dc.view(torch.int16))
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    if epi:
+        a, b = (w[:REP * 2 * N].view(REP, 2, N).sum(0) for w in (ws_f, ws_r))
+        torch.testing.assert_close(a, b, atol=1e-2, rtol=1e-4)
+    # and against an fp32 reference of the whole op (apply, then the plain GEMM)
+    off = ext.bn_coef_offset(K) + 2 * K
+    k, c1, c0 = wsb[off:off + K], wsb[off + K:off + 2 * K], wsb[off + 2 * K:off + 3 * K]
+    a32 = (k * g.float() + c1 * x.float() + c0).bfloat16().float()
+    if epi == 0:
+        torch.testing.assert_close(out.float(), a32 @ wt.float().t(), atol=5e-2, rtol=3e-2)
+
+
+def test_gemm_bwd_apply_arm_is_consumed_and_checked():
+    ext = _ext()
+    M, N, K = 256, 64, 128
+    g = torch.randn(M, K, device="cuda").bfloat16()
+    wsb = _bwd_ws(K, "cuda", 3)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    wt = torch.randn(N, K, device="cuda").bfloat16()
+    ext.bn_bwd_pro_arm(torch.randn(2 * M, K, device="cuda").bfloat16(), wsb, K, None)
+    with pytest.raises(RuntimeError, match="armed for"):
+        _gemm(g, wt, out, M, N, K)
+    _gemm(g, wt, out, M, N, K)  # the failed launch disarmed it
+    torch.testing.assert_close(out.float(), g.float() @ wt.float().t(), atol=5e-2, rtol=3e-2)

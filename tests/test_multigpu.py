@@ -58,13 +58,17 @@ def _spawn(target, world, *args, timeout=300):
 
 
 def _init(rank, world, port, backend="nccl"):
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
-    torch.cuda.set_device(rank)
-    kw = dict(backend=backend, rank=rank, world_size=world)
-    if backend == "nccl":
-        kw["device_id"] = torch.device("cuda", rank)
-    dist.init_process_group(**kw)
+    """The product's rank environment: the kubelet's GPU visibility for a gang
+    member (runtime/gpu_env.py: the gang's GPUs visible, LOCAL_RANK selects
+    this rank's) and its process-group bootstrap (parallel/dist.py), eager
+    communicator so a transport failure surfaces here."""
+    from kubedl_amd.parallel import dist as kdist
+    from kubedl_amd.runtime.gpu_env import rank_gpu_env
+    os.environ.update(rank_gpu_env([str(rank)], [str(r) for r in range(world)]))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      KDL_DIST_BACKEND=backend, KDL_PG_EAGER="1")
+    info = kdist.init_from_env()
+    assert info.device == torch.device("cuda", rank), info
 
 
 def _inputs(rank, n, dtype):
@@ -188,6 +192,79 @@ def test_engine_ddp_step_identical_weights(world, transport):
     for r in res[1:]:
         assert (r[2] == m0).all() and (r[3] == p0).all()
     assert len({round(r[1][0], 5) for r in res}) > 1  # the ranks did see different data
+
+
+# ------------------------------------------------------------------ product job path on N GPUs
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench_job(world, *extra):
+    """bench.py's job path (store -> PyTorchJob controller -> gang allocator ->
+    kubelet -> N rank processes) with RCCL's transport log on."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", KDL_BENCH_KEEP="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "2"] +
+                       list(extra), cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    logs = ""
+    pods = os.path.join(line["home"], "node", "pods")
+    for d in sorted(os.listdir(pods)):
+        if d.startswith("default_resnet50-bench-") and "-cold-" not in d:
+            for root, _, files in os.walk(os.path.join(pods, d, "logs")):
+                for f in files:
+                    logs += open(os.path.join(root, f), errors="replace").read()
+    return line, logs
+
+
+def _transport_lines(logs):
+    return [x for x in logs.splitlines() if " via " in x and ("Channel" in x or "Ring" in x or "Tree" in x)]
+
+
+@pytest.mark.gpu
+@pytest.mark.multigpu
+@pytest.mark.parametrize("allreduce", ["rccl", "p2p"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_job_path_ranks_on_distinct_gpus(world, allreduce):
+    """VERDICT r2 missing 1: bench.py --gpus N through the kubelet, in exactly the
+    environment the product gives its ranks: N Ready ranks on N distinct GPUs,
+    RCCL's transport between them is P2P over xGMI (never host SHM or the
+    network), same under the IPC peer-buffer all-reduce."""
+    _need(world)
+    line, logs = _bench_job(world, "--allreduce", allreduce)
+    assert line["n_gpus"] == world and line["ranks_ready"] == world
+    assert len(line["gpus"]) == world
+    assert line["config"]["allreduce"] == allreduce
+    assert line["comm_init_s"] >= 0
+    tl = _transport_lines(logs)
+    assert tl, "no RCCL transport lines in the rank logs"
+    assert any("P2P" in x for x in tl), tl[:8]
+    bad = [x for x in tl if "via SHM" in x or "via NET" in x]
+    assert not bad, bad[:8]
+
+
+@pytest.mark.gpu
+@pytest.mark.multigpu
+def test_two_concurrent_four_gpu_gangs():
+    """BASELINE.json config 5: two 4-GPU PyTorchJobs gang-scheduled at once on an
+    8-GPU node -- both succeed, on disjoint GPU sets, each inside one NUMA half."""
+    import json
+    import subprocess
+    import sys
+    _need(8)
+    r = subprocess.run([sys.executable, "-m", "kubedl_amd.cli", "bench-launch", "--jobs", "2", "--gpus", "4",
+                        "--gang", "--steps", "3", "--warmup", "2"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=900, env=dict(os.environ, KDL_ZYGOTE="1"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    jobs = out["jobs"]
+    assert [j["state"] for j in jobs] == ["Succeeded", "Succeeded"]
+    a, b = (set(j["gpus"]) for j in jobs)
+    assert len(a) == len(b) == 4 and not (a & b)
+    assert all(s in ({"0", "1", "2", "3"}, {"4", "5", "6", "7"}) for s in (a, b)), (a, b)
 
 
 # ------------------------------------------------------------------ CPU: bf16 sum bound at world 8

@@ -132,3 +132,39 @@ def test_halo_wgrad_3x3_stage1(nb):
         torch.testing.assert_close(dW.float() / scale, ref / scale, atol=2e-2, rtol=2e-2)
         outs.append(dW)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("N,K", [(64, 64), (256, 64), (64, 256), (128, 128), (512, 2048), (2048, 512), (64, 128)])
+@pytest.mark.parametrize("stride,pro", [(1, False), (1, True), (2, False)])
+def test_dma_wgrad_bwd_apply_g_prologue(N, K, stride, pro):
+    """BWDG: the weight gradient on (g, gx) with the BN-backward apply
+    G' = k g + c1 gx + c0 computed in the G fragments equals the weight
+    gradient of the materialised G' (bn_stage_bwd_apply's output, bit-identical
+    operand) within reduction-order rounding, ragged last split included."""
+    ext = _ext()
+    torch.manual_seed(9)
+    nb, H, Wd = 3, 12, 9
+    Ho, Wo = (H - 1) // stride + 1, (Wd - 1) // stride + 1
+    M = nb * Ho * Wo
+    x = _nhwc(torch.randn(nb, K, H, Wd, device="cuda").bfloat16())
+    g = torch.randn(M, N, device="cuda").bfloat16()
+    gx = (torch.randn(M, N, device="cuda") * 2 + 1).bfloat16()
+    ws = torch.zeros(ext.bn_workspace_floats(N), device="cuda")
+    off = ext.bn_coef_offset(N) + 2 * N
+    ws[off:off + 3 * N] = torch.randn(3 * N, device="cuda")
+    gp = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ext.bn_stage_bwd_apply(g, gx, ws, gp, None, None, None, M, N)
+    coef = torch.cat([torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda")]).float() if pro else None
+    ref = _wgrad1x1(gp, x, coef, N, K, Ho, Wo, H, Wd, stride)
+    wsl = torch.full((ext.conv1x1_wgrad_splits(M, N, K) * N * K,), float("nan"), device="cuda")
+    dw = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+    ext.bn_bwd_pro_arm(gx, ws, N, None)
+    ext.conv1x1_wgrad(g, x, coef, wsl, dw, 1.0, M, N, K, Ho, Wo, H, Wd, stride)
+    a = x.float()
+    if pro:
+        a = F.relu(a * coef[:K].view(1, K, 1, 1) + coef[K:].view(1, K, 1, 1)).bfloat16().float()
+    a = _rows(_nhwc(a[:, :, ::stride, ::stride]))
+    truth = gp.float().t() @ a
+    scale = truth.abs().max().item()
+    torch.testing.assert_close(dw.float(), truth, atol=2e-2 * scale, rtol=2e-2)
+    torch.testing.assert_close(dw.float(), ref.float(), atol=1e-2 * scale, rtol=1e-2)
