@@ -561,8 +561,14 @@ void embed_gather(const at::Tensor& table, const at::Tensor& idx, int64_t F, at:
             "embed_gather");
 }
 
+const int* opt_count(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "ucount: int32 GPU tensor");
+  return t->data_ptr<int>();
+}
+
 at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64_t D, const at::Tensor& order,
-                          const at::Tensor& seg) {
+                          const at::Tensor& seg, const c10::optional<at::Tensor>& ucount) {
   TORCH_CHECK(rows.is_cuda() && rows.dim() == 2 && rows.stride(1) == 1, "segment_reduce: rows [B, ld]");
   TORCH_CHECK(order.scalar_type() == at::kLong && seg.scalar_type() == at::kLong && order.is_contiguous() &&
                   seg.is_contiguous(),
@@ -573,14 +579,15 @@ at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64
   auto out = at::empty({U, D}, rows.options().dtype(at::kFloat));
   check_hip(kdl::segment_reduce(rows.data_ptr(), dtype_code(rows), static_cast<int>(F), static_cast<int>(rows.stride(0)),
                                 static_cast<int>(col0), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
-                                static_cast<int>(U), static_cast<int>(D), out.data_ptr<float>(), cur_stream()),
+                                static_cast<int>(U), static_cast<int>(D), out.data_ptr<float>(), cur_stream(),
+                                opt_count(ucount)),
             "segment_reduce");
   return out;
 }
 
 void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at::Tensor& seg,
                      const at::Tensor& rows_local, at::Tensor table, at::Tensor accum, double lr, double eps,
-                     double scale) {
+                     double scale, const c10::optional<at::Tensor>& ucount) {
   TORCH_CHECK(grads.is_cuda() && grads.scalar_type() == at::kFloat && grads.is_contiguous(), "segment_adagrad: grads");
   TORCH_CHECK(table.scalar_type() == at::kFloat && accum.scalar_type() == at::kFloat && table.is_contiguous() &&
                   accum.is_contiguous() && table.sizes() == accum.sizes(),
@@ -592,8 +599,65 @@ void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at:
                                  rows_local.data_ptr<int64_t>(), static_cast<int>(seg.numel() - 1),
                                  static_cast<int>(table.size(1)), table.data_ptr<float>(), accum.data_ptr<float>(),
                                  static_cast<float>(lr), static_cast<float>(eps), static_cast<float>(scale),
-                                 cur_stream()),
+                                 cur_stream(), opt_count(ucount)),
             "segment_adagrad");
+}
+
+int64_t dedup_table_slots(int64_t n) { return kdl::dedup_table_slots(static_cast<int>(n)); }
+
+// the CSR half of dedup_csr, later in the step (sizes from that dedup_csr call)
+void csr_from_inverse_only(const at::Tensor& inv, const at::Tensor& sizes, const at::Tensor& count, at::Tensor bsum,
+                           at::Tensor cursor, at::Tensor seg, at::Tensor order) {
+  const int64_t n = inv.numel();
+  TORCH_CHECK(n > 0 && inv.is_cuda() && inv.scalar_type() == at::kLong && inv.is_contiguous(), "csr: inv");
+  TORCH_CHECK(sizes.scalar_type() == at::kInt && sizes.numel() >= n + 1 && cursor.scalar_type() == at::kInt &&
+                  cursor.numel() >= n + 1 && count.scalar_type() == at::kInt && bsum.scalar_type() == at::kInt &&
+                  bsum.numel() >= (n + 1) / 1024 + 1,
+              "csr: int32 sizes/cursor/count/bsum");
+  TORCH_CHECK(seg.scalar_type() == at::kLong && seg.numel() >= n + 1 && order.scalar_type() == at::kLong &&
+                  order.numel() >= n,
+              "csr: int64 seg/order");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(inv.device());
+  check_hip(kdl::csr_from_inverse(inv.data_ptr<int64_t>(), static_cast<int>(n), sizes.data_ptr<int>(),
+                                  count.data_ptr<int>(), bsum.data_ptr<int>(), cursor.data_ptr<int>(),
+                                  seg.data_ptr<int64_t>(), order.data_ptr<int64_t>(), cur_stream()),
+            "csr_from_inverse");
+}
+
+// ws: (keys int64 [T] filled -1, slot_of int32 [n], slot_uid int32 [T], bsum int32 [T/1024 + n/1024 + 2],
+//      sizes int32 [n + 1], cursor int32 [n + 1]); returns nothing, fills uniq/inv/count/seg/order
+void dedup_csr(const at::Tensor& ids, at::Tensor keys, at::Tensor slot_of, at::Tensor slot_uid, at::Tensor bsum,
+               at::Tensor sizes, at::Tensor cursor, at::Tensor uniq, at::Tensor inv, at::Tensor count, at::Tensor seg,
+               at::Tensor order, bool with_csr) {
+  const int64_t n = ids.numel();
+  const int64_t T = kdl::dedup_table_slots(static_cast<int>(n));
+  auto chk = [](const at::Tensor& t, at::ScalarType st, int64_t numel, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == st && t.is_contiguous() && t.numel() >= numel, "dedup_csr: ", what);
+  };
+  chk(ids, at::kLong, n, "ids int64");
+  chk(keys, at::kLong, T, "keys int64 [T]");
+  chk(slot_of, at::kInt, n, "slot_of");
+  chk(slot_uid, at::kInt, T, "slot_uid");
+  chk(bsum, at::kInt, T / 1024 + (n + 1) / 1024 + 2, "bsum");
+  chk(sizes, at::kInt, n + 1, "sizes");
+  chk(cursor, at::kInt, n + 1, "cursor");
+  chk(uniq, at::kLong, n, "uniq");
+  chk(inv, at::kLong, n, "inv");
+  chk(count, at::kInt, 1, "count");
+  chk(seg, at::kLong, n + 1, "seg");
+  chk(order, at::kLong, n, "order");
+  TORCH_CHECK(n > 0 && n < (1 << 30), "dedup_csr: 0 < n < 2^30");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(ids.device());
+  check_hip(kdl::dedup_ids(ids.data_ptr<int64_t>(), static_cast<int>(n), keys.data_ptr(), static_cast<int>(T),
+                           slot_of.data_ptr<int>(), slot_uid.data_ptr<int>(), bsum.data_ptr<int>(),
+                           uniq.data_ptr<int64_t>(), inv.data_ptr<int64_t>(), count.data_ptr<int>(),
+                           sizes.data_ptr<int>(), cur_stream()),
+            "dedup_ids");
+  if (with_csr)
+    check_hip(kdl::csr_from_inverse(inv.data_ptr<int64_t>(), static_cast<int>(n), sizes.data_ptr<int>(),
+                                    count.data_ptr<int>(), bsum.data_ptr<int>(), cursor.data_ptr<int>(),
+                                    seg.data_ptr<int64_t>(), order.data_ptr<int64_t>(), cur_stream()),
+              "csr_from_inverse");
 }
 
 
@@ -1250,6 +1314,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
+  m.def("dedup_table_slots", &dedup_table_slots, "hash-table slots dedup_csr needs for n ids");
+  m.def("csr_from_inverse_only", &csr_from_inverse_only, "CSR (seg, order) of a dedup_csr inverse, positions ascending per id");
+  m.def("dedup_csr", &dedup_csr, "sync-free id de-duplication (uniq/inv/count on the device) + optional CSR of the inverse");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
   m.def("bn_bwd_pro_arm", &bn_bwd_pro_arm, "fuse this BN's backward apply (input x, workspace ws) into the next conv1x1_gemm's A (or conv1x1_wgrad's G) staging; optional write-through tensor");

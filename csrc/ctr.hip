@@ -220,14 +220,16 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__
 // Row j = b*F + f of a [B, ld] activation-gradient matrix lives at
 // rows + b*ld + col0 + f*D (the layout embed_gather wrote).  Rows order[j]
 // are summed per segment [seg[u], seg[u+1]); one wave per segment.
+// ``ucount`` (optional): the live segment count on the device (U is then the
+// capacity the grid was sized for) -- no host round trip for data-dependent U.
 template <typename T>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, int ld, int col0,
                                                              const int64_t* __restrict__ order,
                                                              const int64_t* __restrict__ seg, int U, int D,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, const int* __restrict__ ucount) {
   const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (u >= U) return;
+  if (u >= (ucount ? *ucount : U)) return;
   const int64_t s0 = seg[u], s1 = seg[u + 1];
   for (int c = lane * 4; c < D; c += 256) {
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -254,10 +256,11 @@ __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __res
                                                               const int64_t* __restrict__ seg,
                                                               const int64_t* __restrict__ rows_local, int U, int D,
                                                               float* __restrict__ table, float* __restrict__ accum,
-                                                              float lr, float eps, float scale) {
+                                                              float lr, float eps, float scale,
+                                                              const int* __restrict__ ucount) {
   const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (u >= U) return;
+  if (u >= (ucount ? *ucount : U)) return;
   const int64_t s0 = seg[u], s1 = seg[u + 1];
   const int64_t row = rows_local[u];
   float* w = table + row * static_cast<int64_t>(D);
@@ -448,23 +451,269 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
 }
 
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
-                          const int64_t* seg, int U, int D, float* out, hipStream_t s) {
+                          const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount) {
   if (U <= 0) return hipSuccess;
   dim3 grid((U + 3) / 4);
   if (dtype == 1)
     hipLaunchKernelGGL((segment_reduce_kernel<bf16_t>), grid, dim3(256), 0, s, static_cast<const bf16_t*>(rows), F,
-                       ld, col0, order, seg, U, D, out);
+                       ld, col0, order, seg, U, D, out, ucount);
   else
     hipLaunchKernelGGL((segment_reduce_kernel<float>), grid, dim3(256), 0, s, static_cast<const float*>(rows), F, ld,
-                       col0, order, seg, U, D, out);
+                       col0, order, seg, U, D, out, ucount);
   return hipGetLastError();
 }
 
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
-                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s) {
+                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s,
+                           const int* ucount) {
   if (U <= 0) return hipSuccess;
   hipLaunchKernelGGL(segment_adagrad_kernel, dim3((U + 3) / 4), dim3(256), 0, s, grads, order, seg, rows_local, U, D,
-                     table, accum, lr, eps, scale);
+                     table, accum, lr, eps, scale, ucount);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- sync-free dedup + CSR
+// torch.unique / argsort / bincount of the embedding exchange return
+// data-dependent sizes, i.e. a device -> host copy every step, and run as
+// rocprim merge sorts.  Here every size is a CAPACITY (n ids -> at most n
+// unique ids) and the live count stays on the device:
+//
+//   insert   open-addressing hash table (T = pow2 >= 2n slots of int64 keys,
+//            empty = -1, linear probing, 64-bit atomicCAS): slot_of[i]
+//   count    occupied slots per 1024-slot chunk
+//   assign   unique id of each occupied slot = its rank in slot order
+//            (chunk prefix + in-chunk scan): uniq[uid] = key; the key is reset
+//            to empty (the table cleans itself for the next call); the last
+//            chunk writes the count
+//   inverse  inv[i] = uid of slot_of[i]; uniq[count..n) padded with uniq[0]
+//            (a fixed-size gather over the capacity stays in bounds);
+//            segment sizes by atomic counting
+//   csr      seg = exclusive scan of the sizes (count + assign again), the
+//            positions scattered into their segments (atomic cursors: any
+//            order), then each segment sorted by position (one wave per
+//            segment) -- the gradient sums run in position order: bitwise
+//            reproducible, unlike an atomic float accumulation.
+// Which slot an id lands in depends on insertion races, so unique-id ORDER is
+// not reproducible; nothing numeric depends on it (per-row sums and updates).
+namespace {
+constexpr int kChunk = 1024;  // slots (or counts) per scan block: 256 threads x 4
+constexpr long long kEmpty = -1;
+
+__device__ __forceinline__ uint32_t hash64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+__global__ __launch_bounds__(256) void dedup_insert_kernel(const int64_t* __restrict__ ids, int n,
+                                                           unsigned long long* __restrict__ keys, uint32_t mask,
+                                                           int* __restrict__ slot_of) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long id = static_cast<unsigned long long>(ids[i]);
+  uint32_t h = hash64(id) & mask;
+  // T >= 2n: at most n keys, so a free or matching slot exists within T probes
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long k = keys[h];
+    if (k == id) break;
+    if (k == static_cast<unsigned long long>(kEmpty)) {
+      const unsigned long long prev = atomicCAS(keys + h, static_cast<unsigned long long>(kEmpty), id);
+      if (prev == static_cast<unsigned long long>(kEmpty) || prev == id) break;
+    }
+    h = (h + 1) & mask;
+  }
+  slot_of[i] = static_cast<int>(h);
+}
+
+// Block b: the number of non-zero flags in [b * kChunk, +kChunk) -> bsum[b].
+// mode 0: flags are occupied hash slots (keys != empty); mode 1: int counts.
+__global__ __launch_bounds__(256) void chunk_count_kernel(const unsigned long long* __restrict__ keys,
+                                                          const int* __restrict__ vals, int len, int mode,
+                                                          int* __restrict__ bsum) {
+  __shared__ int part[256];
+  const int base = blockIdx.x * kChunk + threadIdx.x * 4;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = base + k;
+    if (j < len) c += mode == 0 ? (keys[j] != static_cast<unsigned long long>(kEmpty)) : vals[j];
+  }
+  part[threadIdx.x] = c;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = part[0];
+}
+
+// exclusive prefix of this block's chunk: sum of bsum[0..b) + in-chunk scan
+__device__ __forceinline__ int chunk_prefix(const int* bsum, int* part) {
+  int acc = 0;
+  for (int j = threadIdx.x; j < static_cast<int>(blockIdx.x); j += 256) acc += bsum[j];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  const int pre = part[0];
+  __syncthreads();
+  return pre;
+}
+
+__device__ __forceinline__ int block_exclusive_scan(int v, int* part) {
+  part[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive
+    const int add = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += add;
+    __syncthreads();
+  }
+  const int incl = part[threadIdx.x];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(256) void dedup_assign_kernel(unsigned long long* __restrict__ keys, int T,
+                                                           const int* __restrict__ bsum, int* __restrict__ slot_uid,
+                                                           int64_t* __restrict__ uniq, int* __restrict__ count) {
+  __shared__ int part[256];
+  const int pre = chunk_prefix(bsum, part);
+  const int base = blockIdx.x * kChunk + threadIdx.x * 4;
+  unsigned long long k4[4];
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = base + k;
+    k4[k] = j < T ? keys[j] : static_cast<unsigned long long>(kEmpty);
+    c += k4[k] != static_cast<unsigned long long>(kEmpty);
+  }
+  int uid = pre + block_exclusive_scan(c, part);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = base + k;
+    if (k4[k] != static_cast<unsigned long long>(kEmpty)) {
+      slot_uid[j] = uid;
+      uniq[uid] = static_cast<int64_t>(k4[k]);
+      keys[j] = static_cast<unsigned long long>(kEmpty);  // clean for the next call
+      ++uid;
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) *count = uid;
+}
+
+__global__ __launch_bounds__(256) void dedup_inverse_kernel(const int* __restrict__ slot_of, int n,
+                                                            const int* __restrict__ slot_uid,
+                                                            int64_t* __restrict__ inv, int64_t* __restrict__ uniq,
+                                                            const int* __restrict__ count, int* __restrict__ sizes) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int u = slot_uid[slot_of[i]];
+  inv[i] = u;
+  atomicAdd(sizes + u, 1);
+  if (i >= *count) uniq[i] = uniq[0];
+}
+
+// seg[u] = exclusive prefix of sizes (u <= n); cursor[u] = 0 for the scatter
+__global__ __launch_bounds__(256) void csr_assign_kernel(const int* __restrict__ sizes, int len,
+                                                         const int* __restrict__ bsum, int64_t* __restrict__ seg,
+                                                         int* __restrict__ cursor) {
+  __shared__ int part[256];
+  const int pre = chunk_prefix(bsum, part);
+  const int base = blockIdx.x * kChunk + threadIdx.x * 4;
+  int v[4], c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = base + k < len ? sizes[base + k] : 0;
+    c += v[k];
+  }
+  int off = pre + block_exclusive_scan(c, part);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = base + k;
+    if (j < len) {
+      seg[j] = off;
+      cursor[j] = 0;
+    }
+    off += v[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void csr_scatter_kernel(const int64_t* __restrict__ inv, int n,
+                                                          const int64_t* __restrict__ seg, int* __restrict__ cursor,
+                                                          int64_t* __restrict__ order) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int u = static_cast<int>(inv[i]);
+  order[seg[u] + atomicAdd(cursor + u, 1)] = i;
+}
+
+// one wave per segment: sort its positions ascending, in place
+__global__ __launch_bounds__(256) void csr_sort_kernel(const int64_t* __restrict__ seg, int64_t* __restrict__ order,
+                                                       const int* __restrict__ count) {
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (u >= *count) return;
+  const int64_t s0 = seg[u], len = seg[u + 1] - s0;
+  if (len <= 1) return;
+  int64_t* o = order + s0;
+  if (len <= 64) {  // wave bitonic sort of one value per lane (pad: INT64_MAX)
+    int64_t v = lane < len ? o[lane] : INT64_MAX;
+    for (int k = 2; k <= 64; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int64_t w = __shfl_xor(v, j);
+        const bool up = (lane & k) == 0;
+        const bool lower = (lane & j) == 0;
+        const int64_t lo = v < w ? v : w, hi = v < w ? w : v;
+        v = (lower == up) ? lo : hi;
+      }
+    }
+    if (lane < len) o[lane] = v;
+    return;
+  }
+  // long segment (a hot id): odd-even transposition sort, the wave sweeping pairs
+  for (int64_t pass = 0; pass < len; ++pass) {
+    for (int64_t a = (pass & 1) + 2 * lane; a + 1 < len; a += 128) {
+      const int64_t x = o[a], y = o[a + 1];
+      if (x > y) { o[a] = y; o[a + 1] = x; }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pass's swaps land before the next pass reads
+  }
+}
+}  // namespace
+
+int dedup_table_slots(int n) {
+  int T = 1024;
+  while (T < 2 * n) T <<= 1;
+  return T;
+}
+
+hipError_t dedup_ids(const int64_t* ids, int n, void* keys, int T, int* slot_of, int* slot_uid, int* bsum,
+                     int64_t* uniq, int64_t* inv, int* count, int* sizes, hipStream_t s) {
+  if (n <= 0 || T < 2 * n || (T & (T - 1)) || T % kChunk) return hipErrorInvalidValue;
+  KDL_CHECK_HIP(hipMemsetAsync(sizes, 0, static_cast<size_t>(n + 1) * sizeof(int), s));
+  auto* k = static_cast<unsigned long long*>(keys);
+  hipLaunchKernelGGL(dedup_insert_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ids, n, k,
+                     static_cast<uint32_t>(T - 1), slot_of);
+  const int nb = T / kChunk;
+  hipLaunchKernelGGL(chunk_count_kernel, dim3(nb), dim3(256), 0, s, k, static_cast<const int*>(nullptr), T, 0, bsum);
+  hipLaunchKernelGGL(dedup_assign_kernel, dim3(nb), dim3(256), 0, s, k, T, bsum, slot_uid, uniq, count);
+  hipLaunchKernelGGL(dedup_inverse_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slot_of, n, slot_uid, inv, uniq,
+                     count, sizes);
+  return hipGetLastError();
+}
+
+hipError_t csr_from_inverse(const int64_t* inv, int n, const int* sizes, const int* count, int* bsum, int* cursor,
+                            int64_t* seg, int64_t* order, hipStream_t s) {
+  if (n <= 0) return hipErrorInvalidValue;
+  const int len = n + 1;
+  const int nb = (len + kChunk - 1) / kChunk;
+  hipLaunchKernelGGL(chunk_count_kernel, dim3(nb), dim3(256), 0, s, static_cast<const unsigned long long*>(nullptr),
+                     sizes, len, 1, bsum);
+  hipLaunchKernelGGL(csr_assign_kernel, dim3(nb), dim3(256), 0, s, sizes, len, bsum, seg, cursor);
+  hipLaunchKernelGGL(csr_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, inv, n, seg, cursor, order);
+  hipLaunchKernelGGL(csr_sort_kernel, dim3((n + 3) / 4), dim3(256), 0, s, seg, order, count);
   return hipGetLastError();
 }
 

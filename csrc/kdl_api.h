@@ -181,10 +181,23 @@ hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float
                         int K, void* dx, float* dw_part, float* db_part, hipStream_t s);
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s);
+// ucount (optional): the live segment count on the device; U is then a capacity
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
-                          const int64_t* seg, int U, int D, float* out, hipStream_t s);
+                          const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount = nullptr);
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
-                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s);
+                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s,
+                           const int* ucount = nullptr);
+// Sync-free de-duplication of n int64 ids (csrc/ctr.hip): uniq [n] (first *count
+// valid, the rest padded with uniq[0]), inv [n], count [1] and the segment sizes
+// [n + 1] on the device.  keys: T = dedup_table_slots(n) int64 slots, all -1
+// initially (the call leaves them -1 again); slot_of [n], slot_uid [T], bsum [T / 1024].
+int dedup_table_slots(int n);
+hipError_t dedup_ids(const int64_t* ids, int n, void* keys, int T, int* slot_of, int* slot_uid, int* bsum,
+                     int64_t* uniq, int64_t* inv, int* count, int* sizes, hipStream_t s);
+// CSR of the inverse map: seg [n + 1] (exclusive scan of sizes), order [n] =
+// positions grouped by unique id, ascending within each group (deterministic sums).
+hipError_t csr_from_inverse(const int64_t* inv, int n, const int* sizes, const int* count, int* bsum, int* cursor,
+                            int64_t* seg, int64_t* order, hipStream_t s);
 
 
 // ---- conv1x1.hip (ResNet 1x1 convs as MFMA GEMMs with fused BN prologue/epilogues)

@@ -28,6 +28,7 @@ On CPU (tests) every op has a torch composition with the same semantics.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -160,6 +161,56 @@ class DenseTower(nn.Module):
 
 
 # ---------------------------------------------------------------- sparse embedding
+class DeviceDedup:
+    """Sync-free de-duplication of a step's ids on the GPU (csrc/ctr.hip
+    ``dedup_csr``): every output is sized by the CAPACITY n (the id count) and
+    the number of unique ids stays on the device, so the exchange never copies
+    a size to the host (``torch.unique`` / ``argsort`` / ``bincount`` do, and
+    run rocprim merge sorts).  Workspaces are kept per n; the hash table
+    cleans itself in each call."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._ws = {}
+        self._ar = {}
+
+    def _buffers(self, n: int):
+        ws = self._ws.get(n)
+        if ws is None:
+            ext = _ext.load()
+            T = ext.dedup_table_slots(n)
+            i32 = dict(dtype=torch.int32, device=self.device)
+            i64 = dict(dtype=torch.int64, device=self.device)
+            ws = dict(keys=torch.full((T,), -1, **i64), slot_of=torch.empty(n, **i32),
+                      slot_uid=torch.empty(T, **i32), bsum=torch.empty(T // 1024 + (n + 1) // 1024 + 2, **i32),
+                      sizes=torch.empty(n + 1, **i32), cursor=torch.empty(n + 1, **i32))
+            self._ws[n] = ws
+        return ws
+
+    def arange(self, n: int):
+        """(order, seg) of n distinct segments of one row each (a push of the
+        pull's already-unique ids)."""
+        a = self._ar.get(n)
+        if a is None:
+            a = self._ar[n] = (torch.arange(n, device=self.device), torch.arange(n + 1, device=self.device))
+        return a
+
+    def __call__(self, ids: torch.Tensor, csr: bool = True):
+        """ids [n] int64 -> (uniq [n], inv [n], count [1] int32, seg [n+1], order [n])
+        with uniq[:count] the distinct ids (padded with uniq[0]) and order/seg
+        the positions of each unique id, ascending (valid when ``csr``)."""
+        n = ids.numel()
+        ws = self._buffers(n)
+        uniq = torch.empty(n, dtype=torch.int64, device=self.device)
+        inv = torch.empty(n, dtype=torch.int64, device=self.device)
+        count = torch.empty(1, dtype=torch.int32, device=self.device)
+        seg = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        order = torch.empty(n, dtype=torch.int64, device=self.device)
+        _ext.load().dedup_csr(ids.contiguous(), ws["keys"], ws["slot_of"], ws["slot_uid"], ws["bsum"], ws["sizes"],
+                              ws["cursor"], uniq, inv, count, seg, order, csr)
+        return uniq, inv, count, seg, order
+
+
 def _a2a(out_splits: List[int], in_splits: List[int], t: torch.Tensor, group) -> torch.Tensor:
     out = t.new_empty((sum(out_splits),) + tuple(t.shape[1:]))
     dist.all_to_all_single(out, t.contiguous(), out_splits, in_splits, group=group)
@@ -171,7 +222,8 @@ class ShardedEmbedding:
     the owner ranks of ``group``; Adagrad state lives next to each shard."""
 
     def __init__(self, vocab: int, dim: int, owners: List[int], rank: int, world: int, device,
-                 group=None, lr: float = 0.05, eps: float = 1e-8, init_std: float = 0.01, seed: int = 0):
+                 group=None, lr: float = 0.05, eps: float = 1e-8, init_std: float = 0.01, seed: int = 0,
+                 max_ids: Optional[int] = None, slack: Optional[float] = None):
         self.vocab, self.dim = vocab, dim
         self.owners = list(owners)
         self.n_own = len(owners)
@@ -187,6 +239,25 @@ class ShardedEmbedding:
         self.accum = torch.zeros(rows, dim, device=self.device)
         self.use_hip = self.device.type == "cuda" and _ext.available()
         self._ctx = None
+        # the sync-free path (DeviceDedup, capacity-sized buffers, device-side
+        # counts) serves one-owner embeddings on the GPU
+        self.dedup = DeviceDedup(self.device) if self.use_hip else None
+        # Multi-rank exchange at FIXED capacity (``max_ids`` = the per-pull id bound
+        # every rank knows from the job config, e.g. batch x fields): each rank sends
+        # every owner a slot block of ``cap`` ids, so all_to_all_single runs with
+        # equal splits and no per-step size exchange to the host.  cap = max_ids
+        # cannot overflow; ``slack`` (KDL_CTR_A2A_SLACK) sizes it to slack x the
+        # uniform share max_ids / n_own instead -- an overflow is flagged on the
+        # device and raised at the next pull.
+        self.max_ids = max_ids
+        if max_ids is not None:
+            sl = slack if slack is not None else float(os.environ.get("KDL_CTR_A2A_SLACK", "0") or 0)
+            self.cap = max_ids if sl <= 0 else min(max_ids, int(math.ceil(sl * max_ids / self.n_own)) + 64)
+            self.cap = max(self.cap, 1)
+            self._owner_rank = torch.tensor(self.owners, dtype=torch.int64, device=self.device)
+            self._ovf = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._ovf_host = torch.zeros(1, dtype=torch.int32, pin_memory=self.device.type == "cuda")
+            self._ovf_evt = None
 
     # ------------------------------------------------------------ helpers
     def _local_gather(self, local_rows: torch.Tensor) -> torch.Tensor:
@@ -217,7 +288,7 @@ class ShardedEmbedding:
             seg[1:] = torch.cumsum(counts, 0)
         if self.use_hip:
             _ext.load().segment_adagrad(grads.contiguous().float(), order, seg, uniq, self.table, self.accum,
-                                        self.lr, self.eps, scale)
+                                        self.lr, self.eps, scale, None)
             return
         g = torch.zeros(uniq.numel(), self.dim, device=self.device).index_add_(0, inv, grads.float()) * scale
         a = self.accum[uniq] + g * g
@@ -225,8 +296,111 @@ class ShardedEmbedding:
         self.table[uniq] -= self.lr * g / (a.sqrt() + self.eps)
 
     # ------------------------------------------------------------ pull / push
+    # ------------------------------------------------------------ fixed-capacity exchange
+    def _dedup_any(self, ids: torch.Tensor):
+        """(uniq [n] padded, inv [n], count [1] int32) on the device (GPU kernel) or by
+        torch.unique on the CPU, in the capacity format either way."""
+        n = ids.numel()
+        if self.dedup is not None and n > 0:
+            uniq, inv, count, _, _ = self.dedup(ids, csr=False)
+            return uniq, inv, count
+        u, inv = torch.unique(ids, return_inverse=True)
+        uniq = torch.zeros(n, dtype=torch.int64, device=ids.device)
+        uniq[: u.numel()] = u
+        if 0 < u.numel() < n:
+            uniq[u.numel():] = u[0]
+        return uniq, inv, torch.tensor([u.numel()], dtype=torch.int32, device=ids.device)
+
+    def _check_overflow(self) -> None:
+        """Raise on an exchange-capacity overflow flagged by an earlier pull (read
+        from pinned memory once its copy has landed: no stall on the step)."""
+        if self._ovf_evt is not None and (self.device.type != "cuda" or self._ovf_evt.query()):
+            if int(self._ovf_host[0]) != 0:
+                raise RuntimeError(f"CTR exchange overflow: more than {self.cap} ids for one owner; "
+                                   f"raise KDL_CTR_A2A_SLACK (0 = no limit below max_ids)")
+            self._ovf_evt = None
+
+    def _pull_fixed(self, ids: torch.Tensor):
+        self._check_overflow()
+        W, cap, dev = self.world, self.cap, self.device
+        n = ids.numel()
+        if n > self.max_ids:
+            raise ValueError(f"pull of {n} ids > max_ids {self.max_ids}")
+        uniq, inv, count = self._dedup_any(ids)
+        if n:
+            valid = torch.arange(n, device=dev) < count.to(torch.int64)
+            dest = torch.where(valid, self._owner_rank[uniq % self.n_own], torch.full_like(uniq, W))
+            onehot = torch.zeros(n, W + 1, dtype=torch.int32, device=dev).scatter_(1, dest[:, None], 1)
+            pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None]).squeeze(1).to(torch.int64)
+            ok = valid & (pos < cap)
+            self._ovf.copy_((valid & (pos >= cap)).any().to(torch.int32).reshape(1))
+            slot = torch.where(ok, dest * cap + pos, torch.full_like(pos, W * cap))  # W * cap: dump slot
+        else:
+            slot = torch.empty(0, dtype=torch.int64, device=dev)
+            self._ovf.zero_()
+        if dev.type == "cuda":
+            self._ovf_host.copy_(self._ovf, non_blocking=True)
+            self._ovf_evt = torch.cuda.Event()
+            self._ovf_evt.record()
+        else:
+            self._ovf_host.copy_(self._ovf)
+            self._ovf_evt = True
+            self._check_overflow()
+        send = torch.full((W * cap + 1,), -1, dtype=torch.int64, device=dev)
+        if n:
+            send.scatter_(0, slot, uniq)
+        recv = torch.empty(W * cap, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv, send[: W * cap], group=self.group)  # equal splits: no size exchange
+        if self.is_owner:
+            rows = self._local_gather(torch.where(recv >= 0, recv // self.n_own, torch.zeros_like(recv)))
+        else:
+            rows = torch.zeros(W * cap, self.dim, device=dev)
+        got = torch.empty(W * cap + 1, self.dim, device=dev)
+        got[W * cap].zero_()
+        dist.all_to_all_single(got[: W * cap], rows.contiguous(), group=self.group)
+        emb = got[slot] if n else got[:0]
+        self._ctx = ("fixed", slot, recv, count)
+        return emb, inv
+
+    def _push_fixed(self, grad_unique: torch.Tensor, scale: float) -> None:
+        _, slot, recv, _ = self._ctx
+        W, cap, dev = self.world, self.cap, self.device
+        gsend = torch.zeros(W * cap + 1, self.dim, device=dev)
+        if slot.numel():
+            gsend[slot] = grad_unique.float()  # (the dump slot may take several rows: never sent)
+        grecv = torch.empty(W * cap, self.dim, device=dev)
+        dist.all_to_all_single(grecv, gsend[: W * cap], group=self.group)
+        if self.is_owner:
+            # padding slots carry id -1 and zero gradient: mapped to row 0 they are
+            # exact no-ops of Adagrad (g = 0 leaves acc and w unchanged)
+            local = torch.where(recv >= 0, recv // self.n_own, torch.zeros_like(recv))
+            self._apply_updates_dev(local, grecv, scale)
+
+    def _apply_updates_dev(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:
+        """Owner update with the duplicate-sum on the device (no size to the host):
+        DeviceDedup's CSR gives each row's contributions in position order."""
+        if self.dedup is None:
+            self._apply_updates(ids_local, grads, scale)
+            return
+        uniq, inv, count, seg, order = self.dedup(ids_local, csr=True)
+        _ext.load().segment_adagrad(grads.contiguous().float(), order, seg, uniq, self.table, self.accum,
+                                    self.lr, self.eps, scale, count)
+
+    def _sync_free(self, ids: torch.Tensor) -> bool:
+        return (self.dedup is not None and ids.numel() > 0 and self.n_own == 1 and
+                (self.world == 1 or self.group is None and not dist.is_initialized()))
+
     def pull(self, ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """ids [n] int64 (any, may repeat) -> (unique rows [U, dim], inverse [n])."""
+        """ids [n] int64 (any, may repeat) -> (unique rows [U, dim], inverse [n]).
+        On the sync-free path U is the capacity n: rows past the live count are
+        gathered from a valid id and never referenced by ``inverse``."""
+        if self._sync_free(ids):
+            uniq, inv, count, _, _ = self.dedup(ids, csr=False)
+            emb = self._local_gather(uniq)
+            self._ctx = ("dev", uniq, count)
+            return emb, inv
+        if self.max_ids is not None and self.world > 1:
+            return self._pull_fixed(ids)
         uniq, inv = torch.unique(ids, return_inverse=True)
         owner = uniq % self.n_own
         order = torch.argsort(owner, stable=True)
@@ -255,6 +429,16 @@ class ShardedEmbedding:
     def push(self, grad_unique: torch.Tensor, scale: float = 1.0) -> None:
         """grad rows aligned with the unique ids of the last pull."""
         ctx = self._ctx
+        kind = ctx[0] if isinstance(ctx[0], str) else None
+        if kind == "fixed":
+            self._push_fixed(grad_unique, scale)
+            return
+        if kind == "dev":  # one row per unique id, count on the device
+            _, uniq, count = ctx
+            order, seg = self.dedup.arange(uniq.numel())
+            _ext.load().segment_adagrad(grad_unique.contiguous().float(), order, seg, uniq, self.table, self.accum,
+                                        self.lr, self.eps, scale, count)
+            return
         uniq_sorted, order = ctx[0], ctx[1]
         g_sorted = grad_unique[order]
         if ctx[2] is None:
@@ -307,12 +491,27 @@ class CTRModel:
 
     def push_grads(self, xgrad: torch.Tensor, inv: torch.Tensor, U: int, scale: float) -> None:
         B = xgrad.shape[0]
+        ctx = self.emb._ctx
+        kind = ctx[0] if ctx is not None and isinstance(ctx[0], str) else None
+        count = ctx[2] if kind == "dev" else ctx[3] if kind == "fixed" else None
+        if kind is not None and self.emb.dedup is not None and inv.numel() > 0:
+            # CSR of the inverse on the device (positions ascending per unique id:
+            # the same summation order as the argsort path), live count on the device
+            dd = self.emb.dedup
+            n = inv.numel()
+            ws = dd._buffers(n)
+            seg = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+            order = torch.empty(n, dtype=torch.int64, device=self.device)
+            _ext.load().csr_from_inverse_only(inv, ws["sizes"], count, ws["bsum"], ws["cursor"], seg, order)
+            g_u = _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg, count)
+            self.emb.push(g_u, scale)
+            return
         order = torch.argsort(inv, stable=True)
         counts = torch.bincount(inv, minlength=U)
         seg = torch.zeros(U + 1, dtype=torch.int64, device=self.device)
         seg[1:] = torch.cumsum(counts, 0)
         if self.device.type == "cuda" and _ext.available():
-            g_u = _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg)
+            g_u = _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg, None)
         else:
             rows = xgrad[:, : self.F * self.D].reshape(B * self.F, self.D).float()
             g_u = torch.zeros(U, self.D, device=self.device).index_add_(0, inv, rows)

@@ -128,6 +128,7 @@ class HipKernels:
         # the default keeps the separate finalize kernels
         self.fuse_fin = os.environ.get("KDL_BN_FIN", "kernel") != "kernel"
         self._fin_ptrs = {}
+        self.stem_path = None  # "kdl" | "miopen" once a forward ran (reported by bench / smoke)
 
     def fin_desc(self, st, dgamma, dbeta):
         """(Re)write st's finalize descriptor when a pointer it holds changed."""
@@ -220,7 +221,16 @@ class HipKernels:
                 and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
             c0 = _nhwc_empty(x.shape[0], 64, 112, 112, x)
             self.ext.stem7x7_fwd(x, stem_weights(w), c0, st.mod.running_mean, self._fwd_acc(st))
+            self.stem_path = "kdl"
             return c0, True
+        # csrc/stem.hip is specialised to the 224 x 224 x 3 geometry the benchmark
+        # trains on; any other input runs the stem conv on MIOpen -- reported, not silent
+        if self.stem_path != "miopen":
+            import logging
+            logging.getLogger("kubedl_amd.engine").warning(
+                "stem conv on MIOpen: the kdl stem kernel serves 3x224x224 bf16 NHWC only (got %s)",
+                tuple(x.shape[1:]))
+        self.stem_path = "miopen"
         return F.conv2d(x, w, stride=2, padding=3).contiguous(memory_format=torch.channels_last), False
 
     def stem_fwd(self, c0, st, gemm_stats=False):
@@ -671,9 +681,17 @@ class ResNetEngine:
         # BN-backward apply passes of bn3 / downsample BN / bn1 fused into their
         # 1x1 data-gradient GEMMs (csrc/conv1x1.hip PRO_BWD); KDL_BN_BWD_FUSE=0: separate passes
         # (1: dgrad A prologue + write-through; 2: dgrad A prologue + weight-gradient G
-        # prologue, never materialised), for BNs of at most KDL_BN_BWD_FUSE_KMAX channels
-        self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "0"))
-        self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "4096"))
+        # prologue, never materialised), for BNs of at most KDL_BN_BWD_FUSE_KMAX channels.
+        # Per-layer A/B (profiles/r03_bn_bwd_fuse_layers.jsonl, apply + dgrad vs fused
+        # dgrad, uncontended): mode 1 wins where the dgrad has ONE output-channel tile
+        # -- bn3 / downsample BN into conv3 / downsample dgrads at K = 4C <= 512
+        # (stage 1: 390 -> 287 us, down 371 -> 258; stage 2: 192 -> 157); it loses on
+        # conv1's dgrad (N = 4C output tiles each re-transform the A tile) and at
+        # K >= 1024 (the register-staged loop vs the LDS-DMA one: 88 -> 138 us); the
+        # G prologue (mode 2) loses to reading the written-through tensor (106 -> 354 us)
+        self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "1"))
+        self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "512"))
+        self.fuse_bn1 = os.environ.get("KDL_BN_BWD_FUSE_BN1", "0") == "1"
         self.side = None
         if self.K.name == "hip" and os.environ.get("KDL_WGRAD_STREAM", "1") == "1":
             from kubedl_amd.ops.streams import side_stream
@@ -873,17 +891,19 @@ class ResNetEngine:
                 g, a, weight, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
             self._g(weight).copy_(dw)
 
-    def _fuse_mode(self, C: int) -> int:
+    def _fuse_mode(self, C: int, bn1: bool = False) -> int:
         """How the BN-backward apply of a C-channel BN reaches its 1x1 consumers:
         0 its own pass; 1 inside the data-gradient GEMM's A staging, written
         through for the weight gradient; 2 inside both GEMMs' operand staging
         (never materialised)."""
+        if bn1 and not self.fuse_bn1:
+            return 0
         return self.fuse_bwd if C <= self.fuse_kmax else 0
 
-    def _bn_bwd_operand(self, g, x, st):
+    def _bn_bwd_operand(self, g, x, st, bn1: bool = False):
         """(dgrad A, dgrad bpro, wgrad G, wgrad gbpro) for the BN-backward apply
         dc = k g + c1 x + c0 of BN ``st`` (input ``x``) per ``_fuse_mode``."""
-        mode = self._fuse_mode(x.shape[1])
+        mode = self._fuse_mode(x.shape[1], bn1)
         if mode == 0:
             dc, _ = self.K.bn_bwd_apply(g, x, st)
             return dc, None, dc, None
@@ -984,7 +1004,7 @@ class ResNetEngine:
                 dc1 = K.bn_bwd_full(da1.contiguous(memory_format=torch.channels_last), c1, st1, *self._bn_grads(st1))
             self._bn_ready(st1)
             # bn1 backward apply: its own pass, or (fused) inside conv1's dgrad below
-            op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1)
+            op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1, bn1=True)
             # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
             if blk.down_conv is not None:
                 ds = blk.down_conv.stride[0]

@@ -102,8 +102,11 @@ def run(args, launcher: str) -> int:
     kdist.barrier(info)
     sync(info)
     t0 = time.perf_counter()
+    host = 0.0  # time spent issuing the steps (no sync): = ms_per_step when host-bound
     for _ in range(args.steps):
+        th = time.perf_counter()
         trainer.step()
+        host += time.perf_counter() - th
     sync(info)
     kdist.barrier(info)
     sync(info)
@@ -141,10 +144,13 @@ def run(args, launcher: str) -> int:
                 "conv_benchmark": bool(args.conv_benchmark),
                 "allreduce": args.allreduce if n > 1 else None,
                 "launcher": launcher,
+                "stem": getattr(getattr(getattr(trainer, "engine", None), "K", None), "stem_path", None),
+                "bn_bwd_fuse": getattr(getattr(trainer, "engine", None), "fuse_bwd", None),
             },
             "steps_per_sec": round(args.steps / dt, 4),
             "rank_ready_s": round(rank_ready_s, 3),
             "comm_init_s": round(comm_init_s, 3),
+            "host_issue_ms_per_step": round(host / args.steps * 1e3, 3),
             "final_loss": round(loss, 4),
         }
         print(json.dumps(out), flush=True)
