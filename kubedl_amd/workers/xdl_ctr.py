@@ -106,8 +106,11 @@ def main(argv=None) -> int:
     workers = [r for r in range(world) if r >= n_ps]
     wgroup = dist.new_group(workers) if world > 1 else None
     is_worker = rank in workers
+    # every rank knows the per-pull id bound (batch x fields) from the job's
+    # command line: the multi-rank exchange runs at that fixed capacity, with
+    # equal all-to-all splits and no per-step size round trip to the host
     emb = ShardedEmbedding(args.fields * args.vocab, args.dim, owners, rank, world, device,
-                           group=None, lr=args.emb_lr)
+                           group=None, lr=args.emb_lr, max_ids=args.batch * args.fields)
     total = args.warmup + args.steps
     if not is_worker:  # PS: serve pull/push rounds
         for _ in range(total):
