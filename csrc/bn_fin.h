@@ -59,24 +59,30 @@ __device__ __forceinline__ void fin_stp(void* p, int bf, int i, float v) {
 }
 
 // sum the 32 replicas of (row[c], row[C + c]) with agent-scope loads (the adds
-// came from blocks on every XCD) and re-zero them
+// came from blocks on every XCD) and re-zero them.  Eight replicas per batch of
+// loads: all 64 values at once cost the host GEMM kernels ~90 spilled VGPRs
+// (this tail is inlined into their epilogues); the sum order is unchanged.
 __device__ __forceinline__ void fin_sum(float* acc, int C, int c, float& s1, float& s2) {
-  float va[kFinReplicas], vb[kFinReplicas];
-#pragma unroll
-  for (int r = 0; r < kFinReplicas; ++r) {
-    float* row = acc + static_cast<int64_t>(r) * 2 * C;
-    va[r] = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    vb[r] = __hip_atomic_load(row + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  constexpr int kB = 8;
   s1 = 0.f;
   s2 = 0.f;
+#pragma unroll 1
+  for (int r0 = 0; r0 < kFinReplicas; r0 += kB) {
+    float va[kB], vb[kB];
 #pragma unroll
-  for (int r = 0; r < kFinReplicas; ++r) {
-    s1 += va[r];
-    s2 += vb[r];
-    float* row = acc + static_cast<int64_t>(r) * 2 * C;
-    row[c] = 0.f;
-    row[C + c] = 0.f;
+    for (int r = 0; r < kB; ++r) {
+      float* row = acc + static_cast<int64_t>(r0 + r) * 2 * C;
+      va[r] = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vb[r] = __hip_atomic_load(row + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int r = 0; r < kB; ++r) {
+      s1 += va[r];
+      s2 += vb[r];
+      float* row = acc + static_cast<int64_t>(r0 + r) * 2 * C;
+      row[c] = 0.f;
+      row[C + c] = 0.f;
+    }
   }
 }
 

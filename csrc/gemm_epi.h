@@ -74,6 +74,10 @@ struct GemmParams {
   // dx pixels (2i + py, 2j + px).  mc = Nb Hin Win rows per class, padded to
   // mc_pad (a multiple of BM, set by the launcher); M = 4 mc_pad.
   int mc, mc_pad;
+  // Ticketed tile schedule (tile_tickets): per output-column tile c, tk[2c] hands
+  // out M tiles in arrival order and tk[2c + 1] counts the blocks that drew
+  // past the end (the last one resets both); null = the static per-block list
+  unsigned* tk;
   // BN finalize folded into this GEMM (csrc/bn_fin.h): the workspace of the BN
   // whose sums the epilogue produces (second one: RESBITS' downsample BN), and
   // that BN's element count; null = the host launches the finalize
@@ -108,6 +112,11 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
 int igemm_pick(int M, int N, int K);
 bool g_forced_cfg_unset();  // no KDL_IGEMM_CFG / set_igemm_cfg override in force
 hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t s);
+// n zeroed ticket counters for one launch, from a per-device ring (self-resetting:
+// every kernel that draws from them leaves them zero); null while a stream capture
+// is under way on a device whose ring does not exist yet
+unsigned* tile_tickets(int n, hipStream_t s);
+bool tickets_enabled();
 // csrc/halo3x3.hip: 3x3 stride-1 conv with an LDS-resident input halo (Cin 64 @ 56x56);
 // hipErrorInvalidValue when the geometry is not one it serves
 hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s);
@@ -176,7 +185,8 @@ struct Epilogue {
   static constexpr int CPR = BN / 8;           // 16-B chunks per output row
   static constexpr int RPP = NT / CPR;         // rows per epilogue pass
   static constexpr int NP = BM / RPP;          // rows per thread per tile
-  static constexpr int PG = (EPI == EPI_RESBITS) ? (NP > 4 ? 4 : NP) : (NP > 8 ? 8 : NP);  // prefetch group
+  // prefetch group (4 rows where 8 spill: RESBITS, and MASKX beside the 256x256 tile's 128 accumulators)
+  static constexpr int PG = (EPI == EPI_RESBITS || (EPI == EPI_MASKX && BM * BN >= 256 * 256)) ? (NP > 4 ? 4 : NP) : (NP > 8 ? 8 : NP);
   static constexpr bool LX = EPI == EPI_MASKX || EPI == EPI_RESBITS;
   static constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES;
   static constexpr bool REDUCE = EPI == EPI_STATS || EPI == EPI_MASKX || EPI == EPI_RESBITS;

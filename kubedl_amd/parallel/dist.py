@@ -116,10 +116,12 @@ def first_collective(info: DistInfo, stream=None) -> float:
     a process group.
 
     ``stream``: issue it from the stream the job's collectives run on (the
-    trainer's compute stream).  Bootstrapping the communicator from the NULL
-    stream instead left every later step 38 % slower at world 1 on MI355X
-    (19.5 -> 26.9 ms, same box, A/B against the lazy in-step bootstrap), the
-    same null-stream interaction ops/streams.py documents."""
+    trainer's compute stream).  Call it only after the trainer's streams have
+    run a kernel (workers/resnet50.py ResNetTrainer.touch_streams): the
+    communicator's bootstrap creates RCCL's own streams, and streams first used
+    after that shared hardware queues with them -- the weight-gradient side
+    stream lost its overlap, 19.4 -> 22.0 ms per ResNet-50 step at world 1
+    (26.9 ms bootstrapped from the null stream); profiles/r03_stream_touch_ab.txt."""
     import contextlib
     import time
     if not dist.is_initialized():

@@ -85,8 +85,11 @@ def run(args, launcher: str) -> int:
     t_model = time.time()
     # the first collective builds the RCCL communicator (lazy: init_process_group
     # returns after the TCP-store rendezvous, dist.py) -- timed on its own so the
-    # bootstrap cost is reported instead of hiding in the warm-up steps
-    comm_init_s = kdist.first_collective(info, getattr(trainer, "stream", None))
+    # bootstrap cost is reported instead of hiding in the warm-up steps; after
+    # the trainer has touched its streams (ResNetTrainer.touch_streams)
+    comm_init_s = 0.0
+    if os.environ.get("KDL_COMM_PROBE", "1") != "0":
+        comm_init_s = kdist.first_collective(info, getattr(trainer, "stream", None))
     kdist.barrier(info)
     # process start -> model resident on every rank
     rank_ready_s = kdist.all_reduce_max(time.time() - T_PROC_START, info)

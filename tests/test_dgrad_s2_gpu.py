@@ -87,3 +87,32 @@ def test_s2_dgrad_weights_match_engine_table():
     for blk in eng.blocks:
         if blk.conv2.stride[0] == 2:
             torch.testing.assert_close(eng._ball(blk.conv2), s2_dgrad_weights(blk.conv2.weight), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("C,Hd", [(128, 28), (256, 14), (512, 7)])
+def test_s2_dgrad_maskx_full_batch_writes_every_pixel(C, Hd):
+    """ResNet-50 b256 shapes with the output pre-filled with NaN: every pixel is
+    written (a zero dy gives exact zeros), and a random dy matches the reference."""
+    ext = _ext()
+    nb = 256
+    torch.manual_seed(24)
+    w = _nhwc((torch.randn(C, C, 3, 3, device="cuda") / (3 * C ** 0.5)).bfloat16())
+    xbn = _nhwc(torch.randn(nb, C, 2 * Hd, 2 * Hd, device="cuda").bfloat16())
+    coef = torch.cat([torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.5]).float()
+    mean = torch.randn(C, device="cuda") * 0.1
+    for zero in (True, False):
+        dy = _nhwc(torch.randn(nb, C, Hd, Hd, device="cuda").bfloat16())
+        if zero:
+            dy.zero_()
+        acc = torch.zeros(REP * 2 * C, device="cuda")
+        out = _nhwc(torch.full((nb, C, 2 * Hd, 2 * Hd), float("nan"), device="cuda", dtype=torch.bfloat16))
+        ext.conv3x3_s2_dgrad(dy, s2_dgrad_weights(w), out, nb, Hd, Hd, C, C, 2, acc, xbn, mean, coef)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out.float()).all(), "dx pixels left unwritten"
+        if zero:
+            assert float(out.float().abs().max()) == 0.0
+            continue
+        dx = torch.nn.grad.conv2d_input(xbn.shape, w.float(), dy.float(), stride=2, padding=1)
+        mask = (xbn.float() * coef[:C].view(1, C, 1, 1) + coef[C:].view(1, C, 1, 1)) > 0
+        ref = torch.where(mask, dx.bfloat16().float(), torch.zeros_like(dx))
+        torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
