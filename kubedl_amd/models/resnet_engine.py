@@ -121,12 +121,13 @@ class HipKernels:
         self.dev = dev
         self._dw32 = {}
         self.stem_native = os.environ.get("KDL_STEM", "kdl") != "miopen"  # KDL_STEM=miopen: vendor stem conv
-        # KDL_BN_FIN=gemm: BN finalize folded into the producing conv GEMM's last
-        # arriving blocks (csrc/bn_fin.h).  Measured neutral (12,612 / 12,617 vs
-        # 12,629 / 12,598 img/s, profiles/r02_bn_fin_ab.txt): the last arriver's
-        # acquire + replica reads cost what the ~106 separate launches did, so
-        # the default keeps the separate finalize kernels
-        self.fuse_fin = os.environ.get("KDL_BN_FIN", "kernel") != "kernel"
+        # BN finalize folded into the producing conv GEMM's last arriving blocks
+        # (csrc/bn_fin.h; KDL_BN_FIN=kernel: separate finalize launches).  Round 2
+        # measured it neutral while its inlined tail made every MASKX/STATS GEMM
+        # spill ~90 VGPRs; with the tail's replica sum chunked (no spills) it is
+        # 19.33 / 19.37 vs 19.41 / 19.47 ms per step (profiles/r03_knob_sweep.txt)
+        # and ~106 fewer launches
+        self.fuse_fin = os.environ.get("KDL_BN_FIN", "gemm") != "kernel"
         self._fin_ptrs = {}
         self.stem_path = None  # "kdl" | "miopen" once a forward ran (reported by bench / smoke)
 
