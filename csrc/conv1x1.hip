@@ -67,14 +67,23 @@ constexpr int BK = 64;
 // tiles stay within 80 KiB of LDS (two blocks per CU) up to K = 512, 64-wide
 // tiles up to K = 2048 (the widest ResNet-50 data-gradient K)
 __host__ __device__ constexpr int bwd_kmax(int bn) { return bn >= 128 ? 512 : 2048; }
+// widest second K segment (the BN2 width of a recompute block's conv3: C <= 512)
+constexpr int kSegKmax = 512;
 
 // PRO: 0 none, PRO_FWD = BN+ReLU of the previous layer, PRO_BWD = BN-backward
-// apply (GemmParams::bx / bcoef; dense rows only)
-enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2 };
+// apply (GemmParams::bx / bcoef; dense rows only), PRO_SEG / PRO_RECOMP = a
+// second K segment (GemmParams::A2 / B2 / K2) staged through the BN+ReLU
+// prologue, summed into the output (SEG) or into a second accumulator whose
+// bf16 tile is the epilogue's BN input x (RECOMP: a conv output recomputed
+// instead of read back -- csrc/gemm_epi.h XL)
+enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_SEG = 3, PRO_RECOMP = 4 };
 
 template <int BM, int BN, int MINB, int PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
   static_assert(PRO != PRO_BWD || GATHER == G_DENSE, "the backward-apply prologue reads dense rows");
+  constexpr bool SEG = PRO == PRO_SEG || PRO == PRO_RECOMP;
+  static_assert(!SEG || GATHER == G_DENSE, "two-segment K reads dense rows");
+  static_assert(PRO != PRO_RECOMP || EPI == EPI_RESBITS, "the recomputed tile feeds the RESBITS epilogue");
   // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
   // [BM][BN + 8] output tile and finally as the reduction scratch.
   constexpr int LDK = KBK + 8;  // padded LDS row (bf16): 16-B slot stride odd -> conflict-free fragment reads
@@ -84,7 +93,13 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // once per block behind the operand buffers (one __shared__ array: a second
   // one can make hipcc drain the pipeline, cdna_hip_programming.md §5 item 4a)
   constexpr int KT = PRO == PRO_BWD ? bwd_kmax(BN) : 0;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kBuf + 6 * KT];
+  // SEG / RECOMP: segment 2's BN scale | shift staged once per block (read in
+  // swrite: no coefficient registers live across the K loop), K2 <= kSegKmax
+  constexpr int KS = (PRO == PRO_SEG || PRO == PRO_RECOMP) ? 2 * kSegKmax : 0;
+  // RECOMP: a third region holds the recomputed x tile [BM][BN + 8] beside the
+  // two stage buffers, so the next tile's first K-step still overlaps the epilogue
+  constexpr int XT = PRO == PRO_RECOMP ? BM * (BN + 8) : 0;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kBuf + 6 * KT + XT + 2 * KS];
   float* coef_lds = reinterpret_cast<float*>(lds + 2 * kBuf);
   (void)coef_lds;
   constexpr int WN = (BN >= 64 && BM >= 64) ? 2 : 1;  // waves along N
@@ -100,6 +115,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // buffer, so the next tile's first K-step stays in registers through the
   // epilogue (which then owns both buffers) and is staged after it.
   constexpr bool SPLIT_C = BM * LDC > kBuf;
+  static_assert(!SPLIT_C || PRO != PRO_RECOMP, "RECOMP: 64-deep K-steps");
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int nblk = gridDim.x;
@@ -109,7 +125,9 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   const int gm = q / tiles_n;
   const int n0 = tile_n * BN;
   const int K = p.K, M = p.M, N = p.N;
-  const int nk = K / KBK;
+  const int nk1 = K / KBK;                           // segment-1 K-steps
+  const int nk = SEG ? nk1 + p.K2 / KBK : nk1;
+  const int ldb = SEG ? p.ldb : K;
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
 
   // staging coordinates (fixed per thread)
@@ -138,9 +156,21 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   uint32_t a_valid = 0;
   const bool wthru = PRO == PRO_BWD && p.aout != nullptr && tile_n == 0;
   (void)rx; (void)st_k0; (void)a_valid; (void)wthru;
+  // SEG / RECOMP: the chunk's row (segment 2 has its own row stride) and
+  // whether the K-step held in ra is a segment-2 one (prologue applies)
+  int a_m[SEG ? A_CH : 1];
+  bool st_seg2 = false;
+  (void)a_m; (void)st_seg2;
   if constexpr (PRO == PRO_BWD) {
     for (int i = t; i < 3 * K / 4; i += kThreads)
       reinterpret_cast<float4*>(coef_lds)[i] = reinterpret_cast<const float4*>(p.bcoef)[i];
+    __syncthreads();
+  }
+  float* seg_coef = reinterpret_cast<float*>(lds + 2 * kBuf + 6 * KT + XT);  // [2 K2] scale | shift
+  (void)seg_coef;
+  if constexpr (KS > 0) {
+    for (int i = t; i < 2 * p.K2 / 4; i += kThreads)
+      reinterpret_cast<float4*>(seg_coef)[i] = reinterpret_cast<const float4*>(p.pro_coef)[i];
     __syncthreads();
   }
 
@@ -164,10 +194,35 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           a_iw[i] = ow * p.stride - 1;
         }
       }
-      a_off[i] = src * K;
+      if constexpr (SEG) a_m[i] = m;
+      else a_off[i] = src * K;
     }
   };
   auto gload = [&](int kt) {
+    if constexpr (SEG) {  // dense rows; segment 2 through the BN+ReLU prologue
+      const bool s2 = kt >= nk1;
+      const int k0 = (s2 ? kt - nk1 : kt) * KBK;
+      if (s2) {
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) ra[i] = ld16(p.A2 + static_cast<int64_t>(a_m[i]) * p.K2 + k0 + a_kc[i]);
+#pragma unroll
+        for (int i = 0; i < B_CH; ++i) {
+          const int c = t + i * kThreads;
+          rb[i] = ld16(p.B2 + static_cast<int64_t>(n0 + c / CPRK) * p.ldb2 + k0 + (c % CPRK) * 8);
+        }
+        st_k0 = k0;
+      } else {
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) ra[i] = ld16(p.A + static_cast<int64_t>(a_m[i]) * K + k0 + a_kc[i]);
+#pragma unroll
+        for (int i = 0; i < B_CH; ++i) {
+          const int c = t + i * kThreads;
+          rb[i] = ld16(p.B + static_cast<int64_t>(n0 + c / CPRK) * ldb + k0 + (c % CPRK) * 8);
+        }
+      }
+      st_seg2 = s2;
+      return;
+    }
     const int k0 = kt * KBK;
     int kc0 = k0;  // channel offset of this K-step within a tap
     if constexpr (GATHER == G_CONV3) {
@@ -227,10 +282,24 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         bc0[j] = z.x; bc0[j + 1] = z.y; bc0[j + 2] = z.z; bc0[j + 3] = z.w;
       }
     }
+    bool fwd_pro = PRO == PRO_FWD;
+    if constexpr (SEG) {
+      fwd_pro = st_seg2;
+      if (fwd_pro) {  // this thread's 8 channels of the staged segment-2 K-step, from LDS
+        const int c = st_k0 + a_kc[0];
+#pragma unroll
+        for (int j = 0; j < 8; j += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(seg_coef + c + j);
+          const float4 b = *reinterpret_cast<const float4*>(seg_coef + p.K2 + c + j);
+          psc[j] = a.x; psc[j + 1] = a.y; psc[j + 2] = a.z; psc[j + 3] = a.w;
+          psf[j] = b.x; psf[j + 1] = b.y; psf[j + 2] = b.z; psf[j + 3] = b.w;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint4 v = ra[i];
-      if constexpr (PRO == PRO_FWD) {
+      if (fwd_pro) {
         float f[8];
         unpack8(v, f);
 #pragma unroll
@@ -261,7 +330,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   };
 
-  Epilogue<BM, BN, kThreads, EPI> epi;
+  Epilogue<BM, BN, kThreads, EPI, G_DENSE, PRO == PRO_RECOMP> epi;
   epi.init(t, n0);
 
   int tm = gm;
@@ -279,16 +348,9 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool more_k = kt + 1 < nk;
-      const bool more = more_k || tm + GM < tiles_m;
-      if (more_k) {
-        gload(kt + 1);
-      } else if (more) {
-        setup_rows(tm + GM);
-        gload(0);
-      }
-      const bf16_t* As = lds + cur * kBuf;
+    // one staged K-step's fragments + MFMAs into ``a`` (static indices only:
+    // the RECOMP accumulator choice is a branch around two inlined copies)
+    auto mma = [&](const bf16_t* As, f32x16_t (&a)[TN][TM]) {
       const bf16_t* Bs = As + BM * LDK;
 #pragma unroll
       for (int s = 0; s < KBK / 16; ++s) {
@@ -303,7 +365,30 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         for (int i = 0; i < TN; ++i)
 #pragma unroll
           for (int j = 0; j < TM; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+            a[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], a[i][j], 0, 0, 0);
+      }
+    };
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more_k = kt + 1 < nk;
+      const bool more = more_k || tm + GM < tiles_m;
+      if (more_k) {
+        gload(kt + 1);
+      } else if (more) {
+        setup_rows(tm + GM);
+        gload(0);
+      }
+      const bf16_t* As = lds + cur * kBuf;
+      mma(As, acc);
+      if constexpr (PRO == PRO_RECOMP) {
+        // segment 1 done: its tile goes to the third LDS region and the same
+        // accumulators recompute the x tile (one accumulator set: 256 VGPRs)
+        if (kt == nk1 - 1) {
+          acc_to_lds<TN, TM>(acc, lds + 2 * kBuf, LDC, wm0, wn0, lane);
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
+        }
       }
       if (more_k || (more && !SPLIT_C)) swrite(cur ^ 1);
       __syncthreads();
@@ -317,8 +402,13 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     // tile's first K-step)
     bf16_t* Cs = SPLIT_C ? lds : lds + (cur ^ 1) * kBuf;
     acc_to_lds<TN, TM>(acc, Cs, LDC, wm0, wn0, lane);
+    bf16_t* Xs = nullptr;
+    if constexpr (PRO == PRO_RECOMP) {  // acc holds the recomputed conv output (x of the RESBITS sums)
+      Xs = Cs;
+      Cs = lds + 2 * kBuf;  // (KT == 0: no coefficient table in between)
+    }
     __syncthreads();
-    epi.rows(p, Cs, tm);
+    epi.rows(p, Cs, tm, Xs);
     __syncthreads();  // Cs (buffer cur^1) is restaged by the next tile's second K-step
     if constexpr (SPLIT_C) {  // stage the next tile's first K-step now that the epilogue is done
       if (tm + GM < tiles_m) swrite(0);
@@ -582,7 +672,13 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
 // backward-apply prologue feeds only the dense dgrad epilogues
 template <int BM, int BN, int MINB, int PRO, int GATHER, int KBK>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
-  if constexpr (PRO == PRO_BWD) {
+  if constexpr (PRO == PRO_SEG) {  // the BN-folded conv3 data gradient
+    if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
+    return hipErrorInvalidValue;
+  } else if constexpr (PRO == PRO_RECOMP) {  // conv1 dgrad + residual, recomputing the previous conv3
+    if (epi == EPI_RESBITS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
+    return hipErrorInvalidValue;
+  } else if constexpr (PRO == PRO_BWD) {
     switch (epi) {
       case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
       case EPI_MASKX: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
@@ -594,6 +690,9 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     switch (epi) {
       case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
       case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
+    }
+    if constexpr (PRO == PRO_FWD && GATHER == G_DENSE && KBK == BK && BM == 128 && MINB == 2) {  // recomputed conv3 + closing BN/residual/ReLU
+      if (epi == EPI_APPLY) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_APPLY, KBK>(p, s);
     }
     if constexpr (PRO == PRO_NONE && GATHER == G_DENSE) {
       switch (epi) {
@@ -611,9 +710,15 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
 
 template <int BM, int BN, int MINB, int KBK = BK>
 hipError_t dispatch_pg(const GemmParams& p, int epi, int pro, int gather, hipStream_t s) {
-  if (pro == PRO_BWD) {
-    if constexpr (BM == 128 && MINB == 2 && KBK == BK)  // the two configs conv1x1_gemm routes it to
-      return gather == G_DENSE ? dispatch_epi<BM, BN, MINB, PRO_BWD, G_DENSE, KBK>(p, epi, s) : hipErrorInvalidValue;
+  if (pro == PRO_BWD || pro == PRO_SEG || pro == PRO_RECOMP) {
+    if constexpr (BM == 128 && MINB == 2 && KBK == BK) {  // the two configs conv1x1_gemm routes them to
+      if (gather != G_DENSE) return hipErrorInvalidValue;
+      if (pro == PRO_BWD) return dispatch_epi<BM, BN, MINB, PRO_BWD, G_DENSE, KBK>(p, epi, s);
+      if constexpr (BN == 64) {  // (the 128 x 64 tiles conv1x1_gemm routes them to)
+        if (pro == PRO_SEG) return dispatch_epi<BM, BN, MINB, PRO_SEG, G_DENSE, KBK>(p, epi, s);
+        return dispatch_epi<BM, BN, MINB, PRO_RECOMP, G_DENSE, KBK>(p, epi, s);
+      }
+    }
     return hipErrorInvalidValue;
   }
   if (gather == G_CONV3)
@@ -671,10 +776,24 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.ebits = a.ebits; p.ex2 = static_cast<const bf16_t*>(a.ex2); p.emean2 = a.emean2; p.acc2 = a.acc2;
   p.fin_ws = a.fin_ws; p.fin_ws2 = a.fin_ws2; p.fin_M = a.fin_M;
   p.bx = static_cast<const bf16_t*>(a.bx); p.bcoef = a.bcoef; p.aout = static_cast<bf16_t*>(a.aout);
+  p.A2 = static_cast<const bf16_t*>(a.A2); p.B2 = static_cast<const bf16_t*>(a.B2);
+  p.K2 = a.K2; p.ldb = a.ldb > 0 ? a.ldb : a.K; p.ldb2 = a.ldb2;
+  p.ebias = a.ebias; p.obits = a.obits;
   const bool bpro = a.bx != nullptr;
-  if (bpro && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS))
+  if (bpro && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS || a.seg))
     return hipErrorInvalidValue;
-  const int pro = bpro ? PRO_BWD : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
+  if (a.seg) {  // two-segment K: dense rows, segment 2 through the BN+ReLU prologue
+    if ((a.seg != 1 && a.seg != 2) || !a.A2 || !a.B2 || !a.pro_coef || a.K2 <= 0 || a.K2 % BK || a.K2 > kSegKmax ||
+        a.stride > 1 ||
+        a.ksize == 3 || p.ldb < a.K || a.ldb2 < a.K2 || (a.seg == 1 && a.epi != EPI_MASKX) ||
+        (a.seg == 2 && a.epi != EPI_RESBITS))
+      return hipErrorInvalidValue;
+  }
+  if (a.epi == EPI_APPLY && (!a.pro_coef || !a.obits || !a.ecoef || !a.eres || a.stride > 1 || a.ksize == 3 ||
+                             p.res_stride != 1 || a.N % 128))
+    return hipErrorInvalidValue;
+  const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP : bpro ? PRO_BWD
+                : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
   int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
   p.Cin = a.K;
   if (a.ksize == 3) {
@@ -711,6 +830,10 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
     const hipError_t e = igemm(p, epi, gather, cfg, s);
     if (e != hipErrorInvalidValue) return e;
   }
+  // 128 x 64 tiles: at 128 x 128 the second accumulator (RECOMP) or the segment
+  // bookkeeping + MASKX bias (SEG) spill (752 / 76 B of scratch per lane)
+  if (pro == PRO_SEG || pro == PRO_RECOMP) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
+  if (epi == EPI_APPLY) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
   if (pro == PRO_BWD) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
     if (p.N % 128 == 0 && p.K <= bwd_kmax(128)) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
     if (p.K <= bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
@@ -863,9 +986,11 @@ namespace {
 // big: the workspace holds wgrad_splits(M, N, K, true) slabs (3x3 256-tile configs)
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
-                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr) {
+                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr,
+                      bool grelu = false) {
   if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
   const bool bwd = gx != nullptr;
+  if (grelu && (bwd || !gcoef || !pro_coef || mode != G_DENSE || gemm_core_mode() == 0)) return hipErrorInvalidValue;
   // the G prologue exists on the LDS-DMA kernel only
   if (bwd && (gemm_core_mode() == 0 || !gcoef || mode == G_CONV3 || (pro_coef && mode != G_DENSE)))
     return hipErrorInvalidValue;
@@ -883,7 +1008,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
   if (gemm_core_mode() != 0) {  // LDS-DMA pipeline (csrc/wgrad_dma.hip) unless forced off
     WgParams wp{};
     wp.G = g; wp.A = x; wp.pro = pro_coef; wp.dw32 = dw32;
-    wp.gx = static_cast<const bf16_t*>(gx); wp.gcoef = gcoef;
+    wp.gx = static_cast<const bf16_t*>(gx); wp.gcoef = gcoef; wp.grelu = grelu ? 1 : 0;
     wp.M = M; wp.N = N; wp.K = K; wp.Hout = Hout; wp.Wout = Wout; wp.Hin = Hin; wp.Win = Win;
     wp.stride = stride; wp.cin = cin; wp.rps = rps; wp.tiles_k = tiles_k; wp.mode = mode;
     wp.a_rows = mode == G_DENSE ? M : static_cast<int64_t>(M / (Hout * Wout)) * Hin * Win;
@@ -895,7 +1020,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     if (e != hipSuccess && e != hipErrorInvalidValue) return e;
     done = e == hipSuccess;
   }
-  if (!done && bwd) return hipErrorInvalidValue;
+  if (!done && (bwd || grelu)) return hipErrorInvalidValue;
   if (!done) {
     if (tn > 128 || tk > 128) {  // the register-staged kernel has no 256 tiles: same splits, 128 tiles
       tn = tk = 128;
@@ -914,9 +1039,9 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
 
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
-                         const void* gx, const float* gcoef) {
+                         const void* gx, const float* gcoef, bool grelu) {
   return wgrad_impl(G, A, pro_coef, dw32, dW, scale, M, N, K, Hout, Wout, Hin, Win, stride,
-                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef);
+                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef, grelu);
 }
 
 int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {

@@ -16,8 +16,15 @@
 //            the previous block's packed ReLU bits, + bn3 (and downsample BN)
 //            backward sums
 //   RES      g = dgrad + d(identity), no mask (network stem)
+//   APPLY    out = relu(y * scale + shift + residual) with the packed 1-bit
+//            ReLU mask (the bottleneck's closing BN + residual + ReLU, applied
+//            to a recomputed conv3 whose output is never stored: the same
+//            fmaf / add / compare sequence as bn_act.hip bn_fwd_apply_kernel)
 // and after its last tile folds the per-thread sums in LDS and adds them to
 // the BN workspace replica of the block (one atomic per channel per block).
+// STATS with C == null stores nothing (the statistics pass of a recomputed conv).
+// XL: the BN input x of MASKX / RESBITS is a second LDS tile (the conv output
+// recomputed by the same kernel, csrc/conv1x1.hip PRO_RECOMP), not a global load.
 #pragma once
 
 #include "bn_fin.h"
@@ -33,7 +40,7 @@ typedef __attribute__((ext_vector_type(2))) float f2_t;
 
 constexpr int kRep = 32;  // replica count of the BN workspace (== bn_act.hip kReplicas)
 
-enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4, EPI_APPLY = 5 };
 // A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s) |
 // data gradient of a stride-2 3x3 pad-1 conv as four sub-pixel class GEMMs (csrc/igemm.hip)
 enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2, G_DGRAD2 = 3 };
@@ -84,6 +91,16 @@ struct GemmParams {
   float* fin_ws;
   float* fin_ws2;
   float fin_M;
+  // Two-segment K (csrc/conv1x1.hip PRO_SEG / PRO_RECOMP, dense rows): the K-steps
+  // past K read segment 2 -- A2 [M, K2] through the BN+ReLU prologue pro_coef
+  // ([2 K2] scale | shift) against B2 [N, ldb2]; segment 1 is A [M, K] against
+  // B [N, ldb].  PRO_SEG sums both into the output, PRO_RECOMP keeps segment 2
+  // in a second accumulator (the epilogue's XL tile).
+  const bf16_t* A2;
+  const bf16_t* B2;
+  int K2, ldb, ldb2;
+  const float* ebias;  // MASKX: per-output-channel bias added before the mask (null: none)
+  uint8_t* obits;      // APPLY: packed ReLU mask [M, N/8] (out)
 };
 
 // csrc/wgrad_dma.hip: weight gradient on the LDS-DMA pipeline into fp32
@@ -95,7 +112,8 @@ struct WgParams {
   // optional BN-backward-apply prologue of G: G' = k[n] G + c1[n] gx + c0[n]
   // (GemmParams::bx / bcoef semantics, per output channel n)
   const bf16_t* gx;       // [M][N]
-  const float* gcoef;     // [3N]
+  const float* gcoef;     // [3N] (grelu: [2N] scale | shift of G' = relu(G scale + shift))
+  int grelu;              // G is a BN+ReLU output (csrc/wgrad_dma.hip GRELU), gx unused
   float* dw32;
   int M, N, K;            // K = 9 * cin for 3x3
   int Hout, Wout, Hin, Win, stride, cin;
@@ -179,16 +197,23 @@ __device__ __forceinline__ void acc_to_lds(const f32x16_t (&acc)[TN][TM], bf16_t
       }
 }
 
-template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE>
+template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE, bool XL = false>
 struct Epilogue {
   static constexpr int LDC = BN + 8;
   static constexpr int CPR = BN / 8;           // 16-B chunks per output row
   static constexpr int RPP = NT / CPR;         // rows per epilogue pass
   static constexpr int NP = BM / RPP;          // rows per thread per tile
   // prefetch group (4 rows where 8 spill: RESBITS, and MASKX beside the 256x256 tile's 128 accumulators)
-  static constexpr int PG = (EPI == EPI_RESBITS || (EPI == EPI_MASKX && BM * BN >= 256 * 256)) ? (NP > 4 ? 4 : NP) : (NP > 8 ? 8 : NP);
-  static constexpr bool LX = EPI == EPI_MASKX || EPI == EPI_RESBITS;
-  static constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES;
+  // (2 beside the recompute variant's second accumulator)
+  static constexpr int PG = XL ? (NP > 2 ? 2 : NP)
+                          : (EPI == EPI_RESBITS || EPI == EPI_APPLY || (EPI == EPI_MASKX && BM * BN >= 256 * 256))
+                              ? (NP > 4 ? 4 : NP) : (NP > 8 ? 8 : NP);
+  static_assert(!XL || EPI == EPI_MASKX || EPI == EPI_RESBITS, "an LDS x tile feeds MASKX / RESBITS");
+  static constexpr bool LX = (EPI == EPI_MASKX || EPI == EPI_RESBITS) && !XL;  // x from global memory
+  static constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES || EPI == EPI_APPLY;
+  // RESBITS' optional second BN input (downsample branch); the recompute
+  // variant (XL) serves blocks without one, and its registers are scarce
+  static constexpr bool X2 = EPI == EPI_RESBITS && !XL;
   static constexpr bool REDUCE = EPI == EPI_STATS || EPI == EPI_MASKX || EPI == EPI_RESBITS;
   // LDS scratch of finish(): 3 sums x NT threads x 8 channels
   static constexpr int kScratchBytes = REDUCE ? 3 * NT * 8 * 4 : 0;
@@ -234,7 +259,7 @@ struct Epilogue {
       if constexpr (LX) pxv[i] = ok ? ld16(p.ex + go) : make_uint4(0, 0, 0, 0);
       if constexpr (EPI == EPI_RESBITS) {
         pbv[i] = ok ? p.ebits[static_cast<int64_t>(m) * (p.N / 8) + (ch0 >> 3)] : 0u;
-        px2[i] = (ok && p.ex2) ? ld16(p.ex2 + go) : make_uint4(0, 0, 0, 0);
+        if constexpr (X2) px2[i] = (ok && p.ex2) ? ld16(p.ex2 + go) : make_uint4(0, 0, 0, 0);
       }
       if constexpr (LR) {
         const bf16_t* rp = nullptr;
@@ -285,6 +310,13 @@ struct Epilogue {
         em[q] = ld2(p.emean, ch0 + 2 * q);
         ea[q] = ld2(p.ecoef, ch0 + 2 * q);
         eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
+        if (p.ebias) em2[q] = ld2(p.ebias, ch0 + 2 * q);  // (em2 is free in MASKX)
+      }
+    } else if constexpr (EPI == EPI_APPLY) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ea[q] = ld2(p.ecoef, ch0 + 2 * q);
+        eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
       }
     } else if constexpr (EPI == EPI_RESBITS) {
 #pragma unroll
@@ -295,8 +327,10 @@ struct Epilogue {
     }
   }
 
-  // the tile's rows, from Cs[BM][LDC] (after a barrier that follows acc_to_lds)
-  __device__ __forceinline__ void rows(const GemmParams& p, const bf16_t* Cs, int tm) {
+  // the tile's rows, from Cs[BM][LDC] (after a barrier that follows acc_to_lds;
+  // XL: the BN input x from Xs[BM][LDC] likewise)
+  __device__ __forceinline__ void rows(const GemmParams& p, const bf16_t* Cs, int tm, const bf16_t* Xs = nullptr) {
+    (void)Xs;
     const int N = p.N;
 #pragma unroll
     for (int g0 = 0; g0 < NP; g0 += PG) {
@@ -316,6 +350,10 @@ struct Epilogue {
         if (m < 0) continue;
         const uint4 raw = *reinterpret_cast<const uint4*>(&Cs[row * LDC + ec * 8]);
         const int64_t go = static_cast<int64_t>(m) * N + ch0;
+        uint4 xin = make_uint4(0, 0, 0, 0);  // MASKX / RESBITS: the BN input x of this row chunk
+        (void)xin;
+        if constexpr (XL) xin = *reinterpret_cast<const uint4*>(&Xs[row * LDC + ec * 8]);
+        else if constexpr (LX) xin = cxv[i];
         uint4 out = raw;  // PLAIN / STATS store the tile as it is
         if constexpr (EPI != EPI_PLAIN) {
           f2_t v[4];
@@ -330,7 +368,11 @@ struct Epilogue {
             }
           } else if constexpr (EPI == EPI_MASKX) {
             f2_t x[4];
-            unpack4x2(cxv[i], x);
+            unpack4x2(xin, x);
+            if (p.ebias) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] += em2[q];
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const f2_t z = pfma(x[q], ea[q], eb[q]);
@@ -340,6 +382,19 @@ struct Epilogue {
               o[q] = pack2(g);
             }
             out = make_uint4(o[0], o[1], o[2], o[3]);
+          } else if constexpr (EPI == EPI_APPLY) {  // relu(y * scale + shift + residual) + mask bits
+            f2_t r[4];
+            unpack4x2(crv[i], r);
+            uint32_t bits = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f2_t z = pfma(v[q], ea[q], eb[q]) + r[q];
+              bits |= (z.x > 0.f ? 1u : 0u) << (2 * q);
+              bits |= (z.y > 0.f ? 1u : 0u) << (2 * q + 1);
+              o[q] = pack2(f2_t{z.x > 0.f ? z.x : 0.f, z.y > 0.f ? z.y : 0.f});
+            }
+            out = make_uint4(o[0], o[1], o[2], o[3]);
+            p.obits[static_cast<int64_t>(m) * (N / 8) + (ch0 >> 3)] = static_cast<uint8_t>(bits);
           } else if constexpr (LR) {  // RESBITS / RES: add d(identity), rounded to bf16
             if (crok[i]) {
               f2_t r[4];
@@ -352,7 +407,7 @@ struct Epilogue {
               unpack4x2(out, v);
               const uint32_t bits = cbv[i];
               f2_t x[4];
-              unpack4x2(cxv[i], x);
+              unpack4x2(xin, x);
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
                 const f2_t g = f2_t{(bits >> (2 * q)) & 1u ? v[q].x : 0.f, (bits >> (2 * q + 1)) & 1u ? v[q].y : 0.f};
@@ -361,7 +416,7 @@ struct Epilogue {
                 s2[q] = pfma(g, x[q] - em[q], s2[q]);
                 o[q] = pack2(g);
               }
-              if (p.ex2) {
+              if (X2 && p.ex2) {
                 f2_t x2[4];
                 unpack4x2(cx2[i], x2);
 #pragma unroll
@@ -371,7 +426,7 @@ struct Epilogue {
             }
           }
         }
-        *reinterpret_cast<uint4*>(p.C + go) = out;
+        if (EPI != EPI_STATS || p.C) *reinterpret_cast<uint4*>(p.C + go) = out;
       }
     }
   }

@@ -163,6 +163,9 @@ class HipKernels:
     def fcoef(self, st):  # [2C] scale | shift view of the workspace
         return st.ws[st.coef_off:st.coef_off + 2 * st.C]
 
+    def bcoef(self, st):  # [3C] k | c1 | c0 backward coefficients (csrc/bn_act.hip ws_bcoef)
+        return st.ws[st.coef_off + 2 * st.C:st.coef_off + 5 * st.C]
+
     def _fwd_acc(self, st):
         return st.ws[:REP * 2 * st.C]
 
@@ -193,6 +196,79 @@ class HipKernels:
         self.ext.conv3x3_gemm(x, w, y, n, h, wd, cin, cout, stride, None, 1, out.mod.running_mean,
                               self._fwd_acc(out), None, None, None)
         return y
+
+    def conv1x1_stats(self, x, w, pro: BNState, out: BNState):
+        """Statistics-only pass of a 1x1 conv (STATS epilogue, nothing stored):
+        the recomputed conv3 of a "recompute" block (csrc/bnfold.hip)."""
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        M = n * h * wd
+        self._arm(out, M)
+        self.ext.conv_seg_arm(0, None, None, None, 0, 0, 0, None, True)
+        self.ext.conv1x1_gemm(x, w, x, M, cout, cin, h, wd, h, wd, 1, self.fcoef(pro), 1, out.mod.running_mean,
+                              self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
+
+    def conv1x1_apply(self, x, w, pro: BNState, st: BNState, res):
+        """out = relu(B_st(conv1x1(relu(B_pro(x)))) + res) and its packed ReLU
+        mask, the conv recomputed in the GEMM (APPLY epilogue, csrc/gemm_epi.h)."""
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        M = n * h * wd
+        y = _nhwc_empty(n, cout, h, wd, x)
+        mb = torch.empty(M * cout // 8, dtype=torch.uint8, device=x.device)
+        self.ext.conv1x1_gemm(x, w, y, M, cout, cin, h, wd, h, wd, 1, self.fcoef(pro), 5, None, None, None, None,
+                              self.fcoef(st), res, 1, 0, 0, mb, None, None, None)
+        return y, mb
+
+    def _fold_bufs(self, N4, C, dev):
+        key = ("fold", N4, C)
+        b = self._dw32.get(key)
+        if b is None:
+            b = (torch.empty(C, N4 + C, dtype=torch.bfloat16, device=dev), torch.empty(C, device=dev))
+            self._dw32[key] = b
+        return b
+
+    def dgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3):
+        """conv3 data gradient of a recompute block with BN3's backward apply
+        folded into the weights (csrc/bnfold.hip): [g | relu(B2(c2))] .
+        [diag(k) W3 ; W3^T diag(c1) W3] + W3^T c0, masked by B2's ReLU, + B2's
+        backward sums; w3 = W3 [4C, C]."""
+        n, N4, h, w = g.shape
+        C = w3.shape[1]
+        M = n * h * w
+        bp, bias = self._fold_bufs(N4, C, g.device)
+        self.ext.bn_fold_dgrad(w3, self.bcoef(st3), bp, bias)
+        out = _nhwc_empty(n, C, h, w, g)
+        self._arm(st2, M, fwd=False)
+        self.ext.conv_seg_arm(1, c2, None, self.fcoef(st2), C, N4 + C, 0, bias, False)
+        self.ext.conv1x1_gemm(g, bp, out, M, C, N4, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), c2,
+                              st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
+        return out
+
+    def _ws32(self, key, n):
+        t = self._dw32.get(key)
+        if t is None or t.numel() < n:
+            t = self._dw32[key] = torch.empty(n, device=self.dev)
+        return t
+
+    def wgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3, dW):
+        """conv3 weight gradient of a recompute block: diag(k) G + diag(c1) W3 Q
+        + c0 sum(a2)^T with G = g^T a2, Q = a2^T a2, a2 = relu(B2(c2)) (split-M
+        MFMA GEMMs into fp32, csrc/bnfold.hip combines)."""
+        n, N4, h, w = g.shape
+        C = w3.shape[1]
+        M = n * h * w
+        pro = self.fcoef(st2)
+        dg = self._ws32(("fold_g", M, N4, C), self.ext.conv1x1_wgrad_splits(M, N4, C) * N4 * C)
+        self.ext.conv1x1_wgrad(g, c2, pro, dg, None, 1.0, M, N4, C, h, w, h, w, 1)
+        dq = self._ws32(("fold_q", M, C), self.ext.conv1x1_wgrad_splits(M, C, C) * C * C)
+        self.ext.wgrad_grelu_arm(pro)
+        self.ext.conv1x1_wgrad(c2, c2, pro, dq, None, 1.0, M, C, C, h, w, h, w, 1)
+        parts = self.ext.relu_colsum_parts(M)
+        part = self._ws32(("fold_s", M, C), parts * C)
+        self.ext.relu_colsum(c2, pro, C, part)
+        self.ext.slab_reduce_f32(part, C, parts)
+        self.ext.bn_fold_wgrad(w3, self.bcoef(st3), dg, dq, part, 1, dW.view(N4, C))
 
     def bn_stats(self, x, st):
         self.ext.bn_stage_fwd_stats(x, st.ws, x.numel() // st.C, st.C)
@@ -332,13 +408,25 @@ class HipKernels:
                               None, 1, 0, 0, None, None, None, None)
         return out
 
-    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None):
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None, recomp=None):
         """conv1 dgrad + d(identity); with ``prev`` = (mbits, c3, st3, cd, std) the
-        previous block's ReLU mask is applied and its BN sums accumulated."""
+        previous block's ReLU mask is applied and its BN sums accumulated.
+        ``recomp`` = (c2, w3, st2) of a previous recompute block (c3 = None): its
+        conv3 output is recomputed in the same GEMM (csrc/conv1x1.hip PRO_RECOMP)."""
         n, cout, h, w = g.shape
         cin = wt.shape[0]
         out = _nhwc_empty(n, cin, h, w, g)
         M = n * h * w
+        if recomp is not None:
+            assert bpro is None and prev is not None and prev[3] is None
+            mbits, _, st3, _, _ = prev
+            c2p, w3p, st2p = recomp
+            cp = w3p.shape[1]
+            self._arm(st3, M, fwd=False)
+            self.ext.conv_seg_arm(2, c2p, w3p, self.fcoef(st2p), cp, 0, cp, None, False)
+            self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, self._bwd_acc(st3), None,
+                                  st3.save_mean, None, eres, res_stride, h, w, mbits, None, None, None)
+            return out
         if prev is None:
             self._arm_bpro(bpro, cout)
             self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 4, None, None, None, None, None, eres,
@@ -469,6 +557,47 @@ class TorchKernels:
         self._stats(y, out, out.mod.running_mean.clone())
         return y.contiguous(memory_format=torch.channels_last)
 
+    def _conv3(self, x, w, pro):
+        """bf16 output of a 1x1 conv on relu(B_pro(x)) (the recomputed conv3)."""
+        return _bfr(F.conv2d(self._pro(x, pro), w.float()[:, :, None, None]))
+
+    def conv1x1_stats(self, x, w, pro, out):
+        self._stats(self._conv3(x, w, pro), out, out.mod.running_mean.clone())
+
+    def conv1x1_apply(self, x, w, pro, st, res):
+        y = self._conv3(x, w, pro).to(x.dtype).contiguous(memory_format=torch.channels_last)
+        return self.bn_apply(y, st, relu=True, res=res, want_mask=True)
+
+    @staticmethod
+    def bcoef(st):
+        return st.bcoef
+
+    def dgrad_folded(self, g, c2, st2, st3, w3):
+        """HipKernels.dgrad_folded semantics: bf16 folded weights, fp32 GEMM,
+        bf16 rounding of the GEMM output, fp32 bias, B2 mask + sums."""
+        k, c1, c0 = st3.bcoef
+        w = w3.float()                                    # [N4, C]
+        wk = _bfr(k[:, None] * w)                         # diag(k) W3
+        S = _bfr(w.t() @ (c1[:, None] * w))               # W3^T diag(c1) W3 [C, C] (symmetric)
+        bias = w.t() @ c0                                 # [C]
+        a2 = self._pro(c2, st2)
+        d = F.conv2d(g.float(), wk.t()[:, :, None, None]) + F.conv2d(a2, S.t()[:, :, None, None])
+        d = _bfr(d) + bias.view(1, -1, 1, 1)
+        sc, sf = st2.fcoef
+        mask = (c2.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
+        d = torch.where(mask, d, torch.zeros_like(d))
+        self._bsum(d, c2, st2)
+        return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
+
+    def wgrad_folded(self, g, c2, st2, st3, w3, dW):
+        k, c1, c0 = st3.bcoef
+        a2 = _rows(self._pro(c2, st2).contiguous(memory_format=torch.channels_last))  # [M, C]
+        G = _rows(g.float()).t() @ a2                     # [N4, C]
+        Q = a2.t() @ a2                                   # [C, C]
+        asum = a2.sum(0)
+        dw = k[:, None] * G + c1[:, None] * (w3.float() @ Q) + c0[:, None] * asum[None, :]
+        dW.copy_(dw.view_as(dW))
+
     def _stats(self, y, st, shift):
         d = _rows(y.float()) - shift
         st.fsum = (d.sum(0), (d * d).sum(0), shift)
@@ -595,7 +724,7 @@ class TorchKernels:
         return F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)).to(g.dtype).contiguous(
             memory_format=torch.channels_last)
 
-    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None):
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None, recomp=None):
         g = self._bpro(g, bpro)
         d = _bfr(F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)))
         r = torch.zeros_like(d)
@@ -603,6 +732,9 @@ class TorchKernels:
         d = _bfr(d + r)
         if prev is not None:
             mask, c3, st3, cd, std_ = prev
+            if recomp is not None:  # the previous block's conv3 output, recomputed
+                c2p, w3p, st2p = recomp
+                c3 = self._conv3(c2p, w3p, st2p)
             d = torch.where(mask, d, torch.zeros_like(d))
             self._bsum(d, c3, st3)
             if cd is not None:
@@ -690,6 +822,22 @@ class ResNetEngine:
         # conv1's dgrad (N = 4C output tiles each re-transform the A tile) and at
         # K >= 1024 (the register-staged loop vs the LDS-DMA one: 88 -> 138 us); the
         # G prologue (mode 2) loses to reading the written-through tensor (106 -> 354 us)
+        # "Recompute" blocks (csrc/bnfold.hip): a bottleneck without a downsample
+        # branch whose successor's conv1 data gradient can recompute its conv3
+        # output never stores that output (c3, the step's widest tensors at the
+        # early stages): the forward runs conv3 twice -- a statistics-only pass,
+        # then the GEMM that applies BN3 + residual + ReLU in its epilogue --, the
+        # successor's RESBITS GEMM recomputes c3 tiles for BN3's backward sums,
+        # and BN3's backward apply reaches conv3's data / weight gradients folded
+        # into the weights.  KDL_RECOMP=0: off; KDL_RECOMP_MAXC: widest 4C served.
+        # Measured per block (single-stream rocprofv3, profiles/r03_recompute_*): at the 56x56
+        # stage (4C = 256) forward conv3 + BN3 apply 400 -> 297 us and conv3 dgrad 275 -> 160 us,
+        # against +50 us in the successor's RESBITS; at 28x28 the recomputing RESBITS (+80-150 us)
+        # outweighs the rest -- so 4C <= 256 by default.
+        maxc = int(os.environ.get("KDL_RECOMP_MAXC", "256")) if os.environ.get("KDL_RECOMP", "1") == "1" else 0
+        nb = len(self.blocks)
+        self.recomp = [b.down_conv is None and i < nb - 1 and b.conv3.out_channels <= maxc
+                       for i, b in enumerate(self.blocks)]
         self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "1"))
         self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "512"))
         self.fuse_bn1 = os.environ.get("KDL_BN_BWD_FUSE_BN1", "0") == "1"
@@ -822,7 +970,7 @@ class ResNetEngine:
         x1, idx = K.stem_fwd(c0, st0, gemm_stats)
         saved = []
         cur = x1
-        for blk in self.blocks:
+        for bi, blk in enumerate(self.blocks):
             s = blk.conv2.stride[0]
             st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
             n, _, h, w = cur.shape
@@ -839,6 +987,14 @@ class ResNetEngine:
                 ho, wo = c2.shape[-2:]
                 K.bn_stats(c2, st2)
                 K.bn_finalize(st2, n * ho * wo, x=c2)
+            if self.recomp[bi]:  # conv3 never stored: statistics pass, then the applying GEMM
+                w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
+                K.conv1x1_stats(c2, w3, st2, st3)
+                K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
+                out, mbits = K.conv1x1_apply(c2, w3, st2, st3, cur)
+                saved.append((cur, c1, a1, c2, None, None, mbits))
+                cur = out
+                continue
             c3 = K.conv1x1_fwd(c2, blk.conv3.weight.view(blk.conv3.out_channels, -1), 1, st2, st3)
             K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
             cd = None
@@ -944,7 +1100,7 @@ class ResNetEngine:
             blk = self.blocks[i]
             cur_in, c1, a1, c2, c3, cd, mbits = saved[i]
             st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
-            n, _, ho, wo = c3.shape
+            n, _, ho, wo = g.shape
             Mo = n * ho * wo
             # bn3 (+ downsample BN) backward: one apply pass over g for both branches
             K.bn_bwd_finalize(st3, Mo, *self._bn_grads(st3))
@@ -953,16 +1109,24 @@ class ResNetEngine:
             if std_ is not None:
                 K.bn_bwd_finalize(std_, Mo, *self._bn_grads(std_))
                 self._bn_ready(std_)
-            if std_ is not None and self._fuse_mode(c3.shape[1]) == 0:
-                dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches
-                op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
+            opd = None
+            if self.recomp[i]:
+                # c3 was never stored: BN3's backward apply folded into conv3's weights
+                w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
+                g2 = K.dgrad_folded(g, c2, st2, st3, w3)
+                with self._on_side(g):
+                    K.wgrad_folded(g, c2, st2, st3, w3, self._g(blk.conv3.weight))
             else:
-                op3 = self._bn_bwd_operand(g, c3, st3)
-                opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
-            # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
-            g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
-            with self._on_side(*self._side_of(op3)):
-                K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
+                if std_ is not None and self._fuse_mode(c3.shape[1]) == 0:
+                    dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches
+                    op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
+                else:
+                    op3 = self._bn_bwd_operand(g, c3, st3)
+                    opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
+                # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
+                g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
+                with self._on_side(*self._side_of(op3)):
+                    K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
             self.on_ready(blk.conv3.weight)
             K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
             self._bn_ready(st2)
@@ -1006,6 +1170,15 @@ class ResNetEngine:
             self._bn_ready(st1)
             # bn1 backward apply: its own pass, or (fused) inside conv1's dgrad below
             op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1, bn1=True)
+            rc = None
+            if i > 0 and self.recomp[i - 1]:
+                # the previous block's conv3 output is recomputed in conv1's dgrad (its
+                # second K segment), which then has no room for the bn1 A prologue
+                pb = self.blocks[i - 1]
+                rc = (saved[i - 1][3], pb.conv3.weight.view(pb.conv3.out_channels, -1), self.bn[pb.bn2])
+                if op1[1] is not None:
+                    dc1, _ = K.bn_bwd_apply(g1, c1, st1)
+                    op1 = (dc1, None, dc1, None)
             # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
             if blk.down_conv is not None:
                 ds = blk.down_conv.stride[0]
@@ -1018,7 +1191,7 @@ class ResNetEngine:
                 pblk = self.blocks[i - 1]
                 p_std = self.bn[pblk.down_bn] if pblk.down_bn is not None else None
                 g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride,
-                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std), bpro=op1[1])
+                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std), bpro=op1[1], recomp=rc)
             else:
                 g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride, None, bpro=op1[1])
             with self._on_side(*self._side_of(op1), *(self._side_of(opd) if opd is not None else ())):
