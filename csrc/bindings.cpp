@@ -776,24 +776,35 @@ struct SegArm {
   const void* B2 = nullptr;
   const float* pro2 = nullptr;
   const float* ebias = nullptr;
-  int64_t K2 = 0, ldb = 0, ldb2 = 0, a2_rows = 0, b2_numel = 0, bias_n = 0;
+  const float* seg1_scale = nullptr;
+  int64_t K2 = 0, K2a = 0, ldb = 0, ldb2 = 0, a2_rows = 0, b2_numel = 0, bias_n = 0, s1_n = 0;
   bool nostore = false;
 };
 thread_local SegArm g_seg_arm;
 
 void conv_seg_arm(int64_t seg, const c10::optional<at::Tensor>& A2, const c10::optional<at::Tensor>& B2,
                   const c10::optional<at::Tensor>& pro2, int64_t K2, int64_t ldb, int64_t ldb2,
-                  const c10::optional<at::Tensor>& ebias, bool nostore) {
+                  const c10::optional<at::Tensor>& ebias, bool nostore, int64_t K2a,
+                  const c10::optional<at::Tensor>& seg1_scale) {
   TORCH_CHECK(seg >= 0 && seg <= 2, "conv_seg_arm: seg 0 (none), 1 (summed) or 2 (recompute)");
   SegArm a;
   a.seg = static_cast<int>(seg);
   a.nostore = nostore;
   if (seg) {
-    TORCH_CHECK(K2 > 0 && K2 % 64 == 0 && opt_ptr(A2) && opt_ptr(pro2), "conv_seg_arm: A2, pro2, K2 % 64 == 0");
-    need_bf16(*A2, K2, "conv_seg_arm A2");
-    need_opt_f32(pro2, 2 * K2, "conv_seg_arm pro2");
+    if (K2a <= 0) K2a = K2;
+    TORCH_CHECK(K2 > 0 && K2 % 64 == 0 && K2a % 64 == 0 && K2 % K2a == 0 && opt_ptr(A2) && opt_ptr(pro2),
+                "conv_seg_arm: A2, pro2, K2 % 64 == 0, K2a | K2");
+    need_bf16(*A2, K2a, "conv_seg_arm A2");
+    need_opt_f32(pro2, 2 * K2a, "conv_seg_arm pro2");
     a.A2 = A2->data_ptr();
-    a.a2_rows = A2->numel() / K2;
+    a.a2_rows = A2->numel() / K2a;
+    a.K2a = K2a;
+    if (opt_ptr(seg1_scale)) {
+      TORCH_CHECK(seg == 1, "conv_seg_arm: seg1_scale with seg 1");
+      need_opt_f32(seg1_scale, 1, "conv_seg_arm seg1_scale");
+      a.seg1_scale = seg1_scale->data_ptr<float>();
+      a.s1_n = seg1_scale->numel();
+    }
     a.pro2 = pro2->data_ptr<float>();
     a.K2 = K2;
     a.ldb = ldb;
@@ -892,6 +903,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
     TORCH_CHECK(sg.seg == 1 ? epi == 2 : epi == 3, "conv_seg_arm: seg 1 feeds MASKX, seg 2 RESBITS");
   }
   if (sg.ebias) TORCH_CHECK(epi == 2 && sg.bias_n >= N, "conv_seg_arm: ebias [N] for a MASKX epilogue");
+  if (sg.seg1_scale) TORCH_CHECK(sg.s1_n >= K, "conv_seg_arm: seg1_scale [K]");
   if (sg.nostore) TORCH_CHECK(epi == 1, "conv_seg_arm: statistics-only launches are STATS");
   if (bw.x) {
     TORCH_CHECK(bw.C == K && bw.rows == M, "bn_bwd_pro_arm: armed for [", bw.rows, ", ", bw.C,
@@ -914,8 +926,8 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   }
   if (epi == 5) {  // APPLY: relu(y * scale + shift + eres) + packed mask out
     TORCH_CHECK(opt_ptr(pro_coef) && opt_ptr(ecoef) && opt_ptr(eres) && opt_ptr(ebits) && stride == 1 &&
-                    res_stride <= 1 && N % 128 == 0,
-                "epi APPLY needs pro_coef, ecoef, eres, ebits (out), dense rows, N % 128 == 0");
+                    res_stride <= 1,
+                "epi APPLY needs pro_coef, ecoef, eres, ebits (out), dense rows");
     need_opt_f32(ecoef, 2 * N, "ecoef");
     need_opt_bf16(eres, M * N, "eres");
     TORCH_CHECK(ebits->scalar_type() == at::kByte && ebits->is_contiguous() && ebits->numel() >= M * N / 8, "ebits");
@@ -945,6 +957,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   kdl::Conv1x1Args a{};
   a.A = A.data_ptr(); a.B = B.data_ptr(); a.C = sg.nostore ? nullptr : C.data_ptr();
   a.seg = sg.seg; a.A2 = sg.A2; a.K2 = static_cast<int>(sg.K2); a.ldb = static_cast<int>(ldb);
+  a.K2a = static_cast<int>(sg.K2a); a.seg1_scale = sg.seg1_scale;
   a.B2 = sg.seg ? (sg.B2 ? sg.B2 : static_cast<const void*>(static_cast<const uint16_t*>(B.data_ptr()) + K)) : nullptr;
   a.ldb2 = static_cast<int>(sg.B2 ? sg.ldb2 : ldb);
   a.ebias = sg.ebias;
@@ -1176,7 +1189,7 @@ void bn_fold_dgrad(const at::Tensor& w3, const at::Tensor& bcoef, at::Tensor bp,
   const int64_t N4 = w3.size(0), C = w3.size(1);
   need_bf16(w3, N4 * C, "bn_fold_dgrad w3");
   need_opt_f32(bcoef, 3 * N4, "bn_fold_dgrad bcoef");
-  need_bf16(bp, C * (N4 + C), "bn_fold_dgrad bp");
+  need_bf16(bp, C * 2 * C, "bn_fold_dgrad bp");
   need_opt_f32(bias, C, "bn_fold_dgrad bias");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(w3.device());
   check_hip(kdl::bn_fold_dgrad(w3.data_ptr(), bcoef.data_ptr<float>(), static_cast<int>(N4), static_cast<int>(C),

@@ -10,10 +10,12 @@
 // consumers of the BN3 backward apply dc3 = k g + c1 c3 + c0 take it in
 // algebraic form, because c3 is linear in a2:
 //
-//   conv3 data gradient   dc3 W3 = g (diag(k) W3) + a2 S + 1 b^T,
+//   conv3 data gradient   dc3 W3 = (diag(k) g) W3 + a2 S + 1 b^T,
 //                         S = W3^T diag(c1) W3 [C, C],  b = W3^T c0 [C]
-//     -> one two-segment GEMM [g | a2] . [diag(k) W3 ; S] (csrc/conv1x1.hip
-//        PRO_SEG, bias in the MASKX epilogue): B' = fold_dgrad below;
+//     -> one two-segment GEMM [k g | a2 | a2] . [W3 ; S_hi ; S_lo] (csrc/conv1x1.hip
+//        PRO_SEG: k applied per element while staging g -- random rounding, as
+//        the materialised dc3 had --, S as a bf16 hi + lo pair, bias in the
+//        MASKX epilogue): S_hi | S_lo and b from fold_dgrad below;
 //   conv3 weight gradient dW3 = dc3^T a2 = diag(k) G + diag(c1) W3 Q + c0 sum(a2)^T,
 //                         G = g^T a2, Q = a2^T a2 (both split-M MFMA GEMMs on
 //                         the LDS-DMA weight-gradient kernel, Q with the GRELU
@@ -35,41 +37,40 @@ constexpr int kFoldThreads = 256;
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
 
 // Small fp32 GEMM tiles out[m][n] = sum_k a(m, k) b(k, n) over 16 x 16 output
-// tiles, one output per thread, K staged through LDS in 64-deep chunks (both
-// operands coalesced along the tile's 16-wide side), fixed summation order.
-constexpr int kT = 16, kKC = 64;
+// tiles, one output per thread.  The whole K range (<= kMaxK) of both operand
+// panels is staged through LDS in one pass -- every load of the block issued
+// back to back, one memory latency instead of one per K chunk -- then summed in
+// a fixed order.
+constexpr int kT = 16, kMaxK = 512;
 
 template <typename FA, typename FB>
 __device__ __forceinline__ float tile_dot(int K, int m0, int n0, FA a, FB b, float (*as)[kT + 1],
                                           float (*bs)[kT + 1]) {
   const int t = threadIdx.x, tm = t / kT, tn = t % kT;
-  float acc = 0.f;
-  for (int k0 = 0; k0 < K; k0 += kKC) {
-    for (int e = t; e < kKC * kT; e += kFoldThreads) {  // e = kk * 16 + i
-      const int kk = e / kT, i = e % kT;
-      const bool ok = k0 + kk < K;
-      as[kk][i] = ok ? a(m0 + i, k0 + kk) : 0.f;
-      bs[kk][i] = ok ? b(k0 + kk, n0 + i) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll 16
-    for (int kk = 0; kk < kKC; ++kk) acc = fmaf(as[kk][tm], bs[kk][tn], acc);
-    __syncthreads();
+  for (int e = t; e < K * kT; e += kFoldThreads) {  // e = k * 16 + i
+    const int k = e / kT, i = e % kT;
+    as[k][i] = a(m0 + i, k);
+    bs[k][i] = b(k, n0 + i);
   }
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll 16
+  for (int k = 0; k < K; ++k) acc = fmaf(as[k][tm], bs[k][tn], acc);
+  __syncthreads();
   return acc;
 }
 
-// Blocks [0, (C/16)^2): S tiles, S[l][j] = sum_c W3[c][l] c1_c W3[c][j] -> Bp[j][N4 + l].
-// Blocks past them: 16 columns j each, Bp[j][c] = bf16(k_c W3[c][j]) and
-// bias[j] = sum_c c0_c W3[c][j].
+// Blocks [0, (C/16)^2): tiles of S = W3^T diag(c1) W3 [C, C] as a bf16 hi + lo
+// pair, S2[j][l] = bf16(S[l][j]), S2[j][C + l] = bf16(S[l][j] - S2[j][l]) (~16
+// significant bits: S multiplies every pixel's a2, so a plain bf16 rounding of
+// it would be one systematic error repeated across the whole batch).  Blocks
+// past them: 16 columns j each, bias[j] = sum_c c0_c W3[c][j] (fp32).
 __global__ __launch_bounds__(kFoldThreads) void fold_dgrad_kernel(const uint16_t* __restrict__ w3,
                                                                   const float* __restrict__ bcoef, int N4, int C,
-                                                                  uint16_t* __restrict__ bp, float* __restrict__ bias) {
-  __shared__ float as[kKC][kT + 1], bs[kKC][kT + 1];
-  const float* k = bcoef;
+                                                                  uint16_t* __restrict__ s2, float* __restrict__ bias) {
+  __shared__ float as[kMaxK][kT + 1], bs[kMaxK][kT + 1];
   const float* c1 = bcoef + N4;
   const float* c0 = bcoef + 2 * N4;
-  const int ldp = N4 + C;
   const int tiles = C / kT, t = threadIdx.x;
   if (static_cast<int>(blockIdx.x) < tiles * tiles) {
     const int l0 = (blockIdx.x / tiles) * kT, j0 = (blockIdx.x % tiles) * kT;
@@ -77,7 +78,9 @@ __global__ __launch_bounds__(kFoldThreads) void fold_dgrad_kernel(const uint16_t
         N4, l0, j0, [&](int l, int c) { return bf2f(w3[static_cast<int64_t>(c) * C + l]); },
         [&](int c, int j) { return c1[c] * bf2f(w3[static_cast<int64_t>(c) * C + j]); }, as, bs);
     const int l = l0 + t / kT, j = j0 + t % kT;
-    bp[static_cast<int64_t>(j) * ldp + N4 + l] = f32_to_bf16(s);
+    const uint16_t hi = f32_to_bf16(s);
+    s2[static_cast<int64_t>(j) * 2 * C + l] = hi;
+    s2[static_cast<int64_t>(j) * 2 * C + C + l] = f32_to_bf16(s - bf2f(hi));
     return;
   }
   const int j0 = (blockIdx.x - tiles * tiles) * kT;
@@ -85,13 +88,9 @@ __global__ __launch_bounds__(kFoldThreads) void fold_dgrad_kernel(const uint16_t
 #pragma unroll
   for (int i = 0; i < kT; ++i) b[i] = 0.f;
   for (int c = t; c < N4; c += kFoldThreads) {
-    const float kc = k[c], cc = c0[c];
+    const float cc = c0[c];
 #pragma unroll
-    for (int i = 0; i < kT; ++i) {
-      const float w = bf2f(w3[static_cast<int64_t>(c) * C + j0 + i]);
-      bp[static_cast<int64_t>(j0 + i) * ldp + c] = f32_to_bf16(kc * w);
-      b[i] = fmaf(cc, w, b[i]);
-    }
+    for (int i = 0; i < kT; ++i) b[i] = fmaf(cc, bf2f(w3[static_cast<int64_t>(c) * C + j0 + i]), b[i]);
   }
   float* red = &as[0][0];  // [kT][kFoldThreads / 64] wave partials
 #pragma unroll
@@ -160,7 +159,7 @@ __global__ __launch_bounds__(kFoldThreads) void fold_wgrad_kernel(const uint16_t
                                                                   const float* __restrict__ Q,
                                                                   const float* __restrict__ part, int nparts, int N4,
                                                                   int C, uint16_t* __restrict__ dw) {
-  __shared__ float as[kKC][kT + 1], bs[kKC][kT + 1];
+  __shared__ float as[kMaxK][kT + 1], bs[kMaxK][kT + 1];
   const int tj = C / kT;
   const int c0i = (blockIdx.x / tj) * kT, j0 = (blockIdx.x % tj) * kT;
   const float q = tile_dot(
@@ -177,7 +176,7 @@ __global__ __launch_bounds__(kFoldThreads) void fold_wgrad_kernel(const uint16_t
 }  // namespace
 
 hipError_t bn_fold_dgrad(const void* w3, const float* bcoef, int N4, int C, void* bp, float* bias, hipStream_t s) {
-  if (N4 <= 0 || C <= 0 || C % kT || N4 % kT) return hipErrorInvalidValue;
+  if (N4 <= 0 || C <= 0 || C % kT || N4 % kT || N4 > kMaxK) return hipErrorInvalidValue;
   const int tiles = C / kT;
   hipLaunchKernelGGL(fold_dgrad_kernel, dim3(tiles * tiles + tiles), dim3(kFoldThreads), 0, s,
                      static_cast<const uint16_t*>(w3), bcoef, N4, C, static_cast<uint16_t*>(bp), bias);
@@ -198,7 +197,7 @@ hipError_t relu_colsum(const void* x, const float* coef, int64_t M, int C, float
 
 hipError_t bn_fold_wgrad(const void* w3, const float* bcoef, const float* G, const float* Q, const float* part,
                          int nparts, int N4, int C, void* dw, hipStream_t s) {
-  if (N4 <= 0 || C <= 0 || nparts <= 0 || C % kT || N4 % kT) return hipErrorInvalidValue;
+  if (N4 <= 0 || C <= 0 || nparts <= 0 || C % kT || N4 % kT || C > kMaxK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fold_wgrad_kernel, dim3((N4 / kT) * (C / kT)), dim3(kFoldThreads), 0, s,
                      static_cast<const uint16_t*>(w3), bcoef, G, Q, part, nparts, N4, C, static_cast<uint16_t*>(dw));
   return hipGetLastError();

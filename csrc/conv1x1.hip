@@ -67,8 +67,9 @@ constexpr int BK = 64;
 // tiles stay within 80 KiB of LDS (two blocks per CU) up to K = 512, 64-wide
 // tiles up to K = 2048 (the widest ResNet-50 data-gradient K)
 __host__ __device__ constexpr int bwd_kmax(int bn) { return bn >= 128 ? 512 : 2048; }
-// widest second K segment (the BN2 width of a recompute block's conv3: C <= 512)
-constexpr int kSegKmax = 512;
+// widest second K segment (A2 row: the BN2 width of a recompute block's conv3,
+// C <= 512) and widest first segment with a per-channel scale (4C <= 2048)
+constexpr int kSegKmax = 512, kSeg1Kmax = 2048;
 
 // PRO: 0 none, PRO_FWD = BN+ReLU of the previous layer, PRO_BWD = BN-backward
 // apply (GemmParams::bx / bcoef; dense rows only), PRO_SEG / PRO_RECOMP = a
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   constexpr int KT = PRO == PRO_BWD ? bwd_kmax(BN) : 0;
   // SEG / RECOMP: segment 2's BN scale | shift staged once per block (read in
   // swrite: no coefficient registers live across the K loop), K2 <= kSegKmax
-  constexpr int KS = (PRO == PRO_SEG || PRO == PRO_RECOMP) ? 2 * kSegKmax : 0;
+  constexpr int KS = (PRO == PRO_SEG || PRO == PRO_RECOMP) ? 2 * kSegKmax + (PRO == PRO_SEG ? kSeg1Kmax : 0) : 0;
   // RECOMP: a third region holds the recomputed x tile [BM][BN + 8] beside the
   // two stage buffers, so the next tile's first K-step still overlaps the epilogue
   constexpr int XT = PRO == PRO_RECOMP ? BM * (BN + 8) : 0;
@@ -166,11 +167,19 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       reinterpret_cast<float4*>(coef_lds)[i] = reinterpret_cast<const float4*>(p.bcoef)[i];
     __syncthreads();
   }
-  float* seg_coef = reinterpret_cast<float*>(lds + 2 * kBuf + 6 * KT + XT);  // [2 K2] scale | shift
-  (void)seg_coef;
+  // [2 K2a] segment-2 scale | shift, then (PRO_SEG) [K] segment-1 scale
+  float* seg_coef = reinterpret_cast<float*>(lds + 2 * kBuf + 6 * KT + XT);
+  float* seg1_sc = seg_coef + 2 * kSegKmax;
+  (void)seg_coef; (void)seg1_sc;
+  const int K2a = SEG ? p.K2a : 0;
   if constexpr (KS > 0) {
-    for (int i = t; i < 2 * p.K2 / 4; i += kThreads)
+    for (int i = t; i < 2 * K2a / 4; i += kThreads)
       reinterpret_cast<float4*>(seg_coef)[i] = reinterpret_cast<const float4*>(p.pro_coef)[i];
+    if constexpr (PRO == PRO_SEG) {
+      if (p.seg1_scale)
+        for (int i = t; i < K / 4; i += kThreads)
+          reinterpret_cast<float4*>(seg1_sc)[i] = reinterpret_cast<const float4*>(p.seg1_scale)[i];
+    }
     __syncthreads();
   }
 
@@ -204,7 +213,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       const int k0 = (s2 ? kt - nk1 : kt) * KBK;
       if (s2) {
 #pragma unroll
-        for (int i = 0; i < A_CH; ++i) ra[i] = ld16(p.A2 + static_cast<int64_t>(a_m[i]) * p.K2 + k0 + a_kc[i]);
+        for (int i = 0; i < A_CH; ++i)
+          ra[i] = ld16(p.A2 + static_cast<int64_t>(a_m[i]) * K2a + k0 % K2a + a_kc[i]);
 #pragma unroll
         for (int i = 0; i < B_CH; ++i) {
           const int c = t + i * kThreads;
@@ -219,6 +229,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           const int c = t + i * kThreads;
           rb[i] = ld16(p.B + static_cast<int64_t>(n0 + c / CPRK) * ldb + k0 + (c % CPRK) * 8);
         }
+        st_k0 = k0;
       }
       st_seg2 = s2;
       return;
@@ -283,14 +294,25 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       }
     }
     bool fwd_pro = PRO == PRO_FWD;
+    bool seg1_scaled = false;
+    (void)seg1_scaled;
     if constexpr (SEG) {
       fwd_pro = st_seg2;
-      if (fwd_pro) {  // this thread's 8 channels of the staged segment-2 K-step, from LDS
+      if constexpr (PRO == PRO_SEG) seg1_scaled = !st_seg2 && p.seg1_scale != nullptr;
+      if (seg1_scaled) {  // segment 1: one scale per K channel (psc reused, no shift)
         const int c = st_k0 + a_kc[0];
 #pragma unroll
         for (int j = 0; j < 8; j += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(seg1_sc + c + j);
+          psc[j] = a.x; psc[j + 1] = a.y; psc[j + 2] = a.z; psc[j + 3] = a.w;
+        }
+      }
+      if (fwd_pro) {  // this thread's 8 channels of the staged segment-2 K-step, from LDS
+        const int c = st_k0 % K2a + a_kc[0];
+#pragma unroll
+        for (int j = 0; j < 8; j += 4) {
           const float4 a = *reinterpret_cast<const float4*>(seg_coef + c + j);
-          const float4 b = *reinterpret_cast<const float4*>(seg_coef + p.K2 + c + j);
+          const float4 b = *reinterpret_cast<const float4*>(seg_coef + K2a + c + j);
           psc[j] = a.x; psc[j + 1] = a.y; psc[j + 2] = a.z; psc[j + 3] = a.w;
           psf[j] = b.x; psf[j + 1] = b.y; psf[j + 2] = b.z; psf[j + 3] = b.w;
         }
@@ -307,6 +329,12 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           const float o = fmaf(f[j], psc[j], psf[j]);
           f[j] = o > 0.f ? o : 0.f;
         }
+        v = pack8(f);
+      } else if (seg1_scaled) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= psc[j];
         v = pack8(f);
       } else if constexpr (PRO == PRO_BWD) {
         float f[8], x[8];
@@ -332,6 +360,23 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 
   Epilogue<BM, BN, kThreads, EPI, G_DENSE, PRO == PRO_RECOMP> epi;
   epi.init(t, n0);
+  // RSTATS: each lane's running shifted sums of its accumulator slots -- slot
+  // (i, r) is output channel n0 + wn0 + 32 i + (r & 3) + 8 (r >> 2) + 4 fh for
+  // every tile of the block -- over the bf16-rounded outputs (the values STATS
+  // would have summed), reduced across lanes / waves once after the last tile
+  constexpr bool RSTATS = EPI == EPI_RSTATS;
+  constexpr int RS = RSTATS ? TN : 1;
+  float rs1[RS][16], rs2[RS][16], rsh[RS][16];
+  if constexpr (RSTATS) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        rsh[i][r] = p.shift[n0 + wn0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * ((lane & 63) >> 5)];
+        rs1[i][r] = 0.f;
+        rs2[i][r] = 0.f;
+      }
+  }
 
   int tm = gm;
   if (tm < tiles_m) {
@@ -342,6 +387,12 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   __syncthreads();
   int cur = 0;
   const int fr = lane & 31, fh = lane >> 5;
+  // Overlapped epilogue (run between the tile's last MFMAs and the staging of
+  // the next tile's first K-step, whose loads are then in flight during it):
+  // measured SLOWER on every variant that fits it in registers (APPLY 197 ->
+  // 287 us, recompute RESBITS 305 -> 396 us, folded dgrad 150 -> 164 us at the
+  // 56x56 stage), so compiled out; kept for the record of the experiment
+  constexpr bool OVL = false;
   for (; tm < tiles_m; tm += GM) {
     f32x16_t acc[TN][TM];
 #pragma unroll
@@ -368,6 +419,38 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
             a[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], a[i][j], 0, 0, 0);
       }
     };
+    // the tile's epilogue (csrc/gemm_epi.h) with its output tile in LDS at Cb
+    // (RSTATS: register sums, no LDS); row-side operands of the first prefetch
+    // group are issued before the accumulators go to LDS
+    auto epilogue = [&](bf16_t* Cb) {
+      if constexpr (RSTATS) {  // statistics only: no LDS round trip, nothing stored
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          if (tm * BM + wm0 + 32 * j + fr >= M) continue;  // rows past M (this lane's column)
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float y = __uint_as_float(static_cast<uint32_t>(f32_to_bf16(acc[i][j][r])) << 16);
+              const float d = y - rsh[i][r];
+              rs1[i][r] += d;
+              rs2[i][r] = fmaf(d, d, rs2[i][r]);
+            }
+        }
+        return;
+      }
+      epi.begin(p, tm);
+      bf16_t* Cs = Cb;
+      acc_to_lds<TN, TM>(acc, Cs, LDC, wm0, wn0, lane);
+      bf16_t* Xs = nullptr;
+      if constexpr (PRO == PRO_RECOMP) {  // acc holds the recomputed conv output (x of the RESBITS sums)
+        Xs = Cs;
+        Cs = lds + 2 * kBuf;  // (KT == 0: no coefficient table in between)
+      }
+      __syncthreads();
+      epi.rows(p, Cs, tm, Xs);
+      __syncthreads();  // Cs is restaged by a later K-step
+    };
     for (int kt = 0; kt < nk; ++kt) {
       const bool more_k = kt + 1 < nk;
       const bool more = more_k || tm + GM < tiles_m;
@@ -390,26 +473,23 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
             for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
         }
       }
+      if (OVL && !more_k) {
+        // overlapped epilogue: the tile's last K-step is consumed (after this
+        // barrier buffer cur is free for the output tile) and the next tile's
+        // first K-step is still in flight to registers -- its load latency hides
+        // under the epilogue instead of stalling swrite below
+        __syncthreads();
+        epilogue(lds + cur * kBuf);
+      }
       if (more_k || (more && !SPLIT_C)) swrite(cur ^ 1);
       __syncthreads();
       cur ^= 1;
     }
-    // ---- epilogue (csrc/gemm_epi.h): row-side operands of the first
-    // prefetch group are issued before the accumulators go to LDS.
-    epi.begin(p, tm);
+    if constexpr (OVL) continue;
     // D[n][m] -> LDS [m][n] (buffer cur^1 is free: its last reader was the final
     // K-step, which ended with a barrier; buffer cur may already hold the next
     // tile's first K-step)
-    bf16_t* Cs = SPLIT_C ? lds : lds + (cur ^ 1) * kBuf;
-    acc_to_lds<TN, TM>(acc, Cs, LDC, wm0, wn0, lane);
-    bf16_t* Xs = nullptr;
-    if constexpr (PRO == PRO_RECOMP) {  // acc holds the recomputed conv output (x of the RESBITS sums)
-      Xs = Cs;
-      Cs = lds + 2 * kBuf;  // (KT == 0: no coefficient table in between)
-    }
-    __syncthreads();
-    epi.rows(p, Cs, tm, Xs);
-    __syncthreads();  // Cs (buffer cur^1) is restaged by the next tile's second K-step
+    epilogue(SPLIT_C ? lds : lds + (cur ^ 1) * kBuf);
     if constexpr (SPLIT_C) {  // stage the next tile's first K-step now that the epilogue is done
       if (tm + GM < tiles_m) swrite(0);
       cur = 0;
@@ -417,6 +497,48 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   }
 
+  if constexpr (RSTATS) {
+    // lanes of one half-wave (same fh) share channels: butterfly over the 32
+    // columns, then the WM wave rows of each channel column through LDS
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          rs1[i][r] += __shfl_xor(rs1[i][r], o);
+          rs2[i][r] += __shfl_xor(rs2[i][r], o);
+        }
+    float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2] (the last K-step ended with a barrier)
+    const int wr = wave / WN;
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ch = wn0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          red[(wr * BN + ch) * 2] = rs1[i][r];
+          red[(wr * BN + ch) * 2 + 1] = rs2[i][r];
+        }
+    }
+    __syncthreads();
+    if (t < BN && gm < tiles_m) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int w = 0; w < WM; ++w) {  // fixed order
+        a1 += red[(w * BN + t) * 2];
+        a2 += red[(w * BN + t) * 2 + 1];
+      }
+      float* rep = p.acc + static_cast<int64_t>(b % kRep) * 2 * N + n0 + t;
+      atomic_add_f32(rep, a1);
+      atomic_add_f32(rep + N, a2);
+    }
+    if (p.fin_ws) {  // (every block arrives, as Epilogue::finish)
+      Epilogue<BM, BN, kThreads, EPI_STATS> fe;
+      fe.init(t, n0);
+      fe.finalize_last(p, red + 2 * WM * BN);
+    }
+    return;
+  }
   epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
 }
 
@@ -693,6 +815,8 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     }
     if constexpr (PRO == PRO_FWD && GATHER == G_DENSE && KBK == BK && BM == 128 && MINB == 2) {  // recomputed conv3 + closing BN/residual/ReLU
       if (epi == EPI_APPLY) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_APPLY, KBK>(p, s);
+      if constexpr (BN == 64)
+        if (epi == EPI_RSTATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RSTATS, KBK>(p, s);
     }
     if constexpr (PRO == PRO_NONE && GATHER == G_DENSE) {
       switch (epi) {
@@ -778,19 +902,21 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.bx = static_cast<const bf16_t*>(a.bx); p.bcoef = a.bcoef; p.aout = static_cast<bf16_t*>(a.aout);
   p.A2 = static_cast<const bf16_t*>(a.A2); p.B2 = static_cast<const bf16_t*>(a.B2);
   p.K2 = a.K2; p.ldb = a.ldb > 0 ? a.ldb : a.K; p.ldb2 = a.ldb2;
+  p.K2a = a.K2a > 0 ? a.K2a : a.K2; p.seg1_scale = a.seg1_scale;
   p.ebias = a.ebias; p.obits = a.obits;
   const bool bpro = a.bx != nullptr;
   if (bpro && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS || a.seg))
     return hipErrorInvalidValue;
   if (a.seg) {  // two-segment K: dense rows, segment 2 through the BN+ReLU prologue
-    if ((a.seg != 1 && a.seg != 2) || !a.A2 || !a.B2 || !a.pro_coef || a.K2 <= 0 || a.K2 % BK || a.K2 > kSegKmax ||
+    if ((a.seg != 1 && a.seg != 2) || !a.A2 || !a.B2 || !a.pro_coef || a.K2 <= 0 || a.K2 % BK || p.K2a % BK ||
+        p.K2a > kSegKmax || a.K2 % p.K2a || (a.seg1_scale && (a.seg != 1 || a.K > kSeg1Kmax)) ||
         a.stride > 1 ||
         a.ksize == 3 || p.ldb < a.K || a.ldb2 < a.K2 || (a.seg == 1 && a.epi != EPI_MASKX) ||
         (a.seg == 2 && a.epi != EPI_RESBITS))
       return hipErrorInvalidValue;
   }
   if (a.epi == EPI_APPLY && (!a.pro_coef || !a.obits || !a.ecoef || !a.eres || a.stride > 1 || a.ksize == 3 ||
-                             p.res_stride != 1 || a.N % 128))
+                             p.res_stride != 1))
     return hipErrorInvalidValue;
   const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP : bpro ? PRO_BWD
                 : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
@@ -833,7 +959,12 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   // 128 x 64 tiles: at 128 x 128 the second accumulator (RECOMP) or the segment
   // bookkeeping + MASKX bias (SEG) spill (752 / 76 B of scratch per lane)
   if (pro == PRO_SEG || pro == PRO_RECOMP) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
-  if (epi == EPI_APPLY) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
+  if (epi == EPI_APPLY && p.N % 128 == 0) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
+  if (epi == EPI_APPLY) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
+  // statistics-only forward conv (the recompute blocks' conv3): register sums
+  static const bool rstats = [] { const char* e = getenv("KDL_RSTATS"); return !e || e[0] != '0'; }();
+  if (epi == EPI_STATS && !p.C && pro == PRO_FWD && gather == G_DENSE && rstats)
+    return dispatch_pg<128, 64, 2>(p, EPI_RSTATS, pro, gather, s);  // (128 x 128: 32 slots per lane spill)
   if (pro == PRO_BWD) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
     if (p.N % 128 == 0 && p.K <= bwd_kmax(128)) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
     if (p.K <= bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);

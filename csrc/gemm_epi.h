@@ -40,7 +40,9 @@ typedef __attribute__((ext_vector_type(2))) float f2_t;
 
 constexpr int kRep = 32;  // replica count of the BN workspace (== bn_act.hip kReplicas)
 
-enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4, EPI_APPLY = 5 };
+// EPI_RSTATS: STATS without a stored output, summed straight from the accumulator
+// registers across the block's tiles (csrc/conv1x1.hip; no per-tile LDS round trip)
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4, EPI_APPLY = 5, EPI_RSTATS = 6 };
 // A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s) |
 // data gradient of a stride-2 3x3 pad-1 conv as four sub-pixel class GEMMs (csrc/igemm.hip)
 enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2, G_DGRAD2 = 3 };
@@ -99,6 +101,9 @@ struct GemmParams {
   const bf16_t* A2;
   const bf16_t* B2;
   int K2, ldb, ldb2;
+  int K2a;                 // A2 row width: segment-2 K column k reads A2 column k % K2a (K2 = 2 K2a: a
+                           // bf16 hi + lo split of B2 against the same A2 columns)
+  const float* seg1_scale; // segment 1: A' = bf16(seg1_scale[k] A) per K channel (null: A as is)
   const float* ebias;  // MASKX: per-output-channel bias added before the mask (null: none)
   uint8_t* obits;      // APPLY: packed ReLU mask [M, N/8] (out)
 };

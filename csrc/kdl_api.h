@@ -243,6 +243,8 @@ struct Conv1x1Args {
   const void* A2;
   const void* B2;
   int K2, ldb, ldb2;
+  int K2a;                           // A2 row width (0: K2); K2 = 2 K2a re-reads A2 against a hi | lo B2
+  const float* seg1_scale;           // seg 1: [K] per-channel scale of A (bf16(scale A)), null: none
   const float* ebias;                // epi 2: per-output-channel bias before the mask
   uint8_t* obits;                    // epi 5 (APPLY: relu(y*ecoef + shift + eres)): ReLU mask out [M, N/8]
 };
@@ -297,7 +299,7 @@ hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, fl
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
 
 // ---- bnfold.hip (BN3 folded through the closing 1x1 conv: c3 never stored)
-// bp [C][N4 + C] bf16 = [diag(k) W3 ; W3^T diag(c1) W3]^T rows, bias [C] = W3^T c0;
+// bp [C][2C] bf16 = W3^T diag(c1) W3 (transposed rows) as hi | lo, bias [C] = W3^T c0;
 // w3 [N4][C] bf16, bcoef = [3 N4] k | c1 | c0 of BN3
 hipError_t bn_fold_dgrad(const void* w3, const float* bcoef, int N4, int C, void* bp, float* bias, hipStream_t s);
 // part [relu_colsum_parts(M)][C] fp32 = per-block column sums of relu(x scale + shift)

@@ -204,7 +204,7 @@ class HipKernels:
         cout = w.shape[0]
         M = n * h * wd
         self._arm(out, M)
-        self.ext.conv_seg_arm(0, None, None, None, 0, 0, 0, None, True)
+        self.ext.conv_seg_arm(0, None, None, None, 0, 0, 0, None, True, 0, None)
         self.ext.conv1x1_gemm(x, w, x, M, cout, cin, h, wd, h, wd, 1, self.fcoef(pro), 1, out.mod.running_mean,
                               self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
 
@@ -220,28 +220,29 @@ class HipKernels:
                               self.fcoef(st), res, 1, 0, 0, mb, None, None, None)
         return y, mb
 
-    def _fold_bufs(self, N4, C, dev):
-        key = ("fold", N4, C)
+    def _fold_bufs(self, C, dev):
+        key = ("fold", C)
         b = self._dw32.get(key)
         if b is None:
-            b = (torch.empty(C, N4 + C, dtype=torch.bfloat16, device=dev), torch.empty(C, device=dev))
+            b = (torch.empty(C, 2 * C, dtype=torch.bfloat16, device=dev), torch.empty(C, device=dev))
             self._dw32[key] = b
         return b
 
-    def dgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3):
+    def dgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3, w3t):
         """conv3 data gradient of a recompute block with BN3's backward apply
-        folded into the weights (csrc/bnfold.hip): [g | relu(B2(c2))] .
-        [diag(k) W3 ; W3^T diag(c1) W3] + W3^T c0, masked by B2's ReLU, + B2's
-        backward sums; w3 = W3 [4C, C]."""
+        folded in (csrc/bnfold.hip): [k g | a2 | a2] . [W3 ; S_hi ; S_lo] + W3^T c0,
+        a2 = relu(B2(c2)), S = W3^T diag(c1) W3 as a bf16 hi + lo pair, masked by
+        B2's ReLU, + B2's backward sums; w3 = W3 [4C, C], w3t = W3^T [C, 4C]."""
         n, N4, h, w = g.shape
         C = w3.shape[1]
         M = n * h * w
-        bp, bias = self._fold_bufs(N4, C, g.device)
-        self.ext.bn_fold_dgrad(w3, self.bcoef(st3), bp, bias)
+        s2, bias = self._fold_bufs(C, g.device)
+        bco = self.bcoef(st3)
+        self.ext.bn_fold_dgrad(w3, bco, s2, bias)
         out = _nhwc_empty(n, C, h, w, g)
         self._arm(st2, M, fwd=False)
-        self.ext.conv_seg_arm(1, c2, None, self.fcoef(st2), C, N4 + C, 0, bias, False)
-        self.ext.conv1x1_gemm(g, bp, out, M, C, N4, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), c2,
+        self.ext.conv_seg_arm(1, c2, s2, self.fcoef(st2), 2 * C, N4, 2 * C, bias, False, C, bco[:N4])
+        self.ext.conv1x1_gemm(g, w3t, out, M, C, N4, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), c2,
                               st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
         return out
 
@@ -423,7 +424,7 @@ class HipKernels:
             c2p, w3p, st2p = recomp
             cp = w3p.shape[1]
             self._arm(st3, M, fwd=False)
-            self.ext.conv_seg_arm(2, c2p, w3p, self.fcoef(st2p), cp, 0, cp, None, False)
+            self.ext.conv_seg_arm(2, c2p, w3p, self.fcoef(st2p), cp, 0, cp, None, False, cp, None)
             self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, self._bwd_acc(st3), None,
                                   st3.save_mean, None, eres, res_stride, h, w, mbits, None, None, None)
             return out
@@ -572,16 +573,20 @@ class TorchKernels:
     def bcoef(st):
         return st.bcoef
 
-    def dgrad_folded(self, g, c2, st2, st3, w3):
-        """HipKernels.dgrad_folded semantics: bf16 folded weights, fp32 GEMM,
-        bf16 rounding of the GEMM output, fp32 bias, B2 mask + sums."""
+    def dgrad_folded(self, g, c2, st2, st3, w3, w3t=None):
+        """HipKernels.dgrad_folded semantics: A = bf16(k g) per element, exact
+        W3, S as a bf16 hi + lo pair, fp32 GEMM, bf16 rounding of the GEMM
+        output, fp32 bias, B2 mask + sums."""
         k, c1, c0 = st3.bcoef
         w = w3.float()                                    # [N4, C]
-        wk = _bfr(k[:, None] * w)                         # diag(k) W3
-        S = _bfr(w.t() @ (c1[:, None] * w))               # W3^T diag(c1) W3 [C, C] (symmetric)
+        S = w.t() @ (c1[:, None] * w)                     # W3^T diag(c1) W3 [C, C] (symmetric)
+        s_hi = _bfr(S)
+        s_lo = _bfr(S - s_hi)
         bias = w.t() @ c0                                 # [C]
         a2 = self._pro(c2, st2)
-        d = F.conv2d(g.float(), wk.t()[:, :, None, None]) + F.conv2d(a2, S.t()[:, :, None, None])
+        gk = _bfr(g.float() * k.view(1, -1, 1, 1))
+        d = (F.conv2d(gk, w.t()[:, :, None, None]) + F.conv2d(a2, s_hi.t()[:, :, None, None])
+             + F.conv2d(a2, s_lo.t()[:, :, None, None]))
         d = _bfr(d) + bias.view(1, -1, 1, 1)
         sc, sf = st2.fcoef
         mask = (c2.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
@@ -834,7 +839,7 @@ class ResNetEngine:
         # stage (4C = 256) forward conv3 + BN3 apply 400 -> 297 us and conv3 dgrad 275 -> 160 us,
         # against +50 us in the successor's RESBITS; at 28x28 the recomputing RESBITS (+80-150 us)
         # outweighs the rest -- so 4C <= 256 by default.
-        maxc = int(os.environ.get("KDL_RECOMP_MAXC", "256")) if os.environ.get("KDL_RECOMP", "1") == "1" else 0
+        maxc = min(512, int(os.environ.get("KDL_RECOMP_MAXC", "256"))) if os.environ.get("KDL_RECOMP", "1") == "1" else 0
         nb = len(self.blocks)
         self.recomp = [b.down_conv is None and i < nb - 1 and b.conv3.out_channels <= maxc
                        for i, b in enumerate(self.blocks)]
@@ -1113,7 +1118,7 @@ class ResNetEngine:
             if self.recomp[i]:
                 # c3 was never stored: BN3's backward apply folded into conv3's weights
                 w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
-                g2 = K.dgrad_folded(g, c2, st2, st3, w3)
+                g2 = K.dgrad_folded(g, c2, st2, st3, w3, self._wt(blk.conv3))
                 with self._on_side(g):
                     K.wgrad_folded(g, c2, st2, st3, w3, self._g(blk.conv3.weight))
             else:
