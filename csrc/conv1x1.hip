@@ -813,6 +813,9 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
       case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
       case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
     }
+    if constexpr (PRO == PRO_FWD && GATHER == G_DENSE && KBK == BK && BM == 64 && BN == 64) {  // (RSTATS A/B tile)
+      if (epi == EPI_RSTATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RSTATS, KBK>(p, s);
+    }
     if constexpr (PRO == PRO_FWD && GATHER == G_DENSE && KBK == BK && BM == 128 && MINB == 2) {  // recomputed conv3 + closing BN/residual/ReLU
       if (epi == EPI_APPLY) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_APPLY, KBK>(p, s);
       if constexpr (BN == 64)
@@ -962,9 +965,12 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (epi == EPI_APPLY && p.N % 128 == 0) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
   if (epi == EPI_APPLY) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
   // statistics-only forward conv (the recompute blocks' conv3): register sums
-  static const bool rstats = [] { const char* e = getenv("KDL_RSTATS"); return !e || e[0] != '0'; }();
-  if (epi == EPI_STATS && !p.C && pro == PRO_FWD && gather == G_DENSE && rstats)
+  // (KDL_RSTATS: 0 = the LDS epilogue with no store, 2 = 64 x 64 tiles at 3 blocks per CU)
+  static const int rstats = [] { const char* e = getenv("KDL_RSTATS"); return e ? atoi(e) : 1; }();
+  if (epi == EPI_STATS && !p.C && pro == PRO_FWD && gather == G_DENSE && rstats) {
+    if (rstats == 2) return dispatch_pg<64, 64, 3>(p, EPI_RSTATS, pro, gather, s);
     return dispatch_pg<128, 64, 2>(p, EPI_RSTATS, pro, gather, s);  // (128 x 128: 32 slots per lane spill)
+  }
   if (pro == PRO_BWD) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
     if (p.N % 128 == 0 && p.K <= bwd_kmax(128)) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
     if (p.K <= bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);

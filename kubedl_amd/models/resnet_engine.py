@@ -252,23 +252,32 @@ class HipKernels:
             t = self._dw32[key] = torch.empty(n, device=self.dev)
         return t
 
-    def wgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3, dW):
-        """conv3 weight gradient of a recompute block: diag(k) G + diag(c1) W3 Q
-        + c0 sum(a2)^T with G = g^T a2, Q = a2^T a2, a2 = relu(B2(c2)) (split-M
-        MFMA GEMMs into fp32, csrc/bnfold.hip combines)."""
-        n, N4, h, w = g.shape
-        C = w3.shape[1]
+    def fold_moments(self, c2, st2: BNState):
+        """Q = a2^T a2 (fp32 [C, C]) and sum(a2) of a recompute block, a2 =
+        relu(B2(c2)): forward-only values, issued on the side stream during the
+        forward (idle there) instead of in the backward's weight-gradient tail."""
+        n, C, h, w = c2.shape
         M = n * h * w
         pro = self.fcoef(st2)
-        dg = self._ws32(("fold_g", M, N4, C), self.ext.conv1x1_wgrad_splits(M, N4, C) * N4 * C)
-        self.ext.conv1x1_wgrad(g, c2, pro, dg, None, 1.0, M, N4, C, h, w, h, w, 1)
-        dq = self._ws32(("fold_q", M, C), self.ext.conv1x1_wgrad_splits(M, C, C) * C * C)
+        dq = torch.empty(self.ext.conv1x1_wgrad_splits(M, C, C) * C * C, device=c2.device)
         self.ext.wgrad_grelu_arm(pro)
         self.ext.conv1x1_wgrad(c2, c2, pro, dq, None, 1.0, M, C, C, h, w, h, w, 1)
         parts = self.ext.relu_colsum_parts(M)
-        part = self._ws32(("fold_s", M, C), parts * C)
+        part = torch.empty(parts * C, device=c2.device)
         self.ext.relu_colsum(c2, pro, C, part)
         self.ext.slab_reduce_f32(part, C, parts)
+        return dq, part
+
+    def wgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3, dW, moments):
+        """conv3 weight gradient of a recompute block: diag(k) G + diag(c1) W3 Q
+        + c0 sum(a2)^T with G = g^T a2 (split-M MFMA GEMM into fp32) and
+        ``moments`` = fold_moments(c2, st2); csrc/bnfold.hip combines."""
+        n, N4, h, w = g.shape
+        C = w3.shape[1]
+        M = n * h * w
+        dg = self._ws32(("fold_g", M, N4, C), self.ext.conv1x1_wgrad_splits(M, N4, C) * N4 * C)
+        self.ext.conv1x1_wgrad(g, c2, self.fcoef(st2), dg, None, 1.0, M, N4, C, h, w, h, w, 1)
+        dq, part = moments
         self.ext.bn_fold_wgrad(w3, self.bcoef(st3), dg, dq, part, 1, dW.view(N4, C))
 
     def bn_stats(self, x, st):
@@ -594,12 +603,15 @@ class TorchKernels:
         self._bsum(d, c2, st2)
         return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
 
-    def wgrad_folded(self, g, c2, st2, st3, w3, dW):
+    def fold_moments(self, c2, st2):
+        a2 = _rows(self._pro(c2, st2).contiguous(memory_format=torch.channels_last))  # [M, C]
+        return a2.t() @ a2, a2.sum(0)
+
+    def wgrad_folded(self, g, c2, st2, st3, w3, dW, moments):
         k, c1, c0 = st3.bcoef
         a2 = _rows(self._pro(c2, st2).contiguous(memory_format=torch.channels_last))  # [M, C]
         G = _rows(g.float()).t() @ a2                     # [N4, C]
-        Q = a2.t() @ a2                                   # [C, C]
-        asum = a2.sum(0)
+        Q, asum = moments                                 # a2^T a2 [C, C], sum(a2) [C]
         dw = k[:, None] * G + c1[:, None] * (w3.float() @ Q) + c0[:, None] * asum[None, :]
         dW.copy_(dw.view_as(dW))
 
@@ -970,6 +982,7 @@ class ResNetEngine:
                 self._refresh_wt()
                 self._wt_evt = torch.cuda.Event()
                 self._wt_evt.record(self.side)
+        self._moments = {}
         st0 = self.bn[m.bn1]
         c0, gemm_stats = K.stem_conv(x, m.conv1.weight, st0)
         x1, idx = K.stem_fwd(c0, st0, gemm_stats)
@@ -994,6 +1007,8 @@ class ResNetEngine:
                 K.bn_finalize(st2, n * ho * wo, x=c2)
             if self.recomp[bi]:  # conv3 never stored: statistics pass, then the applying GEMM
                 w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
+                with self._on_side(c2):  # conv3's weight-gradient moments, off the backward's tail
+                    self._moments[bi] = K.fold_moments(c2, st2)
                 K.conv1x1_stats(c2, w3, st2, st3)
                 K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
                 out, mbits = K.conv1x1_apply(c2, w3, st2, st3, cur)
@@ -1120,7 +1135,7 @@ class ResNetEngine:
                 w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
                 g2 = K.dgrad_folded(g, c2, st2, st3, w3, self._wt(blk.conv3))
                 with self._on_side(g):
-                    K.wgrad_folded(g, c2, st2, st3, w3, self._g(blk.conv3.weight))
+                    K.wgrad_folded(g, c2, st2, st3, w3, self._g(blk.conv3.weight), self._moments.pop(i))
             else:
                 if std_ is not None and self._fuse_mode(c3.shape[1]) == 0:
                     dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches

@@ -162,7 +162,7 @@ def test_folded_dgrad_and_wgrad_match_materialised_dc3(n, h, w, C):
     dWa = torch.empty(N4, C, device="cuda", dtype=torch.bfloat16)
     dWb = torch.empty_like(dWa)
     K.wgrad(dc3, c2, 1, sta, dWa)
-    K.wgrad_folded(g, c2, stb, st3, w3, dWb)
+    K.wgrad_folded(g, c2, stb, st3, w3, dWb, K.fold_moments(c2, stb))
     sums = []
     for s in (sta, stb):
         dg, db = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
