@@ -847,11 +847,14 @@ class ResNetEngine:
         # successor's RESBITS GEMM recomputes c3 tiles for BN3's backward sums,
         # and BN3's backward apply reaches conv3's data / weight gradients folded
         # into the weights.  KDL_RECOMP=0: off; KDL_RECOMP_MAXC: widest 4C served.
-        # Measured per block (single-stream rocprofv3, profiles/r03_recompute_*): at the 56x56
-        # stage (4C = 256) forward conv3 + BN3 apply 400 -> 297 us and conv3 dgrad 275 -> 160 us,
-        # against +50 us in the successor's RESBITS; at 28x28 the recomputing RESBITS (+80-150 us)
-        # outweighs the rest -- so 4C <= 256 by default.
-        maxc = min(512, int(os.environ.get("KDL_RECOMP_MAXC", "256"))) if os.environ.get("KDL_RECOMP", "1") == "1" else 0
+        # Measured (profiles/r03_step_1stream_*.txt, docs/perf_notes.md): at the 56x56 stage
+        # (4C = 256) forward conv3 + BN3 apply 400 -> 290 us and conv3 dgrad 275 -> 160 us
+        # per block against +50-100 us in the successor's RESBITS, the main stream 0.47 ms
+        # shorter per step -- but the folded weight gradient lengthens the side stream's
+        # tail, and the job-path step measured 13,216-13,227 (on) vs 13,233-13,264 img/s
+        # (off); at 28x28 the recomputing RESBITS (+80-150 us) outweighs the rest.  Opt-in:
+        # KDL_RECOMP=1 (4C <= KDL_RECOMP_MAXC, default 256).
+        maxc = min(512, int(os.environ.get("KDL_RECOMP_MAXC", "256"))) if os.environ.get("KDL_RECOMP", "0") == "1" else 0
         nb = len(self.blocks)
         self.recomp = [b.down_conv is None and i < nb - 1 and b.conv3.out_channels <= maxc
                        for i, b in enumerate(self.blocks)]
