@@ -358,7 +358,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   };
 
-  Epilogue<BM, BN, kThreads, EPI, G_DENSE, PRO == PRO_RECOMP> epi;
+  Epilogue<BM, BN, kThreads, EPI, G_DENSE, PRO == PRO_RECOMP, PRO == PRO_SEG> epi;
   epi.init(t, n0);
   // RSTATS: each lane's running shifted sums of its accumulator slots -- slot
   // (i, r) is output channel n0 + wn0 + 32 i + (r & 3) + 8 (r >> 2) + 4 fh for

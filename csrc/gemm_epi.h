@@ -202,7 +202,10 @@ __device__ __forceinline__ void acc_to_lds(const f32x16_t (&acc)[TN][TM], bf16_t
       }
 }
 
-template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE, bool XL = false>
+// BIAS: MASKX adds GemmParams::ebias before the mask (compile-time: the runtime
+// check alone cost the 256x256 implicit-GEMM MASKX tile 44 more bytes of spill,
+// and spilling LDS-DMA variants computed wrong rows -- docs/perf_notes.md)
+template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE, bool XL = false, bool BIAS = false>
 struct Epilogue {
   static constexpr int LDC = BN + 8;
   static constexpr int CPR = BN / 8;           // 16-B chunks per output row
@@ -315,7 +318,7 @@ struct Epilogue {
         em[q] = ld2(p.emean, ch0 + 2 * q);
         ea[q] = ld2(p.ecoef, ch0 + 2 * q);
         eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
-        if (p.ebias) em2[q] = ld2(p.ebias, ch0 + 2 * q);  // (em2 is free in MASKX)
+        if constexpr (BIAS) em2[q] = ld2(p.ebias, ch0 + 2 * q);  // (em2 is free in MASKX)
       }
     } else if constexpr (EPI == EPI_APPLY) {
 #pragma unroll
@@ -374,7 +377,7 @@ struct Epilogue {
           } else if constexpr (EPI == EPI_MASKX) {
             f2_t x[4];
             unpack4x2(xin, x);
-            if (p.ebias) {
+            if constexpr (BIAS) {
 #pragma unroll
               for (int q = 0; q < 4; ++q) v[q] += em2[q];
             }

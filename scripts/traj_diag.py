@@ -1,6 +1,8 @@
 """Multi-step engine run reporting, per step, the parameters whose gradient or
 master weight is non-finite / huge (first offenders by flat order).
-usage: traj_diag.py [steps] [batch]   (env: KDL_RECOMP, KDL_WGRAD_STREAM, ...)"""
+usage: traj_diag.py [steps] [batch] [autograd_first]   (env: KDL_RECOMP, KDL_WGRAD_STREAM, ...)
+autograd_first = 1: run the autograd trainer for ``steps`` first in the same
+process (as tests/test_trajectory_gpu.py's truth fixture does)"""
 import json
 import sys
 
@@ -14,6 +16,10 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     info = DistInfo(0, 1, 0, torch.device("cuda", 0), "nccl")
+    if len(sys.argv) > 3 and sys.argv[3] == "1":
+        ag = ResNetTrainer(info, batch=batch, image=224, engine="autograd", bn_backend="auto", seed=5)
+        print(json.dumps({"autograd": [float(ag.step()) for _ in range(steps)]}), flush=True)
+        del ag
     tr = ResNetTrainer(info, batch=batch, image=224, engine="fused", bn_backend="auto", seed=5)
     sp = tr.space
     for s in range(steps):
