@@ -857,6 +857,9 @@ class ResNetEngine:
         nb = len(self.blocks)
         self.recomp = [b.down_conv is None and i < nb - 1 and b.conv3.out_channels <= maxc
                        for i, b in enumerate(self.blocks)]
+        # downsample branch conv of the forward on the side stream (KDL_FWD_DOWN_SIDE=0: in
+        # line): 13,333-13,347 vs 13,252-13,279 img/s, profiles/r03b_fwd_down_side_ab.txt
+        self.down_side = os.environ.get("KDL_FWD_DOWN_SIDE", "1") == "1"
         self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "1"))
         self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "512"))
         self.fuse_bn1 = os.environ.get("KDL_BN_BWD_FUSE_BN1", "0") == "1"
@@ -993,6 +996,22 @@ class ResNetEngine:
             s = blk.conv2.stride[0]
             st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
             n, _, h, w = cur.shape
+            down_evt = None
+            if blk.down_conv is not None and self.down_side and self.side is not None:
+                # the downsample branch needs only the block input: on the side stream
+                # (idle in the forward but for the weight transposes), concurrent with
+                # conv1 -> conv2 -> conv3; the BN-apply that joins the branches waits on it
+                std_ = self.bn[blk.down_bn]
+                main = torch.cuda.current_stream(self.dev)
+                with self._on_side(cur):
+                    hd = (h - 1) // blk.down_conv.stride[0] + 1
+                    wd_ = (w - 1) // blk.down_conv.stride[0] + 1
+                    cd = K.conv1x1_fwd(cur, blk.down_conv.weight.view(blk.down_conv.out_channels, -1),
+                                       blk.down_conv.stride[0], None, std_)
+                    K.bn_finalize(std_, n * hd * wd_, gemm_shift=True)
+                    down_evt = torch.cuda.Event()
+                    down_evt.record(self.side)
+                cd.record_stream(main)
             c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
             a1, _ = K.bn_apply(c1, st1, relu=True)
@@ -1016,14 +1035,18 @@ class ResNetEngine:
                 continue
             c3 = K.conv1x1_fwd(c2, blk.conv3.weight.view(blk.conv3.out_channels, -1), 1, st2, st3)
             K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
-            cd = None
-            if blk.down_conv is not None:
+            if down_evt is not None:
+                torch.cuda.current_stream(self.dev).wait_event(down_evt)
+                out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
+            elif blk.down_conv is not None:
                 std_ = self.bn[blk.down_bn]
                 cd = K.conv1x1_fwd(cur, blk.down_conv.weight.view(blk.down_conv.out_channels, -1),
                                    blk.down_conv.stride[0], None, std_)
                 K.bn_finalize(std_, n * ho * wo, gemm_shift=True)
                 out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
             else:
+                cd = None
+            if blk.down_conv is None:
                 out, mbits = K.bn_apply(c3, st3, relu=True, res=cur, want_mask=True)
             saved.append((cur, c1, a1, c2, c3, cd, mbits))
             cur = out
