@@ -992,13 +992,34 @@ int64_t conv1x1_wgrad_splits(int64_t M, int64_t N, int64_t K) {
 //   epi 0 PLAIN, 1 STATS (shift = rm, acc = fwd replicas), 2 MASKX (dgrad:
 //   ex = that BN's input [M, Cout], emean, ecoef).  pro_coef [2Cin] applies
 //   relu(x*scale + shift) to in-image taps; padding taps are zero.
+// conv3x3_aout_arm(a): the next conv3x3_gemm with a BN + ReLU prologue also
+// writes relu(B(x)) into ``a`` (the 56x56 halo kernel; elsewhere it fails)
+thread_local void* g_aout_arm = nullptr;
+thread_local int64_t g_aout_n = 0;
+void conv3x3_aout_arm(const c10::optional<at::Tensor>& a) {
+  if (a) {
+    TORCH_CHECK(a->is_cuda() && a->scalar_type() == at::kBFloat16, "conv3x3_aout_arm: bf16 GPU tensor");
+    g_aout_arm = a->data_ptr();
+    g_aout_n = a->numel();
+  } else {
+    g_aout_arm = nullptr;
+    g_aout_n = 0;
+  }
+}
+
 void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_t Nb, int64_t H, int64_t Wd,
                   int64_t Cin, int64_t Cout, int64_t stride, const c10::optional<at::Tensor>& pro_coef, int64_t epi,
                   const c10::optional<at::Tensor>& shift, const c10::optional<at::Tensor>& acc,
                   const c10::optional<at::Tensor>& ex, const c10::optional<at::Tensor>& emean,
                   const c10::optional<at::Tensor>& ecoef) {
   const FinArm fin = take_fin_arm();
+  void* aout = g_aout_arm;
+  const int64_t aout_n = g_aout_n;
+  g_aout_arm = nullptr;
+  g_aout_n = 0;
   TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && Nb > 0 && stride >= 1, "conv3x3_gemm: need Cin, Cout % 64 == 0");
+  TORCH_CHECK(!aout || (opt_ptr(pro_coef) && epi == 1 && stride == 1 && aout_n == Nb * H * Wd * Cin),
+              "conv3x3_gemm: the write-through needs the prologue, STATS, stride 1 and an [N, H, W, Cin] tensor");
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 2, "conv3x3_gemm: epilogue must be PLAIN, STATS or MASKX");
   TORCH_CHECK(!(epi == 2 && opt_ptr(pro_coef)), "conv3x3_gemm: MASKX runs without a prologue");
   const int64_t Ho = (H - 1) / stride + 1, Wo = (Wd - 1) / stride + 1;
@@ -1025,6 +1046,7 @@ void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_
   a.shift = opt_fptr(shift); a.acc = opt_fptr(acc);
   a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
   a.res_stride = 1;
+  a.aout = aout;
   apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv3x3_gemm");
 }
@@ -1505,6 +1527,7 @@ PYBIND11_MODULE(_C, m) {
         "fp32 slab count of stem7x7_wgrad's workspace");
   m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");
   m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
+  m.def("conv3x3_aout_arm", &conv3x3_aout_arm, "next prologue conv3x3_gemm also writes relu(B(x)) here (56x56 halo)");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 pad-1 conv weight gradient (implicit GEMM, split-M slabs)");

@@ -942,6 +942,13 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   }
   // long K without an A prologue: the LDS-DMA main loop (csrc/igemm.hip)
   const int core = gemm_core_mode();
+  // 56x56 3x3 forward with the BN + ReLU prologue: the halo kernel applies it in LDS
+  if (pro == PRO_FWD && gather == G_CONV3 && core != 0 && p.K % 64 == 0) {
+    p.a_rows = static_cast<int64_t>(p.M / (a.Hout * a.Wout)) * a.Hin * a.Win;
+    const hipError_t h = halo3x3(p, epi, s);
+    if (h != hipErrorInvalidValue) return h;
+    if (p.aout) return hipErrorInvalidValue;  // the write-through of relu(B(x)) is the halo kernel's only
+  }
   const int min_k = gather == G_CONV3 ? 0 : 512;
   // (the backward-apply prologue transforms A in registers: register-staged loop)
   if (!pro && core != 0 && (core == 1 || p.K >= min_k) && p.K % 64 == 0) {
@@ -1194,9 +1201,9 @@ hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, fl
                          void* dW, float scale, int Nb, int Hin, int Win, int Cin, int Cout, int stride,
                          hipStream_t s) {
   if (Cin % 64 || Cout % 64 || Nb <= 0 || stride < 1) return hipErrorInvalidValue;
-  if (!pro_coef && gemm_core_mode() != 0) {  // 56x56 stage: input halo staged once per tile (csrc/halo3x3.hip)
+  if (gemm_core_mode() != 0) {  // 56x56 stage: input halo staged once per tile (csrc/halo3x3.hip)
     int nslabs = 0;
-    const hipError_t e = halo3x3_wgrad(G, A, dw32, dw32_floats, Nb, Hin, Win, Cin, Cout, stride, &nslabs, s);
+    const hipError_t e = halo3x3_wgrad(G, A, pro_coef, dw32, dw32_floats, Nb, Hin, Win, Cin, Cout, stride, &nslabs, s);
     if (e == hipSuccess)
       return wgrad_reduce(dw32, static_cast<int64_t>(Cout) * 9 * Cin, nslabs, scale, static_cast<bf16_t*>(dW), s);
     if (e != hipErrorInvalidValue) return e;

@@ -143,10 +143,11 @@ bool tickets_enabled();
 // csrc/halo3x3.hip: 3x3 stride-1 conv with an LDS-resident input halo (Cin 64 @ 56x56);
 // hipErrorInvalidValue when the geometry is not one it serves
 hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s);
-// its weight gradient (no prologue) into one fp32 [64][576] slab per block (*nslabs)
+// its weight gradient (optional BN + ReLU prologue on A: pro = [scale | shift])
+// into one fp32 [64][576] slab per block (*nslabs)
 int halo3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride);
-hipError_t halo3x3_wgrad(const void* G, const void* A, float* dw32, int64_t dw32_floats, int Nb, int Hin, int Win,
-                         int Cin, int Cout, int stride, int* nslabs, hipStream_t s);
+hipError_t halo3x3_wgrad(const void* G, const void* A, const float* pro, float* dw32, int64_t dw32_floats, int Nb,
+                         int Hin, int Win, int Cin, int Cout, int stride, int* nslabs, hipStream_t s);
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 

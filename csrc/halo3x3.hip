@@ -73,7 +73,11 @@ __device__ __forceinline__ void dma16(i32x4_t r, lds_void_t* dst, uint32_t voff)
 #endif
 }
 
-template <int CIN, int BN, int TH, bool DOUBLE, int EPI>
+// PRO: the previous layer's BN + ReLU, relu(x * scale + shift) with
+// p.pro_coef = [scale | shift] per input channel, applied to the halo in LDS
+// once it has landed (each lane transforms the 16-B chunks it DMA'd; padding
+// pixels stay zero), so the activation a = relu(B(x)) is never written to HBM
+template <int CIN, int BN, int TH, bool DOUBLE, int EPI, bool PRO = false>
 __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, int W, int tiles_m, int tiles_n) {
   constexpr int RP = CIN / 64;             // 128-B LDS rows per pixel
   constexpr int TN = BN / 32;              // 32-wide MFMA column blocks per wave
@@ -136,6 +140,60 @@ __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, in
     hcol[i] = hp - hr * WP - 1;
     hsub[i] = (kc * 64 + 8 * c) * 2;
   }
+  // PRO: this lane's chunk of slot i covers channels hsub[i] / 2 .. + 7; the
+  // chunk alternates between two channel groups with the slot parity (R's
+  // swizzle term (R >> 1) & 7 = (4 wave + 4 i + (lane >> 4)) & 7), so two
+  // coefficient sets are held in registers (no loads inside the DMA pipeline)
+  static_assert(!PRO || CIN == 64, "halo prologue: one 128-B row per pixel");
+  float psc[PRO ? 2 : 1][8], psf[PRO ? 2 : 1][8];
+  (void)psc; (void)psf;
+  if constexpr (PRO) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c0 = 8 * ((lane & 7) ^ ((4 * wave + 4 * e + (lane >> 4)) & 7));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        psc[e][j] = p.pro_coef[c0 + j];
+        psf[e][j] = p.pro_coef[CIN + c0 + j];
+      }
+    }
+  }
+  auto halo_ok = [&](int tm, int i) {
+    const int tpi = H / TH;
+    const int img = tm / tpi, r0 = (tm - img * tpi) * TH;
+    (void)img;
+    const int ih = r0 + hrow[i], iw = hcol[i];
+    return static_cast<unsigned>(ih) < static_cast<unsigned>(H) && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+  };
+  // relu(x * scale + shift) on this lane's in-image chunks of halo buffer ``b``;
+  // with p.aout the tile's own pixels (the halo's interior rows) are written
+  // through: every pixel of the image is interior to exactly one tile, so the
+  // activation is stored once, as the apply pass would have
+  auto transform_halo = [&](int tm, int b) {
+    char* base = Hs + b * HALO_BYTES;
+    const int tpi = H / TH;
+    const int img = tm / tpi, r0 = (tm - img * tpi) * TH;
+#pragma unroll
+    for (int i = 0; i < HIPW; ++i) {
+      const int g = wave + i * kWaves;
+      if (g < HI && halo_ok(tm, i)) {
+        uint4* q = reinterpret_cast<uint4*>(base + g * 1024 + 16 * lane);
+        float f[8];
+        unpack8(*q, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = fmaf(f[j], psc[i & 1][j], psf[i & 1][j]);
+          f[j] = o > 0.f ? o : 0.f;
+        }
+        const uint4 v = pack8(f);
+        *q = v;
+        if (p.aout && static_cast<unsigned>(hrow[i]) < static_cast<unsigned>(TH)) {
+          const int64_t px = (static_cast<int64_t>(img) * H + r0 + hrow[i]) * W + hcol[i];
+          *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p.aout) + px * (CIN * 2) + hsub[i]) = v;
+        }
+      }
+    }
+  };
   auto issue_halo = [&](int tm, int buf) {
     const int tpi = H / TH;
     const int img = tm / tpi, r0 = (tm - img * tpi) * TH;
@@ -207,6 +265,14 @@ __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (PRO) {
+      // the landed halo -> relu(B(x)) in place; raw barrier (a __syncthreads
+      // fence would drain the next halo's DMA, vmcnt(0))
+      transform_halo(tm, buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
 
     const char* Hb = Hs + buf * HALO_BYTES;
     f32x16_t acc[TN][1];
@@ -266,6 +332,7 @@ __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, in
 
 template <int CIN, int BN, int TH, bool DOUBLE>
 hipError_t launch(const GemmParams& p, int epi, int H, int W, hipStream_t s) {
+  if (p.pro_coef && epi != EPI_STATS) return hipErrorInvalidValue;  // the forward conv's prologue only
   const int tiles_m = p.M / kBM;
   const int tiles_n = p.N / BN;
   int per_n = 256 / tiles_n;  // one resident block per CU, each pinned to one N tile
@@ -279,7 +346,11 @@ hipError_t launch(const GemmParams& p, int epi, int H, int W, hipStream_t s) {
       hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_PLAIN>), grid, block, 0, s, q, H, W, tiles_m, tiles_n);
       break;
     case EPI_STATS:
-      hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_STATS>), grid, block, 0, s, q, H, W, tiles_m, tiles_n);
+      if (p.pro_coef)
+        hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_STATS, true>), grid, block, 0, s, q, H, W, tiles_m,
+                           tiles_n);
+      else
+        hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_STATS>), grid, block, 0, s, q, H, W, tiles_m, tiles_n);
       break;
     case EPI_MASKX:
       hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_MASKX>), grid, block, 0, s, q, H, W, tiles_m, tiles_n);
@@ -292,6 +363,10 @@ hipError_t launch(const GemmParams& p, int epi, int H, int W, hipStream_t s) {
 
 int g_halo = [] {  // KDL_HALO=0 keeps every 3x3 on the implicit GEMM
   const char* e = getenv("KDL_HALO");
+  return e ? atoi(e) : 1;
+}();
+int g_halo_pro = [] {  // KDL_HALO_PRO=0: no BN + ReLU prologue on the halo kernels
+  const char* e = getenv("KDL_HALO_PRO");
   return e ? atoi(e) : 1;
 }();
 
@@ -338,8 +413,12 @@ __device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
 
 __device__ __forceinline__ int trswz(int R) { return ((R >> 1) & 1) * 4; }
 
+// PRO: A is the BN input x and the operand is relu(x * pro[c] + pro[64 + c]),
+// applied to the landed halo in LDS (padding pixels stay zero) -- the forward's
+// activation is never materialised
+template <bool PRO>
 __global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G, const bf16_t* A, float* dw32,
-                                                                  int nimg, int tiles, int per) {
+                                                                  int nimg, int tiles, int per, const float* pro) {
   constexpr int H = 56, W = 56, WP = 58, TPI = H / 4;
   __shared__ __attribute__((aligned(1024))) char lds[2 * kWgStage];
   const int t = threadIdx.x, lane = t & 63;
@@ -388,6 +467,46 @@ __global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G
 #pragma unroll
   for (int i = 0; i < 9; ++i) acc[i] = f32x16_t{};
 
+  // PRO: a halo slot's chunk is logical chunk (lane & 7) ^ trswz(R) with
+  // trswz(R) = ((lane >> 4) & 1) * 4 for every halo row R = 8 g - 224 + (lane >> 3):
+  // one channel group per lane, its 8 scales / shifts held in registers
+  float psc[PRO ? 8 : 1], psf[PRO ? 8 : 1];
+  (void)psc; (void)psf;
+  if constexpr (PRO) {
+    const int c0 = 8 * ((lane & 7) ^ (((lane >> 4) & 1) * 4));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      psc[j] = pro[c0 + j];
+      psf[j] = pro[64 + c0 + j];
+    }
+  }
+  auto transform = [&](int tile, int b) {
+    const int img = tile / TPI, r0 = (tile - img * TPI) * 4;
+    char* base = lds + b * kWgStage;
+#pragma unroll
+    for (int i = 0; i < kWgIPW; ++i) {
+      const int g = wave + i * kWgWaves;
+      if (8 * g >= kWgDyRows) {
+        const int R = 8 * g - kWgDyRows + (lane >> 3);
+        const int hr = R / WP;
+        const int ih = r0 + hr - 1, iw = R - hr * WP - 1;
+        const bool ok = R < 6 * WP && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+        if (ok) {
+          uint4* q = reinterpret_cast<uint4*>(base + g * 1024 + 16 * lane);
+          float f[8];
+          unpack8(*q, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float o = fmaf(f[j], psc[j], psf[j]);
+            f[j] = o > 0.f ? o : 0.f;
+          }
+          *q = pack8(f);
+        }
+      }
+    }
+  };
+
   int buf = 0;
   if (tb < te) issue(tb, 0);
   for (int tile = tb; tile < te; ++tile) {
@@ -403,6 +522,12 @@ __global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G
     }
     __builtin_amdgcn_s_barrier();  // ... on every wave
     asm volatile("" ::: "memory");
+    if constexpr (PRO) {  // landed halo -> relu(B(x)) in place, then published (raw barrier: next DMA in flight)
+      transform(tile, buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     const char* Dy = lds + buf * kWgStage;
     const char* Hs = Dy + kWgDyRows * 128;
 #pragma unroll 1
@@ -468,11 +593,11 @@ int wg_blocks(int tiles, int* per) {
 void set_halo3x3(int on) { g_halo = on; }
 
 namespace gemm {
-// 3x3 / stride 1 / pad 1 / dense A (no prologue) on the halo kernel when the
-// geometry is one it serves (56x56, Cin 64); hipErrorInvalidValue = "not
-// here, use igemm".
+// 3x3 / stride 1 / pad 1 on the halo kernel when the geometry is one it
+// serves (56x56, Cin 64; the forward may carry the BN + ReLU prologue);
+// hipErrorInvalidValue = "not here, use igemm / the register-staged loop".
 hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s) {
-  if (!g_halo || p.stride != 1 || p.pro_coef != nullptr) return hipErrorInvalidValue;
+  if (!g_halo || p.stride != 1 || (p.pro_coef != nullptr && !g_halo_pro)) return hipErrorInvalidValue;
   const int H = p.Hin, W = p.Win;
   if (p.Hout != H || p.Wout != W || p.M % (H * W) || p.K != 9 * p.Cin) return hipErrorInvalidValue;
   if (static_cast<int64_t>(p.a_rows) * p.Cin * 2 >= (int64_t(1) << 31)) return hipErrorInvalidValue;
@@ -487,17 +612,23 @@ int halo3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride)
   return wg_blocks(Nb * 14, &per);
 }
 
-// dw32: >= halo3x3_wgrad_slabs(...) x 64 x 576 fp32; hipErrorInvalidValue = "not here"
-hipError_t halo3x3_wgrad(const void* G, const void* A, float* dw32, int64_t dw32_floats, int Nb, int Hin, int Win,
-                         int Cin, int Cout, int stride, int* nslabs, hipStream_t s) {
+// dw32: >= halo3x3_wgrad_slabs(...) x 64 x 576 fp32; hipErrorInvalidValue = "not here";
+// pro (optional): [scale | shift] of the BN + ReLU between A and the conv
+hipError_t halo3x3_wgrad(const void* G, const void* A, const float* pro, float* dw32, int64_t dw32_floats, int Nb,
+                         int Hin, int Win, int Cin, int Cout, int stride, int* nslabs, hipStream_t s) {
+  if (pro && !g_halo_pro) return hipErrorInvalidValue;
   const int n = halo3x3_wgrad_slabs(Nb, Hin, Win, Cin, Cout, stride);
   if (n == 0 || dw32_floats < static_cast<int64_t>(n) * 64 * 576) return hipErrorInvalidValue;
   if (static_cast<int64_t>(Nb) * 56 * 56 * 128 >= (int64_t(1) << 32)) return hipErrorInvalidValue;
   const int tiles = Nb * 14;
   int per;
   const int grid = wg_blocks(tiles, &per);
-  hipLaunchKernelGGL(halo3x3_wgrad_kernel, dim3(grid), dim3(kWgNT), 0, s, static_cast<const bf16_t*>(G),
-                     static_cast<const bf16_t*>(A), dw32, Nb, tiles, per);
+  if (pro)
+    hipLaunchKernelGGL(halo3x3_wgrad_kernel<true>, dim3(grid), dim3(kWgNT), 0, s, static_cast<const bf16_t*>(G),
+                       static_cast<const bf16_t*>(A), dw32, Nb, tiles, per, pro);
+  else
+    hipLaunchKernelGGL(halo3x3_wgrad_kernel<false>, dim3(grid), dim3(kWgNT), 0, s, static_cast<const bf16_t*>(G),
+                       static_cast<const bf16_t*>(A), dw32, Nb, tiles, per, pro);
   *nslabs = grid;
   return hipGetLastError();
 }

@@ -10,7 +10,7 @@ GEMMs of ``csrc/conv1x1.hip``:
 forward, per bottleneck (``B`` = BatchNorm, ``R`` = ReLU)::
 
     c1 = conv1(x)                [GEMM, epilogue: B1 statistics]
-    a1 = R(B1(c1))               [apply pass]
+    a1 = R(B1(c1))               [apply pass; at 56x56 inside conv2 (halo prologue)]
     c2 = conv2(a1)               [3x3 implicit GEMM (csrc/igemm.hip), epilogue: B2 stats]
     c3 = conv3(R(B2(c2)))        [GEMM, prologue: B2+R while staging A -- the
                                   B2 output never reaches HBM; epilogue: B3 stats]
@@ -185,16 +185,20 @@ class HipKernels:
                               self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
         return y
 
-    def conv3x3_fwd(self, x, w, stride, out: BNState):
+    def conv3x3_fwd(self, x, w, stride, out: BNState, pro: BNState | None = None, aout=None):
         """3x3 pad-1 conv as an implicit GEMM (LDS-DMA main loop, csrc/igemm.hip)
-        with ``out``'s BN statistics in the epilogue (no separate stats pass)."""
+        with ``out``'s BN statistics in the epilogue (no separate stats pass);
+        ``pro``: the input is relu(B_pro(x)), applied inside the conv (at 56x56 to
+        the input halo in LDS, csrc/halo3x3.hip), written through to ``aout``."""
         n, cin, h, wd = x.shape
         cout = w.shape[0]
         ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
         y = _nhwc_empty(n, cout, ho, wo, x)
         self._arm(out, n * ho * wo)
-        self.ext.conv3x3_gemm(x, w, y, n, h, wd, cin, cout, stride, None, 1, out.mod.running_mean,
-                              self._fwd_acc(out), None, None, None)
+        if aout is not None:
+            self.ext.conv3x3_aout_arm(aout)
+        self.ext.conv3x3_gemm(x, w, y, n, h, wd, cin, cout, stride, self.fcoef(pro) if pro is not None else None, 1,
+                              out.mod.running_mean, self._fwd_acc(out), None, None, None)
         return y
 
     def conv1x1_stats(self, x, w, pro: BNState, out: BNState):
@@ -466,10 +470,11 @@ class HipKernels:
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
                                M, cout, cin, ho, wo, h, w, stride)
 
-    def wgrad3x3(self, g, x, stride, dW):
+    def wgrad3x3(self, g, x, stride, dW, pro: BNState | None = None):
         """3x3 pad-1 weight gradient straight into ``dW`` (channels_last = OHWI):
         the 56x56 stage's input halo kernel (csrc/halo3x3.hip) or the LDS-DMA
-        implicit GEMM (csrc/wgrad_dma.hip), into fp32 slabs + fixed-order reduce."""
+        implicit GEMM (csrc/wgrad_dma.hip), into fp32 slabs + fixed-order reduce;
+        ``pro``: the conv input is relu(B_pro(x)), applied while staging."""
         n, cout, ho, wo = g.shape
         _, cin, h, w = x.shape
         M = n * ho * wo
@@ -478,7 +483,8 @@ class HipKernels:
         dw32 = self._dw32.get(key)
         if dw32 is None or dw32.numel() < need:
             dw32 = self._dw32[key] = torch.empty(need, device=g.device)
-        self.ext.conv3x3_wgrad(g, x, None, dw32, dW, 1.0, n, h, w, cin, cout, stride)
+        self.ext.conv3x3_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW, 1.0, n, h, w, cin, cout,
+                               stride)
 
     def stem_wgrad(self, dc0, x, dw):
         """Stem conv weight gradient into ``dw`` ([64, 3, 7, 7]): csrc/stem.hip
@@ -561,8 +567,11 @@ class TorchKernels:
         self._stats(y, out, out.mod.running_mean.clone())
         return y.contiguous(memory_format=torch.channels_last)
 
-    def conv3x3_fwd(self, x, w, stride, out):
-        y = F.conv2d(x.float(), w.float(), stride=stride, padding=1).to(x.dtype)
+    def conv3x3_fwd(self, x, w, stride, out, pro=None, aout=None):
+        a = self._pro(x, pro) if pro is not None else x.float()
+        if aout is not None:
+            aout.copy_(a)
+        y = F.conv2d(a, w.float(), stride=stride, padding=1).to(x.dtype)
         self._stats(y, out, out.mod.running_mean.clone())
         return y.contiguous(memory_format=torch.channels_last)
 
@@ -764,8 +773,9 @@ class TorchKernels:
         a = _rows(a[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last))
         dW.copy_((_rows(g.float()).t() @ a).view_as(dW))
 
-    def wgrad3x3(self, g, x, stride, dW):
-        dW.copy_(torch.nn.grad.conv2d_weight(x.float(), tuple(dW.shape), g.float(), stride=stride, padding=1))
+    def wgrad3x3(self, g, x, stride, dW, pro=None):
+        a = self._pro(x, pro) if pro is not None else x.float()
+        dW.copy_(torch.nn.grad.conv2d_weight(a, tuple(dW.shape), g.float(), stride=stride, padding=1))
 
     def stem_backward(self, dp, idx, c0, x, st, dgamma, dbeta, dw):
         self.stem_wgrad(self.stem_bwd(dp, idx, c0, st, dgamma, dbeta), x, dw)
@@ -860,6 +870,12 @@ class ResNetEngine:
         # downsample branch conv of the forward on the side stream (KDL_FWD_DOWN_SIDE=0: in
         # line): 13,333-13,347 vs 13,252-13,279 img/s, profiles/r03b_fwd_down_side_ab.txt
         self.down_side = os.environ.get("KDL_FWD_DOWN_SIDE", "1") == "1"
+        # bn1 + ReLU of the stride-1 56x56 3x3 convs applied inside the halo kernels,
+        # which stage the input halo in LDS and transform it there (KDL_HALO_PRO):
+        # 1 = the forward conv does, writing a1 = relu(B1(c1)) through for the weight
+        # gradient (no apply pass); 2 = the weight gradient transforms its halo too
+        # (a1 never written); 0 = apply pass
+        self.halo_pro = int(os.environ.get("KDL_HALO_PRO", "1")) if os.environ.get("KDL_HALO", "1") != "0" else 0
         self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "1"))
         self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "512"))
         self.fuse_bn1 = os.environ.get("KDL_BN_BWD_FUSE_BN1", "0") == "1"
@@ -1014,13 +1030,21 @@ class ResNetEngine:
                 cd.record_stream(main)
             c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
-            a1, _ = K.bn_apply(c1, st1, relu=True)
-            if self.conv3_native:
+            if self.conv3_native and self._halo_pro_ok(c1, s):
+                # the conv applies B1 + ReLU to its input halo (csrc/halo3x3.hip) and
+                # writes a1 through (mode 1) or a1 is never stored (mode 2)
+                a1 = torch.empty_like(c1) if self.halo_pro == 1 else None
+                c2 = K.conv3x3_fwd(c1, blk.conv2.weight, s, st2, pro=st1, aout=a1)
+                ho, wo = c2.shape[-2:]
+                K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
+            elif self.conv3_native:
+                a1, _ = K.bn_apply(c1, st1, relu=True)
                 # implicit GEMM + B2 statistics in the epilogue (shift = running mean)
                 c2 = K.conv3x3_fwd(a1, blk.conv2.weight, s, st2)
                 ho, wo = c2.shape[-2:]
                 K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
             else:
+                a1, _ = K.bn_apply(c1, st1, relu=True)
                 c2 = F.conv2d(a1, blk.conv2.weight, stride=s, padding=1).contiguous(memory_format=torch.channels_last)
                 ho, wo = c2.shape[-2:]
                 K.bn_stats(c2, st2)
@@ -1080,11 +1104,18 @@ class ResNetEngine:
             return wt
         return conv.weight.view(conv.out_channels, -1).t().contiguous()
 
-    def _wgrad3x3(self, g, a, stride, weight):
+    def _halo_pro_ok(self, c1, stride) -> bool:
+        """B1 + ReLU inside conv2 (forward and weight gradient): the stride-1
+        56x56 / 64-channel geometry of the halo kernels (csrc/halo3x3.hip), HIP path."""
+        n, c, h, w = c1.shape
+        return self.halo_pro > 0 and self.K.name == "hip" and stride == 1 and c == 64 and h == 56 and w == 56
+
+    def _wgrad3x3(self, g, a, stride, weight, pro=None):
         """conv2's weight gradient: the implicit-GEMM kernel writing straight into
-        the gradient buffer, or (KDL_CONV3=miopen) MIOpen + a copy."""
+        the gradient buffer, or (KDL_CONV3=miopen) MIOpen + a copy; ``pro``: ``a``
+        is the BN input and the operand relu(B_pro(a)) (halo kernel prologue)."""
         if self.conv3_native:
-            self.K.wgrad3x3(g, a, stride, self._g(weight))
+            self.K.wgrad3x3(g, a, stride, self._g(weight), pro=pro)
         else:
             _, dw, _ = torch.ops.aten.convolution_backward(
                 g, a, weight, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
@@ -1181,7 +1212,10 @@ class ResNetEngine:
             s = blk.conv2.stride[0]
             if s == 1:
                 with self._on_side(dc2):
-                    self._wgrad3x3(dc2, a1, 1, blk.conv2.weight)
+                    if a1 is None:  # a1 never stored: the halo weight gradient applies B1 + ReLU to c1
+                        self._wgrad3x3(dc2, c1, 1, blk.conv2.weight, pro=st1)
+                    else:
+                        self._wgrad3x3(dc2, a1, 1, blk.conv2.weight)
                 self.on_ready(blk.conv2.weight)
                 g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
