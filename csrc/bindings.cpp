@@ -738,6 +738,8 @@ struct BwdArm {
   const float* coef = nullptr;
   void* out = nullptr;
   int64_t C = 0, rows = 0;
+  int res = 0;              // 1: forward residual-apply prologue (bn_res_pro_arm)
+  uint8_t* bits = nullptr;  // its packed ReLU mask out
 };
 thread_local BwdArm g_bwd_arm;
 
@@ -756,6 +758,30 @@ void bn_bwd_pro_arm(const at::Tensor& x, const at::Tensor& ws, int64_t C, const 
   }
   g_bwd_arm.C = C;
   g_bwd_arm.rows = x.numel() / C;
+}
+
+// The next conv1x1_gemm (forward, STATS) applies the previous block's closing
+// BN + residual + ReLU to its A = that block's conv3 output:
+// A' = relu(A * coef[k] + coef[K + k] + res), written through to ``out`` with
+// its packed ReLU mask in ``bits`` [M, K / 8] -- bit-identical to
+// bn_stage_fwd_apply(A, ws, res, ..., out, bits) (csrc/conv1x1.hip PRO_RES).
+void bn_res_pro_arm(const at::Tensor& res, const at::Tensor& coef, int64_t C, const at::Tensor& out,
+                    const at::Tensor& bits) {
+  TORCH_CHECK(C > 0 && C % 64 == 0 && res.numel() % C == 0, "bn_res_pro_arm: C % 64 == 0 dividing res");
+  need_bf16(res, res.numel(), "bn_res_pro_arm res");
+  need_bf16(out, res.numel(), "bn_res_pro_arm out");
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() >= 2 * C,
+              "bn_res_pro_arm: coef fp32 [2C] (scale | shift)");
+  TORCH_CHECK(bits.is_cuda() && bits.scalar_type() == at::kByte && bits.is_contiguous() &&
+                  bits.numel() >= res.numel() / 8,
+              "bn_res_pro_arm: bits uint8 [M * C / 8]");
+  g_bwd_arm.x = res.data_ptr();
+  g_bwd_arm.coef = coef.data_ptr<float>();
+  g_bwd_arm.out = out.data_ptr();
+  g_bwd_arm.C = C;
+  g_bwd_arm.rows = res.numel() / C;
+  g_bwd_arm.res = 1;
+  g_bwd_arm.bits = bits.data_ptr<uint8_t>();
 }
 
 BwdArm take_bwd_arm() {
@@ -908,8 +934,13 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   if (bw.x) {
     TORCH_CHECK(bw.C == K && bw.rows == M, "bn_bwd_pro_arm: armed for [", bw.rows, ", ", bw.C,
                 "], the GEMM's A is [", M, ", ", K, "]");
-    TORCH_CHECK(stride == 1 && !opt_ptr(pro_coef) && epi != 1,
-                "conv1x1_gemm: the backward-apply prologue serves dense data-gradient GEMMs");
+    if (bw.res) {
+      TORCH_CHECK(stride == 1 && !opt_ptr(pro_coef) && epi == 1 && K <= 2048,
+                  "conv1x1_gemm: the residual-apply prologue serves dense forward (STATS) GEMMs, K <= 2048");
+    } else {
+      TORCH_CHECK(stride == 1 && !opt_ptr(pro_coef) && epi != 1,
+                  "conv1x1_gemm: the backward-apply prologue serves dense data-gradient GEMMs");
+    }
   }
   const int64_t rows_in = stride > 1 ? (M / (Hout * Wout)) * Hin * Win : M;
   if (stride > 1) TORCH_CHECK(M % (Hout * Wout) == 0 && (Hout - 1) * stride < Hin && (Wout - 1) * stride < Win,
@@ -974,6 +1005,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
   a.ex2 = opt_ptr(ex2); a.emean2 = opt_fptr(emean2); a.acc2 = opt_fptr(acc2);
   a.bx = bw.x; a.bcoef = bw.coef; a.aout = bw.out;
+  if (bw.res) { a.bres = 1; a.obits = bw.bits; }
   apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");
 }
@@ -1527,6 +1559,7 @@ PYBIND11_MODULE(_C, m) {
         "fp32 slab count of stem7x7_wgrad's workspace");
   m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");
   m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
+  m.def("bn_res_pro_arm", &bn_res_pro_arm, "next forward conv1x1_gemm applies relu(A*scale+shift+res), written through + mask");
   m.def("conv3x3_aout_arm", &conv3x3_aout_arm, "next prologue conv3x3_gemm also writes relu(B(x)) here (56x56 halo)");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");

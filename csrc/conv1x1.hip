@@ -77,11 +77,16 @@ constexpr int kSegKmax = 512, kSeg1Kmax = 2048;
 // prologue, summed into the output (SEG) or into a second accumulator whose
 // bf16 tile is the epilogue's BN input x (RECOMP: a conv output recomputed
 // instead of read back -- csrc/gemm_epi.h XL)
-enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_SEG = 3, PRO_RECOMP = 4 };
+// PRO_RES = the previous block's closing BN + residual + ReLU, relu(A * scale +
+// shift + R) with R = GemmParams::bx, written through (the blocks of output
+// tile 0) as the block output and its packed ReLU mask (GemmParams::obits):
+// the apply pass feeding the next block's conv1, fused into that conv
+enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_SEG = 3, PRO_RECOMP = 4, PRO_RES = 5 };
 
 template <int BM, int BN, int MINB, int PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
-  static_assert(PRO != PRO_BWD || GATHER == G_DENSE, "the backward-apply prologue reads dense rows");
+  static_assert((PRO != PRO_BWD && PRO != PRO_RES) || GATHER == G_DENSE, "the two-input prologues read dense rows");
+  constexpr bool TWO_IN = PRO == PRO_BWD || PRO == PRO_RES;  // A and a second row operand bx per chunk
   constexpr bool SEG = PRO == PRO_SEG || PRO == PRO_RECOMP;
   static_assert(!SEG || GATHER == G_DENSE, "two-segment K reads dense rows");
   static_assert(PRO != PRO_RECOMP || EPI == EPI_RESBITS, "the recomputed tile feeds the RESBITS epilogue");
@@ -93,7 +98,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // PRO_BWD: the backward coefficients k | c1 | c0 of every K channel, staged
   // once per block behind the operand buffers (one __shared__ array: a second
   // one can make hipcc drain the pipeline, cdna_hip_programming.md §5 item 4a)
-  constexpr int KT = PRO == PRO_BWD ? bwd_kmax(BN) : 0;
+  constexpr int KT = TWO_IN ? bwd_kmax(BN) : 0;
   // SEG / RECOMP: segment 2's BN scale | shift staged once per block (read in
   // swrite: no coefficient registers live across the K loop), K2 <= kSegKmax
   constexpr int KS = (PRO == PRO_SEG || PRO == PRO_RECOMP) ? 2 * kSegKmax + (PRO == PRO_SEG ? kSeg1Kmax : 0) : 0;
@@ -152,18 +157,18 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   (void)psc; (void)psf;
   // PRO_BWD: the BN input rows beside A, the staged K-step's k0 and the
   // chunks whose row is < M (write-through of A')
-  uint4 rx[PRO == PRO_BWD ? A_CH : 1];
+  uint4 rx[TWO_IN ? A_CH : 1];
   int st_k0 = 0;
   uint32_t a_valid = 0;
-  const bool wthru = PRO == PRO_BWD && p.aout != nullptr && tile_n == 0;
+  const bool wthru = TWO_IN && p.aout != nullptr && tile_n == 0;
   (void)rx; (void)st_k0; (void)a_valid; (void)wthru;
   // SEG / RECOMP: the chunk's row (segment 2 has its own row stride) and
   // whether the K-step held in ra is a segment-2 one (prologue applies)
   int a_m[SEG ? A_CH : 1];
   bool st_seg2 = false;
   (void)a_m; (void)st_seg2;
-  if constexpr (PRO == PRO_BWD) {
-    for (int i = t; i < 3 * K / 4; i += kThreads)
+  if constexpr (TWO_IN) {  // PRO_BWD: k | c1 | c0; PRO_RES: scale | shift
+    for (int i = t; i < (PRO == PRO_BWD ? 3 : 2) * K / 4; i += kThreads)
       reinterpret_cast<float4*>(coef_lds)[i] = reinterpret_cast<const float4*>(p.bcoef)[i];
     __syncthreads();
   }
@@ -254,7 +259,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
 #pragma unroll
       for (int i = 0; i < A_CH; ++i)
         ra[i] = ld16(p.A + a_off[i] + k0 + a_kc[i]);  // rows >= M read row 0: their outputs are never stored
-      if constexpr (PRO == PRO_BWD) {
+      if constexpr (TWO_IN) {
 #pragma unroll
         for (int i = 0; i < A_CH; ++i) rx[i] = ld16(p.bx + a_off[i] + k0 + a_kc[i]);
       }
@@ -264,7 +269,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       const int c = t + i * kThreads;
       rb[i] = ld16(p.B + static_cast<int64_t>(n0 + c / CPRK) * K + k0 + (c % CPRK) * 8);
     }
-    if constexpr (PRO == PRO_BWD) st_k0 = k0;
+    if constexpr (TWO_IN) st_k0 = k0;
     if constexpr (PRO == PRO_FWD) {
       const int kcoef = GATHER == G_CONV3 ? p.Cin : K;
       const float4* sp = reinterpret_cast<const float4*>(p.pro_coef + kc0 + a_kc[0]);
@@ -281,16 +286,18 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     bf16_t* Bs = As + BM * LDK;
     float bk[8], bc1[8], bc0[8];  // PRO_BWD: this thread's 8 channels of the staged K-step
     (void)bk; (void)bc1; (void)bc0;
-    if constexpr (PRO == PRO_BWD) {
+    if constexpr (TWO_IN) {
       const int c = st_k0 + a_kc[0];
 #pragma unroll
       for (int j = 0; j < 8; j += 4) {
         const float4 a = *reinterpret_cast<const float4*>(coef_lds + c + j);
         const float4 b = *reinterpret_cast<const float4*>(coef_lds + K + c + j);
-        const float4 z = *reinterpret_cast<const float4*>(coef_lds + 2 * K + c + j);
         bk[j] = a.x; bk[j + 1] = a.y; bk[j + 2] = a.z; bk[j + 3] = a.w;
         bc1[j] = b.x; bc1[j + 1] = b.y; bc1[j + 2] = b.z; bc1[j + 3] = b.w;
-        bc0[j] = z.x; bc0[j + 1] = z.y; bc0[j + 2] = z.z; bc0[j + 3] = z.w;
+        if constexpr (PRO == PRO_BWD) {
+          const float4 z = *reinterpret_cast<const float4*>(coef_lds + 2 * K + c + j);
+          bc0[j] = z.x; bc0[j + 1] = z.y; bc0[j + 2] = z.z; bc0[j + 3] = z.w;
+        }
       }
     }
     bool fwd_pro = PRO == PRO_FWD;
@@ -345,6 +352,23 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         v = pack8(f);
         if (wthru && ((a_valid >> i) & 1u))
           *reinterpret_cast<uint4*>(p.aout + a_off[i] + st_k0 + a_kc[i]) = v;
+      } else if constexpr (PRO == PRO_RES) {  // bn_fwd_apply's expression order: fmaf, + residual, mask, ReLU
+        float f[8], r[8];
+        unpack8(v, f);
+        unpack8(rx[i], r);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = fmaf(f[j], bk[j], bc1[j]) + r[j];
+          bits |= (o > 0.f ? 1u : 0u) << j;
+          f[j] = o > 0.f ? o : 0.f;
+        }
+        v = pack8(f);
+        if (wthru && ((a_valid >> i) & 1u)) {
+          const int64_t e = a_off[i] + st_k0 + a_kc[i];
+          *reinterpret_cast<uint4*>(p.aout + e) = v;
+          p.obits[e >> 3] = static_cast<uint8_t>(bits);
+        }
       }
       if constexpr (GATHER == G_CONV3) {
         if (!((ra_ok >> i) & 1u)) v = make_uint4(0, 0, 0, 0);  // zero padding (after BN+ReLU)
@@ -800,6 +824,9 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   } else if constexpr (PRO == PRO_RECOMP) {  // conv1 dgrad + residual, recomputing the previous conv3
     if (epi == EPI_RESBITS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
     return hipErrorInvalidValue;
+  } else if constexpr (PRO == PRO_RES) {  // the next block's conv1 (forward, bn1 statistics)
+    if (epi == EPI_STATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
+    return hipErrorInvalidValue;
   } else if constexpr (PRO == PRO_BWD) {
     switch (epi) {
       case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
@@ -837,10 +864,11 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
 
 template <int BM, int BN, int MINB, int KBK = BK>
 hipError_t dispatch_pg(const GemmParams& p, int epi, int pro, int gather, hipStream_t s) {
-  if (pro == PRO_BWD || pro == PRO_SEG || pro == PRO_RECOMP) {
+  if (pro == PRO_BWD || pro == PRO_RES || pro == PRO_SEG || pro == PRO_RECOMP) {
     if constexpr (BM == 128 && MINB == 2 && KBK == BK) {  // the two configs conv1x1_gemm routes them to
       if (gather != G_DENSE) return hipErrorInvalidValue;
       if (pro == PRO_BWD) return dispatch_epi<BM, BN, MINB, PRO_BWD, G_DENSE, KBK>(p, epi, s);
+      if (pro == PRO_RES) return dispatch_epi<BM, BN, MINB, PRO_RES, G_DENSE, KBK>(p, epi, s);
       if constexpr (BN == 64) {  // (the 128 x 64 tiles conv1x1_gemm routes them to)
         if (pro == PRO_SEG) return dispatch_epi<BM, BN, MINB, PRO_SEG, G_DENSE, KBK>(p, epi, s);
         return dispatch_epi<BM, BN, MINB, PRO_RECOMP, G_DENSE, KBK>(p, epi, s);
@@ -908,7 +936,10 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.K2a = a.K2a > 0 ? a.K2a : a.K2; p.seg1_scale = a.seg1_scale;
   p.ebias = a.ebias; p.obits = a.obits;
   const bool bpro = a.bx != nullptr;
-  if (bpro && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS || a.seg))
+  if (bpro && !a.bres && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS || a.seg))
+    return hipErrorInvalidValue;
+  if (bpro && a.bres && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi != EPI_STATS || a.seg ||
+                         !a.aout || !a.obits || a.K > bwd_kmax(64)))
     return hipErrorInvalidValue;
   if (a.seg) {  // two-segment K: dense rows, segment 2 through the BN+ReLU prologue
     if ((a.seg != 1 && a.seg != 2) || !a.A2 || !a.B2 || !a.pro_coef || a.K2 <= 0 || a.K2 % BK || p.K2a % BK ||
@@ -921,7 +952,7 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (a.epi == EPI_APPLY && (!a.pro_coef || !a.obits || !a.ecoef || !a.eres || a.stride > 1 || a.ksize == 3 ||
                              p.res_stride != 1))
     return hipErrorInvalidValue;
-  const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP : bpro ? PRO_BWD
+  const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP : bpro ? (a.bres ? PRO_RES : PRO_BWD)
                 : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
   int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
   p.Cin = a.K;
@@ -978,7 +1009,7 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
     if (rstats == 2) return dispatch_pg<64, 64, 3>(p, EPI_RSTATS, pro, gather, s);
     return dispatch_pg<128, 64, 2>(p, EPI_RSTATS, pro, gather, s);  // (128 x 128: 32 slots per lane spill)
   }
-  if (pro == PRO_BWD) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
+  if (pro == PRO_BWD || pro == PRO_RES) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
     if (p.N % 128 == 0 && p.K <= bwd_kmax(128)) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
     if (p.K <= bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
     return hipErrorInvalidValue;

@@ -234,6 +234,10 @@ struct Conv1x1Args {
   const void* bx;                    // that BN's input [M, K]
   const float* bcoef;                // [3K] its backward coefficients (ws_bcoef)
   void* aout;                        // [M, K]
+  // bres = 1: the prologue is the closing BN + residual + ReLU of the previous
+  // block, relu(A * bcoef[k] + bcoef[K + k] + bx), written through to aout
+  // with its packed ReLU mask in obits [M, K / 8] (forward conv1, STATS)
+  int bres;
   // Two-segment K (seg 1: summed, the BN-folded conv3 data gradient with MASKX;
   // seg 2: a second accumulator whose bf16 tile is the RESBITS epilogue's x --
   // the previous block's conv3 output recomputed, ex unused): segment 2 reads

@@ -185,6 +185,26 @@ class HipKernels:
                               self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
         return y
 
+    @staticmethod
+    def relu_mask_like(x):  # bn_apply's packed ReLU mask: 1 bit per element
+        return torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
+
+    def conv1x1_fwd_res(self, c3, w, st3: BNState, res, xout, mbits, out: BNState):
+        """The next block's conv1 on x = relu(B3(c3) + res), the previous block's
+        closing apply done in the GEMM's A staging (csrc/conv1x1.hip PRO_RES) and
+        written through to ``xout`` with its packed ReLU mask ``mbits`` -- the
+        same bits as bn_apply(c3, st3, res=res, want_mask=True); ``out``'s BN
+        statistics in the epilogue."""
+        n, cin, h, wd = c3.shape
+        cout = w.shape[0]
+        y = _nhwc_empty(n, cout, h, wd, c3)
+        M = n * h * wd
+        self._arm(out, M)
+        self.ext.bn_res_pro_arm(res, self.fcoef(st3), cin, xout, mbits)
+        self.ext.conv1x1_gemm(c3, w, y, M, cout, cin, h, wd, h, wd, 1, None, 1, out.mod.running_mean,
+                              self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
+        return y
+
     def conv3x3_fwd(self, x, w, stride, out: BNState, pro: BNState | None = None, aout=None):
         """3x3 pad-1 conv as an implicit GEMM (LDS-DMA main loop, csrc/igemm.hip)
         with ``out``'s BN statistics in the epilogue (no separate stats pass);
@@ -567,6 +587,16 @@ class TorchKernels:
         self._stats(y, out, out.mod.running_mean.clone())
         return y.contiguous(memory_format=torch.channels_last)
 
+    @staticmethod
+    def relu_mask_like(x):  # bn_apply's mask: a bool tensor here
+        return torch.empty(x.shape, dtype=torch.bool, device=x.device)
+
+    def conv1x1_fwd_res(self, c3, w, st3, res, xout, mbits, out):
+        x, mb = self.bn_apply(c3, st3, relu=True, res=res, want_mask=True)
+        xout.copy_(x)
+        mbits.copy_(mb)
+        return self.conv1x1_fwd(xout, w, 1, None, out)
+
     def conv3x3_fwd(self, x, w, stride, out, pro=None, aout=None):
         a = self._pro(x, pro) if pro is not None else x.float()
         if aout is not None:
@@ -870,6 +900,13 @@ class ResNetEngine:
         # downsample branch conv of the forward on the side stream (KDL_FWD_DOWN_SIDE=0: in
         # line): 13,333-13,347 vs 13,252-13,279 img/s, profiles/r03b_fwd_down_side_ab.txt
         self.down_side = os.environ.get("KDL_FWD_DOWN_SIDE", "1") == "1"
+        # the closing BN3 + residual + ReLU of a block whose successor has no
+        # downsample branch, applied in the successor's conv1 A staging and written
+        # through (csrc/conv1x1.hip PRO_RES) instead of its own pass, up to
+        # KDL_RES_PRO_KMAX channels (the register-staged loop; beyond, the LDS-DMA
+        # GEMM + apply pass); KDL_RES_PRO=0: apply pass
+        self.res_pro_kmax = int(os.environ.get("KDL_RES_PRO_KMAX", "512")) \
+            if os.environ.get("KDL_RES_PRO", "1") == "1" else 0
         # bn1 + ReLU of the stride-1 56x56 3x3 convs applied inside the halo kernels,
         # which stage the input halo in LDS and transform it there (KDL_HALO_PRO):
         # 1 = the forward conv does, writing a1 = relu(B1(c1)) through for the weight
@@ -1008,6 +1045,8 @@ class ResNetEngine:
         x1, idx = K.stem_fwd(c0, st0, gemm_stats)
         saved = []
         cur = x1
+        pend = None  # (c3, st3, residual, mbits) of a closing apply deferred into this block's conv1
+        nb = len(self.blocks)
         for bi, blk in enumerate(self.blocks):
             s = blk.conv2.stride[0]
             st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
@@ -1028,7 +1067,12 @@ class ResNetEngine:
                     down_evt = torch.cuda.Event()
                     down_evt.record(self.side)
                 cd.record_stream(main)
-            c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
+            if pend is not None:  # cur is written by this conv1 (the previous block's closing apply)
+                c1 = K.conv1x1_fwd_res(pend[0], blk.conv1.weight.view(blk.conv1.out_channels, -1), pend[1], pend[2],
+                                       cur, pend[3], st1)
+                pend = None
+            else:
+                c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
             if self.conv3_native and self._halo_pro_ok(c1, s):
                 # the conv applies B1 + ReLU to its input halo (csrc/halo3x3.hip) and
@@ -1070,7 +1114,13 @@ class ResNetEngine:
                 out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
             else:
                 cd = None
-            if blk.down_conv is None:
+            if blk.down_conv is None and bi + 1 < nb and self.blocks[bi + 1].down_conv is None \
+                    and c3.shape[1] <= self.res_pro_kmax:
+                # deferred: the successor's conv1 applies it and writes out / mbits
+                out = torch.empty_like(c3)
+                mbits = K.relu_mask_like(c3)
+                pend = (c3, st3, cur, mbits)
+            elif blk.down_conv is None:
                 out, mbits = K.bn_apply(c3, st3, relu=True, res=cur, want_mask=True)
             saved.append((cur, c1, a1, c2, c3, cd, mbits))
             cur = out

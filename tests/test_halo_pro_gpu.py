@@ -1,4 +1,6 @@
-"""BN + ReLU prologue of the 56x56 halo kernels (csrc/halo3x3.hip PRO): the
+"""BN-apply prologues fused into their conv consumers.
+
+BN + ReLU prologue of the 56x56 halo kernels (csrc/halo3x3.hip PRO): the
 forward 3x3 conv and its weight gradient read the BN input c1 and transform
 the landed input halo in LDS, relu(c1 * scale + shift), instead of reading a
 materialised a1 = bn_apply(c1).  Same fmaf / ReLU / bf16 rounding as the apply
@@ -90,3 +92,37 @@ def test_halo_wgrad_prologue_matches_apply_pass(n):
     ref = torch.nn.grad.conv2d_weight(_a1_ref(c1, coef), tuple(w.shape), g.float(), padding=1)
     err = ((dWb.float() - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
+
+
+# ---- the closing BN + residual + ReLU of a block in the next conv1's A staging
+# (csrc/conv1x1.hip PRO_RES): conv output, written-through block output and its
+# packed ReLU mask are bit-identical to bn_apply(..., want_mask=True) + conv1x1_fwd
+
+RES_SHAPES = [(3, 10, 9, 256, 64), (2, 14, 14, 512, 128), (2, 7, 7, 1024, 256), (4, 8, 8, 256, 128)]
+
+
+@pytest.mark.parametrize("n,h,w,K4,N1", RES_SHAPES)
+def test_residual_prologue_matches_apply_pass(n, h, w, K4, N1):
+    torch.manual_seed(11)
+    K = _kern()
+    coef = torch.cat([torch.rand(K4) + 0.5, torch.randn(K4) * 0.5]).cuda()
+    st3 = _st(K, K4, 2, coef)
+    nhwc = dict(memory_format=torch.channels_last)
+    c3 = torch.randn(n, K4, h, w, device="cuda").bfloat16().contiguous(**nhwc)
+    res = torch.randn(n, K4, h, w, device="cuda").bfloat16().contiguous(**nhwc)
+    w1 = (torch.randn(N1, K4, device="cuda") / K4 ** 0.5).bfloat16()
+    M = n * h * w
+    sta, stb = _st(K, N1, 5), _st(K, N1, 5)
+    xa, mba = K.bn_apply(c3, st3, relu=True, res=res, want_mask=True)
+    ya = K.conv1x1_fwd(xa, w1, 1, None, sta)
+    K.bn_finalize(sta, M, gemm_shift=True)
+    xb = torch.full_like(c3, float("nan"))
+    mbb = torch.full_like(mba, 0x5A)
+    yb = K.conv1x1_fwd_res(c3, w1, st3, res, xb, mbb, stb)
+    K.bn_finalize(stb, M, gemm_shift=True)
+    torch.cuda.synchronize()
+    assert torch.equal(xb, xa)
+    assert torch.equal(mbb, mba)
+    assert torch.equal(yb, ya)
+    torch.testing.assert_close(stb.save_mean, sta.save_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(stb.save_invstd, sta.save_invstd, rtol=1e-5, atol=1e-6)
