@@ -907,6 +907,9 @@ class ResNetEngine:
         # GEMM + apply pass); KDL_RES_PRO=0: apply pass
         self.res_pro_kmax = int(os.environ.get("KDL_RES_PRO_KMAX", "512")) \
             if os.environ.get("KDL_RES_PRO", "1") == "1" else 0
+        # ... also before a downsample block (its conv1 then runs before the side-stream
+        # downsample conv, which reads the written-through block output)
+        self.res_pro_down = os.environ.get("KDL_RES_PRO_DOWN", "1") == "1"
         # bn1 + ReLU of the stride-1 56x56 3x3 convs applied inside the halo kernels,
         # which stage the input halo in LDS and transform it there (KDL_HALO_PRO):
         # 1 = the forward conv does, writing a1 = relu(B1(c1)) through for the weight
@@ -1052,6 +1055,13 @@ class ResNetEngine:
             st1, st2, st3 = self.bn[blk.bn1], self.bn[blk.bn2], self.bn[blk.bn3]
             n, _, h, w = cur.shape
             down_evt = None
+            c1 = None
+            if pend is not None:
+                # cur is written by this conv1 (the previous block's closing apply), so
+                # it runs before the downsample branch that reads cur is issued
+                c1 = K.conv1x1_fwd_res(pend[0], blk.conv1.weight.view(blk.conv1.out_channels, -1), pend[1], pend[2],
+                                       cur, pend[3], st1)
+                pend = None
             if blk.down_conv is not None and self.down_side and self.side is not None:
                 # the downsample branch needs only the block input: on the side stream
                 # (idle in the forward but for the weight transposes), concurrent with
@@ -1067,11 +1077,7 @@ class ResNetEngine:
                     down_evt = torch.cuda.Event()
                     down_evt.record(self.side)
                 cd.record_stream(main)
-            if pend is not None:  # cur is written by this conv1 (the previous block's closing apply)
-                c1 = K.conv1x1_fwd_res(pend[0], blk.conv1.weight.view(blk.conv1.out_channels, -1), pend[1], pend[2],
-                                       cur, pend[3], st1)
-                pend = None
-            else:
+            if c1 is None:
                 c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
             if self.conv3_native and self._halo_pro_ok(c1, s):
@@ -1114,8 +1120,8 @@ class ResNetEngine:
                 out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
             else:
                 cd = None
-            if blk.down_conv is None and bi + 1 < nb and self.blocks[bi + 1].down_conv is None \
-                    and c3.shape[1] <= self.res_pro_kmax:
+            if blk.down_conv is None and bi + 1 < nb and c3.shape[1] <= self.res_pro_kmax \
+                    and (self.res_pro_down or self.blocks[bi + 1].down_conv is None):
                 # deferred: the successor's conv1 applies it and writes out / mbits
                 out = torch.empty_like(c3)
                 mbits = K.relu_mask_like(c3)
