@@ -765,8 +765,12 @@ void bn_bwd_pro_arm(const at::Tensor& x, const at::Tensor& ws, int64_t C, const 
 // A' = relu(A * coef[k] + coef[K + k] + res), written through to ``out`` with
 // its packed ReLU mask in ``bits`` [M, K / 8] -- bit-identical to
 // bn_stage_fwd_apply(A, ws, res, ..., out, bits) (csrc/conv1x1.hip PRO_RES).
+// coefd (optional) [2C]: ``res`` is a downsample branch's BN input, the residual
+// res * coefd[k] + coefd[C + k] (bn_stage_fwd_apply's dual form); coef and coefd
+// are copied into one [4C] table owned by the arm
+thread_local at::Tensor g_res_coef4;
 void bn_res_pro_arm(const at::Tensor& res, const at::Tensor& coef, int64_t C, const at::Tensor& out,
-                    const at::Tensor& bits) {
+                    const at::Tensor& bits, const c10::optional<at::Tensor>& coefd) {
   TORCH_CHECK(C > 0 && C % 64 == 0 && res.numel() % C == 0, "bn_res_pro_arm: C % 64 == 0 dividing res");
   need_bf16(res, res.numel(), "bn_res_pro_arm res");
   need_bf16(out, res.numel(), "bn_res_pro_arm out");
@@ -777,10 +781,18 @@ void bn_res_pro_arm(const at::Tensor& res, const at::Tensor& coef, int64_t C, co
               "bn_res_pro_arm: bits uint8 [M * C / 8]");
   g_bwd_arm.x = res.data_ptr();
   g_bwd_arm.coef = coef.data_ptr<float>();
+  g_bwd_arm.res = 1;
+  if (coefd.has_value() && coefd->defined()) {
+    TORCH_CHECK(coefd->is_cuda() && coefd->scalar_type() == at::kFloat && coefd->is_contiguous() &&
+                    coefd->numel() >= 2 * C,
+                "bn_res_pro_arm: coefd fp32 [2C]");
+    g_res_coef4 = at::cat({coef.narrow(0, 0, 2 * C), coefd->narrow(0, 0, 2 * C)});
+    g_bwd_arm.coef = g_res_coef4.data_ptr<float>();
+    g_bwd_arm.res = 2;
+  }
   g_bwd_arm.out = out.data_ptr();
   g_bwd_arm.C = C;
   g_bwd_arm.rows = res.numel() / C;
-  g_bwd_arm.res = 1;
   g_bwd_arm.bits = bits.data_ptr<uint8_t>();
 }
 
@@ -1005,7 +1017,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
   a.ex2 = opt_ptr(ex2); a.emean2 = opt_fptr(emean2); a.acc2 = opt_fptr(acc2);
   a.bx = bw.x; a.bcoef = bw.coef; a.aout = bw.out;
-  if (bw.res) { a.bres = 1; a.obits = bw.bits; }
+  if (bw.res) { a.bres = bw.res; a.obits = bw.bits; }
   apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");
 }

@@ -81,12 +81,15 @@ constexpr int kSegKmax = 512, kSeg1Kmax = 2048;
 // shift + R) with R = GemmParams::bx, written through (the blocks of output
 // tile 0) as the block output and its packed ReLU mask (GemmParams::obits):
 // the apply pass feeding the next block's conv1, fused into that conv
-enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_SEG = 3, PRO_RECOMP = 4, PRO_RES = 5 };
+// PRO_RES2 = the same after a downsample block: R = bx * scale_d + shift_d (the
+// downsample branch's BN), bn_fwd_apply_dual's expression
+enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_SEG = 3, PRO_RECOMP = 4, PRO_RES = 5, PRO_RES2 = 6 };
 
 template <int BM, int BN, int MINB, int PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
-  static_assert((PRO != PRO_BWD && PRO != PRO_RES) || GATHER == G_DENSE, "the two-input prologues read dense rows");
-  constexpr bool TWO_IN = PRO == PRO_BWD || PRO == PRO_RES;  // A and a second row operand bx per chunk
+  static_assert((PRO != PRO_BWD && PRO != PRO_RES && PRO != PRO_RES2) || GATHER == G_DENSE,
+                "the two-input prologues read dense rows");
+  constexpr bool TWO_IN = PRO == PRO_BWD || PRO == PRO_RES || PRO == PRO_RES2;  // A and a second row operand bx
   constexpr bool SEG = PRO == PRO_SEG || PRO == PRO_RECOMP;
   static_assert(!SEG || GATHER == G_DENSE, "two-segment K reads dense rows");
   static_assert(PRO != PRO_RECOMP || EPI == EPI_RESBITS, "the recomputed tile feeds the RESBITS epilogue");
@@ -167,8 +170,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   int a_m[SEG ? A_CH : 1];
   bool st_seg2 = false;
   (void)a_m; (void)st_seg2;
-  if constexpr (TWO_IN) {  // PRO_BWD: k | c1 | c0; PRO_RES: scale | shift
-    for (int i = t; i < (PRO == PRO_BWD ? 3 : 2) * K / 4; i += kThreads)
+  if constexpr (TWO_IN) {  // PRO_BWD: k | c1 | c0; PRO_RES: scale | shift; PRO_RES2: + scale_d | shift_d
+    for (int i = t; i < (PRO == PRO_BWD ? 3 : PRO == PRO_RES2 ? 4 : 2) * K / 4; i += kThreads)
       reinterpret_cast<float4*>(coef_lds)[i] = reinterpret_cast<const float4*>(p.bcoef)[i];
     __syncthreads();
   }
@@ -284,8 +287,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   auto swrite = [&](int buf) {
     bf16_t* As = lds + buf * kBuf;
     bf16_t* Bs = As + BM * LDK;
-    float bk[8], bc1[8], bc0[8];  // PRO_BWD: this thread's 8 channels of the staged K-step
-    (void)bk; (void)bc1; (void)bc0;
+    float bk[8], bc1[8], bc0[8], bd[8];  // PRO_BWD / RES / RES2: this thread's 8 channels of the staged K-step
+    (void)bk; (void)bc1; (void)bc0; (void)bd;
     if constexpr (TWO_IN) {
       const int c = st_k0 + a_kc[0];
 #pragma unroll
@@ -294,9 +297,13 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         const float4 b = *reinterpret_cast<const float4*>(coef_lds + K + c + j);
         bk[j] = a.x; bk[j + 1] = a.y; bk[j + 2] = a.z; bk[j + 3] = a.w;
         bc1[j] = b.x; bc1[j + 1] = b.y; bc1[j + 2] = b.z; bc1[j + 3] = b.w;
-        if constexpr (PRO == PRO_BWD) {
+        if constexpr (PRO == PRO_BWD || PRO == PRO_RES2) {
           const float4 z = *reinterpret_cast<const float4*>(coef_lds + 2 * K + c + j);
           bc0[j] = z.x; bc0[j + 1] = z.y; bc0[j + 2] = z.z; bc0[j + 3] = z.w;
+        }
+        if constexpr (PRO == PRO_RES2) {
+          const float4 z = *reinterpret_cast<const float4*>(coef_lds + 3 * K + c + j);
+          bd[j] = z.x; bd[j + 1] = z.y; bd[j + 2] = z.z; bd[j + 3] = z.w;
         }
       }
     }
@@ -352,14 +359,15 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         v = pack8(f);
         if (wthru && ((a_valid >> i) & 1u))
           *reinterpret_cast<uint4*>(p.aout + a_off[i] + st_k0 + a_kc[i]) = v;
-      } else if constexpr (PRO == PRO_RES) {  // bn_fwd_apply's expression order: fmaf, + residual, mask, ReLU
+      } else if constexpr (PRO == PRO_RES || PRO == PRO_RES2) {
+        // bn_fwd_apply('s dual) expression order: fmaf, + residual (its own fmaf), mask, ReLU
         float f[8], r[8];
         unpack8(v, f);
         unpack8(rx[i], r);
         uint32_t bits = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float o = fmaf(f[j], bk[j], bc1[j]) + r[j];
+          const float o = fmaf(f[j], bk[j], bc1[j]) + (PRO == PRO_RES2 ? fmaf(r[j], bc0[j], bd[j]) : r[j]);
           bits |= (o > 0.f ? 1u : 0u) << j;
           f[j] = o > 0.f ? o : 0.f;
         }
@@ -824,7 +832,7 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   } else if constexpr (PRO == PRO_RECOMP) {  // conv1 dgrad + residual, recomputing the previous conv3
     if (epi == EPI_RESBITS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
     return hipErrorInvalidValue;
-  } else if constexpr (PRO == PRO_RES) {  // the next block's conv1 (forward, bn1 statistics)
+  } else if constexpr (PRO == PRO_RES || PRO == PRO_RES2) {  // the next block's conv1 (forward, bn1 statistics)
     if (epi == EPI_STATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
     return hipErrorInvalidValue;
   } else if constexpr (PRO == PRO_BWD) {
@@ -864,11 +872,13 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
 
 template <int BM, int BN, int MINB, int KBK = BK>
 hipError_t dispatch_pg(const GemmParams& p, int epi, int pro, int gather, hipStream_t s) {
-  if (pro == PRO_BWD || pro == PRO_RES || pro == PRO_SEG || pro == PRO_RECOMP) {
+  if (pro == PRO_BWD || pro == PRO_RES || pro == PRO_RES2 || pro == PRO_SEG || pro == PRO_RECOMP) {
     if constexpr (BM == 128 && MINB == 2 && KBK == BK) {  // the two configs conv1x1_gemm routes them to
       if (gather != G_DENSE) return hipErrorInvalidValue;
       if (pro == PRO_BWD) return dispatch_epi<BM, BN, MINB, PRO_BWD, G_DENSE, KBK>(p, epi, s);
       if (pro == PRO_RES) return dispatch_epi<BM, BN, MINB, PRO_RES, G_DENSE, KBK>(p, epi, s);
+      if constexpr (BN == 64)  // (128 x 128 spills with the fourth coefficient row)
+        if (pro == PRO_RES2) return dispatch_epi<BM, BN, MINB, PRO_RES2, G_DENSE, KBK>(p, epi, s);
       if constexpr (BN == 64) {  // (the 128 x 64 tiles conv1x1_gemm routes them to)
         if (pro == PRO_SEG) return dispatch_epi<BM, BN, MINB, PRO_SEG, G_DENSE, KBK>(p, epi, s);
         return dispatch_epi<BM, BN, MINB, PRO_RECOMP, G_DENSE, KBK>(p, epi, s);
@@ -952,7 +962,8 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (a.epi == EPI_APPLY && (!a.pro_coef || !a.obits || !a.ecoef || !a.eres || a.stride > 1 || a.ksize == 3 ||
                              p.res_stride != 1))
     return hipErrorInvalidValue;
-  const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP : bpro ? (a.bres ? PRO_RES : PRO_BWD)
+  const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP
+                : bpro ? (a.bres == 2 ? PRO_RES2 : a.bres ? PRO_RES : PRO_BWD)
                 : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
   int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
   p.Cin = a.K;
@@ -1008,6 +1019,10 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   if (epi == EPI_STATS && !p.C && pro == PRO_FWD && gather == G_DENSE && rstats) {
     if (rstats == 2) return dispatch_pg<64, 64, 3>(p, EPI_RSTATS, pro, gather, s);
     return dispatch_pg<128, 64, 2>(p, EPI_RSTATS, pro, gather, s);  // (128 x 128: 32 slots per lane spill)
+  }
+  if (pro == PRO_RES2) {  // four coefficient rows; 128 x 64 tiles (128 x 128 spills 12 B)
+    if (4 * p.K <= 3 * bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
+    return hipErrorInvalidValue;
   }
   if (pro == PRO_BWD || pro == PRO_RES) {  // coefficient table in LDS: 128-wide tiles to K = 512, 64-wide beyond
     if (p.N % 128 == 0 && p.K <= bwd_kmax(128)) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);

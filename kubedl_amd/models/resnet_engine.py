@@ -189,18 +189,19 @@ class HipKernels:
     def relu_mask_like(x):  # bn_apply's packed ReLU mask: 1 bit per element
         return torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
 
-    def conv1x1_fwd_res(self, c3, w, st3: BNState, res, xout, mbits, out: BNState):
+    def conv1x1_fwd_res(self, c3, w, st3: BNState, res, xout, mbits, out: BNState, dual: BNState | None = None):
         """The next block's conv1 on x = relu(B3(c3) + res), the previous block's
         closing apply done in the GEMM's A staging (csrc/conv1x1.hip PRO_RES) and
         written through to ``xout`` with its packed ReLU mask ``mbits`` -- the
         same bits as bn_apply(c3, st3, res=res, want_mask=True); ``out``'s BN
-        statistics in the epilogue."""
+        statistics in the epilogue; ``dual``: ``res`` is the downsample branch's
+        BN input and the residual B_dual(res) (bn_apply's ``other``)."""
         n, cin, h, wd = c3.shape
         cout = w.shape[0]
         y = _nhwc_empty(n, cout, h, wd, c3)
         M = n * h * wd
         self._arm(out, M)
-        self.ext.bn_res_pro_arm(res, self.fcoef(st3), cin, xout, mbits)
+        self.ext.bn_res_pro_arm(res, self.fcoef(st3), cin, xout, mbits, self.fcoef(dual) if dual is not None else None)
         self.ext.conv1x1_gemm(c3, w, y, M, cout, cin, h, wd, h, wd, 1, None, 1, out.mod.running_mean,
                               self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
         return y
@@ -591,8 +592,11 @@ class TorchKernels:
     def relu_mask_like(x):  # bn_apply's mask: a bool tensor here
         return torch.empty(x.shape, dtype=torch.bool, device=x.device)
 
-    def conv1x1_fwd_res(self, c3, w, st3, res, xout, mbits, out):
-        x, mb = self.bn_apply(c3, st3, relu=True, res=res, want_mask=True)
+    def conv1x1_fwd_res(self, c3, w, st3, res, xout, mbits, out, dual=None):
+        if dual is not None:
+            x, mb = self.bn_apply(c3, st3, relu=True, other=(res, dual), want_mask=True)
+        else:
+            x, mb = self.bn_apply(c3, st3, relu=True, res=res, want_mask=True)
         xout.copy_(x)
         mbits.copy_(mb)
         return self.conv1x1_fwd(xout, w, 1, None, out)
@@ -910,6 +914,9 @@ class ResNetEngine:
         # ... also before a downsample block (its conv1 then runs before the side-stream
         # downsample conv, which reads the written-through block output)
         self.res_pro_down = os.environ.get("KDL_RES_PRO_DOWN", "1") == "1"
+        # ... and after a downsample block: the residual is the downsample branch's BN
+        # output, applied in the same prologue (PRO_RES2)
+        self.res_pro_dual = os.environ.get("KDL_RES_PRO_DUAL", "1") == "1"
         # bn1 + ReLU of the stride-1 56x56 3x3 convs applied inside the halo kernels,
         # which stage the input halo in LDS and transform it there (KDL_HALO_PRO):
         # 1 = the forward conv does, writing a1 = relu(B1(c1)) through for the weight
@@ -1060,7 +1067,7 @@ class ResNetEngine:
                 # cur is written by this conv1 (the previous block's closing apply), so
                 # it runs before the downsample branch that reads cur is issued
                 c1 = K.conv1x1_fwd_res(pend[0], blk.conv1.weight.view(blk.conv1.out_channels, -1), pend[1], pend[2],
-                                       cur, pend[3], st1)
+                                       cur, pend[3], st1, dual=pend[4])
                 pend = None
             if blk.down_conv is not None and self.down_side and self.side is not None:
                 # the downsample branch needs only the block input: on the side stream
@@ -1109,24 +1116,27 @@ class ResNetEngine:
                 continue
             c3 = K.conv1x1_fwd(c2, blk.conv3.weight.view(blk.conv3.out_channels, -1), 1, st2, st3)
             K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
+            # the closing apply deferred into the successor's conv1 (which writes out / mbits)?
+            defer = bi + 1 < nb and c3.shape[1] <= self.res_pro_kmax and \
+                (self.res_pro_down or self.blocks[bi + 1].down_conv is None) and \
+                (blk.down_conv is None or self.res_pro_dual)
             if down_evt is not None:
                 torch.cuda.current_stream(self.dev).wait_event(down_evt)
-                out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
             elif blk.down_conv is not None:
                 std_ = self.bn[blk.down_bn]
                 cd = K.conv1x1_fwd(cur, blk.down_conv.weight.view(blk.down_conv.out_channels, -1),
                                    blk.down_conv.stride[0], None, std_)
                 K.bn_finalize(std_, n * ho * wo, gemm_shift=True)
-                out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
             else:
                 cd = None
-            if blk.down_conv is None and bi + 1 < nb and c3.shape[1] <= self.res_pro_kmax \
-                    and (self.res_pro_down or self.blocks[bi + 1].down_conv is None):
-                # deferred: the successor's conv1 applies it and writes out / mbits
+            if defer:
                 out = torch.empty_like(c3)
                 mbits = K.relu_mask_like(c3)
-                pend = (c3, st3, cur, mbits)
-            elif blk.down_conv is None:
+                # (residual: the block input, or the downsample branch's BN input + its BN)
+                pend = (c3, st3, cur, mbits, None) if cd is None else (c3, st3, cd, mbits, std_)
+            elif cd is not None:
+                out, mbits = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
+            else:
                 out, mbits = K.bn_apply(c3, st3, relu=True, res=cur, want_mask=True)
             saved.append((cur, c1, a1, c2, c3, cd, mbits))
             cur = out

@@ -126,3 +126,30 @@ def test_residual_prologue_matches_apply_pass(n, h, w, K4, N1):
     assert torch.equal(yb, ya)
     torch.testing.assert_close(stb.save_mean, sta.save_mean, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(stb.save_invstd, sta.save_invstd, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,h,w,K4,N1", [(3, 10, 9, 256, 64), (2, 14, 14, 512, 128), (2, 8, 8, 384, 128)])
+def test_dual_residual_prologue_matches_apply_pass(n, h, w, K4, N1):
+    """After a downsample block: residual = the downsample branch's BN (PRO_RES2)."""
+    torch.manual_seed(12)
+    K = _kern()
+    st3 = _st(K, K4, 2, torch.cat([torch.rand(K4) + 0.5, torch.randn(K4) * 0.5]).cuda())
+    std_ = _st(K, K4, 3, torch.cat([torch.rand(K4) + 0.5, torch.randn(K4) * 0.5]).cuda())
+    nhwc = dict(memory_format=torch.channels_last)
+    c3 = torch.randn(n, K4, h, w, device="cuda").bfloat16().contiguous(**nhwc)
+    cd = torch.randn(n, K4, h, w, device="cuda").bfloat16().contiguous(**nhwc)
+    w1 = (torch.randn(N1, K4, device="cuda") / K4 ** 0.5).bfloat16()
+    M = n * h * w
+    sta, stb = _st(K, N1, 5), _st(K, N1, 5)
+    xa, mba = K.bn_apply(c3, st3, relu=True, other=(cd, std_), want_mask=True)
+    ya = K.conv1x1_fwd(xa, w1, 1, None, sta)
+    K.bn_finalize(sta, M, gemm_shift=True)
+    xb = torch.full_like(c3, float("nan"))
+    mbb = torch.full_like(mba, 0x5A)
+    yb = K.conv1x1_fwd_res(c3, w1, st3, cd, xb, mbb, stb, dual=std_)
+    K.bn_finalize(stb, M, gemm_shift=True)
+    torch.cuda.synchronize()
+    assert torch.equal(xb, xa)
+    assert torch.equal(mbb, mba)
+    assert torch.equal(yb, ya)
+    torch.testing.assert_close(stb.save_mean, sta.save_mean, rtol=1e-5, atol=1e-6)

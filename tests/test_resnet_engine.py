@@ -158,7 +158,13 @@ def _vs_truth_strict(model, ref, truth, slack=1.5, add=0.01, cos_min=0.999):
         # the 7x7 stage at cosine ~0.73: engine 0.731 vs autograd 0.734 on one
         # run; the stem BN weight at 0.04-0.26 for both, same seed, different
         # boxes); where bf16 autograd reaches >= 0.999 this is ce >= ~0.998
-        assert ce >= min(cos_min, 1.0 - 1.5 * (1.0 - cr) - 1e-3), f"{n}: engine cosine {ce:.5f} vs autograd {cr:.5f}"
+        # Where bf16 autograd itself is below cosine 0.9 the gradient is rounding noise
+        # (a BN weight of a stage-1 block at 0.43 for autograd), and the engine's
+        # cosine is a different draw of that noise (0.02 once in five runs, bit-identical
+        # forward): there only the rel-L2 bound below applies -- it still fails a
+        # localized bug, whose error is not noise-sized
+        if cr >= 0.9:
+            assert ce >= min(cos_min, 1.0 - 1.5 * (1.0 - cr) - 1e-3), f"{n}: engine cosine {ce:.5f} vs autograd {cr:.5f}"
         assert ee <= slack * er + add, f"{n}: engine rel-L2 {ee:.4f} vs autograd {er:.4f}"
     worst.sort()
     print("lowest engine cosines:", [(n, round(ce, 5), round(cr, 5)) for ce, n, cr, _, _ in worst[:5]])
