@@ -597,7 +597,8 @@ void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at:
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   check_hip(kdl::segment_adagrad(grads.data_ptr<float>(), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
                                  rows_local.data_ptr<int64_t>(), static_cast<int>(seg.numel() - 1),
-                                 static_cast<int>(table.size(1)), table.data_ptr<float>(), accum.data_ptr<float>(),
+                                 static_cast<int>(table.size(1)), table.size(0), table.data_ptr<float>(),
+                                 accum.data_ptr<float>(),
                                  static_cast<float>(lr), static_cast<float>(eps), static_cast<float>(scale),
                                  cur_stream(), opt_count(ucount)),
             "segment_adagrad");
@@ -605,14 +606,15 @@ void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at:
 
 int64_t dedup_table_slots(int64_t n) { return kdl::dedup_table_slots(static_cast<int>(n)); }
 
-// the CSR half of dedup_csr, later in the step (sizes from that dedup_csr call)
-void csr_from_inverse_only(const at::Tensor& inv, const at::Tensor& sizes, const at::Tensor& count, at::Tensor bsum,
+// the CSR half of dedup_csr, later in the step (sizes from that dedup_csr call;
+// sizes and cursor are scratch of the long-segment sort afterwards)
+void csr_from_inverse_only(const at::Tensor& inv, at::Tensor sizes, const at::Tensor& count, at::Tensor bsum,
                            at::Tensor cursor, at::Tensor seg, at::Tensor order) {
   const int64_t n = inv.numel();
   TORCH_CHECK(n > 0 && inv.is_cuda() && inv.scalar_type() == at::kLong && inv.is_contiguous(), "csr: inv");
   TORCH_CHECK(sizes.scalar_type() == at::kInt && sizes.numel() >= n + 1 && cursor.scalar_type() == at::kInt &&
                   cursor.numel() >= n + 1 && count.scalar_type() == at::kInt && bsum.scalar_type() == at::kInt &&
-                  bsum.numel() >= (n + 1) / 1024 + 1,
+                  bsum.numel() >= kdl::csr_bsum_slots(static_cast<int>(n)),
               "csr: int32 sizes/cursor/count/bsum");
   TORCH_CHECK(seg.scalar_type() == at::kLong && seg.numel() >= n + 1 && order.scalar_type() == at::kLong &&
                   order.numel() >= n,

@@ -257,12 +257,15 @@ __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __res
                                                               const int64_t* __restrict__ rows_local, int U, int D,
                                                               float* __restrict__ table, float* __restrict__ accum,
                                                               float lr, float eps, float scale,
-                                                              const int* __restrict__ ucount) {
+                                                              const int* __restrict__ ucount, int64_t nrows) {
   const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (u >= (ucount ? *ucount : U)) return;
   const int64_t s0 = seg[u], s1 = seg[u + 1];
   const int64_t row = rows_local[u];
+  // rows outside the shard are exchange padding (distinct negative sentinels,
+  // models/ctr.py _push_fixed): nothing to update
+  if (row < 0 || row >= nrows) return;
   float* w = table + row * static_cast<int64_t>(D);
   float* a = accum + row * static_cast<int64_t>(D);
   for (int c = lane * 4; c < D; c += 256) {
@@ -464,11 +467,11 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
 }
 
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
-                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s,
-                           const int* ucount) {
+                           int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,
+                           hipStream_t s, const int* ucount) {
   if (U <= 0) return hipSuccess;
   hipLaunchKernelGGL(segment_adagrad_kernel, dim3((U + 3) / 4), dim3(256), 0, s, grads, order, seg, rows_local, U, D,
-                     table, accum, lr, eps, scale, ucount);
+                     table, accum, lr, eps, scale, ucount, nrows);
   return hipGetLastError();
 }
 
@@ -618,8 +621,9 @@ __global__ __launch_bounds__(256) void dedup_inverse_kernel(const int* __restric
 // seg[u] = exclusive prefix of sizes (u <= n); cursor[u] = 0 for the scatter
 __global__ __launch_bounds__(256) void csr_assign_kernel(const int* __restrict__ sizes, int len,
                                                          const int* __restrict__ bsum, int64_t* __restrict__ seg,
-                                                         int* __restrict__ cursor) {
+                                                         int* __restrict__ cursor, int* __restrict__ nlong) {
   __shared__ int part[256];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *nlong = 0;  // (read by csr_sort_kernel, a later launch)
   const int pre = chunk_prefix(bsum, part);
   const int base = blockIdx.x * kChunk + threadIdx.x * 4;
   int v[4], c = 0;
@@ -649,9 +653,13 @@ __global__ __launch_bounds__(256) void csr_scatter_kernel(const int64_t* __restr
   order[seg[u] + atomicAdd(cursor + u, 1)] = i;
 }
 
-// one wave per segment: sort its positions ascending, in place
+// one wave per segment: sort its positions ascending, in place.  Segments of
+// up to 64 positions are a wave bitonic sort in registers; longer ones (hot
+// ids) are appended to ``list`` (counter *nlong, reset by csr_assign_kernel)
+// for csr_sort_long_kernel.
 __global__ __launch_bounds__(256) void csr_sort_kernel(const int64_t* __restrict__ seg, int64_t* __restrict__ order,
-                                                       const int* __restrict__ count) {
+                                                       const int* __restrict__ count, int* __restrict__ nlong,
+                                                       int* __restrict__ list) {
   const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (u >= *count) return;
@@ -672,13 +680,82 @@ __global__ __launch_bounds__(256) void csr_sort_kernel(const int64_t* __restrict
     if (lane < len) o[lane] = v;
     return;
   }
-  // long segment (a hot id): odd-even transposition sort, the wave sweeping pairs
-  for (int64_t pass = 0; pass < len; ++pass) {
-    for (int64_t a = (pass & 1) + 2 * lane; a + 1 < len; a += 128) {
-      const int64_t x = o[a], y = o[a + 1];
-      if (x > y) { o[a] = y; o[a + 1] = x; }
+  if (lane == 0) list[atomicAdd(nlong, 1)] = u;
+}
+
+constexpr int kLongSort = 8192;                 // positions sorted in LDS by one block
+constexpr int kBitWindow = kLongSort * 32;      // positions per bitmap window (same 32 KiB)
+
+// One block per long segment (grid-stride over the list).  Up to kLongSort
+// positions: block bitonic sort of int32 positions in LDS, O(L log^2 L).
+// Longer: the positions are distinct integers in [0, n), so their ascending
+// order is a bitmap scan -- per window of kBitWindow positions set one bit per
+// member, then every thread emits the set bits of its 32 words at its scanned
+// offset; O(L + n / 32) per segment, and at most n / kLongSort such segments.
+__global__ __launch_bounds__(256) void csr_sort_long_kernel(const int64_t* __restrict__ seg,
+                                                            int64_t* __restrict__ order,
+                                                            const int* __restrict__ nlong,
+                                                            const int* __restrict__ list, int* __restrict__ scratch,
+                                                            int n) {
+  __shared__ unsigned int buf[kLongSort];
+  __shared__ int part[256];
+  const int nl = *nlong;
+  for (int li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int u = list[li];
+    const int64_t s0 = seg[u];
+    const int len = static_cast<int>(seg[u + 1] - s0);
+    int64_t* o = order + s0;
+    if (len <= kLongSort) {
+      int P = 128;
+      while (P < len) P <<= 1;
+      for (int i = threadIdx.x; i < P; i += 256) buf[i] = i < len ? static_cast<unsigned int>(o[i]) : 0xffffffffu;
+      __syncthreads();
+      for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = threadIdx.x; i < P; i += 256) {
+            const int l = i ^ j;
+            if (l > i) {
+              const unsigned int a = buf[i], b = buf[l];
+              const bool up = (i & k) == 0;
+              if ((a > b) == up) { buf[i] = b; buf[l] = a; }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      for (int i = threadIdx.x; i < len; i += 256) o[i] = static_cast<int64_t>(buf[i]);
+      __syncthreads();
+      continue;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pass's swaps land before the next pass reads
+    // bitmap scan: the members are copied to ``scratch`` (int32, this
+    // segment's own range of it) so every window reads them there while the
+    // sorted positions are written to o[]
+    for (int i = threadIdx.x; i < len; i += 256) scratch[s0 + i] = static_cast<int>(o[i]);
+    __syncthreads();
+    int base = 0;  // positions emitted by earlier windows
+    for (int w0 = 0; w0 < n; w0 += kBitWindow) {
+      for (int i = threadIdx.x; i < kLongSort; i += 256) buf[i] = 0u;
+      __syncthreads();
+      for (int i = threadIdx.x; i < len; i += 256) {
+        const int p = scratch[s0 + i] - w0;
+        if (p >= 0 && p < kBitWindow) atomicOr(&buf[p >> 5], 1u << (p & 31));
+      }
+      __syncthreads();
+      int c = 0;
+      for (int k = 0; k < 32; ++k) c += __popc(buf[threadIdx.x * 32 + k]);
+      int off = base + block_exclusive_scan(c, part);
+      const int tot = part[255];  // inclusive scan: the window's member count
+      for (int k = 0; k < 32; ++k) {
+        unsigned int m = buf[threadIdx.x * 32 + k];
+        while (m) {
+          const int bit = __ffs(m) - 1;
+          m &= m - 1;
+          o[off++] = static_cast<int64_t>(w0 + (threadIdx.x * 32 + k) * 32 + bit);
+        }
+      }
+      base += tot;
+      __syncthreads();
+    }
   }
 }
 }  // namespace
@@ -704,16 +781,23 @@ hipError_t dedup_ids(const int64_t* ids, int n, void* keys, int T, int* slot_of,
   return hipGetLastError();
 }
 
-hipError_t csr_from_inverse(const int64_t* inv, int n, const int* sizes, const int* count, int* bsum, int* cursor,
+int csr_bsum_slots(int n) { return (n + 1 + kChunk - 1) / kChunk + 1; }
+
+hipError_t csr_from_inverse(const int64_t* inv, int n, int* sizes, const int* count, int* bsum, int* cursor,
                             int64_t* seg, int64_t* order, hipStream_t s) {
   if (n <= 0) return hipErrorInvalidValue;
   const int len = n + 1;
   const int nb = (len + kChunk - 1) / kChunk;
+  int* nlong = bsum + nb;  // long-segment counter; the list itself reuses cursor once the scatter is done
   hipLaunchKernelGGL(chunk_count_kernel, dim3(nb), dim3(256), 0, s, static_cast<const unsigned long long*>(nullptr),
                      sizes, len, 1, bsum);
-  hipLaunchKernelGGL(csr_assign_kernel, dim3(nb), dim3(256), 0, s, sizes, len, bsum, seg, cursor);
+  hipLaunchKernelGGL(csr_assign_kernel, dim3(nb), dim3(256), 0, s, sizes, len, bsum, seg, cursor, nlong);
   hipLaunchKernelGGL(csr_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, inv, n, seg, cursor, order);
-  hipLaunchKernelGGL(csr_sort_kernel, dim3((n + 3) / 4), dim3(256), 0, s, seg, order, count);
+  // long segments (at most n / 65): their list reuses cursor and their
+  // scratch reuses sizes -- both are dead once the scatter has run
+  hipLaunchKernelGGL(csr_sort_kernel, dim3((n + 3) / 4), dim3(256), 0, s, seg, order, count, nlong, cursor);
+  const int gl = std::min(n / 65 + 1, 1024);
+  hipLaunchKernelGGL(csr_sort_long_kernel, dim3(gl), dim3(256), 0, s, seg, order, nlong, cursor, sizes, n);
   return hipGetLastError();
 }
 

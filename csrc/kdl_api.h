@@ -184,9 +184,10 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
 // ucount (optional): the live segment count on the device; U is then a capacity
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
                           const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount = nullptr);
+// rows_local outside [0, nrows) are skipped (exchange padding sentinels)
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
-                           int U, int D, float* table, float* accum, float lr, float eps, float scale, hipStream_t s,
-                           const int* ucount = nullptr);
+                           int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,
+                           hipStream_t s, const int* ucount = nullptr);
 // Sync-free de-duplication of n int64 ids (csrc/ctr.hip): uniq [n] (first *count
 // valid, the rest padded with uniq[0]), inv [n], count [1] and the segment sizes
 // [n + 1] on the device.  keys: T = dedup_table_slots(n) int64 slots, all -1
@@ -196,7 +197,10 @@ hipError_t dedup_ids(const int64_t* ids, int n, void* keys, int T, int* slot_of,
                      int64_t* uniq, int64_t* inv, int* count, int* sizes, hipStream_t s);
 // CSR of the inverse map: seg [n + 1] (exclusive scan of sizes), order [n] =
 // positions grouped by unique id, ascending within each group (deterministic sums).
-hipError_t csr_from_inverse(const int64_t* inv, int n, const int* sizes, const int* count, int* bsum, int* cursor,
+// bsum: csr_bsum_slots(n) ints.  sizes and cursor are clobbered (scratch of the
+// long-segment sort).
+int csr_bsum_slots(int n);
+hipError_t csr_from_inverse(const int64_t* inv, int n, int* sizes, const int* count, int* bsum, int* cursor,
                             int64_t* seg, int64_t* order, hipStream_t s);
 
 

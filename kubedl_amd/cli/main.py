@@ -229,8 +229,14 @@ def cmd_run(a) -> int:
     import tempfile
     from kubedl_amd.engine.manager import Manager, ManagerOptions
     home = a.home or tempfile.mkdtemp(prefix="kdl-run-")
-    mgr = Manager(ManagerOptions(home=home, gang_scheduler_name="kdl-gang" if a.gang else "",
-                                 gpus=a.gpus)).start()
+    # an explicit --home may be a running `kdl manager`'s: take its leader lock
+    # (refuse at once if held) so two node runtimes never drive one home
+    try:
+        mgr = Manager(ManagerOptions(home=home, gang_scheduler_name="kdl-gang" if a.gang else "",
+                                     gpus=a.gpus, leader_election=bool(a.home), leader_wait_s=0.0)).start()
+    except TimeoutError as e:
+        print(f"kdl run: {e} (a kdl manager runs on this home: submit with `kdl apply` instead)", file=sys.stderr)
+        return 1
     rc = 0
     try:
         jobs = []

@@ -34,11 +34,16 @@ from prometheus_client.core import GaugeMetricFamily
 
 from kubedl_amd.api import common as c
 
-# Default prometheus buckets stop at 10 s; rank launch on a local node is
-# sub-second to tens of seconds, so add finer low buckets (the names/labels are
-# what dashboards key on; the reference uses the client default buckets).
-_DELAY_BUCKETS = (0.05, 0.1, 0.25, 0.5, 1.0, 2.0, 3.0, 5.0, 7.5, 10.0, 15.0, 30.0, 60.0, 120.0,
-                  300.0, float("inf"))
+# The reference's two launch-delay histograms use the Go client's default
+# buckets (prometheus.DefBuckets; pkg/metrics/job_metrics.go:53-60 sets none);
+# their ``le`` boundaries are visible to scrapers, so they are kept exactly.
+# (Python's client default adds .075/.75/7.5 -- not the same set.)
+GO_DEF_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0, float("inf"))
+# Finer local-node buckets (rank launch is sub-second warm, seconds cold, up to
+# minutes for a gang waiting on GPUs) under a separately named kdl_* metric
+# with bounded labels {kind, phase}.
+FINE_DELAY_BUCKETS = (0.05, 0.1, 0.2, 0.3, 0.5, 0.75, 1.0, 1.5, 2.0, 3.0, 5.0, 7.5, 10.0, 15.0, 30.0, 60.0,
+                      120.0, 300.0, float("inf"))
 
 
 class _StatusGauges:
@@ -80,11 +85,15 @@ class MetricsRegistry:
         self.first_pod_delay = Histogram(
             "kubedl_jobs_first_pod_launch_delay_seconds",
             "Histogram for recording launch delay duration(from job created to first pod running).",
-            ["kind", "name", "namespace", "uid"], registry=r, buckets=_DELAY_BUCKETS)
+            ["kind", "name", "namespace", "uid"], registry=r, buckets=GO_DEF_BUCKETS)
         self.all_pods_delay = Histogram(
             "kubedl_jobs_all_pods_launch_delay_seconds",
             "Histogram for recording sync launch delay duration(from job created to all pods running).",
-            ["kind", "name", "namespace", "uid"], registry=r, buckets=_DELAY_BUCKETS)
+            ["kind", "name", "namespace", "uid"], registry=r, buckets=GO_DEF_BUCKETS)
+        self.launch_delay_fine = Histogram(
+            "kdl_jobs_launch_delay_seconds",
+            "Launch delay (job created -> first / all ranks Ready) in local-node buckets; phase = first | all.",
+            ["kind", "phase"], registry=r, buckets=FINE_DELAY_BUCKETS)
         self.steps_per_sec = Gauge("kdl_job_steps_per_second", "Training steps/s reported by rank 0",
                                    ["kind", "name", "namespace"], registry=r)
         self.gpus_allocated = Gauge("kdl_gpus_allocated", "GPUs held by gang allocations", registry=r)
@@ -146,6 +155,7 @@ class JobMetrics:
         md = job["metadata"]
         delay = earliest - c.to_epoch(md["creationTimestamp"])
         self.reg.first_pod_delay.labels(self.kind, md["name"], md["namespace"], md["uid"]).observe(delay)
+        self.reg.launch_delay_fine.labels(self.kind, "first").observe(delay)
         with self.reg._lock:
             self.reg.observed["first"][md["uid"]] = delay
         return delay
@@ -166,6 +176,7 @@ class JobMetrics:
                 final = t
         delay = final - created
         self.reg.all_pods_delay.labels(self.kind, md["name"], md["namespace"], md["uid"]).observe(delay)
+        self.reg.launch_delay_fine.labels(self.kind, "all").observe(delay)
         with self.reg._lock:
             self.reg.observed["all"][md["uid"]] = delay
         return delay

@@ -27,6 +27,7 @@ On CPU (tests) every op has a torch composition with the same semantics.
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 from typing import List, Optional, Tuple
@@ -221,6 +222,9 @@ class ShardedEmbedding:
     """One logical [vocab, dim] fp32 table sharded by ``id % n_owners`` across
     the owner ranks of ``group``; Adagrad state lives next to each shard."""
 
+    LAG = 2            # pulls between a fill's exchange and every rank reading it
+    FILL_WINDOW = 8    # recent agreed fills the capacity is sized from
+
     def __init__(self, vocab: int, dim: int, owners: List[int], rank: int, world: int, device,
                  group=None, lr: float = 0.05, eps: float = 1e-8, init_std: float = 0.01, seed: int = 0,
                  max_ids: Optional[int] = None, slack: Optional[float] = None):
@@ -242,22 +246,32 @@ class ShardedEmbedding:
         # the sync-free path (DeviceDedup, capacity-sized buffers, device-side
         # counts) serves one-owner embeddings on the GPU
         self.dedup = DeviceDedup(self.device) if self.use_hip else None
-        # Multi-rank exchange at FIXED capacity (``max_ids`` = the per-pull id bound
-        # every rank knows from the job config, e.g. batch x fields): each rank sends
-        # every owner a slot block of ``cap`` ids, so all_to_all_single runs with
-        # equal splits and no per-step size exchange to the host.  cap = max_ids
-        # cannot overflow; ``slack`` (KDL_CTR_A2A_SLACK) sizes it to slack x the
-        # uniform share max_ids / n_own instead -- an overflow is flagged on the
-        # device and raised at the next pull.
+        # Multi-rank exchange at a capacity every rank agrees on: each rank sends
+        # every owner a slot block of ``cap`` ids (+ one header slot), so
+        # all_to_all_single runs with equal splits and no per-step size exchange
+        # to the host.  ``max_ids`` = the per-pull id bound every rank knows from
+        # the job config (batch x fields) -- the first steps run at cap = max_ids
+        # (cannot overflow).  The header carries the sender's largest
+        # per-owner fill, so after the id exchange every rank holds the same
+        # global max fill; LAG steps later (its pinned copy long landed) every
+        # rank reads it and resizes ``cap`` by the same rule to ``slack`` x the
+        # recent max fill (KDL_CTR_A2A_SLACK, default 1.5; <= 0 keeps max_ids).
+        # A step whose fill exceeds its cap (the id distribution shifted within
+        # LAG steps) drops the excess ids to a dump slot: their rows read as
+        # zeros and their gradients are lost FOR THAT STEP; the overflow is
+        # counted (``overflow_steps``, raised with KDL_CTR_A2A_STRICT=1), the
+        # capacity grows, and ``finalize()`` reports the last steps too.
         self.max_ids = max_ids
         if max_ids is not None:
-            sl = slack if slack is not None else float(os.environ.get("KDL_CTR_A2A_SLACK", "0") or 0)
-            self.cap = max_ids if sl <= 0 else min(max_ids, int(math.ceil(sl * max_ids / self.n_own)) + 64)
-            self.cap = max(self.cap, 1)
+            sl = slack if slack is not None else float(os.environ.get("KDL_CTR_A2A_SLACK", "1.5") or 0)
+            self.slack = sl
+            self.cap = max(int(max_ids), 1)
+            self.strict = os.environ.get("KDL_CTR_A2A_STRICT", "0") == "1"
             self._owner_rank = torch.tensor(self.owners, dtype=torch.int64, device=self.device)
-            self._ovf = torch.zeros(1, dtype=torch.int32, device=self.device)
-            self._ovf_host = torch.zeros(1, dtype=torch.int32, pin_memory=self.device.type == "cuda")
-            self._ovf_evt = None
+            self._fills = collections.deque(maxlen=self.FILL_WINDOW)  # agreed max fills, oldest first
+            self._pending = collections.deque()  # (cap used, pinned fill, event) per pull not yet read
+            self.overflow_steps = 0
+            self.exchange_bytes = 0  # bytes this rank sent in its fixed exchanges (ids + rows)
 
     # ------------------------------------------------------------ helpers
     def _local_gather(self, local_rows: torch.Tensor) -> torch.Tensor:
@@ -274,6 +288,10 @@ class ShardedEmbedding:
         """Sum duplicate rows and apply Adagrad on the owned shard.  ``distinct``:
         the caller's ids are already unique (a world-1 push of the pull's
         de-duplicated ids) -- every segment is one row, no sort needed."""
+        if not self.use_hip and not distinct:
+            keep = ids_local >= 0  # exchange padding (negative sentinels)
+            if not bool(keep.all()):
+                ids_local, grads = ids_local[keep], grads[keep]
         n = ids_local.numel()
         if n == 0:
             return
@@ -311,69 +329,102 @@ class ShardedEmbedding:
             uniq[u.numel():] = u[0]
         return uniq, inv, torch.tensor([u.numel()], dtype=torch.int32, device=ids.device)
 
-    def _check_overflow(self) -> None:
-        """Raise on an exchange-capacity overflow flagged by an earlier pull (read
-        from pinned memory once its copy has landed: no stall on the step)."""
-        if self._ovf_evt is not None and (self.device.type != "cuda" or self._ovf_evt.query()):
-            if int(self._ovf_host[0]) != 0:
-                raise RuntimeError(f"CTR exchange overflow: more than {self.cap} ids for one owner; "
-                                   f"raise KDL_CTR_A2A_SLACK (0 = no limit below max_ids)")
-            self._ovf_evt = None
+    def _agree(self, drain: bool = False) -> None:
+        """Read the agreed fills of pulls at least LAG back (all of them with
+        ``drain``) and resize ``cap`` -- a pure function of values every rank
+        holds, evaluated at the same pull on every rank."""
+        changed = False
+        while self._pending and (drain or len(self._pending) > self.LAG):
+            cap_used, host, evt = self._pending.popleft()
+            if evt is not None:
+                evt.synchronize()
+            fill = int(host[0])
+            self._fills.append(fill)
+            if fill > cap_used:
+                self.overflow_steps += 1
+                if self.strict:
+                    raise RuntimeError(f"CTR exchange overflow: {fill} ids for one owner > capacity {cap_used} "
+                                       f"(KDL_CTR_A2A_SLACK={self.slack}); that step's excess rows were dropped")
+            changed = True
+        if not changed or self.slack <= 0 or drain:
+            return
+        need = min(self.max_ids, int(math.ceil(self.slack * max(self._fills))) + 64)
+        need = min(self.max_ids, (need + 63) // 64 * 64)
+        if self._fills[-1] > self.cap:  # overflowed at the current cap: grow at least 2x
+            self.cap = min(self.max_ids, max(need, 2 * self.cap))
+        elif need > self.cap or need < 0.75 * self.cap:
+            self.cap = max(need, 1)
+
+    def finalize(self) -> dict:
+        """Read every outstanding agreed fill (syncs): call after the last step so
+        an overflow in the final LAG pulls is counted (and raised if strict)."""
+        if self.max_ids is not None and self.world > 1:
+            self._agree(drain=True)
+            return {"exchange_cap": self.cap, "exchange_overflow_steps": self.overflow_steps,
+                    "exchange_bytes": self.exchange_bytes}
+        return {}
 
     def _pull_fixed(self, ids: torch.Tensor):
-        self._check_overflow()
+        self._agree()
         W, cap, dev = self.world, self.cap, self.device
         n = ids.numel()
         if n > self.max_ids:
             raise ValueError(f"pull of {n} ids > max_ids {self.max_ids}")
+        # id blocks of cap + 1 slots per destination; slot cap = header (the
+        # sender's largest per-owner fill, the same value to every destination)
+        send = torch.full((W * (cap + 1) + 1,), -1, dtype=torch.int64, device=dev)
         uniq, inv, count = self._dedup_any(ids)
         if n:
             valid = torch.arange(n, device=dev) < count.to(torch.int64)
             dest = torch.where(valid, self._owner_rank[uniq % self.n_own], torch.full_like(uniq, W))
-            onehot = torch.zeros(n, W + 1, dtype=torch.int32, device=dev).scatter_(1, dest[:, None], 1)
-            pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None]).squeeze(1).to(torch.int64)
+            onehot = torch.zeros(n, W + 1, dtype=torch.int64, device=dev).scatter_(1, dest[:, None], 1)
+            pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None]).squeeze(1)
             ok = valid & (pos < cap)
-            self._ovf.copy_((valid & (pos >= cap)).any().to(torch.int32).reshape(1))
-            slot = torch.where(ok, dest * cap + pos, torch.full_like(pos, W * cap))  # W * cap: dump slot
+            rslot = torch.where(ok, dest * cap + pos, torch.full_like(pos, W * cap))  # W * cap: dump slot
+            send.scatter_(0, torch.where(ok, dest * (cap + 1) + pos, torch.full_like(pos, W * (cap + 1))), uniq)
+            send[cap: W * (cap + 1): cap + 1] = onehot[:, :W].sum(0).max()
         else:
-            slot = torch.empty(0, dtype=torch.int64, device=dev)
-            self._ovf.zero_()
+            rslot = torch.empty(0, dtype=torch.int64, device=dev)
+            send[cap: W * (cap + 1): cap + 1] = 0
+        recv = torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv, send[: W * (cap + 1)], group=self.group)  # equal splits: no size exchange
+        rv = recv.view(W, cap + 1)
+        fill = rv[:, cap].max().reshape(1)  # the global max fill: identical on every rank
+        req = rv[:, :cap].reshape(-1)       # ids asked of me, -1 = padding
         if dev.type == "cuda":
-            self._ovf_host.copy_(self._ovf, non_blocking=True)
-            self._ovf_evt = torch.cuda.Event()
-            self._ovf_evt.record()
+            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+            host.copy_(fill, non_blocking=True)
+            evt = torch.cuda.Event()
+            evt.record()
         else:
-            self._ovf_host.copy_(self._ovf)
-            self._ovf_evt = True
-            self._check_overflow()
-        send = torch.full((W * cap + 1,), -1, dtype=torch.int64, device=dev)
-        if n:
-            send.scatter_(0, slot, uniq)
-        recv = torch.empty(W * cap, dtype=torch.int64, device=dev)
-        dist.all_to_all_single(recv, send[: W * cap], group=self.group)  # equal splits: no size exchange
+            host, evt = fill.clone(), None
+        self._pending.append((cap, host, evt))
         if self.is_owner:
-            rows = self._local_gather(torch.where(recv >= 0, recv // self.n_own, torch.zeros_like(recv)))
+            rows = self._local_gather(torch.where(req >= 0, req // self.n_own, torch.zeros_like(req)))
         else:
             rows = torch.zeros(W * cap, self.dim, device=dev)
         got = torch.empty(W * cap + 1, self.dim, device=dev)
         got[W * cap].zero_()
         dist.all_to_all_single(got[: W * cap], rows.contiguous(), group=self.group)
-        emb = got[slot] if n else got[:0]
-        self._ctx = ("fixed", slot, recv, count)
+        emb = got[rslot] if n else got[:0]
+        self.exchange_bytes += W * (cap + 1) * 8 + W * cap * self.dim * 4
+        self._ctx = ("fixed", rslot, req, count, cap)
         return emb, inv
 
     def _push_fixed(self, grad_unique: torch.Tensor, scale: float) -> None:
-        _, slot, recv, _ = self._ctx
-        W, cap, dev = self.world, self.cap, self.device
+        _, rslot, req, _, cap = self._ctx
+        W, dev = self.world, self.device
         gsend = torch.zeros(W * cap + 1, self.dim, device=dev)
-        if slot.numel():
-            gsend[slot] = grad_unique.float()  # (the dump slot may take several rows: never sent)
+        if rslot.numel():
+            gsend[rslot] = grad_unique.float()  # (the dump slot may take several rows: never sent)
         grecv = torch.empty(W * cap, self.dim, device=dev)
         dist.all_to_all_single(grecv, gsend[: W * cap], group=self.group)
+        self.exchange_bytes += W * cap * self.dim * 4
         if self.is_owner:
-            # padding slots carry id -1 and zero gradient: mapped to row 0 they are
-            # exact no-ops of Adagrad (g = 0 leaves acc and w unchanged)
-            local = torch.where(recv >= 0, recv // self.n_own, torch.zeros_like(recv))
+            # padding slots (id -1, zero gradient) become DISTINCT negative rows:
+            # one-row segments that the update skips -- never one giant segment
+            pad = -2 - torch.arange(req.numel(), device=dev)
+            local = torch.where(req >= 0, req // self.n_own, pad)
             self._apply_updates_dev(local, grecv, scale)
 
     def _apply_updates_dev(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:

@@ -61,6 +61,17 @@ def apply_hbm_limit(dev: torch.device) -> float | None:
     return frac
 
 
+def local_device(use_gpu: bool = True) -> torch.device:
+    """This rank's device: ``cuda:LOCAL_RANK`` (0 for a kubelet-launched rank,
+    whose own GPU heads ``HIP_VISIBLE_DEVICES``, runtime/gpu_env.py; the
+    node-local rank under ``torch.distributed.run``), or the CPU.  Every GPU
+    worker picks its device here."""
+    if not (use_gpu and torch.cuda.is_available()):
+        return torch.device("cpu")
+    ndev = torch.cuda.device_count()
+    return torch.device("cuda", env_int("LOCAL_RANK", 0) % max(ndev, 1))
+
+
 def init_from_env(device: str | None = None, timeout_s: float | None = None,
                   world1_group: bool = False) -> DistInfo:
     """``world1_group``: also build a (one-rank) process group at WORLD_SIZE=1,
@@ -73,8 +84,7 @@ def init_from_env(device: str | None = None, timeout_s: float | None = None,
     local_rank = env_int("LOCAL_RANK", 0)
     use_gpu = device != "cpu" and torch.cuda.is_available()
     if use_gpu:
-        ndev = torch.cuda.device_count()
-        dev = torch.device("cuda", local_rank % max(ndev, 1))
+        dev = local_device()
         torch.cuda.set_device(dev)
         apply_hbm_limit(dev)
         # KDL_DIST_BACKEND=gloo: rehearse a multi-rank job on fewer GPUs than
@@ -181,6 +191,13 @@ def is_comm_failure(exc: BaseException) -> bool:
         return True
     net_error = getattr(dist, "DistNetworkError", None)
     if net_error is not None and isinstance(exc, net_error):
+        return True
+    # rendezvous: a peer died before (or while) joining the TCP store -- rank 0
+    # times out "waiting for clients", the others lose the store
+    store_error = getattr(dist, "DistStoreError", None)
+    if store_error is not None and isinstance(exc, store_error):
+        return True
+    if "waiting for clients" in msg or ("store" in msg and "timed out" in msg):
         return True
     if not isinstance(exc, (RuntimeError, ConnectionError)):
         return False

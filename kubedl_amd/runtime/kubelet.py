@@ -15,9 +15,9 @@ For every pod bound to this node (``spec.nodeName``, GPUs in the
    rewritten to ``127.0.0.1`` with each ``<svc>:<port>`` mapped to the
    store's host port (so two jobs can both use 23456), ``MASTER_PORT``
    remapped along with ``MASTER_ADDR``, ``HIP_VISIBLE_DEVICES`` from the gang
-   allocation -- a gang member sees the gang's whole GPU set and selects its
-   own with ``LOCAL_RANK`` / ``LOCAL_WORLD_SIZE`` (torch.distributed.run's
-   process shape, runtime/gpu_env.py) -- and ``KDL_*`` sandbox variables;
+   allocation -- a gang member's own GPU is ``cuda:0`` as in a pod, with the
+   rest of the gang's GPUs visible behind it for the xGMI P2P transports
+   (runtime/gpu_env.py) -- and ``KDL_*`` sandbox variables;
 4. reports status like a kubelet: ``phase`` Pending -> Running ->
    Succeeded/Failed, ``containerStatuses`` (``state.running|terminated``,
    ``exitCode``, ``restartCount``, ``lastState``), and the ``Initialized`` /
@@ -206,8 +206,8 @@ class PodWorker(threading.Thread):
             if v in mounts:
                 raw[k] = mounts[v]
         env.update(raw)
-        # GPU visibility: the gang's whole set + LOCAL_RANK / LOCAL_WORLD_SIZE
-        # (torch.distributed.run's process shape, runtime/gpu_env.py), else own GPUs
+        # GPU visibility: own GPU first (cuda:0, as in a pod), then the rest of
+        # the gang's set (runtime/gpu_env.py); outside a gang only its own GPUs
         gang = [g for g in ((self.pod["metadata"].get("annotations") or {}).get(GANG_GPUS_ANNOTATION) or "")
                 .split(",") if g]
         for k, v in rank_gpu_env(self.gpus, gang).items():

@@ -33,6 +33,7 @@ import torch.distributed as dist
 
 from kubedl_amd.models.ctr import CTRModel, ShardedEmbedding
 from kubedl_amd.ops.optim import FlatParamSpace, FusedAdam
+from kubedl_amd.parallel import dist as kdist
 from kubedl_amd.parallel.ddp import FlatDDP
 from kubedl_amd.workers import common
 
@@ -88,11 +89,11 @@ def main(argv=None) -> int:
         host, port = ep.rsplit(":", 1)
         os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = host, port
     use_gpu = (not args.cpu) and torch.cuda.is_available()
-    device = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
+    # LOCAL_RANK picks this rank's GPU out of the gang's visible set
+    device = kdist.local_device(use_gpu)
     if use_gpu:
         torch.cuda.set_device(device)
-        from kubedl_amd.parallel.dist import apply_hbm_limit
-        apply_hbm_limit(device)
+        kdist.apply_hbm_limit(device)
     backend = "nccl" if use_gpu else "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -115,6 +116,7 @@ def main(argv=None) -> int:
     if not is_worker:  # PS: serve pull/push rounds
         for _ in range(total):
             emb.participate()
+        emb.finalize()
         dist.barrier()
         dist.destroy_process_group()
         return 0
@@ -154,6 +156,7 @@ def main(argv=None) -> int:
     if use_gpu:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0 if t0 is not None else 0.0
+    xstats = emb.finalize()  # (after the timed region: reads the last exchanges' agreed fills)
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=wgroup)
@@ -166,7 +169,7 @@ def main(argv=None) -> int:
                           "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
                           "samples_per_sec": args.steps * args.batch * len(workers) / dt if dt > 0 else 0.0,
                           "loss_first": first, "loss_last": last, "device": str(device),
-                          "hip_kernels": emb.use_hip}), flush=True)
+                          "hip_kernels": emb.use_hip, **xstats}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -86,6 +86,31 @@ def test_comm_failure_classification():
     net = getattr(__import__("torch").distributed, "DistNetworkError", None)
     if net is not None:
         assert kdist.is_comm_failure(net("store went away"))
+    # rendezvous timeout: a peer died before joining the store
+    import torch.distributed as tdist
+    assert kdist.is_comm_failure(tdist.DistStoreError("Timed out after 601 seconds waiting for clients. 1/2 clients"
+                                                      " joined."))
+    assert kdist.is_comm_failure(RuntimeError("Socket Timeout: wait timed out on the store for key rank1"))
     assert kdist.COMM_FAILURE_EXIT == 138
     from kubedl_amd.api import common as c
     assert c.is_retryable_exit_code(kdist.COMM_FAILURE_EXIT)
+
+
+def test_rendezvous_timeout_exits_retryable():
+    """a rank whose peer never reaches the rendezvous (rank 0's TCP
+    store times out waiting for clients) exits 138 -- retryable, so the job
+    restarts its gang instead of failing permanently."""
+    import subprocess
+    import sys
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", RANK="0",
+               KDL_PG_TIMEOUT_S="2")
+    r = subprocess.run([sys.executable, "-c", "import sys\nfrom kubedl_amd.parallel import dist as kd\n"
+                        "sys.exit(kd.run_rank(lambda: kd.init_from_env('cpu') and 0))"],
+                       env=env, capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == kdist.COMM_FAILURE_EXIT, r.stderr[-2000:]

@@ -135,12 +135,13 @@ def test_per_container_hbm_and_malformed_request_isolated(tmp_path, monkeypatch)
 
 
 def test_gang_ranks_see_the_gang_gpu_set(tmp_path, monkeypatch):
-    """VERDICT r2 missing 1: gang members get the product's torchrun-shaped GPU
-    env -- HIP_VISIBLE_DEVICES = the gang's GPUs, LOCAL_RANK = own position,
-    LOCAL_WORLD_SIZE = gang size; two concurrent 4-rank gangs get disjoint sets."""
+    """Gang members see the gang's GPUs with their own first (cuda:0 is the
+    rank's GPU, as in a pod; peers visible for the xGMI transports),
+    LOCAL_RANK = 0, LOCAL_WORLD_SIZE = gang size; two concurrent 4-rank gangs
+    get disjoint sets."""
     from kubedl_amd.runtime.gpu_env import rank_gpu_env
-    assert rank_gpu_env(["5"], ["7", "5", "6", "4"]) == {"HIP_VISIBLE_DEVICES": "4,5,6,7", "LOCAL_RANK": "1",
-                                                         "LOCAL_WORLD_SIZE": "4"}
+    assert rank_gpu_env(["5"], ["7", "5", "6", "4"]) == {"HIP_VISIBLE_DEVICES": "5,4,6,7", "LOCAL_RANK": "0",
+                                                         "LOCAL_WORLD_SIZE": "4", "KDL_GANG_GPU_INDEX": "1"}
     assert rank_gpu_env(["3"]) == {"HIP_VISIBLE_DEVICES": "3", "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": "1"}
     monkeypatch.setenv("KDL_ZYGOTE", "0")
     m = Manager(ManagerOptions(home=str(tmp_path / "home"), gpus=8, gang_scheduler_name="kdl-gang")).start()
@@ -162,11 +163,12 @@ def test_gang_ranks_see_the_gang_gpu_set(tmp_path, monkeypatch):
         sets = {}
         for name in ("ga", "gb"):
             rows = [(out / f"{name}-{r}").read_text().split() for r in range(4)]
-            vis = {row[0] for row in rows}
+            vis = {",".join(sorted(row[0].split(","), key=int)) for row in rows}
             assert len(vis) == 1, rows  # every rank of a job sees the same set
             gl = vis.pop().split(",")
-            assert len(gl) == 4 and all(row[2] == "4" for row in rows)
-            assert sorted(int(row[1]) for row in rows) == [0, 1, 2, 3]  # each rank its own device
+            assert len(gl) == 4 and all(row[2] == "4" and row[1] == "0" for row in rows)
+            # each rank's own device (cuda:0 = first visible) is distinct
+            assert sorted(row[0].split(",")[0] for row in rows) == sorted(gl)
             sets[name] = set(gl)
         assert not (sets["ga"] & sets["gb"])  # disjoint gangs
         # each gang inside one NUMA half of the node (allocator best fit)

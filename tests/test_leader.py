@@ -176,3 +176,26 @@ def test_manager_serves_both_metrics_endpoints_by_default(tmp_path):
     finally:
         p.terminate()
         p.wait(30)
+
+
+def test_kdl_run_refuses_a_home_held_by_a_manager(tmp_path):
+    """`kdl run --home X` next to a `kdl manager --home X` must not
+    start a second node runtime on that home (the leader lock is taken, and
+    refused at once while held)."""
+    home = str(tmp_path / "home")
+    os.makedirs(home)
+    holder = LeaderLock(home, "manager")
+    assert holder.try_acquire()
+    manifest = tmp_path / "job.yaml"
+    manifest.write_text("apiVersion: kubeflow.org/v1\nkind: PyTorchJob\nmetadata: {name: j}\nspec:\n"
+                        "  pytorchReplicaSpecs:\n    Master:\n      replicas: 1\n      template:\n"
+                        "        spec:\n          containers: [{name: pytorch, image: x, command: [\"true\"]}]\n")
+    try:
+        r = subprocess.run([PY, "-m", "kubedl_amd.cli", "run", "-f", str(manifest), "--home", home, "--timeout", "30"],
+                           cwd=ROOT, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 1 and "not leader" in r.stderr, (r.returncode, r.stderr[-2000:])
+    finally:
+        holder.release()
+    r = subprocess.run([PY, "-m", "kubedl_amd.cli", "run", "-f", str(manifest), "--home", home, "--timeout", "60"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=180, env=dict(os.environ, KDL_ZYGOTE="0"))
+    assert r.returncode == 0 and '"Succeeded"' in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])

@@ -1,6 +1,7 @@
 """Cross-device tier of the data-parallel path.
 
-Every rank is its own process on its OWN GPU (``cuda:<rank>``), so these tests
+Every rank is its own process on its OWN GPU (physical GPU ``<rank>``, visible
+as ``cuda:0`` with the peers behind it, runtime/gpu_env.py), so these tests
 exercise what the one-GPU suite cannot: RCCL rings over xGMI, P2P all-reduce
 kernels reading peer HBM through IPC mappings across device boundaries
 (system-scope release/acquire between GPUs), and a DDP training step whose
@@ -59,16 +60,17 @@ def _spawn(target, world, *args, timeout=300):
 
 def _init(rank, world, port, backend="nccl"):
     """The product's rank environment: the kubelet's GPU visibility for a gang
-    member (runtime/gpu_env.py: the gang's GPUs visible, LOCAL_RANK selects
-    this rank's) and its process-group bootstrap (parallel/dist.py), eager
-    communicator so a transport failure surfaces here."""
+    member (runtime/gpu_env.py: own GPU first = cuda:0, the gang's other GPUs
+    visible behind it) and its process-group bootstrap (parallel/dist.py),
+    eager communicator so a transport failure surfaces here."""
     from kubedl_amd.parallel import dist as kdist
     from kubedl_amd.runtime.gpu_env import rank_gpu_env
     os.environ.update(rank_gpu_env([str(rank)], [str(r) for r in range(world)]))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       KDL_DIST_BACKEND=backend, KDL_PG_EAGER="1")
     info = kdist.init_from_env()
-    assert info.device == torch.device("cuda", rank), info
+    assert info.device == torch.device("cuda", 0), info
+    assert os.environ["HIP_VISIBLE_DEVICES"].split(",")[0] == str(rank)
 
 
 def _inputs(rank, n, dtype):
@@ -89,7 +91,7 @@ def _rccl_worker(rank, world, port, q, n):
         torch.cuda.synchronize()
         out[name] = ((t.double().cpu() - truth).abs().max().item(), truth.abs().max().item())
     q.put((rank, out))
-    dist.barrier(device_ids=[rank])
+    dist.barrier(device_ids=[0])
     dist.destroy_process_group()
 
 
@@ -122,7 +124,7 @@ def _p2p_worker(rank, world, port, q, dtype_name, n):
     for mode, (lo, hi) in (("oneshot", (0, 32768 // buf.element_size())), ("twoshot", (0, n))):
         buf.copy_(xs[rank].cuda())
         torch.cuda.synchronize()
-        dist.barrier(device_ids=[rank])
+        dist.barrier(device_ids=[0])
         ar.all_reduce_(lo, hi, oneshot=(mode == "oneshot"))
         torch.cuda.synchronize()
         ar.check()
@@ -135,7 +137,7 @@ def _p2p_worker(rank, world, port, q, dtype_name, n):
         res[mode + "_rccl"] = (t.double().cpu() - truth[lo:hi]).abs().max().item()
     ar.close()
     q.put((rank, res))
-    dist.barrier(device_ids=[rank])
+    dist.barrier(device_ids=[0])
     dist.destroy_process_group()
 
 
@@ -166,14 +168,14 @@ def _ddp_step_worker(rank, world, port, q, transport):
     from kubedl_amd.workers.resnet50 import ResNetTrainer
     os.environ["KDL_ALLREDUCE"] = transport
     _init(rank, world, port)
-    info = DistInfo(rank, world, rank, torch.device("cuda", rank), "nccl")
+    info = DistInfo(rank, world, 0, torch.device("cuda", 0), "nccl")
     tr = ResNetTrainer(info, batch=16, image=64, num_classes=10, bn_backend="hip", seed=0)
     losses = [float(tr.step()) for _ in range(2)]
     torch.cuda.synchronize()
     tr.check_transport()
     # numpy, not tensors: a tensor in a Queue is shared through an fd that dies with this process
     q.put((rank, losses, tr.space.master.cpu().numpy(), tr.space.param.float().cpu().numpy(), tr.engine_kind))
-    dist.barrier(device_ids=[rank])
+    dist.barrier(device_ids=[0])
     dist.destroy_process_group()
 
 
