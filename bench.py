@@ -136,6 +136,10 @@ def launch_job(args) -> int:
         #    operator) -- ranks forked from the pre-imported zygote
         z = mgr.kubelet.zygote if mgr.kubelet is not None else None
         zygote_ready = bool(z is not None and z.ready.wait(timeout=min(args.timeout, 300)))
+        # ... and its device libraries in the page cache (runtime/zygote.py
+        # PREFETCH_LIBS: the first collective's RCCL code-object read)
+        if z is not None:
+            z.prefetched.wait(timeout=min(args.timeout, 120))
         t_submit = time.time()
         job = mgr.apply(make_job(args))
         uid = job["metadata"]["uid"]
@@ -172,8 +176,14 @@ def launch_job(args) -> int:
         res["job_wall_s"] = (round(c.to_epoch(st["completionTime"]) - created, 3)
                              if st.get("completionTime") else None)
         res["submit_to_done_s"] = round(time.time() - t_submit, 3)
+        if res.get("t_first_step_unix"):
+            # job creation -> every rank has finished its first training step:
+            # launch delay + model build + communicator bootstrap + step 1
+            res["time_to_first_step_s"] = round(res["t_first_step_unix"] - created, 3)
         res["ranks_ready"] = len(ready)
         res["launch"] = "warm (zygote)" if zygote_ready else "cold (no zygote)"
+        if z is not None and z.prefetch_s is not None:
+            res["node_prefetch_s"] = round(z.prefetch_s, 3)
         res.update(cold)
         if os.environ.get("KDL_BENCH_KEEP"):
             res["home"] = home

@@ -97,8 +97,12 @@ def run(args, launcher: str) -> int:
           f"{t_pg - t_import:.3f}s, model+data {t_model - t_pg:.3f}s", file=sys.stderr, flush=True)
 
     fault = bool(os.environ.get("KDL_FAULT"))
+    t_first_step = None
     for i in range(args.warmup):
         trainer.step()
+        if i == 0:  # (untimed warm-up) wall clock of the first finished step, all ranks
+            sync(info)
+            t_first_step = kdist.all_reduce_max(time.time(), info)
         if fault:
             common.maybe_inject_fault(info.rank, i)
     sync(info)
@@ -153,6 +157,10 @@ def run(args, launcher: str) -> int:
             "steps_per_sec": round(args.steps / dt, 4),
             "rank_ready_s": round(rank_ready_s, 3),
             "comm_init_s": round(comm_init_s, 3),
+            # process start -> first finished step (max over ranks); the job path
+            # adds time_to_first_step_s = job creation -> first finished step
+            "first_step_s": round(t_first_step - T_PROC_START, 3) if t_first_step else None,
+            "t_first_step_unix": round(t_first_step, 3) if t_first_step else None,
             "host_issue_ms_per_step": round(host / args.steps * 1e3, 3),
             "final_loss": round(loss, 4),
         }

@@ -21,3 +21,5 @@ cat gpurun_out/r04_ddp_timeline.txt
 s=$(find gpurun_out/r04_prof_ddp -name "*kernel_stats.csv" | head -1)
 python3 scripts/prof_summary.py "$s" 12 > gpurun_out/r04_ddp_summary.txt
 head -60 gpurun_out/r04_ddp_summary.txt
+python3 scripts/stray_kernels.py "$f" > gpurun_out/r04_stray.txt
+tail -30 gpurun_out/r04_stray.txt

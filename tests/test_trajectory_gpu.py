@@ -23,19 +23,26 @@ def _traj(monkeypatch, engine, side="1", batch=64):
     return torch.cat(losses).cpu(), tr.space.master.detach().double().clone()
 
 
-@pytest.fixture(scope="module")
-def truth():
-    mp = pytest.MonkeyPatch()
-    try:
-        return _traj(mp, "autograd")
-    finally:
-        mp.undo()
+_TRUTH = {}
 
 
+def _truth(batch):
+    """The autograd trajectory of ``batch`` (computed once per module run)."""
+    if batch not in _TRUTH:
+        mp = pytest.MonkeyPatch()
+        try:
+            _TRUTH[batch] = _traj(mp, "autograd", batch=batch)
+        finally:
+            mp.undo()
+    return _TRUTH[batch]
+
+
+@pytest.mark.parametrize("batch", [64, 256], ids=["b64", "b256"])
 @pytest.mark.parametrize("side", ["1", "0"], ids=["two_stream", "one_stream"])
-def test_engine_trajectory_matches_autograd(monkeypatch, truth, side):
-    lt, wt = truth
-    le, we = _traj(monkeypatch, "fused", side)
+def test_engine_trajectory_matches_autograd(monkeypatch, side, batch):
+    """Batch 256 = the benchmarked shape."""
+    lt, wt = _truth(batch)
+    le, we = _traj(monkeypatch, "fused", side, batch=batch)
     assert torch.isfinite(le).all() and torch.isfinite(we).all()
     # the losses fall ~0.2 per step at this lr: a corrupted update shows as a
     # step-to-step drift far beyond bf16 noise (~1e-3)
