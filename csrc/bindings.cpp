@@ -691,6 +691,71 @@ void need_opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char*
                 ": fp32 contiguous GPU tensor of >= ", numel, " elements expected");
 }
 
+// ------------------------------------------------------------------ classifier head (csrc/head.hip)
+std::vector<int64_t> head_splits(int64_t Nb, int64_t C, int64_t L) {
+  int s1 = 0, s2 = 0;
+  kdl::head_splits(static_cast<int>(Nb), static_cast<int>(C), static_cast<int>(L), &s1, &s2);
+  return {s1, s2};
+}
+
+void need_f32(const at::Tensor& t, int64_t numel, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() >= numel, what,
+              ": fp32 contiguous GPU tensor of >= ", numel, " elements expected");
+}
+
+// x [Nb, C, H, W] channels_last (the last block's output); ws = (feat, part1, lrow, dl, dlT)
+void head_forward(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b, const at::Tensor& y,
+                  at::Tensor feat, at::Tensor part1, at::Tensor lrow, at::Tensor dl, at::Tensor dlT) {
+  TORCH_CHECK(x.dim() == 4 && is_nhwc_dense(x), "head_forward: x must be [Nb, C, H, W] channels_last");
+  const int64_t Nb = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == C && w.is_contiguous(), "head_forward: w must be [L, C] contiguous");
+  const int64_t L = w.size(0);
+  TORCH_CHECK(C % 8 == 0 && L <= 8192, "head_forward: C % 8 == 0, L <= 8192");
+  need_bf16(x, Nb * C * HW, "head x");
+  need_bf16(w, L * C, "head w");
+  need_opt_bf16(b, L, "head b");
+  TORCH_CHECK(!b.has_value() || !b->defined() || b->is_contiguous(), "head b: contiguous");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kLong && y.is_contiguous() && y.numel() == Nb, "head y: int64 [Nb]");
+  auto sp = head_splits(Nb, C, L);
+  need_bf16(feat, Nb * C, "head feat");
+  need_f32(part1, sp[0] * Nb * L, "head part1");
+  need_f32(lrow, Nb, "head lrow");
+  need_bf16(dl, Nb * L, "head dl");
+  need_bf16(dlT, L * Nb, "head dlT");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check_hip(kdl::head_forward(x.data_ptr(), static_cast<int>(Nb), static_cast<int>(HW), static_cast<int>(C),
+                              w.data_ptr(), opt_ptr(b), static_cast<int>(L), y.data_ptr<int64_t>(), feat.data_ptr(),
+                              part1.data_ptr<float>(), lrow.data_ptr<float>(), dl.data_ptr(), dlT.data_ptr(),
+                              cur_stream()),
+            "head_forward");
+}
+
+void head_backward(const at::Tensor& feat, const at::Tensor& w, const at::Tensor& dl, const at::Tensor& dlT,
+                   at::Tensor part2, at::Tensor dfeat, at::Tensor dW, at::Tensor db, const at::Tensor& lrow,
+                   at::Tensor loss) {
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "head_backward: w [L, C] contiguous");
+  const int64_t L = w.size(0), C = w.size(1), Nb = feat.numel() / C;
+  TORCH_CHECK(Nb % 8 == 0 && L % 8 == 0 && C % 8 == 0, "head_backward: Nb, L, C multiples of 8");
+  auto sp = head_splits(Nb, C, L);
+  need_bf16(feat, Nb * C, "head feat");
+  need_bf16(w, L * C, "head w");
+  need_bf16(dl, Nb * L, "head dl");
+  need_bf16(dlT, L * Nb, "head dlT");
+  need_f32(part2, sp[1] * Nb * C, "head part2");
+  need_bf16(dfeat, Nb * C, "head dfeat");
+  need_bf16(dW, L * C, "head dW");
+  TORCH_CHECK(dW.is_contiguous() && db.is_contiguous(), "head dW/db: contiguous");
+  need_bf16(db, L, "head db");
+  need_f32(lrow, Nb, "head lrow");
+  need_f32(loss, 1, "head loss");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  check_hip(kdl::head_backward(feat.data_ptr(), w.data_ptr(), dl.data_ptr(), dlT.data_ptr(), static_cast<int>(Nb),
+                               static_cast<int>(C), static_cast<int>(L), part2.data_ptr<float>(), dfeat.data_ptr(),
+                               dW.data_ptr(), db.data_ptr(), lrow.data_ptr<float>(), loss.data_ptr<float>(),
+                               cur_stream()),
+            "head_backward");
+}
+
 // BN finalize folded into the next conv GEMM launch (csrc/bn_fin.h): bn_fin_arm
 // names the workspace(s) whose BN the next conv1x1_gemm / conv3x3_gemm /
 // conv3x3_s2_dgrad call on this thread finalizes in its epilogue's last
@@ -1104,14 +1169,16 @@ void stem7x7_fwd(const at::Tensor& x, const at::Tensor& wp, at::Tensor y, const 
               "stem7x7_fwd: x must be [Nb, 3, 224, 224] channels_last");
   const int64_t Nb = x.size(0);
   need_bf16(x, Nb * 224 * 224 * 3, "stem7x7_fwd x");
-  need_bf16(wp, 64 * 224, "stem7x7_fwd wp");
+  // wp: the nn.Conv2d weight [64, 3, 7, 7] (reordered inside the kernel) or [64, 224] in K order
+  const bool raw_w = wp.numel() == 64 * 3 * 7 * 7;
+  need_bf16(wp, raw_w ? 64 * 147 : 64 * 224, "stem7x7_fwd wp");
   need_bf16(y, Nb * 112 * 112 * 64, "stem7x7_fwd y");
   TORCH_CHECK(!opt_ptr(acc) || opt_ptr(shift), "stem7x7_fwd: statistics need a shift");
   need_opt_f32(shift, 64, "shift");
   need_opt_f32(acc, 32 * 2 * 64, "acc");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check_hip(kdl::stem7x7_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), static_cast<int>(Nb), opt_fptr(shift),
-                             opt_fptr(acc), cur_stream()),
+                             opt_fptr(acc), cur_stream(), raw_w),
             "stem7x7_fwd");
 }
 
@@ -1125,14 +1192,15 @@ void stem7x7_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor dw32, a
               "stem7x7_wgrad: dy must be [Nb, 64, 112, 112] channels_last");
   need_bf16(x, Nb * 224 * 224 * 3, "stem7x7_wgrad x");
   need_bf16(dy, Nb * 112 * 112 * 64, "stem7x7_wgrad dy");
-  need_bf16(dW, 64 * 224, "stem7x7_wgrad dW");
+  const bool raw_out = dW.numel() == 64 * 3 * 7 * 7;  // [64, 3, 7, 7] (else [64, 224] K order)
+  need_bf16(dW, raw_out ? 64 * 147 : 64 * 224, "stem7x7_wgrad dW");
   const int64_t slabs = kdl::stem7x7_wgrad_slabs(static_cast<int>(Nb));
   TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
                   dw32.numel() >= slabs * 64 * 224,
               "stem7x7_wgrad: dw32 must hold stem7x7_wgrad_slabs(Nb) x 64 x 224 fp32");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check_hip(kdl::stem7x7_wgrad(dy.data_ptr(), x.data_ptr(), dw32.data_ptr<float>(), dW.data_ptr(),
-                               static_cast<int>(Nb), cur_stream()),
+                               static_cast<int>(Nb), cur_stream(), raw_out),
             "stem7x7_wgrad");
 }
 
@@ -1154,7 +1222,8 @@ void stem7x7_wgrad_bn(const at::Tensor& c0, const at::Tensor& dp, const at::Tens
   need_bf16(x, Nb * 224 * 224 * 3, "x");
   need_bf16(c0, Nb * 112 * 112 * 64, "c0");
   need_bf16(dp, Nb * 56 * 56 * 64, "dp");
-  need_bf16(dW, 64 * 224, "dW");
+  const bool raw_out = dW.numel() == 64 * 3 * 7 * 7;
+  need_bf16(dW, raw_out ? 64 * 147 : 64 * 224, "dW");
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() &&
                   ws.numel() >= kdl::bn_workspace_floats(64),
               "stem7x7_wgrad_bn: ws must be the stem BN workspace");
@@ -1165,7 +1234,7 @@ void stem7x7_wgrad_bn(const at::Tensor& c0, const at::Tensor& dp, const at::Tens
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check_hip(kdl::stem7x7_wgrad_bn(c0.data_ptr(), dp.data_ptr(), idx.data_ptr<uint8_t>(),
                                   ws.data_ptr<float>() + 32 * 4 * 64 /* bn_coef_offset(64) */, x.data_ptr(), dw32.data_ptr<float>(),
-                                  dW.data_ptr(), static_cast<int>(Nb), cur_stream()),
+                                  dW.data_ptr(), static_cast<int>(Nb), cur_stream(), raw_out),
             "stem7x7_wgrad_bn");
 }
 
@@ -1571,6 +1640,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem7x7_wgrad", &stem7x7_wgrad, "ResNet stem 7x7/s2/p3 conv weight gradient -> [64][224] bf16 (stem K order)");
   m.def("stem7x7_wgrad_slabs", [](int64_t nb) { return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb)); },
         "fp32 slab count of stem7x7_wgrad's workspace");
+  m.def("head_splits", &head_splits, "K splits (fc forward, dfeat) of the classifier head kernels");
+  m.def("head_forward", &head_forward, "classifier head forward: mean pool + fc (MFMA) + softmax CE + dlogits");
+  m.def("head_backward", &head_backward, "classifier head backward: dfeat, dW, db (MFMA) + mean loss");
   m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");
   m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
   m.def("bn_res_pro_arm", &bn_res_pro_arm, "next forward conv1x1_gemm applies relu(A*scale+shift+res), written through + mask");

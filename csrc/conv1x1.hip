@@ -769,9 +769,13 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
 // columns (early layers: 256 slabs of a 64x256 weight) go through two passes:
 // partial sums over y-chunks of splits, then the chunk partials.
 constexpr int kRedCols = 16, kRedGroups = kThreads / kRedCols;
+// ``layout`` 1 (the stem, csrc/stem.hip): the slabs are [64][224] in the stem
+// kernel's K order (k = r * 32 + s * 4 + c, s < 8, c < 4) and ``out`` is the
+// nn.Conv2d weight gradient [64, 3, 7, 7] channels_last ([n][r][s][c] in
+// memory): padding columns are dropped.
 __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restrict__ dw32, int64_t nk, int count,
                                                                 int chunk, int stride, float scale,
-                                                                bf16_t* __restrict__ out) {
+                                                                bf16_t* __restrict__ out, int layout) {
   __shared__ float4 part[kRedGroups][kRedCols];
   const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
   const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kRedCols + col) * 4;
@@ -794,7 +798,15 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restric
       const float4 v = part[g][col];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
-    if (out) {
+    if (out && layout == 1) {
+      const float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = static_cast<int>(i4) + q, n = idx / 224, k = idx - n * 224;
+        const int r = k >> 5, sc = (k >> 2) & 7, c = k & 3;
+        if (sc < 7 && c < 3) out[n * 147 + (r * 7 + sc) * 3 + c] = f32_to_bf16(v[q] * scale);
+      }
+    } else if (out) {
       const uint32_t lo = pack_bf16x2(a.x * scale, a.y * scale);
       const uint32_t hi = pack_bf16x2(a.z * scale, a.w * scale);
       *reinterpret_cast<uint2*>(out + i4) = make_uint2(lo, hi);
@@ -1145,7 +1157,8 @@ void launch_wgrad(dim3 grid, hipStream_t s, const bf16_t* g, const bf16_t* x, co
 namespace {
 // Fixed-order sum of ``nsplit`` fp32 slabs into bf16 dW: one pass, or two when
 // the columns alone would leave the chip idle (chunk partials first).
-hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t* dW, hipStream_t s) {
+hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t* dW, hipStream_t s,
+                        int layout = 0) {
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
   // y-blocks to reach ~KDL_WGRAD_RED_BLOCKS (2048) blocks in the first pass
   static const int red_target = [] { const char* e = getenv("KDL_WGRAD_RED_BLOCKS"); return e ? atoi(e) : 2048; }();
@@ -1154,22 +1167,23 @@ hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t
   if (groups > by_work) groups = by_work;
   if (groups <= 1) {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, nsplit, nsplit, 1, scale,
-                       dW);
+                       dW, layout);
     return hipGetLastError();
   }
   const int chunk = (nsplit + groups - 1) / groups;
   groups = (nsplit + chunk - 1) / chunk;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid, groups), dim3(kThreads), 0, s, dw32, nk, nsplit, chunk, 1,
-                     1.0f, static_cast<bf16_t*>(nullptr));
+                     1.0f, static_cast<bf16_t*>(nullptr), 0);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(rgrid), dim3(kThreads), 0, s, dw32, nk, groups, groups, chunk, scale,
-                     dW);
+                     dW, layout);
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s) {
-  return wgrad_reduce(dw32, nk, nsplit, scale, static_cast<bf16_t*>(dW), s);
+hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s,
+                             int layout) {
+  return wgrad_reduce(dw32, nk, nsplit, scale, static_cast<bf16_t*>(dW), s, layout);
 }
 
 namespace {

@@ -267,21 +267,39 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s);
 // weights as [64][224] bf16 (k = r * 32 + s * 4 + c, zero for s = 7 / c = 3),
 // y [Nb, 112, 112, 64] NHWC; acc != null: BN statistics around shift into the
 // forward replicas (STATS epilogue), else a plain store.
+// raw_w: wp is the nn.Conv2d weight [64][3][7][7] itself (reordered while the
+// kernel stages it), else [64][224] in stem_weights' K order.
 hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const float* shift, float* acc,
-                       hipStream_t s);
+                       hipStream_t s, bool raw_w = false);
 // stem weight gradient: dy [Nb, 112, 112, 64], x [Nb, 224, 224, 3] (NHWC bf16)
 // -> dW [64][224] bf16 in stem_weights' K order; dw32 = stem7x7_wgrad_slabs(Nb)
 // x [64][224] fp32 slabs (no initialisation needed)
 int stem7x7_wgrad_slabs(int Nb);
-hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s);
+// raw_out: dW is written as the nn.Conv2d gradient [64][3][7][7] instead.
+hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s,
+                         bool raw_out = false);
 // the same with the stem BN + ReLU + max-pool backward folded in: dy is built
 // per tile from c0 [Nb, 112, 112, 64], the pooled gradient dp [Nb, 56, 56, 64],
 // its argmax bytes idx and coef5 = [5][64] (forward scale | shift, backward
 // k | c1 | c0 of the BN workspace, after bn_pool_backward(with_dx = false))
 hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, const float* coef5, const void* x,
-                            float* dw32, void* dW, int Nb, hipStream_t s);
-// fixed-order sum of nsplit fp32 [nk] slabs into bf16 (scaled), csrc/conv1x1.hip
-hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s);
+                            float* dw32, void* dW, int Nb, hipStream_t s, bool raw_out = false);
+// Classifier head (csrc/head.hip): x [Nb, HW, C] NHWC bf16 (last block output),
+// fc weight w [L][C] bf16, bias b [L] bf16 (optional), labels y [Nb] int64.
+// Forward: feat [Nb][C] bf16 (mean pool), part1 [s1][Nb][L] fp32 (split-K fc
+// partials), lrow [Nb] per-image loss, dl [Nb][L] / dlT [L][Nb] bf16 dlogits
+// (mean reduction).  Backward: part2 [s2][Nb][C] fp32, dfeat [Nb][C] bf16,
+// dW [L][C] / db [L] bf16, loss [1] fp32 (mean).  s1 / s2 from head_splits.
+void head_splits(int Nb, int C, int L, int* s1, int* s2);
+hipError_t head_forward(const void* x, int Nb, int HW, int C, const void* w, const void* b, int L, const int64_t* y,
+                        void* feat, float* part1, float* lrow, void* dl, void* dlT, hipStream_t s);
+hipError_t head_backward(const void* feat, const void* w, const void* dl, const void* dlT, int Nb, int C, int L,
+                         float* part2, void* dfeat, void* dW, void* db, const float* lrow, float* loss,
+                         hipStream_t s);
+// fixed-order sum of nsplit fp32 [nk] slabs into bf16 (scaled), csrc/conv1x1.hip;
+// layout 1: the stem's [64][224] K order written out as [64][3][7][7]
+hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s,
+                             int layout = 0);
 void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)
 int conv1x1_wgrad_splits(int M, int N, int K);
 // 256 x 256 weight-gradient tiles: 0 off, 1 3x3 only (default), 2 3x3 + 1x1 (ignored under KDL_WGRAD_BIG)

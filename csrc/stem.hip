@@ -92,9 +92,21 @@ __global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tile
 
   // weights (row n: 224 bf16 = 28 uint4) and a zeroed halo (the column and
   // channel padding is never written again)
-  for (int i = t; i < 64 * (kK / 8); i += kNT) {
-    const int n = i / (kK / 8), c = i - n * (kK / 8);
-    *reinterpret_cast<uint4*>(Bs + n * kLDB + 8 * c) = *reinterpret_cast<const uint4*>(p.B + n * kK + 8 * c);
+  if (p.Cin == 3) {
+    // the nn.Conv2d weight [64, 3, 7, 7] itself, channels_last in memory
+    // ([n][r][s][c], the engine's parameter layout), reordered to
+    // k = r * 32 + s * 4 + c here (padding s = 7 / c = 3 zero): no per-step
+    // reformat launch
+    for (int i = t; i < 64 * kK; i += kNT) {
+      const int n = i / kK, k = i - n * kK;
+      const int r = k >> 5, sc = (k >> 2) & 7, c = k & 3;
+      Bs[n * kLDB + k] = (sc < 7 && c < 3) ? p.B[n * 147 + (r * 7 + sc) * 3 + c] : static_cast<bf16_t>(0);
+    }
+  } else {
+    for (int i = t; i < 64 * (kK / 8); i += kNT) {
+      const int n = i / (kK / 8), c = i - n * (kK / 8);
+      *reinterpret_cast<uint4*>(Bs + n * kLDB + 8 * c) = *reinterpret_cast<const uint4*>(p.B + n * kK + 8 * c);
+    }
   }
   for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
 
@@ -400,7 +412,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
 void set_stem_drop(int bits) { g_stem_drop = bits; }
 
 hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const float* shift, float* acc,
-                       hipStream_t s) {
+                       hipStream_t s, bool raw_w) {
   if (Nb <= 0) return hipErrorInvalidValue;
   GemmParams p{};
   p.A = static_cast<const bf16_t*>(x);
@@ -412,6 +424,7 @@ hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const flo
   p.shift = shift;
   p.acc = acc;
   p.price_drop = g_stem_drop;
+  p.Cin = raw_w ? 3 : 0;
   const int tiles = Nb * (kOH / 2);
   const int grid = tiles < 512 ? tiles : 512;  // two resident blocks per CU
   if (acc) {
@@ -427,7 +440,8 @@ int stem7x7_wgrad_slabs(int Nb) {
   return tiles < 512 ? tiles : 512;
 }
 
-hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s) {
+hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s,
+                         bool raw_out) {
   if (Nb <= 0) return hipErrorInvalidValue;
   const int64_t dy_bytes = static_cast<int64_t>(Nb) * kOH * kOW * 64 * 2;
   if (dy_bytes >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit buffer offsets
@@ -437,11 +451,11 @@ hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, i
                      static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes, StemBnBwd{});
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s);
+  return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s, raw_out ? 1 : 0);
 }
 
 hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, const float* coef5, const void* x,
-                            float* dw32, void* dW, int Nb, hipStream_t s) {
+                            float* dw32, void* dW, int Nb, hipStream_t s, bool raw_out) {
   if (Nb <= 0) return hipErrorInvalidValue;
   const int tiles = Nb * (kOH / 2);
   const int grid = stem7x7_wgrad_slabs(Nb);
@@ -450,7 +464,7 @@ hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, 
                      static_cast<const bf16_t*>(x), dw32, tiles, int64_t(0), bn);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s);
+  return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s, raw_out ? 1 : 0);
 }
 
 }  // namespace kdl

@@ -331,7 +331,10 @@ class HipKernels:
         if (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(w.shape) == (64, 3, 7, 7)
                 and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
             c0 = _nhwc_empty(x.shape[0], 64, 112, 112, x)
-            self.ext.stem7x7_fwd(x, stem_weights(w), c0, st.mod.running_mean, self._fwd_acc(st))
+            # the channels_last [64, 3, 7, 7] parameter itself (the kernel reorders it
+            # while staging); contiguous NCHW weights (tests) take the K-order copy
+            wk = w if w.is_contiguous(memory_format=torch.channels_last) else stem_weights(w)
+            self.ext.stem7x7_fwd(x, wk, c0, st.mod.running_mean, self._fwd_acc(st))
             self.stem_path = "kdl"
             return c0, True
         # csrc/stem.hip is specialised to the 224 x 224 x 3 geometry the benchmark
@@ -513,8 +516,11 @@ class HipKernels:
         forward ran on it, else MIOpen."""
         if self._stem_native_bwd(x, dc0, dw):
             ws = self._stem_ws(x.shape[0], x.device)
-            self.ext.stem7x7_wgrad(dc0, x, ws[0], ws[1])
-            dw.copy_(stem_grad_from_k(ws[1]))
+            if dw.is_contiguous(memory_format=torch.channels_last):  # written in place, raw layout
+                self.ext.stem7x7_wgrad(dc0, x, ws[0], dw)
+            else:
+                self.ext.stem7x7_wgrad(dc0, x, ws[0], ws[1])
+                dw.copy_(stem_grad_from_k(ws[1]))
             return
         _, dw0, _ = torch.ops.aten.convolution_backward(
             dc0, x, dw, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False])
@@ -552,8 +558,40 @@ class HipKernels:
         st.xam = None
         nb = x.shape[0]
         ws = self._stem_ws(nb, x.device)
-        self.ext.stem7x7_wgrad_bn(c0, dp, idx, st.ws, x, ws[0], ws[1])
-        dw.copy_(stem_grad_from_k(ws[1]))
+        if dw.is_contiguous(memory_format=torch.channels_last):  # written in place, raw layout
+            self.ext.stem7x7_wgrad_bn(c0, dp, idx, st.ws, x, ws[0], dw)
+        else:
+            self.ext.stem7x7_wgrad_bn(c0, dp, idx, st.ws, x, ws[0], ws[1])
+            dw.copy_(stem_grad_from_k(ws[1]))
+
+    def head_ok(self, fmap, w, y) -> bool:
+        n, c = fmap.shape[:2]
+        L = w.shape[0]
+        return (fmap.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
+                and fmap.is_contiguous(memory_format=torch.channels_last) and n % 8 == 0 and c % 8 == 0
+                and L % 8 == 0 and L <= 8192 and y.dtype == torch.int64)
+
+    def head(self, fmap, w, b, y, dw, db):
+        """Pool -> fc -> softmax CE -> backward on csrc/head.hip: (loss [1],
+        dfeat [n, c] bf16); dW / db written into ``dw`` / ``db``."""
+        n, c = fmap.shape[:2]
+        L = w.shape[0]
+        key = ("head", n, c, L)
+        ws = self._dw32.get(key)
+        if ws is None:
+            s1, s2 = self.ext.head_splits(n, c, L)
+            bf = dict(dtype=torch.bfloat16, device=fmap.device)
+            f32 = dict(dtype=torch.float32, device=fmap.device)
+            ws = self._dw32[key] = dict(feat=torch.empty(n, c, **bf), part1=torch.empty(s1 * n * L, **f32),
+                                        lrow=torch.empty(n, **f32), dl=torch.empty(n, L, **bf),
+                                        dlT=torch.empty(L, n, **bf), part2=torch.empty(s2 * n * c, **f32),
+                                        dfeat=torch.empty(n, c, **bf))
+        yc = y if y.is_contiguous() else y.contiguous()
+        self.ext.head_forward(fmap, w, b, yc, ws["feat"], ws["part1"], ws["lrow"], ws["dl"], ws["dlT"])
+        loss = torch.empty(1, dtype=torch.float32, device=fmap.device)  # fresh per step (returned)
+        self.ext.head_backward(ws["feat"], w, ws["dl"], ws["dlT"], ws["part2"], ws["dfeat"], dw, db, ws["lrow"],
+                               loss)
+        return loss.view(()), ws["dfeat"]
 
     def _stem_ws(self, nb, device):
         key = ("stem", nb)
@@ -1149,7 +1187,16 @@ class ResNetEngine:
         m = self.model
         feat_map = self.forward(x)
         n, c, h, w = feat_map.shape
-        with torch.enable_grad():  # the pooling head (0.1% of the FLOPs) runs under autograd
+        head = getattr(self.K, "head", None)
+        if head is not None and self.K.head_ok(feat_map, m.fc.weight, y):
+            # csrc/head.hip: pool + fc + softmax CE + their backward, dW / db straight
+            # into the gradient buffer (no autograd, no vendor GEMM)
+            loss, dfeat = head(feat_map, m.fc.weight, m.fc.bias, y, self._g(m.fc.weight), self._g(m.fc.bias))
+            self.on_ready(m.fc.weight)
+            self.on_ready(m.fc.bias)
+            self.backward(dfeat, h * w)
+            return loss
+        with torch.enable_grad():  # torch backend / unsupported shapes: the head under autograd
             feat = feat_map.mean((2, 3), dtype=torch.float32).detach().requires_grad_(True)
             fcw = m.fc.weight.detach().requires_grad_(True)
             fcb = m.fc.bias.detach().requires_grad_(True)

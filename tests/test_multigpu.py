@@ -348,14 +348,14 @@ def test_xdljob_ps_scheduler_workers_on_distinct_gpus(tmp_path, monkeypatch):
     sched = {"spec": {"containers": [{"name": "xdl", "image": "kubedl-amd/xdl-ctr", "args": args}]}}
     job = {"apiVersion": "xdl.kubedl.io/v1alpha1", "kind": "XDLJob",
            "metadata": {"name": "ctr6", "namespace": "default"},
-           "spec": {"xdlReplicaSpecs": {
+           "spec": {"cleanPodPolicy": "None", "xdlReplicaSpecs": {
                "PS": {"replicas": 2, "restartPolicy": "Never", "template": _gpu_tmpl("xdl", "kubedl-amd/xdl-ctr", args)},
                "Scheduler": {"replicas": 1, "restartPolicy": "Never", "template": sched},
                "Worker": {"replicas": 4, "restartPolicy": "Never", "template": _gpu_tmpl("xdl", "kubedl-amd/xdl-ctr", args)}}}}
     _, pods = _run_gang_job(tmp_path, monkeypatch, job)
     ranks = [f"ctr6-ps-{i}" for i in range(2)] + [f"ctr6-worker-{i}" for i in range(4)]
     _assert_xgmi_ranks(pods, ranks)
-    assert pods.get("ctr6-scheduler-0", ("", ""))[0] == ""  # (removed by cleanPodPolicy Running)
+    assert pods["ctr6-scheduler-0"][0] == ""  # (pods kept: cleanPodPolicy None)
     res = [json.loads(x) for x in pods["ctr6-worker-0"][1].splitlines() if x.startswith("{")][-1]
     assert res["workers"] == 4 and res["ps"] == 2 and res["exchange_overflow_steps"] == 0, res
     assert res["loss_last"] < res["loss_first"], res
@@ -379,7 +379,7 @@ def test_xgboost_and_xdl_gang_jobs_cpu_rehearsal(tmp_path, monkeypatch):
     sched = {"spec": {"containers": [{"name": "xdl", "image": "kubedl-amd/xdl-ctr", "args": args}]}}
     job = {"apiVersion": "xdl.kubedl.io/v1alpha1", "kind": "XDLJob",
            "metadata": {"name": "ctr4", "namespace": "default"},
-           "spec": {"xdlReplicaSpecs": {
+           "spec": {"cleanPodPolicy": "None", "xdlReplicaSpecs": {
                "PS": {"replicas": 2, "restartPolicy": "Never", "template": _gpu_tmpl("xdl", "kubedl-amd/xdl-ctr", args)},
                "Scheduler": {"replicas": 1, "restartPolicy": "Never", "template": sched},
                "Worker": {"replicas": 2, "restartPolicy": "Never", "template": _gpu_tmpl("xdl", "kubedl-amd/xdl-ctr", args)}}}}

@@ -127,3 +127,29 @@ def test_stem_wgrad_bn_fused_matches_unfused(nb):
     ext.stem7x7_wgrad_bn(c0, dp, idx, ws2, x, slabs, got)
     scale = ref.float().abs().max().item()
     torch.testing.assert_close(got.float(), ref.float(), atol=2e-3 * scale, rtol=1e-2)
+
+
+@pytest.mark.parametrize("nb", [2, 3])
+def test_stem_raw_weight_layout_bit_exact(nb):
+    """The channels_last [64, 3, 7, 7] parameter passed as is: the forward
+    reorders it while staging (no per-step stem_weights launch) and the weight
+    gradient lands directly in the parameter's layout -- both bit-identical to
+    the K-order path (the same sums, only the index map differs)."""
+    from kubedl_amd.ops.conv import stem_grad_from_k
+    ext = _ext()
+    x, w = _inputs(nb, 35)
+    assert w.is_contiguous(memory_format=torch.channels_last)
+    ya = torch.empty(nb, 64, 112, 112, device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    yb = torch.empty_like(ya)
+    ext.stem7x7_fwd(x, stem_weights(w), ya, None, None)
+    ext.stem7x7_fwd(x, w, yb, None, None)
+    assert torch.equal(ya, yb)
+    dy = torch.randn(nb, 112, 112, 64, device="cuda").bfloat16().permute(0, 3, 1, 2)
+    ws = torch.empty(ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device="cuda")
+    dwk = torch.empty(64, 224, device="cuda", dtype=torch.bfloat16)
+    ext.stem7x7_wgrad(dy, x, ws, dwk)
+    raw = torch.full((64, 3, 7, 7), float("nan"), device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ext.stem7x7_wgrad(dy, x, ws, raw)
+    assert torch.equal(raw, stem_grad_from_k(dwk))
