@@ -1159,6 +1159,10 @@ namespace {
 // the columns alone would leave the chip idle (chunk partials first).
 hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t* dW, hipStream_t s,
                         int layout = 0) {
+  // timing-only (KDL_PRICE_WGRAD_REDUCE=0): skip the slab reduce to price its
+  // cost in the two-stream step (weight gradients are then garbage)
+  static const bool skip = [] { const char* e = getenv("KDL_PRICE_WGRAD_REDUCE"); return e && e[0] == '0'; }();
+  if (skip) return hipSuccess;
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
   // y-blocks to reach ~KDL_WGRAD_RED_BLOCKS (2048) blocks in the first pass
   static const int red_target = [] { const char* e = getenv("KDL_WGRAD_RED_BLOCKS"); return e ? atoi(e) : 2048; }();

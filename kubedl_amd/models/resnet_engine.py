@@ -56,6 +56,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import dataclasses
 import os
 
 import torch
@@ -115,19 +116,20 @@ class HipKernels:
 
     name = "hip"
 
-    def __init__(self, dev):
+    def __init__(self, dev, fuse_fin: bool = True):
         from kubedl_amd.ops import _ext
         self.ext = _ext.load()
         self.dev = dev
         self._dw32 = {}
-        self.stem_native = os.environ.get("KDL_STEM", "kdl") != "miopen"  # KDL_STEM=miopen: vendor stem conv
+        # the kdl stem kernel serves the 3x224x224 geometry the benchmark trains on
+        self.stem_native = True
         # BN finalize folded into the producing conv GEMM's last arriving blocks
-        # (csrc/bn_fin.h; KDL_BN_FIN=kernel: separate finalize launches).  Round 2
-        # measured it neutral while its inlined tail made every MASKX/STATS GEMM
-        # spill ~90 VGPRs; with the tail's replica sum chunked (no spills) it is
-        # 19.33 / 19.37 vs 19.41 / 19.47 ms per step (profiles/r03_knob_sweep.txt)
-        # and ~106 fewer launches
-        self.fuse_fin = os.environ.get("KDL_BN_FIN", "gemm") != "kernel"
+        # (csrc/bn_fin.h; EngineOptions.bn_fin = "kernel": separate finalize
+        # launches).  Round 2 measured it neutral while its inlined tail made every
+        # MASKX/STATS GEMM spill ~90 VGPRs; with the tail's replica sum chunked (no
+        # spills) it is 19.33 / 19.37 vs 19.41 / 19.47 ms per step
+        # (profiles/r03_knob_sweep.txt) and ~106 fewer launches
+        self.fuse_fin = fuse_fin
         self._fin_ptrs = {}
         self.stem_path = None  # "kdl" | "miopen" once a forward ran (reported by bench / smoke)
 
@@ -593,6 +595,11 @@ class HipKernels:
                                loss)
         return loss.view(()), ws["dfeat"]
 
+    @staticmethod
+    def dgrad3x3_strided_bn(g, w, stride, x1, st1, dgamma, dbeta):
+        raise NotImplementedError(f"HIP engine: stride-{stride} 3x3 data gradient needs an even input size "
+                                  f"(got {tuple(x1.shape[-2:])} -> {tuple(g.shape[-2:])})")
+
     def _stem_ws(self, nb, device):
         key = ("stem", nb)
         ws = self._dw32.get(key)
@@ -852,6 +859,12 @@ class TorchKernels:
     def stem_backward(self, dp, idx, c0, x, st, dgamma, dbeta, dw):
         self.stem_wgrad(self.stem_bwd(dp, idx, c0, st, dgamma, dbeta), x, dw)
 
+    def dgrad3x3_strided_bn(self, g, w, stride, x1, st1, dgamma, dbeta):
+        """Strided 3x3 data gradient at any geometry + bn1's ReLU mask / backward."""
+        dx = torch.nn.grad.conv2d_input(tuple(x1.shape), w.float(), g.float(), stride=stride, padding=1)
+        return self.bn_bwd_full(dx.to(x1.dtype).contiguous(memory_format=torch.channels_last), x1, st1, dgamma,
+                                dbeta)
+
     @staticmethod
     def stem_wgrad(dc0, x, dw):
         dw.copy_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dc0.float(), stride=2, padding=3))
@@ -868,6 +881,51 @@ class TorchKernels:
 
 
 # ---------------------------------------------------------------------------- engine
+@dataclasses.dataclass
+class EngineOptions:
+    """Schedule choices of the engine.  Every default is the measured winner
+    (docs/perf_notes.md, profiles/r03*_ab.txt); A/B experiments override them
+    through ONE variable, ``KDL_ENGINE="key=value,..."`` (e.g.
+    ``KDL_ENGINE=side=0`` for the single-stream schedule)."""
+    # weight gradients on a second HIP stream (0: single stream -- 10.7k vs
+    # 11.3k img/s when introduced); side_prio: its HIP stream priority
+    side: bool = True
+    side_prio: int = 0
+    # BN finalize in the producing GEMM's last blocks ("gemm") or own launches ("kernel")
+    bn_fin: str = "gemm"
+    # recompute blocks up to this 4C width (0 = off: measured 13,216-13,227 on vs
+    # 13,233-13,264 img/s off, see below)
+    recomp: int = 0
+    # downsample conv of the forward on the side stream
+    down_side: bool = True
+    # closing BN3 + residual + ReLU in the successor's conv1 staging (up to this K;
+    # 0 = apply pass), also before / after downsample blocks
+    res_pro_kmax: int = 512
+    res_pro_down: bool = True
+    res_pro_dual: bool = True
+    # bn1 + ReLU inside the 56x56 halo kernels: 1 forward + write-through, 2 also
+    # the weight gradient's halo, 0 apply pass
+    halo_pro: int = 1
+    # BN-backward apply fused into 1x1 data-gradient GEMMs (1 write-through, 2 both
+    # operands, 0 own pass) up to this many channels; bn1 too (measured slower)
+    bn_bwd_fuse: int = 1
+    bn_bwd_fuse_kmax: int = 512
+    bn_bwd_fuse_bn1: bool = False
+
+    @classmethod
+    def from_env(cls) -> "EngineOptions":
+        o = cls()
+        spec = os.environ.get("KDL_ENGINE", "")
+        for item in filter(None, (x.strip() for x in spec.split(","))):
+            key, _, val = item.partition("=")
+            f = {x.name: x for x in dataclasses.fields(cls)}.get(key)
+            if f is None:
+                raise ValueError(f"KDL_ENGINE: unknown option {key!r} (known: {[x.name for x in dataclasses.fields(cls)]})")
+            typ = type(getattr(o, key))
+            setattr(o, key, (val.lower() in ("1", "true", "on")) if typ is bool else typ(val))
+        return o
+
+
 class ResNetEngine:
     """Hand-scheduled training step of a ``ResNet`` built from ``Bottleneck``s.
 
@@ -875,13 +933,15 @@ class ResNetEngine:
     gradient (a view of the flat gradient buffer); ``on_ready(param)`` is
     called once that gradient is final (DP bucket launch)."""
 
-    def __init__(self, model: ResNet, backend: str = "auto", grad_view=None, on_ready=None):
+    def __init__(self, model: ResNet, backend: str = "auto", grad_view=None, on_ready=None,
+                 options: EngineOptions | None = None):
         self.model = model
         p = next(model.parameters())
         self.dev = p.device
         if backend == "auto":
             backend = "hip" if self.dev.type == "cuda" else "torch"
-        self.K = HipKernels(self.dev) if backend == "hip" else TorchKernels(self.dev)
+        o = self.opts = options or EngineOptions.from_env()
+        self.K = HipKernels(self.dev, fuse_fin=o.bn_fin != "kernel") if backend == "hip" else TorchKernels(self.dev)
         self.grad_view = grad_view or self._own_grad
         self.on_ready = on_ready or (lambda prm: None)
         self.bn = {}
@@ -894,15 +954,16 @@ class ResNetEngine:
         assert len(self.blocks) == len(model.layers), "engine supports Bottleneck stacks only"
         self._wt_ptrs = None
         self._wt_buf = {}
-        # 3x3 forward convs and weight gradients on the LDS-DMA implicit-GEMM kernels
-        # (KDL_CONV3=miopen: MIOpen + a separate statistics pass + gradient copies;
-        # per-layer A/B: profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl, r02_wgrad_dma_vs_reg_vs_miopen.jsonl)
-        self.conv3_native = os.environ.get("KDL_CONV3", "kdl") != "miopen" and all(
-            b.conv2.in_channels % 64 == 0 and b.conv2.out_channels % 64 == 0 for b in self.blocks)
-        # stride-2 3x3 data gradients as sub-pixel class GEMMs (KDL_DGRAD_S2=0: MIOpen)
-        self.dgrad_s2 = self.conv3_native and os.environ.get("KDL_DGRAD_S2", "1") == "1"
-        # Weight gradients on a second HIP stream (default; KDL_WGRAD_STREAM=0 turns
-        # it off -- 10.7k -> 11.3k img/s at batch 256, profiles/): a wgrad
+        # 3x3 forward convs, data and weight gradients on the kdl implicit-GEMM /
+        # halo / sub-pixel kernels (per-layer A/B vs MIOpen:
+        # profiles/r02_igemm_v1_vs_reg_vs_miopen.jsonl, r02_wgrad_dma_vs_reg_vs_miopen.jsonl,
+        # r02_dgrad_s2_vs_miopen.jsonl): their operand chunks are 64 channels wide
+        if self.K.name == "hip" and not all(b.conv2.in_channels % 64 == 0 and b.conv2.out_channels % 64 == 0
+                                            for b in self.blocks):
+            raise ValueError("the HIP engine's 3x3 kernels need channel counts that are multiples of 64 "
+                             "(use backend='torch' or the autograd model for other widths)")
+        # Weight gradients on a second HIP stream (default; EngineOptions.side = False
+        # turns it off -- 10.7k -> 11.3k img/s at batch 256, profiles/): a wgrad
         # depends only on its layer's output gradient and saved input, and nothing
         # in the rest of backward reads it, so it runs concurrently with the next
         # layers' BN-backward / data-gradient kernels on the main stream.  The
@@ -910,9 +971,9 @@ class ResNetEngine:
         # (csrc/bn_act.hip ws_bcoef) so a wgrad's recomputed BN never races the
         # main stream's backward finalize of the same BN.
         # BN-backward apply passes of bn3 / downsample BN / bn1 fused into their
-        # 1x1 data-gradient GEMMs (csrc/conv1x1.hip PRO_BWD); KDL_BN_BWD_FUSE=0: separate passes
+        # 1x1 data-gradient GEMMs (csrc/conv1x1.hip PRO_BWD); bn_bwd_fuse = 0: separate passes
         # (1: dgrad A prologue + write-through; 2: dgrad A prologue + weight-gradient G
-        # prologue, never materialised), for BNs of at most KDL_BN_BWD_FUSE_KMAX channels.
+        # prologue, never materialised), for BNs of at most bn_bwd_fuse_kmax channels.
         # Per-layer A/B (profiles/r03_bn_bwd_fuse_layers.jsonl, apply + dgrad vs fused
         # dgrad, uncontended): mode 1 wins where the dgrad has ONE output-channel tile
         # -- bn3 / downsample BN into conv3 / downsample dgrads at K = 4C <= 512
@@ -927,47 +988,46 @@ class ResNetEngine:
         # then the GEMM that applies BN3 + residual + ReLU in its epilogue --, the
         # successor's RESBITS GEMM recomputes c3 tiles for BN3's backward sums,
         # and BN3's backward apply reaches conv3's data / weight gradients folded
-        # into the weights.  KDL_RECOMP=0: off; KDL_RECOMP_MAXC: widest 4C served.
+        # into the weights.  EngineOptions.recomp = widest 4C served (0: off).
         # Measured (profiles/r03_step_1stream_*.txt, docs/perf_notes.md): at the 56x56 stage
         # (4C = 256) forward conv3 + BN3 apply 400 -> 290 us and conv3 dgrad 275 -> 160 us
         # per block against +50-100 us in the successor's RESBITS, the main stream 0.47 ms
         # shorter per step -- but the folded weight gradient lengthens the side stream's
         # tail, and the job-path step measured 13,216-13,227 (on) vs 13,233-13,264 img/s
         # (off); at 28x28 the recomputing RESBITS (+80-150 us) outweighs the rest.  Opt-in:
-        # KDL_RECOMP=1 (4C <= KDL_RECOMP_MAXC, default 256).
-        maxc = min(512, int(os.environ.get("KDL_RECOMP_MAXC", "256"))) if os.environ.get("KDL_RECOMP", "0") == "1" else 0
+        # KDL_ENGINE=recomp=256.
+        maxc = min(512, o.recomp)
         nb = len(self.blocks)
         self.recomp = [b.down_conv is None and i < nb - 1 and b.conv3.out_channels <= maxc
                        for i, b in enumerate(self.blocks)]
-        # downsample branch conv of the forward on the side stream (KDL_FWD_DOWN_SIDE=0: in
+        # downsample branch conv of the forward on the side stream (down_side = False: in
         # line): 13,333-13,347 vs 13,252-13,279 img/s, profiles/r03b_fwd_down_side_ab.txt
-        self.down_side = os.environ.get("KDL_FWD_DOWN_SIDE", "1") == "1"
+        self.down_side = o.down_side
         # the closing BN3 + residual + ReLU of a block whose successor has no
         # downsample branch, applied in the successor's conv1 A staging and written
         # through (csrc/conv1x1.hip PRO_RES) instead of its own pass, up to
-        # KDL_RES_PRO_KMAX channels (the register-staged loop; beyond, the LDS-DMA
-        # GEMM + apply pass); KDL_RES_PRO=0: apply pass
-        self.res_pro_kmax = int(os.environ.get("KDL_RES_PRO_KMAX", "512")) \
-            if os.environ.get("KDL_RES_PRO", "1") == "1" else 0
+        # res_pro_kmax channels (the register-staged loop; beyond, the LDS-DMA
+        # GEMM + apply pass); 0: apply pass
+        self.res_pro_kmax = o.res_pro_kmax
         # ... also before a downsample block (its conv1 then runs before the side-stream
         # downsample conv, which reads the written-through block output)
-        self.res_pro_down = os.environ.get("KDL_RES_PRO_DOWN", "1") == "1"
+        self.res_pro_down = o.res_pro_down
         # ... and after a downsample block: the residual is the downsample branch's BN
         # output, applied in the same prologue (PRO_RES2)
-        self.res_pro_dual = os.environ.get("KDL_RES_PRO_DUAL", "1") == "1"
+        self.res_pro_dual = o.res_pro_dual
         # bn1 + ReLU of the stride-1 56x56 3x3 convs applied inside the halo kernels,
-        # which stage the input halo in LDS and transform it there (KDL_HALO_PRO):
+        # which stage the input halo in LDS and transform it there (halo_pro):
         # 1 = the forward conv does, writing a1 = relu(B1(c1)) through for the weight
         # gradient (no apply pass); 2 = the weight gradient transforms its halo too
         # (a1 never written); 0 = apply pass
-        self.halo_pro = int(os.environ.get("KDL_HALO_PRO", "1")) if os.environ.get("KDL_HALO", "1") != "0" else 0
-        self.fuse_bwd = int(os.environ.get("KDL_BN_BWD_FUSE", "1"))
-        self.fuse_kmax = int(os.environ.get("KDL_BN_BWD_FUSE_KMAX", "512"))
-        self.fuse_bn1 = os.environ.get("KDL_BN_BWD_FUSE_BN1", "0") == "1"
+        self.halo_pro = o.halo_pro
+        self.fuse_bwd = o.bn_bwd_fuse
+        self.fuse_kmax = o.bn_bwd_fuse_kmax
+        self.fuse_bn1 = o.bn_bwd_fuse_bn1
         self.side = None
-        if self.K.name == "hip" and os.environ.get("KDL_WGRAD_STREAM", "1") == "1":
+        if self.K.name == "hip" and o.side:
             from kubedl_amd.ops.streams import side_stream
-            self.side = side_stream(self.dev, int(os.environ.get("KDL_SIDE_PRIO", "0")))  # (ops/streams.py)
+            self.side = side_stream(self.dev, o.side_prio)  # (ops/streams.py)
             # overlapped with the main stream, the 1x1 weight gradients gain from 256x256
             # tiles too (fewer, heavier side-stream blocks; csrc/conv1x1.hip wgrad_tiles)
             self.K.ext.set_wgrad_big(2)
@@ -982,7 +1042,7 @@ class ResNetEngine:
             return
         convs = [c for b in self.blocks for c in (b.conv1, b.conv3, b.down_conv) if c is not None]
         c3s = [b.conv2 for b in self.blocks if b.conv2.stride[0] == 1]
-        c3s2 = [b.conv2 for b in self.blocks if b.conv2.stride[0] == 2] if self.dgrad_s2 else []
+        c3s2 = [b.conv2 for b in self.blocks if b.conv2.stride[0] == 2]
         ptrs = tuple(c.weight.data_ptr() for c in convs + c3s + c3s2)
         if ptrs != self._wt_ptrs:
             rows = []
@@ -1125,25 +1185,19 @@ class ResNetEngine:
             if c1 is None:
                 c1 = K.conv1x1_fwd(cur, blk.conv1.weight.view(blk.conv1.out_channels, -1), 1, None, st1)
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
-            if self.conv3_native and self._halo_pro_ok(c1, s):
+            if self._halo_pro_ok(c1, s):
                 # the conv applies B1 + ReLU to its input halo (csrc/halo3x3.hip) and
                 # writes a1 through (mode 1) or a1 is never stored (mode 2)
                 a1 = torch.empty_like(c1) if self.halo_pro == 1 else None
                 c2 = K.conv3x3_fwd(c1, blk.conv2.weight, s, st2, pro=st1, aout=a1)
                 ho, wo = c2.shape[-2:]
                 K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
-            elif self.conv3_native:
+            else:
                 a1, _ = K.bn_apply(c1, st1, relu=True)
                 # implicit GEMM + B2 statistics in the epilogue (shift = running mean)
                 c2 = K.conv3x3_fwd(a1, blk.conv2.weight, s, st2)
                 ho, wo = c2.shape[-2:]
                 K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
-            else:
-                a1, _ = K.bn_apply(c1, st1, relu=True)
-                c2 = F.conv2d(a1, blk.conv2.weight, stride=s, padding=1).contiguous(memory_format=torch.channels_last)
-                ho, wo = c2.shape[-2:]
-                K.bn_stats(c2, st2)
-                K.bn_finalize(st2, n * ho * wo, x=c2)
             if self.recomp[bi]:  # conv3 never stored: statistics pass, then the applying GEMM
                 w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
                 K.conv1x1_stats(c2, w3, st2, st3)
@@ -1224,15 +1278,10 @@ class ResNetEngine:
         return self.halo_pro > 0 and self.K.name == "hip" and stride == 1 and c == 64 and h == 56 and w == 56
 
     def _wgrad3x3(self, g, a, stride, weight, pro=None):
-        """conv2's weight gradient: the implicit-GEMM kernel writing straight into
-        the gradient buffer, or (KDL_CONV3=miopen) MIOpen + a copy; ``pro``: ``a``
-        is the BN input and the operand relu(B_pro(a)) (halo kernel prologue)."""
-        if self.conv3_native:
-            self.K.wgrad3x3(g, a, stride, self._g(weight), pro=pro)
-        else:
-            _, dw, _ = torch.ops.aten.convolution_backward(
-                g, a, weight, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
-            self._g(weight).copy_(dw)
+        """conv2's weight gradient: the implicit-GEMM / halo kernel writing straight
+        into the gradient buffer; ``pro``: ``a`` is the BN input and the operand
+        relu(B_pro(a)) (halo kernel prologue)."""
+        self.K.wgrad3x3(g, a, stride, self._g(weight), pro=pro)
 
     def _fuse_mode(self, C: int, bn1: bool = False) -> int:
         """How the BN-backward apply of a C-channel BN reaches its 1x1 consumers:
@@ -1334,7 +1383,7 @@ class ResNetEngine:
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
                 dc1 = None
-            elif self.dgrad_s2 and c1.shape[-2:] == (2 * dc2.shape[-2], 2 * dc2.shape[-1]):
+            elif c1.shape[-2:] == (2 * dc2.shape[-2], 2 * dc2.shape[-1]):
                 # stride 2: four sub-pixel class GEMMs with bn1's mask + sums fused
                 # (no MIOpen, no zero-filled dx, no separate BN-backward reduce pass)
                 with self._on_side(dc2):
@@ -1344,20 +1393,11 @@ class ResNetEngine:
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
                 dc1 = None
-            else:
-                if self.side is None:
-                    da1, dw2, _ = torch.ops.aten.convolution_backward(
-                        dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                        [True, True, False])
-                    self._g(blk.conv2.weight).copy_(dw2)
-                else:  # weight gradient on the side stream, data gradient on the main one
-                    with self._on_side(dc2):
-                        self._wgrad3x3(dc2, a1, s, blk.conv2.weight)
-                    da1, _, _ = torch.ops.aten.convolution_backward(
-                        dc2, a1, blk.conv2.weight, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                        [True, False, False])
+            else:  # odd input size at a stride-2 block: the reference backend only
+                with self._on_side(dc2):
+                    self._wgrad3x3(dc2, a1, s, blk.conv2.weight)
                 self.on_ready(blk.conv2.weight)
-                dc1 = K.bn_bwd_full(da1.contiguous(memory_format=torch.channels_last), c1, st1, *self._bn_grads(st1))
+                dc1 = K.dgrad3x3_strided_bn(dc2, blk.conv2.weight, s, c1, st1, *self._bn_grads(st1))
             self._bn_ready(st1)
             # bn1 backward apply: its own pass, or (fused) inside conv1's dgrad below
             op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1, bn1=True)

@@ -1,5 +1,5 @@
 """Diagnostic: per-tensor differences of the engine's gradients between
-KDL_WGRAD_STREAM=0 runs (baseline noise) and =1 runs (side-stream wgrads)."""
+KDL_ENGINE=side=0 runs (baseline noise) and side=1 runs (side-stream wgrads)."""
 import os
 import sys
 
@@ -11,7 +11,7 @@ from kubedl_amd.models.resnet_engine import ResNetEngine  # noqa: E402
 
 
 def run(flag, steps=int(os.environ.get("DIAG_STEPS", "2"))):
-    os.environ["KDL_WGRAD_STREAM"] = flag
+    os.environ["KDL_ENGINE"] = f"side={flag}"
     model, _, x, y = _setup((2, 2, 2, 2), 64, "cuda", int(os.environ.get("DIAG_IMAGE", "96")), int(os.environ.get("DIAG_BATCH", "8")))
     eng = ResNetEngine(model, backend="hip")
     for _ in range(steps):

@@ -41,7 +41,7 @@ want bench2 && run_step bench_job2 600 python bench.py --gpus 1 --steps 20 --war
 want benchab && run_step bench_torch 600 python bench.py --direct --steps 20 --warmup 8 --bn-backend torch
 want prof   && run_step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --direct --steps 5 --warmup 3
 if want prof1s; then
-  KDL_WGRAD_STREAM=0 run_step prof_1stream 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1s -o run -- python bench.py --direct --steps 5 --warmup 3
+  KDL_ENGINE=side=0 run_step prof_1stream 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1s -o run -- python bench.py --direct --steps 5 --warmup 3
 fi
 want benchfind && run_step bench_find 900 python bench.py --direct --steps 20 --warmup 8 --conv-benchmark 1
 want launch && run_step bench_launch 600 python -m kubedl_amd.cli bench-launch --jobs 1 --gpus 1 --steps 20 --warmup 5

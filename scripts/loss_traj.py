@@ -1,5 +1,5 @@
 """Loss trajectory of the ResNet-50 training step under one configuration
-(env switches such as KDL_WGRAD_STREAM / KDL_BN_BWD_FUSE / AMD_SERIALIZE_KERNEL
+(env switches such as KDL_ENGINE=side=0,bn_bwd_fuse=0 / AMD_SERIALIZE_KERNEL
 apply as usual): prints one JSON line with the per-step losses and a weight
 checksum, so configurations that must compute the same thing can be compared.
 

@@ -1,6 +1,6 @@
 """Multi-step engine run reporting, per step, the parameters whose gradient or
 master weight is non-finite / huge (first offenders by flat order).
-usage: traj_diag.py [steps] [batch] [autograd_first]   (env: KDL_RECOMP, KDL_WGRAD_STREAM, ...)
+usage: traj_diag.py [steps] [batch] [autograd_first]   (env: KDL_ENGINE=recomp=256,side=0 ...)
 autograd_first = 1: run the autograd trainer for ``steps`` first in the same
 process (as tests/test_trajectory_gpu.py's truth fixture does)"""
 import json

@@ -95,7 +95,7 @@ def test_engine_recompute_blocks_match_autograd_fp32(recomp, monkeypatch):
     autograd, and as the engine with every c3 materialised."""
     import kubedl_amd.models.resnet_engine as RE
     monkeypatch.setattr(RE, "_bfr", lambda t: t.float())
-    monkeypatch.setenv("KDL_RECOMP", recomp)
+    monkeypatch.setenv("KDL_ENGINE", "recomp=256" if recomp == "1" else "")
     torch.manual_seed(0)
     model = ResNet((3, 2, 2, 2), num_classes=10, width=8)
     with torch.no_grad():
@@ -202,7 +202,7 @@ def test_engine_hip_matches_autograd(layers, image, batch, wgrad_stream, monkeyp
     stream rewrites -- shows up as a gradient far off the fp32 truth).  The two
     schedules are not compared with each other: the first MIOpen call of a
     process may pick a different solver, so runs differ at bf16-noise level."""
-    monkeypatch.setenv("KDL_WGRAD_STREAM", wgrad_stream)
+    monkeypatch.setenv("KDL_ENGINE", f"side={wgrad_stream}")
     model, ref, x, y = _setup(layers, 64, "cuda", image, batch)
     truth, tloss = _truth_of(ref, x, y)
     eng = ResNetEngine(model, backend="hip")
@@ -228,7 +228,7 @@ def test_engine_hip_full_resnet50_224_matches_fp32_truth(batch):
     model, ref, x, y = _setup((3, 4, 6, 3), 64, "cuda", 224, batch, classes=1000)
     truth, tloss = _truth_of(ref, x, y)
     eng = ResNetEngine(model, backend="hip")
-    assert eng.conv3_native and eng.side is not None
+    assert eng.side is not None
     loss = eng.forward_backward(x, y)
     _ref_step(ref, x, y)
     torch.cuda.synchronize()
@@ -331,12 +331,12 @@ def test_engine_ddp_two_ranks_hip_gpu():
 @pytest.mark.gpu
 def test_engine_bn_finalize_in_gemm_matches_kernel_finalize(monkeypatch):
     """BN finalize folded into the producing GEMMs' last arriving blocks
-    (csrc/bn_fin.h, KDL_BN_FIN=gemm) vs the separate finalize launches
-    (KDL_BN_FIN=kernel): the difference must be at the level of two runs of the
+    (csrc/bn_fin.h, KDL_ENGINE=bn_fin=gemm) vs the separate finalize launches
+    (KDL_ENGINE=bn_fin=kernel): the difference must be at the level of two runs of the
     same mode (replica atomics make BN sums order-nondeterministic)."""
     results = []
     for mode in ("kernel", "kernel", "gemm"):
-        monkeypatch.setenv("KDL_BN_FIN", mode)
+        monkeypatch.setenv("KDL_ENGINE", f"bn_fin={mode}")
         model, ref, x, y = _setup((2, 2, 2, 2), 64, "cuda", 112, 16, classes=10, seed=3)
         eng = ResNetEngine(model, backend="hip")
         assert eng.K.fuse_fin == (mode == "gemm")
@@ -361,3 +361,17 @@ def test_engine_bn_finalize_in_gemm_matches_kernel_finalize(monkeypatch):
     bfused = rel(results[2][2], results[0][2])
     for n in bfused:
         assert bfused[n] <= 3 * bnoise[n] + 1e-4, (n, bfused[n], bnoise[n])
+
+
+def test_engine_options_from_one_variable(monkeypatch):
+    """the engine's schedule variants are one dataclass whose
+    defaults are the measured winners; A/B overrides come from KDL_ENGINE only."""
+    from kubedl_amd.models.resnet_engine import EngineOptions
+    monkeypatch.delenv("KDL_ENGINE", raising=False)
+    assert EngineOptions.from_env() == EngineOptions()
+    monkeypatch.setenv("KDL_ENGINE", "side=0, recomp=256,bn_fin=kernel,halo_pro=2")
+    o = EngineOptions.from_env()
+    assert (o.side, o.recomp, o.bn_fin, o.halo_pro) == (False, 256, "kernel", 2)
+    monkeypatch.setenv("KDL_ENGINE", "no_such_knob=1")
+    with pytest.raises(ValueError, match="unknown option"):
+        EngineOptions.from_env()

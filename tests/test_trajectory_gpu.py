@@ -13,7 +13,7 @@ STEPS = 6
 
 
 def _traj(monkeypatch, engine, side="1", batch=64):
-    monkeypatch.setenv("KDL_WGRAD_STREAM", side)
+    monkeypatch.setenv("KDL_ENGINE", f"side={side}")
     from kubedl_amd.parallel.dist import DistInfo
     from kubedl_amd.workers.resnet50 import ResNetTrainer
     info = DistInfo(0, 1, 0, torch.device("cuda", 0), "nccl")
