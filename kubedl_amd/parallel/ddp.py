@@ -73,6 +73,11 @@ class FlatDDP:
         self._hooks = []
         self.transport = None
         self.reduce_fp32 = reduce_fp32_wanted()
+        # timing: per-step device time the caller's stream waits for the buckets
+        # in finish() (the EXPOSED all-reduce time; everything else overlapped the
+        # backward) -- CUDA events, read once by exposed_ms()
+        self.timing = False
+        self._tev = []
         # producers on a second stream (the ResNet engine's weight-gradient
         # stream): a bucket's collective is issued on that stream after it has
         # joined the current one, so it waits for both without stalling the
@@ -158,6 +163,10 @@ class FlatDDP:
         for b in self.buckets:
             if b.handle is None:
                 self._launch(b)
+        timed = self.timing and self.space.grad.is_cuda
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         for b in self.buckets:
             b.handle.wait()
             b.handle = None
@@ -167,12 +176,37 @@ class FlatDDP:
                 if b.wide.is_cuda:  # allocated on the join stream, last read here
                     b.wide.record_stream(torch.cuda.current_stream())
                 b.wide = None
+        if timed:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._tev.append((e0, e1))
         if self.transport is not None:
             # bits of EARLIER steps only (no sync here); the authoritative check
             # follows a device sync: ResNetTrainer.check_transport, run before
             # every checkpoint and after the last step
             self.transport.check()
         self.space.mark_packed()
+
+    def exposed_ms(self, reset: bool = True) -> float | None:
+        """Mean device time per step the compute stream waited for the bucket
+        collectives (syncs on the recorded events)."""
+        if not self._tev:
+            return None
+        self._tev[-1][1].synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self._tev) / len(self._tev)
+        if reset:
+            self._tev.clear()
+        return ms
+
+    def describe(self) -> dict:
+        """The bucket plan (bench JSON ``ddp`` block)."""
+        esz = self.space.grad.element_size()
+        return {"active": self.active, "world": self.world,
+                "transport": ("p2p" if self.transport is not None else "rccl") if self.active else None,
+                "buckets": len(self.buckets),
+                "bucket_mb": [round((b.hi - b.lo) * esz / 2 ** 20, 2) for b in self.buckets],
+                "grad_mb": round(self.space.numel * esz / 2 ** 20, 2),
+                "reduce_dtype": "fp32" if self.reduce_fp32 else str(self.space.grad.dtype).replace("torch.", "")}
 
     @property
     def grad_scale(self) -> float:

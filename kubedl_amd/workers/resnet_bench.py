@@ -108,6 +108,9 @@ def run(args, launcher: str) -> int:
     sync(info)
     kdist.barrier(info)
     sync(info)
+    ddp = getattr(trainer, "ddp", None)
+    if ddp is not None and ddp.active and info.device.type == "cuda":
+        ddp.timing = True  # two events per step around the bucket waits (exposed time)
     t0 = time.perf_counter()
     host = 0.0  # time spent issuing the steps (no sync): = ms_per_step when host-bound
     for _ in range(args.steps):
@@ -118,6 +121,11 @@ def run(args, launcher: str) -> int:
     kdist.barrier(info)
     sync(info)
     dt = kdist.all_reduce_max(time.perf_counter() - t0, info)
+    ddp_block = ddp.describe() if ddp is not None else None
+    if ddp_block is not None:
+        ex = ddp.exposed_ms() if ddp.timing else None
+        ddp_block["exposed_ms_per_step"] = round(ex, 3) if ex is not None else None
+        ddp.timing = False
     trainer.check_transport()  # a timed-out P2P all-reduce must fail the run, not report a number
     loss = float(trainer.loss().float().item())
 
@@ -163,6 +171,9 @@ def run(args, launcher: str) -> int:
             "t_first_step_unix": round(t_first_step, 3) if t_first_step else None,
             "host_issue_ms_per_step": round(host / args.steps * 1e3, 3),
             "final_loss": round(loss, 4),
+            # DP gradient buckets: plan + the all-reduce time the step's compute
+            # stream waited for (the rest overlapped the backward)
+            "ddp": ddp_block,
         }
         print(json.dumps(out), flush=True)
     kdist.shutdown(info)

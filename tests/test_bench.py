@@ -64,6 +64,12 @@ def test_bench_contract_two_ranks_cpu():
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
     assert line["config"]["global_batch"] == 16 and line["config"]["allreduce"] == "rccl"
     assert abs(line["value"] - 16 * 1000.0 / line["ms_per_step"]) / line["value"] < 0.01
+    # the DP bucket plan in the JSON (CPU: no device events, so
+    # no exposed time; the GPU bench reports it)
+    d = line["ddp"]
+    assert d["active"] and d["world"] == 2 and d["transport"] == "rccl" and d["buckets"] >= 1
+    assert abs(sum(d["bucket_mb"]) - d["grad_mb"]) < 0.05 * d["grad_mb"] + 0.01
+    assert "exposed_ms_per_step" in d
 
 
 import pytest  # noqa: E402
