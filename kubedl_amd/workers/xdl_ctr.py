@@ -94,12 +94,14 @@ def main(argv=None) -> int:
     if use_gpu:
         torch.cuda.set_device(device)
         kdist.apply_hbm_limit(device)
-    backend = "nccl" if use_gpu else "gloo"
+    # KDL_DIST_BACKEND=gloo: rehearse a multi-rank job on fewer GPUs than ranks
+    # (RCCL refuses two ranks on one device; parallel/dist.py init_from_env)
+    backend = os.environ.get("KDL_DIST_BACKEND", "nccl") if use_gpu else "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
     common.signal_ready({"rank": rank, "task": task})

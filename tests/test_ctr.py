@@ -424,3 +424,50 @@ def test_xdl_worker_takes_its_device_from_the_rank_env(monkeypatch, env, want):
     with pytest.raises(Stop) as e:
         xdl_ctr.main(["--steps", "1"])
     assert e.value.args[0] == torch.device("cuda", want)
+
+
+def _gpu_exchange_worker(rank, world, port, out):
+    """Two ranks sharing the box's one GPU over gloo: the fixed-capacity exchange
+    with the device dedup / CSR / segment-Adagrad kernels (the ADVICE r3 path:
+    padding rows, long hot-id segments)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    for dev in ("cuda", "cpu"):
+        emb = ShardedEmbedding(1 << 20, 16, [0, 1], rank, world, dev, lr=0.1, max_ids=4096, slack=1.5)
+        assert emb.use_hip == (dev == "cuda")
+        g = torch.Generator().manual_seed(50 + rank)
+        for step in range(6):
+            ids = torch.randint(0, 1 << 20, (4096,), generator=g)
+            ids[: 1500] = 12345  # a hot id: one segment far longer than a wave
+            rows, inv = emb.pull(ids.to(dev))
+            u = _uniq_of(rows.cpu(), inv.cpu(), ids)
+            emb.push(_grad_of(u, 16).to(dev))
+        res[dev] = (emb.table.cpu(), emb.accum.cpu(), emb.finalize())
+    out[f"r{rank}"] = res
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ctr_fixed_exchange_two_ranks_on_gpu_matches_cpu():
+    """the multi-rank fixed-capacity exchange ON THE GPU (dedup
+    kernels, padding kept out of the owner update, long-segment sort) lands on
+    the same tables as the CPU path; capacity shrinks with no overflow."""
+    import torch.multiprocessing as mp
+    port = _port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_gpu_exchange_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        res = out[f"r{r}"]
+        (tg, ag, sg), (tc, ac, sc) = res["cuda"], res["cpu"]
+        torch.testing.assert_close(tg, tc, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(ag, ac, atol=1e-5, rtol=1e-5)
+        assert sg["exchange_overflow_steps"] == 0 and sg["exchange_cap"] < 4096
