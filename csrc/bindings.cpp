@@ -1162,45 +1162,49 @@ void conv3x3_gemm(const at::Tensor& A, const at::Tensor& W, at::Tensor C, int64_
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv3x3_gemm");
 }
 
-// ResNet stem 7x7 / stride 2 / pad 3 conv, 224x224x3 -> 112x112x64 (csrc/stem.hip).
+// ResNet stem 7x7 / stride 2 / pad 3 conv, [Nb, 3, H, W] -> [Nb, 64, OH, OW] (csrc/stem.hip).
 void stem7x7_fwd(const at::Tensor& x, const at::Tensor& wp, at::Tensor y, const c10::optional<at::Tensor>& shift,
                  const c10::optional<at::Tensor>& acc) {
-  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && x.size(2) == 224 && x.size(3) == 224 && is_nhwc_dense(x),
-              "stem7x7_fwd: x must be [Nb, 3, 224, 224] channels_last");
-  const int64_t Nb = x.size(0);
-  need_bf16(x, Nb * 224 * 224 * 3, "stem7x7_fwd x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && is_nhwc_dense(x), "stem7x7_fwd: x must be [Nb, 3, H, W] channels_last");
+  const int64_t Nb = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  need_bf16(x, Nb * H * W * 3, "stem7x7_fwd x");
   // wp: the nn.Conv2d weight [64, 3, 7, 7] (reordered inside the kernel) or [64, 224] in K order
   const bool raw_w = wp.numel() == 64 * 3 * 7 * 7;
   need_bf16(wp, raw_w ? 64 * 147 : 64 * 224, "stem7x7_fwd wp");
-  need_bf16(y, Nb * 112 * 112 * 64, "stem7x7_fwd y");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == Nb && y.size(1) == 64 && y.size(2) == OH && y.size(3) == OW,
+              "stem7x7_fwd: y must be [Nb, 64, OH, OW]");
+  need_bf16(y, Nb * OH * OW * 64, "stem7x7_fwd y");
+  TORCH_CHECK(Nb * OH * OW * 128 < (int64_t(1) << 31), "stem7x7_fwd: 32-bit row offsets");
   TORCH_CHECK(!opt_ptr(acc) || opt_ptr(shift), "stem7x7_fwd: statistics need a shift");
   need_opt_f32(shift, 64, "shift");
   need_opt_f32(acc, 32 * 2 * 64, "acc");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  check_hip(kdl::stem7x7_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), static_cast<int>(Nb), opt_fptr(shift),
-                             opt_fptr(acc), cur_stream(), raw_w),
+  check_hip(kdl::stem7x7_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), static_cast<int>(Nb), static_cast<int>(H),
+                             static_cast<int>(W), opt_fptr(shift), opt_fptr(acc), cur_stream(), raw_w),
             "stem7x7_fwd");
 }
 
 // stem weight gradient -> dW [64][224] bf16 (kubedl_amd.ops.conv.stem_weights K order)
+// or [64, 3, 7, 7] channels_last (the parameter's own layout)
 void stem7x7_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor dw32, at::Tensor dW) {
-  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && x.size(2) == 224 && x.size(3) == 224 && is_nhwc_dense(x),
-              "stem7x7_wgrad: x must be [Nb, 3, 224, 224] channels_last");
-  const int64_t Nb = x.size(0);
-  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == Nb && dy.size(1) == 64 && dy.size(2) == 112 && dy.size(3) == 112 &&
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && is_nhwc_dense(x), "stem7x7_wgrad: x must be [Nb, 3, H, W] channels_last");
+  const int64_t Nb = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == Nb && dy.size(1) == 64 && dy.size(2) == OH && dy.size(3) == OW &&
                   is_nhwc_dense(dy),
-              "stem7x7_wgrad: dy must be [Nb, 64, 112, 112] channels_last");
-  need_bf16(x, Nb * 224 * 224 * 3, "stem7x7_wgrad x");
-  need_bf16(dy, Nb * 112 * 112 * 64, "stem7x7_wgrad dy");
+              "stem7x7_wgrad: dy must be [Nb, 64, OH, OW] channels_last");
+  need_bf16(x, Nb * H * W * 3, "stem7x7_wgrad x");
+  need_bf16(dy, Nb * OH * OW * 64, "stem7x7_wgrad dy");
   const bool raw_out = dW.numel() == 64 * 3 * 7 * 7;  // [64, 3, 7, 7] (else [64, 224] K order)
   need_bf16(dW, raw_out ? 64 * 147 : 64 * 224, "stem7x7_wgrad dW");
-  const int64_t slabs = kdl::stem7x7_wgrad_slabs(static_cast<int>(Nb));
+  const int64_t slabs = kdl::stem7x7_wgrad_slabs(static_cast<int>(Nb), static_cast<int>(H), static_cast<int>(W));
   TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
                   dw32.numel() >= slabs * 64 * 224,
-              "stem7x7_wgrad: dw32 must hold stem7x7_wgrad_slabs(Nb) x 64 x 224 fp32");
+              "stem7x7_wgrad: dw32 must hold stem7x7_wgrad_slabs(Nb, H, W) x 64 x 224 fp32");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check_hip(kdl::stem7x7_wgrad(dy.data_ptr(), x.data_ptr(), dw32.data_ptr<float>(), dW.data_ptr(),
-                               static_cast<int>(Nb), cur_stream(), raw_out),
+                               static_cast<int>(Nb), static_cast<int>(H), static_cast<int>(W), cur_stream(), raw_out),
             "stem7x7_wgrad");
 }
 
@@ -1638,8 +1642,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fin_desc", &bn_fin_desc, "write a BN layer's finalize descriptor into its workspace tail");
   m.def("stem7x7_wgrad_bn", &stem7x7_wgrad_bn, "stem weight gradient with the stem BN+ReLU+max-pool backward folded in");
   m.def("stem7x7_wgrad", &stem7x7_wgrad, "ResNet stem 7x7/s2/p3 conv weight gradient -> [64][224] bf16 (stem K order)");
-  m.def("stem7x7_wgrad_slabs", [](int64_t nb) { return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb)); },
-        "fp32 slab count of stem7x7_wgrad's workspace");
+  m.def("stem7x7_wgrad_slabs", [](int64_t nb, int64_t h, int64_t w) {
+          return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb), static_cast<int>(h), static_cast<int>(w)); },
+        "fp32 slab count of stem7x7_wgrad's workspace", py::arg("nb"), py::arg("h") = 224, py::arg("w") = 224);
   m.def("head_splits", &head_splits, "K splits (fc forward, dfeat) of the classifier head kernels");
   m.def("head_forward", &head_forward, "classifier head forward: mean pool + fc (MFMA) + softmax CE + dlogits");
   m.def("head_backward", &head_backward, "classifier head backward: dfeat, dW, db (MFMA) + mean loss");

@@ -45,7 +45,11 @@ constexpr int kRep = 32;  // replica count of the BN workspace (== bn_act.hip kR
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4, EPI_APPLY = 5, EPI_RSTATS = 6 };
 // A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s) |
 // data gradient of a stride-2 3x3 pad-1 conv as four sub-pixel class GEMMs (csrc/igemm.hip)
-enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2, G_DGRAD2 = 3 };
+// G_STEM (csrc/stem.hip): a tile is 2 output rows x 112 columns of one image
+// (column chunk cc of ceil(OW / 112)); GEMM row m = 224 tile + l maps to output
+// pixel (2 tr + l / 112, 112 cc + l % 112), masked past OH / OW.  Params: Hout
+// = OH, Wout = OW, Hin = tile rows per image (ceil(OH / 2)), Win = column chunks.
+enum { G_DENSE = 0, G_STRIDED = 1, G_CONV3 = 2, G_DGRAD2 = 3, G_STEM = 4 };
 
 struct GemmParams {
   const bf16_t* A;
@@ -246,7 +250,15 @@ struct Epilogue {
 
   // output row of GEMM row m (-1: padding row past M / past a class's rows)
   __device__ __forceinline__ int row_of(const GemmParams& p, int m) const {
-    if constexpr (GATHER == G_DGRAD2) {
+    if constexpr (GATHER == G_STEM) {
+      if (p.Wout == 112 && (p.Hout & 1) == 0) return m < p.M ? m : -1;  // 224-px images: identity
+      const int tm = m / 224, l = m - tm * 224;
+      const int per = p.Hin * p.Win, img = tm / per, rem = tm - img * per;
+      const int tr = rem / p.Win, cc = rem - tr * p.Win;
+      const int oh = 2 * tr + (l >= 112 ? 1 : 0), ow = 112 * cc + (l >= 112 ? l - 112 : l);
+      if (oh >= p.Hout || ow >= p.Wout) return -1;
+      return (img * p.Hout + oh) * p.Wout + ow;
+    } else if constexpr (GATHER == G_DGRAD2) {
       const int cls = m / p.mc_pad, r = m - cls * p.mc_pad;
       if (r >= p.mc) return -1;
       const int hw = p.Hin * p.Win;

@@ -269,16 +269,18 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s);
 // forward replicas (STATS epilogue), else a plain store.
 // raw_w: wp is the nn.Conv2d weight [64][3][7][7] itself (reordered while the
 // kernel stages it), else [64][224] in stem_weights' K order.
-hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const float* shift, float* acc,
+// x [Nb, H, W, 3] NHWC (any H, W: 2-row x 112-column tiles, masked edges),
+// y [Nb, OH, OW, 64], OH = (H - 1) / 2 + 1.
+hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, int H, int W, const float* shift, float* acc,
                        hipStream_t s, bool raw_w = false);
-// stem weight gradient: dy [Nb, 112, 112, 64], x [Nb, 224, 224, 3] (NHWC bf16)
-// -> dW [64][224] bf16 in stem_weights' K order; dw32 = stem7x7_wgrad_slabs(Nb)
+// stem weight gradient: dy [Nb, OH, OW, 64], x [Nb, H, W, 3] (NHWC bf16)
+// -> dW [64][224] bf16 in stem_weights' K order; dw32 = stem7x7_wgrad_slabs(Nb, H, W)
 // x [64][224] fp32 slabs (no initialisation needed)
-int stem7x7_wgrad_slabs(int Nb);
+int stem7x7_wgrad_slabs(int Nb, int H = 224, int W = 224);
 // raw_out: dW is written as the nn.Conv2d gradient [64][3][7][7] instead.
-hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s,
+hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, int H, int W, hipStream_t s,
                          bool raw_out = false);
-// the same with the stem BN + ReLU + max-pool backward folded in: dy is built
+// the same with the stem BN + ReLU + max-pool backward folded in (224 x 224 only): dy is built
 // per tile from c0 [Nb, 112, 112, 64], the pooled gradient dp [Nb, 56, 56, 64],
 // its argmax bytes idx and coef5 = [5][64] (forward scale | shift, backward
 // k | c1 | c0 of the BN workspace, after bn_pool_backward(with_dx = false))

@@ -38,25 +38,92 @@ constexpr int kHC = 232;                 // halo pixels per row: iw = -3 .. 228 
 constexpr int kK = 224;                  // 7 r x 8 s x 4 c
 constexpr int kLDB = kK + 8;             // weight row stride (bf16): conflict-free fragment reads
 
-// The 9 input rows of a tile -> LDS halo [9][kHC][4] bf16 (channel 3 and the
-// column padding stay zero): thread-pairs of pixels, 12 B per global load
-// (one dwordx3), two 8-B LDS writes; rows outside the image are written as
-// zeros.  load() runs under the previous tile's MFMAs, store() after them.
+// Geometry of a stem launch.  A tile is two output rows x 112 columns of one
+// image (column chunk cc of ceil(OW / 112)), 224 GEMM rows; slots past OH / OW
+// are masked (the epilogue's G_STEM row map, csrc/gemm_epi.h).  At 224 x 224
+// (OH = OW = 112) a tile is two whole output rows and the map is the identity.
+struct StemGeo {
+  int H, W, OH, OW, TR, CC;  // TR = ceil(OH / 2) tile rows per image, CC = ceil(OW / 112)
+  __device__ __forceinline__ void tile(int tm, int& img, int& tr, int& cc) const {
+    const int per = TR * CC;
+    img = tm / per;
+    const int rem = tm - img * per;
+    tr = rem / CC;
+    cc = rem - tr * CC;
+  }
+  // output row (pixel index) of tile slot l in [0, 224), or -1 past OH / OW
+  __device__ __forceinline__ int out_row(int tm, int l) const {
+    int img, tr, cc;
+    tile(tm, img, tr, cc);
+    const int oh = 2 * tr + (l >= kOW ? 1 : 0), ow = kOW * cc + (l >= kOW ? l - kOW : l);
+    return (oh < OH && ow < OW) ? (img * OH + oh) * OW + ow : -1;
+  }
+};
+
+StemGeo stem_geo(int H, int W) {
+  StemGeo g;
+  g.H = H;
+  g.W = W;
+  g.OH = (H - 1) / 2 + 1;  // 7x7, stride 2, pad 3
+  g.OW = (W - 1) / 2 + 1;
+  g.TR = (g.OH + 1) / 2;
+  g.CC = (g.OW + kOW - 1) / kOW;
+  return g;
+}
+
+// The 9 input rows of a tile -> LDS halo [9][kHC][4] bf16 (channel 3 stays
+// zero): halo column j holds input column 224 cc - 3 + j.  Thread-pairs of
+// pixels, 12 B per global load (one dwordx3), two 8-B LDS writes; rows outside
+// the image are written as zeros.  load() runs under the previous tile's
+// MFMAs, store() after them.
+// GEN = false: 224 x 224 images (one column chunk; the halo's padding columns
+// 0..2 / 227.. are never written again after the kernel zeroes them).
+// GEN = true: any H x W -- pairs pr = -2 .. 113 (input columns 224 cc + 2 pr),
+// per-pixel loads at the image edge or in odd-width rows, zeros written for
+// pixels outside the image (every halo column a tile reads is rewritten, so
+// column chunks of different tiles never leak into each other).
+template <bool GEN>
 struct HaloStager {
-  static constexpr int kPairs = kHR * (kW / 2);           // 1008 pixel pairs per tile
+  static constexpr int kPPR = GEN ? kOW + 4 : kOW;        // pixel pairs per halo row
+  static constexpr int kP0 = GEN ? 2 : 0;                 // pr = j % kPPR - kP0
+  static constexpr int kPairs = kHR * kPPR;               // 1008 (224 px) / 1044 per tile
   static constexpr int kIt = (kPairs + kNT - 1) / kNT;    // 3 per thread
   uint3 v[kIt];
 
-  __device__ __forceinline__ void load(const bf16_t* x, int tm, int t) {
-    const int img = tm / (kOH / 2), ih0 = (tm - img * (kOH / 2)) * 4 - 3;
+  __device__ __forceinline__ void load(const bf16_t* x, int tm, int t, const StemGeo& g) {
+    int img, tr, cc;
+    if constexpr (GEN) {
+      g.tile(tm, img, tr, cc);
+    } else {
+      img = tm / (kOH / 2);
+      tr = tm - img * (kOH / 2);
+      cc = 0;
+    }
+    const int H = GEN ? g.H : kH, W = GEN ? g.W : kW;
+    const int ih0 = tr * 4 - 3, iw0 = kOW * 2 * cc;
 #pragma unroll
     for (int q = 0; q < kIt; ++q) {
       const int j = t + q * kNT;
-      const int hr = j / (kW / 2), pr = j - hr * (kW / 2);
-      const int ih = ih0 + hr;
+      const int hr = j / kPPR, pr = j - hr * kPPR - kP0;
+      const int ih = ih0 + hr, c = iw0 + 2 * pr;
       v[q] = make_uint3(0u, 0u, 0u);
-      if (j < kPairs && static_cast<unsigned>(ih) < static_cast<unsigned>(kH))
-        v[q] = *reinterpret_cast<const uint3*>(x + ((static_cast<int64_t>(img) * kH + ih) * kW + 2 * pr) * 3);
+      if (!GEN) {  // (the round-3 address arithmetic, register-lean: the fused stem wgrad sits at 128 VGPRs)
+        if (j < kPairs && static_cast<unsigned>(ih) < static_cast<unsigned>(kH))
+          v[q] = *reinterpret_cast<const uint3*>(x + ((static_cast<int64_t>(img) * kH + ih) * kW + 2 * pr) * 3);
+      } else if (j < kPairs && static_cast<unsigned>(ih) < static_cast<unsigned>(H)) {
+        const bf16_t* row = x + (static_cast<int64_t>(img) * H + ih) * W * 3;
+        if (c >= 0 && c + 1 < W && (W & 1) == 0) {
+          v[q] = *reinterpret_cast<const uint3*>(row + c * 3);
+        } else {
+          uint32_t e[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            const int cx = c + k / 3;
+            e[k] = (cx >= 0 && cx < W) ? row[cx * 3 + k % 3] : 0u;
+          }
+          v[q] = make_uint3(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16));
+        }
+      }
     }
   }
   __device__ __forceinline__ void store(bf16_t* Hs, int t) const {
@@ -64,18 +131,19 @@ struct HaloStager {
     for (int q = 0; q < kIt; ++q) {
       const int j = t + q * kNT;
       if (j < kPairs) {
-        const int hr = j / (kW / 2), pr = j - hr * (kW / 2);
-        uint2* d = reinterpret_cast<uint2*>(Hs + (hr * kHC + 2 * pr + 3) * 4);
-        d[0] = make_uint2(v[q].x, v[q].y & 0xffffu);
+        const int hr = j / kPPR, pr = j - hr * kPPR - kP0;
+        const int jc = 2 * pr + 3;  // halo column of the pair's first pixel
+        uint2* d = reinterpret_cast<uint2*>(Hs + (hr * kHC + jc) * 4);
+        if (!GEN || jc >= 0) d[0] = make_uint2(v[q].x, v[q].y & 0xffffu);
         d[1] = make_uint2((v[q].y >> 16) | (v[q].z << 16), v[q].z >> 16);
       }
     }
   }
 };
 
-template <int EPI>
-__global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tiles) {
-  using Epi = Epilogue<kBM, 64, kNT, EPI>;
+template <int EPI, bool GEN>
+__global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tiles, StemGeo geo) {
+  using Epi = Epilogue<kBM, 64, kNT, EPI, G_STEM>;
   constexpr int LDC = Epi::LDC;
   constexpr int B_BYTES = 64 * kLDB * 2;
   constexpr int H_BYTES = kHR * kHC * 8;
@@ -110,7 +178,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tile
   }
   for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
 
-  HaloStager hs;
+  HaloStager<GEN> hs;
 
   // this lane's output pixel of the tile: m = wave * 32 + fr -> (row ohl, col ow);
   // K-step ks reads halo row 2 ohl + ks / 2, pixels 2 ow + s0, +1 (s0 = 4 (ks & 1) + 2 fh)
@@ -125,14 +193,14 @@ __global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tile
 
   int tm = blockIdx.x;
   if (tm < tiles) {
-    hs.load(p.A, tm, t);
+    hs.load(p.A, tm, t, geo);
     hs.store(Hs, t);
   }
   __syncthreads();
   for (; tm < tiles; tm += gridDim.x) {
     const int next = tm + gridDim.x;
     const int drop = p.price_drop;  // timing-only breakdown (set_stem_drop): 1 MFMA, 2 epilogue, 4 input
-    if (next < tiles && !(drop & 4)) hs.load(p.A, next, t);  // lands under the MFMAs
+    if (next < tiles && !(drop & 4)) hs.load(p.A, next, t, geo);  // lands under the MFMAs
     f32x16_t acc[2][1];
     acc[0][0] = f32x16_t{};
     acc[1][0] = f32x16_t{};
@@ -211,10 +279,11 @@ struct StemBnBwd {
 };
 
 // (second launch bound = min waves per SIMD: 2 blocks of 7 waves need 4 -> <= 128 VGPRs)
-template <bool FUSE>
+template <bool FUSE, bool GEN>
 __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ x, float* __restrict__ dw32,
-                                                             int tiles, int64_t dy_bytes, StemBnBwd bn) {
+                                                             int tiles, int64_t dy_bytes, StemBnBwd bn,
+                                                             StemGeo geo) {
   constexpr int G_BYTES = kBM * 128;  // 224 pixel rows x 64 channels
   constexpr int H_BYTES = kHR * kHC * 8;
   constexpr int NG = FUSE ? 1 : 2;    // the fused tile is built in place, not DMA'd ahead
@@ -243,12 +312,18 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
       const int g = wave * 4 + i;
       const int r = 8 * g + (lane >> 3);
       const int c = (lane & 7) ^ (((r >> 1) & 1) * 4);
-      dma16(rG, (lds_void_t*)(Gs + buf * G_BYTES + g * 1024),
-            static_cast<uint32_t>((static_cast<int64_t>(tm) * kBM + r) * 128 + 16 * c));
+      uint32_t voff;
+      if constexpr (GEN) {
+        const int row = geo.out_row(tm, r);  // masked slots: an OOB load = zeros
+        voff = row >= 0 ? static_cast<uint32_t>(static_cast<int64_t>(row) * 128 + 16 * c) : kOOB;
+      } else {
+        voff = static_cast<uint32_t>((static_cast<int64_t>(tm) * kBM + r) * 128 + 16 * c);
+      }
+      dma16(rG, (lds_void_t*)(Gs + buf * G_BYTES + g * 1024), voff);
     }
   };
 
-  HaloStager hs;
+  HaloStager<GEN> hs;
 
   // FUSE: tile tm (output rows 2k, 2k + 1) only sees pooled rows k and k + 1
   // (row 2k: window k; row 2k + 1: windows k and k + 1).  Their gradient and
@@ -360,7 +435,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
     } else {
       issue_g(tm, 0);
     }
-    hs.load(x, tm, t);
+    hs.load(x, tm, t, geo);
     hs.store(Hs, t);
   }
   for (; tm < tiles; tm += gridDim.x) {
@@ -369,7 +444,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
     if (next < tiles) {
       if constexpr (FUSE) issue_pool(next);  // this tile's pooled rows were consumed by its build
       else issue_g(next, buf ^ 1);
-      hs.load(x, next, t);
+      hs.load(x, next, t, geo);
     }
     const char* G = Gs + buf * G_BYTES;
 #pragma unroll
@@ -411,44 +486,58 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
 
 void set_stem_drop(int bits) { g_stem_drop = bits; }
 
-hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, const float* shift, float* acc,
+hipError_t stem7x7_fwd(const void* x, const void* wp, void* y, int Nb, int H, int W, const float* shift, float* acc,
                        hipStream_t s, bool raw_w) {
-  if (Nb <= 0) return hipErrorInvalidValue;
+  if (Nb <= 0 || H < 1 || W < 1) return hipErrorInvalidValue;
+  const StemGeo g = stem_geo(H, W);
   GemmParams p{};
   p.A = static_cast<const bf16_t*>(x);
   p.B = static_cast<const bf16_t*>(wp);
   p.C = static_cast<bf16_t*>(y);
-  p.M = Nb * kOH * kOW;
+  p.M = Nb * g.OH * g.OW;
   p.N = 64;
   p.K = kK;
+  p.Hout = g.OH;  // (the epilogue's G_STEM row map)
+  p.Wout = g.OW;
+  p.Hin = g.TR;
+  p.Win = g.CC;
   p.shift = shift;
   p.acc = acc;
   p.price_drop = g_stem_drop;
   p.Cin = raw_w ? 3 : 0;
-  const int tiles = Nb * (kOH / 2);
+  const int tiles = Nb * g.TR * g.CC;
   const int grid = tiles < 512 ? tiles : 512;  // two resident blocks per CU
+  const bool gen = !(H == kH && W == kW);  // the 224-px benchmark geometry keeps the specialised halo loads
   if (acc) {
-    hipLaunchKernelGGL(stem_fwd_kernel<EPI_STATS>, dim3(grid), dim3(kNT), 0, s, p, tiles);
+    if (gen) hipLaunchKernelGGL((stem_fwd_kernel<EPI_STATS, true>), dim3(grid), dim3(kNT), 0, s, p, tiles, g);
+    else hipLaunchKernelGGL((stem_fwd_kernel<EPI_STATS, false>), dim3(grid), dim3(kNT), 0, s, p, tiles, g);
   } else {
-    hipLaunchKernelGGL(stem_fwd_kernel<EPI_PLAIN>, dim3(grid), dim3(kNT), 0, s, p, tiles);
+    if (gen) hipLaunchKernelGGL((stem_fwd_kernel<EPI_PLAIN, true>), dim3(grid), dim3(kNT), 0, s, p, tiles, g);
+    else hipLaunchKernelGGL((stem_fwd_kernel<EPI_PLAIN, false>), dim3(grid), dim3(kNT), 0, s, p, tiles, g);
   }
   return hipGetLastError();
 }
 
-int stem7x7_wgrad_slabs(int Nb) {
-  const int tiles = Nb * (kOH / 2);
+int stem7x7_wgrad_slabs(int Nb, int H, int W) {
+  const StemGeo g = stem_geo(H, W);
+  const int tiles = Nb * g.TR * g.CC;
   return tiles < 512 ? tiles : 512;
 }
 
-hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, hipStream_t s,
+hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, int Nb, int H, int W, hipStream_t s,
                          bool raw_out) {
-  if (Nb <= 0) return hipErrorInvalidValue;
-  const int64_t dy_bytes = static_cast<int64_t>(Nb) * kOH * kOW * 64 * 2;
+  if (Nb <= 0 || H < 1 || W < 1) return hipErrorInvalidValue;
+  const StemGeo g = stem_geo(H, W);
+  const int64_t dy_bytes = static_cast<int64_t>(Nb) * g.OH * g.OW * 64 * 2;
   if (dy_bytes >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit buffer offsets
-  const int tiles = Nb * (kOH / 2);
-  const int grid = stem7x7_wgrad_slabs(Nb);
-  hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(dy),
-                     static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes, StemBnBwd{});
+  const int tiles = Nb * g.TR * g.CC;
+  const int grid = stem7x7_wgrad_slabs(Nb, H, W);
+  if (H == kH && W == kW)
+    hipLaunchKernelGGL((stem_wgrad_kernel<false, false>), dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(dy),
+                       static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes, StemBnBwd{}, g);
+  else
+    hipLaunchKernelGGL((stem_wgrad_kernel<false, true>), dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(dy),
+                       static_cast<const bf16_t*>(x), dw32, tiles, dy_bytes, StemBnBwd{}, g);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s, raw_out ? 1 : 0);
@@ -457,11 +546,12 @@ hipError_t stem7x7_wgrad(const void* dy, const void* x, float* dw32, void* dW, i
 hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, const float* coef5, const void* x,
                             float* dw32, void* dW, int Nb, hipStream_t s, bool raw_out) {
   if (Nb <= 0) return hipErrorInvalidValue;
-  const int tiles = Nb * (kOH / 2);
-  const int grid = stem7x7_wgrad_slabs(Nb);
+  const StemGeo g = stem_geo(kH, kW);  // the pooled-gradient gather is specialised to 112 -> 56
+  const int tiles = Nb * g.TR * g.CC;
+  const int grid = stem7x7_wgrad_slabs(Nb, kH, kW);
   StemBnBwd bn{static_cast<const bf16_t*>(c0), static_cast<const bf16_t*>(dp), idx, coef5};
-  hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(nullptr),
-                     static_cast<const bf16_t*>(x), dw32, tiles, int64_t(0), bn);
+  hipLaunchKernelGGL((stem_wgrad_kernel<true, false>), dim3(grid), dim3(kNT), 0, s, static_cast<const bf16_t*>(nullptr),
+                     static_cast<const bf16_t*>(x), dw32, tiles, int64_t(0), bn, g);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return wgrad_slab_reduce(dw32, static_cast<int64_t>(64) * kK, grid, 1.0f, dW, s, raw_out ? 1 : 0);

@@ -121,8 +121,6 @@ class HipKernels:
         self.ext = _ext.load()
         self.dev = dev
         self._dw32 = {}
-        # the kdl stem kernel serves the 3x224x224 geometry the benchmark trains on
-        self.stem_native = True
         # BN finalize folded into the producing conv GEMM's last arriving blocks
         # (csrc/bn_fin.h; EngineOptions.bn_fin = "kernel": separate finalize
         # launches).  Round 2 measured it neutral while its inlined tail made every
@@ -327,27 +325,21 @@ class HipKernels:
         return y, mb
 
     def stem_conv(self, x, w, st):
-        """7x7 / stride 2 stem conv: csrc/stem.hip (MFMA, the stem BN's statistics
-        in the epilogue) at the 224-px geometry it serves, else MIOpen.  Returns
-        (c0, statistics already in st's workspace)."""
-        if (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(w.shape) == (64, 3, 7, 7)
-                and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
-            c0 = _nhwc_empty(x.shape[0], 64, 112, 112, x)
-            # the channels_last [64, 3, 7, 7] parameter itself (the kernel reorders it
-            # while staging); contiguous NCHW weights (tests) take the K-order copy
-            wk = w if w.is_contiguous(memory_format=torch.channels_last) else stem_weights(w)
-            self.ext.stem7x7_fwd(x, wk, c0, st.mod.running_mean, self._fwd_acc(st))
-            self.stem_path = "kdl"
-            return c0, True
-        # csrc/stem.hip is specialised to the 224 x 224 x 3 geometry the benchmark
-        # trains on; any other input runs the stem conv on MIOpen -- reported, not silent
-        if self.stem_path != "miopen":
-            import logging
-            logging.getLogger("kubedl_amd.engine").warning(
-                "stem conv on MIOpen: the kdl stem kernel serves 3x224x224 bf16 NHWC only (got %s)",
-                tuple(x.shape[1:]))
-        self.stem_path = "miopen"
-        return F.conv2d(x, w, stride=2, padding=3).contiguous(memory_format=torch.channels_last), False
+        """7x7 / stride 2 stem conv on csrc/stem.hip (MFMA, the stem BN's
+        statistics in the epilogue) at any input size.  Returns (c0, statistics
+        already in st's workspace)."""
+        if not (tuple(w.shape) == (64, 3, 7, 7) and x.shape[1] == 3 and x.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            raise ValueError(f"HIP engine stem: 3-channel bf16 NHWC input and a [64, 3, 7, 7] conv expected "
+                             f"(got x {tuple(x.shape)} {x.dtype}, w {tuple(w.shape)})")
+        oh, ow = (x.shape[2] - 1) // 2 + 1, (x.shape[3] - 1) // 2 + 1
+        c0 = _nhwc_empty(x.shape[0], 64, oh, ow, x)
+        # the channels_last [64, 3, 7, 7] parameter itself (the kernel reorders it
+        # while staging); contiguous NCHW weights (tests) take the K-order copy
+        wk = w if w.is_contiguous(memory_format=torch.channels_last) else stem_weights(w)
+        self.ext.stem7x7_fwd(x, wk, c0, st.mod.running_mean, self._fwd_acc(st))
+        self.stem_path = "kdl"
+        return c0, True
 
     def stem_fwd(self, c0, st, gemm_stats=False):
         m = st.mod
@@ -514,19 +506,13 @@ class HipKernels:
 
     def stem_wgrad(self, dc0, x, dw):
         """Stem conv weight gradient into ``dw`` ([64, 3, 7, 7]): csrc/stem.hip
-        (both operands read pixel-major from LDS, no patch matrix) where the
-        forward ran on it, else MIOpen."""
-        if self._stem_native_bwd(x, dc0, dw):
-            ws = self._stem_ws(x.shape[0], x.device)
-            if dw.is_contiguous(memory_format=torch.channels_last):  # written in place, raw layout
-                self.ext.stem7x7_wgrad(dc0, x, ws[0], dw)
-            else:
-                self.ext.stem7x7_wgrad(dc0, x, ws[0], ws[1])
-                dw.copy_(stem_grad_from_k(ws[1]))
-            return
-        _, dw0, _ = torch.ops.aten.convolution_backward(
-            dc0, x, dw, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False])
-        dw.copy_(dw0)
+        (both operands read pixel-major from LDS, no patch matrix), any input size."""
+        ws = self._stem_ws(x.shape[0], x.device, x.shape[2], x.shape[3])
+        if dw.is_contiguous(memory_format=torch.channels_last):  # written in place, raw layout
+            self.ext.stem7x7_wgrad(dc0, x, ws[0], dw)
+        else:
+            self.ext.stem7x7_wgrad(dc0, x, ws[0], ws[1])
+            dw.copy_(stem_grad_from_k(ws[1]))
 
     def stem_bwd(self, dp, idx, c0, st, dgamma, dbeta, with_dx=True):
         m = st.mod
@@ -537,7 +523,10 @@ class HipKernels:
         return dx
 
     def _stem_native_bwd(self, x, c0, dw):
-        return (self.stem_native and tuple(x.shape[1:]) == (3, 224, 224) and tuple(dw.shape) == (64, 3, 7, 7)
+        """The fused pool-backward + weight-gradient kernel serves 3x224x224 (its
+        pooled-gradient gather is specialised to 112 -> 56); other sizes take the
+        pooling backward pass + the general weight-gradient kernel."""
+        return (tuple(x.shape[1:]) == (3, 224, 224) and tuple(dw.shape) == (64, 3, 7, 7)
                 and x.is_contiguous(memory_format=torch.channels_last)
                 and c0.is_contiguous(memory_format=torch.channels_last))
 
@@ -600,11 +589,11 @@ class HipKernels:
         raise NotImplementedError(f"HIP engine: stride-{stride} 3x3 data gradient needs an even input size "
                                   f"(got {tuple(x1.shape[-2:])} -> {tuple(g.shape[-2:])})")
 
-    def _stem_ws(self, nb, device):
-        key = ("stem", nb)
+    def _stem_ws(self, nb, device, h=224, w=224):
+        key = ("stem", nb, h, w)
         ws = self._dw32.get(key)
         if ws is None:
-            ws = (torch.empty(self.ext.stem7x7_wgrad_slabs(nb) * 64 * 224, device=device),
+            ws = (torch.empty(self.ext.stem7x7_wgrad_slabs(nb, h, w) * 64 * 224, device=device),
                   torch.empty(64, 224, device=device, dtype=torch.bfloat16))
             self._dw32[key] = ws
         return ws

@@ -153,3 +153,34 @@ def test_stem_raw_weight_layout_bit_exact(nb):
         memory_format=torch.channels_last)
     ext.stem7x7_wgrad(dy, x, ws, raw)
     assert torch.equal(raw, stem_grad_from_k(dwk))
+
+
+@pytest.mark.parametrize("nb,h,w", [(2, 64, 64), (1, 97, 250), (3, 33, 17)])
+def test_stem_any_geometry_matches_fp32(nb, h, w):
+    """the stem kernel at sizes other than 224 (2-row x
+    112-column tiles, masked edges, odd heights / widths, more than one column
+    chunk) -- forward with the BN-statistics epilogue and the weight gradient vs
+    fp32 PyTorch; no MIOpen fallback remains."""
+    ext = _ext()
+    torch.manual_seed(h * 1000 + w)
+    x = torch.randn(nb, h, w, 3, device="cuda").bfloat16().permute(0, 3, 1, 2)
+    wt = (torch.randn(64, 3, 7, 7, device="cuda") / 12).bfloat16().contiguous(memory_format=torch.channels_last)
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = torch.full((nb, 64, oh, ow), float("nan"), device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    rm = torch.randn(64, device="cuda") * 0.1
+    ws = torch.zeros(ext.bn_workspace_floats(64), device="cuda")
+    ext.stem7x7_fwd(x, wt, y, rm, ws[:REP * 2 * 64])
+    ref = F.conv2d(x.float(), wt.float(), stride=2, padding=3)
+    assert torch.isfinite(y.float()).all()
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+    yr = y.float().permute(0, 2, 3, 1).reshape(-1, 64) - rm
+    s = ws[:REP * 2 * 64].view(REP, 2, 64).sum(0)
+    torch.testing.assert_close(s[0], yr.sum(0), atol=0.5, rtol=1e-3)  # masked slots add nothing
+    dy = torch.randn(nb, oh, ow, 64, device="cuda").bfloat16().permute(0, 3, 1, 2)
+    slabs = torch.empty(ext.stem7x7_wgrad_slabs(nb, h, w) * 64 * 224, device="cuda")
+    dw = torch.full((64, 3, 7, 7), float("nan"), device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ext.stem7x7_wgrad(dy, x, slabs, dw)
+    gref = torch.nn.grad.conv2d_weight(x.float(), (64, 3, 7, 7), dy.float(), stride=2, padding=3)
+    torch.testing.assert_close(dw.float(), gref, atol=1e-2 * gref.abs().max().item(), rtol=1e-2)
