@@ -803,6 +803,7 @@ FinArm take_fin_arm() {
 struct BwdArm {
   const void* x = nullptr;
   const float* coef = nullptr;
+  const float* coef2 = nullptr;  // res 2: the downsample BN's scale | shift
   void* out = nullptr;
   int64_t C = 0, rows = 0;
   int res = 0;              // 1: forward residual-apply prologue (bn_res_pro_arm)
@@ -834,8 +835,7 @@ void bn_bwd_pro_arm(const at::Tensor& x, const at::Tensor& ws, int64_t C, const 
 // bn_stage_fwd_apply(A, ws, res, ..., out, bits) (csrc/conv1x1.hip PRO_RES).
 // coefd (optional) [2C]: ``res`` is a downsample branch's BN input, the residual
 // res * coefd[k] + coefd[C + k] (bn_stage_fwd_apply's dual form); coef and coefd
-// are copied into one [4C] table owned by the arm
-thread_local at::Tensor g_res_coef4;
+// are read by the kernel from both tables (no concatenated copy)
 void bn_res_pro_arm(const at::Tensor& res, const at::Tensor& coef, int64_t C, const at::Tensor& out,
                     const at::Tensor& bits, const c10::optional<at::Tensor>& coefd) {
   TORCH_CHECK(C > 0 && C % 64 == 0 && res.numel() % C == 0, "bn_res_pro_arm: C % 64 == 0 dividing res");
@@ -853,8 +853,7 @@ void bn_res_pro_arm(const at::Tensor& res, const at::Tensor& coef, int64_t C, co
     TORCH_CHECK(coefd->is_cuda() && coefd->scalar_type() == at::kFloat && coefd->is_contiguous() &&
                     coefd->numel() >= 2 * C,
                 "bn_res_pro_arm: coefd fp32 [2C]");
-    g_res_coef4 = at::cat({coef.narrow(0, 0, 2 * C), coefd->narrow(0, 0, 2 * C)});
-    g_bwd_arm.coef = g_res_coef4.data_ptr<float>();
+    g_bwd_arm.coef2 = coefd->data_ptr<float>();
     g_bwd_arm.res = 2;
   }
   g_bwd_arm.out = out.data_ptr();
@@ -1083,7 +1082,7 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   a.res_W = static_cast<int>(res_W);
   a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
   a.ex2 = opt_ptr(ex2); a.emean2 = opt_fptr(emean2); a.acc2 = opt_fptr(acc2);
-  a.bx = bw.x; a.bcoef = bw.coef; a.aout = bw.out;
+  a.bx = bw.x; a.bcoef = bw.coef; a.bcoef2 = bw.coef2; a.aout = bw.out;
   if (bw.res) { a.bres = bw.res; a.obits = bw.bits; }
   apply_fin_arm(fin, a, N, epi);
   check_hip(kdl::conv1x1_gemm(a, cur_stream()), "conv1x1_gemm");

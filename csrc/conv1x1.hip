@@ -172,7 +172,9 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   (void)a_m; (void)st_seg2;
   if constexpr (TWO_IN) {  // PRO_BWD: k | c1 | c0; PRO_RES: scale | shift; PRO_RES2: + scale_d | shift_d
     for (int i = t; i < (PRO == PRO_BWD ? 3 : PRO == PRO_RES2 ? 4 : 2) * K / 4; i += kThreads)
-      reinterpret_cast<float4*>(coef_lds)[i] = reinterpret_cast<const float4*>(p.bcoef)[i];
+      reinterpret_cast<float4*>(coef_lds)[i] = (PRO == PRO_RES2 && i >= K / 2)
+                                                   ? reinterpret_cast<const float4*>(p.bcoef2)[i - K / 2]
+                                                   : reinterpret_cast<const float4*>(p.bcoef)[i];
     __syncthreads();
   }
   // [2 K2a] segment-2 scale | shift, then (PRO_SEG) [K] segment-1 scale
@@ -952,7 +954,8 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.res_H = a.res_H; p.res_W = a.res_W;
   p.ebits = a.ebits; p.ex2 = static_cast<const bf16_t*>(a.ex2); p.emean2 = a.emean2; p.acc2 = a.acc2;
   p.fin_ws = a.fin_ws; p.fin_ws2 = a.fin_ws2; p.fin_M = a.fin_M;
-  p.bx = static_cast<const bf16_t*>(a.bx); p.bcoef = a.bcoef; p.aout = static_cast<bf16_t*>(a.aout);
+  p.bx = static_cast<const bf16_t*>(a.bx); p.bcoef = a.bcoef; p.bcoef2 = a.bcoef2;
+  p.aout = static_cast<bf16_t*>(a.aout);
   p.A2 = static_cast<const bf16_t*>(a.A2); p.B2 = static_cast<const bf16_t*>(a.B2);
   p.K2 = a.K2; p.ldb = a.ldb > 0 ? a.ldb : a.K; p.ldb2 = a.ldb2;
   p.K2a = a.K2a > 0 ? a.K2a : a.K2; p.seg1_scale = a.seg1_scale;

@@ -67,6 +67,7 @@ struct GemmParams {
   // is bit-identical to the tensor that pass would have written.
   const bf16_t* bx;       // that BN's input x [M, K]
   const float* bcoef;     // [3K] k | c1 | c0 (the BN workspace's backward coefficients)
+  const float* bcoef2;    // PRO_RES2: the downsample BN's [2K] scale | shift (LDS after bcoef's [2K])
   bf16_t* aout;           // optional write-through of A' [M, K] (the blocks of output tile 0)
   // epilogue operands
   const float* shift;   // STATS: [N]

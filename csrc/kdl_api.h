@@ -237,6 +237,7 @@ struct Conv1x1Args {
   // bit-identical to bn_stage_bwd_apply's output; aout (optional) receives A'
   const void* bx;                    // that BN's input [M, K]
   const float* bcoef;                // [3K] its backward coefficients (ws_bcoef)
+  const float* bcoef2;               // bres 2: the residual BN's [2K] scale | shift (no concatenated copy)
   void* aout;                        // [M, K]
   // bres = 1: the prologue is the closing BN + residual + ReLU of the previous
   // block, relu(A * bcoef[k] + bcoef[K + k] + bx), written through to aout
