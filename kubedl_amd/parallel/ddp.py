@@ -66,8 +66,15 @@ class FlatDDP:
         self.world = world_size
         # KDL_DDP_WORLD1=1: a world-1 job still buckets and all-reduces (RCCL's
         # one-rank all-reduce) -- exercises the collective path the N-GPU job
-        # takes; off by default (it is an identity)
-        self.active = world_size > 1 or (os.environ.get("KDL_DDP_WORLD1", "0") == "1" and dist.is_initialized())
+        # takes; off by default (it is an identity).  RCCL's one-rank in-place
+        # all-reduce launches nothing, so KDL_DDP_WORLD1=copy issues each bucket
+        # as a one-rank all_gather into a scratch buffer instead: a bucket-sized
+        # RCCL copy on the process group's own stream, event-joined like the
+        # N-GPU collective (the stream / hardware-queue shape of world 8)
+        w1 = os.environ.get("KDL_DDP_WORLD1", "0")
+        self.active = world_size > 1 or (w1 in ("1", "copy") and dist.is_initialized())
+        self.world1_copy = world_size == 1 and w1 == "copy" and self.active
+        self._w1_scratch = None
         self.pg = process_group
         self.buckets: list[Bucket] = []
         self._hooks = []
@@ -136,6 +143,12 @@ class FlatDDP:
             self._issue(b)
 
     def _issue(self, b: Bucket) -> None:
+        if self.world1_copy:
+            if self._w1_scratch is None:
+                self._w1_scratch = torch.empty_like(self.space.grad)
+            b.handle = dist.all_gather_into_tensor(self._w1_scratch[b.lo:b.hi], self.space.grad[b.lo:b.hi],
+                                                   group=self.pg, async_op=True)
+            return
         if self.transport is not None:
             b.handle = self.transport.launch(b.lo, b.hi)
         elif self.reduce_fp32 and self.space.grad.dtype != torch.float32:
