@@ -720,7 +720,7 @@ void head_forward(const at::Tensor& x, const at::Tensor& w, const c10::optional<
   need_bf16(feat, Nb * C, "head feat");
   need_f32(part1, sp[0] * Nb * L, "head part1");
   need_f32(lrow, Nb, "head lrow");
-  need_bf16(dl, Nb * L, "head dl");
+  need_bf16(dl, Nb * kdl::head_lpad(static_cast<int>(L)), "head dl");
   need_bf16(dlT, L * Nb, "head dlT");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check_hip(kdl::head_forward(x.data_ptr(), static_cast<int>(Nb), static_cast<int>(HW), static_cast<int>(C),
@@ -735,11 +735,11 @@ void head_backward(const at::Tensor& feat, const at::Tensor& w, const at::Tensor
                    at::Tensor loss) {
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "head_backward: w [L, C] contiguous");
   const int64_t L = w.size(0), C = w.size(1), Nb = feat.numel() / C;
-  TORCH_CHECK(Nb % 8 == 0 && L % 8 == 0 && C % 8 == 0, "head_backward: Nb, L, C multiples of 8");
+  TORCH_CHECK(Nb % 8 == 0 && C % 8 == 0, "head_backward: Nb, C multiples of 8");
   auto sp = head_splits(Nb, C, L);
   need_bf16(feat, Nb * C, "head feat");
   need_bf16(w, L * C, "head w");
-  need_bf16(dl, Nb * L, "head dl");
+  need_bf16(dl, Nb * kdl::head_lpad(static_cast<int>(L)), "head dl");
   need_bf16(dlT, L * Nb, "head dlT");
   need_f32(part2, sp[1] * Nb * C, "head part2");
   need_bf16(dfeat, Nb * C, "head dfeat");
@@ -1645,6 +1645,7 @@ PYBIND11_MODULE(_C, m) {
           return kdl::stem7x7_wgrad_slabs(static_cast<int>(nb), static_cast<int>(h), static_cast<int>(w)); },
         "fp32 slab count of stem7x7_wgrad's workspace", py::arg("nb"), py::arg("h") = 224, py::arg("w") = 224);
   m.def("head_splits", &head_splits, "K splits (fc forward, dfeat) of the classifier head kernels");
+  m.def("head_lpad", [](int64_t L) { return kdl::head_lpad(static_cast<int>(L)); }, "row pitch of the head's dl");
   m.def("head_forward", &head_forward, "classifier head forward: mean pool + fc (MFMA) + softmax CE + dlogits");
   m.def("head_backward", &head_backward, "classifier head backward: dfeat, dW, db (MFMA) + mean loss");
   m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");

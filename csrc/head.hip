@@ -7,7 +7,8 @@
 //   pool      feat[n][c]   = bf16(mean_p x[n][p][c])       (x = last block output, NHWC)
 //   fwd GEMM  part1[s][n][l] = sum_{c in split s} feat[n][c] W[l][c]
 //   ce        z = b + sum_s part1; loss_n = lse(z) - z[y]; dl = (softmax - onehot) / N
-//             written row-major dl [N][L] and transposed dlT [L][N] (bf16)
+//             written row-major dl [N][Lp] (rows padded to Lp = L rounded up to 8,
+//             zeros) and transposed dlT [L][N] (bf16)
 //   bwd GEMMs part2[s][n][c] = sum_{l in split s} dlT[l][n] W[l][c]        (dfeat)
 //             dW[l][c]       = sum_n dl[n][l] feat[n][c]; db[l] = sum_n dl[n][l]
 //             (one launch: the two problems share the block range)
@@ -220,6 +221,7 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
 }
 
 __global__ __launch_bounds__(256) void head_ce_kernel(const float* __restrict__ part1, int splits, int Nb, int L,
+                                                      int Lp,
                                                       const bf16_t* __restrict__ bias,
                                                       const int64_t* __restrict__ y, float inv_n,
                                                       float* __restrict__ lrow, bf16_t* __restrict__ dl,
@@ -241,11 +243,11 @@ __global__ __launch_bounds__(256) void head_ce_kernel(const float* __restrict__ 
   const int yn = static_cast<int>(y[n]);
   if (t == 0) lrow[n] = __logf(se) + mx - z[yn];
   const float rse = 1.f / se;
-  for (int l = t; l < L; l += 256) {
-    const float g = (__expf(z[l] - mx) * rse - (l == yn ? 1.f : 0.f)) * inv_n;
+  for (int l = t; l < Lp; l += 256) {  // dl rows padded to Lp (16-B rows for the backward's loads)
+    const float g = l < L ? (__expf(z[l] - mx) * rse - (l == yn ? 1.f : 0.f)) * inv_n : 0.f;
     const bf16_t gb = f32_to_bf16(g);
-    dl[static_cast<int64_t>(n) * L + l] = gb;
-    dlT[static_cast<int64_t>(l) * Nb + n] = gb;
+    dl[static_cast<int64_t>(n) * Lp + l] = gb;
+    if (l < L) dlT[static_cast<int64_t>(l) * Nb + n] = gb;
   }
 }
 
@@ -300,6 +302,8 @@ HeadGemm make_gemm(const bf16_t* A, const bf16_t* B, int M, int N, int K, int ld
 
 }  // namespace
 
+int head_lpad(int L) { return (L + 7) / 8 * 8; }
+
 void head_splits(int Nb, int C, int L, int* s1, int* s2) {
   *s1 = splits_for(((Nb + kT - 1) / kT) * ((L + kT - 1) / kT), C);
   *s2 = splits_for(((Nb + kT - 1) / kT) * ((C + kT - 1) / kT), L);
@@ -316,7 +320,7 @@ hipError_t head_forward(const void* x, int Nb, int HW, int C, const void* w, con
   g.part = part1;
   HeadGemm none{};
   hipLaunchKernelGGL((head_gemm_kernel<false, false>), dim3(g.blocks), dim3(256), 0, s, g, none);
-  hipLaunchKernelGGL(head_ce_kernel, dim3(Nb), dim3(256), L * sizeof(float), s, part1, s1, Nb, L,
+  hipLaunchKernelGGL(head_ce_kernel, dim3(Nb), dim3(256), L * sizeof(float), s, part1, s1, Nb, L, head_lpad(L),
                      static_cast<const bf16_t*>(b), y, 1.f / static_cast<float>(Nb), lrow, static_cast<bf16_t*>(dl),
                      static_cast<bf16_t*>(dlT));
   return hipGetLastError();
@@ -325,14 +329,15 @@ hipError_t head_forward(const void* x, int Nb, int HW, int C, const void* w, con
 hipError_t head_backward(const void* feat, const void* w, const void* dl, const void* dlT, int Nb, int C, int L,
                          float* part2, void* dfeat, void* dW, void* db, const float* lrow, float* loss,
                          hipStream_t s) {
-  if (Nb <= 0 || C % 8 || L <= 0 || Nb % 8 || L % 8) return hipErrorInvalidValue;
+  if (Nb <= 0 || C % 8 || L <= 0 || Nb % 8) return hipErrorInvalidValue;
   int s1, s2;
   head_splits(Nb, C, L, &s1, &s2);
   // dfeat partials: sum_l dlT[l][n] W[l][c] (k = l is the row of both)
   HeadGemm gd = make_gemm(static_cast<const bf16_t*>(dlT), static_cast<const bf16_t*>(w), Nb, C, L, Nb, C, s2);
   gd.part = part2;
   // dW[l][c] = sum_n dl[n][l] feat[n][c]; db[l] = sum_n dl[n][l]
-  HeadGemm gw = make_gemm(static_cast<const bf16_t*>(dl), static_cast<const bf16_t*>(feat), L, C, Nb, L, C, 1);
+  HeadGemm gw = make_gemm(static_cast<const bf16_t*>(dl), static_cast<const bf16_t*>(feat), L, C, Nb, head_lpad(L), C,
+                          1);
   gw.out = static_cast<bf16_t*>(dW);
   gw.rowsum = static_cast<bf16_t*>(db);
   hipLaunchKernelGGL((head_gemm_kernel<true, true>), dim3(gd.blocks + gw.blocks), dim3(256), 0, s, gd, gw);

@@ -290,10 +290,11 @@ hipError_t stem7x7_wgrad_bn(const void* c0, const void* dp, const uint8_t* idx, 
 // Classifier head (csrc/head.hip): x [Nb, HW, C] NHWC bf16 (last block output),
 // fc weight w [L][C] bf16, bias b [L] bf16 (optional), labels y [Nb] int64.
 // Forward: feat [Nb][C] bf16 (mean pool), part1 [s1][Nb][L] fp32 (split-K fc
-// partials), lrow [Nb] per-image loss, dl [Nb][L] / dlT [L][Nb] bf16 dlogits
+// partials), lrow [Nb] per-image loss, dl [Nb][Lp] / dlT [L][Nb] bf16 dlogits
 // (mean reduction).  Backward: part2 [s2][Nb][C] fp32, dfeat [Nb][C] bf16,
 // dW [L][C] / db [L] bf16, loss [1] fp32 (mean).  s1 / s2 from head_splits.
 void head_splits(int Nb, int C, int L, int* s1, int* s2);
+int head_lpad(int L);  // dl's row pitch: L rounded up to 8
 hipError_t head_forward(const void* x, int Nb, int HW, int C, const void* w, const void* b, int L, const int64_t* y,
                         void* feat, float* part1, float* lrow, void* dl, void* dlT, hipStream_t s);
 hipError_t head_backward(const void* feat, const void* w, const void* dl, const void* dlT, int Nb, int C, int L,

@@ -560,7 +560,7 @@ class HipKernels:
         L = w.shape[0]
         return (fmap.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
                 and fmap.is_contiguous(memory_format=torch.channels_last) and n % 8 == 0 and c % 8 == 0
-                and L % 8 == 0 and L <= 8192 and y.dtype == torch.int64)
+                and L <= 8192 and y.dtype == torch.int64)
 
     def head(self, fmap, w, b, y, dw, db):
         """Pool -> fc -> softmax CE -> backward on csrc/head.hip: (loss [1],
@@ -574,7 +574,7 @@ class HipKernels:
             bf = dict(dtype=torch.bfloat16, device=fmap.device)
             f32 = dict(dtype=torch.float32, device=fmap.device)
             ws = self._dw32[key] = dict(feat=torch.empty(n, c, **bf), part1=torch.empty(s1 * n * L, **f32),
-                                        lrow=torch.empty(n, **f32), dl=torch.empty(n, L, **bf),
+                                        lrow=torch.empty(n, **f32), dl=torch.empty(n, self.ext.head_lpad(L), **bf),
                                         dlT=torch.empty(L, n, **bf), part2=torch.empty(s2 * n * c, **f32),
                                         dfeat=torch.empty(n, c, **bf))
         yc = y if y.is_contiguous() else y.contiguous()

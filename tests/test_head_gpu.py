@@ -23,7 +23,7 @@ def _run(n, c, L, hw, seed):
     y = torch.randint(0, L, (n,), device="cuda", generator=g)
     s1, s2 = ext.head_splits(n, c, L)
     bf = dict(dtype=torch.bfloat16, device="cuda")
-    feat, dl, dlT = torch.empty(n, c, **bf), torch.empty(n, L, **bf), torch.empty(L, n, **bf)
+    feat, dl, dlT = torch.empty(n, c, **bf), torch.empty(n, ext.head_lpad(L), **bf), torch.empty(L, n, **bf)
     part1, part2 = torch.empty(s1 * n * L, device="cuda"), torch.empty(s2 * n * c, device="cuda")
     lrow, loss = torch.empty(n, device="cuda"), torch.empty(1, device="cuda")
     dfeat, dw, db = torch.empty(n, c, **bf), torch.full((L, c), float("nan"), **bf), torch.empty(L, **bf)
@@ -40,7 +40,7 @@ def _run(n, c, L, hw, seed):
                 db=(db, br.grad), dl=(dl, dlT))
 
 
-@pytest.mark.parametrize("n,c,L,hw", [(256, 2048, 1000, 7), (24, 136, 40, 3)])
+@pytest.mark.parametrize("n,c,L,hw", [(256, 2048, 1000, 7), (24, 136, 40, 3), (8, 64, 10, 2)])
 def test_head_matches_fp32(n, c, L, hw):
     r = _run(n, c, L, hw, 7)
     torch.testing.assert_close(r["feat"][0].float(), r["feat"][1], atol=2e-2, rtol=1e-2)
@@ -52,7 +52,8 @@ def test_head_matches_fp32(n, c, L, hw):
         cos = F.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
         assert cos > 0.9999, (k, cos)
     dl, dlT = r["dl"]
-    assert torch.equal(dl.t(), dlT)  # both layouts of the same rounded values
+    assert torch.equal(dl[:, :L].t(), dlT)  # both layouts of the same rounded values
+    assert not dl[:, L:].any()  # row padding is zero
 
 
 def test_head_deterministic():
