@@ -16,6 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 f=$(find gpurun_out/r04_prof -name "*kernel_trace.csv" | head -1)
 python3 scripts/timeline.py "$f" --steps 6 > gpurun_out/r04_timeline.txt
 python3 scripts/stray_kernels.py "$f" > gpurun_out/r04_stray.txt
-cat gpurun_out/r04_timeline.txt; tail -12 gpurun_out/r04_stray.txt
+python3 scripts/main_gaps.py "$f" 15 > gpurun_out/r04_main_gaps.txt
+cat gpurun_out/r04_timeline.txt; tail -12 gpurun_out/r04_stray.txt; head -12 gpurun_out/r04_main_gaps.txt
 if [ "${PMC:-0}" = "1" ]; then bash scripts/gpu_r04_pmc.sh || exit $?; fi
 exit 0
