@@ -37,8 +37,8 @@ def main():
         if g >= lim:
             big += g
             ov = sorted({nm(s[3]) for s in other if s[0] < b[0] and s[1] > a[1]})
-            out.append(f"{g:7.1f} us at {(a[1] - t0) / 1e3:8.1f} ms  {nm(a[3])} -> {nm(b[3])}  other streams: {ov[:3]}")
-    print(f"step {(step[-1][1] - step[0][1]) / 1e3:.3f} us; main-stream gaps {tot:.1f} us in total, "
+            out.append(f"{g:7.1f} us at {(a[1] - t0) / 1e3:8.1f} us  {nm(a[3])} -> {nm(b[3])}  other streams: {ov[:3]}")
+    print(f"step {(step[-1][1] - step[0][1]) / 1e3:.1f} us; main-stream gaps {tot:.1f} us in total, "
           f"{big:.1f} us in {len(out)} gaps >= {lim} us")
     print("\n".join(out))
 
