@@ -18,5 +18,8 @@ python3 scripts/timeline.py "$f" --steps 6 > gpurun_out/r04_timeline.txt
 python3 scripts/stray_kernels.py "$f" > gpurun_out/r04_stray.txt
 python3 scripts/main_gaps.py "$f" 15 > gpurun_out/r04_main_gaps.txt
 cat gpurun_out/r04_timeline.txt; tail -12 gpurun_out/r04_stray.txt; head -12 gpurun_out/r04_main_gaps.txt
+timeout -k 10 300 rocprofv3 --hip-runtime-trace --output-format csv -d gpurun_out/r04_host -o run -- python bench.py --direct --steps 6 --warmup 4 > gpurun_out/r04_host.log 2>&1 || exit $?
+h=$(find gpurun_out/r04_host -name "*hip_api_trace.csv" | head -1)
+[ -n "$h" ] && python3 scripts/host_api_summary.py "$h" > gpurun_out/r04_host_summary.txt && head -40 gpurun_out/r04_host_summary.txt
 if [ "${PMC:-0}" = "1" ]; then bash scripts/gpu_r04_pmc.sh || exit $?; fi
 exit 0
