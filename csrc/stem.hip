@@ -177,6 +177,11 @@ __global__ __launch_bounds__(kNT, 4) void stem_fwd_kernel(GemmParams p, int tile
     }
   }
   for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
+  // every zero lands before any thread stores its first halo pixels (without this
+  // barrier a slow thread's zeroing could overwrite a fast thread's halo data: a
+  // wrong column band in the first tile of a block, seen with the raw-weight
+  // staging's longer prologue, tests/test_stem_gpu.py)
+  __syncthreads();
 
   HaloStager<GEN> hs;
 
@@ -300,6 +305,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   for (int i = t; i < H_BYTES / 16; i += kNT) reinterpret_cast<uint4*>(Hs)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();  // (the zeroed halo before any first-tile store: see stem_fwd_kernel)
 
   // dY rows by LDS-DMA; fused: the c0 rows the tile's dY is built from (in place)
   const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(
