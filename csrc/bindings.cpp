@@ -868,71 +868,6 @@ BwdArm take_bwd_arm() {
   return b;
 }
 
-// A second K segment (and the BN-folded dgrad's bias, or a statistics-only
-// launch) armed for the next conv1x1_gemm on this thread (csrc/conv1x1.hip
-// PRO_SEG / PRO_RECOMP): seg 1 sums A2 [M, K2] . B2^T into the output (B2 null:
-// B's own columns K.. of its ldb-wide rows), seg 2 keeps it in a second
-// accumulator whose tile is the RESBITS epilogue's BN input (ex unused);
-// pro2 = [2 K2] BN scale | shift applied (with ReLU) to A2.  Consumed by the launch.
-struct SegArm {
-  int seg = 0;
-  const void* A2 = nullptr;
-  const void* B2 = nullptr;
-  const float* pro2 = nullptr;
-  const float* ebias = nullptr;
-  const float* seg1_scale = nullptr;
-  int64_t K2 = 0, K2a = 0, ldb = 0, ldb2 = 0, a2_rows = 0, b2_numel = 0, bias_n = 0, s1_n = 0;
-  bool nostore = false;
-};
-thread_local SegArm g_seg_arm;
-
-void conv_seg_arm(int64_t seg, const c10::optional<at::Tensor>& A2, const c10::optional<at::Tensor>& B2,
-                  const c10::optional<at::Tensor>& pro2, int64_t K2, int64_t ldb, int64_t ldb2,
-                  const c10::optional<at::Tensor>& ebias, bool nostore, int64_t K2a,
-                  const c10::optional<at::Tensor>& seg1_scale) {
-  TORCH_CHECK(seg >= 0 && seg <= 2, "conv_seg_arm: seg 0 (none), 1 (summed) or 2 (recompute)");
-  SegArm a;
-  a.seg = static_cast<int>(seg);
-  a.nostore = nostore;
-  if (seg) {
-    if (K2a <= 0) K2a = K2;
-    TORCH_CHECK(K2 > 0 && K2 % 64 == 0 && K2a % 64 == 0 && K2 % K2a == 0 && opt_ptr(A2) && opt_ptr(pro2),
-                "conv_seg_arm: A2, pro2, K2 % 64 == 0, K2a | K2");
-    need_bf16(*A2, K2a, "conv_seg_arm A2");
-    need_opt_f32(pro2, 2 * K2a, "conv_seg_arm pro2");
-    a.A2 = A2->data_ptr();
-    a.a2_rows = A2->numel() / K2a;
-    a.K2a = K2a;
-    if (opt_ptr(seg1_scale)) {
-      TORCH_CHECK(seg == 1, "conv_seg_arm: seg1_scale with seg 1");
-      need_opt_f32(seg1_scale, 1, "conv_seg_arm seg1_scale");
-      a.seg1_scale = seg1_scale->data_ptr<float>();
-      a.s1_n = seg1_scale->numel();
-    }
-    a.pro2 = pro2->data_ptr<float>();
-    a.K2 = K2;
-    a.ldb = ldb;
-    a.ldb2 = ldb2;
-    if (opt_ptr(B2)) {
-      need_bf16(*B2, K2, "conv_seg_arm B2");
-      a.B2 = B2->data_ptr();
-      a.b2_numel = B2->numel();
-    }
-  }
-  if (opt_ptr(ebias)) {
-    need_opt_f32(ebias, 1, "conv_seg_arm ebias");
-    a.ebias = ebias->data_ptr<float>();
-    a.bias_n = ebias->numel();
-  }
-  g_seg_arm = a;
-}
-
-SegArm take_seg_arm() {
-  const SegArm a = g_seg_arm;
-  g_seg_arm = SegArm{};
-  return a;
-}
-
 void apply_fin_arm(const FinArm& f, kdl::Conv1x1Args& a, int64_t N, int64_t epi) {
   if (!f.ws) return;
   TORCH_CHECK(f.C == N, "bn_fin_arm: armed for C = ", f.C, ", the GEMM has N = ", N);
@@ -992,23 +927,8 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
                   const c10::optional<at::Tensor>& emean2, const c10::optional<at::Tensor>& acc2) {
   const FinArm fin = take_fin_arm();
   const BwdArm bw = take_bwd_arm();
-  const SegArm sg = take_seg_arm();
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_gemm: need K % 64 == 0, N % 64 == 0");
-  TORCH_CHECK(!(sg.seg && bw.x), "conv1x1_gemm: a second K segment and a backward-apply prologue exclude each other");
-  const int64_t ldb = sg.seg && sg.ldb > 0 ? sg.ldb : K;
-  if (sg.seg) {
-    TORCH_CHECK(stride == 1 && sg.a2_rows >= M, "conv_seg_arm: dense rows, A2 [M, K2]");
-    TORCH_CHECK(ldb >= K, "conv_seg_arm: ldb >= K");
-    if (sg.B2) {
-      TORCH_CHECK(sg.ldb2 >= sg.K2 && sg.b2_numel >= (N - 1) * sg.ldb2 + sg.K2, "conv_seg_arm: B2 [N, ldb2]");
-    } else {
-      TORCH_CHECK(ldb >= K + sg.K2, "conv_seg_arm: B holds both segments (ldb >= K + K2)");
-    }
-    TORCH_CHECK(sg.seg == 1 ? epi == 2 : epi == 3, "conv_seg_arm: seg 1 feeds MASKX, seg 2 RESBITS");
-  }
-  if (sg.ebias) TORCH_CHECK(epi == 2 && sg.bias_n >= N, "conv_seg_arm: ebias [N] for a MASKX epilogue");
-  if (sg.seg1_scale) TORCH_CHECK(sg.s1_n >= K, "conv_seg_arm: seg1_scale [K]");
-  if (sg.nostore) TORCH_CHECK(epi == 1, "conv_seg_arm: statistics-only launches are STATS");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "conv1x1_gemm: epi 0 (plain) .. 4 (res)");
   if (bw.x) {
     TORCH_CHECK(bw.C == K && bw.rows == M, "bn_bwd_pro_arm: armed for [", bw.rows, ", ", bw.C,
                 "], the GEMM's A is [", M, ", ", K, "]");
@@ -1024,22 +944,14 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   if (stride > 1) TORCH_CHECK(M % (Hout * Wout) == 0 && (Hout - 1) * stride < Hin && (Wout - 1) * stride < Win,
                               "conv1x1_gemm: gather geometry");
   need_bf16(A, rows_in * K, "conv1x1_gemm A");
-  need_bf16(B, (N - 1) * ldb + K, "conv1x1_gemm B");
-  if (!sg.nostore) need_bf16(C, M * N, "conv1x1_gemm C");
-  if (!sg.seg) need_opt_f32(pro_coef, 2 * K, "pro_coef");
+  need_bf16(B, N * K, "conv1x1_gemm B");
+  need_bf16(C, M * N, "conv1x1_gemm C");
+  need_opt_f32(pro_coef, 2 * K, "pro_coef");
   const int64_t rep = 32 * 2 * N;
   if (epi == 1) { TORCH_CHECK(opt_ptr(shift) && opt_ptr(acc), "epi STATS needs shift, acc"); need_opt_f32(shift, N, "shift"); need_opt_f32(acc, rep, "acc"); }
   if (epi == 2) {
     TORCH_CHECK(opt_ptr(ex) && opt_ptr(emean) && opt_ptr(ecoef) && opt_ptr(acc), "epi MASKX needs ex, emean, ecoef, acc");
     need_opt_bf16(ex, M * N, "ex"); need_opt_f32(emean, N, "emean"); need_opt_f32(ecoef, 2 * N, "ecoef"); need_opt_f32(acc, rep, "acc");
-  }
-  if (epi == 5) {  // APPLY: relu(y * scale + shift + eres) + packed mask out
-    TORCH_CHECK(opt_ptr(pro_coef) && opt_ptr(ecoef) && opt_ptr(eres) && opt_ptr(ebits) && stride == 1 &&
-                    res_stride <= 1,
-                "epi APPLY needs pro_coef, ecoef, eres, ebits (out), dense rows");
-    need_opt_f32(ecoef, 2 * N, "ecoef");
-    need_opt_bf16(eres, M * N, "eres");
-    TORCH_CHECK(ebits->scalar_type() == at::kByte && ebits->is_contiguous() && ebits->numel() >= M * N / 8, "ebits");
   }
   if (epi == 3 || epi == 4) {
     TORCH_CHECK(opt_ptr(eres), "epi RES/RESBITS needs eres");
@@ -1052,9 +964,9 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
     }
   }
   if (epi == 3) {
-    TORCH_CHECK((opt_ptr(ex) || sg.seg == 2) && opt_ptr(emean) && opt_ptr(acc) && opt_ptr(ebits),
-                "epi RESBITS needs ex (or a recompute segment), emean, acc, ebits");
-    if (sg.seg != 2) need_opt_bf16(ex, M * N, "ex");
+    TORCH_CHECK(opt_ptr(ex) && opt_ptr(emean) && opt_ptr(acc) && opt_ptr(ebits),
+                "epi RESBITS needs ex, emean, acc, ebits");
+    need_opt_bf16(ex, M * N, "ex");
     need_opt_f32(emean, N, "emean"); need_opt_f32(acc, rep, "acc");
     TORCH_CHECK(ebits->scalar_type() == at::kByte && ebits->is_contiguous() && ebits->numel() >= M * N / 8, "ebits");
     if (opt_ptr(ex2)) {
@@ -1064,20 +976,14 @@ void conv1x1_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor C, int64_
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
   kdl::Conv1x1Args a{};
-  a.A = A.data_ptr(); a.B = B.data_ptr(); a.C = sg.nostore ? nullptr : C.data_ptr();
-  a.seg = sg.seg; a.A2 = sg.A2; a.K2 = static_cast<int>(sg.K2); a.ldb = static_cast<int>(ldb);
-  a.K2a = static_cast<int>(sg.K2a); a.seg1_scale = sg.seg1_scale;
-  a.B2 = sg.seg ? (sg.B2 ? sg.B2 : static_cast<const void*>(static_cast<const uint16_t*>(B.data_ptr()) + K)) : nullptr;
-  a.ldb2 = static_cast<int>(sg.B2 ? sg.ldb2 : ldb);
-  a.ebias = sg.ebias;
-  if (epi == 5) a.obits = ebits->data_ptr<uint8_t>();
+  a.A = A.data_ptr(); a.B = B.data_ptr(); a.C = C.data_ptr();
   a.M = static_cast<int>(M); a.N = static_cast<int>(N); a.K = static_cast<int>(K);
   a.Hout = static_cast<int>(Hout); a.Wout = static_cast<int>(Wout); a.Hin = static_cast<int>(Hin);
   a.Win = static_cast<int>(Win); a.stride = static_cast<int>(stride);
-  a.pro_coef = sg.seg ? sg.pro2 : opt_fptr(pro_coef);
+  a.pro_coef = opt_fptr(pro_coef);
   a.epi = static_cast<int>(epi);
   a.shift = opt_fptr(shift); a.acc = opt_fptr(acc);
-  a.ex = sg.seg == 2 ? nullptr : opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
+  a.ex = opt_ptr(ex); a.emean = opt_fptr(emean); a.ecoef = opt_fptr(ecoef);
   a.eres = opt_ptr(eres); a.res_stride = static_cast<int>(res_stride); a.res_H = static_cast<int>(res_H);
   a.res_W = static_cast<int>(res_W);
   a.ebits = ebits.has_value() && ebits->defined() ? ebits->data_ptr<uint8_t>() : nullptr;
@@ -1274,28 +1180,10 @@ void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor d
   check_hip(kdl::conv3x3_dgrad_s2(a, cur_stream()), "conv3x3_s2_dgrad");
 }
 
-// G prologue relu(G scale + shift) armed for the next conv1x1_wgrad on this
-// thread (csrc/wgrad_dma.hip GRELU: the a^T a of a BN+ReLU output); coef = [2N]
-thread_local const float* g_grelu_arm = nullptr;
-thread_local int64_t g_grelu_n = 0;
-void wgrad_grelu_arm(const at::Tensor& coef) {
-  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() % 2 == 0,
-              "wgrad_grelu_arm: fp32 [2N] scale | shift");
-  g_grelu_arm = coef.data_ptr<float>();
-  g_grelu_n = coef.numel() / 2;
-}
-
 void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
                    at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t M, int64_t N, int64_t K,
                    int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride) {
   const BwdArm bw = take_bwd_arm();
-  const float* grelu = g_grelu_arm;
-  const int64_t grelu_n = g_grelu_n;
-  g_grelu_arm = nullptr;
-  if (grelu) {
-    TORCH_CHECK(!bw.x && grelu_n >= N && stride == 1 && opt_ptr(pro_coef),
-                "wgrad_grelu_arm: dense rows with an A prologue, coef [2N], no backward-apply arm");
-  }
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_wgrad: need K % 64 == 0, N % 64 == 0");
   if (bw.x) {
     TORCH_CHECK(bw.C == N && bw.rows == M, "bn_bwd_pro_arm: armed for [", bw.rows, ", ", bw.C,
@@ -1319,53 +1207,8 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
                                dW.has_value() && dW->defined() ? dW->data_ptr() : nullptr, static_cast<float>(scale),
                                static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Hout),
                                static_cast<int>(Wout), static_cast<int>(Hin), static_cast<int>(Win),
-                               static_cast<int>(stride), cur_stream(), bw.x, grelu ? grelu : bw.coef, grelu != nullptr),
+                               static_cast<int>(stride), cur_stream(), bw.x, bw.coef),
             "conv1x1_wgrad");
-}
-
-// ---- bnfold.hip
-void bn_fold_dgrad(const at::Tensor& w3, const at::Tensor& bcoef, at::Tensor bp, at::Tensor bias) {
-  TORCH_CHECK(w3.dim() == 2, "bn_fold_dgrad: w3 [N4, C]");
-  const int64_t N4 = w3.size(0), C = w3.size(1);
-  need_bf16(w3, N4 * C, "bn_fold_dgrad w3");
-  need_opt_f32(bcoef, 3 * N4, "bn_fold_dgrad bcoef");
-  need_bf16(bp, C * 2 * C, "bn_fold_dgrad bp");
-  need_opt_f32(bias, C, "bn_fold_dgrad bias");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(w3.device());
-  check_hip(kdl::bn_fold_dgrad(w3.data_ptr(), bcoef.data_ptr<float>(), static_cast<int>(N4), static_cast<int>(C),
-                               bp.data_ptr(), bias.data_ptr<float>(), cur_stream()),
-            "bn_fold_dgrad");
-}
-
-int64_t relu_colsum_parts(int64_t M) { return kdl::relu_colsum_parts(M); }
-
-void relu_colsum(const at::Tensor& x, const at::Tensor& coef, int64_t C, at::Tensor part) {
-  TORCH_CHECK(C > 0 && C % 8 == 0 && x.numel() % C == 0, "relu_colsum: C % 8 == 0 dividing x");
-  const int64_t M = x.numel() / C;
-  need_bf16(x, M * C, "relu_colsum x");
-  need_opt_f32(coef, 2 * C, "relu_colsum coef");
-  need_opt_f32(part, kdl::relu_colsum_parts(M) * C, "relu_colsum part");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  check_hip(kdl::relu_colsum(x.data_ptr(), coef.data_ptr<float>(), M, static_cast<int>(C), part.data_ptr<float>(),
-                             cur_stream()),
-            "relu_colsum");
-}
-
-void bn_fold_wgrad(const at::Tensor& w3, const at::Tensor& bcoef, const at::Tensor& G, const at::Tensor& Q,
-                   const at::Tensor& part, int64_t nparts, at::Tensor dw) {
-  TORCH_CHECK(w3.dim() == 2, "bn_fold_wgrad: w3 [N4, C]");
-  const int64_t N4 = w3.size(0), C = w3.size(1);
-  need_bf16(w3, N4 * C, "bn_fold_wgrad w3");
-  need_opt_f32(bcoef, 3 * N4, "bn_fold_wgrad bcoef");
-  need_opt_f32(G, N4 * C, "bn_fold_wgrad G");
-  need_opt_f32(Q, C * C, "bn_fold_wgrad Q");
-  need_opt_f32(part, nparts * C, "bn_fold_wgrad part");
-  need_bf16(dw, N4 * C, "bn_fold_wgrad dw");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(w3.device());
-  check_hip(kdl::bn_fold_wgrad(w3.data_ptr(), bcoef.data_ptr<float>(), G.data_ptr<float>(), Q.data_ptr<float>(),
-                               part.data_ptr<float>(), static_cast<int>(nparts), static_cast<int>(N4),
-                               static_cast<int>(C), dw.data_ptr(), cur_stream()),
-            "bn_fold_wgrad");
 }
 
 // fixed-order sum of nsplit fp32 [nk] slabs into the first (fp32, in place)
@@ -1629,13 +1472,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dedup_csr", &dedup_csr, "sync-free id de-duplication (uniq/inv/count on the device) + optional CSR of the inverse");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
-  m.def("wgrad_grelu_arm", &wgrad_grelu_arm, "arm the next conv1x1_wgrad: G <- relu(G scale + shift), coef [2N]");
-  m.def("bn_fold_dgrad", &bn_fold_dgrad, "BN3-folded conv3 data-gradient weights [C][4C + C] + bias [C]");
-  m.def("relu_colsum_parts", &relu_colsum_parts, "partial rows relu_colsum writes for M rows");
-  m.def("relu_colsum", &relu_colsum, "per-block column sums of relu(x scale + shift)");
-  m.def("bn_fold_wgrad", &bn_fold_wgrad, "BN3-folded conv3 weight gradient from G = g^T a2, Q = a2^T a2, sum(a2)");
   m.def("slab_reduce_f32", &slab_reduce_f32, "fixed-order fp32 sum of slabs into the first");
-  m.def("conv_seg_arm", &conv_seg_arm, "arm the next conv1x1_gemm: a second K segment (1 summed, 2 recompute), MASKX bias, statistics-only");
   m.def("bn_bwd_pro_arm", &bn_bwd_pro_arm, "fuse this BN's backward apply (input x, workspace ws) into the next conv1x1_gemm's A (or conv1x1_wgrad's G) staging; optional write-through tensor");
   m.def("bn_fin_arm", &bn_fin_arm, "fold the BN finalize of this workspace (C channels, M elements) into the next conv GEMM launch");
   m.def("bn_fin_desc", &bn_fin_desc, "write a BN layer's finalize descriptor into its workspace tail");

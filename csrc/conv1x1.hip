@@ -67,32 +67,22 @@ constexpr int BK = 64;
 // tiles stay within 80 KiB of LDS (two blocks per CU) up to K = 512, 64-wide
 // tiles up to K = 2048 (the widest ResNet-50 data-gradient K)
 __host__ __device__ constexpr int bwd_kmax(int bn) { return bn >= 128 ? 512 : 2048; }
-// widest second K segment (A2 row: the BN2 width of a recompute block's conv3,
-// C <= 512) and widest first segment with a per-channel scale (4C <= 2048)
-constexpr int kSegKmax = 512, kSeg1Kmax = 2048;
 
 // PRO: 0 none, PRO_FWD = BN+ReLU of the previous layer, PRO_BWD = BN-backward
-// apply (GemmParams::bx / bcoef; dense rows only), PRO_SEG / PRO_RECOMP = a
-// second K segment (GemmParams::A2 / B2 / K2) staged through the BN+ReLU
-// prologue, summed into the output (SEG) or into a second accumulator whose
-// bf16 tile is the epilogue's BN input x (RECOMP: a conv output recomputed
-// instead of read back -- csrc/gemm_epi.h XL)
+// apply (GemmParams::bx / bcoef; dense rows only)
 // PRO_RES = the previous block's closing BN + residual + ReLU, relu(A * scale +
 // shift + R) with R = GemmParams::bx, written through (the blocks of output
 // tile 0) as the block output and its packed ReLU mask (GemmParams::obits):
 // the apply pass feeding the next block's conv1, fused into that conv
 // PRO_RES2 = the same after a downsample block: R = bx * scale_d + shift_d (the
 // downsample branch's BN), bn_fwd_apply_dual's expression
-enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_SEG = 3, PRO_RECOMP = 4, PRO_RES = 5, PRO_RES2 = 6 };
+enum { PRO_NONE = 0, PRO_FWD = 1, PRO_BWD = 2, PRO_RES = 5, PRO_RES2 = 6 };
 
 template <int BM, int BN, int MINB, int PRO, int GATHER, int EPI, int KBK = BK>
 __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
   static_assert((PRO != PRO_BWD && PRO != PRO_RES && PRO != PRO_RES2) || GATHER == G_DENSE,
                 "the two-input prologues read dense rows");
   constexpr bool TWO_IN = PRO == PRO_BWD || PRO == PRO_RES || PRO == PRO_RES2;  // A and a second row operand bx
-  constexpr bool SEG = PRO == PRO_SEG || PRO == PRO_RECOMP;
-  static_assert(!SEG || GATHER == G_DENSE, "two-segment K reads dense rows");
-  static_assert(PRO != PRO_RECOMP || EPI == EPI_RESBITS, "the recomputed tile feeds the RESBITS epilogue");
   // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
   // [BM][BN + 8] output tile and finally as the reduction scratch.
   constexpr int LDK = KBK + 8;  // padded LDS row (bf16): 16-B slot stride odd -> conflict-free fragment reads
@@ -102,13 +92,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // once per block behind the operand buffers (one __shared__ array: a second
   // one can make hipcc drain the pipeline, cdna_hip_programming.md §5 item 4a)
   constexpr int KT = TWO_IN ? bwd_kmax(BN) : 0;
-  // SEG / RECOMP: segment 2's BN scale | shift staged once per block (read in
-  // swrite: no coefficient registers live across the K loop), K2 <= kSegKmax
-  constexpr int KS = (PRO == PRO_SEG || PRO == PRO_RECOMP) ? 2 * kSegKmax + (PRO == PRO_SEG ? kSeg1Kmax : 0) : 0;
-  // RECOMP: a third region holds the recomputed x tile [BM][BN + 8] beside the
-  // two stage buffers, so the next tile's first K-step still overlaps the epilogue
-  constexpr int XT = PRO == PRO_RECOMP ? BM * (BN + 8) : 0;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kBuf + 6 * KT + XT + 2 * KS];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kBuf + 6 * KT];
   float* coef_lds = reinterpret_cast<float*>(lds + 2 * kBuf);
   (void)coef_lds;
   constexpr int WN = (BN >= 64 && BM >= 64) ? 2 : 1;  // waves along N
@@ -124,7 +108,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   // buffer, so the next tile's first K-step stays in registers through the
   // epilogue (which then owns both buffers) and is staged after it.
   constexpr bool SPLIT_C = BM * LDC > kBuf;
-  static_assert(!SPLIT_C || PRO != PRO_RECOMP, "RECOMP: 64-deep K-steps");
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int nblk = gridDim.x;
@@ -134,9 +117,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   const int gm = q / tiles_n;
   const int n0 = tile_n * BN;
   const int K = p.K, M = p.M, N = p.N;
-  const int nk1 = K / KBK;                           // segment-1 K-steps
-  const int nk = SEG ? nk1 + p.K2 / KBK : nk1;
-  const int ldb = SEG ? p.ldb : K;
+  const int nk = K / KBK;
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
 
   // staging coordinates (fixed per thread)
@@ -165,11 +146,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   uint32_t a_valid = 0;
   const bool wthru = TWO_IN && p.aout != nullptr && tile_n == 0;
   (void)rx; (void)st_k0; (void)a_valid; (void)wthru;
-  // SEG / RECOMP: the chunk's row (segment 2 has its own row stride) and
-  // whether the K-step held in ra is a segment-2 one (prologue applies)
-  int a_m[SEG ? A_CH : 1];
-  bool st_seg2 = false;
-  (void)a_m; (void)st_seg2;
   if constexpr (TWO_IN) {  // PRO_BWD: k | c1 | c0; PRO_RES: scale | shift; PRO_RES2: + scale_d | shift_d
     for (int i = t; i < (PRO == PRO_BWD ? 3 : PRO == PRO_RES2 ? 4 : 2) * K / 4; i += kThreads)
       reinterpret_cast<float4*>(coef_lds)[i] = (PRO == PRO_RES2 && i >= K / 2)
@@ -177,22 +153,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
                                                    : reinterpret_cast<const float4*>(p.bcoef)[i];
     __syncthreads();
   }
-  // [2 K2a] segment-2 scale | shift, then (PRO_SEG) [K] segment-1 scale
-  float* seg_coef = reinterpret_cast<float*>(lds + 2 * kBuf + 6 * KT + XT);
-  float* seg1_sc = seg_coef + 2 * kSegKmax;
-  (void)seg_coef; (void)seg1_sc;
-  const int K2a = SEG ? p.K2a : 0;
-  if constexpr (KS > 0) {
-    for (int i = t; i < 2 * K2a / 4; i += kThreads)
-      reinterpret_cast<float4*>(seg_coef)[i] = reinterpret_cast<const float4*>(p.pro_coef)[i];
-    if constexpr (PRO == PRO_SEG) {
-      if (p.seg1_scale)
-        for (int i = t; i < K / 4; i += kThreads)
-          reinterpret_cast<float4*>(seg1_sc)[i] = reinterpret_cast<const float4*>(p.seg1_scale)[i];
-    }
-    __syncthreads();
-  }
-
   auto setup_rows = [&](int tm) {
     a_valid = 0;
 #pragma unroll
@@ -213,37 +173,10 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           a_iw[i] = ow * p.stride - 1;
         }
       }
-      if constexpr (SEG) a_m[i] = m;
-      else a_off[i] = src * K;
+      a_off[i] = src * K;
     }
   };
   auto gload = [&](int kt) {
-    if constexpr (SEG) {  // dense rows; segment 2 through the BN+ReLU prologue
-      const bool s2 = kt >= nk1;
-      const int k0 = (s2 ? kt - nk1 : kt) * KBK;
-      if (s2) {
-#pragma unroll
-        for (int i = 0; i < A_CH; ++i)
-          ra[i] = ld16(p.A2 + static_cast<int64_t>(a_m[i]) * K2a + k0 % K2a + a_kc[i]);
-#pragma unroll
-        for (int i = 0; i < B_CH; ++i) {
-          const int c = t + i * kThreads;
-          rb[i] = ld16(p.B2 + static_cast<int64_t>(n0 + c / CPRK) * p.ldb2 + k0 + (c % CPRK) * 8);
-        }
-        st_k0 = k0;
-      } else {
-#pragma unroll
-        for (int i = 0; i < A_CH; ++i) ra[i] = ld16(p.A + static_cast<int64_t>(a_m[i]) * K + k0 + a_kc[i]);
-#pragma unroll
-        for (int i = 0; i < B_CH; ++i) {
-          const int c = t + i * kThreads;
-          rb[i] = ld16(p.B + static_cast<int64_t>(n0 + c / CPRK) * ldb + k0 + (c % CPRK) * 8);
-        }
-        st_k0 = k0;
-      }
-      st_seg2 = s2;
-      return;
-    }
     const int k0 = kt * KBK;
     int kc0 = k0;  // channel offset of this K-step within a tap
     if constexpr (GATHER == G_CONV3) {
@@ -309,35 +242,11 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
         }
       }
     }
-    bool fwd_pro = PRO == PRO_FWD;
-    bool seg1_scaled = false;
-    (void)seg1_scaled;
-    if constexpr (SEG) {
-      fwd_pro = st_seg2;
-      if constexpr (PRO == PRO_SEG) seg1_scaled = !st_seg2 && p.seg1_scale != nullptr;
-      if (seg1_scaled) {  // segment 1: one scale per K channel (psc reused, no shift)
-        const int c = st_k0 + a_kc[0];
-#pragma unroll
-        for (int j = 0; j < 8; j += 4) {
-          const float4 a = *reinterpret_cast<const float4*>(seg1_sc + c + j);
-          psc[j] = a.x; psc[j + 1] = a.y; psc[j + 2] = a.z; psc[j + 3] = a.w;
-        }
-      }
-      if (fwd_pro) {  // this thread's 8 channels of the staged segment-2 K-step, from LDS
-        const int c = st_k0 % K2a + a_kc[0];
-#pragma unroll
-        for (int j = 0; j < 8; j += 4) {
-          const float4 a = *reinterpret_cast<const float4*>(seg_coef + c + j);
-          const float4 b = *reinterpret_cast<const float4*>(seg_coef + K2a + c + j);
-          psc[j] = a.x; psc[j + 1] = a.y; psc[j + 2] = a.z; psc[j + 3] = a.w;
-          psf[j] = b.x; psf[j + 1] = b.y; psf[j + 2] = b.z; psf[j + 3] = b.w;
-        }
-      }
-    }
+    constexpr bool fwd_pro = PRO == PRO_FWD;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint4 v = ra[i];
-      if (fwd_pro) {
+      if constexpr (fwd_pro) {
         float f[8];
         unpack8(v, f);
 #pragma unroll
@@ -345,12 +254,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
           const float o = fmaf(f[j], psc[j], psf[j]);
           f[j] = o > 0.f ? o : 0.f;
         }
-        v = pack8(f);
-      } else if (seg1_scaled) {
-        float f[8];
-        unpack8(v, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= psc[j];
         v = pack8(f);
       } else if constexpr (PRO == PRO_BWD) {
         float f[8], x[8];
@@ -392,26 +295,8 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   };
 
-  Epilogue<BM, BN, kThreads, EPI, G_DENSE, PRO == PRO_RECOMP, PRO == PRO_SEG> epi;
+  Epilogue<BM, BN, kThreads, EPI, G_DENSE> epi;
   epi.init(t, n0);
-  // RSTATS: each lane's running shifted sums of its accumulator slots -- slot
-  // (i, r) is output channel n0 + wn0 + 32 i + (r & 3) + 8 (r >> 2) + 4 fh for
-  // every tile of the block -- over the bf16-rounded outputs (the values STATS
-  // would have summed), reduced across lanes / waves once after the last tile
-  constexpr bool RSTATS = EPI == EPI_RSTATS;
-  constexpr int RS = RSTATS ? TN : 1;
-  float rs1[RS][16], rs2[RS][16], rsh[RS][16];
-  if constexpr (RSTATS) {
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        rsh[i][r] = p.shift[n0 + wn0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * ((lane & 63) >> 5)];
-        rs1[i][r] = 0.f;
-        rs2[i][r] = 0.f;
-      }
-  }
-
   int tm = gm;
   if (tm < tiles_m) {
     setup_rows(tm);
@@ -421,20 +306,13 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   __syncthreads();
   int cur = 0;
   const int fr = lane & 31, fh = lane >> 5;
-  // Overlapped epilogue (run between the tile's last MFMAs and the staging of
-  // the next tile's first K-step, whose loads are then in flight during it):
-  // measured SLOWER on every variant that fits it in registers (APPLY 197 ->
-  // 287 us, recompute RESBITS 305 -> 396 us, folded dgrad 150 -> 164 us at the
-  // 56x56 stage), so compiled out; kept for the record of the experiment
-  constexpr bool OVL = false;
   for (; tm < tiles_m; tm += GM) {
     f32x16_t acc[TN][TM];
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-    // one staged K-step's fragments + MFMAs into ``a`` (static indices only:
-    // the RECOMP accumulator choice is a branch around two inlined copies)
+    // one staged K-step's fragments + MFMAs into ``a``
     auto mma = [&](const bf16_t* As, f32x16_t (&a)[TN][TM]) {
       const bf16_t* Bs = As + BM * LDK;
 #pragma unroll
@@ -453,36 +331,15 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
             a[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], a[i][j], 0, 0, 0);
       }
     };
-    // the tile's epilogue (csrc/gemm_epi.h) with its output tile in LDS at Cb
-    // (RSTATS: register sums, no LDS); row-side operands of the first prefetch
-    // group are issued before the accumulators go to LDS
+    // the tile's epilogue (csrc/gemm_epi.h) with its output tile in LDS at Cb;
+    // row-side operands of the first prefetch group are issued before the
+    // accumulators go to LDS
     auto epilogue = [&](bf16_t* Cb) {
-      if constexpr (RSTATS) {  // statistics only: no LDS round trip, nothing stored
-#pragma unroll
-        for (int j = 0; j < TM; ++j) {
-          if (tm * BM + wm0 + 32 * j + fr >= M) continue;  // rows past M (this lane's column)
-#pragma unroll
-          for (int i = 0; i < TN; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float y = __uint_as_float(static_cast<uint32_t>(f32_to_bf16(acc[i][j][r])) << 16);
-              const float d = y - rsh[i][r];
-              rs1[i][r] += d;
-              rs2[i][r] = fmaf(d, d, rs2[i][r]);
-            }
-        }
-        return;
-      }
       epi.begin(p, tm);
       bf16_t* Cs = Cb;
       acc_to_lds<TN, TM>(acc, Cs, LDC, wm0, wn0, lane);
-      bf16_t* Xs = nullptr;
-      if constexpr (PRO == PRO_RECOMP) {  // acc holds the recomputed conv output (x of the RESBITS sums)
-        Xs = Cs;
-        Cs = lds + 2 * kBuf;  // (KT == 0: no coefficient table in between)
-      }
       __syncthreads();
-      epi.rows(p, Cs, tm, Xs);
+      epi.rows(p, Cs, tm);
       __syncthreads();  // Cs is restaged by a later K-step
     };
     for (int kt = 0; kt < nk; ++kt) {
@@ -496,30 +353,10 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       }
       const bf16_t* As = lds + cur * kBuf;
       mma(As, acc);
-      if constexpr (PRO == PRO_RECOMP) {
-        // segment 1 done: its tile goes to the third LDS region and the same
-        // accumulators recompute the x tile (one accumulator set: 256 VGPRs)
-        if (kt == nk1 - 1) {
-          acc_to_lds<TN, TM>(acc, lds + 2 * kBuf, LDC, wm0, wn0, lane);
-#pragma unroll
-          for (int i = 0; i < TN; ++i)
-#pragma unroll
-            for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-        }
-      }
-      if (OVL && !more_k) {
-        // overlapped epilogue: the tile's last K-step is consumed (after this
-        // barrier buffer cur is free for the output tile) and the next tile's
-        // first K-step is still in flight to registers -- its load latency hides
-        // under the epilogue instead of stalling swrite below
-        __syncthreads();
-        epilogue(lds + cur * kBuf);
-      }
       if (more_k || (more && !SPLIT_C)) swrite(cur ^ 1);
       __syncthreads();
       cur ^= 1;
     }
-    if constexpr (OVL) continue;
     // D[n][m] -> LDS [m][n] (buffer cur^1 is free: its last reader was the final
     // K-step, which ended with a barrier; buffer cur may already hold the next
     // tile's first K-step)
@@ -531,48 +368,6 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
     }
   }
 
-  if constexpr (RSTATS) {
-    // lanes of one half-wave (same fh) share channels: butterfly over the 32
-    // columns, then the WM wave rows of each channel column through LDS
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          rs1[i][r] += __shfl_xor(rs1[i][r], o);
-          rs2[i][r] += __shfl_xor(rs2[i][r], o);
-        }
-    float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2] (the last K-step ended with a barrier)
-    const int wr = wave / WN;
-    if (fr == 0) {
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ch = wn0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          red[(wr * BN + ch) * 2] = rs1[i][r];
-          red[(wr * BN + ch) * 2 + 1] = rs2[i][r];
-        }
-    }
-    __syncthreads();
-    if (t < BN && gm < tiles_m) {
-      float a1 = 0.f, a2 = 0.f;
-      for (int w = 0; w < WM; ++w) {  // fixed order
-        a1 += red[(w * BN + t) * 2];
-        a2 += red[(w * BN + t) * 2 + 1];
-      }
-      float* rep = p.acc + static_cast<int64_t>(b % kRep) * 2 * N + n0 + t;
-      atomic_add_f32(rep, a1);
-      atomic_add_f32(rep + N, a2);
-    }
-    if (p.fin_ws) {  // (every block arrives, as Epilogue::finish)
-      Epilogue<BM, BN, kThreads, EPI_STATS> fe;
-      fe.init(t, n0);
-      fe.finalize_last(p, red + 2 * WM * BN);
-    }
-    return;
-  }
   epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
 }
 
@@ -840,13 +635,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
 // backward-apply prologue feeds only the dense dgrad epilogues
 template <int BM, int BN, int MINB, int PRO, int GATHER, int KBK>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
-  if constexpr (PRO == PRO_SEG) {  // the BN-folded conv3 data gradient
-    if (epi == EPI_MASKX) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_MASKX, KBK>(p, s);
-    return hipErrorInvalidValue;
-  } else if constexpr (PRO == PRO_RECOMP) {  // conv1 dgrad + residual, recomputing the previous conv3
-    if (epi == EPI_RESBITS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RESBITS, KBK>(p, s);
-    return hipErrorInvalidValue;
-  } else if constexpr (PRO == PRO_RES || PRO == PRO_RES2) {  // the next block's conv1 (forward, bn1 statistics)
+  if constexpr (PRO == PRO_RES || PRO == PRO_RES2) {  // the next block's conv1 (forward, bn1 statistics)
     if (epi == EPI_STATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
     return hipErrorInvalidValue;
   } else if constexpr (PRO == PRO_BWD) {
@@ -861,14 +650,6 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     switch (epi) {
       case EPI_PLAIN: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_PLAIN, KBK>(p, s);
       case EPI_STATS: return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_STATS, KBK>(p, s);
-    }
-    if constexpr (PRO == PRO_FWD && GATHER == G_DENSE && KBK == BK && BM == 64 && BN == 64) {  // (RSTATS A/B tile)
-      if (epi == EPI_RSTATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RSTATS, KBK>(p, s);
-    }
-    if constexpr (PRO == PRO_FWD && GATHER == G_DENSE && KBK == BK && BM == 128 && MINB == 2) {  // recomputed conv3 + closing BN/residual/ReLU
-      if (epi == EPI_APPLY) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_APPLY, KBK>(p, s);
-      if constexpr (BN == 64)
-        if (epi == EPI_RSTATS) return launch_gemm<BM, BN, MINB, PRO, GATHER, EPI_RSTATS, KBK>(p, s);
     }
     if constexpr (PRO == PRO_NONE && GATHER == G_DENSE) {
       switch (epi) {
@@ -886,17 +667,13 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
 
 template <int BM, int BN, int MINB, int KBK = BK>
 hipError_t dispatch_pg(const GemmParams& p, int epi, int pro, int gather, hipStream_t s) {
-  if (pro == PRO_BWD || pro == PRO_RES || pro == PRO_RES2 || pro == PRO_SEG || pro == PRO_RECOMP) {
+  if (pro == PRO_BWD || pro == PRO_RES || pro == PRO_RES2) {
     if constexpr (BM == 128 && MINB == 2 && KBK == BK) {  // the two configs conv1x1_gemm routes them to
       if (gather != G_DENSE) return hipErrorInvalidValue;
       if (pro == PRO_BWD) return dispatch_epi<BM, BN, MINB, PRO_BWD, G_DENSE, KBK>(p, epi, s);
       if (pro == PRO_RES) return dispatch_epi<BM, BN, MINB, PRO_RES, G_DENSE, KBK>(p, epi, s);
       if constexpr (BN == 64)  // (128 x 128 spills with the fourth coefficient row)
         if (pro == PRO_RES2) return dispatch_epi<BM, BN, MINB, PRO_RES2, G_DENSE, KBK>(p, epi, s);
-      if constexpr (BN == 64) {  // (the 128 x 64 tiles conv1x1_gemm routes them to)
-        if (pro == PRO_SEG) return dispatch_epi<BM, BN, MINB, PRO_SEG, G_DENSE, KBK>(p, epi, s);
-        return dispatch_epi<BM, BN, MINB, PRO_RECOMP, G_DENSE, KBK>(p, epi, s);
-      }
     }
     return hipErrorInvalidValue;
   }
@@ -956,29 +733,16 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
   p.fin_ws = a.fin_ws; p.fin_ws2 = a.fin_ws2; p.fin_M = a.fin_M;
   p.bx = static_cast<const bf16_t*>(a.bx); p.bcoef = a.bcoef; p.bcoef2 = a.bcoef2;
   p.aout = static_cast<bf16_t*>(a.aout);
-  p.A2 = static_cast<const bf16_t*>(a.A2); p.B2 = static_cast<const bf16_t*>(a.B2);
-  p.K2 = a.K2; p.ldb = a.ldb > 0 ? a.ldb : a.K; p.ldb2 = a.ldb2;
-  p.K2a = a.K2a > 0 ? a.K2a : a.K2; p.seg1_scale = a.seg1_scale;
-  p.ebias = a.ebias; p.obits = a.obits;
+  p.obits = a.obits;
   const bool bpro = a.bx != nullptr;
-  if (bpro && !a.bres && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS || a.seg))
+  if (bpro && !a.bres && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi == EPI_STATS))
     return hipErrorInvalidValue;
-  if (bpro && a.bres && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi != EPI_STATS || a.seg ||
+  if (bpro && a.bres && (!a.bcoef || a.pro_coef || a.stride > 1 || a.ksize == 3 || a.epi != EPI_STATS ||
                          !a.aout || !a.obits || a.K > bwd_kmax(64)))
     return hipErrorInvalidValue;
-  if (a.seg) {  // two-segment K: dense rows, segment 2 through the BN+ReLU prologue
-    if ((a.seg != 1 && a.seg != 2) || !a.A2 || !a.B2 || !a.pro_coef || a.K2 <= 0 || a.K2 % BK || p.K2a % BK ||
-        p.K2a > kSegKmax || a.K2 % p.K2a || (a.seg1_scale && (a.seg != 1 || a.K > kSeg1Kmax)) ||
-        a.stride > 1 ||
-        a.ksize == 3 || p.ldb < a.K || a.ldb2 < a.K2 || (a.seg == 1 && a.epi != EPI_MASKX) ||
-        (a.seg == 2 && a.epi != EPI_RESBITS))
-      return hipErrorInvalidValue;
-  }
-  if (a.epi == EPI_APPLY && (!a.pro_coef || !a.obits || !a.ecoef || !a.eres || a.stride > 1 || a.ksize == 3 ||
-                             p.res_stride != 1))
+  if (a.epi != EPI_PLAIN && a.epi != EPI_STATS && a.epi != EPI_MASKX && a.epi != EPI_RESBITS && a.epi != EPI_RES)
     return hipErrorInvalidValue;
-  const int pro = a.seg == 1 ? PRO_SEG : a.seg == 2 ? PRO_RECOMP
-                : bpro ? (a.bres == 2 ? PRO_RES2 : a.bres ? PRO_RES : PRO_BWD)
+  const int pro = bpro ? (a.bres == 2 ? PRO_RES2 : a.bres ? PRO_RES : PRO_BWD)
                 : a.pro_coef != nullptr ? PRO_FWD : PRO_NONE;
   int gather = a.stride > 1 ? G_STRIDED : G_DENSE;
   p.Cin = a.K;
@@ -1022,18 +786,6 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
     if (gather == G_CONV3 && p.N == 512 && g_forced_cfg_unset()) cfg = 1;
     const hipError_t e = igemm(p, epi, gather, cfg, s);
     if (e != hipErrorInvalidValue) return e;
-  }
-  // 128 x 64 tiles: at 128 x 128 the second accumulator (RECOMP) or the segment
-  // bookkeeping + MASKX bias (SEG) spill (752 / 76 B of scratch per lane)
-  if (pro == PRO_SEG || pro == PRO_RECOMP) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
-  if (epi == EPI_APPLY && p.N % 128 == 0) return dispatch_pg<128, 128, 2>(p, epi, pro, gather, s);
-  if (epi == EPI_APPLY) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
-  // statistics-only forward conv (the recompute blocks' conv3): register sums
-  // (KDL_RSTATS: 0 = the LDS epilogue with no store, 2 = 64 x 64 tiles at 3 blocks per CU)
-  static const int rstats = [] { const char* e = getenv("KDL_RSTATS"); return e ? atoi(e) : 1; }();
-  if (epi == EPI_STATS && !p.C && pro == PRO_FWD && gather == G_DENSE && rstats) {
-    if (rstats == 2) return dispatch_pg<64, 64, 3>(p, EPI_RSTATS, pro, gather, s);
-    return dispatch_pg<128, 64, 2>(p, EPI_RSTATS, pro, gather, s);  // (128 x 128: 32 slots per lane spill)
   }
   if (pro == PRO_RES2) {  // four coefficient rows; 128 x 64 tiles (128 x 128 spills 12 B)
     if (4 * p.K <= 3 * bwd_kmax(64)) return dispatch_pg<128, 64, 2>(p, epi, pro, gather, s);
@@ -1197,11 +949,9 @@ namespace {
 // big: the workspace holds wgrad_splits(M, N, K, true) slabs (3x3 256-tile configs)
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
-                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr,
-                      bool grelu = false) {
+                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr) {
   if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
   const bool bwd = gx != nullptr;
-  if (grelu && (bwd || !gcoef || !pro_coef || mode != G_DENSE || gemm_core_mode() == 0)) return hipErrorInvalidValue;
   // the G prologue exists on the LDS-DMA kernel only
   if (bwd && (gemm_core_mode() == 0 || !gcoef || mode == G_CONV3 || (pro_coef && mode != G_DENSE)))
     return hipErrorInvalidValue;
@@ -1219,7 +969,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
   if (gemm_core_mode() != 0) {  // LDS-DMA pipeline (csrc/wgrad_dma.hip) unless forced off
     WgParams wp{};
     wp.G = g; wp.A = x; wp.pro = pro_coef; wp.dw32 = dw32;
-    wp.gx = static_cast<const bf16_t*>(gx); wp.gcoef = gcoef; wp.grelu = grelu ? 1 : 0;
+    wp.gx = static_cast<const bf16_t*>(gx); wp.gcoef = gcoef;
     wp.M = M; wp.N = N; wp.K = K; wp.Hout = Hout; wp.Wout = Wout; wp.Hin = Hin; wp.Win = Win;
     wp.stride = stride; wp.cin = cin; wp.rps = rps; wp.tiles_k = tiles_k; wp.mode = mode;
     wp.a_rows = mode == G_DENSE ? M : static_cast<int64_t>(M / (Hout * Wout)) * Hin * Win;
@@ -1231,7 +981,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     if (e != hipSuccess && e != hipErrorInvalidValue) return e;
     done = e == hipSuccess;
   }
-  if (!done && (bwd || grelu)) return hipErrorInvalidValue;
+  if (!done && bwd) return hipErrorInvalidValue;
   if (!done) {
     if (tn > 128 || tk > 128) {  // the register-staged kernel has no 256 tiles: same splits, 128 tiles
       tn = tk = 128;
@@ -1250,9 +1000,9 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
 
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
-                         const void* gx, const float* gcoef, bool grelu) {
+                         const void* gx, const float* gcoef) {
   return wgrad_impl(G, A, pro_coef, dw32, dW, scale, M, N, K, Hout, Wout, Hin, Win, stride,
-                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef, grelu);
+                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef);
 }
 
 int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {

@@ -16,15 +16,8 @@
 //            the previous block's packed ReLU bits, + bn3 (and downsample BN)
 //            backward sums
 //   RES      g = dgrad + d(identity), no mask (network stem)
-//   APPLY    out = relu(y * scale + shift + residual) with the packed 1-bit
-//            ReLU mask (the bottleneck's closing BN + residual + ReLU, applied
-//            to a recomputed conv3 whose output is never stored: the same
-//            fmaf / add / compare sequence as bn_act.hip bn_fwd_apply_kernel)
 // and after its last tile folds the per-thread sums in LDS and adds them to
 // the BN workspace replica of the block (one atomic per channel per block).
-// STATS with C == null stores nothing (the statistics pass of a recomputed conv).
-// XL: the BN input x of MASKX / RESBITS is a second LDS tile (the conv output
-// recomputed by the same kernel, csrc/conv1x1.hip PRO_RECOMP), not a global load.
 #pragma once
 
 #include "bn_fin.h"
@@ -40,9 +33,7 @@ typedef __attribute__((ext_vector_type(2))) float f2_t;
 
 constexpr int kRep = 32;  // replica count of the BN workspace (== bn_act.hip kReplicas)
 
-// EPI_RSTATS: STATS without a stored output, summed straight from the accumulator
-// registers across the block's tiles (csrc/conv1x1.hip; no per-tile LDS round trip)
-enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4, EPI_APPLY = 5, EPI_RSTATS = 6 };
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
 // A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s) |
 // data gradient of a stride-2 3x3 pad-1 conv as four sub-pixel class GEMMs (csrc/igemm.hip)
 // G_STEM (csrc/stem.hip): a tile is 2 output rows x 112 columns of one image
@@ -88,29 +79,13 @@ struct GemmParams {
   // dx pixels (2i + py, 2j + px).  mc = Nb Hin Win rows per class, padded to
   // mc_pad (a multiple of BM, set by the launcher); M = 4 mc_pad.
   int mc, mc_pad;
-  // Ticketed tile schedule (tile_tickets): per output-column tile c, tk[2c] hands
-  // out M tiles in arrival order and tk[2c + 1] counts the blocks that drew
-  // past the end (the last one resets both); null = the static per-block list
-  unsigned* tk;
   // BN finalize folded into this GEMM (csrc/bn_fin.h): the workspace of the BN
   // whose sums the epilogue produces (second one: RESBITS' downsample BN), and
   // that BN's element count; null = the host launches the finalize
   float* fin_ws;
   float* fin_ws2;
   float fin_M;
-  // Two-segment K (csrc/conv1x1.hip PRO_SEG / PRO_RECOMP, dense rows): the K-steps
-  // past K read segment 2 -- A2 [M, K2] through the BN+ReLU prologue pro_coef
-  // ([2 K2] scale | shift) against B2 [N, ldb2]; segment 1 is A [M, K] against
-  // B [N, ldb].  PRO_SEG sums both into the output, PRO_RECOMP keeps segment 2
-  // in a second accumulator (the epilogue's XL tile).
-  const bf16_t* A2;
-  const bf16_t* B2;
-  int K2, ldb, ldb2;
-  int K2a;                 // A2 row width: segment-2 K column k reads A2 column k % K2a (K2 = 2 K2a: a
-                           // bf16 hi + lo split of B2 against the same A2 columns)
-  const float* seg1_scale; // segment 1: A' = bf16(seg1_scale[k] A) per K channel (null: A as is)
-  const float* ebias;  // MASKX: per-output-channel bias added before the mask (null: none)
-  uint8_t* obits;      // APPLY: packed ReLU mask [M, N/8] (out)
+  uint8_t* obits;      // PRO_RES / PRO_RES2 write-through: packed ReLU mask [M, N/8] (out)
 };
 
 // csrc/wgrad_dma.hip: weight gradient on the LDS-DMA pipeline into fp32
@@ -122,8 +97,7 @@ struct WgParams {
   // optional BN-backward-apply prologue of G: G' = k[n] G + c1[n] gx + c0[n]
   // (GemmParams::bx / bcoef semantics, per output channel n)
   const bf16_t* gx;       // [M][N]
-  const float* gcoef;     // [3N] (grelu: [2N] scale | shift of G' = relu(G scale + shift))
-  int grelu;              // G is a BN+ReLU output (csrc/wgrad_dma.hip GRELU), gx unused
+  const float* gcoef;     // [3N]
   float* dw32;
   int M, N, K;            // K = 9 * cin for 3x3
   int Hout, Wout, Hin, Win, stride, cin;
@@ -143,8 +117,6 @@ hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t 
 // n zeroed ticket counters for one launch, from a per-device ring (self-resetting:
 // every kernel that draws from them leaves them zero); null while a stream capture
 // is under way on a device whose ring does not exist yet
-unsigned* tile_tickets(int n, hipStream_t s);
-bool tickets_enabled();
 // csrc/halo3x3.hip: 3x3 stride-1 conv with an LDS-resident input halo (Cin 64 @ 56x56);
 // hipErrorInvalidValue when the geometry is not one it serves
 hipError_t halo3x3(const GemmParams& p, int epi, hipStream_t s);
@@ -208,26 +180,19 @@ __device__ __forceinline__ void acc_to_lds(const f32x16_t (&acc)[TN][TM], bf16_t
       }
 }
 
-// BIAS: MASKX adds GemmParams::ebias before the mask (compile-time: the runtime
-// check alone cost the 256x256 implicit-GEMM MASKX tile 44 more bytes of spill,
-// and spilling LDS-DMA variants computed wrong rows -- docs/perf_notes.md)
-template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE, bool XL = false, bool BIAS = false>
+template <int BM, int BN, int NT, int EPI, int GATHER = G_DENSE>
 struct Epilogue {
   static constexpr int LDC = BN + 8;
   static constexpr int CPR = BN / 8;           // 16-B chunks per output row
   static constexpr int RPP = NT / CPR;         // rows per epilogue pass
   static constexpr int NP = BM / RPP;          // rows per thread per tile
   // prefetch group (4 rows where 8 spill: RESBITS, and MASKX beside the 256x256 tile's 128 accumulators)
-  // (2 beside the recompute variant's second accumulator)
-  static constexpr int PG = XL ? (NP > 2 ? 2 : NP)
-                          : (EPI == EPI_RESBITS || EPI == EPI_APPLY || (EPI == EPI_MASKX && BM * BN >= 256 * 256))
-                              ? (NP > 4 ? 4 : NP) : (NP > 8 ? 8 : NP);
-  static_assert(!XL || EPI == EPI_MASKX || EPI == EPI_RESBITS, "an LDS x tile feeds MASKX / RESBITS");
-  static constexpr bool LX = (EPI == EPI_MASKX || EPI == EPI_RESBITS) && !XL;  // x from global memory
-  static constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES || EPI == EPI_APPLY;
-  // RESBITS' optional second BN input (downsample branch); the recompute
-  // variant (XL) serves blocks without one, and its registers are scarce
-  static constexpr bool X2 = EPI == EPI_RESBITS && !XL;
+  static constexpr int PG = (EPI == EPI_RESBITS || (EPI == EPI_MASKX && BM * BN >= 256 * 256))
+                                ? (NP > 4 ? 4 : NP) : (NP > 8 ? 8 : NP);
+  static constexpr bool LX = EPI == EPI_MASKX || EPI == EPI_RESBITS;  // the BN input x
+  static constexpr bool LR = EPI == EPI_RESBITS || EPI == EPI_RES;
+  // RESBITS' optional second BN input (downsample branch)
+  static constexpr bool X2 = EPI == EPI_RESBITS;
   static constexpr bool REDUCE = EPI == EPI_STATS || EPI == EPI_MASKX || EPI == EPI_RESBITS;
   // LDS scratch of finish(): 3 sums x NT threads x 8 channels
   static constexpr int kScratchBytes = REDUCE ? 3 * NT * 8 * 4 : 0;
@@ -332,13 +297,6 @@ struct Epilogue {
         em[q] = ld2(p.emean, ch0 + 2 * q);
         ea[q] = ld2(p.ecoef, ch0 + 2 * q);
         eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
-        if constexpr (BIAS) em2[q] = ld2(p.ebias, ch0 + 2 * q);  // (em2 is free in MASKX)
-      }
-    } else if constexpr (EPI == EPI_APPLY) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ea[q] = ld2(p.ecoef, ch0 + 2 * q);
-        eb[q] = ld2(p.ecoef, N + ch0 + 2 * q);
       }
     } else if constexpr (EPI == EPI_RESBITS) {
 #pragma unroll
@@ -349,10 +307,8 @@ struct Epilogue {
     }
   }
 
-  // the tile's rows, from Cs[BM][LDC] (after a barrier that follows acc_to_lds;
-  // XL: the BN input x from Xs[BM][LDC] likewise)
-  __device__ __forceinline__ void rows(const GemmParams& p, const bf16_t* Cs, int tm, const bf16_t* Xs = nullptr) {
-    (void)Xs;
+  // the tile's rows, from Cs[BM][LDC] (after a barrier that follows acc_to_lds)
+  __device__ __forceinline__ void rows(const GemmParams& p, const bf16_t* Cs, int tm) {
     const int N = p.N;
 #pragma unroll
     for (int g0 = 0; g0 < NP; g0 += PG) {
@@ -374,8 +330,7 @@ struct Epilogue {
         const int64_t go = static_cast<int64_t>(m) * N + ch0;
         uint4 xin = make_uint4(0, 0, 0, 0);  // MASKX / RESBITS: the BN input x of this row chunk
         (void)xin;
-        if constexpr (XL) xin = *reinterpret_cast<const uint4*>(&Xs[row * LDC + ec * 8]);
-        else if constexpr (LX) xin = cxv[i];
+        if constexpr (LX) xin = cxv[i];
         uint4 out = raw;  // PLAIN / STATS store the tile as it is
         if constexpr (EPI != EPI_PLAIN) {
           f2_t v[4];
@@ -391,10 +346,6 @@ struct Epilogue {
           } else if constexpr (EPI == EPI_MASKX) {
             f2_t x[4];
             unpack4x2(xin, x);
-            if constexpr (BIAS) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] += em2[q];
-            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const f2_t z = pfma(x[q], ea[q], eb[q]);
@@ -404,19 +355,6 @@ struct Epilogue {
               o[q] = pack2(g);
             }
             out = make_uint4(o[0], o[1], o[2], o[3]);
-          } else if constexpr (EPI == EPI_APPLY) {  // relu(y * scale + shift + residual) + mask bits
-            f2_t r[4];
-            unpack4x2(crv[i], r);
-            uint32_t bits = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const f2_t z = pfma(v[q], ea[q], eb[q]) + r[q];
-              bits |= (z.x > 0.f ? 1u : 0u) << (2 * q);
-              bits |= (z.y > 0.f ? 1u : 0u) << (2 * q + 1);
-              o[q] = pack2(f2_t{z.x > 0.f ? z.x : 0.f, z.y > 0.f ? z.y : 0.f});
-            }
-            out = make_uint4(o[0], o[1], o[2], o[3]);
-            p.obits[static_cast<int64_t>(m) * (N / 8) + (ch0 >> 3)] = static_cast<uint8_t>(bits);
           } else if constexpr (LR) {  // RESBITS / RES: add d(identity), rounded to bf16
             if (crok[i]) {
               f2_t r[4];

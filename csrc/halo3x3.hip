@@ -221,36 +221,10 @@ __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, in
   Epi epi;
   epi.init(t, n0);
 
-  // Ticketed schedule (p.tk, double-buffered form): the N tile's M tiles go to
-  // blocks in arrival order, so a block whose CU is held by the other stream's
-  // kernels takes fewer tiles instead of finishing a fixed list last.  Tickets
-  // run two ahead (the current tile, the one whose halo is in flight); the next
-  // is drawn at the start of a tile and broadcast through the padding row of
-  // the current halo buffer (rows >= nh: never read by the MFMAs, zeroed again
-  // by that buffer's next DMA after everyone has read it).
-  constexpr bool kTk = DOUBLE && HROWS > (TH + 2) * HW_MAX * RP && HALO_BYTES - 16 >= kBM * LDC * 2 &&
-                       HALO_BYTES - 16 >= Epi::kScratchBytes;
-  unsigned* tkc = kTk && p.tk ? p.tk + 2 * tile_n : nullptr;
-  auto slot = [&](int b) { return reinterpret_cast<int*>(Hs + b * HALO_BYTES + HALO_BYTES - 16); };
   int tm = gm0, next = gm0 + gstride;
-  if (tkc) {
-    if (t == 0) {
-      slot(1)[0] = static_cast<int>(__hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      slot(1)[1] = static_cast<int>(__hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();
-    tm = slot(1)[0];
-    next = slot(1)[1];
-    __syncthreads();  // read before buffer 1 takes its first halo
-  }
-  bool any = false;
   int buf = 0;
   if (tm < tiles_m) issue_halo(tm, 0);
   while (tm < tiles_m) {
-    any = true;
-    unsigned drawn = static_cast<unsigned>(tiles_m);
-    if (tkc && t == 0 && next < tiles_m)
-      drawn = __hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (DOUBLE) {
       if (next < tiles_m) {
         issue_halo(next, buf ^ 1);
@@ -302,12 +276,10 @@ __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, in
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (tkc && t == 0) slot(buf)[0] = static_cast<int>(drawn);
     epi.begin(p, tm);
     bf16_t* Cs = reinterpret_cast<bf16_t*>(Hs + buf * HALO_BYTES);
     acc_to_lds<TN, 1>(acc, Cs, LDC, wave * 32, 0, lane);
     __syncthreads();
-    const int after = tkc ? slot(buf)[0] : next + gstride;
     epi.rows(p, Cs, tm);
     __syncthreads();  // the C tile is read out before the buffer takes a halo again
     if constexpr (DOUBLE) {
@@ -316,18 +288,11 @@ __global__ __launch_bounds__(kNT, 1) void halo3x3_kernel(GemmParams p, int H, in
       if (next < tiles_m) issue_halo(next, 0);
     }
     tm = next;
-    next = after;
-  }
-  if (tkc && t == 0) {  // this block draws no more: the N tile's last block resets its counters
-    const unsigned done = __hip_atomic_fetch_add(tkc + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == static_cast<unsigned>(gstride) - 1) {
-      __hip_atomic_store(tkc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(tkc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    next += gstride;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  epi.finish(p, reinterpret_cast<float*>(Hs), blockIdx.x, tkc ? any : gm0 < tiles_m);
+  epi.finish(p, reinterpret_cast<float*>(Hs), blockIdx.x, gm0 < tiles_m);
 }
 
 template <int CIN, int BN, int TH, bool DOUBLE>
@@ -339,8 +304,7 @@ hipError_t launch(const GemmParams& p, int epi, int H, int W, hipStream_t s) {
   if (per_n > tiles_m) per_n = tiles_m;
   if (per_n < 1) per_n = 1;
   const dim3 grid(per_n * tiles_n), block(kNT);
-  GemmParams q = p;
-  q.tk = DOUBLE && tickets_enabled() ? tile_tickets(2 * tiles_n, s) : nullptr;
+  const GemmParams& q = p;
   switch (epi) {
     case EPI_PLAIN:
       hipLaunchKernelGGL((halo3x3_kernel<CIN, BN, TH, DOUBLE, EPI_PLAIN>), grid, block, 0, s, q, H, W, tiles_m, tiles_n);

@@ -110,10 +110,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   constexpr bool TAPS = GATHER == G_CONV3 || GATHER == G_DGRAD2;
   constexpr int LDC = Epi::LDC;
   constexpr int LDS_BYTES = cmax<cmax<STAGES * STAGE, BM * LDC * 2>::v, Epi::kScratchBytes>::v;
-  // ONE __shared__ object (a second one makes hipcc drain vmcnt before ds_reads);
-  // 16 bytes past the tiles: the ticket broadcast slots
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES + 16];
-  int* tslot = reinterpret_cast<int*>(lds + LDS_BYTES);
+  // ONE __shared__ object (a second one makes hipcc drain vmcnt before ds_reads)
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -267,23 +265,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   Epi epi;
   epi.init(t, n0);
 
-  // Ticketed schedule (p.tk): the column's M tiles go to blocks in arrival
-  // order, so a block that starts late (its CU held by the other stream's
-  // kernels) takes fewer tiles instead of finishing a fixed list last.  The next
-  // ticket is drawn at the start of a tile and published in LDS behind the
-  // tile's barriers (its latency hides under the MFMAs).
-  unsigned* tkc = p.tk ? p.tk + 2 * tile_n : nullptr;
   int tm = gm;
-  if (tkc) {
-    if (t == 0) tslot[0] = static_cast<int>(__hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    tm = tslot[0];
-  }
-  bool any = false;
-  for (int it = 0; tm < tiles_m; ++it) {
-    any = true;
-    unsigned nxt = 0;
-    if (tkc && t == 0) nxt = __hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (; tm < tiles_m; tm += GM) {
     if constexpr (GATHER == G_DGRAD2) {
       // class 0 (py, px) = (0, 0): 1 tap; 1 = (0, 1): 2; 2 = (1, 0): 2; 3 = (1, 1): 4
       const int cls = tm / (p.mc_pad / BM);
@@ -347,7 +330,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
         cur = cur == 2 ? 0 : cur + 1;
       }
     }
-    if (tkc && t == 0) tslot[1 + (it & 1)] = static_cast<int>(nxt);
     __syncthreads();  // every wave's last fragment reads are done: the stages become the C tile
     epi.begin(p, tm);
     bf16_t* Cs = reinterpret_cast<bf16_t*>(lds);
@@ -355,16 +337,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     __syncthreads();
     epi.rows(p, Cs, tm);
     __syncthreads();  // the next tile's DMA overwrites Cs
-    tm = tkc ? tslot[1 + (it & 1)] : tm + GM;
   }
-  if (tkc && t == 0) {  // drew past the end: the column's last block resets its counters
-    const unsigned done = __hip_atomic_fetch_add(tkc + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == static_cast<unsigned>(GM) - 1) {
-      __hip_atomic_store(tkc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(tkc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  epi.finish(p, reinterpret_cast<float*>(lds), b, tkc ? any : gm < tiles_m);
+  epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
 }
 
 template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES, int BPC>
@@ -383,7 +357,6 @@ hipError_t launch(const GemmParams& p, hipStream_t s) {
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
-  q.tk = tickets_enabled() ? tile_tickets(2 * tiles_n, s) : nullptr;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB, STAGES>), dim3(GM * tiles_n), dim3(64 * WM * WN),
                      0, s, q, GM, tiles_m, tiles_n);
   return hipGetLastError();
@@ -443,39 +416,6 @@ bool g_forced_cfg_unset() { return g_forced_cfg < 0; }
 }  // namespace gemm
 
 namespace gemm {
-// KDL_TICKETS=1: ticketed tile schedules on the persistent conv kernels
-bool tickets_enabled() {
-  static const bool on = [] { const char* e = getenv("KDL_TICKETS"); return e && e[0] == '1'; }();
-  return on;
-}
-
-unsigned* tile_tickets(int n, hipStream_t s) {
-  constexpr size_t kRing = size_t(1) << 20;  // counters; a slot is reused after ~10^4 launches
-  static std::mutex mu;
-  static unsigned* ring[64] = {};
-  static size_t head[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || n <= 0 || static_cast<size_t>(n) > kRing)
-    return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  if (!ring[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    unsigned* p = nullptr;
-    if (hipMalloc(&p, kRing * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, kRing * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(p);
-      return nullptr;
-    }
-    ring[dev] = p;
-  }
-  const size_t need = (static_cast<size_t>(n) + 31) / 32 * 32;  // 128-B aligned blocks of counters
-  if (head[dev] + need > kRing) head[dev] = 0;
-  unsigned* p = ring[dev] + head[dev];
-  head[dev] += need;
-  return p;
-}
-
 int igemm_pick(int M, int N, int K) {
   const int forced = g_forced_cfg;
   if (forced >= 0 && forced <= 4) {

@@ -243,19 +243,7 @@ struct Conv1x1Args {
   // block, relu(A * bcoef[k] + bcoef[K + k] + bx), written through to aout
   // with its packed ReLU mask in obits [M, K / 8] (forward conv1, STATS)
   int bres;
-  // Two-segment K (seg 1: summed, the BN-folded conv3 data gradient with MASKX;
-  // seg 2: a second accumulator whose bf16 tile is the RESBITS epilogue's x --
-  // the previous block's conv3 output recomputed, ex unused): segment 2 reads
-  // A2 [M, K2] through the BN+ReLU prologue pro_coef ([2 K2]) against B2 [N, ldb2];
-  // segment 1 is A [M, K] against B with row stride ldb (0: K)
-  int seg;
-  const void* A2;
-  const void* B2;
-  int K2, ldb, ldb2;
-  int K2a;                           // A2 row width (0: K2); K2 = 2 K2a re-reads A2 against a hi | lo B2
-  const float* seg1_scale;           // seg 1: [K] per-channel scale of A (bf16(scale A)), null: none
-  const float* ebias;                // epi 2: per-output-channel bias before the mask
-  uint8_t* obits;                    // epi 5 (APPLY: relu(y*ecoef + shift + eres)): ReLU mask out [M, N/8]
+  uint8_t* obits;                    // bres: the written-through block output's ReLU mask [M, K/8]
 };
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 // Data gradient of a 3x3 / pad 1 / stride 2 conv as four sub-pixel class GEMMs
@@ -315,9 +303,7 @@ void set_wgrad_big(int mode);
 // (gcoef = [3N] k | c1 | c0), computed while staging it (LDS-DMA kernel only).
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
-                         const void* gx = nullptr, const float* gcoef = nullptr, bool grelu = false);
-// (grelu: G is replaced by relu(G scale + shift), gcoef = [2N] scale | shift, gx null;
-// dense rows with an A prologue -- the a^T a of one BN+ReLU output)
+                         const void* gx = nullptr, const float* gcoef = nullptr);
 // 3x3 / pad 1: dW[Cout][3][3][Cin] = sum_m G[m, :]^T pro(A)_tap(m); dw32 holds
 // conv3x3_wgrad_slabs(...) x [Cout, 9 Cin] fp32 (dw32_floats: its size; a smaller
 // workspace of conv1x1_wgrad_splits(M, Cout, 9 Cin) slabs keeps the implicit GEMM).
@@ -327,17 +313,6 @@ hipError_t conv3x3_wgrad(const void* G, const void* A, const float* pro_coef, fl
                          hipStream_t s);
 
 hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t n, hipStream_t s);
-
-// ---- bnfold.hip (BN3 folded through the closing 1x1 conv: c3 never stored)
-// bp [C][2C] bf16 = W3^T diag(c1) W3 (transposed rows) as hi | lo, bias [C] = W3^T c0;
-// w3 [N4][C] bf16, bcoef = [3 N4] k | c1 | c0 of BN3
-hipError_t bn_fold_dgrad(const void* w3, const float* bcoef, int N4, int C, void* bp, float* bias, hipStream_t s);
-// part [relu_colsum_parts(M)][C] fp32 = per-block column sums of relu(x scale + shift)
-int relu_colsum_parts(int64_t M);
-hipError_t relu_colsum(const void* x, const float* coef, int64_t M, int C, float* part, hipStream_t s);
-// dw [N4][C] bf16 = diag(k) G + diag(c1) W3 Q + c0 (sum_p part[p])^T; G [N4][C], Q [C][C] fp32
-hipError_t bn_fold_wgrad(const void* w3, const float* bcoef, const float* G, const float* Q, const float* part,
-                         int nparts, int N4, int C, void* dw, hipStream_t s);
 
 // ---- streams.hip
 // dedicated = the stream gets a hardware queue of its own (full CU mask).

@@ -72,13 +72,8 @@ __device__ __forceinline__ bf16x8_t frag8(v4s_t lo, v4s_t hi) {
 // DMA as G into PN panels of its own, read with G's transposed reads, and
 // combined per fragment -- each lane's G fragment is ONE output channel n, so
 // (k, c1, c0) are per-lane constants, exactly as the A prologue's (scale, shift).
-//
-// GRELU: G is itself a BN+ReLU output never written, G' = relu(G gk[n] + gsh[n])
-// (gcoef = [2N] scale | shift): the second-moment matrix a^T a of a BN+ReLU
-// activation (the BN-folded conv3 weight gradient, kubedl_amd/models/resnet_engine.py).
-template <int TN_, int TK_, int GATHER, bool PRO, int WN = 2, int WK = 2, bool BWDG = false, bool GRELU = false>
+template <int TN_, int TK_, int GATHER, bool PRO, int WN = 2, int WK = 2, bool BWDG = false>
 __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dma_kernel(WgParams p) {
-  static_assert(!(BWDG && GRELU), "one G prologue");
   constexpr int NW = WN * WK;
   constexpr int PN = TN_ / 64, PK = TK_ / 64;  // 64-column panels per operand
   constexpr int PX = BWDG ? PN : 0;            // gx panels (BWDG)
@@ -215,10 +210,6 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
       gk[i] = p.gcoef[n];
       gc1[i] = p.gcoef[p.N + n];
       gc0[i] = p.gcoef[2 * p.N + n];
-    } else if constexpr (GRELU) {
-      const int n = n0 + wn0 + 32 * i + (lane & 31);
-      gk[i] = p.gcoef[n];
-      gc0[i] = p.gcoef[p.N + n];
     }
   }
   (void)gk; (void)gc1; (void)gc0;
@@ -235,7 +226,7 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
     __syncthreads();  // stage st landed everywhere; the other stage is free
     if (m0 + MK < mend) issue(m0 + MK, st ^ 1);
     const char* S = lds + st * STAGE;
-    const bool tail = (PRO || BWDG || GRELU) && m0 + MK > mend;  // rows past the range: zero after the prologue
+    const bool tail = (PRO || BWDG) && m0 + MK > mend;  // rows past the range: zero after the prologue
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8_t gf[TN], af[TK];
@@ -254,16 +245,6 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
           for (int e = 0; e < 8; ++e) {
             const float o = fmaf(gk[i], f[e], fmaf(gc1[i], x[e], gc0[i]));  // bn_bwd_apply_kernel's nesting
             f[e] = (!tail || mrow + e < mend) ? o : 0.f;
-          }
-          gf[i] = __builtin_bit_cast(bf16x8_t, pack8(f));
-        } else if constexpr (GRELU) {
-          float f[8];
-          unpack8(__builtin_bit_cast(uint4, gf[i]), f);
-          const int mrow = m0 + 16 * s + 8 * (lane >> 5);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float o = fmaf(f[e], gk[i], gc0[i]);  // the A prologue's expression
-            f[e] = (o > 0.f && (!tail || mrow + e < mend)) ? o : 0.f;
           }
           gf[i] = __builtin_bit_cast(bf16x8_t, pack8(f));
         }
@@ -336,13 +317,6 @@ void launch_bwdg(const WgParams& p, int grid, hipStream_t s) {
 #undef KDL_WGB
 }
 
-// G prologue GRELU: dense rows, A prologue on (the a^T a of one BN+ReLU output)
-template <int TN_, int TK_, int WN, int WK>
-void launch_grelu(const WgParams& p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((wgrad_dma_kernel<TN_, TK_, G_DENSE, true, WN, WK, false, true>), dim3(grid), dim3(64 * WN * WK), 0,
-                     s, p);
-}
-
 }  // namespace
 
 hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t s) {
@@ -356,16 +330,6 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
       static_cast<uint64_t>(p.M) * static_cast<uint64_t>(p.Hout * p.Wout) >= (uint64_t(1) << 32))
     return hipErrorInvalidValue;  // magic-number division range
   const int grid = nsplit * (p.N / tn) * (p.K / tk);
-  if (p.grelu) {
-    if (!p.gcoef || !p.pro || p.mode != G_DENSE || p.gx) return hipErrorInvalidValue;
-    if (tn == 128 && tk == 128) launch_grelu<128, 128, 2, 2>(p, grid, s);
-    else if (tn == 128 && tk == 64) launch_grelu<128, 64, 2, 2>(p, grid, s);
-    else if (tn == 64 && tk == 128) launch_grelu<64, 128, 2, 2>(p, grid, s);
-    else if (tn == 64 && tk == 64) launch_grelu<64, 64, 2, 2>(p, grid, s);
-    else if (tn == 256 && tk == 256) launch_grelu<256, 256, 2, 4>(p, grid, s);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
   if (p.gx) {  // G prologue: the wgrad_tiles(bwd) configs, gx panels beside G's
     if (!p.gcoef || p.mode == G_CONV3 || (p.pro && p.mode != G_DENSE)) return hipErrorInvalidValue;
     if (tn == 128 && tk == 256) launch_bwdg<128, 256, 2, 4>(p, grid, s);

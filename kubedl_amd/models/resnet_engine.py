@@ -222,87 +222,11 @@ class HipKernels:
                               out.mod.running_mean, self._fwd_acc(out), None, None, None)
         return y
 
-    def conv1x1_stats(self, x, w, pro: BNState, out: BNState):
-        """Statistics-only pass of a 1x1 conv (STATS epilogue, nothing stored):
-        the recomputed conv3 of a "recompute" block (csrc/bnfold.hip)."""
-        n, cin, h, wd = x.shape
-        cout = w.shape[0]
-        M = n * h * wd
-        self._arm(out, M)
-        self.ext.conv_seg_arm(0, None, None, None, 0, 0, 0, None, True, 0, None)
-        self.ext.conv1x1_gemm(x, w, x, M, cout, cin, h, wd, h, wd, 1, self.fcoef(pro), 1, out.mod.running_mean,
-                              self._fwd_acc(out), None, None, None, None, 1, 0, 0, None, None, None, None)
-
-    def conv1x1_apply(self, x, w, pro: BNState, st: BNState, res):
-        """out = relu(B_st(conv1x1(relu(B_pro(x)))) + res) and its packed ReLU
-        mask, the conv recomputed in the GEMM (APPLY epilogue, csrc/gemm_epi.h)."""
-        n, cin, h, wd = x.shape
-        cout = w.shape[0]
-        M = n * h * wd
-        y = _nhwc_empty(n, cout, h, wd, x)
-        mb = torch.empty(M * cout // 8, dtype=torch.uint8, device=x.device)
-        self.ext.conv1x1_gemm(x, w, y, M, cout, cin, h, wd, h, wd, 1, self.fcoef(pro), 5, None, None, None, None,
-                              self.fcoef(st), res, 1, 0, 0, mb, None, None, None)
-        return y, mb
-
-    def _fold_bufs(self, C, dev):
-        key = ("fold", C)
-        b = self._dw32.get(key)
-        if b is None:
-            b = (torch.empty(C, 2 * C, dtype=torch.bfloat16, device=dev), torch.empty(C, device=dev))
-            self._dw32[key] = b
-        return b
-
-    def dgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3, w3t):
-        """conv3 data gradient of a recompute block with BN3's backward apply
-        folded in (csrc/bnfold.hip): [k g | a2 | a2] . [W3 ; S_hi ; S_lo] + W3^T c0,
-        a2 = relu(B2(c2)), S = W3^T diag(c1) W3 as a bf16 hi + lo pair, masked by
-        B2's ReLU, + B2's backward sums; w3 = W3 [4C, C], w3t = W3^T [C, 4C]."""
-        n, N4, h, w = g.shape
-        C = w3.shape[1]
-        M = n * h * w
-        s2, bias = self._fold_bufs(C, g.device)
-        bco = self.bcoef(st3)
-        self.ext.bn_fold_dgrad(w3, bco, s2, bias)
-        out = _nhwc_empty(n, C, h, w, g)
-        self._arm(st2, M, fwd=False)
-        self.ext.conv_seg_arm(1, c2, s2, self.fcoef(st2), 2 * C, N4, 2 * C, bias, False, C, bco[:N4])
-        self.ext.conv1x1_gemm(g, w3t, out, M, C, N4, 0, 0, 0, 0, 1, None, 2, None, self._bwd_acc(st2), c2,
-                              st2.save_mean, self.fcoef(st2), None, 1, 0, 0, None, None, None, None)
-        return out
-
     def _ws32(self, key, n):
         t = self._dw32.get(key)
         if t is None or t.numel() < n:
             t = self._dw32[key] = torch.empty(n, device=self.dev)
         return t
-
-    def fold_moments(self, c2, st2: BNState):
-        """Q = a2^T a2 (fp32 [C, C]) and sum(a2) of a recompute block, a2 =
-        relu(B2(c2)) (the GRELU weight-gradient GEMM + column sums)."""
-        n, C, h, w = c2.shape
-        M = n * h * w
-        pro = self.fcoef(st2)
-        dq = torch.empty(self.ext.conv1x1_wgrad_splits(M, C, C) * C * C, device=c2.device)
-        self.ext.wgrad_grelu_arm(pro)
-        self.ext.conv1x1_wgrad(c2, c2, pro, dq, None, 1.0, M, C, C, h, w, h, w, 1)
-        parts = self.ext.relu_colsum_parts(M)
-        part = torch.empty(parts * C, device=c2.device)
-        self.ext.relu_colsum(c2, pro, C, part)
-        self.ext.slab_reduce_f32(part, C, parts)
-        return dq, part
-
-    def wgrad_folded(self, g, c2, st2: BNState, st3: BNState, w3, dW, moments):
-        """conv3 weight gradient of a recompute block: diag(k) G + diag(c1) W3 Q
-        + c0 sum(a2)^T with G = g^T a2 (split-M MFMA GEMM into fp32) and
-        ``moments`` = fold_moments(c2, st2); csrc/bnfold.hip combines."""
-        n, N4, h, w = g.shape
-        C = w3.shape[1]
-        M = n * h * w
-        dg = self._ws32(("fold_g", M, N4, C), self.ext.conv1x1_wgrad_splits(M, N4, C) * N4 * C)
-        self.ext.conv1x1_wgrad(g, c2, self.fcoef(st2), dg, None, 1.0, M, N4, C, h, w, h, w, 1)
-        dq, part = moments
-        self.ext.bn_fold_wgrad(w3, self.bcoef(st3), dg, dq, part, 1, dW.view(N4, C))
 
     def bn_stats(self, x, st):
         self.ext.bn_stage_fwd_stats(x, st.ws, x.numel() // st.C, st.C)
@@ -439,25 +363,13 @@ class HipKernels:
                               None, 1, 0, 0, None, None, None, None)
         return out
 
-    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None, recomp=None):
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None):
         """conv1 dgrad + d(identity); with ``prev`` = (mbits, c3, st3, cd, std) the
-        previous block's ReLU mask is applied and its BN sums accumulated.
-        ``recomp`` = (c2, w3, st2) of a previous recompute block (c3 = None): its
-        conv3 output is recomputed in the same GEMM (csrc/conv1x1.hip PRO_RECOMP)."""
+        previous block's ReLU mask is applied and its BN sums accumulated."""
         n, cout, h, w = g.shape
         cin = wt.shape[0]
         out = _nhwc_empty(n, cin, h, w, g)
         M = n * h * w
-        if recomp is not None:
-            assert bpro is None and prev is not None and prev[3] is None
-            mbits, _, st3, _, _ = prev
-            c2p, w3p, st2p = recomp
-            cp = w3p.shape[1]
-            self._arm(st3, M, fwd=False)
-            self.ext.conv_seg_arm(2, c2p, w3p, self.fcoef(st2p), cp, 0, cp, None, False, cp, None)
-            self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 3, None, self._bwd_acc(st3), None,
-                                  st3.save_mean, None, eres, res_stride, h, w, mbits, None, None, None)
-            return out
         if prev is None:
             self._arm_bpro(bpro, cout)
             self.ext.conv1x1_gemm(g, wt, out, M, cin, cout, 0, 0, 0, 0, 1, None, 4, None, None, None, None, None, eres,
@@ -643,53 +555,9 @@ class TorchKernels:
         self._stats(y, out, out.mod.running_mean.clone())
         return y.contiguous(memory_format=torch.channels_last)
 
-    def _conv3(self, x, w, pro):
-        """bf16 output of a 1x1 conv on relu(B_pro(x)) (the recomputed conv3)."""
-        return _bfr(F.conv2d(self._pro(x, pro), w.float()[:, :, None, None]))
-
-    def conv1x1_stats(self, x, w, pro, out):
-        self._stats(self._conv3(x, w, pro), out, out.mod.running_mean.clone())
-
-    def conv1x1_apply(self, x, w, pro, st, res):
-        y = self._conv3(x, w, pro).to(x.dtype).contiguous(memory_format=torch.channels_last)
-        return self.bn_apply(y, st, relu=True, res=res, want_mask=True)
-
     @staticmethod
     def bcoef(st):
         return st.bcoef
-
-    def dgrad_folded(self, g, c2, st2, st3, w3, w3t=None):
-        """HipKernels.dgrad_folded semantics: A = bf16(k g) per element, exact
-        W3, S as a bf16 hi + lo pair, fp32 GEMM, bf16 rounding of the GEMM
-        output, fp32 bias, B2 mask + sums."""
-        k, c1, c0 = st3.bcoef
-        w = w3.float()                                    # [N4, C]
-        S = w.t() @ (c1[:, None] * w)                     # W3^T diag(c1) W3 [C, C] (symmetric)
-        s_hi = _bfr(S)
-        s_lo = _bfr(S - s_hi)
-        bias = w.t() @ c0                                 # [C]
-        a2 = self._pro(c2, st2)
-        gk = _bfr(g.float() * k.view(1, -1, 1, 1))
-        d = (F.conv2d(gk, w.t()[:, :, None, None]) + F.conv2d(a2, s_hi.t()[:, :, None, None])
-             + F.conv2d(a2, s_lo.t()[:, :, None, None]))
-        d = _bfr(d) + bias.view(1, -1, 1, 1)
-        sc, sf = st2.fcoef
-        mask = (c2.float() * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)) > 0
-        d = torch.where(mask, d, torch.zeros_like(d))
-        self._bsum(d, c2, st2)
-        return d.to(g.dtype).contiguous(memory_format=torch.channels_last)
-
-    def fold_moments(self, c2, st2):
-        a2 = _rows(self._pro(c2, st2).contiguous(memory_format=torch.channels_last))  # [M, C]
-        return a2.t() @ a2, a2.sum(0)
-
-    def wgrad_folded(self, g, c2, st2, st3, w3, dW, moments):
-        k, c1, c0 = st3.bcoef
-        a2 = _rows(self._pro(c2, st2).contiguous(memory_format=torch.channels_last))  # [M, C]
-        G = _rows(g.float()).t() @ a2                     # [N4, C]
-        Q, asum = moments                                 # a2^T a2 [C, C], sum(a2) [C]
-        dw = k[:, None] * G + c1[:, None] * (w3.float() @ Q) + c0[:, None] * asum[None, :]
-        dW.copy_(dw.view_as(dW))
 
     def _stats(self, y, st, shift):
         d = _rows(y.float()) - shift
@@ -817,7 +685,7 @@ class TorchKernels:
         return F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)).to(g.dtype).contiguous(
             memory_format=torch.channels_last)
 
-    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None, recomp=None):
+    def dgrad_res(self, g, wt, eres, res_stride, prev=None, bpro=None):
         g = self._bpro(g, bpro)
         d = _bfr(F.conv2d(g.float(), wt.float().unsqueeze(-1).unsqueeze(-1)))
         r = torch.zeros_like(d)
@@ -825,9 +693,6 @@ class TorchKernels:
         d = _bfr(d + r)
         if prev is not None:
             mask, c3, st3, cd, std_ = prev
-            if recomp is not None:  # the previous block's conv3 output, recomputed
-                c2p, w3p, st2p = recomp
-                c3 = self._conv3(c2p, w3p, st2p)
             d = torch.where(mask, d, torch.zeros_like(d))
             self._bsum(d, c3, st3)
             if cd is not None:
@@ -882,9 +747,6 @@ class EngineOptions:
     side_prio: int = 0
     # BN finalize in the producing GEMM's last blocks ("gemm") or own launches ("kernel")
     bn_fin: str = "gemm"
-    # recompute blocks up to this 4C width (0 = off: measured 13,216-13,227 on vs
-    # 13,233-13,264 img/s off, see below)
-    recomp: int = 0
     # downsample conv of the forward on the side stream
     down_side: bool = True
     # closing BN3 + residual + ReLU in the successor's conv1 staging (up to this K;
@@ -970,25 +832,6 @@ class ResNetEngine:
         # conv1's dgrad (N = 4C output tiles each re-transform the A tile) and at
         # K >= 1024 (the register-staged loop vs the LDS-DMA one: 88 -> 138 us); the
         # G prologue (mode 2) loses to reading the written-through tensor (106 -> 354 us)
-        # "Recompute" blocks (csrc/bnfold.hip): a bottleneck without a downsample
-        # branch whose successor's conv1 data gradient can recompute its conv3
-        # output never stores that output (c3, the step's widest tensors at the
-        # early stages): the forward runs conv3 twice -- a statistics-only pass,
-        # then the GEMM that applies BN3 + residual + ReLU in its epilogue --, the
-        # successor's RESBITS GEMM recomputes c3 tiles for BN3's backward sums,
-        # and BN3's backward apply reaches conv3's data / weight gradients folded
-        # into the weights.  EngineOptions.recomp = widest 4C served (0: off).
-        # Measured (profiles/r03_step_1stream_*.txt, docs/perf_notes.md): at the 56x56 stage
-        # (4C = 256) forward conv3 + BN3 apply 400 -> 290 us and conv3 dgrad 275 -> 160 us
-        # per block against +50-100 us in the successor's RESBITS, the main stream 0.47 ms
-        # shorter per step -- but the folded weight gradient lengthens the side stream's
-        # tail, and the job-path step measured 13,216-13,227 (on) vs 13,233-13,264 img/s
-        # (off); at 28x28 the recomputing RESBITS (+80-150 us) outweighs the rest.  Opt-in:
-        # KDL_ENGINE=recomp=256.
-        maxc = min(512, o.recomp)
-        nb = len(self.blocks)
-        self.recomp = [b.down_conv is None and i < nb - 1 and b.conv3.out_channels <= maxc
-                       for i, b in enumerate(self.blocks)]
         # downsample branch conv of the forward on the side stream (down_side = False: in
         # line): 13,333-13,347 vs 13,252-13,279 img/s, profiles/r03b_fwd_down_side_ab.txt
         self.down_side = o.down_side
@@ -1187,14 +1030,6 @@ class ResNetEngine:
                 c2 = K.conv3x3_fwd(a1, blk.conv2.weight, s, st2)
                 ho, wo = c2.shape[-2:]
                 K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
-            if self.recomp[bi]:  # conv3 never stored: statistics pass, then the applying GEMM
-                w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
-                K.conv1x1_stats(c2, w3, st2, st3)
-                K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
-                out, mbits = K.conv1x1_apply(c2, w3, st2, st3, cur)
-                saved.append((cur, c1, a1, c2, None, None, mbits))
-                cur = out
-                continue
             c3 = K.conv1x1_fwd(c2, blk.conv3.weight.view(blk.conv3.out_channels, -1), 1, st2, st3)
             K.bn_finalize(st3, n * ho * wo, gemm_shift=True)
             # the closing apply deferred into the successor's conv1 (which writes out / mbits)?
@@ -1333,26 +1168,16 @@ class ResNetEngine:
             if std_ is not None:
                 K.bn_bwd_finalize(std_, Mo, *self._bn_grads(std_))
                 self._bn_ready(std_)
-            opd = None
-            if self.recomp[i]:
-                # c3 was never stored: BN3's backward apply folded into conv3's weights
-                w3 = blk.conv3.weight.view(blk.conv3.out_channels, -1)
-                g2 = K.dgrad_folded(g, c2, st2, st3, w3, self._wt(blk.conv3))
-                # (the moments a2^T a2, sum(a2) issued on the side stream during the forward
-                # instead measured 0.7 % slower again: ~1 ms of idle GPU per step)
-                with self._on_side(g):
-                    K.wgrad_folded(g, c2, st2, st3, w3, self._g(blk.conv3.weight), K.fold_moments(c2, st2))
+            if std_ is not None and self._fuse_mode(c3.shape[1]) == 0:
+                dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches
+                op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
             else:
-                if std_ is not None and self._fuse_mode(c3.shape[1]) == 0:
-                    dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches
-                    op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
-                else:
-                    op3 = self._bn_bwd_operand(g, c3, st3)
-                    opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
-                # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
-                g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
-                with self._on_side(*self._side_of(op3)):
-                    K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
+                op3 = self._bn_bwd_operand(g, c3, st3)
+                opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
+            # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
+            g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
+            with self._on_side(*self._side_of(op3)):
+                K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
             self.on_ready(blk.conv3.weight)
             K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
             self._bn_ready(st2)
@@ -1390,15 +1215,6 @@ class ResNetEngine:
             self._bn_ready(st1)
             # bn1 backward apply: its own pass, or (fused) inside conv1's dgrad below
             op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1, bn1=True)
-            rc = None
-            if i > 0 and self.recomp[i - 1]:
-                # the previous block's conv3 output is recomputed in conv1's dgrad (its
-                # second K segment), which then has no room for the bn1 A prologue
-                pb = self.blocks[i - 1]
-                rc = (saved[i - 1][3], pb.conv3.weight.view(pb.conv3.out_channels, -1), self.bn[pb.bn2])
-                if op1[1] is not None:
-                    dc1, _ = K.bn_bwd_apply(g1, c1, st1)
-                    op1 = (dc1, None, dc1, None)
             # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
             if blk.down_conv is not None:
                 ds = blk.down_conv.stride[0]
@@ -1411,7 +1227,7 @@ class ResNetEngine:
                 pblk = self.blocks[i - 1]
                 p_std = self.bn[pblk.down_bn] if pblk.down_bn is not None else None
                 g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride,
-                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std), bpro=op1[1], recomp=rc)
+                                     (p_mbits, p_c3, self.bn[pblk.bn3], p_cd, p_std), bpro=op1[1])
             else:
                 g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride, None, bpro=op1[1])
             with self._on_side(*self._side_of(op1), *(self._side_of(opd) if opd is not None else ())):

@@ -88,14 +88,13 @@ def test_engine_torch_backend_matches_autograd_fp32(layers, width, monkeypatch):
         torch.testing.assert_close(b, c, atol=1e-5, rtol=1e-5, msg=n)
 
 
-@pytest.mark.parametrize("recomp", ["0", "1"])
-def test_engine_recompute_blocks_match_autograd_fp32(recomp, monkeypatch):
-    """Recompute blocks (c3 never stored, BN3 folded into conv3's data / weight
-    gradients, csrc/bnfold.hip) are exact in fp32: the same gradients as
-    autograd, and as the engine with every c3 materialised."""
+def test_engine_width8_stack_matches_autograd_fp32(monkeypatch):
+    """A (3, 2, 2, 2) width-8 stack (stage-1 blocks without downsample, stride-2
+    blocks at every later stage) is exact in fp32: the same gradients and BN
+    buffers as autograd."""
     import kubedl_amd.models.resnet_engine as RE
     monkeypatch.setattr(RE, "_bfr", lambda t: t.float())
-    monkeypatch.setenv("KDL_ENGINE", "recomp=256" if recomp == "1" else "")
+    monkeypatch.delenv("KDL_ENGINE", raising=False)
     torch.manual_seed(0)
     model = ResNet((3, 2, 2, 2), num_classes=10, width=8)
     with torch.no_grad():
@@ -108,8 +107,6 @@ def test_engine_recompute_blocks_match_autograd_fp32(recomp, monkeypatch):
     x = torch.randn(4, 3, 64, 64)
     y = torch.randint(0, 10, (4,))
     eng = RE.ResNetEngine(model, backend="torch")
-    # width 8: stage 1 blocks 1, 2, stages 2-3 block 1 (4C <= 256); never a downsample block or the last one
-    assert sum(eng.recomp) == (4 if recomp == "1" else 0), eng.recomp
     loss = eng.forward_backward(x, y)
     rloss = _ref_step(ref, x, y)
     torch.testing.assert_close(loss, rloss, atol=1e-5, rtol=1e-5)
@@ -369,9 +366,9 @@ def test_engine_options_from_one_variable(monkeypatch):
     from kubedl_amd.models.resnet_engine import EngineOptions
     monkeypatch.delenv("KDL_ENGINE", raising=False)
     assert EngineOptions.from_env() == EngineOptions()
-    monkeypatch.setenv("KDL_ENGINE", "side=0, recomp=256,bn_fin=kernel,halo_pro=2")
+    monkeypatch.setenv("KDL_ENGINE", "side=0, res_pro_kmax=256,bn_fin=kernel,halo_pro=2")
     o = EngineOptions.from_env()
-    assert (o.side, o.recomp, o.bn_fin, o.halo_pro) == (False, 256, "kernel", 2)
+    assert (o.side, o.res_pro_kmax, o.bn_fin, o.halo_pro) == (False, 256, "kernel", 2)
     monkeypatch.setenv("KDL_ENGINE", "no_such_knob=1")
     with pytest.raises(ValueError, match="unknown option"):
         EngineOptions.from_env()
