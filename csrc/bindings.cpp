@@ -1149,15 +1149,20 @@ void stem7x7_wgrad_bn(const at::Tensor& c0, const at::Tensor& dp, const at::Tens
 
 // dx of a 3x3 / pad 1 / stride 2 conv: dy [Nb, Hd, Wd, Cd] (channels_last),
 // ball = the weights regrouped class-major [N][9 Cd] (kubedl_amd.ops.conv.s2_dgrad_weights),
-// dx [Nb, 2 Hd, 2 Wd, N]; epi 0 PLAIN, 2 MASKX (ex = that BN's input [Nb, 2Hd, 2Wd, N]).
+// dx [Nb, Hx, Wx, N] with Hx = 2 Hd or 2 Hd - 1 (an odd conv input; 0: 2 Hd),
+// likewise Wx; epi 0 PLAIN, 2 MASKX (ex = that BN's input [Nb, Hx, Wx, N]).
 void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor dx, int64_t Nb, int64_t Hd,
                       int64_t Wd, int64_t Cd, int64_t N, int64_t epi, const c10::optional<at::Tensor>& acc,
                       const c10::optional<at::Tensor>& ex, const c10::optional<at::Tensor>& emean,
-                      const c10::optional<at::Tensor>& ecoef) {
+                      const c10::optional<at::Tensor>& ecoef, int64_t Hx, int64_t Wx) {
   const FinArm fin = take_fin_arm();
   TORCH_CHECK(Cd % 64 == 0 && N % 64 == 0 && Nb > 0 && Hd > 0 && Wd > 0, "conv3x3_s2_dgrad: need Cd, N % 64 == 0");
   TORCH_CHECK(epi == 0 || epi == 2, "conv3x3_s2_dgrad: epilogue must be PLAIN or MASKX");
-  const int64_t Mdx = Nb * 4 * Hd * Wd;
+  if (Hx <= 0) Hx = 2 * Hd;
+  if (Wx <= 0) Wx = 2 * Wd;
+  TORCH_CHECK((Hx == 2 * Hd || Hx == 2 * Hd - 1) && (Wx == 2 * Wd || Wx == 2 * Wd - 1),
+              "conv3x3_s2_dgrad: dx must be (2 Hd or 2 Hd - 1) x (2 Wd or 2 Wd - 1)");
+  const int64_t Mdx = Nb * Hx * Wx;
   need_bf16(dy, Nb * Hd * Wd * Cd, "conv3x3_s2_dgrad dy");
   need_bf16(ball, N * 9 * Cd, "conv3x3_s2_dgrad ball");
   need_bf16(dx, Mdx * N, "conv3x3_s2_dgrad dx");
@@ -1171,7 +1176,7 @@ void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor d
   a.A = dy.data_ptr(); a.B = ball.data_ptr(); a.C = dx.data_ptr();
   a.M = static_cast<int>(Nb * Hd * Wd); a.N = static_cast<int>(N); a.K = static_cast<int>(9 * Cd);
   a.Hin = static_cast<int>(Hd); a.Win = static_cast<int>(Wd);
-  a.Hout = static_cast<int>(2 * Hd); a.Wout = static_cast<int>(2 * Wd); a.stride = 2;
+  a.Hout = static_cast<int>(Hx); a.Wout = static_cast<int>(Wx); a.stride = 2;
   a.ksize = 3; a.Cin = static_cast<int>(Cd);
   a.epi = static_cast<int>(epi);
   a.acc = opt_fptr(acc);
@@ -1411,9 +1416,9 @@ void bn_stage_bwd_apply(const at::Tensor& g, const at::Tensor& x, const at::Tens
 }  // namespace
 
 // ------------------------------------------------------------------ streams
-int64_t make_stream_py(bool dedicated, int64_t priority) {
+int64_t make_stream_py(bool dedicated, int64_t priority, int64_t cus) {
   hipStream_t s = nullptr;
-  check_hip(kdl::make_stream(dedicated, static_cast<int>(priority), &s), "make_stream");
+  check_hip(kdl::make_stream(dedicated, static_cast<int>(priority), &s, static_cast<int>(cus)), "make_stream");
   return reinterpret_cast<int64_t>(s);
 }
 
@@ -1428,8 +1433,9 @@ void register_gbdt(pybind11::module& m);  // gbdt_grower.cpp
 
 PYBIND11_MODULE(_C, m) {
   register_gbdt(m);
-  m.def("make_stream", &make_stream_py, "new HIP stream (dedicated=True: own hardware queue via a full CU mask)",
-        py::arg("dedicated"), py::arg("priority") = 0);
+  m.def("make_stream", &make_stream_py,
+        "new HIP stream (dedicated=True: own hardware queue via a full CU mask; cus > 0: that many CUs)",
+        py::arg("dedicated"), py::arg("priority") = 0, py::arg("cus") = 0);
   m.def("destroy_stream", &destroy_stream_py, "destroy a stream from make_stream");
   m.def("set_gemm_core", &kdl::set_gemm_core_mode, "conv GEMM main loop: -1 by shape, 0 register-staged, 1 LDS-DMA");
   m.def("set_igemm_cfg", &kdl::set_igemm_cfg, "force an LDS-DMA tile config (-1 = by shape)");
@@ -1486,7 +1492,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_forward", &head_forward, "classifier head forward: mean pool + fc (MFMA) + softmax CE + dlogits");
   m.def("head_backward", &head_backward, "classifier head backward: dfeat, dW, db (MFMA) + mean loss");
   m.def("stem7x7_fwd", &stem7x7_fwd, "ResNet stem 7x7/s2/p3 conv (224 -> 112, 3 -> 64 channels) with BN statistics epilogue");
-  m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue");
+  m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad,
+        "stride-2 3x3 pad-1 conv data gradient: four sub-pixel class GEMMs, PLAIN or MASKX epilogue",
+        py::arg("dy"), py::arg("ball"), py::arg("dx"), py::arg("Nb"), py::arg("Hd"), py::arg("Wd"), py::arg("Cd"),
+        py::arg("N"), py::arg("epi"), py::arg("acc"), py::arg("ex"), py::arg("emean"), py::arg("ecoef"),
+        py::arg("Hx") = 0, py::arg("Wx") = 0);
   m.def("bn_res_pro_arm", &bn_res_pro_arm, "next forward conv1x1_gemm applies relu(A*scale+shift+res), written through + mask");
   m.def("conv3x3_aout_arm", &conv3x3_aout_arm, "next prologue conv3x3_gemm also writes relu(B(x)) here (56x56 halo)");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");

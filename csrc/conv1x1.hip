@@ -806,7 +806,8 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
 }
 
 hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
-  if (a.Cin <= 0 || a.Cin % 64 || a.N % 64 || a.K != 9 * a.Cin || a.Hout != 2 * a.Hin || a.Wout != 2 * a.Win ||
+  if (a.Cin <= 0 || a.Cin % 64 || a.N % 64 || a.K != 9 * a.Cin || (a.Hout != 2 * a.Hin && a.Hout != 2 * a.Hin - 1) ||
+      (a.Wout != 2 * a.Win && a.Wout != 2 * a.Win - 1) ||
       a.M <= 0 || a.M % (a.Hin * a.Win) || (a.epi != EPI_PLAIN && a.epi != EPI_MASKX) || a.pro_coef)
     return hipErrorInvalidValue;
   GemmParams p{};

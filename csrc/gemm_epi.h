@@ -75,7 +75,7 @@ struct GemmParams {
   float* acc2;          // its replicas [kRep][2N]
   int price_drop;       // timing-only builds (KDL_IGEMM_PRICE): bit 0 drops A's loads, bit 1 B's
   // G_DGRAD2: A = dy [Nb, Hin, Win, Cin] (Hin x Win = each class's pixel grid),
-  // C = dx [Nb, Hout = 2 Hin, Wout = 2 Win, N]; class c = 2 py + px owns the
+  // C = dx [Nb, Hout = 2 Hin (or 2 Hin - 1), Wout = 2 Win (or 2 Win - 1), N]; class c = 2 py + px owns the
   // dx pixels (2i + py, 2j + px).  mc = Nb Hin Win rows per class, padded to
   // mc_pad (a multiple of BM, set by the launcher); M = 4 mc_pad.
   int mc, mc_pad;
@@ -230,7 +230,9 @@ struct Epilogue {
       const int hw = p.Hin * p.Win;
       const int nimg = r / hw, rem = r - nimg * hw;
       const int i = rem / p.Win, j = rem - i * p.Win;
-      return (nimg * p.Hout + 2 * i + (cls >> 1)) * p.Wout + 2 * j + (cls & 1);
+      const int oh = 2 * i + (cls >> 1), ow = 2 * j + (cls & 1);
+      if (oh >= p.Hout || ow >= p.Wout) return -1;  // odd input size: the last sub-pixel row / column
+      return (nimg * p.Hout + oh) * p.Wout + ow;
     } else {
       return m < p.M ? m : -1;
     }

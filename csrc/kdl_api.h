@@ -249,7 +249,8 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s);
 // Data gradient of a 3x3 / pad 1 / stride 2 conv as four sub-pixel class GEMMs
 // on the LDS-DMA core (one launch): A = dy [Nb, Hin, Win, Cin], B = the weights
 // regrouped class-major [N][9 Cin] (conv3x3_s2_dgrad_weights), C = dx
-// [Nb, Hout = 2 Hin, Wout = 2 Win, N]; M = Nb * Hin * Win; epi PLAIN or MASKX
+// [Nb, Hout, Wout, N] with Hout = 2 Hin or 2 Hin - 1 (an odd conv input: the last
+// sub-pixel row is masked), likewise Wout; M = Nb * Hin * Win; epi PLAIN or MASKX
 // (ex / emean / ecoef / acc as conv1x1_gemm, indexed by dx rows).
 hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s);
 // ResNet stem conv (csrc/stem.hip): x [Nb, 224, 224, 3] NHWC bf16, wp = the
@@ -316,7 +317,7 @@ hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t
 
 // ---- streams.hip
 // dedicated = the stream gets a hardware queue of its own (full CU mask).
-hipError_t make_stream(bool dedicated, int priority, hipStream_t* out);
+hipError_t make_stream(bool dedicated, int priority, hipStream_t* out, int cus = 0);
 // one wave busy-waiting ``microseconds`` (queue-concurrency probe)
 hipError_t spin(hipStream_t s, double microseconds);
 

@@ -4,7 +4,9 @@
 // its own (HIP shares the process's GPU_MAX_HW_QUEUES queues among ordinary
 // streams).  Used by kubedl_amd/ops/streams.py's ``dedicated`` mode; measured
 // slower than pool streams for the ResNet step (profiles/
-// r02_world1_pg_streams_ab.txt), so not the default.  The spin kernel is the
+// r02_world1_pg_streams_ab.txt), so not the default.  ``cus`` < the CU count
+// restricts the stream to that many CUs (a partial mask: the engine's
+// weight-gradient side stream, EngineOptions.side_cus).  The spin kernel is the
 // probe of scripts/probe_queues.py: one wave per launch, so two launches on
 // different hardware queues overlap and two on one queue serialise.
 #include <vector>
@@ -26,17 +28,22 @@ __global__ void spin_kernel(uint64_t ticks) {
 
 }  // namespace
 
-hipError_t make_stream(bool dedicated, int priority, hipStream_t* out) {
+hipError_t make_stream(bool dedicated, int priority, hipStream_t* out, int cus) {
   *out = nullptr;
-  if (!dedicated) return hipStreamCreateWithPriority(out, hipStreamNonBlocking, priority);
+  if (!dedicated && cus <= 0) return hipStreamCreateWithPriority(out, hipStreamNonBlocking, priority);
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   int ncu = 0;
   e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
+  if (cus <= 0 || cus > ncu) cus = ncu;
+  // cus < ncu: a Bresenham-spread subset of the CU ids (every XCD and shader
+  // engine keeps a share: consecutive ids are spread over the dies)
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
+  for (int i = 0; i < ncu; ++i)
+    if ((static_cast<int64_t>(i + 1) * cus) / ncu != (static_cast<int64_t>(i) * cus) / ncu) mask[i / 32] |= 1u << (i % 32);
+  // (a CU-masked stream takes no priority: it keeps the default)
   return hipExtStreamCreateWithCUMask(out, static_cast<uint32_t>(mask.size()), mask.data());
 }
 

@@ -345,13 +345,16 @@ class HipKernels:
     def dgrad3x3s2_maskx(self, g, ball, x1, st1):
         """Stride-2 3x3 dgrad as four sub-pixel class GEMMs in one launch
         (csrc/igemm.hip G_DGRAD2; ball = class-major weights [Cin][9 Cout],
-        kubedl_amd/ops/conv.py) with bn1's mask and backward sums fused."""
+        kubedl_amd/ops/conv.py) with bn1's mask and backward sums fused.  The
+        input x1 is 2h x 2w or, for an odd input size, 2h - 1 (2w - 1): the
+        last sub-pixel row / column is masked in the epilogue."""
         n, cout, h, w = g.shape
         cin = ball.shape[0]
-        out = _nhwc_empty(n, cin, 2 * h, 2 * w, g)
-        self._arm(st1, n * 4 * h * w, fwd=False)
+        hx, wx = x1.shape[-2:]
+        out = _nhwc_empty(n, cin, hx, wx, g)
+        self._arm(st1, n * hx * wx, fwd=False)
         self.ext.conv3x3_s2_dgrad(g, ball, out, n, h, w, cout, cin, 2, self._bwd_acc(st1), x1, st1.save_mean,
-                                  self.fcoef(st1))
+                                  self.fcoef(st1), hx, wx)
         return out
 
     def dgrad_plain(self, g, wt, bpro=None):
@@ -495,11 +498,6 @@ class HipKernels:
         self.ext.head_backward(ws["feat"], w, ws["dl"], ws["dlT"], ws["part2"], ws["dfeat"], dw, db, ws["lrow"],
                                loss)
         return loss.view(()), ws["dfeat"]
-
-    @staticmethod
-    def dgrad3x3_strided_bn(g, w, stride, x1, st1, dgamma, dbeta):
-        raise NotImplementedError(f"HIP engine: stride-{stride} 3x3 data gradient needs an even input size "
-                                  f"(got {tuple(x1.shape[-2:])} -> {tuple(g.shape[-2:])})")
 
     def _stem_ws(self, nb, device, h=224, w=224):
         key = ("stem", nb, h, w)
@@ -713,12 +711,6 @@ class TorchKernels:
     def stem_backward(self, dp, idx, c0, x, st, dgamma, dbeta, dw):
         self.stem_wgrad(self.stem_bwd(dp, idx, c0, st, dgamma, dbeta), x, dw)
 
-    def dgrad3x3_strided_bn(self, g, w, stride, x1, st1, dgamma, dbeta):
-        """Strided 3x3 data gradient at any geometry + bn1's ReLU mask / backward."""
-        dx = torch.nn.grad.conv2d_input(tuple(x1.shape), w.float(), g.float(), stride=stride, padding=1)
-        return self.bn_bwd_full(dx.to(x1.dtype).contiguous(memory_format=torch.channels_last), x1, st1, dgamma,
-                                dbeta)
-
     @staticmethod
     def stem_wgrad(dc0, x, dw):
         dw.copy_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dc0.float(), stride=2, padding=3))
@@ -745,6 +737,9 @@ class EngineOptions:
     # 11.3k img/s when introduced); side_prio: its HIP stream priority
     side: bool = True
     side_prio: int = 0
+    # CUs the side stream may use (0: all, a pool stream); a partial CU mask keeps its
+    # weight-gradient blocks off the rest of the chip (ops/streams.py side_stream)
+    side_cus: int = 0
     # BN finalize in the producing GEMM's last blocks ("gemm") or own launches ("kernel")
     bn_fin: str = "gemm"
     # downsample conv of the forward on the side stream
@@ -859,7 +854,7 @@ class ResNetEngine:
         self.side = None
         if self.K.name == "hip" and o.side:
             from kubedl_amd.ops.streams import side_stream
-            self.side = side_stream(self.dev, o.side_prio)  # (ops/streams.py)
+            self.side = side_stream(self.dev, o.side_prio, o.side_cus)  # (ops/streams.py)
             # overlapped with the main stream, the 1x1 weight gradients gain from 256x256
             # tiles too (fewer, heavier side-stream blocks; csrc/conv1x1.hip wgrad_tiles)
             self.K.ext.set_wgrad_big(2)
@@ -1196,25 +1191,21 @@ class ResNetEngine:
                 g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
-                dc1 = None
-            elif c1.shape[-2:] == (2 * dc2.shape[-2], 2 * dc2.shape[-1]):
+            elif s == 2:
                 # stride 2: four sub-pixel class GEMMs with bn1's mask + sums fused
-                # (no MIOpen, no zero-filled dx, no separate BN-backward reduce pass)
+                # (no MIOpen, no zero-filled dx, no separate BN-backward reduce pass;
+                # an odd input size masks the last sub-pixel row / column)
                 with self._on_side(dc2):
                     self._wgrad3x3(dc2, a1, s, blk.conv2.weight)
                 self.on_ready(blk.conv2.weight)
                 g1 = K.dgrad3x3s2_maskx(dc2, self._ball(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape
                 K.bn_bwd_finalize(st1, n1 * h1 * w1, *self._bn_grads(st1))
-                dc1 = None
-            else:  # odd input size at a stride-2 block: the reference backend only
-                with self._on_side(dc2):
-                    self._wgrad3x3(dc2, a1, s, blk.conv2.weight)
-                self.on_ready(blk.conv2.weight)
-                dc1 = K.dgrad3x3_strided_bn(dc2, blk.conv2.weight, s, c1, st1, *self._bn_grads(st1))
+            else:
+                raise NotImplementedError(f"engine: 3x3 stride {s} (Bottleneck strides are 1 or 2)")
             self._bn_ready(st1)
             # bn1 backward apply: its own pass, or (fused) inside conv1's dgrad below
-            op1 = (dc1, None, dc1, None) if dc1 is not None else self._bn_bwd_operand(g1, c1, st1, bn1=True)
+            op1 = self._bn_bwd_operand(g1, c1, st1, bn1=True)
             # conv1 dgrad + identity gradient (+ previous block's mask and BN sums)
             if blk.down_conv is not None:
                 ds = blk.down_conv.stride[0]

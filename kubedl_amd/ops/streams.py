@@ -45,20 +45,23 @@ def compute_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     return side_stream(device, int(os.environ.get("KDL_MAIN_PRIO", "-1")))
 
 
-def side_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:
-    if mode() == "dedicated":
-        return dedicated_stream(device, priority)
+def side_stream(device: torch.device, priority: int = 0, cus: int = 0) -> torch.cuda.Stream:
+    """``cus`` > 0: the stream may use only that many CUs (a partial CU mask,
+    spread over the XCDs; csrc/streams.hip), so its kernels never hold the
+    other CUs the critical path's persistent kernels are sized for."""
+    if mode() == "dedicated" or cus > 0:
+        return dedicated_stream(device, priority, cus)
     return torch.cuda.Stream(device=device, priority=priority)
 
 
-def dedicated_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:
-    """A stream on a hardware queue of its own (full CU mask)."""
+def dedicated_stream(device: torch.device, priority: int = 0, cus: int = 0) -> torch.cuda.Stream:
+    """A stream on a hardware queue of its own (a full CU mask, or ``cus`` CUs)."""
     if device.type != "cuda":
         raise ValueError("dedicated_stream needs a GPU device")
     from kubedl_amd.ops import _ext
     ext = _ext.load()
     with torch.cuda.device(device):
-        h = ext.make_stream(True, priority)
+        h = ext.make_stream(True, priority, cus)
     _KEEP.append(h)
     return torch.cuda.ExternalStream(h, device=device)
 

@@ -116,3 +116,35 @@ def test_s2_dgrad_maskx_full_batch_writes_every_pixel(C, Hd):
         mask = (xbn.float() * coef[:C].view(1, C, 1, 1) + coef[C:].view(1, C, 1, 1)) > 0
         ref = torch.where(mask, dx.bfloat16().float(), torch.zeros_like(dx))
         torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("C,Hx,Wx,nb", [(128, 27, 27, 2), (256, 13, 14, 2), (64, 7, 7, 3), (128, 55, 56, 1)])
+def test_s2_dgrad_maskx_odd_input(C, Hx, Wx, nb):
+    """Odd conv input (dx = 2 Hd - 1 rows / columns): the last sub-pixel row /
+    column is masked in the epilogue -- every dx pixel written once, nothing past
+    the tensor (a NaN guard region behind it stays NaN), BN sums over dx only."""
+    torch.manual_seed(25)
+    ext = _ext()
+    Hd, Wd = (Hx - 1) // 2 + 1, (Wx - 1) // 2 + 1
+    dy = _nhwc(torch.randn(nb, C, Hd, Wd, device="cuda").bfloat16())
+    w = _nhwc((torch.randn(C, C, 3, 3, device="cuda") / (3 * C ** 0.5)).bfloat16())
+    xbn = _nhwc(torch.randn(nb, C, Hx, Wx, device="cuda").bfloat16())
+    coef = torch.cat([torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.5]).float()
+    mean = torch.randn(C, device="cuda") * 0.1
+    acc = torch.zeros(REP * 2 * C, device="cuda")
+    n_out = nb * C * Hx * Wx
+    buf = torch.full((n_out + 4096 * C,), float("nan"), device="cuda", dtype=torch.bfloat16)
+    out = buf[:n_out].view(nb, Hx, Wx, C).permute(0, 3, 1, 2)  # channels_last view of the buffer head
+    ext.conv3x3_s2_dgrad(dy, s2_dgrad_weights(w), out, nb, Hd, Wd, C, C, 2, acc, xbn, mean, coef, Hx, Wx)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all(), "dx pixels left unwritten"
+    assert torch.isnan(buf[n_out:].float()).all(), "write past the end of dx"
+    dx = torch.nn.grad.conv2d_input(xbn.shape, w.float(), dy.float(), stride=2, padding=1)
+    mask = (xbn.float() * coef[:C].view(1, C, 1, 1) + coef[C:].view(1, C, 1, 1)) > 0
+    ref = torch.where(mask, dx.bfloat16().float(), torch.zeros_like(dx))
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
+    g = _rows(out.float()).double()
+    s = acc.view(REP, 2, C).sum(0).double()
+    torch.testing.assert_close(s[0], g.sum(0), atol=0.3, rtol=1e-2)
+    torch.testing.assert_close(s[1], (g * (_rows(xbn.float()).double() - mean.double())).sum(0), atol=0.3,
+                               rtol=1e-2)
