@@ -136,10 +136,11 @@ def launch_job(args) -> int:
         #    operator) -- ranks forked from the pre-imported zygote
         z = mgr.kubelet.zygote if mgr.kubelet is not None else None
         zygote_ready = bool(z is not None and z.ready.wait(timeout=min(args.timeout, 300)))
-        # ... and its device libraries in the page cache (runtime/zygote.py
-        # PREFETCH_LIBS: the first collective's RCCL code-object read)
+        # ... its device libraries in the page cache and the node warm-up done
+        # (runtime/zygote.py, runtime/node_warm.py: the code-object cache the
+        # first communicator of a fresh node otherwise fills, ~2.6 s)
         if z is not None:
-            z.prefetched.wait(timeout=min(args.timeout, 120))
+            z.prefetched.wait(timeout=min(args.timeout, 240))
         t_submit = time.time()
         job = mgr.apply(make_job(args))
         uid = job["metadata"]["uid"]
@@ -184,6 +185,8 @@ def launch_job(args) -> int:
         res["launch"] = "warm (zygote)" if zygote_ready else "cold (no zygote)"
         if z is not None and z.prefetch_s is not None:
             res["node_prefetch_s"] = round(z.prefetch_s, 3)
+        if z is not None and z.warm is not None:
+            res["node_warm"] = z.warm
         res.update(cold)
         if os.environ.get("KDL_BENCH_KEEP"):
             res["home"] = home

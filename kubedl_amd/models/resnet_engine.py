@@ -737,9 +737,6 @@ class EngineOptions:
     # 11.3k img/s when introduced); side_prio: its HIP stream priority
     side: bool = True
     side_prio: int = 0
-    # CUs the side stream may use (0: all, a pool stream); a partial CU mask keeps its
-    # weight-gradient blocks off the rest of the chip (ops/streams.py side_stream)
-    side_cus: int = 0
     # BN finalize in the producing GEMM's last blocks ("gemm") or own launches ("kernel")
     bn_fin: str = "gemm"
     # downsample conv of the forward on the side stream
@@ -854,7 +851,7 @@ class ResNetEngine:
         self.side = None
         if self.K.name == "hip" and o.side:
             from kubedl_amd.ops.streams import side_stream
-            self.side = side_stream(self.dev, o.side_prio, o.side_cus)  # (ops/streams.py)
+            self.side = side_stream(self.dev, o.side_prio)  # (ops/streams.py)
             # overlapped with the main stream, the 1x1 weight gradients gain from 256x256
             # tiles too (fewer, heavier side-stream blocks; csrc/conv1x1.hip wgrad_tiles)
             self.K.ext.set_wgrad_big(2)

@@ -45,12 +45,11 @@ def compute_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     return side_stream(device, int(os.environ.get("KDL_MAIN_PRIO", "-1")))
 
 
-def side_stream(device: torch.device, priority: int = 0, cus: int = 0) -> torch.cuda.Stream:
-    """``cus`` > 0: the stream may use only that many CUs (a partial CU mask,
-    spread over the XCDs; csrc/streams.hip), so its kernels never hold the
-    other CUs the critical path's persistent kernels are sized for."""
-    if mode() == "dedicated" or cus > 0:
-        return dedicated_stream(device, priority, cus)
+def side_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:
+    # (a CU-masked side stream -- any mask, even all 256 CUs -- runs the ResNet-50
+    # step at ~9.7k img/s vs 13.6k: profiles/r04_side_stream_cu_mask_ab.txt)
+    if mode() == "dedicated":
+        return dedicated_stream(device, priority)
     return torch.cuda.Stream(device=device, priority=priority)
 
 

@@ -167,12 +167,13 @@ def serve(sock_path: str) -> None:
             conn.close()
 
 
-# Device libraries a rank maps on its first GPU work.  librccl.so (~340 MB,
-# nearly all of it gfx code objects) is read when the first collective builds
-# the communicator: on a fresh box with a cold page cache that first read took
-# comm_init_s to 3.5 s vs 0.9 s warm (profiles/r04_comm_init.txt).  A running
-# node keeps them cached; the node runtime reads them once at start-up -- pure
-# file IO in the kubelet process, no GPU initialisation.
+# Device libraries a rank maps on its first GPU work (librccl.so is ~340 MB,
+# nearly all of it gfx code objects): the node runtime reads them once at
+# start-up -- pure file IO in the kubelet process, no GPU initialisation.  The
+# first communicator's 3.5 s on a fresh node (vs 0.9 s after) turned out NOT to
+# be this read (prefetched, it stayed 3.4 s) but the code-object manager's disk
+# cache, which the node warm-up below fills (runtime/node_warm.py,
+# profiles/r04_comgr_cache.txt).
 PREFETCH_LIBS = ("librccl.so", "libamdhip64.so", "libhsa-runtime64.so")
 
 
@@ -210,6 +211,22 @@ def prefetch_files(paths: List[str], chunk: int = 8 << 20) -> int:
     return n
 
 
+def warm_node(env: dict, timeout: float = 180.0) -> dict:
+    """Run runtime/node_warm.py in a child process (one world-1 RCCL
+    communicator on the first visible GPU) and return its JSON result."""
+    import subprocess
+    t0 = time.time()
+    try:
+        p = subprocess.run([sys.executable, "-m", "kubedl_amd.runtime.node_warm"], env=env or None,
+                           capture_output=True, text=True, timeout=timeout)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        res = json.loads(lines[-1]) if lines else {"warm": False, "error": (p.stderr or "")[-300:]}
+    except (OSError, subprocess.TimeoutExpired, ValueError) as e:
+        res = {"warm": False, "error": f"{type(e).__name__}: {e}"}
+    res["wall_s"] = round(time.time() - t0, 3)
+    return res
+
+
 class ZygoteClient:
     """Kubelet side: start the zygote lazily and ask it for rank processes."""
 
@@ -222,6 +239,8 @@ class ZygoteClient:
         self.ready = threading.Event()
         self.prefetched = threading.Event()
         self.prefetch_s: Optional[float] = None
+        self.warm: Optional[dict] = None
+        self._env: dict = {}
 
     def start(self, env: dict) -> None:
         with self._lock:
@@ -233,6 +252,7 @@ class ZygoteClient:
                 env.pop(k, None)
             argv = [sys.executable, "-u", "-m", "kubedl_amd.runtime.zygote", self.sock]
             self.pid = self.native.spawn(argv, [f"{k}={v}" for k, v in env.items()], None, self.log, self.log)
+            self._env = env
         threading.Thread(target=self._wait_ready, daemon=True).start()
         threading.Thread(target=self._prefetch, daemon=True).start()
 
@@ -240,8 +260,12 @@ class ZygoteClient:
         t0 = time.time()
         try:
             prefetch_files(device_library_paths())
-        finally:
             self.prefetch_s = time.time() - t0
+            if os.environ.get("KDL_NODE_WARM", "1") != "0" and os.path.exists("/dev/kfd"):
+                self.warm = warm_node(self._env)
+        finally:
+            if self.prefetch_s is None:
+                self.prefetch_s = time.time() - t0
             self.prefetched.set()
 
     def _wait_ready(self, timeout: float = 300.0) -> None:

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4 A/B: the weight-gradient side stream on a partial CU mask
 # (EngineOptions.side_cus; 0 = pool stream on all CUs, 256 = full-mask own queue).
-# bench.py --direct, interleaved, two rounds.
+# bench.py --direct, interleaved, two rounds.  (Historical: every mask lost ~29 %,
+# profiles/r04_side_stream_cu_mask_ab.txt, and the option was removed again.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -35,3 +35,13 @@ def test_zygote_launch(tmp_path, monkeypatch):
         assert m.metrics.observed["first"]
     finally:
         m.stop()
+
+
+def test_node_warm_child_reports_json():
+    """runtime/node_warm.py runs in a child process and reports one JSON line
+    (on a CPU host: no GPU, nothing warmed, no error)."""
+    import os
+    from kubedl_amd.runtime.zygote import warm_node
+    res = warm_node(dict(os.environ), timeout=120)
+    assert "warm_s" in res and "wall_s" in res, res
+    assert res["warm"] is False and res.get("reason") == "no GPU", res
