@@ -170,30 +170,41 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ y,
                                                              bf16_t* __restrict__ dz, float* __restrict__ dbias,
                                                              int M, int N, int rows_per_block) {
-  const int cg = blockIdx.y * 32 + (threadIdx.x & 31);  // 8-column group
-  const int r0 = threadIdx.x >> 5;                        // 8 row lanes
-  if (cg * 8 >= N) return;
+  __shared__ float red[8][32 * 8];
+  const int cl = threadIdx.x & 31;        // column group within the block
+  const int cg = blockIdx.y * 32 + cl;    // 8-column group
+  const int r0 = threadIdx.x >> 5;        // 8 row lanes
   float s[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s[i] = 0.f;
-  const int mb = blockIdx.x * rows_per_block;
-  const int me = (mb + rows_per_block) < M ? (mb + rows_per_block) : M;
-  for (int m = mb + r0; m < me; m += 8) {
-    float g[8], yy[8];
-    const int64_t o = static_cast<int64_t>(m) * N + cg * 8;
-    Vec<bf16_t, 8>::load(dy + o, g);
-    if (y != nullptr) {
-      Vec<bf16_t, 8>::load(y + o, yy);
+  if (cg * 8 < N) {
+    const int mb = blockIdx.x * rows_per_block;
+    const int me = (mb + rows_per_block) < M ? (mb + rows_per_block) : M;
+    for (int m = mb + r0; m < me; m += 8) {
+      float g[8], yy[8];
+      const int64_t o = static_cast<int64_t>(m) * N + cg * 8;
+      Vec<bf16_t, 8>::load(dy + o, g);
+      if (y != nullptr) {
+        Vec<bf16_t, 8>::load(y + o, yy);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
-      Vec<bf16_t, 8>::store(dz + o, g);
+        for (int i = 0; i < 8; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
+        Vec<bf16_t, 8>::store(dz + o, g);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += g[i];
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] += g[i];
   }
+  // the 8 row lanes' sums folded in LDS: one atomic per column per block
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (s[i] != 0.f) __hip_atomic_fetch_add(dbias + cg * 8 + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = 0; i < 8; ++i) red[r0][cl * 8 + i] = s[i];
+  __syncthreads();
+  const int c = threadIdx.x;  // 256 columns of this block
+  if (blockIdx.y * 256 + c < N) {
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a += red[r][c];
+    if (a != 0.f) __hip_atomic_fetch_add(dbias + blockIdx.y * 256 + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------- embeddings
@@ -433,12 +444,12 @@ hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* 
 
 hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* dbias, int M, int N, hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  // ~1024 blocks (a 4096 x 1024 layer at 256 rows per block was 64 blocks on 256
-  // CUs: 44 us per launch); each block adds 8 column sums per thread once
+  // ~256 blocks of 64+ rows (a 4096 x 1024 layer at 256 rows per block was 64 blocks
+  // on 256 CUs, 44 us); partial sums folded in LDS, one atomic per column per block
   const int ncg = (N / 8 + 31) / 32;
-  int rows_per_block = static_cast<int>((static_cast<int64_t>(M) * ncg + 1023) / 1024);
+  int rows_per_block = static_cast<int>((static_cast<int64_t>(M) * ncg + 255) / 256);
   rows_per_block = (rows_per_block + 7) / 8 * 8;
-  if (rows_per_block < 16) rows_per_block = 16;
+  if (rows_per_block < 64) rows_per_block = 64;
   dim3 grid((M + rows_per_block - 1) / rows_per_block, ncg);
   hipLaunchKernelGGL(relu_bwd_dbias_kernel, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dy),
                      static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dz), dbias, M, N, rows_per_block);

@@ -259,6 +259,23 @@ def test_fused_linear_backward_matches_autograd():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,relu", [(4096, 1024, True), (4100, 1000, True), (77, 264, False), (8192, 256, True)])
+def test_relu_bwd_dbias_matches_fp32(M, N, relu):
+    """ReLU-mask backward + bias gradient (csrc/ctr.hip): dz = dy * [y > 0], db =
+    sum over rows -- row tails, a partial 256-column block, no-mask mode."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(3)
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    y = torch.relu(torch.randn(M, N, device="cuda")).bfloat16()
+    dz, db = ext.relu_bwd_dbias(dy, y if relu else None)
+    ref = torch.where(y.float() > 0, dy.float(), torch.zeros_like(dy.float())) if relu else dy.float()
+    if relu:
+        torch.testing.assert_close(dz.float(), ref, atol=0, rtol=0)
+    torch.testing.assert_close(db.float(), ref.sum(0), atol=5e-2, rtol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,K", [(4096, 256), (1000, 128), (77, 520)])
 def test_head_bce_matches_fp32(M, K):
     """Fused logit layer + sigmoid BCE (csrc/ctr.hip head_bce_*) vs fp32 autograd,
