@@ -52,6 +52,11 @@ using namespace gemm;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int IBK = 64;                 // K per stage (one 128-B LDS row per operand row)
+// 1: the two-stage loop issues the next K-step's DMA a quarter at a time in
+// front of each 16-deep MFMA sub-step instead of all of it after the barrier
+#ifndef KDL_IGEMM_SPREAD
+#define KDL_IGEMM_SPREAD 0
+#endif
 constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load returns zeros
 
 template <int A, int B> struct cmax { static constexpr int v = A > B ? A : B; };
@@ -217,7 +222,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     }
   };
 
-  auto issue = [&](int kt, int stage) {
+  auto issue = [&](int kt, int stage, int i0 = 0, int i1 = 1 << 30) {
     const int k0 = kt * IBK;
     char* base = lds + stage * STAGE;
     int tap = 0, kc0 = k0, r3 = 0, q3 = 0;
@@ -237,6 +242,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     }
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
+      if (i < i0 || i >= i1) continue;
       const int g = wave * IPW + i;
       lds_void_t* dst = (lds_void_t*)(base + g * 1024);
       if (g < BM / 8) {
@@ -282,10 +288,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-    auto compute = [&](const char* As) {
+    // nxt >= 0: also issue K-step nxt's DMA into stage nst, a quarter per sub-step
+    auto compute = [&](const char* As, int nxt = -1, int nst = 0) {
       const char* Bs = As + SA;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
+        if (KDL_IGEMM_SPREAD && nxt >= 0) issue(nxt, nst, s * IPW / 4, (s + 1) * IPW / 4);
         bf16x8_t wf[TN], xf[TM];
 #pragma unroll
         for (int i = 0; i < TN; ++i)
@@ -304,8 +312,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
       issue(0, 0);
       for (int kt = 0; kt < nk; ++kt) {
         __syncthreads();  // stage kt landed (every wave's vmcnt(0) + barrier); stage kt+1 free
-        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-        compute(lds + (kt & 1) * STAGE);
+        if (KDL_IGEMM_SPREAD) {
+          compute(lds + (kt & 1) * STAGE, kt + 1 < nk ? kt + 1 : -1, (kt + 1) & 1);
+        } else {
+          if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+          compute(lds + (kt & 1) * STAGE);
+        }
       }
     } else {
       // three stages, two K-steps of DMA in flight across each barrier: a

@@ -20,6 +20,18 @@ def load():
     if _mod is not None:
         return _mod
     try:
+        alt = os.environ.get("KDL_C_PATH")
+        if alt:  # an A/B build of the same module (ops/build.py ``out`` / ``defines``)
+            import importlib.machinery
+            import importlib.util
+            import sys
+            loader = importlib.machinery.ExtensionFileLoader("kubedl_amd._C", alt)
+            spec = importlib.util.spec_from_file_location("kubedl_amd._C", alt, loader=loader)
+            mod = importlib.util.module_from_spec(spec)
+            loader.exec_module(mod)
+            sys.modules["kubedl_amd._C"] = mod
+            _mod = mod
+            return _mod
         _mod = importlib.import_module("kubedl_amd._C")
         return _mod
     except Exception as e:  # pragma: no cover - depends on build state

@@ -55,12 +55,12 @@ def _headers_digest() -> str:
     return h.hexdigest()
 
 
-def _compile(src: Path, flags, hdr_digest: str, force: bool) -> Path:
+def _compile(src: Path, flags, hdr_digest: str, force: bool, bdir: Path = BUILD) -> Path:
     key = hashlib.sha256(src.read_bytes() + " ".join(flags).encode() + hdr_digest.encode()).hexdigest()[:16]
-    obj = BUILD / f"{src.stem}.{src.suffix[1:]}.{key}.o"
+    obj = bdir / f"{src.stem}.{src.suffix[1:]}.{key}.o"
     if obj.exists() and not force:
         return obj
-    for old in BUILD.glob(f"{src.stem}.{src.suffix[1:]}.*.o"):
+    for old in bdir.glob(f"{src.stem}.{src.suffix[1:]}.*.o"):
         old.unlink()
     cmd = [HIPCC] + flags + ["-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -69,11 +69,16 @@ def _compile(src: Path, flags, hdr_digest: str, force: bool) -> Path:
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True, out: Path | None = None,
+          defines: tuple = ()) -> Path:
+    """``out`` / ``defines``: an A/B variant of the extension (e.g. ``-DKDL_IGEMM_SPREAD=1`` into
+    ``kubedl_amd/_C_alt.so``), loaded instead of ``_C.so`` with ``KDL_C_PATH`` (ops/_ext.py)."""
+    out = Path(out) if out is not None else OUT
+    bdir = BUILD if out == OUT else BUILD / out.stem  # a variant keeps its own objects
+    bdir.mkdir(parents=True, exist_ok=True)
     inc, lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    common = _common_flags(abi)
+    common = _common_flags(abi) + [f"-D{d}" for d in defines]
     hip_flags = common + [f"--offload-arch={ARCH}", "-x", "hip", f"-I{CSRC}",
                           "-munsafe-fp-atomics"]
     cpp_flags = common + [f"-I{CSRC}", f"-I{py_inc}"] + [f"-I{p}" for p in inc] + [
@@ -83,7 +88,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = {ex.submit(_compile, s, hip_flags if s.suffix == ".hip" else cpp_flags, hdr, force): s
+        futs = {ex.submit(_compile, s, hip_flags if s.suffix == ".hip" else cpp_flags, hdr, force, bdir): s
                 for s in srcs}
         objs = []
         for f in cf.as_completed(futs):
@@ -92,21 +97,21 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
                 print(f"[kdl-build] {futs[f].name}", flush=True)
     objs.sort()
     link_key = hashlib.sha256(" ".join(str(o) for o in objs).encode()).hexdigest()[:16]
-    stamp = BUILD / "link.stamp"
-    if OUT.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
-        return OUT
-    tmp = OUT.with_suffix(".so.tmp")
+    stamp = BUILD / ("link.stamp" if out == OUT else f"link.{out.stem}.stamp")
+    if out.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
+        return out
+    tmp = out.with_suffix(".so.tmp")
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + [str(o) for o in objs] + [
         f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
         f"-Wl,-rpath,{lib}", "-Wl,--no-as-needed"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, OUT)
+    os.replace(tmp, out)
     stamp.write_text(link_key)
     if verbose:
-        print(f"[kdl-build] linked {OUT}", flush=True)
-    return OUT
+        print(f"[kdl-build] linked {out}", flush=True)
+    return out
 
 
 NATIVE_OUT = ROOT / "kubedl_amd" / "_native.so"
