@@ -57,6 +57,10 @@ constexpr int IBK = 64;                 // K per stage (one 128-B LDS row per op
 #ifndef KDL_IGEMM_SPREAD
 #define KDL_IGEMM_SPREAD 0
 #endif
+// 1: each 16-deep sub-step's fragment reads are issued one sub-step ahead
+#ifndef KDL_IGEMM_FRAGPIPE
+#define KDL_IGEMM_FRAGPIPE 0
+#endif
 constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load returns zeros
 
 template <int A, int B> struct cmax { static constexpr int v = A > B ? A : B; };
@@ -291,6 +295,35 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     // nxt >= 0: also issue K-step nxt's DMA into stage nst, a quarter per sub-step
     auto compute = [&](const char* As, int nxt = -1, int nst = 0) {
       const char* Bs = As + SA;
+      // (not on 256x256: its second fragment set spills, 12 -> 44 B and 32 -> 64 B)
+      if constexpr (KDL_IGEMM_FRAGPIPE && BM * BN < 256 * 256) {
+        // fragments one sub-step ahead: sub-step s+1's ds_reads are in flight
+        // while sub-step s's MFMAs run (two register sets, static indices)
+        bf16x8_t wf[2][TN], xf[2][TM];
+        auto ld = [&](int s, int b) {
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+            wf[b][i] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + i * 32 + fr) * 128 + xo[s]);
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            xf[b][j] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + j * 32 + fr) * 128 + xo[s]);
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (KDL_IGEMM_SPREAD && nxt >= 0) issue(nxt, nst, s * IPW / 4, (s + 1) * IPW / 4);
+          if (s + 1 < 4) ld(s + 1, (s + 1) & 1);
+          // pin the order: the next reads stay ahead of this sub-step's MFMAs
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][i], xf[s & 1][j], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         if (KDL_IGEMM_SPREAD && nxt >= 0) issue(nxt, nst, s * IPW / 4, (s + 1) * IPW / 4);
