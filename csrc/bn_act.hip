@@ -45,6 +45,7 @@
 #include "bn_fin.h"
 #include "common.h"
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace kdl {
 namespace {
@@ -797,10 +798,7 @@ ReducePlan plan_reduce(int64_t M, int C, int VEC) {
   p.tl = make_tiling(C, VEC);
   int64_t target = 1024 / p.tl.gy;
   if (target < 1) target = 1;
-  static const int64_t kMinRows = [] {
-    const char* e = getenv("KDL_BN_MIN_ROWS");  // tuning knob for sweeps; default measured best
-    return static_cast<int64_t>(e ? atoi(e) : 128);
-  }();
+  static const int64_t kMinRows = tune_int("bn_min_rows", 128);  // sweep knob; default measured best
   int64_t min_rows = static_cast<int64_t>(p.tl.RPI) * 16;
   if (min_rows < kMinRows) min_rows = kMinRows;
   int64_t gx = (M + min_rows - 1) / min_rows;

@@ -55,6 +55,7 @@
 #include "common.h"
 #include "gemm_epi.h"
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace kdl {
 namespace {
@@ -620,7 +621,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tiles_n = p.N / BN;
   // persistent blocks: one round of the resident capacity (256 CUs x MINB), nblk % 8 == 0
   // (1 round measured +2.3% per ResNet-50 step over 2; KDL_GEMM_ROUNDS overrides)
-  static const int rounds = [] { const char* e = getenv("KDL_GEMM_ROUNDS"); return e ? atoi(e) : 1; }();
+  static const int rounds = tune_int("gemm_rounds", 1);
   const int target = 256 * MINB * rounds;
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
@@ -686,10 +687,7 @@ hipError_t dispatch_pg(const GemmParams& p, int epi, int pro, int gather, hipStr
 // Tile configs: 0 = 128x128 (2 blocks/CU), 1 = 128x64, 2 = 64x128, 3 = 64x64 (4 blocks/CU),
 // 5 = 128x128 with 32-deep K-steps (40 KiB of LDS, 3 blocks/CU).
 int pick_config(int M, int N, int K, int epi) {
-  static const int forced = [] {
-    const char* e = getenv("KDL_GEMM_CFG");
-    return e ? atoi(e) : -1;
-  }();
+  static const int forced = tune_int("gemm_cfg", -1);
   if (forced >= 0 && forced <= 5) {
     if ((forced == 0 || forced == 2 || forced == 5) && N % 128) return 3;
     if (forced == 4) return N % 128 ? 1 : 0;
@@ -705,12 +703,9 @@ int pick_config(int M, int N, int K, int epi) {
 }  // namespace
 
 namespace {
-// KDL_GEMM_CORE: "reg" = register-staged loop only, "dma" = LDS-DMA loop
-// wherever it applies, unset = by shape (long K / 3x3 without prologue -> DMA)
-int g_core = [] {
-  const char* e = getenv("KDL_GEMM_CORE");
-  return e ? (e[0] == 'r' ? 0 : 1) : -1;
-}();
+// KDL_TUNE gemm_core: 0 = register-staged loop only, 1 = LDS-DMA loop wherever it
+// applies, -1 (default) = by shape (long K / 3x3 without prologue -> DMA)
+int g_core = tune_int("gemm_core", -1);
 }  // namespace
 
 int gemm_core_mode() { return g_core; }
@@ -836,10 +831,10 @@ hipError_t conv3x3_dgrad_s2(const Conv1x1Args& a, hipStream_t s) {
 // img/s (profiles/r02_wgrad_big_tiles_ab.txt).  Without that overlap (the CTR
 // tower's weight gradients) the 1x1 ones stay on 128 tiles (CTR samples/s equal
 // within run-to-run noise either way: 3.19-3.33 M vs 3.12-3.31 M).
-// KDL_WGRAD_BIG: 0 off, 1 3x3 only (default), 2 both -- the ResNet engine selects
+// KDL_TUNE wgrad_big: 0 off, 1 3x3 only (default), 2 both -- the ResNet engine selects
 // 2 when its weight-gradient stream is on (set_wgrad_big, before its workspaces
 // are sized); else 128 or 64 per dimension.
-int g_wgrad_big = [] { const char* e = getenv("KDL_WGRAD_BIG"); return e ? atoi(e) : -1; }();
+int g_wgrad_big = tune_int("wgrad_big", -1);
 // bwd (a BN-backward-apply G prologue, csrc/wgrad_dma.hip BWDG): its gx panels
 // double G's LDS share, so N tiles of at most 128 with K tiles up to 256 (8 waves)
 void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk, bool bwd = false) {
@@ -869,7 +864,7 @@ int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false) {
   // win: they leave CUs to the critical path (job step, same box, 256x256 tiles
   // at half the target: 1024 -> 12,460, 512 -> 12,830, 384 -> 13,047, 320 ->
   // 13,078, 256 -> 12,933, 192 -> 12,715 img/s; profiles/r02_wgrad_blocks_sweep.txt)
-  int target = [] { const char* e = getenv("KDL_WGRAD_BLOCKS"); return e ? atoi(e) : 320; }();
+  int target = tune_int("wgrad_blocks", 320);
   if (tn == 256 || (bwd && !(tn == 64 && tk == 64))) target /= 2;  // one (8-wave) block per CU
   int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;
@@ -883,9 +878,9 @@ int conv1x1_wgrad_splits(int M, int N, int K) {
   return a > b ? a : b;
 }
 
-// the caller's preference (an explicit KDL_WGRAD_BIG wins)
+// the caller's preference (an explicit KDL_TUNE wgrad_big wins)
 void set_wgrad_big(int mode) {
-  static const bool env = getenv("KDL_WGRAD_BIG") != nullptr;
+  static const bool env = tune_has("wgrad_big");
   if (!env) g_wgrad_big = mode;
 }
 
@@ -917,11 +912,11 @@ hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t
                         int layout = 0) {
   // timing-only (KDL_PRICE_WGRAD_REDUCE=0): skip the slab reduce to price its
   // cost in the two-stream step (weight gradients are then garbage)
-  static const bool skip = [] { const char* e = getenv("KDL_PRICE_WGRAD_REDUCE"); return e && e[0] == '0'; }();
+  static const bool skip = tune_int("price_wgrad_reduce", 1) == 0;
   if (skip) return hipSuccess;
   const int rgrid = static_cast<int>((nk / 4 + kRedCols - 1) / kRedCols);
-  // y-blocks to reach ~KDL_WGRAD_RED_BLOCKS (2048) blocks in the first pass
-  static const int red_target = [] { const char* e = getenv("KDL_WGRAD_RED_BLOCKS"); return e ? atoi(e) : 2048; }();
+  // y-blocks to reach ~KDL_TUNE wgrad_red_blocks (2048) blocks in the first pass
+  static const int red_target = tune_int("wgrad_red_blocks", 2048);
   int groups = (red_target + rgrid - 1) / rgrid;
   const int by_work = (nsplit + 31) / 32;             // >= 2 slabs per thread in pass 1
   if (groups > by_work) groups = by_work;

@@ -19,6 +19,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace {
 
@@ -58,9 +59,8 @@ class GbdtGrower {
     // chunks (fewer flushes: 2048 +7 %, 4096 +32 %, 8192 2.3x the histogram time);
     // deeper unrolling, a bank-spread LDS image and a branch-free body were all
     // neutral or slower -- the LDS float-atomic rate bounds the build.
-    // KDL_GBDT_RPB overrides.
-    const char* e = getenv("KDL_GBDT_RPB");
-    const int64_t target = e ? std::max(1, atoi(e)) : 0;
+    // KDL_TUNE gbdt_rpb overrides.
+    const int64_t target = std::max(0, kdl::tune_int("gbdt_rpb", 0));
     rpb_ = 256;
     if (target > 0) {
       rpb_ = static_cast<int>(target);

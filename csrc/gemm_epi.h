@@ -112,7 +112,7 @@ hipError_t wgrad_dma(const WgParams& p, int nsplit, int tn, int tk, hipStream_t 
 // csrc/igemm.hip: LDS-DMA main loop (no A prologue); cfg from igemm_pick.
 // Requires K % 64 == 0 (3x3: Cin % 64 == 0) and 32-bit operand byte offsets.
 int igemm_pick(int M, int N, int K);
-bool g_forced_cfg_unset();  // no KDL_IGEMM_CFG / set_igemm_cfg override in force
+bool g_forced_cfg_unset();  // no KDL_TUNE igemm_cfg / set_igemm_cfg override in force
 hipError_t igemm(const GemmParams& p, int epi, int gather, int cfg, hipStream_t s);
 // n zeroed ticket counters for one launch, from a per-device ring (self-resetting:
 // every kernel that draws from them leaves them zero); null while a stream capture

@@ -38,6 +38,7 @@
 #include "common.h"
 #include "gemm_epi.h"
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace kdl {
 namespace {
@@ -325,14 +326,8 @@ hipError_t launch(const GemmParams& p, int epi, int H, int W, hipStream_t s) {
   return hipGetLastError();
 }
 
-int g_halo = [] {  // KDL_HALO=0 keeps every 3x3 on the implicit GEMM
-  const char* e = getenv("KDL_HALO");
-  return e ? atoi(e) : 1;
-}();
-int g_halo_pro = [] {  // KDL_HALO_PRO=0: no BN + ReLU prologue on the halo kernels
-  const char* e = getenv("KDL_HALO_PRO");
-  return e ? atoi(e) : 1;
-}();
+int g_halo = tune_int("halo", 1);          // 0 keeps every 3x3 on the implicit GEMM
+int g_halo_pro = tune_int("halo_pro", 1);  // 0: no BN + ReLU prologue on the halo kernels
 
 // ---------------------------------------------------------------- weight gradient
 // dW[co][tap][ci] = sum_p dy[p][co] * a[p + tap][ci] for the 56x56, Cin = Cout =
@@ -539,12 +534,11 @@ __global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G
   }
 }
 
-// blocks of the halo weight gradient: at most KDL_HALO_WG_BLOCKS (default 256 =
+// blocks of the halo weight gradient: at most KDL_TUNE halo_wg_blocks (default 256 =
 // one per CU); it runs on the side stream beside the main stream's kernels
 int wg_blocks(int tiles, int* per) {
   static const int cap = [] {
-    const char* e = getenv("KDL_HALO_WG_BLOCKS");
-    const int v = e ? atoi(e) : 256;
+    const int v = tune_int("halo_wg_blocks", 256);
     return v < 8 ? 8 : v;
   }();
   const int p = (tiles + cap - 1) / cap;

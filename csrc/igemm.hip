@@ -43,6 +43,7 @@
 #include "common.h"
 #include "gemm_epi.h"
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace kdl {
 namespace {
@@ -397,7 +398,7 @@ hipError_t launch(const GemmParams& p, hipStream_t s) {
   const int tiles_n = q.N / BN;
   // one round of resident blocks (KDL_IGEMM_ROUNDS > 1: that many rounds -- shorter
   // per-block tile lists, for the two-stream step's contention; A/B knob)
-  static const int rounds = [] { const char* e = getenv("KDL_IGEMM_ROUNDS"); const int v = e ? atoi(e) : 1; return v < 1 ? 1 : v; }();
+  static const int rounds = [] { const int v = tune_int("igemm_rounds", 1); return v < 1 ? 1 : v; }();
   const int target = 256 * BPC * rounds;
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
@@ -451,7 +452,7 @@ hipError_t dispatch_gather(const GemmParams& p, int epi, int gather, hipStream_t
 // 64x128 at 3-4 blocks/CU) lose 15-60 %.  Operand delivery into LDS, not
 // latency, bounds these kernels (~7-10 TB/s of L2->LDS traffic chip-wide).
 namespace {
-int g_forced_cfg = [] { const char* e = getenv("KDL_IGEMM_CFG"); return e ? atoi(e) : -1; }();
+int g_forced_cfg = tune_int("igemm_cfg", -1);
 }  // namespace
 
 void set_igemm_cfg(int cfg) { g_forced_cfg = cfg; }
@@ -479,11 +480,8 @@ int igemm_pick(int M, int N, int K) {
 
 namespace gemm {
 hipError_t igemm(const GemmParams& p_in, int epi, int gather, int cfg, hipStream_t s) {
-  static const int price = [] {  // timing-only: price one operand's traffic (outputs are wrong)
-    const char* e = getenv("KDL_IGEMM_PRICE");
-    if (!e) return 0;
-    return (strchr(e, 'A') ? 1 : 0) | (strchr(e, 'B') ? 2 : 0);
-  }();
+  // timing-only: price one operand's traffic (outputs are wrong): 1 drops A's loads, 2 B's
+  static const int price = tune_int("igemm_price", 0);
   GemmParams p = p_in;
   p.price_drop = price;
   if (p.K % IBK || p.M <= 0) return hipErrorInvalidValue;

@@ -295,7 +295,7 @@ hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, v
                              int layout = 0);
 void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)
 int conv1x1_wgrad_splits(int M, int N, int K);
-// 256 x 256 weight-gradient tiles: 0 off, 1 3x3 only (default), 2 3x3 + 1x1 (ignored under KDL_WGRAD_BIG)
+// 256 x 256 weight-gradient tiles: 0 off, 1 3x3 only (default), 2 3x3 + 1x1 (ignored under KDL_TUNE wgrad_big)
 void set_wgrad_big(int mode);
 // dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace
 // (conv1x1_wgrad_splits(M, N, K) x [N, K] fp32, no initialisation needed); the

@@ -47,7 +47,7 @@ want benchfind && run_step bench_find 900 python bench.py --direct --steps 20 --
 want launch && run_step bench_launch 600 python -m kubedl_amd.cli bench-launch --jobs 1 --gpus 1 --steps 20 --warmup 5
 if want bnsweep; then
   for mr in ${SWEEP:-128 256 512 1024}; do
-    KDL_BN_MIN_ROWS=$mr run_step bench_minrows_$mr 600 python bench.py --steps 20 --warmup 8
+    KDL_TUNE=bn_min_rows=$mr run_step bench_minrows_$mr 600 python bench.py --steps 20 --warmup 8
   done
 fi
 if want envsweep; then  # SWEEPVAR=<env var> SWEEP="<values>": direct bench per value

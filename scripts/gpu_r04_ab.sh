@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for r in 1 2; do
-  for spec in ${AB:-"base:X=1" "noreduce:KDL_PRICE_WGRAD_REDUCE=0" "ddpcopy:KDL_DDP_WORLD1=copy"}; do
+  for spec in ${AB:-"base:X=1" "noreduce:KDL_TUNE=price_wgrad_reduce=0" "ddpcopy:KDL_DDP_WORLD1=copy"}; do
     name=${spec%%:*}; envs=${spec#*:}
     env $envs timeout -k 10 180 python bench.py --direct --steps 20 --warmup 6 > gpurun_out/ab4_${name}_r$r.log 2>&1 || exit $?
     echo "$name r$r $(grep -o '"value": [0-9.]*' gpurun_out/ab4_${name}_r$r.log) $(grep -o '"exposed_ms_per_step": [0-9.a-z]*' gpurun_out/ab4_${name}_r$r.log)"

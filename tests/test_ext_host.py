@@ -27,7 +27,7 @@ def test_conv3x3_wgrad_slabs_cover_the_halo_path():
         ho = (h - 1) // s + 1
         assert ext.conv3x3_wgrad_slabs(nb, h, h, cin, cout, s) == \
             ext.conv1x1_wgrad_splits(nb * ho * ho, cout, 9 * cin)
-    target = int(os.environ.get("KDL_WGRAD_BLOCKS", "320")) // 2  # 256x256 tiles: one block per CU
+    target = int(320) // 2  # 256x256 tiles: one block per CU
     for nb, h, c, s, tiles in [(256, 14, 256, 1, 9), (256, 7, 512, 1, 36), (256, 14, 512, 2, 36)]:
         ho = (h - 1) // s + 1
         assert ext.conv3x3_wgrad_slabs(nb, h, h, c, c, s) == max(1, target // tiles)
@@ -39,3 +39,27 @@ def test_bn_workspace_layout_size():
     # [32][2C] fwd replicas | [32][2C] bwd | [5C] coefficients | [32] finalize descriptor | [64] tile counters
     for c in (64, 256, 2048):
         assert ext.bn_workspace_floats(c) == 32 * 4 * c + 5 * c + 32 + 64
+
+
+def test_native_tune_knobs_parse(tmp_path):
+    """csrc/tune.h: every native A/B knob comes from the one KDL_TUNE variable."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    gxx = shutil.which("g++")
+    if gxx is None:
+        import pytest
+        pytest.skip("no g++")
+    root = Path(__file__).resolve().parents[1]
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "tune.h"\n#include <cstdio>\n'
+                   'int main() { printf("%d %d %d %d %d\\n", kdl::tune_int("gemm_cfg", -1), kdl::tune_int("igemm_cfg", -1),'
+                   ' kdl::tune_int("halo", 1), (int)kdl::tune_has("wgrad_big"), kdl::tune_int("gemm", 7)); }\n')
+    exe = tmp_path / "t"
+    subprocess.run([gxx, "-std=c++17", f"-I{root / 'csrc'}", str(src), "-o", str(exe)], check=True)
+    env = dict(os.environ, KDL_TUNE="gemm_cfg=5, igemm_cfg=2,wgrad_big=0")
+    out = subprocess.run([str(exe)], env=env, capture_output=True, text=True, check=True).stdout.split()
+    assert out == ["5", "2", "1", "1", "7"], out
+    env.pop("KDL_TUNE")
+    out = subprocess.run([str(exe)], env=env, capture_output=True, text=True, check=True).stdout.split()
+    assert out == ["-1", "-1", "1", "0", "7"], out
