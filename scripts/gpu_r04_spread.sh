@@ -15,6 +15,8 @@ for v in ${VARIANTS:-alt alt2}; do
     tests/test_conv3x3_gpu.py tests/test_dgrad_s2_gpu.py tests/test_igemm_gpu.py > gpurun_out/spread_tests_$v.log 2>&1
   rc=$?; echo "$v tests: $(tail -1 gpurun_out/spread_tests_$v.log)"; [ $rc -eq 0 ] || exit 1
 done
+timeout -k 10 300 python scripts/gemm1x1_core_probe.py > gpurun_out/gemm1x1_core_probe.log 2>&1 || exit $?
+grep -o '"shape.*' gpurun_out/gemm1x1_core_probe.log
 for v in base ${VARIANTS:-alt alt2}; do
   p=$(so $v)
   if [ -n "$p" ]; then export KDL_C_PATH=$p; else unset KDL_C_PATH; fi
