@@ -22,12 +22,11 @@ def load():
     try:
         alt = os.environ.get("KDL_C_PATH")
         if alt:  # an A/B build of the same module (ops/build.py ``out`` / ``defines``)
-            import importlib.machinery
-            import importlib.util
             import sys
-            loader = importlib.machinery.ExtensionFileLoader("kubedl_amd._C", alt)
-            spec = importlib.util.spec_from_file_location("kubedl_amd._C", alt, loader=loader)
-            mod = importlib.util.module_from_spec(spec)
+            from importlib import machinery, util
+            loader = machinery.ExtensionFileLoader("kubedl_amd._C", alt)
+            spec = util.spec_from_file_location("kubedl_amd._C", alt, loader=loader)
+            mod = util.module_from_spec(spec)
             loader.exec_module(mod)
             sys.modules["kubedl_amd._C"] = mod
             _mod = mod
