@@ -63,3 +63,15 @@ def test_native_tune_knobs_parse(tmp_path):
     env.pop("KDL_TUNE")
     out = subprocess.run([str(exe)], env=env, capture_output=True, text=True, check=True).stdout.split()
     assert out == ["-1", "-1", "1", "0", "7"], out
+
+
+def test_extension_loads_on_the_host():
+    """ops/_ext.load() imports the in-tree kubedl_amd/_C.so (no GPU needed to
+    import it), and KDL_C_PATH loads an A/B build of the same module."""
+    from pathlib import Path
+    from kubedl_amd.ops import _ext
+    so = Path(__file__).resolve().parents[1] / "kubedl_amd" / "_C.so"
+    if not so.exists():
+        pytest.skip("extension not built")
+    m = _ext.load()
+    assert hasattr(m, "conv1x1_gemm") and hasattr(m, "set_igemm_pro")
