@@ -1441,7 +1441,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_igemm_cfg", &kdl::set_igemm_cfg, "force an LDS-DMA tile config (-1 = by shape)");
   m.def("set_halo3x3", &kdl::set_halo3x3, "1: stride-1 3x3 convs of the early stages on the halo kernel");
   m.def("get_gemm_core", &kdl::gemm_core_mode, "current conv GEMM main-loop mode");
-  m.def("set_igemm_pro", &kdl::set_igemm_pro, "1: BN+ReLU-prologue forward statistics GEMMs on the LDS-DMA loop");
   m.def("spin", &spin_py, "one wave busy-waiting N microseconds on the current stream");
   m.doc() = "kubedl_amd CDNA4 (gfx950) HIP kernels";
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC");

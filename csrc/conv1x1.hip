@@ -709,10 +709,6 @@ int g_core = tune_int("gemm_core", -1);
 }  // namespace
 
 int gemm_core_mode() { return g_core; }
-// the BN + ReLU A prologue of dense forward statistics GEMMs on the LDS-DMA loop
-// (KDL_TUNE igemm_pro; set_igemm_pro from Python)
-int g_igemm_pro = tune_int("igemm_pro", 0);
-void set_igemm_pro(int on) { g_igemm_pro = on; }
 void set_gemm_core_mode(int m) { g_core = m; }
 
 hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
@@ -768,16 +764,6 @@ hipError_t conv1x1_gemm(const Conv1x1Args& a, hipStream_t s) {
     const hipError_t h = halo3x3(p, epi, s);
     if (h != hipErrorInvalidValue) return h;
     if (p.aout) return hipErrorInvalidValue;  // the write-through of relu(B(x)) is the halo kernel's only
-  }
-  // BN + ReLU prologue on the LDS-DMA loop (csrc/igemm.hip PRO; KDL_TUNE igemm_pro=1):
-  // the dense forward statistics GEMMs the register-staged loop runs latency-bound
-  if (pro == PRO_FWD && gather == G_DENSE && epi == EPI_STATS && core != 0 && !p.aout && p.K % 64 == 0 &&
-      p.K <= 1024 && p.C) {
-    if (g_igemm_pro) {
-      p.a_rows = p.M;
-      const hipError_t e = igemm(p, epi, gather, igemm_pick(p.M, p.N, p.K), s);
-      if (e != hipErrorInvalidValue) return e;
-    }
   }
   const int min_k = gather == G_CONV3 ? 0 : 512;
   // (the backward-apply prologue transforms A in registers: register-staged loop)

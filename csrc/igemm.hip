@@ -53,17 +53,7 @@ using namespace gemm;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int IBK = 64;                 // K per stage (one 128-B LDS row per operand row)
-// 1: the two-stage loop issues the next K-step's DMA a quarter at a time in
-// front of each 16-deep MFMA sub-step instead of all of it after the barrier
-#ifndef KDL_IGEMM_SPREAD
-#define KDL_IGEMM_SPREAD 0
-#endif
-// 1: each 16-deep sub-step's fragment reads are issued one sub-step ahead
-#ifndef KDL_IGEMM_FRAGPIPE
-#define KDL_IGEMM_FRAGPIPE 0
-#endif
 constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load returns zeros
-constexpr int kProKmax = 1024;          // widest K of the A-prologue variant (its LDS coefficient table)
 
 template <int A, int B> struct cmax { static constexpr int v = A > B ? A : B; };
 
@@ -106,19 +96,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst,
 #endif
 }
 
-// PRO (dense rows, two stages only): A is relu(A * scale[k] + shift[k]) with
-// GemmParams::pro_coef = [2K] scale | shift (the BN + ReLU of the previous layer,
-// the register-staged loop's PRO_FWD): each landed A panel is transformed in
-// place -- every thread owns ONE logical 16-B chunk column (8 channels, so one
-// coefficient set per K-step) of BM * 8 / NT rows -- before the MFMAs read it.
-// The same fmaf / ReLU / bf16 rounding as csrc/conv1x1.hip's staging, so A' is
-// bit-identical.  The transform is published by a raw barrier; the next K-step's
-// DMA (inline asm, as the three-stage loop's) is issued after it and overlaps
-// this K-step's MFMAs.
-template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES, bool PRO = false>
+template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
   static_assert(STAGES == 2 || STAGES == 3, "2 or 3 LDS stages");
-  static_assert(!PRO || (GATHER == G_DENSE && STAGES == 2), "the A prologue: dense rows, two stages");
   constexpr int NT = 64 * WM * WN;
   constexpr int NW = WM * WN;
   constexpr int SA = BM * 128, SB = BN * 128, STAGE = SA + SB;  // bytes per stage
@@ -131,12 +111,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   constexpr bool TAPS = GATHER == G_CONV3 || GATHER == G_DGRAD2;
   constexpr int LDC = Epi::LDC;
   constexpr int LDS_BYTES = cmax<cmax<STAGES * STAGE, BM * LDC * 2>::v, Epi::kScratchBytes>::v;
-  // PRO: the [2K] coefficient table behind the tiles (K <= kProKmax)
-  constexpr int PRO_BYTES = PRO ? 2 * kProKmax * 4 : 0;
   // ONE __shared__ object (a second one makes hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES + PRO_BYTES];
-  float* pro_lds = reinterpret_cast<float*>(lds + LDS_BYTES);
-  (void)pro_lds;
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -160,12 +136,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.B), (short)0, bytesB,
                                                                       0x00020000);
   i32x4_t wA{}, wB{};
-  if constexpr (STAGES == 3 || PRO) {
+  if constexpr (STAGES == 3) {
     wA = rsrc_words(p.A, static_cast<uint32_t>(bytesA));
     wB = rsrc_words(p.B, static_cast<uint32_t>(bytesB));
   }
   auto dma = [&](bool is_a, lds_void_t* dst, uint32_t voff, uint32_t soff) {
-    if constexpr (STAGES == 3 || PRO) dma16_asm(is_a ? wA : wB, dst, voff, soff);
+    if constexpr (STAGES == 3) dma16_asm(is_a ? wA : wB, dst, voff, soff);
     else dma16(is_a ? rA : rB, dst, voff, soff);
   };
 
@@ -242,7 +218,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     }
   };
 
-  auto issue = [&](int kt, int stage, int i0 = 0, int i1 = 1 << 30) {
+  auto issue = [&](int kt, int stage) {
     const int k0 = kt * IBK;
     char* base = lds + stage * STAGE;
     int tap = 0, kc0 = k0, r3 = 0, q3 = 0;
@@ -262,7 +238,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     }
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      if (i < i0 || i >= i1) continue;
       const int g = wave * IPW + i;
       lds_void_t* dst = (lds_void_t*)(base + g * 1024);
       if (g < BM / 8) {
@@ -288,40 +263,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
 #pragma unroll
   for (int s = 0; s < 4; ++s) xo[s] = static_cast<uint32_t>((((2 * s + fh) ^ ((fr >> 1) & 7))) * 16);
 
-  if constexpr (PRO) {  // coefficients once per block (K <= kProKmax, host-checked)
-    for (int i = t; i < 2 * K / 4; i += NT)
-      reinterpret_cast<float4*>(pro_lds)[i] = reinterpret_cast<const float4*>(p.pro_coef)[i];
-    __syncthreads();
-  }
-  // PRO: relu(A * scale + shift) over the landed A panel of ``stage`` (K-step kt)
-  auto transform_a = [&](int stage, int kt) {
-    char* base = lds + stage * STAGE;
-    const int c = t & 7;                   // this thread's logical 16-B chunk (channels 8c .. 8c+7)
-    const int ch = kt * IBK + 8 * c;
-    float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; j += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(pro_lds + ch + j);
-      const float4 b = *reinterpret_cast<const float4*>(pro_lds + K + ch + j);
-      sc[j] = a.x; sc[j + 1] = a.y; sc[j + 2] = a.z; sc[j + 3] = a.w;
-      sh[j] = b.x; sh[j + 1] = b.y; sh[j + 2] = b.z; sh[j + 3] = b.w;
-    }
-#pragma unroll
-    for (int i = 0; i < BM * 8 / NT; ++i) {
-      const int r = (t >> 3) + i * (NT / 8);
-      uint4* q = reinterpret_cast<uint4*>(base + r * 128 + ((c ^ ((r >> 1) & 7)) * 16));
-      float f[8];
-      unpack8(*q, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float o = fmaf(f[j], sc[j], sh[j]);
-        f[j] = o > 0.f ? o : 0.f;
-      }
-      *q = pack8(f);
-    }
-  };
-  (void)transform_a;
-
   Epi epi;
   epi.init(t, n0);
 
@@ -342,41 +283,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-    // nxt >= 0: also issue K-step nxt's DMA into stage nst, a quarter per sub-step
-    auto compute = [&](const char* As, int nxt = -1, int nst = 0) {
+    auto compute = [&](const char* As) {
       const char* Bs = As + SA;
-      // (not on 256x256: its second fragment set spills, 12 -> 44 B and 32 -> 64 B)
-      if constexpr (KDL_IGEMM_FRAGPIPE && BM * BN < 256 * 256) {
-        // fragments one sub-step ahead: sub-step s+1's ds_reads are in flight
-        // while sub-step s's MFMAs run (two register sets, static indices)
-        bf16x8_t wf[2][TN], xf[2][TM];
-        auto ld = [&](int s, int b) {
-#pragma unroll
-          for (int i = 0; i < TN; ++i)
-            wf[b][i] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + i * 32 + fr) * 128 + xo[s]);
-#pragma unroll
-          for (int j = 0; j < TM; ++j)
-            xf[b][j] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + j * 32 + fr) * 128 + xo[s]);
-        };
-        ld(0, 0);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          if (KDL_IGEMM_SPREAD && nxt >= 0) issue(nxt, nst, s * IPW / 4, (s + 1) * IPW / 4);
-          if (s + 1 < 4) ld(s + 1, (s + 1) & 1);
-          // pin the order: the next reads stay ahead of this sub-step's MFMAs
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < TN; ++i)
-#pragma unroll
-            for (int j = 0; j < TM; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][i], xf[s & 1][j], acc[i][j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        return;
-      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        if (KDL_IGEMM_SPREAD && nxt >= 0) issue(nxt, nst, s * IPW / 4, (s + 1) * IPW / 4);
         bf16x8_t wf[TN], xf[TM];
 #pragma unroll
         for (int i = 0; i < TN; ++i)
@@ -394,28 +304,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     if constexpr (STAGES == 2) {
       issue(0, 0);
       for (int kt = 0; kt < nk; ++kt) {
-        if constexpr (PRO) {
-          // explicit waits: hipcc does not see the inline-asm DMA, so a
-          // __syncthreads() fence would not wait for it
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's DMA of stage kt landed
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // and its reads of stage kt-1 retired
-          __builtin_amdgcn_s_barrier();                       // stage kt complete; stage kt+1 free
-          asm volatile("" ::: "memory");
-          transform_a(kt & 1, kt);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this thread's transformed chunks written
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-          if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);      // overlaps this K-step's MFMAs
-          compute(lds + (kt & 1) * STAGE);
-          continue;
-        }
         __syncthreads();  // stage kt landed (every wave's vmcnt(0) + barrier); stage kt+1 free
-        if (KDL_IGEMM_SPREAD) {
-          compute(lds + (kt & 1) * STAGE, kt + 1 < nk ? kt + 1 : -1, (kt + 1) & 1);
-        } else {
-          if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-          compute(lds + (kt & 1) * STAGE);
-        }
+        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+        compute(lds + (kt & 1) * STAGE);
       }
     } else {
       // three stages, two K-steps of DMA in flight across each barrier: a
@@ -451,7 +342,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   epi.finish(p, reinterpret_cast<float*>(lds), b, gm < tiles_m);
 }
 
-template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES, int BPC, bool PRO = false>
+template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES, int BPC>
 hipError_t launch(const GemmParams& p, hipStream_t s) {
   GemmParams q = p;
   if constexpr (GATHER == G_DGRAD2) {  // four classes of ceil(mc / BM) tiles each
@@ -467,7 +358,7 @@ hipError_t launch(const GemmParams& p, hipStream_t s) {
   int GM = (target + tiles_n - 1) / tiles_n;
   if (GM > tiles_m) GM = tiles_m;
   while ((GM * tiles_n) % 8) ++GM;
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB, STAGES, PRO>), dim3(GM * tiles_n), dim3(64 * WM * WN),
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, GATHER, EPI, MINB, STAGES>), dim3(GM * tiles_n), dim3(64 * WM * WN),
                      0, s, q, GM, tiles_m, tiles_n);
   return hipGetLastError();
 }
@@ -559,12 +450,6 @@ hipError_t igemm(const GemmParams& p_in, int epi, int gather, int cfg, hipStream
   // exact -- the variant is the one that spills both VGPRs and SGPRs around the
   // LDS-DMA loads.  It runs on 256x128 tiles instead.
   if (gather == G_DGRAD2 && epi == EPI_MASKX && cfg == 0) cfg = 1;
-  if (p.pro_coef) {  // the BN + ReLU A prologue (dense forward GEMMs with the statistics epilogue)
-    if (gather != G_DENSE || epi != EPI_STATS || p.K > kProKmax || price) return hipErrorInvalidValue;
-    if (cfg == 0 && p.N % 256 == 0) return launch<256, 256, 2, 4, G_DENSE, EPI_STATS, 1, 2, 1, true>(p, s);
-    if (p.N % 128 == 0) return launch<128, 128, 2, 2, G_DENSE, EPI_STATS, 2, 2, 2, true>(p, s);
-    return hipErrorInvalidValue;
-  }
   switch (cfg) {
     case 0: if (p.N % 256) break; return dispatch_gather<256, 256, 2, 4, 1>(p, epi, gather, s);
     case 1: if (p.N % 128) break; return dispatch_gather<256, 128, 4, 2, 1>(p, epi, gather, s);

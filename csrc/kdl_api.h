@@ -323,7 +323,6 @@ hipError_t spin(hipStream_t s, double microseconds);
 
 // conv GEMM main-loop selection (-1 by shape, 0 register-staged, 1 LDS-DMA)
 int gemm_core_mode();
-void set_igemm_pro(int on);  // 1: PRO_FWD dense statistics GEMMs on the LDS-DMA loop (csrc/igemm.hip PRO)
 void set_gemm_core_mode(int m);
 // force an LDS-DMA tile config (-1 = by shape; csrc/igemm.hip igemm_pick)
 void set_igemm_cfg(int cfg);

@@ -74,4 +74,4 @@ def test_extension_loads_on_the_host():
     if not so.exists():
         pytest.skip("extension not built")
     m = _ext.load()
-    assert hasattr(m, "conv1x1_gemm") and hasattr(m, "set_igemm_pro")
+    assert hasattr(m, "conv1x1_gemm") and hasattr(m, "set_gemm_core")
