@@ -1,3 +1,5 @@
+#include <map>
+#include <mutex>
 // PyTorch bindings for the kubedl_amd HIP kernels (module ``kubedl_amd._C``).
 //
 // Kernels live in the *.hip translation units and take raw pointers plus a
@@ -485,7 +487,19 @@ at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::op
   return c;
 }
 
-std::vector<at::Tensor> relu_bwd_dbias(const at::Tensor& dy, const c10::optional<at::Tensor>& y) {
+// per-device ticket counters of the in-launch reductions (zeroed once; every
+// kernel re-arms its own): slot 0 = head_bce_fwd, 1 = head_bce_bwd, 64.. = relu_bwd_dbias
+static at::Tensor ticket_counters(const at::Tensor& like, int64_t base) {
+  static std::mutex mu;
+  static std::map<int, at::Tensor> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const int dev = like.get_device();
+  auto it = cache.find(dev);
+  if (it == cache.end()) it = cache.insert_or_assign(dev, at::zeros({1 << 14}, like.options().dtype(at::kInt))).first;
+  return it->second.narrow(0, base, (1 << 14) - base);
+}
+
+std::vector<at::Tensor> relu_bwd_dbias(const at::Tensor& dy, const c10::optional<at::Tensor>& y, bool db_bf16) {
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.is_contiguous(),
               "relu_bwd_dbias: dy bf16 [M,N] contiguous");
   TORCH_CHECK(dy.size(1) % 8 == 0, "relu_bwd_dbias: N % 8 == 0");
@@ -493,9 +507,14 @@ std::vector<at::Tensor> relu_bwd_dbias(const at::Tensor& dy, const c10::optional
   const bool has_y = y.has_value() && y->defined();
   at::Tensor dz = has_y ? at::empty_like(dy) : dy;
   if (has_y) TORCH_CHECK(y->sizes() == dy.sizes() && y->is_contiguous(), "relu_bwd_dbias: y shape");
-  auto db = at::zeros({dy.size(1)}, dy.options().dtype(at::kFloat));
-  check_hip(kdl::relu_bwd_dbias(dy.data_ptr(), has_y ? y->data_ptr() : nullptr, dz.data_ptr(), db.data_ptr<float>(),
-                                static_cast<int>(dy.size(0)), static_cast<int>(dy.size(1)), cur_stream()),
+  const int M = static_cast<int>(dy.size(0)), N = static_cast<int>(dy.size(1));
+  auto db = at::empty({N}, dy.options().dtype(db_bf16 ? at::kBFloat16 : at::kFloat));
+  auto part = at::empty({std::max(1, kdl::relu_bwd_dbias_parts(M, N)), N}, dy.options().dtype(at::kFloat));
+  TORCH_CHECK((N + 255) / 256 <= (1 << 14) - 64, "relu_bwd_dbias: N too wide for the ticket slots");
+  auto cnt = ticket_counters(dy, 64);
+  check_hip(kdl::relu_bwd_dbias(dy.data_ptr(), has_y ? y->data_ptr() : nullptr, dz.data_ptr(), part.data_ptr<float>(),
+                                reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), db.data_ptr(), db_bf16, M, N,
+                                cur_stream()),
             "relu_bwd_dbias");
   return {dz, db};
 }
@@ -511,16 +530,20 @@ std::vector<at::Tensor> head_bce_fwd(const at::Tensor& x, const at::Tensor& w, c
                                      const at::Tensor& y) {
   check_head(x, w, "head_bce_fwd");
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(b.scalar_type() == at::kFloat && b.numel() == 1 && b.is_cuda(), "head_bce_fwd: bias f32 [1]");
+  TORCH_CHECK((b.scalar_type() == at::kFloat || b.scalar_type() == at::kBFloat16) && b.numel() == 1 && b.is_cuda(),
+              "head_bce_fwd: bias f32 / bf16 [1]");
   TORCH_CHECK(y.scalar_type() == at::kFloat && y.numel() == M && y.is_contiguous(), "head_bce_fwd: labels f32 [M]");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto opt = x.options().dtype(at::kFloat);
   auto logit = at::empty({M}, opt), dlogit = at::empty({M}, opt), part = at::empty({(M + 3) / 4}, opt);
-  check_hip(kdl::head_bce_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), y.data_ptr<float>(),
-                              static_cast<int>(M), static_cast<int>(K), logit.data_ptr<float>(),
-                              dlogit.data_ptr<float>(), part.data_ptr<float>(), cur_stream()),
+  auto loss = at::empty({1}, opt);
+  auto cnt = ticket_counters(x, 0);
+  check_hip(kdl::head_bce_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), b.scalar_type() == at::kBFloat16,
+                              y.data_ptr<float>(), static_cast<int>(M), static_cast<int>(K), logit.data_ptr<float>(),
+                              dlogit.data_ptr<float>(), part.data_ptr<float>(),
+                              reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), loss.data_ptr<float>(), cur_stream()),
             "head_bce_fwd");
-  return {logit, dlogit, part};
+  return {logit, dlogit, part, loss};
 }
 
 std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dlogit,
@@ -536,13 +559,16 @@ std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, c
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int nb = kdl::head_bce_bwd_blocks(static_cast<int>(M));
   auto opt = x.options().dtype(at::kFloat);
-  auto dx = at::empty_like(x), dw = at::empty({nb, K}, opt), db = at::empty({nb}, opt);
+  auto dx = at::empty_like(x), dwp = at::empty({nb, K}, opt), dbp = at::empty({nb}, opt);
+  auto dw = at::empty({K}, x.options()), db = at::empty({1}, x.options());  // bf16, summed in block order
+  auto cnt = ticket_counters(x, 1);
   check_hip(kdl::head_bce_bwd(x.data_ptr(), w.data_ptr(), dlogit.data_ptr<float>(), static_cast<float>(scale),
                               has_g ? gscale->data_ptr<float>() : nullptr, static_cast<int>(M), static_cast<int>(K),
-                              dx.data_ptr(), dw.data_ptr<float>(),
-                              db.data_ptr<float>(), cur_stream()),
+                              dx.data_ptr(), dwp.data_ptr<float>(), dbp.data_ptr<float>(),
+                              reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), dw.data_ptr(), db.data_ptr(),
+                              cur_stream()),
             "head_bce_bwd");
-  return {dx, dw, db};
+  return {dx, dw, db, dwp, dbp};
 }
 
 void embed_gather(const at::Tensor& table, const at::Tensor& idx, int64_t F, at::Tensor out, int64_t col0) {
@@ -1467,7 +1493,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
   m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b)");
-  m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient");
+  m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient (deterministic; bf16 or fp32)",
+        py::arg("dy"), py::arg("y"), py::arg("db_bf16") = false);
   m.def("head_bce_fwd", &head_bce_fwd, "1-wide logit layer + sigmoid BCE: (logit, dlogit, per-block loss sums)");
   m.def("head_bce_bwd", &head_bce_bwd, "logit layer backward: (dx, per-block dw partials, per-block db partials)");
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");

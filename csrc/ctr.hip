@@ -166,11 +166,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
 
 // ---------------------------------------------------------------- ReLU backward + dbias
 // dz = dy * (y > 0) (bf16 out), dbias[n] += sum_m dz[m, n]; 16 B along N per lane.
+// Row-block partial column sums go to part[blockIdx.x][N]; the last block of a
+// column block to arrive (agent-scope release + ticket; acquire in the
+// reducer: the in-launch split reduction of cdna_hip_programming.md) sums them
+// in row-block order -- deterministic, no zero-fill, no separate conversion --
+// and writes db as bf16 (db16) or fp32 (db32), then re-arms its ticket.
 __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ y,
-                                                             bf16_t* __restrict__ dz, float* __restrict__ dbias,
-                                                             int M, int N, int rows_per_block) {
+                                                             bf16_t* __restrict__ dz, float* __restrict__ part,
+                                                             unsigned* __restrict__ cnt, bf16_t* __restrict__ db16,
+                                                             float* __restrict__ db32, int M, int N,
+                                                             int rows_per_block) {
   __shared__ float red[8][32 * 8];
+  __shared__ int last;
   const int cl = threadIdx.x & 31;        // column group within the block
   const int cg = blockIdx.y * 32 + cl;    // 8-column group
   const int r0 = threadIdx.x >> 5;        // 8 row lanes
@@ -194,17 +202,39 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
       for (int i = 0; i < 8; ++i) s[i] += g[i];
     }
   }
-  // the 8 row lanes' sums folded in LDS: one atomic per column per block
+  // the 8 row lanes folded in LDS, in order: this block's 256 column sums
 #pragma unroll
   for (int i = 0; i < 8; ++i) red[r0][cl * 8 + i] = s[i];
   __syncthreads();
-  const int c = threadIdx.x;  // 256 columns of this block
-  if (blockIdx.y * 256 + c < N) {
+  const int c = threadIdx.x;
+  const int col = blockIdx.y * 256 + c;
+  if (col < N) {
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) a += red[r][c];
-    if (a != 0.f) __hip_atomic_fetch_add(dbias + blockIdx.y * 256 + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    part[static_cast<int64_t>(blockIdx.x) * N + col] = a;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  if (col < N) {
+    float a = 0.f;
+    for (int r = 0; r < static_cast<int>(gridDim.x); ++r) a += part[static_cast<int64_t>(r) * N + col];
+    if (db16) db16[col] = f32_to_bf16(a);
+    else db32[col] = a;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- embeddings
@@ -301,12 +331,18 @@ __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __res
 // ---------------------------------------------------------------- logit head + BCE
 // one wave per row: logit = x[m,:] . w + b; loss_m = softplus(l) - y l;
 // dlogit_m = sigmoid(l) - y.  Each block writes the sum of its rows' losses.
+// The last block to arrive (agent release / ticket / acquire) sums the block
+// partials in order into the mean loss[0] and re-arms its ticket.  b: the bias,
+// bf16 (b16) or fp32.
 __global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ w, const float* __restrict__ b,
+                                                           const bf16_t* __restrict__ b16,
                                                            const float* __restrict__ y, int M, int K,
                                                            float* __restrict__ logit, float* __restrict__ dlogit,
-                                                           float* __restrict__ loss_part) {
+                                                           float* __restrict__ loss_part, unsigned* __restrict__ cnt,
+                                                           float* __restrict__ loss) {
   __shared__ float wave_loss[4];
+  __shared__ int last;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + wv;
   float l = 0.f;
@@ -322,7 +358,7 @@ __global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restr
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    const float z = acc + b[0];
+    const float z = acc + (b16 ? __uint_as_float(static_cast<uint32_t>(b16[0]) << 16) : b[0]);
     const float t = y[m];
     // softplus(z) - t z, stable for both signs
     l = fmaxf(z, 0.f) - t * z + log1pf(__expf(-fabsf(z)));
@@ -333,7 +369,30 @@ __global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restr
   }
   if (lane == 0) wave_loss[wv] = l;
   __syncthreads();
-  if (threadIdx.x == 0) loss_part[blockIdx.x] = (wave_loss[0] + wave_loss[1]) + (wave_loss[2] + wave_loss[3]);
+  if (threadIdx.x == 0) {
+    loss_part[blockIdx.x] = (wave_loss[0] + wave_loss[1]) + (wave_loss[2] + wave_loss[3]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // fixed order: 256 strided partial sums, then the 4 waves' in LDS order
+  float a = 0.f;
+  for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += 256) a += loss_part[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+  if (lane == 0) wave_loss[wv] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    loss[0] = ((wave_loss[0] + wave_loss[1]) + (wave_loss[2] + wave_loss[3])) / static_cast<float>(M);
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // block = 256 threads = 8 row lanes x 32 column groups of 8 (K <= 256 per
@@ -344,8 +403,11 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
                                                            const float* __restrict__ dlogit, float scale,
                                                            const float* __restrict__ gscale, int M,
                                                            int K, int rpb, bf16_t* __restrict__ dx,
-                                                           float* __restrict__ dw_part, float* __restrict__ db_part) {
+                                                           float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                           unsigned* __restrict__ cnt, bf16_t* __restrict__ dw,
+                                                           bf16_t* __restrict__ db) {
   __shared__ float red[8][257];
+  __shared__ int last;
   if (gscale != nullptr) scale *= gscale[0];  // upstream gradient of the loss, read on the device
   const int rl = threadIdx.x >> 5, cg = threadIdx.x & 31;
   const int m0 = blockIdx.x * rpb;
@@ -392,15 +454,42 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
     }
     __syncthreads();
   }
+  if (dw == nullptr) return;  // partials only (the caller sums them)
+  // the last block to arrive sums the partials in block order into bf16 dw / db
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    float t = 0.f;
+    for (int r = 0; r < static_cast<int>(gridDim.x); ++r) t += dw_part[static_cast<int64_t>(r) * K + k];
+    dw[k] = f32_to_bf16(t);
+  }
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int r = 0; r < static_cast<int>(gridDim.x); ++r) t += db_part[r];
+    db[0] = f32_to_bf16(t);
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace
 
-hipError_t head_bce_fwd(const void* x, const void* w, const float* b, const float* y, int M, int K, float* logit,
-                        float* dlogit, float* loss_part, hipStream_t s) {
+hipError_t head_bce_fwd(const void* x, const void* w, const void* b, bool b_bf16, const float* y, int M, int K,
+                        float* logit, float* dlogit, float* loss_part, unsigned* cnt, float* loss, hipStream_t s) {
   if (M <= 0) return hipSuccess;
   hipLaunchKernelGGL(head_bce_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, s, static_cast<const bf16_t*>(x),
-                     static_cast<const bf16_t*>(w), b, y, M, K, logit, dlogit, loss_part);
+                     static_cast<const bf16_t*>(w), b_bf16 ? nullptr : static_cast<const float*>(b),
+                     b_bf16 ? static_cast<const bf16_t*>(b) : nullptr, y, M, K, logit, dlogit, loss_part, cnt, loss);
   return hipGetLastError();
 }
 
@@ -412,13 +501,14 @@ int head_bce_bwd_blocks(int M) {
 }
 
 hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
-                        int K, void* dx, float* dw_part, float* db_part, hipStream_t s) {
+                        int K, void* dx, float* dw_part, float* db_part, unsigned* cnt, void* dw, void* db,
+                        hipStream_t s) {
   if (M <= 0) return hipSuccess;
   const int nb = head_bce_bwd_blocks(M);
   const int rpb = (M + nb - 1) / nb;
   hipLaunchKernelGGL(head_bce_bwd_kernel, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
                      static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx), dw_part,
-                     db_part);
+                     db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db));
   return hipGetLastError();
 }
 
@@ -442,17 +532,30 @@ hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* 
   return hipGetLastError();
 }
 
-hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* dbias, int M, int N, hipStream_t s) {
-  if (M <= 0 || N <= 0) return hipSuccess;
-  // ~256 blocks of 64+ rows (a 4096 x 1024 layer at 256 rows per block was 64 blocks
-  // on 256 CUs, 44 us); partial sums folded in LDS, one atomic per column per block
+int relu_bwd_dbias_rows(int M, int N) {
+  // ~256 blocks of 64+ rows (a 4096 x 1024 layer at 256 rows per block was 64
+  // blocks on 256 CUs, 44 us)
   const int ncg = (N / 8 + 31) / 32;
   int rows_per_block = static_cast<int>((static_cast<int64_t>(M) * ncg + 255) / 256);
   rows_per_block = (rows_per_block + 7) / 8 * 8;
-  if (rows_per_block < 64) rows_per_block = 64;
+  return rows_per_block < 64 ? 64 : rows_per_block;
+}
+
+int relu_bwd_dbias_parts(int M, int N) {
+  const int rpb = relu_bwd_dbias_rows(M, N);
+  return (M + rpb - 1) / rpb;
+}
+
+hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* part, unsigned* cnt, void* db, bool db_bf16,
+                          int M, int N, hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int ncg = (N / 8 + 31) / 32;
+  const int rows_per_block = relu_bwd_dbias_rows(M, N);
   dim3 grid((M + rows_per_block - 1) / rows_per_block, ncg);
   hipLaunchKernelGGL(relu_bwd_dbias_kernel, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dy),
-                     static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dz), dbias, M, N, rows_per_block);
+                     static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dz), part, cnt,
+                     db_bf16 ? static_cast<bf16_t*>(db) : nullptr, db_bf16 ? nullptr : static_cast<float*>(db), M, N,
+                     rows_per_block);
   return hipGetLastError();
 }
 

@@ -173,12 +173,20 @@ hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32
 // ---- ctr.hip (XDLJob CTR model: MFMA GEMM, embeddings, sparse Adagrad)
 hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, bool relu,
                          hipStream_t s);
-hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* dbias, int M, int N, hipStream_t s);
-hipError_t head_bce_fwd(const void* x, const void* w, const float* b, const float* y, int M, int K, float* logit,
-                        float* dlogit, float* loss_part, hipStream_t s);
+// part: relu_bwd_dbias_parts(M, N) x [N] fp32 scratch; cnt: (N + 255) / 256 counters,
+// zero before the first call (the kernel re-arms them); db: [N] bf16 (db_bf16) or fp32
+int relu_bwd_dbias_parts(int M, int N);
+hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* part, unsigned* cnt, void* db, bool db_bf16,
+                          int M, int N, hipStream_t s);
+// cnt: one ticket counter, zero before the first call (re-armed by the kernel);
+// loss [1] fp32 = the mean loss; b: bf16 (b_bf16) or fp32 [1]
+hipError_t head_bce_fwd(const void* x, const void* w, const void* b, bool b_bf16, const float* y, int M, int K,
+                        float* logit, float* dlogit, float* loss_part, unsigned* cnt, float* loss, hipStream_t s);
 int head_bce_bwd_blocks(int M);
+// dw / db (bf16 [K] / [1], optional): the partials summed in block order by the last block
 hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
-                        int K, void* dx, float* dw_part, float* db_part, hipStream_t s);
+                        int K, void* dx, float* dw_part, float* db_part, unsigned* cnt, void* dw, void* db,
+                        hipStream_t s);
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s);
 // ucount (optional): the live segment count on the device; U is then a capacity

@@ -55,7 +55,8 @@ class _FusedLinearFn(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         ext = _ext.load()
         dy = dy.contiguous()
-        dz, db = ext.relu_bwd_dbias(dy, y if ctx.relu else None)
+        # db straight in the parameter dtype (bf16): no zero-fill, no conversion launch
+        dz, db = ext.relu_bwd_dbias(dy, y if ctx.relu else None, w.dtype == torch.bfloat16)
         fout, fin = w.shape
         # dx = dz . W on the same MFMA kernel as the forward (B operand = W^T rows)
         dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
@@ -69,7 +70,7 @@ class _FusedLinearFn(torch.autograd.Function):
             ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1)
         else:
             dw = (dz.t() @ x).to(w.dtype)
-        return dx, dw, (db.to(w.dtype) if ctx.has_b else None), None
+        return dx, dw, ((db if db.dtype == w.dtype else db.to(w.dtype)) if ctx.has_b else None), None
 
 
 _WS = {}
@@ -100,22 +101,25 @@ class _HeadBCEFn(torch.autograd.Function):
     def forward(ctx, x, w, b, y):
         ext = _ext.load()
         x = x.contiguous()
-        logit, dlogit, part = ext.head_bce_fwd(x, w.reshape(-1).contiguous(), b.float().reshape(1),
-                                               y.float().contiguous())
+        bb = b.reshape(1) if b.dtype in (torch.bfloat16, torch.float32) else b.float().reshape(1)
+        # the kernel's last block folds the per-block losses into the mean (no reduce launch)
+        logit, dlogit, _part, loss = ext.head_bce_fwd(x, w.reshape(-1).contiguous(), bb.contiguous(),
+                                                      y.float().contiguous())
         ctx.save_for_backward(x, w, dlogit)
         ctx.b_dtype = b.dtype
         ctx.mark_non_differentiable(logit)
-        return part.sum() / x.shape[0], logit
+        return loss.view(()), logit
 
     @staticmethod
     def backward(ctx, gloss, _glogit):
         x, w, dlogit = ctx.saved_tensors
         ext = _ext.load()
-        dx, dw_part, db_part = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0],
-                                                gloss.float().reshape(1).contiguous())
-        # per-block partials summed in a fixed order (deterministic)
-        dw = dw_part.sum(0).to(w.dtype).reshape(w.shape)
-        db = db_part.sum().to(ctx.b_dtype).reshape(1)
+        # dW / db summed over the per-block partials in a fixed order by the kernel's
+        # last block (deterministic), already bf16
+        dx, dw, db, _dwp, _dbp = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0],
+                                                  gloss.float().reshape(1).contiguous())
+        dw = dw.reshape(w.shape) if w.dtype == dw.dtype else dw.to(w.dtype).reshape(w.shape)
+        db = db if ctx.b_dtype == db.dtype else db.to(ctx.b_dtype)
         return dx, dw, db, None
 
 

@@ -273,6 +273,12 @@ def test_relu_bwd_dbias_matches_fp32(M, N, relu):
     if relu:
         torch.testing.assert_close(dz.float(), ref, atol=0, rtol=0)
     torch.testing.assert_close(db.float(), ref.sum(0), atol=5e-2, rtol=1e-3)
+    # deterministic (fixed-order partial sums, no atomics on the result), and the bf16 output
+    # is the fp32 one rounded once
+    _, db2 = ext.relu_bwd_dbias(dy, y if relu else None)
+    assert torch.equal(db, db2)
+    _, db16 = ext.relu_bwd_dbias(dy, y if relu else None, True)
+    assert db16.dtype == torch.bfloat16 and torch.equal(db16, db.bfloat16())
 
 
 @pytest.mark.gpu
