@@ -180,6 +180,21 @@ __device__ __forceinline__ uint4 f8_to_u4(const float (&o)[8]) {
   return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
 }
 
+// Sum of part[r * stride] for r in [0, n), in r order; 16 loads in flight per
+// round (one dependent load per partial made the last block's sum the
+// kernel's critical path: 64 partials x L2 latency)
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ part, int n, int64_t stride) {
+  float a = 0.f;
+  for (int r0 = 0; r0 < n; r0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = r0 + j < n ? part[static_cast<int64_t>(r0 + j) * stride] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a += v[j];
+  }
+  return a;
+}
+
 // Row-block partial column sums go to part[blockIdx.x][N]; the last block of a
 // column block to arrive (agent-scope release + ticket; acquire in the
 // reducer: the in-launch split reduction of cdna_hip_programming.md) sums them
@@ -259,8 +274,7 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
   __syncthreads();
   if (!last) return;
   if (col < N) {
-    float a = 0.f;
-    for (int r = 0; r < static_cast<int>(gridDim.x); ++r) a += part[static_cast<int64_t>(r) * N + col];
+    const float a = ordered_sum(part + col, static_cast<int>(gridDim.x), N);
     if (db16) db16[col] = f32_to_bf16(a);
     else db32[col] = a;
   }
@@ -500,13 +514,11 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
   __syncthreads();
   if (!last) return;
   for (int k = threadIdx.x; k < K; k += 256) {
-    float t = 0.f;
-    for (int r = 0; r < static_cast<int>(gridDim.x); ++r) t += dw_part[static_cast<int64_t>(r) * K + k];
+    const float t = ordered_sum(dw_part + k, static_cast<int>(gridDim.x), K);
     dw[k] = f32_to_bf16(t);
   }
   if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int r = 0; r < static_cast<int>(gridDim.x); ++r) t += db_part[r];
+    const float t = ordered_sum(db_part, static_cast<int>(gridDim.x), 1);
     db[0] = f32_to_bf16(t);
     __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
