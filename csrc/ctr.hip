@@ -302,49 +302,85 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__
   }
 }
 
+// 4 consecutive elements -> fp32: one 8-B (bf16) / 16-B (fp32) load when V4
+// (row base and column aligned, host-checked), else element by element up to n
+template <typename T, bool V4>
+__device__ __forceinline__ void ld4(const T* p, int n, float (&o)[4]) {
+  if constexpr (V4) {
+    if constexpr (sizeof(T) == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      o[0] = __uint_as_float(v.x << 16);
+      o[1] = __uint_as_float(v.x & 0xffff0000u);
+      o[2] = __uint_as_float(v.y << 16);
+      o[3] = __uint_as_float(v.y & 0xffff0000u);
+    } else {
+      const float4 v = *reinterpret_cast<const float4*>(p);
+      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = k < n ? Vec1<T>::ld(p + k) : 0.f;
+  }
+}
+
 // Row j = b*F + f of a [B, ld] activation-gradient matrix lives at
 // rows + b*ld + col0 + f*D (the layout embed_gather wrote).  Rows order[j]
-// are summed per segment [seg[u], seg[u+1]); one wave per segment.
+// are summed per segment [seg[u], seg[u+1]), in j order, by a group of G =
+// 2^lg lanes (G*4 >= D when D <= 256: a wave per segment left 48 of 64 lanes
+// idle at D = 64), two rows' loads in flight per step.
 // ``ucount`` (optional): the live segment count on the device (U is then the
 // capacity the grid was sized for) -- no host round trip for data-dependent U.
-template <typename T>
+template <typename T, bool V4>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, int ld, int col0,
                                                              const int64_t* __restrict__ order,
-                                                             const int64_t* __restrict__ seg, int U, int D,
+                                                             const int64_t* __restrict__ seg, int U, int D, int lg,
                                                              float* __restrict__ out, const int* __restrict__ ucount) {
-  const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
   if (u >= (ucount ? *ucount : U)) return;
   const int64_t s0 = seg[u], s1 = seg[u + 1];
-  for (int c = lane * 4; c < D; c += 256) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int64_t j = s0; j < s1; ++j) {
-      const int64_t jj = order[j];
-      const T* r = rows + (jj / F) * static_cast<int64_t>(ld) + col0 + (jj % F) * D + c;
-      a0 += Vec1<T>::ld(r);
-      if (c + 1 < D) a1 += Vec1<T>::ld(r + 1);
-      if (c + 2 < D) a2 += Vec1<T>::ld(r + 2);
-      if (c + 3 < D) a3 += Vec1<T>::ld(r + 3);
+  for (int c = gl * 4; c < D; c += 4 << lg) {
+    const int n = D - c < 4 ? D - c : 4;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t j = s0;
+    for (; j + 1 < s1; j += 2) {
+      const int64_t j0 = order[j], j1 = order[j + 1];
+      float v0[4], v1[4];
+      ld4<T, V4>(rows + (j0 / F) * static_cast<int64_t>(ld) + col0 + (j0 % F) * D + c, n, v0);
+      ld4<T, V4>(rows + (j1 / F) * static_cast<int64_t>(ld) + col0 + (j1 % F) * D + c, n, v1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = (a[k] + v0[k]) + v1[k];
+    }
+    if (j < s1) {
+      const int64_t j0 = order[j];
+      float v0[4];
+      ld4<T, V4>(rows + (j0 / F) * static_cast<int64_t>(ld) + col0 + (j0 % F) * D + c, n, v0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += v0[k];
     }
     float* o = out + static_cast<int64_t>(u) * D + c;
-    o[0] = a0;
-    if (c + 1 < D) o[1] = a1;
-    if (c + 2 < D) o[2] = a2;
-    if (c + 3 < D) o[3] = a3;
+    if (V4) {
+      *reinterpret_cast<float4*>(o) = make_float4(a[0], a[1], a[2], a[3]);
+    } else {
+      for (int k = 0; k < n; ++k) o[k] = a[k];
+    }
   }
 }
 
 // Owner side: sum the received gradient rows of each unique local row and
-// apply Adagrad in place: acc += g^2; w -= lr * g / (sqrt(acc) + eps).
+// apply Adagrad in place: acc += g^2; w -= lr * g / (sqrt(acc) + eps).  Same
+// lane groups as segment_reduce_kernel; V4 when D % 4 == 0 (all rows 16-B aligned).
+template <bool V4>
 __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __restrict__ grads,
                                                               const int64_t* __restrict__ order,
                                                               const int64_t* __restrict__ seg,
                                                               const int64_t* __restrict__ rows_local, int U, int D,
-                                                              float* __restrict__ table, float* __restrict__ accum,
-                                                              float lr, float eps, float scale,
-                                                              const int* __restrict__ ucount, int64_t nrows) {
-  const int u = (blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+                                                              int lg, float* __restrict__ table,
+                                                              float* __restrict__ accum, float lr, float eps,
+                                                              float scale, const int* __restrict__ ucount,
+                                                              int64_t nrows) {
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
   if (u >= (ucount ? *ucount : U)) return;
   const int64_t s0 = seg[u], s1 = seg[u + 1];
   const int64_t row = rows_local[u];
@@ -353,21 +389,40 @@ __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __res
   if (row < 0 || row >= nrows) return;
   float* w = table + row * static_cast<int64_t>(D);
   float* a = accum + row * static_cast<int64_t>(D);
-  for (int c = lane * 4; c < D; c += 256) {
-    float g[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t j = s0; j < s1; ++j) {
-      const float* r = grads + order[j] * static_cast<int64_t>(D) + c;
+  for (int c = gl * 4; c < D; c += 4 << lg) {
+    const int n = D - c < 4 ? D - c : 4;
+    float wv[4], av[4], g[4] = {0.f, 0.f, 0.f, 0.f};
+    ld4<float, V4>(w + c, n, wv);  // issued before the gradient rows
+    ld4<float, V4>(a + c, n, av);
+    int64_t j = s0;
+    for (; j + 1 < s1; j += 2) {
+      const int64_t j0 = order[j], j1 = order[j + 1];
+      float v0[4], v1[4];
+      ld4<float, V4>(grads + j0 * static_cast<int64_t>(D) + c, n, v0);
+      ld4<float, V4>(grads + j1 * static_cast<int64_t>(D) + c, n, v1);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (c + k < D) g[k] += r[k];
+      for (int k = 0; k < 4; ++k) g[k] = (g[k] + v0[k]) + v1[k];
+    }
+    if (j < s1) {
+      float v0[4];
+      ld4<float, V4>(grads + order[j] * static_cast<int64_t>(D) + c, n, v0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] += v0[k];
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (c + k >= D) continue;
       const float gk = g[k] * scale;
-      const float ak = a[c + k] + gk * gk;
-      a[c + k] = ak;
-      w[c + k] -= lr * gk / (sqrtf(ak) + eps);
+      av[k] += gk * gk;
+      wv[k] -= lr * gk / (sqrtf(av[k]) + eps);
+    }
+    if (V4) {
+      *reinterpret_cast<float4*>(a + c) = make_float4(av[0], av[1], av[2], av[3]);
+      *reinterpret_cast<float4*>(w + c) = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    } else {
+      for (int k = 0; k < n; ++k) {
+        a[c + k] = av[k];
+        w[c + k] = wv[k];
+      }
     }
   }
 }
@@ -614,16 +669,32 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
   return hipGetLastError();
 }
 
+// lanes per segment: the power of two G with G*4 >= D (capped at a wave)
+static int seg_lanes_log2(int D) {
+  int lg = 0;
+  while (lg < 6 && (4 << lg) < D) ++lg;
+  return lg;
+}
+
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
                           const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount) {
   if (U <= 0) return hipSuccess;
-  dim3 grid((U + 3) / 4);
-  if (dtype == 1)
-    hipLaunchKernelGGL((segment_reduce_kernel<bf16_t>), grid, dim3(256), 0, s, static_cast<const bf16_t*>(rows), F,
-                       ld, col0, order, seg, U, D, out, ucount);
-  else
-    hipLaunchKernelGGL((segment_reduce_kernel<float>), grid, dim3(256), 0, s, static_cast<const float*>(rows), F, ld,
-                       col0, order, seg, U, D, out, ucount);
+  const int lg = seg_lanes_log2(D);
+  dim3 grid(static_cast<unsigned>((static_cast<int64_t>(U) << lg) + 255) / 256);
+  const size_t esz = dtype == 1 ? 2 : 4;
+  const bool v4 = D % 4 == 0 && ld % 4 == 0 && col0 % 4 == 0 && reinterpret_cast<uintptr_t>(rows) % (4 * esz) == 0 &&
+                  reinterpret_cast<uintptr_t>(out) % 16 == 0;
+#define KDL_SEGRED(T, V)                                                                                      \
+  hipLaunchKernelGGL((segment_reduce_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, ld, \
+                     col0, order, seg, U, D, lg, out, ucount)
+  if (dtype == 1) {
+    if (v4) KDL_SEGRED(bf16_t, true);
+    else KDL_SEGRED(bf16_t, false);
+  } else {
+    if (v4) KDL_SEGRED(float, true);
+    else KDL_SEGRED(float, false);
+  }
+#undef KDL_SEGRED
   return hipGetLastError();
 }
 
@@ -631,8 +702,16 @@ hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64
                            int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,
                            hipStream_t s, const int* ucount) {
   if (U <= 0) return hipSuccess;
-  hipLaunchKernelGGL(segment_adagrad_kernel, dim3((U + 3) / 4), dim3(256), 0, s, grads, order, seg, rows_local, U, D,
-                     table, accum, lr, eps, scale, ucount, nrows);
+  const int lg = seg_lanes_log2(D);
+  dim3 grid(static_cast<unsigned>((static_cast<int64_t>(U) << lg) + 255) / 256);
+  const bool v4 = D % 4 == 0 && reinterpret_cast<uintptr_t>(grads) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(table) % 16 == 0 && reinterpret_cast<uintptr_t>(accum) % 16 == 0;
+  if (v4)
+    hipLaunchKernelGGL(segment_adagrad_kernel<true>, grid, dim3(256), 0, s, grads, order, seg, rows_local, U, D, lg,
+                       table, accum, lr, eps, scale, ucount, nrows);
+  else
+    hipLaunchKernelGGL(segment_adagrad_kernel<false>, grid, dim3(256), 0, s, grads, order, seg, rows_local, U, D, lg,
+                       table, accum, lr, eps, scale, ucount, nrows);
   return hipGetLastError();
 }
 

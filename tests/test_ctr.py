@@ -306,11 +306,14 @@ def test_head_bce_matches_fp32(M, K):
 
 
 @pytest.mark.gpu
-def test_embedding_kernels_match_torch():
+@pytest.mark.parametrize("D,col0,dt", [(64, 0, torch.bfloat16), (13, 0, torch.bfloat16), (300, 4, torch.float32),
+                                       (64, 2, torch.bfloat16), (8, 0, torch.float32)])
+def test_embedding_kernels_match_torch(D, col0, dt):
+    """Lane groups of G = pow2(D/4) per segment; vector (aligned) and scalar paths."""
     from kubedl_amd.ops import _ext
     ext = _ext.load()
     torch.manual_seed(0)
-    V, D, B, F = 1000, 64, 333, 7
+    V, B, F = 1000, 333, 7
     table = torch.randn(V, D, device="cuda")
     idx = torch.randint(0, V, (B * F,), device="cuda")
     out = torch.zeros(B, F * D + 32, device="cuda")
@@ -321,9 +324,10 @@ def test_embedding_kernels_match_torch():
     order = torch.argsort(inv, stable=True)
     seg = torch.zeros(len(uniq) + 1, dtype=torch.int64, device="cuda")
     seg[1:] = torch.cumsum(torch.bincount(inv, minlength=len(uniq)), 0)
-    gx = torch.randn(B, F * D + 32, device="cuda").bfloat16()
-    got = ext.segment_reduce(gx, F, 0, D, order, seg, None)
-    ref = torch.zeros(len(uniq), D, device="cuda").index_add_(0, inv, gx[:, : F * D].reshape(B * F, D).float())
+    gx = torch.randn(B, col0 + F * D + 32, device="cuda").to(dt)
+    got = ext.segment_reduce(gx, F, col0, D, order, seg, None)
+    ref = torch.zeros(len(uniq), D, device="cuda").index_add_(
+        0, inv, gx[:, col0: col0 + F * D].reshape(B * F, D).float())
     torch.testing.assert_close(got, ref, atol=1e-3, rtol=1e-3)
     # fused segment-sum + Adagrad
     tab = torch.randn(V, D, device="cuda")
