@@ -472,16 +472,20 @@ at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::op
   TORCH_CHECK(a.is_contiguous() && w.is_contiguous(), "gemm_bias_act: contiguous operands");
   TORCH_CHECK(a.size(1) % 8 == 0, "gemm_bias_act: K must be a multiple of 8 (16-byte rows)");
   const int64_t M = a.size(0), N = w.size(0), K = a.size(1);
-  const float* bp = nullptr;
+  // bias read in its own dtype (bf16 or fp32): no conversion launch
+  const void* bp = nullptr;
+  bool b16 = false;
   at::Tensor b;
   if (bias.has_value() && bias->defined()) {
-    b = bias->to(at::kFloat).contiguous();
-    TORCH_CHECK(b.numel() == N, "gemm_bias_act: bias size");
-    bp = b.data_ptr<float>();
+    b = bias->scalar_type() == at::kBFloat16 || bias->scalar_type() == at::kFloat ? bias->contiguous()
+                                                                                   : bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b.is_cuda() && b.numel() == N, "gemm_bias_act: bias size");
+    b16 = b.scalar_type() == at::kBFloat16;
+    bp = b.data_ptr();
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   auto c = at::empty({M, N}, a.options());
-  check_hip(kdl::gemm_bias_act(a.data_ptr(), w.data_ptr(), bp, c.data_ptr(), static_cast<int>(M),
+  check_hip(kdl::gemm_bias_act(a.data_ptr(), w.data_ptr(), bp, b16, c.data_ptr(), static_cast<int>(M),
                                static_cast<int>(N), static_cast<int>(K), relu, cur_stream()),
             "gemm_bias_act");
   return c;
@@ -1493,6 +1497,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
   m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b)");
+  m.def("set_ctr_tile", &kdl::set_ctr_tile, "gemm_bias_act tile: -1 by shape, 0/1/2 = 128x128 / 128x64 / 64x64");
+  m.def("ctr_tile_for", &kdl::ctr_tile_for, "the gemm_bias_act tile picked for an M x N output");
   m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient (deterministic; bf16 or fp32)",
         py::arg("dy"), py::arg("y"), py::arg("db_bf16") = false);
   m.def("head_bce_fwd", &head_bce_fwd, "1-wide logit layer + sigmoid BCE: (logit, dlogit, per-block loss sums)");

@@ -28,6 +28,7 @@
 //   order by the caller) -- no vendor GEMM for the N=1 layer.
 #include "common.h"
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace kdl {
 namespace {
@@ -35,23 +36,26 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BK = 64;
 constexpr int LDA = BK + 8;  // padded LDS row (bf16 elements)
 constexpr int kThreads = 256;
 
-__device__ __forceinline__ uint4 ld16_or_zero(const bf16_t* p, bool ok) {
-  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-}
-
-template <bool RELU, bool HAS_BIAS>
+// BM_ x BN_ tile (128x128, 128x64 or 64x64): 4 waves as 2x2, each wave
+// (BM_/2) x (BN_/2) = I x J MFMA 32x32 blocks.  A 4096-row batch gives a
+// 128x128 tiling only 64-256 tiles on 256 CUs (one wave per SIMD, nothing to
+// hide the LDS and barrier latency); the smaller tiles trade MFMA-per-LDS-read
+// for two or more resident blocks per CU (the host picks, gemm_bias_act).
+template <bool RELU, int BM_, int BN_>
 __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
-    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, const float* __restrict__ bias,
-    bf16_t* __restrict__ C, int M, int N, int K, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][BM * LDA];  // [buf][A|B][rows*LDA]
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, const float* __restrict__ bias32,
+    const bf16_t* __restrict__ bias16, bf16_t* __restrict__ C, int M, int N, int K, int tiles_n) {
+  constexpr int I = BM_ / 64, J = BN_ / 64;
+  constexpr int SA = BM_ / 32, SB = BN_ / 32;  // 16-B chunks per thread per k-tile (rows x 8 chunks / 256)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][(BM_ + BN_) * LDA];  // [buf][A rows | B rows]
   // block -> (tile_m, tile_n): groups of 8 N-tiles share one A panel
   const int bid = blockIdx.x;
   const int group = 8;
-  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_m = (M + BM_ - 1) / BM_;
   const int per_group = group * tiles_m;
   const int g = bid / per_group;
   const int first_n = g * group;
@@ -59,57 +63,60 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
   const int in_g = bid % per_group;
   const int tile_m = in_g / gsize;
   const int tile_n = first_n + in_g % gsize;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int m0 = tile_m * BM_, n0 = tile_n * BN_;
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave >> 1) * (BM_ / 2), wn = (wave & 1) * (BN_ / 2);
 
-  // staging: each thread moves 4 x 16 B of A and of B per k-tile
-  // (128 rows x 8 chunks = 1024 chunks / 256 threads)
-  int srow[4], schunk[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cidx = t + i * kThreads;
-    srow[i] = cidx >> 3;
-    schunk[i] = cidx & 7;
-  }
-  uint4 ra[4], rb[4];
+  uint4 ra[SA], rb[SB];
   const int nk = (K + BK - 1) / BK;
 
   // Loads are unconditional (no load behind an exec branch, which makes hipcc
   // drain vmcnt before the next tile's MFMAs): rows past M / N re-read row 0
   // (their outputs are never stored), and K-tail chunks re-read chunk 0 and are
   // zeroed when staged (they would otherwise feed valid outputs).
-  uint32_t kok = 0;
+  uint32_t koka = 0, kokb = 0;
   auto gload = [&](int kt) {
     const int k0 = kt * BK;
-    kok = 0;
+    koka = kokb = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kk = k0 + schunk[i] * 8;
+    for (int i = 0; i < SA; ++i) {
+      const int cidx = t + i * kThreads, row = cidx >> 3, kk = k0 + (cidx & 7) * 8;
       const bool kin = kk < K;
-      kok |= kin ? (1u << i) : 0u;
-      const int kc = kin ? kk : 0;
-      const int am = m0 + srow[i] < M ? m0 + srow[i] : 0, bn = n0 + srow[i] < N ? n0 + srow[i] : 0;
-      ra[i] = *reinterpret_cast<const uint4*>(A + static_cast<int64_t>(am) * K + kc);
-      rb[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(bn) * K + kc);
+      koka |= kin ? (1u << i) : 0u;
+      const int am = m0 + row < M ? m0 + row : 0;
+      ra[i] = *reinterpret_cast<const uint4*>(A + static_cast<int64_t>(am) * K + (kin ? kk : 0));
+    }
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const int cidx = t + i * kThreads, row = cidx >> 3, kk = k0 + (cidx & 7) * 8;
+      const bool kin = kk < K;
+      kokb |= kin ? (1u << i) : 0u;
+      const int bn = n0 + row < N ? n0 + row : 0;
+      rb[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(bn) * K + (kin ? kk : 0));
     }
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool kin = (kok >> i) & 1u;
-      *reinterpret_cast<uint4*>(&lds[buf][0][srow[i] * LDA + schunk[i] * 8]) = kin ? ra[i] : make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(&lds[buf][1][srow[i] * LDA + schunk[i] * 8]) = kin ? rb[i] : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < SA; ++i) {
+      const int cidx = t + i * kThreads;
+      *reinterpret_cast<uint4*>(&lds[buf][(cidx >> 3) * LDA + (cidx & 7) * 8]) =
+          (koka >> i) & 1u ? ra[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const int cidx = t + i * kThreads;
+      *reinterpret_cast<uint4*>(&lds[buf][(BM_ + (cidx >> 3)) * LDA + (cidx & 7) * 8]) =
+          (kokb >> i) & 1u ? rb[i] : make_uint4(0, 0, 0, 0);
     }
   };
 
-  f32x16_t acc[2][2];
+  f32x16_t acc[I][J];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < I; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < J; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -122,21 +129,22 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     if (kt + 1 < nk) gload(kt + 1);
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
-      bf16x8_t af[2], bfr[2];
+      bf16x8_t af[I], bfr[J];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&lds[cur][0][(wm + i * 32 + fr) * LDA + s * 16 + fh * 8]);
+      for (int i = 0; i < I; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&lds[cur][(wm + i * 32 + fr) * LDA + s * 16 + fh * 8]);
         af[i] = __builtin_bit_cast(bf16x8_t, v);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&lds[cur][1][(wn + j * 32 + fr) * LDA + s * 16 + fh * 8]);
+      for (int j = 0; j < J; ++j) {
+        const uint4 v =
+            *reinterpret_cast<const uint4*>(&lds[cur][(BM_ + wn + j * 32 + fr) * LDA + s * 16 + fh * 8]);
         bfr[j] = __builtin_bit_cast(bf16x8_t, v);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < I; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < J; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     // buf cur^1 was last read in iteration kt-1, which ended with a barrier
@@ -145,12 +153,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
   }
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < J; ++j) {
     const int col = n0 + wn + j * 32 + fr;
     float bv = 0.f;
-    if (HAS_BIAS && col < N) bv = bias[col];
+    if (col < N) bv = bias32 ? bias32[col] : bias16 ? bf16_to_f32(bias16[col]) : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < I; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
@@ -609,23 +617,45 @@ hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float
   return hipGetLastError();
 }
 
-hipError_t gemm_bias_act(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, bool relu,
-                         hipStream_t s) {
+static int g_ctr_tile = -2;  // -2: KDL_TUNE ctr_tile, -1: by shape, 0/1/2: 128x128 / 128x64 / 64x64
+
+void set_ctr_tile(int t) { g_ctr_tile = t; }
+
+// the largest tile with >= 2 blocks per CU (512 tiles), else the smallest
+int ctr_tile_for(int M, int N) {
+  if (g_ctr_tile == -2) g_ctr_tile = tune_int("ctr_tile", -1);
+  if (g_ctr_tile >= 0) return g_ctr_tile;
+  const int bm[3] = {128, 128, 64}, bn[3] = {128, 64, 64};
+  for (int c = 0; c < 3; ++c)
+    if (static_cast<int64_t>((M + bm[c] - 1) / bm[c]) * ((N + bn[c] - 1) / bn[c]) >= 512) return c;
+  return 2;
+}
+
+hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bias_bf16, void* C, int M, int N, int K,
+                         bool relu, hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
-  dim3 grid(tiles_n * tiles_m);
   auto a = static_cast<const bf16_t*>(A);
   auto b = static_cast<const bf16_t*>(B);
   auto c = static_cast<bf16_t*>(C);
-  if (relu && bias)
-    hipLaunchKernelGGL((gemm_bias_act_kernel<true, true>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K, tiles_n);
-  else if (relu)
-    hipLaunchKernelGGL((gemm_bias_act_kernel<true, false>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K, tiles_n);
-  else if (bias)
-    hipLaunchKernelGGL((gemm_bias_act_kernel<false, true>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K, tiles_n);
-  else
-    hipLaunchKernelGGL((gemm_bias_act_kernel<false, false>), grid, dim3(kThreads), 0, s, a, b, bias, c, M, N, K,
-                       tiles_n);
+  const float* b32 = bias_bf16 ? nullptr : static_cast<const float*>(bias);
+  const bf16_t* b16 = bias_bf16 ? static_cast<const bf16_t*>(bias) : nullptr;
+  const int cfg = ctr_tile_for(M, N);
+#define KDL_GBA(R, TM, TN)                                                                                 \
+  do {                                                                                                     \
+    const int tn = (N + TN - 1) / TN, tm = (M + TM - 1) / TM;                                              \
+    hipLaunchKernelGGL((gemm_bias_act_kernel<R, TM, TN>), dim3(tn * tm), dim3(kThreads), 0, s, a, b, b32, b16, c, \
+                       M, N, K, tn);                                                                       \
+  } while (0)
+  if (relu) {
+    if (cfg == 0) KDL_GBA(true, 128, 128);
+    else if (cfg == 1) KDL_GBA(true, 128, 64);
+    else KDL_GBA(true, 64, 64);
+  } else {
+    if (cfg == 0) KDL_GBA(false, 128, 128);
+    else if (cfg == 1) KDL_GBA(false, 128, 64);
+    else KDL_GBA(false, 64, 64);
+  }
+#undef KDL_GBA
   return hipGetLastError();
 }
 

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""gemm_bias_act (csrc/ctr.hip) at each tile shape on the CTR tower's GEMMs
+(batch 4096, tower 1728 -> 1024 -> 512 -> 256: forward C = X W^T and data
+gradient dX = dZ W), alone on the GPU.  One JSON line per (shape, tile);
+the ``auto`` row is the tile ctr_tile_for picks."""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+from kubedl_amd.ops import _ext  # noqa: E402
+
+B = 4096
+SHAPES = [("fwd1", B, 1024, 1728), ("fwd2", B, 512, 1024), ("fwd3", B, 256, 512),
+          ("dx1", B, 1728, 1024), ("dx2", B, 1024, 512), ("dx3", B, 512, 256)]
+
+
+def main() -> int:
+    ext = _ext.load()
+    torch.manual_seed(0)
+    for name, M, N, K in SHAPES:
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+        b = torch.randn(N, device="cuda").bfloat16()
+        for tile in (0, 1, 2, -1):
+            ext.set_ctr_tile(tile)
+            for _ in range(5):
+                ext.gemm_bias_act(a, w, b, True)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                ext.gemm_bias_act(a, w, b, True)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / 50
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K,
+                              "tile": ["128x128", "128x64", "64x64"][ext.ctr_tile_for(M, N)] if tile < 0 else
+                              ["128x128", "128x64", "64x64"][tile], "auto": tile < 0, "us": round(us, 2),
+                              "tflops": round(2.0 * M * N * K / us / 1e6, 1)}), flush=True)
+        ext.set_ctr_tile(-1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -227,17 +227,27 @@ def test_ctr_exchange_overflow_counted_and_capacity_grows():
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 72), (4096, 1024, 1680), (1, 128, 64)])
 @pytest.mark.parametrize("relu", [True, False])
-def test_gemm_bias_act_matches_fp32(M, N, K, relu):
+@pytest.mark.parametrize("tile", [0, 1, 2])
+def test_gemm_bias_act_matches_fp32(M, N, K, relu, tile):
+    """Every tile shape (128x128 / 128x64 / 64x64), fp32 and bf16 bias, ragged M/N/K."""
     from kubedl_amd.ops import _ext
+    ext = _ext.load()
     torch.manual_seed(0)
     a = torch.randn(M, K, device="cuda").bfloat16()
     w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
     b = torch.randn(N, device="cuda")
-    y = _ext.load().gemm_bias_act(a, w, b, relu)
+    ext.set_ctr_tile(tile)
+    try:
+        y = ext.gemm_bias_act(a, w, b, relu)
+        y16 = ext.gemm_bias_act(a, w, b.bfloat16(), relu)
+    finally:
+        ext.set_ctr_tile(-1)
     ref = a.float() @ w.float().t() + b
+    ref16 = a.float() @ w.float().t() + b.bfloat16().float()
     if relu:
-        ref = ref.relu()
+        ref, ref16 = ref.relu(), ref16.relu()
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(y16.float(), ref16, atol=3e-2, rtol=2e-2)
 
 
 @pytest.mark.gpu
