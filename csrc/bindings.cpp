@@ -465,14 +465,18 @@ at::Tensor gbdt_route(const at::Tensor& bins, const at::Tensor& rows, const at::
 }
 
 // ------------------------------------------------------------------ CTR
-at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool relu) {
+at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool relu,
+                         bool trans_w) {
   TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
               "gemm_bias_act: bf16 GPU operands");
-  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "gemm_bias_act: A [M,K], W [N,K]");
+  // trans_w: C = A W with W [K, N] (the data gradient through an nn.Linear weight), else C = A W^T, W [N, K]
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(trans_w ? 0 : 1),
+              trans_w ? "gemm_bias_act: A [M,K], W [K,N]" : "gemm_bias_act: A [M,K], W [N,K]");
   TORCH_CHECK(a.is_contiguous() && w.is_contiguous(), "gemm_bias_act: contiguous operands");
   TORCH_CHECK(a.size(1) % 8 == 0, "gemm_bias_act: K must be a multiple of 8 (16-byte rows)");
-  const int64_t M = a.size(0), N = w.size(0), K = a.size(1);
-  // bias read in its own dtype (bf16 or fp32): no conversion launch
+  const int64_t M = a.size(0), N = w.size(trans_w ? 1 : 0), K = a.size(1);
+  TORCH_CHECK(!trans_w || N % 8 == 0, "gemm_bias_act: W [K, N] needs N % 8 == 0");
+// bias read in its own dtype (bf16 or fp32): no conversion launch
   const void* bp = nullptr;
   bool b16 = false;
   at::Tensor b;
@@ -486,7 +490,7 @@ at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::op
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   auto c = at::empty({M, N}, a.options());
   check_hip(kdl::gemm_bias_act(a.data_ptr(), w.data_ptr(), bp, b16, c.data_ptr(), static_cast<int>(M),
-                               static_cast<int>(N), static_cast<int>(K), relu, cur_stream()),
+                               static_cast<int>(N), static_cast<int>(K), relu, trans_w, cur_stream()),
             "gemm_bias_act");
   return c;
 }
@@ -1496,7 +1500,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
-  m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b)");
+  m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b) (trans_w: A W, W [K, N])",
+        py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("trans_w") = false);
   m.def("set_ctr_tile", &kdl::set_ctr_tile, "gemm_bias_act tile: -1 by shape, 0/1/2 = 128x128 / 128x64 / 64x64");
   m.def("ctr_tile_for", &kdl::ctr_tile_for, "the gemm_bias_act tile picked for an M x N output");
   m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient (deterministic; bf16 or fp32)",

@@ -35,6 +35,18 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+// ds_read_b64_tr_b16: per 16-lane group a 4-row x 16-column block, lane i gets
+// column i's 4 rows (device pass only: the host pass has no such builtin)
+__device__ __forceinline__ v4s_t tr_read(const bf16_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(p));
+#else
+  return v4s_t{};
+#endif
+}
 
 constexpr int BK = 64;
 constexpr int LDA = BK + 8;  // padded LDS row (bf16 elements)
@@ -45,13 +57,23 @@ constexpr int kThreads = 256;
 // 128x128 tiling only 64-256 tiles on 256 CUs (one wave per SIMD, nothing to
 // hide the LDS and barrier latency); the smaller tiles trade MFMA-per-LDS-read
 // for two or more resident blocks per CU (the host picks, gemm_bias_act).
-template <bool RELU, int BM_, int BN_>
+//
+// BT: B is [K][N] (N contiguous: the data gradient dX = dZ W reads the
+// nn.Linear weight as it is, no per-step transpose).  Its tile is staged as
+// [BK k][BN_ + 32] (16-B chunks along n, as loaded) and read with
+// ds_read_b64_tr_b16: a 32x32x16 B fragment (8 k of one n per lane) is two
+// transposed reads 4 rows apart.  Row stride 2*BN_ + 64 bytes = 64 or 192 mod 256:
+// the 4 rows of a read land on 4 distinct 16-bank quarters (conflict-free).
+template <bool RELU, int BM_, int BN_, bool BT>
 __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, const float* __restrict__ bias32,
     const bf16_t* __restrict__ bias16, bf16_t* __restrict__ C, int M, int N, int K, int tiles_n) {
   constexpr int I = BM_ / 64, J = BN_ / 64;
   constexpr int SA = BM_ / 32, SB = BN_ / 32;  // 16-B chunks per thread per k-tile (rows x 8 chunks / 256)
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2][(BM_ + BN_) * LDA];  // [buf][A rows | B rows]
+  constexpr int SBT = BN_ + 32;                // BT: B image row (elements)
+  constexpr int BOFF = BM_ * LDA;              // B image offset in a buffer
+  constexpr int BSZ = BT ? BK * SBT : BN_ * LDA;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][BOFF + BSZ];  // [buf][A rows | B image]
   // block -> (tile_m, tile_n): groups of 8 N-tiles share one A panel
   const int bid = blockIdx.x;
   const int group = 8;
@@ -90,11 +112,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     }
 #pragma unroll
     for (int i = 0; i < SB; ++i) {
-      const int cidx = t + i * kThreads, row = cidx >> 3, kk = k0 + (cidx & 7) * 8;
-      const bool kin = kk < K;
-      kokb |= kin ? (1u << i) : 0u;
-      const int bn = n0 + row < N ? n0 + row : 0;
-      rb[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(bn) * K + (kin ? kk : 0));
+      const int cidx = t + i * kThreads;
+      if constexpr (BT) {
+        // 64 k rows x BN_/8 chunks of 8 n; columns past N re-read column 0 (never stored)
+        const int kk = k0 + cidx / (BN_ / 8), n = n0 + (cidx % (BN_ / 8)) * 8;
+        const bool kin = kk < K;
+        kokb |= kin ? (1u << i) : 0u;
+        rb[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(kin ? kk : 0) * N + (n < N ? n : 0));
+      } else {
+        const int row = cidx >> 3, kk = k0 + (cidx & 7) * 8;
+        const bool kin = kk < K;
+        kokb |= kin ? (1u << i) : 0u;
+        const int bn = n0 + row < N ? n0 + row : 0;
+        rb[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(bn) * K + (kin ? kk : 0));
+      }
     }
   };
   auto swrite = [&](int buf) {
@@ -107,8 +138,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
 #pragma unroll
     for (int i = 0; i < SB; ++i) {
       const int cidx = t + i * kThreads;
-      *reinterpret_cast<uint4*>(&lds[buf][(BM_ + (cidx >> 3)) * LDA + (cidx & 7) * 8]) =
-          (kokb >> i) & 1u ? rb[i] : make_uint4(0, 0, 0, 0);
+      const int off = BT ? (cidx / (BN_ / 8)) * SBT + (cidx % (BN_ / 8)) * 8 : (cidx >> 3) * LDA + (cidx & 7) * 8;
+      *reinterpret_cast<uint4*>(&lds[buf][BOFF + off]) = (kokb >> i) & 1u ? rb[i] : make_uint4(0, 0, 0, 0);
     }
   };
 
@@ -137,9 +168,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
       }
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        const uint4 v =
-            *reinterpret_cast<const uint4*>(&lds[cur][(BM_ + wn + j * 32 + fr) * LDA + s * 16 + fh * 8]);
-        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+        if constexpr (BT) {
+          // lane 4q+p of 16-lane group g: row k = s*16 + fh*8 + q (+4), columns 16(g&1) + 4p..+3
+          const bf16_t* b = &lds[cur][BOFF + (s * 16 + fh * 8 + ((lane & 15) >> 2)) * SBT + wn + j * 32 +
+                                      ((lane >> 4) & 1) * 16 + (lane & 3) * 4];
+          const uint2 lo = __builtin_bit_cast(uint2, tr_read(b)), hi = __builtin_bit_cast(uint2, tr_read(b + 4 * SBT));
+          bfr[j] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        } else {
+          const uint4 v = *reinterpret_cast<const uint4*>(&lds[cur][BOFF + (wn + j * 32 + fr) * LDA + s * 16 + fh * 8]);
+          bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+        }
       }
 #pragma unroll
       for (int i = 0; i < I; ++i)
@@ -632,29 +670,33 @@ int ctr_tile_for(int M, int N) {
 }
 
 hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bias_bf16, void* C, int M, int N, int K,
-                         bool relu, hipStream_t s) {
+                         bool relu, bool b_kn, hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  if (b_kn && N % 8) return hipErrorInvalidValue;  // 16-B chunks along N
   auto a = static_cast<const bf16_t*>(A);
   auto b = static_cast<const bf16_t*>(B);
   auto c = static_cast<bf16_t*>(C);
   const float* b32 = bias_bf16 ? nullptr : static_cast<const float*>(bias);
   const bf16_t* b16 = bias_bf16 ? static_cast<const bf16_t*>(bias) : nullptr;
   const int cfg = ctr_tile_for(M, N);
-#define KDL_GBA(R, TM, TN)                                                                                 \
-  do {                                                                                                     \
-    const int tn = (N + TN - 1) / TN, tm = (M + TM - 1) / TM;                                              \
-    hipLaunchKernelGGL((gemm_bias_act_kernel<R, TM, TN>), dim3(tn * tm), dim3(kThreads), 0, s, a, b, b32, b16, c, \
-                       M, N, K, tn);                                                                       \
+#define KDL_GBA(R, TM, TN, T)                                                                                \
+  do {                                                                                                       \
+    const int tn = (N + TN - 1) / TN, tm = (M + TM - 1) / TM;                                                \
+    hipLaunchKernelGGL((gemm_bias_act_kernel<R, TM, TN, T>), dim3(tn * tm), dim3(kThreads), 0, s, a, b, b32, b16, \
+                       c, M, N, K, tn);                                                                      \
   } while (0)
+#define KDL_GBA_T(R, T)                 \
+  if (cfg == 0) KDL_GBA(R, 128, 128, T); \
+  else if (cfg == 1) KDL_GBA(R, 128, 64, T); \
+  else KDL_GBA(R, 64, 64, T)
   if (relu) {
-    if (cfg == 0) KDL_GBA(true, 128, 128);
-    else if (cfg == 1) KDL_GBA(true, 128, 64);
-    else KDL_GBA(true, 64, 64);
+    if (b_kn) { KDL_GBA_T(true, true); }
+    else { KDL_GBA_T(true, false); }
   } else {
-    if (cfg == 0) KDL_GBA(false, 128, 128);
-    else if (cfg == 1) KDL_GBA(false, 128, 64);
-    else KDL_GBA(false, 64, 64);
+    if (b_kn) { KDL_GBA_T(false, true); }
+    else { KDL_GBA_T(false, false); }
   }
+#undef KDL_GBA_T
 #undef KDL_GBA
   return hipGetLastError();
 }

@@ -171,8 +171,9 @@ hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32
                            int32_t* go_right, hipStream_t s);
 
 // ---- ctr.hip (XDLJob CTR model: MFMA GEMM, embeddings, sparse Adagrad)
+// b_kn: B is [K][N] (C = A B), else [N][K] (C = A B^T)
 hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bias_bf16, void* C, int M, int N, int K,
-                         bool relu, hipStream_t s);
+                         bool relu, bool b_kn, hipStream_t s);
 void set_ctr_tile(int t);  // -1 by shape, 0/1/2: 128x128 / 128x64 / 64x64 (csrc/ctr.hip)
 int ctr_tile_for(int M, int N);
 // part: relu_bwd_dbias_parts(M, N) x [N] fp32 scratch; cnt: (N + 255) / 256 counters,

@@ -58,8 +58,12 @@ class _FusedLinearFn(torch.autograd.Function):
         # db straight in the parameter dtype (bf16): no zero-fill, no conversion launch
         dz, db = ext.relu_bwd_dbias(dy, y if ctx.relu else None, w.dtype == torch.bfloat16)
         fout, fin = w.shape
-        # dx = dz . W on the same MFMA kernel as the forward (B operand = W^T rows)
-        dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
+        # dx = dz . W on the same MFMA kernel as the forward, W read as [K, N]
+        # (transposed LDS reads: no per-step W^T copy)
+        if fin % 8 == 0:
+            dx = ext.gemm_bias_act(dz, w.contiguous(), None, False, True)
+        else:
+            dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
         if fout % 64 == 0 and fin % 64 == 0:
             # dW = dz^T x: the reduction over the batch is the weight-gradient
             # form of csrc/wgrad_dma.hip (both operands row-major, LDS-DMA +

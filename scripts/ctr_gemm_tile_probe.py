@@ -24,21 +24,23 @@ def main() -> int:
     torch.manual_seed(0)
     for name, M, N, K in SHAPES:
         a = torch.randn(M, K, device="cuda").bfloat16()
-        w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
-        b = torch.randn(N, device="cuda").bfloat16()
+        # the data gradients read the nn.Linear weight [K, N] as stored (trans_w)
+        tw = name.startswith("dx")
+        w = (torch.randn(K, N, device="cuda") if tw else torch.randn(N, K, device="cuda")).div(K ** 0.5).bfloat16()
+        b = None if tw else torch.randn(N, device="cuda").bfloat16()
         for tile in (0, 1, 2, -1):
             ext.set_ctr_tile(tile)
             for _ in range(5):
-                ext.gemm_bias_act(a, w, b, True)
+                ext.gemm_bias_act(a, w, b, not tw, tw)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(50):
-                ext.gemm_bias_act(a, w, b, True)
+                ext.gemm_bias_act(a, w, b, not tw, tw)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / 50
-            print(json.dumps({"shape": name, "M": M, "N": N, "K": K,
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "trans_w": tw,
                               "tile": ["128x128", "128x64", "64x64"][ext.ctr_tile_for(M, N)] if tile < 0 else
                               ["128x128", "128x64", "64x64"][tile], "auto": tile < 0, "us": round(us, 2),
                               "tflops": round(2.0 * M * N * K / us / 1e6, 1)}), flush=True)

@@ -251,6 +251,25 @@ def test_gemm_bias_act_matches_fp32(M, N, K, relu, tile):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 72), (4096, 1680, 1024), (1, 128, 64), (130, 72, 1000)])
+@pytest.mark.parametrize("tile", [0, 1, 2])
+def test_gemm_trans_w_matches_fp32(M, N, K, tile):
+    """C = A W with W [K, N] (transposed LDS reads of the weight as stored): the
+    CTR tower's data gradient; an asymmetric W catches a row/column swap."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(1)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(K, N, device="cuda") / K ** 0.5 + torch.arange(N, device="cuda") * 1e-3).bfloat16()
+    ext.set_ctr_tile(tile)
+    try:
+        y = ext.gemm_bias_act(a, w, None, False, True)
+    finally:
+        ext.set_ctr_tile(-1)
+    torch.testing.assert_close(y.float(), a.float() @ w.float(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
 def test_fused_linear_backward_matches_autograd():
     from kubedl_amd.models.ctr import fused_linear
     torch.manual_seed(0)
