@@ -539,7 +539,10 @@ class CTRModel:
         B = ids.shape[0]
         gids = (ids + self.field_off).reshape(-1)
         emb_u, inv = self.emb.pull(gids)
-        x = torch.zeros(B, self.k_pad, dtype=self.dtype, device=self.device)
+        # every column is written below except the pad [k_in, k_pad): zero only that
+        x = torch.empty(B, self.k_pad, dtype=self.dtype, device=self.device)
+        if self.k_pad > self.k_in:
+            x[:, self.k_in:].zero_()
         emb_u_c = emb_u.to(self.dtype).contiguous()
         if self.device.type == "cuda" and _ext.available():
             _ext.load().embed_gather(emb_u_c, inv.contiguous(), self.F, x, 0)
