@@ -1033,8 +1033,8 @@ int64_t conv3x3_wgrad_slabs(int64_t Nb, int64_t H, int64_t W, int64_t Cin, int64
                                   static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(stride));
 }
 
-int64_t conv1x1_wgrad_splits(int64_t M, int64_t N, int64_t K) {
-  return kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
+int64_t conv1x1_wgrad_splits(int64_t M, int64_t N, int64_t K, bool solo) {
+  return kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), solo);
 }
 
 // 3x3 / pad 1 convolution as an implicit GEMM on the same MFMA kernel:
@@ -1221,7 +1221,7 @@ void conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& ball, at::Tensor d
 
 void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional<at::Tensor>& pro_coef,
                    at::Tensor dw32, const c10::optional<at::Tensor>& dW, double scale, int64_t M, int64_t N, int64_t K,
-                   int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride) {
+                   int64_t Hout, int64_t Wout, int64_t Hin, int64_t Win, int64_t stride, bool solo) {
   const BwdArm bw = take_bwd_arm();
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && M > 0, "conv1x1_wgrad: need K % 64 == 0, N % 64 == 0");
   if (bw.x) {
@@ -1234,7 +1234,8 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
   need_bf16(G, M * N, "conv1x1_wgrad G");
   need_bf16(A, rows_in * K, "conv1x1_wgrad A");
   need_opt_f32(pro_coef, 2 * K, "pro_coef");
-  const int64_t slabs = kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
+  const int64_t slabs =
+      kdl::conv1x1_wgrad_splits(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), solo);
   TORCH_CHECK(dw32.is_cuda() && dw32.scalar_type() == at::kFloat && dw32.is_contiguous() &&
                   dw32.numel() >= slabs * N * K,
               "conv1x1_wgrad: dw32 must be fp32 contiguous with conv1x1_wgrad_splits(M, N, K) * N * K elements");
@@ -1246,7 +1247,7 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
                                dW.has_value() && dW->defined() ? dW->data_ptr() : nullptr, static_cast<float>(scale),
                                static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Hout),
                                static_cast<int>(Wout), static_cast<int>(Hin), static_cast<int>(Win),
-                               static_cast<int>(stride), cur_stream(), bw.x, bw.coef),
+                               static_cast<int>(stride), cur_stream(), bw.x, bw.coef, solo),
             "conv1x1_wgrad");
 }
 
@@ -1538,11 +1539,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_res_pro_arm", &bn_res_pro_arm, "next forward conv1x1_gemm applies relu(A*scale+shift+res), written through + mask");
   m.def("conv3x3_aout_arm", &conv3x3_aout_arm, "next prologue conv3x3_gemm also writes relu(B(x)) here (56x56 halo)");
   m.def("conv3x3_gemm", &conv3x3_gemm, "3x3 pad-1 conv (fwd or stride-1 dgrad) as implicit MFMA GEMM with fused BN prologue/epilogue");
-  m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast)");
+  m.def("conv1x1_wgrad", &conv1x1_wgrad, "1x1 conv weight gradient (split-M MFMA into fp32 slabs, fixed-order reduce + bf16 cast); solo: no side stream shares the GPU (more splits)",
+        py::arg("G"), py::arg("A"), py::arg("pro_coef"), py::arg("dw32"), py::arg("dW"), py::arg("scale"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("Hout"), py::arg("Wout"), py::arg("Hin"), py::arg("Win"), py::arg("stride"),
+        py::arg("solo") = false);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "3x3 pad-1 conv weight gradient (implicit GEMM, split-M slabs)");
   m.def("conv3x3_wgrad_slabs", &conv3x3_wgrad_slabs, "fp32 [Cout, 9 Cin] slabs conv3x3_wgrad may write (its fastest path)");
   m.def("set_wgrad_big", &kdl::set_wgrad_big, "256x256 weight-gradient tiles: 0 off, 1 3x3 only, 2 3x3 + 1x1");
-  m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad");
+  m.def("conv1x1_wgrad_splits", &conv1x1_wgrad_splits, "M splits (slab count) of conv1x1_wgrad", py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("solo") = false);
   m.def("bn_coef_offset", &bn_coef_offset, "float offset of the coefficient block in a BN workspace");
   m.def("bn_stage_fwd_stats", &bn_stage_fwd_stats, "BN forward statistics into the workspace replicas");
   m.def("bn_stage_fwd_finalize", &bn_stage_fwd_finalize, "BN forward finalize (mean/invstd/coefs/running stats)");

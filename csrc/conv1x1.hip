@@ -852,10 +852,19 @@ void wgrad_tiles(int N, int K, bool conv3, int* tn, int* tk, bool bwd = false) {
   *tk = K % 128 == 0 ? 128 : 64;
 }
 
-int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false) {
+int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false, bool solo = false) {
   int tn, tk;
   wgrad_tiles(N, K, conv3, &tn, &tk, bwd);
   const int tiles = (N / tn) * (K / tk);
+  if (solo) {
+    // nothing else on the GPU (the CTR tower): ~3 blocks per CU, at least 400
+    // batch rows per split so the slab bytes stay below the GEMM's own
+    // (batch 4096: 1024x1728 62 -> 40 us at 3 splits, 512x1024 best at 10,
+    // 256x512 at 20 of 40; profiles/r04_ctr_tile_probe.txt)
+    int splits = 768 / tiles, cap = M / 400;
+    if (splits > cap) splits = cap;
+    return splits < 1 ? 1 : splits;
+  }
   // ~2 blocks per CU (one round): halves the slab bytes of 4 blocks/CU, measured +1.5% per step.
   // Rounded DOWN so the grid never spills a partial second round onto the CUs
   // (3x3 stage-4: 576 blocks = 1.125 rounds took 1.7x the time of 432).
@@ -873,9 +882,10 @@ int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false) {
 }
 
 // slab capacity for either G mode (plain / BN-backward prologue)
-int conv1x1_wgrad_splits(int M, int N, int K) {
+int conv1x1_wgrad_splits(int M, int N, int K, bool solo) {
   const int a = wgrad_splits(M, N, K, false), b = wgrad_splits(M, N, K, false, true);
-  return a > b ? a : b;
+  const int c = solo ? wgrad_splits(M, N, K, false, false, true) : 0;
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
 // the caller's preference (an explicit KDL_TUNE wgrad_big wins)
@@ -945,7 +955,8 @@ namespace {
 // big: the workspace holds wgrad_splits(M, N, K, true) slabs (3x3 256-tile configs)
 hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                       int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int mode, int cin,
-                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr) {
+                      hipStream_t s, bool big = false, const void* gx = nullptr, const float* gcoef = nullptr,
+                      bool solo = false) {
   if (N % 64 || K % 64 || M <= 0) return hipErrorInvalidValue;
   const bool bwd = gx != nullptr;
   // the G prologue exists on the LDS-DMA kernel only
@@ -953,7 +964,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     return hipErrorInvalidValue;
   int tn, tk;
   wgrad_tiles(N, K, big, &tn, &tk, bwd);
-  const int splits = wgrad_splits(M, N, K, big, bwd);
+  const int splits = wgrad_splits(M, N, K, big, bwd, solo && !bwd && !big);
   int rps = (M + splits - 1) / splits;
   rps = (rps + WMK - 1) / WMK * WMK;
   int tiles_k = K / tk;
@@ -996,9 +1007,9 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
 
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
-                         const void* gx, const float* gcoef) {
+                         const void* gx, const float* gcoef, bool solo) {
   return wgrad_impl(G, A, pro_coef, dw32, dW, scale, M, N, K, Hout, Wout, Hin, Win, stride,
-                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef);
+                    stride > 1 ? G_STRIDED : G_DENSE, K, s, false, gx, gcoef, solo);
 }
 
 int conv3x3_wgrad_slabs(int Nb, int Hin, int Win, int Cin, int Cout, int stride) {

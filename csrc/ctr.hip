@@ -659,13 +659,15 @@ static int g_ctr_tile = -2;  // -2: KDL_TUNE ctr_tile, -1: by shape, 0/1/2: 128x
 
 void set_ctr_tile(int t) { g_ctr_tile = t; }
 
-// the largest tile with >= 2 blocks per CU (512 tiles), else the smallest
+// the largest tile with >= 1.5 blocks per CU (384 tiles), else the smallest
+// (batch 4096: 1728-wide dX 128x128 31.7 us vs 128x64 36.9; 1024-wide forward
+// 128x64 30.1 vs 128x128 35.3; 512 / 256 wide 64x64; profiles/r04_ctr_tile_probe.txt)
 int ctr_tile_for(int M, int N) {
   if (g_ctr_tile == -2) g_ctr_tile = tune_int("ctr_tile", -1);
   if (g_ctr_tile >= 0) return g_ctr_tile;
   const int bm[3] = {128, 128, 64}, bn[3] = {128, 64, 64};
   for (int c = 0; c < 3; ++c)
-    if (static_cast<int64_t>((M + bm[c] - 1) / bm[c]) * ((N + bn[c] - 1) / bn[c]) >= 512) return c;
+    if (static_cast<int64_t>((M + bm[c] - 1) / bm[c]) * ((N + bn[c] - 1) / bn[c]) >= 384) return c;
   return 2;
 }
 

@@ -305,7 +305,8 @@ hipError_t head_backward(const void* feat, const void* w, const void* dl, const 
 hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s,
                              int layout = 0);
 void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)
-int conv1x1_wgrad_splits(int M, int N, int K);
+// solo: nothing else shares the GPU (no weight-gradient side stream): more blocks per tile
+int conv1x1_wgrad_splits(int M, int N, int K, bool solo = false);
 // 256 x 256 weight-gradient tiles: 0 off, 1 3x3 only (default), 2 3x3 + 1x1 (ignored under KDL_TUNE wgrad_big)
 void set_wgrad_big(int mode);
 // dW = scale * sum_m G[m, :]^T pro(A)[m, :].  dw32 is the split-M slab workspace
@@ -315,7 +316,7 @@ void set_wgrad_big(int mode);
 // (gcoef = [3N] k | c1 | c0), computed while staging it (LDS-DMA kernel only).
 hipError_t conv1x1_wgrad(const void* G, const void* A, const float* pro_coef, float* dw32, void* dW, float scale,
                          int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride, hipStream_t s,
-                         const void* gx = nullptr, const float* gcoef = nullptr);
+                         const void* gx = nullptr, const float* gcoef = nullptr, bool solo = false);
 // 3x3 / pad 1: dW[Cout][3][3][Cin] = sum_m G[m, :]^T pro(A)_tap(m); dw32 holds
 // conv3x3_wgrad_slabs(...) x [Cout, 9 Cin] fp32 (dw32_floats: its size; a smaller
 // workspace of conv1x1_wgrad_splits(M, Cout, 9 Cin) slabs keeps the implicit GEMM).

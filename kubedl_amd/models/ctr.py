@@ -71,7 +71,9 @@ class _FusedLinearFn(torch.autograd.Function):
             B = x.shape[0]
             ws = _wgrad_workspace(ext, B, fout, fin, x.device)
             dw = torch.empty(fout, fin, dtype=w.dtype, device=w.device)
-            ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1)
+            # solo: no weight-gradient side stream here, so the split count
+            # that fills the chip (not the ResNet engine's two-stream one)
+            ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1, True)
         else:
             dw = (dz.t() @ x).to(w.dtype)
         return dx, dw, ((db if db.dtype == w.dtype else db.to(w.dtype)) if ctx.has_b else None), None
@@ -82,7 +84,7 @@ _WS = {}
 
 def _wgrad_workspace(ext, M, N, K, device):
     key = (M, N, K, str(device))
-    need = ext.conv1x1_wgrad_splits(M, N, K) * N * K  # (the tile mode may change: set_wgrad_big)
+    need = ext.conv1x1_wgrad_splits(M, N, K, True) * N * K  # (the tile mode may change: set_wgrad_big)
     ws = _WS.get(key)
     if ws is None or ws.numel() < need:
         ws = _WS[key] = torch.empty(need, device=device)

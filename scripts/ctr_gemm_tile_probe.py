@@ -49,21 +49,26 @@ def main() -> int:
         dz = torch.randn(B, N, device="cuda").bfloat16()
         x = torch.randn(B, K, device="cuda").bfloat16()
         dw = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
-        for blocks in (160, 320, 512, 768, 1024, 2048):
-            os.environ["KDL_TUNE"] = f"wgrad_blocks={blocks}"
-            ws = torch.empty(ext.conv1x1_wgrad_splits(B, N, K) * N * K, device="cuda")
+        # "solo" = the CTR model's policy (conv1x1_wgrad(..., solo=True))
+        for blocks in (160, 320, 512, 768, 1024, 2048, "solo"):
+            solo = blocks == "solo"
+            if not solo:
+                os.environ["KDL_TUNE"] = f"wgrad_blocks={blocks}"
+            else:
+                os.environ.pop("KDL_TUNE", None)
+            ws = torch.empty(ext.conv1x1_wgrad_splits(B, N, K, solo) * N * K, device="cuda")
             for _ in range(5):
-                ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, N, K, 0, 0, 0, 0, 1)
+                ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, N, K, 0, 0, 0, 0, 1, solo)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(50):
-                ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, N, K, 0, 0, 0, 0, 1)
+                ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, N, K, 0, 0, 0, 0, 1, solo)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / 50
             print(json.dumps({"shape": name, "M": B, "N": N, "K": K, "wgrad_blocks": blocks,
-                              "splits": ext.conv1x1_wgrad_splits(B, N, K), "us": round(us, 2),
+                              "splits": ext.conv1x1_wgrad_splits(B, N, K, solo), "us": round(us, 2),
                               "tflops": round(2.0 * B * N * K / us / 1e6, 1)}), flush=True)
         os.environ.pop("KDL_TUNE", None)
     return 0
