@@ -543,7 +543,7 @@ std::vector<at::Tensor> head_bce_fwd(const at::Tensor& x, const at::Tensor& w, c
   TORCH_CHECK(y.scalar_type() == at::kFloat && y.numel() == M && y.is_contiguous(), "head_bce_fwd: labels f32 [M]");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto opt = x.options().dtype(at::kFloat);
-  auto logit = at::empty({M}, opt), dlogit = at::empty({M}, opt), part = at::empty({(M + 3) / 4}, opt);
+  auto logit = at::empty({M}, opt), dlogit = at::empty({M}, opt), part = at::empty({kdl::head_bce_fwd_blocks(static_cast<int>(M))}, opt);
   auto loss = at::empty({1}, opt);
   auto cnt = ticket_counters(x, 0);
   check_hip(kdl::head_bce_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), b.scalar_type() == at::kBFloat16,

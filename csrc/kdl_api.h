@@ -183,6 +183,7 @@ hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* part, 
                           int M, int N, hipStream_t s);
 // cnt: one ticket counter, zero before the first call (re-armed by the kernel);
 // loss [1] fp32 = the mean loss; b: bf16 (b_bf16) or fp32 [1]
+int head_bce_fwd_blocks(int M);  // = the loss-partial count
 hipError_t head_bce_fwd(const void* x, const void* w, const void* b, bool b_bf16, const float* y, int M, int K,
                         float* logit, float* dlogit, float* loss_part, unsigned* cnt, float* loss, hipStream_t s);
 int head_bce_bwd_blocks(int M);
