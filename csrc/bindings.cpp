@@ -614,7 +614,7 @@ at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64
   check_hip(kdl::segment_reduce(rows.data_ptr(), dtype_code(rows), static_cast<int>(F), static_cast<int>(rows.stride(0)),
                                 static_cast<int>(col0), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
                                 static_cast<int>(U), static_cast<int>(D), out.data_ptr<float>(), cur_stream(),
-                                opt_count(ucount)),
+                                opt_count(ucount), order.numel()),
             "segment_reduce");
   return out;
 }

@@ -328,22 +328,40 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
 }
 
 // ---------------------------------------------------------------- embeddings
+constexpr int kGatherRows = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__ table, const int64_t* __restrict__ idx,
                                                            int n, int F, int D, T* __restrict__ out, int ld_out,
-                                                           int col0) {
-  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave >= n) return;
-  const int b = wave / F, f = wave % F;
-  const T* src = table + idx[wave] * static_cast<int64_t>(D);
-  T* dst = out + static_cast<int64_t>(b) * ld_out + col0 + f * D;
+                                                           int col0, int lg) {
+  // a group of 2^lg lanes per row (16 B each), kGatherRows rows per group with
+  // every load issued before the first store (one wave per 128-256 B row left
+  // 48-56 of 64 lanes idle)
   constexpr int VEC = 16 / sizeof(T);
-  for (int c = lane * VEC; c < D; c += 64 * VEC) {
-    if (c + VEC <= D) {
-      *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(src + c);
-    } else {
-      for (int k = c; k < D; ++k) dst[k] = src[k];
+  const int g = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
+  const int r0 = g * kGatherRows;
+  if (r0 >= n) return;
+  for (int c = gl * VEC; c < D; c += VEC << lg) {
+    const bool full = c + VEC <= D;
+    uint4 v[kGatherRows];
+    const T* src[kGatherRows];
+#pragma unroll
+    for (int i = 0; i < kGatherRows; ++i) {
+      const int r = r0 + i < n ? r0 + i : r0;
+      src[i] = table + idx[r] * static_cast<int64_t>(D);
+      if (full) v[i] = *reinterpret_cast<const uint4*>(src[i] + c);
+    }
+#pragma unroll
+    for (int i = 0; i < kGatherRows; ++i) {
+      const int r = r0 + i;
+      if (r >= n) break;
+      const int b = r / F, f = r - b * F;
+      T* dst = out + static_cast<int64_t>(b) * ld_out + col0 + f * D;
+      if (full) {
+        *reinterpret_cast<uint4*>(dst + c) = v[i];
+      } else {
+        for (int k = c; k < D; ++k) dst[k] = src[i][k];
+      }
     }
   }
 }
@@ -381,9 +399,12 @@ __device__ __forceinline__ void ld4(const T* p, int n, float (&o)[4]) {
 // ``ucount`` (optional): the live segment count on the device (U is then the
 // capacity the grid was sized for) -- no host round trip for data-dependent U.
 constexpr int kSegs = 4;
+// j / F as umulhi(j, mF), mF = ceil(2^32 / F): exact while j * F < 2^32 (host
+// check).  A 64-bit division per row is a branchy call-like sequence that
+// serialised the lock-step loads (97 us with it, profiles/r04_ctr_summary7.txt).
 template <typename T, bool V4>
-__global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, int ld, int col0,
-                                                             const int64_t* __restrict__ order,
+__global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, uint32_t mF, int ld,
+                                                             int col0, const int64_t* __restrict__ order,
                                                              const int64_t* __restrict__ seg, int U, int D, int lg,
                                                              float* __restrict__ out, const int* __restrict__ ucount) {
   const int u0 = ((blockIdx.x * 256 + threadIdx.x) >> lg) * kSegs;
@@ -407,14 +428,16 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict
       for (int i = 0; i < kSegs; ++i) {  // segments past `live` are empty (sb[i] == sb[i+1] == seg[live])
         const bool ok = sb[i] + r < sb[i + 1];
         any |= ok;
-        jj[i] = ok ? order[sb[i] + r] : -1;
+        const int64_t o = order[ok ? sb[i] + r : 0];  // unconditional (order[0] exists)
+        jj[i] = ok ? o : -1;
       }
       if (!any) break;
       float v[kSegs][4];
 #pragma unroll
       for (int i = 0; i < kSegs; ++i) {
-        const int64_t j = jj[i] < 0 ? 0 : jj[i];
-        ld4<T, V4>(rows + (j / F) * static_cast<int64_t>(ld) + col0 + (j % F) * D + c, n, v[i]);
+        const uint32_t j = jj[i] < 0 ? 0u : static_cast<uint32_t>(jj[i]);
+        const uint32_t bi = __umulhi(j, mF), f = j - bi * static_cast<uint32_t>(F);
+        ld4<T, V4>(rows + static_cast<int64_t>(bi) * ld + col0 + static_cast<int64_t>(f) * D + c, n, v[i]);
       }
 #pragma unroll
       for (int i = 0; i < kSegs; ++i)
@@ -777,13 +800,17 @@ hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* part, 
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  dim3 grid((n + 3) / 4);
+  const int vec = dtype == 1 ? 8 : 4;  // elements per 16-B lane piece
+  int lg = 0;
+  while (lg < 6 && (vec << lg) < D) ++lg;
+  const int64_t groups = (n + kGatherRows - 1) / kGatherRows;
+  dim3 grid(static_cast<unsigned>(((groups << lg) + 255) / 256));
   if (dtype == 1)
     hipLaunchKernelGGL((embed_gather_kernel<bf16_t>), grid, dim3(256), 0, s, static_cast<const bf16_t*>(table), idx,
-                       n, F, D, static_cast<bf16_t*>(out), ld_out, col0);
+                       n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg);
   else
     hipLaunchKernelGGL((embed_gather_kernel<float>), grid, dim3(256), 0, s, static_cast<const float*>(table), idx, n,
-                       F, D, static_cast<float*>(out), ld_out, col0);
+                       F, D, static_cast<float*>(out), ld_out, col0, lg);
   return hipGetLastError();
 }
 
@@ -795,16 +822,20 @@ static int seg_lanes_log2(int D) {
 }
 
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
-                          const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount) {
-  if (U <= 0) return hipSuccess;
+                          const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount,
+                          int64_t nrows) {
+  if (U <= 0 || nrows <= 0) return hipSuccess;
   const int lg = seg_lanes_log2(D);
   dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(U) + kSegs - 1) / kSegs << lg) + 255) / 256);
   const size_t esz = dtype == 1 ? 2 : 4;
   const bool v4 = D % 4 == 0 && ld % 4 == 0 && col0 % 4 == 0 && reinterpret_cast<uintptr_t>(rows) % (4 * esz) == 0 &&
                   reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  // rows j < n = B * F; umulhi division exact while j * F < 2^32
+  const uint32_t mF = static_cast<uint32_t>(((uint64_t(1) << 32) + F - 1) / F);
+  if (static_cast<uint64_t>(nrows) * static_cast<uint64_t>(F) >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
 #define KDL_SEGRED(T, V)                                                                                      \
-  hipLaunchKernelGGL((segment_reduce_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, ld, \
-                     col0, order, seg, U, D, lg, out, ucount)
+  hipLaunchKernelGGL((segment_reduce_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, mF, \
+                     ld, col0, order, seg, U, D, lg, out, ucount)
   if (dtype == 1) {
     if (v4) KDL_SEGRED(bf16_t, true);
     else KDL_SEGRED(bf16_t, false);

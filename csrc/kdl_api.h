@@ -195,7 +195,8 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
                         int col0, hipStream_t s);
 // ucount (optional): the live segment count on the device; U is then a capacity
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
-                          const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount = nullptr);
+                          const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount,
+                          int64_t nrows);  // nrows = order's length (B * F)
 // rows_local outside [0, nrows) are skipped (exchange padding sentinels)
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
                            int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,

@@ -349,6 +349,12 @@ def test_embedding_kernels_match_torch(D, col0, dt):
     if D % 4 == 0:  # embed_gather moves 16-B row pieces
         ext.embed_gather(table, idx, F, out, 0)
         torch.testing.assert_close(out[:, : F * D], table[idx].reshape(B, F * D))
+    if D % 8 == 0:  # the bf16 table (the model's pulled rows), written at a column offset
+        t16 = table.bfloat16()
+        o16 = torch.zeros(B, 8 + F * D + 16, device="cuda", dtype=torch.bfloat16)
+        ext.embed_gather(t16, idx, F, o16, 8)
+        assert torch.equal(o16[:, 8: 8 + F * D], t16[idx].reshape(B, F * D))
+        assert not o16[:, :8].any() and not o16[:, 8 + F * D:].any()
     # segment reduce of (b, f) gradient rows by inverse index
     uniq, inv = torch.unique(idx, return_inverse=True)
     order = torch.argsort(inv, stable=True)
