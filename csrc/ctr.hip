@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
 }
 
 // ---------------------------------------------------------------- embeddings
-constexpr int kGatherRows = 4;
+constexpr int kGatherRows = 1;
 template <typename T>
 __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__ table, const int64_t* __restrict__ idx,
                                                            int n, int F, int D, T* __restrict__ out, int ld_out,
@@ -398,7 +398,7 @@ __device__ __forceinline__ void ld4(const T* p, int n, float (&o)[4]) {
 // segments, 40 us).
 // ``ucount`` (optional): the live segment count on the device (U is then the
 // capacity the grid was sized for) -- no host round trip for data-dependent U.
-constexpr int kSegs = 4;
+constexpr int kSegs = 1;
 // j / F as umulhi(j, mF), mF = ceil(2^32 / F): exact while j * F < 2^32 (host
 // check).  A 64-bit division per row is a branchy call-like sequence that
 // serialised the lock-step loads (97 us with it, profiles/r04_ctr_summary7.txt).
