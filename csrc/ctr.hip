@@ -333,9 +333,10 @@ template <typename T>
 __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__ table, const int64_t* __restrict__ idx,
                                                            int n, int F, int D, T* __restrict__ out, int ld_out,
                                                            int col0, int lg) {
-  // a group of 2^lg lanes per row (16 B each), kGatherRows rows per group with
-  // every load issued before the first store (one wave per 128-256 B row left
-  // 48-56 of 64 lanes idle)
+  // a group of 2^lg lanes per row (16 B each; one wave per 128-256 B row left
+  // 48-56 of 64 lanes idle: 20 -> 11 us for the fp32 pull at batch 4096).
+  // kGatherRows > 1 walks that many rows per group with every load issued
+  // before the first store: measured slower at 4 (30 us), so 1.
   constexpr int VEC = 16 / sizeof(T);
   const int g = (blockIdx.x * 256 + threadIdx.x) >> lg;
   const int gl = threadIdx.x & ((1 << lg) - 1);
@@ -391,69 +392,52 @@ __device__ __forceinline__ void ld4(const T* p, int n, float (&o)[4]) {
 // rows + b*ld + col0 + f*D (the layout embed_gather wrote).  Rows order[j]
 // are summed per segment [seg[u], seg[u+1]), in j order, by a group of G =
 // 2^lg lanes (G*4 >= D when D <= 256: a wave per segment left 48 of 64 lanes
-// idle at D = 64).  Each group owns kSegs consecutive segments and walks them
-// in lock step (the r-th row of every segment per step), so kSegs
-// seg -> order -> row load chains are in flight at once: with one segment per
-// group the kernel was bound by that chain's latency (~100k one-row
-// segments, 40 us).
+// idle at D = 64), two rows' loads in flight per step.  (Four segments per
+// group in lock step measured slower: 63 vs 33 us at batch 4096.)
+// j / F as umulhi(j, mF), mF = ceil(2^32 / F): exact while j * F < 2^32 (host
+// check) -- no 64-bit division sequence per row.
 // ``ucount`` (optional): the live segment count on the device (U is then the
 // capacity the grid was sized for) -- no host round trip for data-dependent U.
-constexpr int kSegs = 1;
-// j / F as umulhi(j, mF), mF = ceil(2^32 / F): exact while j * F < 2^32 (host
-// check).  A 64-bit division per row is a branchy call-like sequence that
-// serialised the lock-step loads (97 us with it, profiles/r04_ctr_summary7.txt).
+template <typename T, bool V4>
+__device__ __forceinline__ void seg_row(const T* rows, int64_t jj, uint32_t F, uint32_t mF, int ld, int col0, int D,
+                                        int c, int n, float (&v)[4]) {
+  const uint32_t j = static_cast<uint32_t>(jj);
+  const uint32_t bi = __umulhi(j, mF), f = j - bi * F;
+  ld4<T, V4>(rows + static_cast<int64_t>(bi) * ld + col0 + static_cast<int64_t>(f) * D + c, n, v);
+}
+
 template <typename T, bool V4>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, uint32_t mF, int ld,
                                                              int col0, const int64_t* __restrict__ order,
                                                              const int64_t* __restrict__ seg, int U, int D, int lg,
                                                              float* __restrict__ out, const int* __restrict__ ucount) {
-  const int u0 = ((blockIdx.x * 256 + threadIdx.x) >> lg) * kSegs;
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> lg;
   const int gl = threadIdx.x & ((1 << lg) - 1);
-  const int live = ucount ? *ucount : U;
-  if (u0 >= live) return;
-  int64_t sb[kSegs + 1];
-#pragma unroll
-  for (int i = 0; i <= kSegs; ++i) sb[i] = seg[u0 + i < live ? u0 + i : live];
+  if (u >= (ucount ? *ucount : U)) return;
+  const int64_t s0 = seg[u], s1 = seg[u + 1];
   for (int c = gl * 4; c < D; c += 4 << lg) {
     const int n = D - c < 4 ? D - c : 4;
-    float a[kSegs][4];
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t j = s0;
+    for (; j + 1 < s1; j += 2) {
+      const int64_t j0 = order[j], j1 = order[j + 1];
+      float v0[4], v1[4];
+      seg_row<T, V4>(rows, j0, F, mF, ld, col0, D, c, n, v0);
+      seg_row<T, V4>(rows, j1, F, mF, ld, col0, D, c, n, v1);
 #pragma unroll
-    for (int i = 0; i < kSegs; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[i][k] = 0.f;
-    for (int64_t r = 0;; ++r) {
-      bool any = false;
-      int64_t jj[kSegs];
-#pragma unroll
-      for (int i = 0; i < kSegs; ++i) {  // segments past `live` are empty (sb[i] == sb[i+1] == seg[live])
-        const bool ok = sb[i] + r < sb[i + 1];
-        any |= ok;
-        const int64_t o = order[ok ? sb[i] + r : 0];  // unconditional (order[0] exists)
-        jj[i] = ok ? o : -1;
-      }
-      if (!any) break;
-      float v[kSegs][4];
-#pragma unroll
-      for (int i = 0; i < kSegs; ++i) {
-        const uint32_t j = jj[i] < 0 ? 0u : static_cast<uint32_t>(jj[i]);
-        const uint32_t bi = __umulhi(j, mF), f = j - bi * static_cast<uint32_t>(F);
-        ld4<T, V4>(rows + static_cast<int64_t>(bi) * ld + col0 + static_cast<int64_t>(f) * D + c, n, v[i]);
-      }
-#pragma unroll
-      for (int i = 0; i < kSegs; ++i)
-        if (jj[i] >= 0)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) a[i][k] += v[i][k];
+      for (int k = 0; k < 4; ++k) a[k] = (a[k] + v0[k]) + v1[k];
     }
+    if (j < s1) {
+      float v0[4];
+      seg_row<T, V4>(rows, order[j], F, mF, ld, col0, D, c, n, v0);
 #pragma unroll
-    for (int i = 0; i < kSegs; ++i) {
-      if (u0 + i >= live) break;
-      float* o = out + static_cast<int64_t>(u0 + i) * D + c;
-      if (V4) {
-        *reinterpret_cast<float4*>(o) = make_float4(a[i][0], a[i][1], a[i][2], a[i][3]);
-      } else {
-        for (int k = 0; k < n; ++k) o[k] = a[i][k];
-      }
+      for (int k = 0; k < 4; ++k) a[k] += v0[k];
+    }
+    float* o = out + static_cast<int64_t>(u) * D + c;
+    if (V4) {
+      *reinterpret_cast<float4*>(o) = make_float4(a[0], a[1], a[2], a[3]);
+    } else {
+      for (int k = 0; k < n; ++k) o[k] = a[k];
     }
   }
 }
@@ -826,7 +810,7 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
                           int64_t nrows) {
   if (U <= 0 || nrows <= 0) return hipSuccess;
   const int lg = seg_lanes_log2(D);
-  dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(U) + kSegs - 1) / kSegs << lg) + 255) / 256);
+  dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(U) << lg) + 255) / 256));
   const size_t esz = dtype == 1 ? 2 : 4;
   const bool v4 = D % 4 == 0 && ld % 4 == 0 && col0 % 4 == 0 && reinterpret_cast<uintptr_t>(rows) % (4 * esz) == 0 &&
                   reinterpret_cast<uintptr_t>(out) % 16 == 0;
