@@ -208,14 +208,6 @@ __global__ __launch_bounds__(256) void route_rows_kernel(
 // prefix of ceil(size / rpb), chunk_off[nb] = total).  Each wave keeps UNROLL
 // row slots in flight (row ids, g/h and bin codes loaded before any LDS
 // atomic) so the dependent global loads overlap.
-// Feature histograms in LDS are [fp][2B + kHistPad] floats.  With a dense
-// stride of 2B = 512 the bank of (feature, bin) is 2*bin mod 64 whatever the
-// feature: the 32 features a wave updates together used the 32 even banks only.
-#ifndef KDL_HIST_PAD
-#define KDL_HIST_PAD 0
-#endif
-constexpr int kHistPad = KDL_HIST_PAD;
-
 template <int UNROLL>
 __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
     const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
@@ -236,8 +228,7 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
   const int f0 = blockIdx.y * fp;
   const int nf = (F - f0) < fp ? (F - f0) : fp;
   const int t = threadIdx.x;
-  const int fs = 2 * B + kHistPad;  // LDS floats per feature
-  for (int i = t; i < nf * fs; i += kHistBlock) lds[i] = 0.f;
+  for (int i = t; i < nf * B * 2; i += kHistBlock) lds[i] = 0.f;
   __syncthreads();
   const int lane = t & 63, wave = t >> 6;
   const int rpw = 64 / fp;
@@ -263,7 +254,7 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       if (row[u] >= 0 && fl < nf) {
-        float* p = lds + fl * fs + b[u] * 2;
+        float* p = lds + (fl * B + b[u]) * 2;
         atomicAdd(p, g[u]);
         atomicAdd(p + 1, h[u]);
       }
@@ -272,8 +263,7 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
   __syncthreads();
   float* out = hist + (static_cast<int64_t>(j) * F + f0) * B * 2;
   for (int i = t; i < nf * B * 2; i += kHistBlock) {
-    const int fi = i / (2 * B);
-    const float v = lds[i + fi * kHistPad];
+    const float v = lds[i];
     if (v != 0.f) __hip_atomic_fetch_add(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -504,7 +494,7 @@ static int hist_fp(int F) {
 static hipError_t hist_lds_attr() {
   static bool attr_set = false;
   if (!attr_set) {
-    const int bytes = static_cast<int>(kFTile * (256 * 2 + kHistPad) * sizeof(float));
+    const int bytes = static_cast<int>(kFTile * 256 * 2 * sizeof(float));
     KDL_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<4>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
     attr_set = true;
@@ -520,7 +510,7 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
   const int fp = hist_fp(F);
   KDL_CHECK_HIP(hist_lds_attr());
   dim3 grid(max_chunks, (F + fp - 1) / fp);
-  const size_t lds = static_cast<size_t>(fp) * (B * 2 + kHistPad) * sizeof(float);
+  const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(float);
   hipLaunchKernelGGL((hist_build_wq_kernel<4>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows,
                      blo, bhi, chunk_off, nb, F, B, rpb, fp, hist);
   return hipGetLastError();
