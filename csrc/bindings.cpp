@@ -254,8 +254,7 @@ void sgd_step(const at::Tensor& chunks, at::Tensor master, at::Tensor mom, const
 void adam_step(const at::Tensor& chunks, at::Tensor master, at::Tensor m1, at::Tensor m2,
                const at::Tensor& grad, at::Tensor param, double lr, double beta1, double beta2,
                double eps, int64_t step, double grad_scale, bool adam_w,
-               const std::vector<double>& wd, const std::vector<double>& lr_scale,
-               const c10::optional<at::Tensor>& step_t) {
+               const std::vector<double>& wd, const std::vector<double>& lr_scale) {
   check_chunks(chunks);
   TORCH_CHECK(master.numel() == grad.numel() && grad.numel() == param.numel() &&
                   m1.numel() == master.numel() && m2.numel() == master.numel(),
@@ -264,11 +263,6 @@ void adam_step(const at::Tensor& chunks, at::Tensor master, at::Tensor m1, at::T
   const double bc1 = 1.0 - std::pow(beta1, static_cast<double>(step));
   const double bc2 = 1.0 - std::pow(beta2, static_cast<double>(step));
   auto h = make_hyper(lr, beta1, beta2, eps, bc1, bc2, grad_scale, false, false, adam_w, wd, lr_scale);
-  if (step_t.has_value() && step_t->defined()) {
-    TORCH_CHECK(step_t->is_cuda() && step_t->scalar_type() == at::kFloat && step_t->numel() == 1,
-                "adam_step: step_t must be a float32 [1] GPU tensor");
-    h.step_dev = step_t->data_ptr<float>();
-  }
   check_hip(kdl::fused_adam(reinterpret_cast<const kdl::OptChunk*>(chunks.data_ptr<int64_t>()),
                             static_cast<int>(chunks.size(0)), master.data_ptr<float>(),
                             m1.data_ptr<float>(), m2.data_ptr<float>(), grad.data_ptr(),
@@ -1490,10 +1484,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_pool_bwd", &bn_pool_bwd, "stem BatchNorm + ReLU + max-pool(3,2,1) backward, NHWC bf16");
   m.def("bn_workspace_floats", &bn_ws_floats, "per-layer BN workspace size (fp32 elements)");
   m.def("sgd_step", &sgd_step, "flat chunked fused SGD-momentum with fp32 master weights");
-  m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights (step_t: the step count on the device, for graph replay)",
-        py::arg("chunks"), py::arg("master"), py::arg("m1"), py::arg("m2"), py::arg("grad"), py::arg("param"),
-        py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("step"), py::arg("grad_scale"),
-        py::arg("adam_w"), py::arg("wd"), py::arg("lr_scale"), py::arg("step_t") = py::none());
+  m.def("adam_step", &adam_step, "flat chunked fused Adam/AdamW with fp32 master weights");
   m.def("chunk_sumsq", &chunk_sumsq, "per-chunk sum of squares");
   m.def("cast_copy", &cast_copy, "flat dtype-casting copy");
   m.def("transpose_tiles", &transpose_tiles, "batched bf16 2-D transposes from a static 64x64 tile table");

@@ -86,10 +86,6 @@ struct OptHyper {
   int adam_w;
   float wd[4];
   float lr_scale[4];
-  // Adam: the step count t on the device (bias corrections 1 - beta^t computed in
-  // the kernel; bc1 / bc2 unused) -- a graph-captured step replays with the
-  // current t.  nullptr: bc1 / bc2 from the host.
-  const float* step_dev;
 };
 
 hipError_t fused_sgd(const OptChunk* chunks, int nchunks, float* master, float* mom,

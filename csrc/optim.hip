@@ -75,14 +75,8 @@ __global__ __launch_bounds__(256) void adam_chunk_kernel(const OptChunk* __restr
   const float wd = h.wd[c.group];
   const float lr = h.lr * h.lr_scale[c.group];
   const float b1 = h.momentum, b2 = h.dampening;
-  float bc1 = h.bc1, bc2 = h.bc2;
-  if (h.step_dev != nullptr) {
-    const float t = *h.step_dev;
-    bc1 = 1.f - powf(b1, t);
-    bc2 = 1.f - powf(b2, t);
-  }
-  const float step = lr / bc1;
-  const float inv_sqrt_bc2 = rsqrtf(bc2);
+  const float step = lr / h.bc1;
+  const float inv_sqrt_bc2 = rsqrtf(h.bc2);
   for (int i = threadIdx.x * 8; i < c.len; i += 256 * 8) {
     const int64_t idx = c.start + i;
     float g[8], w[8], a[8], v[8];

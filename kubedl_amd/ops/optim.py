@@ -314,15 +314,6 @@ class FusedAdam(_FusedBase):
         self.adam_w = adam_w
         self.m1 = torch.zeros_like(space.master)
         self.m2 = torch.zeros_like(space.master)
-        self.step_t = None  # device step count (device_step)
-
-    def device_step(self) -> None:
-        """Keep the step count on the device: each ``step()`` increments it
-        there and the kernel derives the bias corrections from it, so a
-        hipGraph-captured step replays with the current count (the host
-        ``step_count`` then stops advancing on replays)."""
-        if self.step_t is None and self._use_hip():
-            self.step_t = torch.full((1,), float(self.step_count), dtype=torch.float32, device=self.space.device)
 
     @torch.no_grad()
     def step(self) -> None:
@@ -331,12 +322,10 @@ class FusedAdam(_FusedBase):
         self.step_count += 1
         b1, b2 = self.betas
         if self._use_hip():
-            if self.step_t is not None:
-                self.step_t.add_(1.0)
             _ext.load().adam_step(sp.chunks, sp.master, self.m1, self.m2, sp.grad, sp.param,
                                   float(self.lr), float(b1), float(b2), float(self.eps),
                                   int(self.step_count), float(self.grad_scale), bool(self.adam_w),
-                                  [float(self.weight_decay), 0.0], [1.0, 1.0], self.step_t)
+                                  [float(self.weight_decay), 0.0], [1.0, 1.0])
             return
         mask = self._groups_mask()
         g = sp.grad.float() * self.grad_scale

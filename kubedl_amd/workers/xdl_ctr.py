@@ -135,27 +135,6 @@ def main(argv=None) -> int:
     # every step's synthetic batch is generated on the device before the timed
     # loop (distinct batches, no host work or H2D copy inside the timed steps)
     batches = [synth_batch(args.batch, args.fields, args.vocab, args.dense, gen, w_true) for _ in range(total)]
-
-    def train_step(ids, dense, y):
-        space.zero_grad()
-        x, inv, U = model.build_input(ids, dense)
-        x.requires_grad_(True)
-        loss, _logit = model.tower.loss(x, y)
-        loss.backward()
-        model.push_grads(x.grad, inv, U, scale=1.0 / len(workers))
-        ddp.finish()
-        opt.step()
-        return loss.detach()
-
-    # One GPU, one worker: the step is ~50 small launches (0.42 ms of kernels)
-    # and sync-free (device dedup, device counts, device Adam step count), so
-    # it is captured once as a hipGraph and replayed; each step copies its
-    # batch into the graph's static inputs.  KDL_CTR_GRAPH=0: eager steps.
-    graph = None
-    use_graph = (use_gpu and world == 1 and emb.dedup is not None and args.warmup >= 2
-                 and os.environ.get("KDL_CTR_GRAPH", "1") != "0")
-    if use_graph:
-        opt.device_step()
     losses = []
     t0 = None
     for it in range(total):
@@ -166,21 +145,15 @@ def main(argv=None) -> int:
                 dist.barrier(group=wgroup)
             t0 = time.perf_counter()
         ids, dense, y = batches[it % len(batches)]
-        if use_graph and it == args.warmup - 1:
-            # capture after eager warm-up steps (workspaces, caches, ticket
-            # counters exist); capturing does not run the step, the replay does
-            torch.cuda.synchronize()
-            static_in = (ids.clone(), dense.clone(), y.clone())
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                static_loss = train_step(*static_in)
-        if graph is not None:
-            for dst, src in zip(static_in, (ids, dense, y)):
-                dst.copy_(src, non_blocking=True)
-            graph.replay()
-            losses.append(static_loss.clone())
-        else:
-            losses.append(train_step(ids, dense, y))
+        space.zero_grad()
+        x, inv, U = model.build_input(ids, dense)
+        x.requires_grad_(True)
+        loss, _logit = model.tower.loss(x, y)
+        loss.backward()
+        model.push_grads(x.grad, inv, U, scale=1.0 / len(workers))
+        ddp.finish()
+        opt.step()
+        losses.append(loss.detach())
         common.report_progress(it + 1)
     if use_gpu:
         torch.cuda.synchronize()
@@ -198,7 +171,7 @@ def main(argv=None) -> int:
                           "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
                           "samples_per_sec": args.steps * args.batch * len(workers) / dt if dt > 0 else 0.0,
                           "loss_first": first, "loss_last": last, "device": str(device),
-                          "hip_kernels": emb.use_hip, "hip_graph": graph is not None, **xstats}), flush=True)
+                          "hip_kernels": emb.use_hip, **xstats}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
