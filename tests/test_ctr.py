@@ -377,6 +377,36 @@ def test_embedding_kernels_match_torch(D, col0, dt):
 
 
 @pytest.mark.gpu
+def test_segment_reduce_skewed_with_device_count():
+    """Skewed segments (one id in 60 % of the rows, the rest near-unique) at the
+    CTR shape (26 fields x 64-d, bf16 rows at ld 1728), the live segment count
+    read on the device (ucount) with a larger capacity, and a fixed summation
+    order: two calls are bitwise equal, and equal to index_add within fp32."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(3)
+    B, F, D, ld = 512, 26, 64, 1728
+    n = B * F
+    ids = torch.randint(0, 50_000, (n,), device="cuda")
+    ids[torch.rand(n, device="cuda") < 0.6] = 7
+    uniq, inv = torch.unique(ids, return_inverse=True)
+    U = len(uniq)
+    order = torch.argsort(inv, stable=True)
+    cap = U + 100  # capacity-sized seg (the sync-free path's shape), live count on the device
+    seg = torch.full((cap + 1,), n, dtype=torch.int64, device="cuda")
+    seg[0] = 0
+    seg[1:U + 1] = torch.cumsum(torch.bincount(inv, minlength=U), 0)
+    count = torch.tensor([U], dtype=torch.int32, device="cuda")
+    gx = torch.randn(B, ld, device="cuda").bfloat16()
+    got = ext.segment_reduce(gx, F, 0, D, order, seg, count)
+    again = ext.segment_reduce(gx, F, 0, D, order, seg, count)
+    assert got.shape == (cap, D)
+    assert torch.equal(got[:U], again[:U])
+    ref = torch.zeros(U, D, device="cuda").index_add_(0, inv, gx[:, : F * D].reshape(n, D).float())
+    torch.testing.assert_close(got[:U], ref, atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
 def test_ctr_worker_trains_on_gpu():
     from kubedl_amd.workers.xdl_ctr import main
     assert main(["--steps", "20", "--warmup", "2", "--batch", "1024", "--fields", "8", "--vocab", "5000",
