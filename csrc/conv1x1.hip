@@ -872,8 +872,11 @@ int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false, bool solo = 
   // With the side stream's gradients overlapping the main stream, FEWER blocks
   // win: they leave CUs to the critical path (job step, same box, 256x256 tiles
   // at half the target: 1024 -> 12,460, 512 -> 12,830, 384 -> 13,047, 320 ->
-  // 13,078, 256 -> 12,933, 192 -> 12,715 img/s; profiles/r02_wgrad_blocks_sweep.txt)
-  int target = tune_int("wgrad_blocks", 320);
+  // 13,078, 256 -> 12,933, 192 -> 12,715 img/s; profiles/r02_wgrad_blocks_sweep.txt).
+  // Re-swept on the round-4 step (kdl head, fewer stray launches): 384 wins,
+  // 13,818-13,837 vs 13,666-13,756 at 320; 352 / 416 / 448 in between, 512
+  // 13,636-13,674, 640 13,215-13,231 (profiles/r04_wgrad_blocks_resweep.txt).
+  int target = tune_int("wgrad_blocks", 384);
   if (tn == 256 || (bwd && !(tn == 64 && tk == 64))) target /= 2;  // one (8-wave) block per CU
   int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;
