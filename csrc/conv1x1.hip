@@ -877,8 +877,7 @@ int wgrad_splits(int M, int N, int K, bool conv3, bool bwd = false, bool solo = 
   // 13,818-13,837 vs 13,666-13,756 at 320; 352 / 416 / 448 in between, 512
   // 13,636-13,674, 640 13,215-13,231 (profiles/r04_wgrad_blocks_resweep.txt).
   int target = tune_int("wgrad_blocks", 384);
-  // one (8-wave) block per CU: half the blocks (KDL_TUNE wgrad_blocks_big overrides)
-  if (tn == 256 || (bwd && !(tn == 64 && tk == 64))) target = tune_int("wgrad_blocks_big", target / 2);
+  if (tn == 256 || (bwd && !(tn == 64 && tk == 64))) target /= 2;  // one (8-wave) block per CU
   int splits = target / tiles;
   const int max_splits = (M + WMK - 1) / WMK;
   if (splits > max_splits) splits = max_splits;
