@@ -293,7 +293,7 @@ def run(args) -> dict:
         "total_steps": total,
     }
     steplog.close()
-    common.report_progress(total, res["steps_per_sec"], loss=loss)
+    common.report_progress(total, res["steps_per_sec"], final=True, loss=loss)
     kdist.shutdown(info)
     return res
 

@@ -106,7 +106,7 @@ def main(argv=None) -> int:
         y = (x[:, 0] > 0).astype(np.float32)
         p = 1.0 / (1.0 + np.exp(-(x @ w)))
         w -= args.learning_rate * x.T @ (p - y) / args.batch_size
-        common.report_progress(s + 1)
+        common.report_progress(s + 1, final=s + 1 == args.steps)
     print(f"tf_stub: {ttype}:{tidx} done {args.steps} steps", flush=True)
     stop.set()
     if srv is not None:

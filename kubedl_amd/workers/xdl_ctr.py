@@ -154,7 +154,7 @@ def main(argv=None) -> int:
         ddp.finish()
         opt.step()
         losses.append(loss.detach())
-        common.report_progress(it + 1)
+        common.report_progress(it + 1, final=it + 1 == total)
     if use_gpu:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0 if t0 is not None else 0.0

@@ -84,7 +84,8 @@ def main(argv=None) -> int:
     X, y = load_data(args, info.rank, info.world_size)
     model = HistGBDT(params, info.device)
     t0 = time.perf_counter()
-    pred = model.fit(X, y, callback=lambda it, _p: common.report_progress(it + 1))
+    pred = model.fit(X, y, callback=lambda it, _p: common.report_progress(
+        it + 1, final=it + 1 == params.n_estimators))
     if info.device.type == "cuda":
         torch.cuda.synchronize()
     dt = kdist.all_reduce_max(time.perf_counter() - t0, info)
