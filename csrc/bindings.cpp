@@ -308,6 +308,24 @@ void pack_grads(const at::Tensor& chunks, const at::Tensor& src_ptrs, at::Tensor
             "pack_tensors");
 }
 
+// the same gather with the source pointers in the kernel arguments (<= kPackArgPtrs
+// tensors; 0 = a parameter without a gradient): no device pointer table to upload
+void pack_grads_ptrs(const at::Tensor& chunks, const std::vector<int64_t>& ptrs, at::Tensor dst, double scale) {
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == at::kLong && chunks.dim() == 2 &&
+                  chunks.size(1) == 3 && chunks.is_contiguous(),
+              "pack_grads_ptrs: chunk table must be a contiguous int64 [n, 3] GPU tensor");
+  TORCH_CHECK(static_cast<int>(ptrs.size()) <= kdl::kPackArgPtrs, "pack_grads_ptrs: at most ", kdl::kPackArgPtrs,
+              " tensors (use pack_grads with a device pointer table)");
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "pack_grads_ptrs: dst must be contiguous on GPU");
+  kdl::PackPtrs a{};
+  for (size_t i = 0; i < ptrs.size(); ++i) a.p[i] = reinterpret_cast<const void*>(ptrs[i]);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  check_hip(kdl::pack_tensors(reinterpret_cast<const kdl::PackChunk*>(chunks.data_ptr<int64_t>()),
+                              static_cast<int>(chunks.size(0)), nullptr, dst.data_ptr(), dtype_code(dst),
+                              static_cast<float>(scale), cur_stream(), &a),
+            "pack_tensors");
+}
+
 void transpose_tiles(const at::Tensor& table) {
   static_assert(sizeof(kdl::TransposeTile) == 40, "TransposeTile layout");
   TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 5 &&
@@ -1498,6 +1516,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("p2p_oneshot_max_units", &kdl::p2p_oneshot_max_units, "largest bucket (16-B units) of the one-shot path");
   m.def("p2p_allreduce", &p2p_allreduce, "in-place two-phase all-reduce over IPC-mapped peer buffers");
   m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
+  m.def("pack_grads_ptrs", &pack_grads_ptrs, "pack_grads with the source pointers as kernel arguments");
+  m.attr("pack_arg_ptrs") = kdl::kPackArgPtrs;
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");

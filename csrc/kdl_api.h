@@ -113,8 +113,14 @@ struct TransposeTile {
   int src_ld, dst_ld;
 };
 hipError_t transpose_tiles(const TransposeTile* tiles, int ntiles, hipStream_t s);
+// source pointers as kernel arguments (pack_tensors ``args``): up to this many tensors
+constexpr int kPackArgPtrs = 256;
+struct PackPtrs {
+  const void* p[kPackArgPtrs];
+};
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
-                        int dtype, float scale, hipStream_t s);
+                        int dtype, float scale, hipStream_t s,
+                        const PackPtrs* args = nullptr);
 
 // ---- p2p.hip (two-phase all-reduce over IPC-mapped peer buffers)
 constexpr int kP2PMaxRanks = 8;

@@ -20,12 +20,15 @@
 namespace kdl {
 namespace {
 
-template <typename T>
+// ARGS: the source pointers travel in the kernel arguments (PackPtrs, up to
+// kPackArgPtrs tensors) instead of a device table: no per-step host->device
+// upload of the table (pinned ring + copy + event) before the launch.
+template <typename T, bool ARGS>
 __global__ __launch_bounds__(256) void pack_kernel(const PackChunk* __restrict__ chunks,
-                                                   const int64_t* __restrict__ src_ptrs,
+                                                   const int64_t* __restrict__ src_ptrs, const PackPtrs args,
                                                    T* __restrict__ dst, float scale) {
   const PackChunk c = chunks[blockIdx.x];
-  const T* src = reinterpret_cast<const T*>(src_ptrs[c.tensor]);
+  const T* src = ARGS ? static_cast<const T*>(args.p[c.tensor]) : reinterpret_cast<const T*>(src_ptrs[c.tensor]);
   T* d = dst + c.dst_off;
   constexpr int VEC = 16 / sizeof(T);
   if (src == nullptr) {
@@ -137,14 +140,25 @@ hipError_t transpose_tiles(const TransposeTile* tiles, int ntiles, hipStream_t s
 }
 
 hipError_t pack_tensors(const PackChunk* chunks, int nchunks, const int64_t* src_ptrs, void* dst,
-                        int dtype, float scale, hipStream_t s) {
+                        int dtype, float scale, hipStream_t s, const PackPtrs* args) {
   if (nchunks <= 0) return hipSuccess;
-  if (dtype == 1)
-    hipLaunchKernelGGL((pack_kernel<bf16_t>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs,
-                       static_cast<bf16_t*>(dst), scale);
-  else
-    hipLaunchKernelGGL((pack_kernel<float>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs,
-                       static_cast<float*>(dst), scale);
+  const PackPtrs none{};
+  const PackPtrs& a = args ? *args : none;
+  if (dtype == 1) {
+    if (args)
+      hipLaunchKernelGGL((pack_kernel<bf16_t, true>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs, a,
+                         static_cast<bf16_t*>(dst), scale);
+    else
+      hipLaunchKernelGGL((pack_kernel<bf16_t, false>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs, a,
+                         static_cast<bf16_t*>(dst), scale);
+  } else {
+    if (args)
+      hipLaunchKernelGGL((pack_kernel<float, true>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs, a,
+                         static_cast<float*>(dst), scale);
+    else
+      hipLaunchKernelGGL((pack_kernel<float, false>), dim3(nchunks), dim3(256), 0, s, chunks, src_ptrs, a,
+                         static_cast<float*>(dst), scale);
+  }
   return hipGetLastError();
 }
 

@@ -115,8 +115,13 @@ class GradPacker:
                                         device=sp.device).copy_(g)
                 s.param.grad = g
             ptrs.append(g.data_ptr())
+        ext = _ext.load()
+        if len(ptrs) <= getattr(ext, "pack_arg_ptrs", 0):
+            # pointers in the kernel arguments: no pinned upload, copy or event per call
+            ext.pack_grads_ptrs(self.chunks, ptrs, sp.grad, float(scale))
+            return
         src = self.ring.upload(ptrs)
-        _ext.load().pack_grads(self.chunks, src, sp.grad, float(scale))
+        ext.pack_grads(self.chunks, src, sp.grad, float(scale))
 
 
 class FlatParamSpace:

@@ -186,6 +186,30 @@ def test_pack_grads_matches_views():
             torch.testing.assert_close(view, grads[s.name], atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("nparams", [5, 300])
+def test_pack_grads_pointer_args_and_table(nparams):
+    """<= pack_arg_ptrs tensors: source pointers as kernel arguments; more: the
+    uploaded device table.  Both gather exactly the per-parameter gradients,
+    zeros for a parameter without one."""
+    from kubedl_amd.ops.optim import FlatParamSpace
+    torch.manual_seed(1)
+    ext = _ext()
+    assert (nparams <= ext.pack_arg_ptrs) == (nparams == 5)
+    m = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(3 + i % 7, device="cuda")) for i in range(nparams)])
+    sp = FlatParamSpace(m, grad_mode="pack")
+    for _ in range(2):  # twice: the second call reuses the packer
+        sp.zero_grad()
+        loss = sum((p * (i + 1)).sum() for i, p in enumerate(m) if i % 11 != 3)
+        loss.backward()
+        sp.pack_grads()
+        for i, s in enumerate(sp.slots):
+            view = sp._view(sp.grad, s)
+            if s.param.grad is None:
+                assert torch.count_nonzero(view) == 0
+            else:
+                torch.testing.assert_close(view, s.param.grad, atol=0, rtol=0)
+
+
 def test_bn_workspace_is_self_cleaning():
     """A persistent per-layer workspace (replicated accumulators re-zeroed by the
     finalize kernels) gives the same results on every reuse as a fresh one."""
