@@ -395,15 +395,23 @@ __device__ __forceinline__ void ld4(const T* p, int n, float (&o)[4]) {
 // idle at D = 64), two rows' loads in flight per step.  (Four segments per
 // group in lock step measured slower: 63 vs 33 us at batch 4096.)
 // j / F as umulhi(j, mF), mF = ceil(2^32 / F): exact while j * F < 2^32 (host
-// check) -- no 64-bit division sequence per row.
+// check; mF = 0 selects the 64-bit division) -- no 64-bit division sequence per row.
 // ``ucount`` (optional): the live segment count on the device (U is then the
 // capacity the grid was sized for) -- no host round trip for data-dependent U.
 template <typename T, bool V4>
 __device__ __forceinline__ void seg_row(const T* rows, int64_t jj, uint32_t F, uint32_t mF, int ld, int col0, int D,
                                         int c, int n, float (&v)[4]) {
-  const uint32_t j = static_cast<uint32_t>(jj);
-  const uint32_t bi = __umulhi(j, mF), f = j - bi * F;
-  ld4<T, V4>(rows + static_cast<int64_t>(bi) * ld + col0 + static_cast<int64_t>(f) * D + c, n, v);
+  int64_t bi, f;
+  if (mF != 0) {  // grid-uniform: the umulhi form is exact for this launch
+    const uint32_t j = static_cast<uint32_t>(jj);
+    const uint32_t q = __umulhi(j, mF);
+    bi = q;
+    f = j - q * F;
+  } else {  // j * F may reach 2^32: 64-bit division
+    bi = jj / F;
+    f = jj - bi * F;
+  }
+  ld4<T, V4>(rows + bi * ld + col0 + f * D + c, n, v);
 }
 
 template <typename T, bool V4>
@@ -815,8 +823,9 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
   const bool v4 = D % 4 == 0 && ld % 4 == 0 && col0 % 4 == 0 && reinterpret_cast<uintptr_t>(rows) % (4 * esz) == 0 &&
                   reinterpret_cast<uintptr_t>(out) % 16 == 0;
   // rows j < n = B * F; umulhi division exact while j * F < 2^32
-  const uint32_t mF = static_cast<uint32_t>(((uint64_t(1) << 32) + F - 1) / F);
-  if (static_cast<uint64_t>(nrows) * static_cast<uint64_t>(F) >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
+  // (mF = 0 when j * F can reach 2^32: the kernel divides in 64 bits instead)
+  const bool fast = static_cast<uint64_t>(nrows) * static_cast<uint64_t>(F) < (uint64_t(1) << 32);
+  const uint32_t mF = fast ? static_cast<uint32_t>(((uint64_t(1) << 32) + F - 1) / F) : 0u;
 #define KDL_SEGRED(T, V)                                                                                      \
   hipLaunchKernelGGL((segment_reduce_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, mF, \
                      ld, col0, order, seg, U, D, lg, out, ucount)

@@ -407,6 +407,27 @@ def test_segment_reduce_skewed_with_device_count():
 
 
 @pytest.mark.gpu
+def test_segment_reduce_wide_field_count_divides_in_64_bits():
+    """n * F >= 2^32 (here 2 rows x 70,000 fields): the umulhi division would be
+    wrong for row ids past 2^32 / F, so the kernel takes its 64-bit division."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(4)
+    B, F, D = 2, 70_000, 4
+    n = B * F
+    assert n * F >= 2 ** 32 and n > 2 ** 32 // F
+    ids = torch.randint(0, 997, (n,), device="cuda")
+    uniq, inv = torch.unique(ids, return_inverse=True)
+    order = torch.argsort(inv, stable=True)
+    seg = torch.zeros(len(uniq) + 1, dtype=torch.int64, device="cuda")
+    seg[1:] = torch.cumsum(torch.bincount(inv, minlength=len(uniq)), 0)
+    gx = torch.randn(B, F * D + 8, device="cuda").bfloat16()
+    got = ext.segment_reduce(gx, F, 0, D, order, seg, None)
+    ref = torch.zeros(len(uniq), D, device="cuda").index_add_(0, inv, gx[:, : F * D].reshape(n, D).float())
+    torch.testing.assert_close(got, ref, atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
 def test_ctr_worker_trains_on_gpu():
     from kubedl_amd.workers.xdl_ctr import main
     assert main(["--steps", "20", "--warmup", "2", "--batch", "1024", "--fields", "8", "--vocab", "5000",
