@@ -597,6 +597,27 @@ std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, c
   return {dx, dw, db, dwp, dbp};
 }
 
+void embed_gather_cast(const at::Tensor& table, const at::Tensor& uniq, const at::Tensor& inv, int64_t F,
+                       at::Tensor out, int64_t col0) {
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous() && table.scalar_type() == at::kFloat,
+              "embed_gather_cast: fp32 table [V, D]");
+  TORCH_CHECK(uniq.scalar_type() == at::kLong && inv.scalar_type() == at::kLong && uniq.is_contiguous() &&
+                  inv.is_contiguous() && uniq.numel() >= 1,
+              "embed_gather_cast: int64 uniq / inv");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16, "embed_gather_cast: bf16 out");
+  const int64_t D = table.size(1), n = inv.numel();
+  TORCH_CHECK(F > 0 && n % F == 0 && out.size(0) * F == n && col0 + F * D <= out.size(1), "embed_gather_cast: shapes");
+  TORCH_CHECK(D % 8 == 0 && out.stride(0) % 8 == 0 && col0 % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(table.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "embed_gather_cast: 16-byte rows (D, the out row stride and col0 multiples of 8)");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  check_hip(kdl::embed_gather_cast(table.data_ptr<float>(), uniq.data_ptr<int64_t>(), inv.data_ptr<int64_t>(),
+                                   static_cast<int>(n), static_cast<int>(F), static_cast<int>(D), out.data_ptr(),
+                                   static_cast<int>(out.stride(0)), static_cast<int>(col0), cur_stream()),
+            "embed_gather_cast");
+}
+
 void embed_gather(const at::Tensor& table, const at::Tensor& idx, int64_t F, at::Tensor out, int64_t col0) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous(), "embed_gather: table [V, D]");
   TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous(), "embed_gather: int64 idx");
@@ -1531,6 +1552,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_bce_bwd", &head_bce_bwd, "logit layer backward: (dx, per-block dw partials, per-block db partials)");
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
+  m.def("embed_gather_cast", &embed_gather_cast, "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("dedup_table_slots", &dedup_table_slots, "hash-table slots dedup_csr needs for n ids");
   m.def("csr_from_inverse_only", &csr_from_inverse_only, "CSR (seg, order) of a dedup_csr inverse, positions ascending per id");

@@ -367,6 +367,30 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__
   }
 }
 
+// Fused pull for one owner: out[b, col0 + f*D : +D] = bf16(table[uniq[inv[r]], :]),
+// r = b*F + f -- the fp32 table rows go straight into the bf16 tower input
+// (no [n, D] fp32 gather and no cast pass in between).  A group of 2^lg lanes
+// per row, 8 elements (two 16-B loads, one 16-B store) per lane; D % 8 == 0 and
+// 16-B aligned rows (host-checked).
+__global__ __launch_bounds__(256) void embed_gather_cast_kernel(const float* __restrict__ table,
+                                                                const int64_t* __restrict__ uniq,
+                                                                const int64_t* __restrict__ inv, int n, int F, int D,
+                                                                bf16_t* __restrict__ out, int ld_out, int col0,
+                                                                int lg) {
+  const int r = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
+  if (r >= n) return;
+  const float* src = table + uniq[inv[r]] * static_cast<int64_t>(D);
+  const int b = r / F, f = r - b * F;
+  bf16_t* dst = out + static_cast<int64_t>(b) * ld_out + col0 + static_cast<int64_t>(f) * D;
+  for (int c = gl * 8; c < D; c += 8 << lg) {
+    const float4 v0 = *reinterpret_cast<const float4*>(src + c);
+    const float4 v1 = *reinterpret_cast<const float4*>(src + c + 4);
+    *reinterpret_cast<uint4*>(dst + c) = make_uint4(pack_bf16x2(v0.x, v0.y), pack_bf16x2(v0.z, v0.w),
+                                                    pack_bf16x2(v1.x, v1.y), pack_bf16x2(v1.z, v1.w));
+  }
+}
+
 // 4 consecutive elements -> fp32: one 8-B (bf16) / 16-B (fp32) load when V4
 // (row base and column aligned, host-checked), else element by element up to n
 template <typename T, bool V4>
@@ -803,6 +827,18 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
   else
     hipLaunchKernelGGL((embed_gather_kernel<float>), grid, dim3(256), 0, s, static_cast<const float*>(table), idx, n,
                        F, D, static_cast<float*>(out), ld_out, col0, lg);
+  return hipGetLastError();
+}
+
+hipError_t embed_gather_cast(const float* table, const int64_t* uniq, const int64_t* inv, int n, int F, int D,
+                             void* out, int ld_out, int col0, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (D % 8 || ld_out % 8 || col0 % 8) return hipErrorInvalidValue;
+  int lg = 0;
+  while (lg < 6 && (8 << lg) < D) ++lg;
+  dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(n) << lg) + 255) / 256));
+  hipLaunchKernelGGL(embed_gather_cast_kernel, grid, dim3(256), 0, s, table, uniq, inv, n, F, D,
+                     static_cast<bf16_t*>(out), ld_out, col0, lg);
   return hipGetLastError();
 }
 

@@ -197,6 +197,9 @@ int head_bce_bwd_blocks(int M);
 hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
                         int K, void* dx, float* dw_part, float* db_part, unsigned* cnt, void* dw, void* db,
                         hipStream_t s);
+// out[b, col0 + f*D : +D] = bf16(table[uniq[inv[b*F + f]]]) (fp32 table, bf16 out)
+hipError_t embed_gather_cast(const float* table, const int64_t* uniq, const int64_t* inv, int n, int F, int D,
+                             void* out, int ld_out, int col0, hipStream_t s);
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s);
 // ucount (optional): the live segment count on the device; U is then a capacity

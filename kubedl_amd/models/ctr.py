@@ -451,6 +451,19 @@ class ShardedEmbedding:
         return (self.dedup is not None and ids.numel() > 0 and self.n_own == 1 and
                 (self.world == 1 or self.group is None and not dist.is_initialized()))
 
+    def pull_into(self, ids: torch.Tensor, out: torch.Tensor, F: int, col0: int = 0) -> Optional[torch.Tensor]:
+        """One-owner sync-free pull written straight into the bf16 tower input:
+        ``out[b, col0 + f*D : +D] = table[ids[b*F + f]]`` (csrc/ctr.hip
+        ``embed_gather_cast``: no fp32 [n, D] gather, no cast pass).  Returns the
+        inverse map, or None when this path does not apply (then use ``pull``)."""
+        if not (self._sync_free(ids) and out.dtype == torch.bfloat16 and self.table.dtype == torch.float32
+                and self.dim % 8 == 0 and out.stride(0) % 8 == 0 and col0 % 8 == 0):
+            return None
+        uniq, inv, count, _, _ = self.dedup(ids, csr=False)
+        _ext.load().embed_gather_cast(self.table, uniq, inv, F, out, col0)
+        self._ctx = ("dev", uniq, count)
+        return inv
+
     def pull(self, ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """ids [n] int64 (any, may repeat) -> (unique rows [U, dim], inverse [n]).
         On the sync-free path U is the capacity n: rows past the live count are
@@ -540,18 +553,23 @@ class CTRModel:
     def build_input(self, ids: torch.Tensor, dense: torch.Tensor):
         B = ids.shape[0]
         gids = (ids + self.field_off).reshape(-1)
-        emb_u, inv = self.emb.pull(gids)
         # every column is written below except the pad [k_in, k_pad): zero only that
         x = torch.empty(B, self.k_pad, dtype=self.dtype, device=self.device)
         if self.k_pad > self.k_in:
             x[:, self.k_in:].zero_()
-        emb_u_c = emb_u.to(self.dtype).contiguous()
-        if self.device.type == "cuda" and _ext.available():
-            _ext.load().embed_gather(emb_u_c, inv.contiguous(), self.F, x, 0)
+        inv = self.emb.pull_into(gids, x, self.F, 0) if self.device.type == "cuda" else None
+        if inv is not None:  # fused one-owner pull: table rows -> bf16 input directly
+            U = gids.numel()
         else:
-            x[:, : self.F * self.D] = emb_u_c[inv].reshape(B, self.F * self.D)
+            emb_u, inv = self.emb.pull(gids)
+            U = emb_u.shape[0]
+            emb_u_c = emb_u.to(self.dtype).contiguous()
+            if self.device.type == "cuda" and _ext.available():
+                _ext.load().embed_gather(emb_u_c, inv.contiguous(), self.F, x, 0)
+            else:
+                x[:, : self.F * self.D] = emb_u_c[inv].reshape(B, self.F * self.D)
         x[:, self.F * self.D: self.k_in] = dense.to(self.dtype)
-        return x, inv, emb_u.shape[0]
+        return x, inv, U
 
     def push_grads(self, xgrad: torch.Tensor, inv: torch.Tensor, U: int, scale: float) -> None:
         B = xgrad.shape[0]

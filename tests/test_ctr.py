@@ -428,6 +428,44 @@ def test_segment_reduce_wide_field_count_divides_in_64_bits():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D,col0", [(64, 0), (8, 16), (200, 8)])
+def test_embed_gather_cast_is_the_cast_gather(D, col0):
+    """Fused one-owner pull (csrc/ctr.hip embed_gather_cast): bf16(table[uniq[inv]])
+    written at its column offset, bitwise the gather-then-cast it replaces, and
+    nothing else of the row touched."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(5)
+    V, B, F = 3000, 129, 13
+    table = torch.randn(V, D, device="cuda")
+    ids = torch.randint(0, V, (B * F,), device="cuda")
+    uniq, inv = torch.unique(ids, return_inverse=True)
+    out = torch.full((B, col0 + F * D + 24), 7.0, device="cuda", dtype=torch.bfloat16)
+    ext.embed_gather_cast(table, uniq, inv, F, out, col0)
+    assert torch.equal(out[:, col0: col0 + F * D], table[ids].bfloat16().reshape(B, F * D))
+    assert bool((out[:, :col0] == 7).all()) and bool((out[:, col0 + F * D:] == 7).all())
+
+
+@pytest.mark.gpu
+def test_fused_pull_builds_the_same_input():
+    """CTRModel.build_input through the fused pull == through pull + cast + gather."""
+    from kubedl_amd.models.ctr import CTRModel, ShardedEmbedding
+    torch.manual_seed(6)
+    F, V, D, nd, B = 6, 500, 16, 5, 64
+    emb = ShardedEmbedding(F * V, D, [0], 0, 1, "cuda")
+    model = CTRModel(F, V, D, nd, (64,), emb, "cuda")
+    ids = torch.randint(0, V, (B, F), device="cuda")
+    dense = torch.randn(B, nd, device="cuda")
+    x1, inv1, _ = model.build_input(ids, dense)
+    gids = (ids + model.field_off).reshape(-1)
+    emb_u, inv2 = emb.pull(gids)
+    ref = torch.zeros(B, model.k_pad, dtype=torch.bfloat16, device="cuda")
+    ref[:, : F * D] = emb_u.bfloat16()[inv2].reshape(B, F * D)
+    ref[:, F * D: model.k_in] = dense.bfloat16()
+    assert torch.equal(x1, ref)
+
+
+@pytest.mark.gpu
 def test_ctr_worker_trains_on_gpu():
     from kubedl_amd.workers.xdl_ctr import main
     assert main(["--steps", "20", "--warmup", "2", "--batch", "1024", "--fields", "8", "--vocab", "5000",
