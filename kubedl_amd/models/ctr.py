@@ -568,7 +568,7 @@ class CTRModel:
                 _ext.load().embed_gather(emb_u_c, inv.contiguous(), self.F, x, 0)
             else:
                 x[:, : self.F * self.D] = emb_u_c[inv].reshape(B, self.F * self.D)
-        x[:, self.F * self.D: self.k_in] = dense.to(self.dtype)
+        x[:, self.F * self.D: self.k_in].copy_(dense)  # cast + strided write in one launch
         return x, inv, U
 
     def push_grads(self, xgrad: torch.Tensor, inv: torch.Tensor, U: int, scale: float) -> None:
