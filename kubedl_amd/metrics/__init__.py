@@ -11,10 +11,10 @@ def start_monitoring(port: int, registry=None, addr: str = "127.0.0.1"):
     "monitoring default registry failed" and keeps the manager running.
     ``registry``: anything with a ``.registry`` CollectorRegistry."""
     import logging
-    from prometheus_client import start_http_server
+    from kubedl_amd.metrics.exposition import serve
     reg = registry or default_registry()
     try:
-        server, _thread = start_http_server(port, addr=addr or "0.0.0.0", registry=reg.registry)
+        server = serve(port, addr or "0.0.0.0", reg.registry)
     except OSError as e:
         logging.getLogger("kubedl_amd.metrics").error("monitoring registry on %s:%d failed, err: %s", addr, port, e)
         return None
@@ -33,6 +33,6 @@ def parse_addr(v, default_host: str = "") -> tuple:
 
 
 def render(registry: MetricsRegistry | None = None) -> str:
-    from prometheus_client import generate_latest
+    from kubedl_amd.metrics.exposition import generate_text
     reg = registry or default_registry()
-    return generate_latest(reg.registry).decode()
+    return generate_text(reg.registry).decode()

@@ -60,5 +60,5 @@ class ControllerMetrics:
         self.queue_latency.labels(controller).observe(seconds)
 
     def render(self) -> str:
-        from prometheus_client import generate_latest
-        return generate_latest(self.registry).decode()
+        from kubedl_amd.metrics.exposition import generate_text
+        return generate_text(self.registry).decode()

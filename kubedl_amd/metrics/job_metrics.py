@@ -29,10 +29,11 @@ from __future__ import annotations
 import threading
 from typing import Callable, Dict, List, Optional
 
-from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram
+from prometheus_client import CollectorRegistry, Gauge, Histogram
 from prometheus_client.core import GaugeMetricFamily
 
 from kubedl_amd.api import common as c
+from kubedl_amd.metrics.exposition import BareCounterVec
 
 # The reference's two launch-delay histograms use the Go client's default
 # buckets (prometheus.DefBuckets; pkg/metrics/job_metrics.go:53-60 sets none);
@@ -75,13 +76,14 @@ class MetricsRegistry:
     def __init__(self, registry: Optional[CollectorRegistry] = None):
         self.registry = registry or CollectorRegistry()
         r = self.registry
-        self.created = Counter("kubedl_jobs_created", "Counts number of jobs created", ["kind"], registry=r)
-        self.deleted = Counter("kubedl_jobs_deleted", "Counts number of jobs deleted", ["kind"], registry=r)
-        self.success = Counter("kubedl_jobs_successful", "Counts number of jobs successfully finished",
-                               ["kind"], registry=r)
-        self.failure = Counter("kubedl_jobs_failed", "Counts number of jobs failed", ["kind"], registry=r)
-        self.restart = Counter("kubedl_jobs_restarted", "Counts number of jobs restarted", ["kind"],
-                               registry=r)
+        # client_golang CounterVecs: exported under these exact names (no _total / _created)
+        self.created = BareCounterVec("kubedl_jobs_created", "Counts number of jobs created", ["kind"], registry=r)
+        self.deleted = BareCounterVec("kubedl_jobs_deleted", "Counts number of jobs deleted", ["kind"], registry=r)
+        self.success = BareCounterVec("kubedl_jobs_successful", "Counts number of jobs successfully finished",
+                                      ["kind"], registry=r)
+        self.failure = BareCounterVec("kubedl_jobs_failed", "Counts number of jobs failed", ["kind"], registry=r)
+        self.restart = BareCounterVec("kubedl_jobs_restarted", "Counts number of jobs restarted", ["kind"],
+                                      registry=r)
         self.first_pod_delay = Histogram(
             "kubedl_jobs_first_pod_launch_delay_seconds",
             "Histogram for recording launch delay duration(from job created to first pod running).",

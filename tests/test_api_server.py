@@ -50,7 +50,7 @@ def test_apply_summary_dashboard_metrics(api):
     code, ctype, body = _get(base + "/dashboard")
     assert code == 200 and ctype.startswith("text/html") and "<td>web</td>" in body and "Succeeded" in body
     code, _, body = _get(base + "/metrics")
-    assert 'kubedl_jobs_successful_total{kind="pytorchjob"} 1.0' in body
+    assert 'kubedl_jobs_successful{kind="pytorchjob"} 1.0' in body
     with pytest.raises(urllib.error.HTTPError) as e:
         _get(base + "/api/objects/pytorchjobs/default/nope")
     assert e.value.code == 404

@@ -59,7 +59,7 @@ def test_gang_restart_two_rank_job_resumes(tmp_path):
         assert all(uids1[n] != uids0[n] for n in uids1), (uids0, uids1)
         # resumed from the step-3 checkpoint written before the fault, ran to 5
         assert json.load(open(ck / "latest.json"))["step"] == 5
-        assert m.metrics.registry.get_sample_value("kubedl_jobs_restarted_total", {"kind": "pytorchjob"}) == 1
+        assert m.metrics.registry.get_sample_value("kubedl_jobs_restarted", {"kind": "pytorchjob"}) == 1
     finally:
         m.stop()
         os.environ.pop("KDL_RESTART_BACKOFF_BASE", None)

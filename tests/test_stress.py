@@ -63,9 +63,9 @@ def test_concurrent_submits_gang_and_reconcile_workers(tmp_path):
         assert not [e for loop in m.loops.values() for e in loop.errors], \
             [e for loop in m.loops.values() for e in loop.errors]
         reg = m.metrics
-        assert reg.created.labels("pytorchjob")._value.get() == 16
-        assert reg.success.labels("pytorchjob")._value.get() == 13
-        assert reg.failure.labels("pytorchjob")._value.get() == 3
+        assert reg.created.labels("pytorchjob").get() == 16
+        assert reg.success.labels("pytorchjob").get() == 13
+        assert reg.failure.labels("pytorchjob").get() == 3
         assert all(c.is_succeeded(j["status"]) or c.is_failed(j["status"]) for j in m.store.list("PyTorchJob"))
     finally:
         stop.set()
