@@ -73,7 +73,7 @@ def _spawner():
 
 class _Container:
     __slots__ = ("spec", "name", "pid", "started_at", "restart_count", "last_term", "term",
-                 "next_start", "ready_file", "readiness", "ready_at", "log_path")
+                 "next_start", "ready_file", "readiness", "ready_at", "log_path", "dns_wait_logged")
 
     def __init__(self, spec: dict, ready_file: str, log_path: str):
         self.spec = spec
@@ -88,6 +88,7 @@ class _Container:
         self.readiness = "start"
         self.ready_at: Optional[str] = None
         self.log_path = log_path
+        self.dns_wait_logged = False
 
 
 class PodWorker(threading.Thread):
@@ -105,6 +106,9 @@ class PodWorker(threading.Thread):
         self.job_label = (md.get("labels") or {}).get(c.JOB_NAME_LABEL, "")
         self.containers: List[_Container] = []
         self.start_time = c.now()
+        self.unresolved: List[str] = []
+        # how long a container waits for an unknown <svc>.<ns>.svc peer to appear
+        self.dns_hold_until = time.monotonic() + kubelet.dns_hold_s
 
     # ------------------------------------------------------------ helpers
     def _patch_status(self, fn) -> bool:
@@ -200,7 +204,8 @@ class PodWorker(threading.Thread):
                                   "metadata.uid": md.get("uid", ""), "status.podIP": "127.0.0.1",
                                   "status.hostIP": "127.0.0.1",
                                   "spec.nodeName": self.pod["spec"].get("nodeName", "")}.get(fr, "")
-        raw = self.k.resolver.resolve(self.ns, self.name, raw)
+        raw = self.k.resolver.resolve(self.ns, self.name, raw, self.pod)
+        self.unresolved = self.k.resolver.unresolved(self.ns, raw)
         # paths that are mount points of this container -> their host directories
         for k, v in list(raw.items()):
             if v in mounts:
@@ -247,6 +252,18 @@ class PodWorker(threading.Thread):
             cwd = mounts[wd]
         os.makedirs(cwd, exist_ok=True)
         env, ready = self._env(ctr, mounts, cidx)
+        if self.unresolved and time.monotonic() < self.dns_hold_until:
+            # a peer name no Service, Pod or replica spec of this job accounts for:
+            # the rank would start with an address nothing on the node answers
+            if not cs.dns_wait_logged:
+                with open(cs.log_path, "a") as f:
+                    f.write(f"[kdl-kubelet] {c.now()} holding {cs.name}: unresolved {self.unresolved}\n")
+                cs.dns_wait_logged = True
+            cs.next_start = time.monotonic() + 0.05
+            return False
+        if self.unresolved:
+            with open(cs.log_path, "a") as f:
+                f.write(f"[kdl-kubelet] {c.now()} starting {cs.name} with unresolved {self.unresolved}\n")
         try:
             os.unlink(ready)
         except FileNotFoundError:
@@ -402,6 +419,9 @@ class PodWorker(threading.Thread):
             ics = _Container(ict, "", os.path.join(logs, f"init-{ict.get('name', i)}.log"))
             while not self.deleted.is_set():
                 ok = self._spawn(ics, ict, vols, f"init{i}")
+                if not ok and ics.term is None:  # held on an unresolved peer name
+                    self.deleted.wait(self.k.poll_interval)
+                    continue
                 code = ics.term["exitCode"] if not ok else self._wait_one(ics)
                 if code is None:
                     return  # deleted while running
@@ -509,19 +529,57 @@ def _read_ready(path: str) -> Optional[str]:
 
 
 class ServiceResolver:
-    """Local DNS: ``<svc>[.<ns>[.svc[.<domain>]]][:<port>]`` -> ``127.0.0.1[:<hostPort>]``."""
+    """Local DNS: ``<svc>[.<ns>[.svc[.<domain>]]][:<port>]`` -> ``127.0.0.1[:<hostPort>]``.
+
+    The reference's cluster-spec endpoints are headless-Service DNS names
+    (``controllers/tensorflow/tensorflow.go:120-139``,
+    ``pkg/job_controller/service.go:263-276``) that resolve whenever the peer's
+    Service exists, however late.  Here a rank's env is rendered once, at spawn,
+    so the names cannot depend on which Services / Pods happen to be in the
+    store at that moment: every ``<job>-<rtype>-<i>`` of the owning job's replica
+    specs (``i < replicas``; the names GenGeneralName gives its pods and
+    services) is resolvable from the job object alone, and ``store.host_port``
+    hands each ``(ns, name, port)`` one stable port whoever asks first -- the
+    peer's Service or a rank that names it."""
 
     def __init__(self, store: Store, domain: Optional[str] = None):
         self.store = store
         self.domain = domain if domain is not None else os.environ.get("CUSTOM_CLUSTER_DOMAIN", "")
 
-    def _names(self, ns: str) -> List[str]:
+    def job_names(self, ns: str, pod: Optional[dict]) -> set:
+        """Deterministic endpoint names of ``pod``'s controlling job."""
+        if not pod:
+            return set()
+        from kubedl_amd.api import kinds as _kinds
+        for ref in (pod.get("metadata") or {}).get("ownerReferences") or []:
+            if not ref.get("controller"):
+                continue
+            job = self.store.try_get(ref.get("kind", ""), ns, ref.get("name", ""))
+            if job is None:
+                return set()
+            jname = job["metadata"]["name"]
+            out = set()
+            for rt, spec in _kinds.replica_specs(job).items():
+                n = (spec or {}).get("replicas")
+                for i in range(1 if n is None else int(n)):
+                    out.add(c.gen_general_name(jname, rt.lower(), i))
+            return out
+        return set()
+
+    def _names(self, ns: str, pod: Optional[dict] = None) -> List[str]:
         names = {s["metadata"]["name"] for s in self.store.list("Service", ns)}
         names |= {p["metadata"]["name"] for p in self.store.list("Pod", ns)}
+        names |= self.job_names(ns, pod)
         return sorted(names, key=len, reverse=True)
 
-    def resolve(self, ns: str, pod_name: str, env: Dict[str, str]) -> Dict[str, str]:
-        names = self._names(ns)
+    def unresolved(self, ns: str, env: Dict[str, str]) -> List[str]:
+        """Service DNS names (``<name>.<ns>.svc...``) still left in a rendered env:
+        a peer this node cannot map to a port."""
+        pat = re.compile("(?<![\\w.-])[a-z0-9]([-a-z0-9]*[a-z0-9])?\\." + re.escape(ns) + "\\.svc(?![\\w-])")
+        return sorted({m.group(0) for k, v in env.items() if isinstance(v, str) for m in pat.finditer(v)})
+
+    def resolve(self, ns: str, pod_name: str, env: Dict[str, str], pod: Optional[dict] = None) -> Dict[str, str]:
+        names = self._names(ns, pod)
         if not names:
             return dict(env)
         alts = []
@@ -572,6 +630,7 @@ class Kubelet:
         self.default_grace = default_grace
         self.backoff_base = float(os.environ.get("KDL_RESTART_BACKOFF_BASE", backoff_base))
         self.backoff_max = backoff_max
+        self.dns_hold_s = 30.0
         self.native = _spawner()
         self.resolver = ServiceResolver(store)
         self._workers: Dict[str, PodWorker] = {}
