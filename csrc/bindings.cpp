@@ -599,8 +599,9 @@ std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, c
 
 void embed_gather_cast(const at::Tensor& table, const at::Tensor& uniq, const at::Tensor& inv, int64_t F,
                        at::Tensor out, int64_t col0) {
-  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous() && table.scalar_type() == at::kFloat,
-              "embed_gather_cast: fp32 table [V, D]");
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous() &&
+                  (table.scalar_type() == at::kFloat || table.scalar_type() == at::kBFloat16),
+              "embed_gather_cast: fp32 or bf16 table [V, D]");
   TORCH_CHECK(uniq.scalar_type() == at::kLong && inv.scalar_type() == at::kLong && uniq.is_contiguous() &&
                   inv.is_contiguous() && uniq.numel() >= 1,
               "embed_gather_cast: int64 uniq / inv");
@@ -612,7 +613,8 @@ void embed_gather_cast(const at::Tensor& table, const at::Tensor& uniq, const at
                   reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
               "embed_gather_cast: 16-byte rows (D, the out row stride and col0 multiples of 8)");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
-  check_hip(kdl::embed_gather_cast(table.data_ptr<float>(), uniq.data_ptr<int64_t>(), inv.data_ptr<int64_t>(),
+  check_hip(kdl::embed_gather_cast(table.data_ptr(), table.scalar_type() == at::kBFloat16, uniq.data_ptr<int64_t>(),
+                                   inv.data_ptr<int64_t>(),
                                    static_cast<int>(n), static_cast<int>(F), static_cast<int>(D), out.data_ptr(),
                                    static_cast<int>(out.stride(0)), static_cast<int>(col0), cur_stream()),
             "embed_gather_cast");
@@ -641,7 +643,8 @@ const int* opt_count(const c10::optional<at::Tensor>& t) {
 }
 
 at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64_t D, const at::Tensor& order,
-                          const at::Tensor& seg, const c10::optional<at::Tensor>& ucount) {
+                          const at::Tensor& seg, const c10::optional<at::Tensor>& ucount,
+                          const c10::optional<at::Tensor>& out_rows, const c10::optional<at::Tensor>& out_opt) {
   TORCH_CHECK(rows.is_cuda() && rows.dim() == 2 && rows.stride(1) == 1, "segment_reduce: rows [B, ld]");
   TORCH_CHECK(order.scalar_type() == at::kLong && seg.scalar_type() == at::kLong && order.is_contiguous() &&
                   seg.is_contiguous(),
@@ -649,13 +652,66 @@ at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64
   TORCH_CHECK(order.numel() == rows.size(0) * F && col0 + F * D <= rows.size(1), "segment_reduce: shapes");
   const int64_t U = seg.numel() - 1;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(rows.device());
-  auto out = at::empty({U, D}, rows.options().dtype(at::kFloat));
+  // out_rows / out: segment u's sum lands in out[out_rows[u]] (the exchange send
+  // buffer, rows >= out.size(0) dropped) instead of a fresh [U, D] tensor
+  const bool mapped = out_rows.has_value() && out_rows->defined();
+  TORCH_CHECK(mapped == (out_opt.has_value() && out_opt->defined()), "segment_reduce: out_rows and out go together");
+  at::Tensor out;
+  if (mapped) {
+    out = *out_opt;
+    TORCH_CHECK(out_rows->scalar_type() == at::kLong && out_rows->is_contiguous() && out_rows->numel() >= U,
+                "segment_reduce: int64 out_rows [U]");
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 2 &&
+                    out.size(1) == D,
+                "segment_reduce: fp32 out [rows, D]");
+  } else {
+    out = at::empty({U, D}, rows.options().dtype(at::kFloat));
+  }
   check_hip(kdl::segment_reduce(rows.data_ptr(), dtype_code(rows), static_cast<int>(F), static_cast<int>(rows.stride(0)),
                                 static_cast<int>(col0), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
                                 static_cast<int>(U), static_cast<int>(D), out.data_ptr<float>(), cur_stream(),
-                                opt_count(ucount), order.numel()),
+                                opt_count(ucount), order.numel(), mapped ? out_rows->data_ptr<int64_t>() : nullptr,
+                                mapped ? out.size(0) : 0),
             "segment_reduce");
   return out;
+}
+
+// Fixed-capacity exchange routing (csrc/ctr.hip a2a_route): send [W * (cap + 1)]
+// int64 and rslot [n] int64 are written; count: int32 [1] live ids (or None = n)
+void a2a_route(const at::Tensor& uniq, const c10::optional<at::Tensor>& count, const at::Tensor& owner_rank,
+               int64_t W, int64_t cap, at::Tensor send, at::Tensor rslot) {
+  TORCH_CHECK(uniq.is_cuda() && uniq.scalar_type() == at::kLong && uniq.is_contiguous(), "a2a_route: int64 uniq");
+  TORCH_CHECK(owner_rank.scalar_type() == at::kLong && owner_rank.is_contiguous() && owner_rank.numel() >= 1,
+              "a2a_route: int64 owner_rank");
+  TORCH_CHECK(W >= 1 && W <= kdl::a2a_max_world() && cap >= 1, "a2a_route: 1 <= W <= ", kdl::a2a_max_world());
+  TORCH_CHECK(send.scalar_type() == at::kLong && send.is_contiguous() && send.numel() >= W * (cap + 1),
+              "a2a_route: int64 send [W * (cap + 1)]");
+  const int64_t n = uniq.numel();
+  TORCH_CHECK(rslot.scalar_type() == at::kLong && rslot.is_contiguous() && rslot.numel() >= n, "a2a_route: rslot [n]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(uniq.device());
+  auto cnt = at::empty({kdl::a2a_route_blocks(static_cast<int>(n)) * W}, uniq.options().dtype(at::kInt));
+  check_hip(kdl::a2a_route(uniq.data_ptr<int64_t>(), opt_count(count), static_cast<int>(n),
+                           owner_rank.data_ptr<int64_t>(), static_cast<int>(owner_rank.numel()), static_cast<int>(W),
+                           static_cast<int>(cap), cnt.data_ptr<int>(), send.data_ptr<int64_t>(),
+                           rslot.data_ptr<int64_t>(), cur_stream()),
+            "a2a_route");
+}
+
+// owner side: (rows [n, D] fp32, local [n] int64) for the requested ids req [n]
+std::vector<at::Tensor> a2a_serve(const at::Tensor& table, const at::Tensor& req, int64_t n_own, bool rows_bf16) {
+  TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous() && table.scalar_type() == at::kFloat &&
+                  table.size(1) % 4 == 0 && reinterpret_cast<uintptr_t>(table.data_ptr()) % 16 == 0,
+              "a2a_serve: fp32 table [V, D], D % 4 == 0");
+  TORCH_CHECK(req.scalar_type() == at::kLong && req.is_contiguous(), "a2a_serve: int64 req");
+  const int64_t n = req.numel(), D = table.size(1);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  auto rows = at::empty({n, D}, table.options().dtype(rows_bf16 ? at::kBFloat16 : at::kFloat));
+  auto local = at::empty({n}, req.options());
+  check_hip(kdl::a2a_serve(table.data_ptr<float>(), req.data_ptr<int64_t>(), static_cast<int>(n),
+                           static_cast<int>(n_own), static_cast<int>(D), rows.data_ptr(), rows_bf16,
+                           local.data_ptr<int64_t>(), cur_stream()),
+            "a2a_serve");
+  return {rows, local};
 }
 
 void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at::Tensor& seg,
@@ -1551,7 +1607,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_bce_fwd", &head_bce_fwd, "1-wide logit layer + sigmoid BCE: (logit, dlogit, per-block loss sums)");
   m.def("head_bce_bwd", &head_bce_bwd, "logit layer backward: (dx, per-block dw partials, per-block db partials)");
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
-  m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows");
+  m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows", py::arg("rows"), py::arg("F"),
+        py::arg("col0"), py::arg("D"), py::arg("order"), py::arg("seg"), py::arg("ucount") = py::none(),
+        py::arg("out_rows") = py::none(), py::arg("out") = py::none());
+  m.def("a2a_route", &a2a_route, "fixed-capacity exchange: per-owner send blocks + header + rslot of unique ids");
+  m.def("a2a_serve", &a2a_serve, "owner side of the fixed exchange: requested rows + local row ids",
+        py::arg("table"), py::arg("req"), py::arg("n_own"), py::arg("rows_bf16") = false);
   m.def("embed_gather_cast", &embed_gather_cast, "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("dedup_table_slots", &dedup_table_slots, "hash-table slots dedup_csr needs for n ids");

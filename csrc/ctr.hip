@@ -371,8 +371,10 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__
 // r = b*F + f -- the fp32 table rows go straight into the bf16 tower input
 // (no [n, D] fp32 gather and no cast pass in between).  A group of 2^lg lanes
 // per row, 8 elements (two 16-B loads, one 16-B store) per lane; D % 8 == 0 and
-// 16-B aligned rows (host-checked).
-__global__ __launch_bounds__(256) void embed_gather_cast_kernel(const float* __restrict__ table,
+// 16-B aligned rows (host-checked).  T = bf16: the rows are already bf16 (the
+// fixed exchange's received rows, rounded once by their owner): one 16-B copy.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_gather_cast_kernel(const T* __restrict__ table,
                                                                 const int64_t* __restrict__ uniq,
                                                                 const int64_t* __restrict__ inv, int n, int F, int D,
                                                                 bf16_t* __restrict__ out, int ld_out, int col0,
@@ -380,14 +382,18 @@ __global__ __launch_bounds__(256) void embed_gather_cast_kernel(const float* __r
   const int r = (blockIdx.x * 256 + threadIdx.x) >> lg;
   const int gl = threadIdx.x & ((1 << lg) - 1);
   if (r >= n) return;
-  const float* src = table + uniq[inv[r]] * static_cast<int64_t>(D);
+  const T* src = table + uniq[inv[r]] * static_cast<int64_t>(D);
   const int b = r / F, f = r - b * F;
   bf16_t* dst = out + static_cast<int64_t>(b) * ld_out + col0 + static_cast<int64_t>(f) * D;
   for (int c = gl * 8; c < D; c += 8 << lg) {
-    const float4 v0 = *reinterpret_cast<const float4*>(src + c);
-    const float4 v1 = *reinterpret_cast<const float4*>(src + c + 4);
-    *reinterpret_cast<uint4*>(dst + c) = make_uint4(pack_bf16x2(v0.x, v0.y), pack_bf16x2(v0.z, v0.w),
-                                                    pack_bf16x2(v1.x, v1.y), pack_bf16x2(v1.z, v1.w));
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(src + c);
+    } else {
+      const float4 v0 = *reinterpret_cast<const float4*>(src + c);
+      const float4 v1 = *reinterpret_cast<const float4*>(src + c + 4);
+      *reinterpret_cast<uint4*>(dst + c) = make_uint4(pack_bf16x2(v0.x, v0.y), pack_bf16x2(v0.z, v0.w),
+                                                      pack_bf16x2(v1.x, v1.y), pack_bf16x2(v1.z, v1.w));
+    }
   }
 }
 
@@ -442,10 +448,15 @@ template <typename T, bool V4>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, uint32_t mF, int ld,
                                                              int col0, const int64_t* __restrict__ order,
                                                              const int64_t* __restrict__ seg, int U, int D, int lg,
-                                                             float* __restrict__ out, const int* __restrict__ ucount) {
+                                                             float* __restrict__ out, const int* __restrict__ ucount,
+                                                             const int64_t* __restrict__ out_row, int64_t out_lim) {
   const int u = (blockIdx.x * 256 + threadIdx.x) >> lg;
   const int gl = threadIdx.x & ((1 << lg) - 1);
   if (u >= (ucount ? *ucount : U)) return;
+  // out_row: segment u's sum goes to row out_row[u] of the exchange send buffer
+  // (rows >= out_lim: the id did not fit the capacity -- nothing to send)
+  const int64_t orow = out_row ? out_row[u] : u;
+  if (orow >= out_lim) return;
   const int64_t s0 = seg[u], s1 = seg[u + 1];
   for (int c = gl * 4; c < D; c += 4 << lg) {
     const int n = D - c < 4 ? D - c : 4;
@@ -465,7 +476,7 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict
 #pragma unroll
       for (int k = 0; k < 4; ++k) a[k] += v0[k];
     }
-    float* o = out + static_cast<int64_t>(u) * D + c;
+    float* o = out + orow * D + c;
     if (V4) {
       *reinterpret_cast<float4*>(o) = make_float4(a[0], a[1], a[2], a[3]);
     } else {
@@ -830,15 +841,19 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
   return hipGetLastError();
 }
 
-hipError_t embed_gather_cast(const float* table, const int64_t* uniq, const int64_t* inv, int n, int F, int D,
-                             void* out, int ld_out, int col0, hipStream_t s) {
+hipError_t embed_gather_cast(const void* table, bool table_bf16, const int64_t* uniq, const int64_t* inv, int n,
+                             int F, int D, void* out, int ld_out, int col0, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (D % 8 || ld_out % 8 || col0 % 8) return hipErrorInvalidValue;
   int lg = 0;
   while (lg < 6 && (8 << lg) < D) ++lg;
   dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(n) << lg) + 255) / 256));
-  hipLaunchKernelGGL(embed_gather_cast_kernel, grid, dim3(256), 0, s, table, uniq, inv, n, F, D,
-                     static_cast<bf16_t*>(out), ld_out, col0, lg);
+  if (table_bf16)
+    hipLaunchKernelGGL(embed_gather_cast_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(table),
+                       uniq, inv, n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg);
+  else
+    hipLaunchKernelGGL(embed_gather_cast_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(table), uniq,
+                       inv, n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg);
   return hipGetLastError();
 }
 
@@ -851,8 +866,9 @@ static int seg_lanes_log2(int D) {
 
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
                           const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount,
-                          int64_t nrows) {
+                          int64_t nrows, const int64_t* out_row, int64_t out_lim) {
   if (U <= 0 || nrows <= 0) return hipSuccess;
+  if (!out_row) out_lim = U;
   const int lg = seg_lanes_log2(D);
   dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(U) << lg) + 255) / 256));
   const size_t esz = dtype == 1 ? 2 : 4;
@@ -864,7 +880,7 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
   const uint32_t mF = fast ? static_cast<uint32_t>(((uint64_t(1) << 32) + F - 1) / F) : 0u;
 #define KDL_SEGRED(T, V)                                                                                      \
   hipLaunchKernelGGL((segment_reduce_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, mF, \
-                     ld, col0, order, seg, U, D, lg, out, ucount)
+                     ld, col0, order, seg, U, D, lg, out, ucount, out_row, out_lim)
   if (dtype == 1) {
     if (v4) KDL_SEGRED(bf16_t, true);
     else KDL_SEGRED(bf16_t, false);
@@ -1176,7 +1192,163 @@ __global__ __launch_bounds__(256) void csr_sort_long_kernel(const int64_t* __res
     }
   }
 }
+// ---------------------------------------------------------------- fixed-capacity exchange (PS + worker)
+// A pull of U de-duplicated ids at a capacity ``cap`` every rank agrees on
+// (models/ctr.py ShardedEmbedding._pull_fixed): the send buffer holds one
+// block of cap + 1 int64 slots per destination rank -- the ids owned by that
+// rank (owner = owner_rank[id % n_own]) in slots [0, fill), -1 padding up to
+// cap, and in slot cap the header: this sender's largest per-destination fill
+// (the same value in every block).  rslot[i] = d * cap + pos names the row of
+// the received [W * cap] rows that answers unique id i (W * cap = the zero
+// dump row: the id did not fit, or i >= *count).  Ids keep their unique order
+// within a destination (a block-stable counting sort: per-block counts, then
+// every block sums the earlier blocks' counts itself), so the route is a pure
+// function of uniq.  Two launches, no host sync, no one-hot [U, W + 1] matrix.
+constexpr int kA2aMaxW = 64;
+
+__global__ __launch_bounds__(256) void a2a_count_kernel(const int64_t* __restrict__ uniq,
+                                                        const int* __restrict__ count, int n,
+                                                        const int64_t* __restrict__ owner_rank, int n_own, int W,
+                                                        int* __restrict__ cnt) {
+  __shared__ int c[kA2aMaxW];
+  for (int d = threadIdx.x; d < W; d += 256) c[d] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int live = count ? *count : n;
+  if (i < n && i < live) atomicAdd(&c[owner_rank[uniq[i] % n_own]], 1);  // LDS counts: order-free
+  __syncthreads();
+  for (int d = threadIdx.x; d < W; d += 256) cnt[blockIdx.x * W + d] = c[d];
+}
+
+__global__ __launch_bounds__(256) void a2a_route_kernel(const int64_t* __restrict__ uniq,
+                                                        const int* __restrict__ count, int n,
+                                                        const int64_t* __restrict__ owner_rank, int n_own, int W,
+                                                        int cap, const int* __restrict__ cnt, int nblk,
+                                                        int64_t* __restrict__ send, int64_t* __restrict__ rslot) {
+  __shared__ int base[kA2aMaxW], tot[kA2aMaxW], wcnt[4][kA2aMaxW];
+  __shared__ int red[4][2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // totals per destination and this block's exclusive base: all threads stride
+  // the per-block counts, wave sums, then the four waves in LDS
+  for (int d = 0; d < W; ++d) {
+    int sb = 0, st = 0;
+    for (int b = t; b < nblk; b += 256) {
+      const int v = cnt[b * W + d];
+      st += v;
+      sb += b < static_cast<int>(blockIdx.x) ? v : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      sb += __shfl_xor(sb, o);
+      st += __shfl_xor(st, o);
+    }
+    if (lane == 0) { red[wv][0] = sb; red[wv][1] = st; }
+    __syncthreads();
+    if (t == 0) {
+      base[d] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+      tot[d] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    }
+    __syncthreads();
+  }
+  for (int k = t; k < 4 * kA2aMaxW; k += 256) (&wcnt[0][0])[k] = 0;
+  const int i = blockIdx.x * 256 + t;
+  const int live = count ? *count : n;
+  const bool valid = i < n && i < live;
+  const int64_t id = valid ? uniq[i] : 0;
+  const int d = valid ? static_cast<int>(owner_rank[id % n_own]) : -1;
+  // lanes of this wave with the same destination (stable: lane order = id order)
+  uint64_t same = 0;
+  uint64_t todo = __ballot(valid);
+  while (todo) {
+    const int leader = __ffsll(static_cast<unsigned long long>(todo)) - 1;
+    const int dl = __shfl(d, leader);
+    const uint64_t m = __ballot(d == dl);
+    if (d == dl) same = m;
+    todo &= ~m;
+  }
+  __syncthreads();  // wcnt zeroed
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  if (valid && (same & below) == 0) wcnt[wv][d] = __popcll(same);  // the lowest lane of its group
+  __syncthreads();
+  if (i < n) {
+    int64_t slot = static_cast<int64_t>(W) * cap;  // dump row
+    if (valid) {
+      int pos = base[d] + __popcll(same & below);
+      for (int w = 0; w < wv; ++w) pos += wcnt[w][d];
+      if (pos < cap) {
+        send[static_cast<int64_t>(d) * (cap + 1) + pos] = id;
+        slot = static_cast<int64_t>(d) * cap + pos;
+      }
+    }
+    rslot[i] = slot;
+  }
+  // padding and headers of every destination block, spread over the grid
+  int hdr = 0;
+  for (int e = 0; e < W; ++e) hdr = tot[e] > hdr ? tot[e] : hdr;
+  const int64_t slots = static_cast<int64_t>(W) * (cap + 1);
+  for (int64_t s = static_cast<int64_t>(blockIdx.x) * 256 + t; s < slots; s += static_cast<int64_t>(gridDim.x) * 256) {
+    const int dd = static_cast<int>(s / (cap + 1));
+    const int p = static_cast<int>(s - static_cast<int64_t>(dd) * (cap + 1));
+    if (p == cap) send[s] = hdr;
+    else if (p >= (tot[dd] < cap ? tot[dd] : cap)) send[s] = -1;
+  }
+}
+
+// Owner side of a fixed exchange: the W * cap requested ids (-1 = padding) ->
+// the rows to send back (padding rows zero) and the local row index of every
+// slot for the push's update (padding -> distinct negative sentinels -2 - r:
+// one-row segments the update skips).  One lane group of 2^lg lanes per slot.
+template <typename T>
+__global__ __launch_bounds__(256) void a2a_serve_kernel(const float* __restrict__ table, const int64_t* __restrict__ req,
+                                                        int n, int n_own, int D, int lg, T* __restrict__ rows,
+                                                        int64_t* __restrict__ local) {
+  const int r = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
+  if (r >= n) return;
+  const int64_t id = req[r];
+  const int64_t row = id >= 0 ? id / n_own : -2 - static_cast<int64_t>(r);
+  if (gl == 0) local[r] = row;
+  T* dst = rows + static_cast<int64_t>(r) * D;
+  const float* src = table + (row >= 0 ? row : 0) * static_cast<int64_t>(D);
+  for (int c = gl * 4; c < D; c += 4 << lg) {
+    const float4 v = row >= 0 ? *reinterpret_cast<const float4*>(src + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (sizeof(T) == 2)  // the bf16 rounding the tower input gets anyway, done once by the owner
+      *reinterpret_cast<uint2*>(dst + c) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+    else
+      *reinterpret_cast<float4*>(dst + c) = v;
+  }
+}
+
 }  // namespace
+
+int a2a_max_world() { return kA2aMaxW; }
+
+hipError_t a2a_route(const int64_t* uniq, const int* count, int n, const int64_t* owner_rank, int n_own, int W,
+                     int cap, int* cnt, int64_t* send, int64_t* rslot, hipStream_t s) {
+  if (W < 1 || W > kA2aMaxW || cap < 1 || n_own < 1 || n < 0) return hipErrorInvalidValue;
+  const int nblk = n > 0 ? (n + 255) / 256 : 1;
+  hipLaunchKernelGGL(a2a_count_kernel, dim3(nblk), dim3(256), 0, s, uniq, count, n, owner_rank, n_own, W, cnt);
+  hipLaunchKernelGGL(a2a_route_kernel, dim3(nblk), dim3(256), 0, s, uniq, count, n, owner_rank, n_own, W, cap, cnt,
+                     nblk, send, rslot);
+  return hipGetLastError();
+}
+
+int a2a_route_blocks(int n) { return n > 0 ? (n + 255) / 256 : 1; }
+
+hipError_t a2a_serve(const float* table, const int64_t* req, int n, int n_own, int D, void* rows, bool rows_bf16,
+                     int64_t* local, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (D % 4 || n_own < 1) return hipErrorInvalidValue;
+  const int lg = seg_lanes_log2(D);
+  dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(n) << lg) + 255) / 256));
+  if (rows_bf16)
+    hipLaunchKernelGGL(a2a_serve_kernel<bf16_t>, grid, dim3(256), 0, s, table, req, n, n_own, D, lg,
+                       static_cast<bf16_t*>(rows), local);
+  else
+    hipLaunchKernelGGL(a2a_serve_kernel<float>, grid, dim3(256), 0, s, table, req, n, n_own, D, lg,
+                       static_cast<float*>(rows), local);
+  return hipGetLastError();
+}
 
 int dedup_table_slots(int n) {
   int T = 1024;

@@ -198,14 +198,27 @@ hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float
                         int K, void* dx, float* dw_part, float* db_part, unsigned* cnt, void* dw, void* db,
                         hipStream_t s);
 // out[b, col0 + f*D : +D] = bf16(table[uniq[inv[b*F + f]]]) (fp32 table, bf16 out)
-hipError_t embed_gather_cast(const float* table, const int64_t* uniq, const int64_t* inv, int n, int F, int D,
-                             void* out, int ld_out, int col0, hipStream_t s);
+hipError_t embed_gather_cast(const void* table, bool table_bf16, const int64_t* uniq, const int64_t* inv, int n,
+                             int F, int D, void* out, int ld_out, int col0, hipStream_t s);
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s);
 // ucount (optional): the live segment count on the device; U is then a capacity
 hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
                           const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount,
-                          int64_t nrows);  // nrows = order's length (B * F)
+                          int64_t nrows,  // nrows = order's length (B * F)
+                          const int64_t* out_row = nullptr, int64_t out_lim = 0);  // out row of segment u (< out_lim)
+// Fixed-capacity embedding exchange (models/ctr.py _pull_fixed / _push_fixed):
+// route n unique ids (first *count live) to W destination blocks of cap + 1
+// slots (send [W * (cap + 1)]: ids, -1 padding, header = the largest fill) and
+// rslot [n] (d * cap + pos, W * cap = dump); cnt: a2a_route_blocks(n) * W ints.
+int a2a_max_world();
+int a2a_route_blocks(int n);
+hipError_t a2a_route(const int64_t* uniq, const int* count, int n, const int64_t* owner_rank, int n_own, int W,
+                     int cap, int* cnt, int64_t* send, int64_t* rslot, hipStream_t s);
+// owner side: rows [n, D] = table[req / n_own] (zero for req < 0; fp32 or bf16),
+// local [n] = req / n_own or -2 - r
+hipError_t a2a_serve(const float* table, const int64_t* req, int n, int n_own, int D, void* rows, bool rows_bf16,
+                     int64_t* local, hipStream_t s);
 // rows_local outside [0, nrows) are skipped (exchange padding sentinels)
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
                            int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,

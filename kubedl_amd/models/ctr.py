@@ -237,7 +237,7 @@ class ShardedEmbedding:
 
     def __init__(self, vocab: int, dim: int, owners: List[int], rank: int, world: int, device,
                  group=None, lr: float = 0.05, eps: float = 1e-8, init_std: float = 0.01, seed: int = 0,
-                 max_ids: Optional[int] = None, slack: Optional[float] = None):
+                 max_ids: Optional[int] = None, slack: Optional[float] = None, force_fixed: bool = False):
         self.vocab, self.dim = vocab, dim
         self.owners = list(owners)
         self.n_own = len(owners)
@@ -260,23 +260,27 @@ class ShardedEmbedding:
         # every owner a slot block of ``cap`` ids (+ one header slot), so
         # all_to_all_single runs with equal splits and no per-step size exchange
         # to the host.  ``max_ids`` = the per-pull id bound every rank knows from
-        # the job config (batch x fields) -- the first steps run at cap = max_ids
-        # (cannot overflow).  The header carries the sender's largest
-        # per-owner fill, so after the id exchange every rank holds the same
-        # global max fill; LAG steps later (its pinned copy long landed) every
-        # rank reads it and resizes ``cap`` by the same rule to ``slack`` x the
-        # recent max fill (KDL_CTR_A2A_SLACK, default 1.5; <= 0 keeps max_ids).
-        # A step whose fill exceeds its cap (the id distribution shifted within
-        # LAG steps) drops the excess ids to a dump slot: their rows read as
-        # zeros and their gradients are lost FOR THAT STEP; the overflow is
-        # counted (``overflow_steps``, raised with KDL_CTR_A2A_STRICT=1), the
-        # capacity grows, and ``finalize()`` reports the last steps too.
+        # the job config (batch x fields).  By default cap = max_ids for the whole
+        # run: exact, an overflow is impossible.  Adaptive capacity is opt-in
+        # (``slack`` / KDL_CTR_A2A_SLACK > 0): the header carries the sender's
+        # largest per-owner fill, so after the id exchange every rank holds the
+        # same global max fill; LAG steps later (its pinned copy long landed)
+        # every rank reads it and resizes ``cap`` by the same rule to slack x the
+        # recent max fill.  A step whose fill exceeds its cap (the id distribution
+        # shifted within LAG steps) would drop the excess ids to a dump slot --
+        # their rows read as zeros and their gradients are lost for that step --
+        # so an overflow RAISES (the rank exits non-zero) unless lossy mode is
+        # asked for explicitly (KDL_CTR_A2A_STRICT=0: counted in
+        # ``overflow_steps``, reported by ``finalize()``, capacity doubled).
+        # ``force_fixed``: take this exchange at world 1 too (the one-GPU
+        # rehearsal of the PS + worker path; RCCL all-to-alls on a 1-rank group).
+        self.force_fixed = bool(force_fixed)
         self.max_ids = max_ids
         if max_ids is not None:
-            sl = slack if slack is not None else float(os.environ.get("KDL_CTR_A2A_SLACK", "1.5") or 0)
+            sl = slack if slack is not None else float(os.environ.get("KDL_CTR_A2A_SLACK", "0") or 0)
             self.slack = sl
             self.cap = max(int(max_ids), 1)
-            self.strict = os.environ.get("KDL_CTR_A2A_STRICT", "0") == "1"
+            self.strict = os.environ.get("KDL_CTR_A2A_STRICT", "1") != "0"
             self._owner_rank = torch.tensor(self.owners, dtype=torch.int64, device=self.device)
             self._fills = collections.deque(maxlen=self.FILL_WINDOW)  # agreed max fills, oldest first
             self._pending = collections.deque()  # (cap used, pinned fill, event) per pull not yet read
@@ -354,7 +358,9 @@ class ShardedEmbedding:
                 self.overflow_steps += 1
                 if self.strict:
                     raise RuntimeError(f"CTR exchange overflow: {fill} ids for one owner > capacity {cap_used} "
-                                       f"(KDL_CTR_A2A_SLACK={self.slack}); that step's excess rows were dropped")
+                                       f"(KDL_CTR_A2A_SLACK={self.slack}); that step's excess rows were dropped. "
+                                       f"Run with a larger slack, KDL_CTR_A2A_SLACK=0 (exact), or accept "
+                                       f"lossy steps with KDL_CTR_A2A_STRICT=0")
             changed = True
         if not changed or self.slack <= 0 or drain:
             return
@@ -368,13 +374,17 @@ class ShardedEmbedding:
     def finalize(self) -> dict:
         """Read every outstanding agreed fill (syncs): call after the last step so
         an overflow in the final LAG pulls is counted (and raised if strict)."""
-        if self.max_ids is not None and self.world > 1:
+        if self._fixed():
             self._agree(drain=True)
             return {"exchange_cap": self.cap, "exchange_overflow_steps": self.overflow_steps,
                     "exchange_bytes": self.exchange_bytes}
         return {}
 
-    def _pull_fixed(self, ids: torch.Tensor):
+    def _pull_fixed(self, ids: torch.Tensor, rows_bf16: bool = False):
+        """The fixed-capacity exchange of a pull -> (received rows [W * cap + 1, dim]
+        (the last row zero), rslot [n], inverse [n]).  ``rows_bf16``: the rows
+        travel as bf16 (the caller casts them to the bf16 tower input anyway:
+        the owner rounds once, bit-identical, half the bytes)."""
         self._agree()
         W, cap, dev = self.world, self.cap, self.device
         n = ids.numel()
@@ -382,20 +392,28 @@ class ShardedEmbedding:
             raise ValueError(f"pull of {n} ids > max_ids {self.max_ids}")
         # id blocks of cap + 1 slots per destination; slot cap = header (the
         # sender's largest per-owner fill, the same value to every destination)
-        send = torch.full((W * (cap + 1) + 1,), -1, dtype=torch.int64, device=dev)
         uniq, inv, count = self._dedup_any(ids)
-        if n:
-            valid = torch.arange(n, device=dev) < count.to(torch.int64)
-            dest = torch.where(valid, self._owner_rank[uniq % self.n_own], torch.full_like(uniq, W))
-            onehot = torch.zeros(n, W + 1, dtype=torch.int64, device=dev).scatter_(1, dest[:, None], 1)
-            pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None]).squeeze(1)
-            ok = valid & (pos < cap)
-            rslot = torch.where(ok, dest * cap + pos, torch.full_like(pos, W * cap))  # W * cap: dump slot
-            send.scatter_(0, torch.where(ok, dest * (cap + 1) + pos, torch.full_like(pos, W * (cap + 1))), uniq)
-            send[cap: W * (cap + 1): cap + 1] = onehot[:, :W].sum(0).max()
+        if self.use_hip:
+            # csrc/ctr.hip a2a_route: a block-stable counting sort of the unique ids
+            # by owner straight into the send blocks, padding and headers written by
+            # the same launch; no one-hot [n, W + 1], no fill of the send buffer
+            send = torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
+            rslot = torch.empty(n, dtype=torch.int64, device=dev)
+            _ext.load().a2a_route(uniq, count if n else None, self._owner_rank, W, cap, send, rslot)
         else:
-            rslot = torch.empty(0, dtype=torch.int64, device=dev)
-            send[cap: W * (cap + 1): cap + 1] = 0
+            send = torch.full((W * (cap + 1) + 1,), -1, dtype=torch.int64, device=dev)
+            if n:
+                valid = torch.arange(n, device=dev) < count.to(torch.int64)
+                dest = torch.where(valid, self._owner_rank[uniq % self.n_own], torch.full_like(uniq, W))
+                onehot = torch.zeros(n, W + 1, dtype=torch.int64, device=dev).scatter_(1, dest[:, None], 1)
+                pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None]).squeeze(1)
+                ok = valid & (pos < cap)
+                rslot = torch.where(ok, dest * cap + pos, torch.full_like(pos, W * cap))  # W * cap: dump slot
+                send.scatter_(0, torch.where(ok, dest * (cap + 1) + pos, torch.full_like(pos, W * (cap + 1))), uniq)
+                send[cap: W * (cap + 1): cap + 1] = onehot[:, :W].sum(0).max()
+            else:
+                rslot = torch.empty(0, dtype=torch.int64, device=dev)
+                send[cap: W * (cap + 1): cap + 1] = 0
         recv = torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
         dist.all_to_all_single(recv, send[: W * (cap + 1)], group=self.group)  # equal splits: no size exchange
         rv = recv.view(W, cap + 1)
@@ -409,32 +427,63 @@ class ShardedEmbedding:
         else:
             host, evt = fill.clone(), None
         self._pending.append((cap, host, evt))
-        if self.is_owner:
+        local = None
+        if self.is_owner and self.use_hip:
+            # csrc/ctr.hip a2a_serve: requested rows (padding rows zero) + every
+            # slot's local row for the push (padding -> distinct negative sentinels)
+            rows, local = _ext.load().a2a_serve(self.table, req, self.n_own, rows_bf16)
+        elif self.is_owner:
             rows = self._local_gather(torch.where(req >= 0, req // self.n_own, torch.zeros_like(req)))
+        elif self.use_hip:  # no id is routed to a non-owner: never read
+            rows = torch.empty(W * cap, self.dim, device=dev, dtype=torch.bfloat16 if rows_bf16 else torch.float32)
         else:
             rows = torch.zeros(W * cap, self.dim, device=dev)
-        got = torch.empty(W * cap + 1, self.dim, device=dev)
-        got[W * cap].zero_()
+        got = self._got_buffer(W * cap, rows.dtype)
         dist.all_to_all_single(got[: W * cap], rows.contiguous(), group=self.group)
-        emb = got[rslot] if n else got[:0]
-        self.exchange_bytes += W * (cap + 1) * 8 + W * cap * self.dim * 4
-        self._ctx = ("fixed", rslot, req, count, cap)
-        return emb, inv
+        self.exchange_bytes += W * (cap + 1) * 8 + W * cap * self.dim * rows.element_size()
+        self._ctx = ("fixed", rslot, req, count, cap, local)
+        return got, rslot, inv
+
+    def _got_buffer(self, rows: int, dtype) -> torch.Tensor:
+        """[rows + 1, dim] receive buffer of the row exchange; row ``rows`` is the
+        zero row every dump slot reads (kept zero: the exchange writes [:rows])."""
+        g = getattr(self, "_got", None)
+        if g is None or g.shape[0] != rows + 1 or g.dtype != dtype:
+            g = self._got = torch.empty(rows + 1, self.dim, device=self.device, dtype=dtype)
+            g[rows].zero_()
+        return g
+
+    def fixed_send_buffer(self, dump_row: bool = False) -> torch.Tensor:
+        """[W * cap (+1), dim] gradient send buffer of the last fixed pull.  On the
+        GPU rows no id was routed to stay unwritten: their slots are padding the
+        owner never reads (no W * cap x dim zero fill).  ``dump_row``: one extra
+        row past the exchange for ids that did not fit."""
+        rows = self.world * self._ctx[4] + (1 if dump_row else 0)
+        if self.use_hip:
+            return torch.empty(rows, self.dim, device=self.device)
+        return torch.zeros(rows, self.dim, device=self.device)
 
     def _push_fixed(self, grad_unique: torch.Tensor, scale: float) -> None:
-        _, rslot, req, _, cap = self._ctx
-        W, dev = self.world, self.device
-        gsend = torch.zeros(W * cap + 1, self.dim, device=dev)
+        rslot = self._ctx[1]
+        gsend = self.fixed_send_buffer(dump_row=True)
         if rslot.numel():
             gsend[rslot] = grad_unique.float()  # (the dump slot may take several rows: never sent)
+        self.push_send(gsend, scale)
+
+    def push_send(self, gsend: torch.Tensor, scale: float) -> None:
+        """Exchange a filled gradient send buffer of the last fixed pull and apply
+        the owner update."""
+        _, _, req, _, cap, local = self._ctx
+        W, dev = self.world, self.device
         grecv = torch.empty(W * cap, self.dim, device=dev)
         dist.all_to_all_single(grecv, gsend[: W * cap], group=self.group)
         self.exchange_bytes += W * cap * self.dim * 4
         if self.is_owner:
-            # padding slots (id -1, zero gradient) become DISTINCT negative rows:
-            # one-row segments that the update skips -- never one giant segment
-            pad = -2 - torch.arange(req.numel(), device=dev)
-            local = torch.where(req >= 0, req // self.n_own, pad)
+            if local is None:
+                # padding slots (id -1, zero gradient) become DISTINCT negative rows:
+                # one-row segments that the update skips -- never one giant segment
+                pad = -2 - torch.arange(req.numel(), device=dev)
+                local = torch.where(req >= 0, req // self.n_own, pad)
             self._apply_updates_dev(local, grecv, scale)
 
     def _apply_updates_dev(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:
@@ -448,7 +497,7 @@ class ShardedEmbedding:
                                     self.lr, self.eps, scale, count)
 
     def _sync_free(self, ids: torch.Tensor) -> bool:
-        return (self.dedup is not None and ids.numel() > 0 and self.n_own == 1 and
+        return (self.dedup is not None and ids.numel() > 0 and self.n_own == 1 and not self.force_fixed and
                 (self.world == 1 or self.group is None and not dist.is_initialized()))
 
     def pull_into(self, ids: torch.Tensor, out: torch.Tensor, F: int, col0: int = 0) -> Optional[torch.Tensor]:
@@ -456,13 +505,24 @@ class ShardedEmbedding:
         ``out[b, col0 + f*D : +D] = table[ids[b*F + f]]`` (csrc/ctr.hip
         ``embed_gather_cast``: no fp32 [n, D] gather, no cast pass).  Returns the
         inverse map, or None when this path does not apply (then use ``pull``)."""
-        if not (self._sync_free(ids) and out.dtype == torch.bfloat16 and self.table.dtype == torch.float32
-                and self.dim % 8 == 0 and out.stride(0) % 8 == 0 and col0 % 8 == 0):
+        if not (out.dtype == torch.bfloat16 and self.table.dtype == torch.float32 and self.use_hip
+                and self.dim % 8 == 0 and out.stride(0) % 8 == 0 and col0 % 8 == 0 and ids.numel() > 0):
+            return None
+        if self._fixed():
+            # fixed exchange: the received rows go straight into the bf16 input
+            # through rslot (dump slots read the zero row)
+            got, rslot, inv = self._pull_fixed(ids, rows_bf16=True)
+            _ext.load().embed_gather_cast(got, rslot, inv, F, out, col0)
+            return inv
+        if not self._sync_free(ids):
             return None
         uniq, inv, count, _, _ = self.dedup(ids, csr=False)
         _ext.load().embed_gather_cast(self.table, uniq, inv, F, out, col0)
         self._ctx = ("dev", uniq, count)
         return inv
+
+    def _fixed(self) -> bool:
+        return self.max_ids is not None and (self.world > 1 or self.force_fixed)
 
     def pull(self, ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """ids [n] int64 (any, may repeat) -> (unique rows [U, dim], inverse [n]).
@@ -473,8 +533,9 @@ class ShardedEmbedding:
             emb = self._local_gather(uniq)
             self._ctx = ("dev", uniq, count)
             return emb, inv
-        if self.max_ids is not None and self.world > 1:
-            return self._pull_fixed(ids)
+        if self._fixed():
+            got, rslot, inv = self._pull_fixed(ids)
+            return (got[rslot] if ids.numel() else got[:0]), inv
         uniq, inv = torch.unique(ids, return_inverse=True)
         owner = uniq % self.n_own
         order = torch.argsort(owner, stable=True)
@@ -585,6 +646,13 @@ class CTRModel:
             seg = torch.empty(n + 1, dtype=torch.int64, device=self.device)
             order = torch.empty(n, dtype=torch.int64, device=self.device)
             _ext.load().csr_from_inverse_only(inv, ws["sizes"], count, ws["bsum"], ws["cursor"], seg, order)
+            if kind == "fixed":
+                # each unique id's summed gradient row lands in its exchange slot
+                # (rslot) of the send buffer: no [U, D] intermediate, no scatter
+                gsend = self.emb.fixed_send_buffer()
+                _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg, count, ctx[1], gsend)
+                self.emb.push_send(gsend, scale)
+                return
             g_u = _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg, count)
             self.emb.push(g_u, scale)
             return

@@ -67,3 +67,11 @@ def maybe_inject_fault(rank: int, step: int) -> None:
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(code)
+
+
+def free_port() -> int:
+    """An unused 127.0.0.1 TCP port (a one-rank process group's rendezvous)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

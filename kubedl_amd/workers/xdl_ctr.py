@@ -63,6 +63,9 @@ def main(argv=None) -> int:
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--emb-lr", type=float, default=0.05)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--exchange", choices=("auto", "fixed"), default="auto",
+                    help="fixed: the PS + worker fixed-capacity exchange even at world 1 (one-GPU rehearsal: "
+                         "RCCL all-to-alls on a 1-rank group, one owner)")
     args, _unknown = ap.parse_known_args(argv)
     # the BASELINE.json config on the GPU; a plumbing-sized job on CPU (the
     # reference's example specs carry no sizes, so they run with these)
@@ -97,9 +100,10 @@ def main(argv=None) -> int:
     # KDL_DIST_BACKEND=gloo: rehearse a multi-rank job on fewer GPUs than ranks
     # (RCCL refuses two ranks on one device; parallel/dist.py init_from_env)
     backend = os.environ.get("KDL_DIST_BACKEND", "nccl") if use_gpu else "gloo"
-    if world > 1:
+    rehearse = args.exchange == "fixed" and world == 1
+    if world > 1 or rehearse:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("MASTER_PORT", str(common.free_port()) if rehearse else "29511")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
         if use_gpu and backend == "nccl":
             kw["device_id"] = device
@@ -113,7 +117,8 @@ def main(argv=None) -> int:
     # command line: the multi-rank exchange runs at that fixed capacity, with
     # equal all-to-all splits and no per-step size round trip to the host
     emb = ShardedEmbedding(args.fields * args.vocab, args.dim, owners, rank, world, device,
-                           group=None, lr=args.emb_lr, max_ids=args.batch * args.fields)
+                           group=None, lr=args.emb_lr, max_ids=args.batch * args.fields,
+                           force_fixed=args.exchange == "fixed")
     total = args.warmup + args.steps
     if not is_worker:  # PS: serve pull/push rounds
         for _ in range(total):
@@ -171,8 +176,9 @@ def main(argv=None) -> int:
                           "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
                           "samples_per_sec": args.steps * args.batch * len(workers) / dt if dt > 0 else 0.0,
                           "loss_first": first, "loss_last": last, "device": str(device),
-                          "hip_kernels": emb.use_hip, **xstats}), flush=True)
-    if world > 1:
+                          "hip_kernels": emb.use_hip, "exchange": "fixed" if emb._fixed() else "sync-free",
+                          **xstats}), flush=True)
+    if world > 1 or rehearse:
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -149,8 +149,11 @@ def _grad_of(u, dim):
 def _exchange_bytes_worker(rank, world, port, out, slack, strict):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # lossy mode is an explicit opt-in (STRICT=0); strict is the default
     if strict:
-        os.environ["KDL_CTR_A2A_STRICT"] = "1"
+        os.environ.pop("KDL_CTR_A2A_STRICT", None)
+    else:
+        os.environ["KDL_CTR_A2A_STRICT"] = "0"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dim, n, vocab = 8, 2048, 1 << 22
     fixed = ShardedEmbedding(vocab, dim, list(range(world)), rank, world, "cpu", lr=0.1, max_ids=n, slack=slack)
@@ -211,10 +214,19 @@ def test_ctr_exchange_capacity_right_sized_w4():
         assert out[f"tables_equal{r}"]
 
 
+def test_ctr_exchange_default_is_exact():
+    """Without an explicit slack the exchange runs at cap = max_ids for the whole
+    run: no overflow is possible and the pulled rows equal the variable exchange's."""
+    import torch.distributed as dist
+    e = ShardedEmbedding(64, 4, [0, 1], 0, 2, "cpu", max_ids=32)
+    assert e.slack == 0 and e.cap == 32 and e.strict
+
+
 def test_ctr_exchange_overflow_counted_and_capacity_grows():
-    """A burst above the agreed capacity (every id owned by one rank) is counted
-    on every rank (read LAG pulls later, or by finalize) and the capacity grows;
-    KDL_CTR_A2A_STRICT=1 raises instead."""
+    """A burst above the agreed capacity (every id owned by one rank) raises on
+    every rank by default (no silent loss); in the explicit lossy
+    mode (KDL_CTR_A2A_STRICT=0) it is counted on every rank (read LAG pulls
+    later, or by finalize) and the capacity grows."""
     out = _run_exchange(0.9)
     for r in range(4):
         assert out[f"stats{r}"]["exchange_overflow_steps"] >= 1, out
@@ -623,3 +635,126 @@ def test_ctr_fixed_exchange_two_ranks_on_gpu_matches_cpu():
         torch.testing.assert_close(tg, tc, atol=1e-5, rtol=1e-5)
         torch.testing.assert_close(ag, ac, atol=1e-5, rtol=1e-5)
         assert sg["exchange_overflow_steps"] == 0 and sg["exchange_cap"] < 4096
+
+
+# ---------------------------------------------------------------- fixed exchange kernels
+def _route_ref(uniq, count, owner_rank, n_own, W, cap):
+    """The torch routing the CPU path runs (models/ctr.py _pull_fixed)."""
+    n = uniq.numel()
+    send = torch.full((W * (cap + 1),), -1, dtype=torch.int64)
+    valid = torch.arange(n) < count
+    dest = torch.where(valid, owner_rank[uniq % n_own], torch.full_like(uniq, W))
+    onehot = torch.zeros(n, W + 1, dtype=torch.int64).scatter_(1, dest[:, None], 1)
+    pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None]).squeeze(1)
+    ok = valid & (pos < cap)
+    rslot = torch.where(ok, dest * cap + pos, torch.full_like(pos, W * cap))
+    full = torch.cat([send, torch.tensor([-1])])
+    full.scatter_(0, torch.where(ok, dest * (cap + 1) + pos, torch.full_like(pos, W * (cap + 1))), uniq)
+    send = full[:-1]
+    send[cap::cap + 1] = onehot[:, :W].sum(0).max() if n else 0
+    return send, rslot
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,live,W,n_own,cap", [(106496, 90000, 8, 8, 16384), (5000, 4999, 3, 2, 700),
+                                                 (257, 257, 64, 64, 3), (1, 1, 1, 1, 1), (0, 0, 4, 4, 8),
+                                                 (20000, 12000, 5, 3, 100000)])
+def test_a2a_route_matches_torch(n, live, W, n_own, cap):
+    """csrc/ctr.hip a2a_route: send blocks (ids in unique order, -1 padding,
+    header = largest fill), and rslot (dump slot for ids past the capacity or
+    the live count) equal the torch routing exactly; owners may be a subset of
+    ranks (PS roles) and fills may overflow the capacity."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g = torch.Generator().manual_seed(n + W)
+    uniq = torch.randperm(max(n, 1) * 7, generator=g)[:n].to(torch.int64)
+    owner_rank = torch.randperm(W, generator=g)[:n_own].to(torch.int64)
+    send_ref, rslot_ref = _route_ref(uniq, live, owner_rank, n_own, W, cap)
+    send = torch.full((W * (cap + 1),), 777, dtype=torch.int64, device="cuda")
+    rslot = torch.full((n,), 777, dtype=torch.int64, device="cuda")
+    count = torch.tensor([live], dtype=torch.int32, device="cuda")
+    ext.a2a_route(uniq.cuda(), count if n else None, owner_rank.cuda(), W, cap, send, rslot)
+    torch.cuda.synchronize()
+    assert torch.equal(send.cpu(), send_ref)
+    assert torch.equal(rslot.cpu(), rslot_ref)
+
+
+@pytest.mark.gpu
+def test_a2a_serve_and_mapped_segment_reduce():
+    """a2a_serve: requested rows (padding zero) + local rows (distinct negative
+    sentinels for padding); segment_reduce with out_rows writes each segment's
+    sum to its exchange slot and skips slots past the buffer (dump)."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(3)
+    table = torch.randn(1000, 64, device="cuda")
+    req = torch.randint(0, 3000, (512,), device="cuda")
+    req[::7] = -1
+    rows, local = ext.a2a_serve(table, req, 3)
+    rows16, local16 = ext.a2a_serve(table, req, 3, True)
+    assert torch.equal(local16, local) and torch.equal(rows16, rows.bfloat16())
+    want_local = torch.where(req >= 0, req // 3, -2 - torch.arange(512, device="cuda"))
+    assert torch.equal(local, want_local)
+    want = torch.where((req >= 0)[:, None], table[torch.where(req >= 0, req // 3, 0)], torch.zeros_like(rows))
+    assert torch.equal(rows, want)
+    # mapped segment sums: 40 segments of the rows of a [B, F*D] gradient
+    B, F, D = 64, 5, 16
+    gx = torch.randn(B, F * D + 8, device="cuda").bfloat16()
+    inv = torch.randint(0, 40, (B * F,), device="cuda")
+    order = torch.argsort(inv, stable=True)
+    seg = torch.zeros(41, dtype=torch.int64, device="cuda")
+    seg[1:] = torch.cumsum(torch.bincount(inv, minlength=40), 0)
+    ref = ext.segment_reduce(gx, F, 0, D, order, seg, None)
+    out_rows = torch.randperm(60, device="cuda")[:40]
+    out_rows[5] = 60  # past the buffer: dropped
+    out = torch.full((60, D), float("nan"), device="cuda")
+    ext.segment_reduce(gx, F, 0, D, order, seg, None, out_rows, out)
+    keep = out_rows < 60
+    assert torch.equal(out[out_rows[keep]], ref[keep])
+    written = torch.zeros(60, dtype=torch.bool, device="cuda")
+    written[out_rows[keep]] = True
+    assert bool(out[~written].isnan().all())
+
+
+@pytest.mark.gpu
+def test_ctr_fixed_exchange_world1_rehearsal_bit_exact():
+    """The world-1 rehearsal of the PS + worker exchange (force_fixed, one owner,
+    RCCL all-to-alls on a 1-rank group) trains to the same table, Adagrad state
+    and losses, bit for bit, as the sync-free one-owner path -- and runs no
+    device->host sync after its first step."""
+    import torch.distributed as dist
+    from kubedl_amd.models.ctr import CTRModel
+    from kubedl_amd.workers.common import free_port
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        g = torch.Generator(device="cuda").manual_seed(9)
+        batches = [(torch.randint(0, 1000, (512, 26), device="cuda", generator=g),
+                    torch.randn(512, 13, device="cuda", generator=g),
+                    torch.randint(0, 2, (512,), device="cuda", generator=g).float()) for _ in range(4)]
+        out = {}
+        for fixed in (True, False):
+            torch.manual_seed(0)
+            emb = ShardedEmbedding(26 * 1000, 64, [0], 0, 1, "cuda", lr=0.05, max_ids=512 * 26, force_fixed=fixed)
+            m = CTRModel(26, 1000, 64, 13, (256, 128), emb, "cuda")
+            losses = []
+            for i, (ids, dense, y) in enumerate(batches):
+                if i > 0:
+                    torch.cuda.set_sync_debug_mode("error")
+                try:
+                    x, inv, U = m.build_input(ids, dense)
+                    x.requires_grad_(True)
+                    loss, _ = m.tower.loss(x, y)
+                    loss.backward()
+                    m.push_grads(x.grad, inv, U, scale=1.0)
+                finally:
+                    torch.cuda.set_sync_debug_mode("default")
+                losses.append(loss.detach())
+            stats = emb.finalize()
+            torch.cuda.synchronize()
+            out[fixed] = (emb.table.clone(), emb.accum.clone(), torch.stack(losses), stats)
+        assert out[True][3]["exchange_overflow_steps"] == 0 and out[True][3]["exchange_cap"] == 512 * 26
+        for k in range(3):
+            assert torch.equal(out[True][k], out[False][k]), k
+    finally:
+        dist.destroy_process_group()
