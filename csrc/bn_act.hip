@@ -842,20 +842,20 @@ hipError_t fwd_impl(const T* x, const T* res, T* y, uint8_t* mbits, const PT* ga
                        beta, rm, rv, eps, save_mean, save_invstd, coef);
   }
   dim3 grid(apply_gx(M, rp.tl), rp.tl.gy);
-#define KDL_FWD_APPLY(R, S, MO)                                                             \
+#define BN_LAUNCH_FWD_APPLY(R, S, MO)                                                             \
   hipLaunchKernelGGL((bn_fwd_apply_kernel<T, VEC, R, S, MO>), grid, dim3(kBlock), 0, s, x, res, \
                      y, mbits, coef, M, C, rp.tl.TPR, rp.tl.RPI)
   if constexpr (VEC == 8) {
     if (relu && res && mbits) {
-      KDL_FWD_APPLY(true, true, true);
+      BN_LAUNCH_FWD_APPLY(true, true, true);
       return hipGetLastError();
     }
   }
-  if (relu && res) KDL_FWD_APPLY(true, true, false);
-  else if (relu) KDL_FWD_APPLY(true, false, false);
-  else if (res) KDL_FWD_APPLY(false, true, false);
-  else KDL_FWD_APPLY(false, false, false);
-#undef KDL_FWD_APPLY
+  if (relu && res) BN_LAUNCH_FWD_APPLY(true, true, false);
+  else if (relu) BN_LAUNCH_FWD_APPLY(true, false, false);
+  else if (res) BN_LAUNCH_FWD_APPLY(false, true, false);
+  else BN_LAUNCH_FWD_APPLY(false, false, false);
+#undef BN_LAUNCH_FWD_APPLY
   return hipGetLastError();
 }
 
@@ -885,17 +885,17 @@ hipError_t bwd_impl(const T* dy, const T* y, const uint8_t* mbits, const T* x, c
                     const float* mean, const float* invstd, T* dx, T* dres, PT* dgamma, PT* dbeta,
                     float* ws, int64_t M, int C, bool relu, bool training, hipStream_t s) {
   ReducePlan rp = plan_reduce(M, C, VEC);
-#define KDL_BWD(MODE)                                                                        \
+#define BN_LAUNCH_BWD(MODE)                                                                        \
   bwd_launch<T, VEC, PT, MODE>(rp, dy, y, mbits, x, gamma, beta, mean, invstd, dx, dres, dgamma, \
                                dbeta, ws, M, C, training, s)
-  if (!relu) KDL_BWD(kMaskNone);
-  else if (mbits != nullptr && VEC == 8) KDL_BWD(kMaskBits);
+  if (!relu) BN_LAUNCH_BWD(kMaskNone);
+  else if (mbits != nullptr && VEC == 8) BN_LAUNCH_BWD(kMaskBits);
   // with a residual the mask must come from y (it saw the residual); without
   // one it is recomputed from x (y is not read)
-  else if (dres == nullptr && beta != nullptr) KDL_BWD(kMaskX);
-  else if (y != nullptr) KDL_BWD(kMaskY);
+  else if (dres == nullptr && beta != nullptr) BN_LAUNCH_BWD(kMaskX);
+  else if (y != nullptr) BN_LAUNCH_BWD(kMaskY);
   else return hipErrorInvalidValue;
-#undef KDL_BWD
+#undef BN_LAUNCH_BWD
   return hipGetLastError();
 }
 
@@ -905,7 +905,7 @@ int64_t bn_workspace_floats(int C) {  // + the folded-finalize descriptor and ti
   return static_cast<int64_t>(kReplicas) * 4 * C + 5 * static_cast<int64_t>(C) + kFinDescFloats + kFinCounters;
 }
 
-#define KDL_DISPATCH_PT(pdtype, ...)              \
+#define BN_DISPATCH_PT(pdtype, ...)              \
   do {                                           \
     if ((pdtype) == 1) {                         \
       using PT = bf16_t;                         \
@@ -916,7 +916,7 @@ int64_t bn_workspace_floats(int C) {  // + the folded-finalize descriptor and ti
     }                                            \
   } while (0)
 
-#define KDL_DISPATCH_T(dtype, C, ...)                                      \
+#define BN_DISPATCH_T(dtype, C, ...)                                      \
   do {                                                                     \
     if ((dtype) == 1) {                                                    \
       using T = bf16_t;                                                    \
@@ -935,7 +935,7 @@ hipError_t bn_act_forward(const void* x, const void* res, void* y, uint8_t* mbit
                           bool relu, bool training, float momentum, float eps, hipStream_t s) {
   if (M <= 0 || C <= 0) return hipSuccess;
   hipError_t e = hipSuccess;
-  KDL_DISPATCH_PT(pdtype, KDL_DISPATCH_T(dtype, C, {
+  BN_DISPATCH_PT(pdtype, BN_DISPATCH_T(dtype, C, {
     e = fwd_impl<T, VEC, PT>(static_cast<const T*>(x), static_cast<const T*>(res),
                              static_cast<T*>(y), mbits, static_cast<const PT*>(gamma),
                              static_cast<const PT*>(beta), rm, rv, save_mean, save_invstd, ws, M,
@@ -950,7 +950,7 @@ hipError_t bn_act_backward(const void* dy, const void* y, const uint8_t* mbits, 
                            int dtype, int pdtype, bool relu, bool training, hipStream_t s) {
   if (M <= 0 || C <= 0) return hipSuccess;
   hipError_t e = hipSuccess;
-  KDL_DISPATCH_PT(pdtype, KDL_DISPATCH_T(dtype, C, {
+  BN_DISPATCH_PT(pdtype, BN_DISPATCH_T(dtype, C, {
     e = bwd_impl<T, VEC, PT>(static_cast<const T*>(dy), static_cast<const T*>(y), mbits,
                              static_cast<const T*>(x), static_cast<const PT*>(gamma),
                              static_cast<const PT*>(beta), mean, invstd, static_cast<T*>(dx),
@@ -976,7 +976,7 @@ hipError_t bn_pool_forward(const void* x, void* y, uint8_t* idx, const void* gam
   float* coef = ws_coef(ws, C);
   const int fin_grid = (C + kBlock - 1) / kBlock;
   const bf16_t* xb = static_cast<const bf16_t*>(x);
-  KDL_DISPATCH_PT(pdtype, {
+  BN_DISPATCH_PT(pdtype, {
     if (training && gemm_stats) {  // sums around rm already in acc (conv epilogue, csrc/stem.hip)
       hipLaunchKernelGGL((bn_fwd_finalize_kernel<bf16_t, PT>), dim3(fin_grid), dim3(kBlock), 0, s,
                          static_cast<const bf16_t*>(nullptr), acc, C, static_cast<float>(M),
@@ -1016,7 +1016,7 @@ hipError_t bn_pool_backward(const void* dyp, const uint8_t* idx, const void* x, 
   float* coef = ws_bcoef(ws, C);
   const bf16_t* db = static_cast<const bf16_t*>(dyp);
   const bf16_t* xb = static_cast<const bf16_t*>(x);
-  KDL_DISPATCH_PT(pdtype, {
+  BN_DISPATCH_PT(pdtype, {
     const PT* g = static_cast<const PT*>(gamma);
     const PT* b = static_cast<const PT*>(beta);
     hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<PT, VEC>), dim3(rp.gx, rp.tl.gy), dim3(kBlock), 0, s,
@@ -1049,7 +1049,7 @@ hipError_t bn_stage_fwd_finalize(const void* x, const float* shift, float* ws, i
                                  int pdtype, bool training, float momentum, float eps, hipStream_t s) {
   const int fin_grid = (C + kBlock - 1) / kBlock;
   float* coef = ws_coef(ws, C);
-  KDL_DISPATCH_PT(pdtype, {
+  BN_DISPATCH_PT(pdtype, {
     if (training)
       hipLaunchKernelGGL((bn_fwd_finalize_kernel<bf16_t, PT>), dim3(fin_grid), dim3(kBlock), 0, s,
                          static_cast<const bf16_t*>(x), ws_acc_fwd(ws, C), C, static_cast<float>(M),
@@ -1081,15 +1081,15 @@ hipError_t bn_stage_fwd_apply(const void* x, const float* ws, const void* res, c
     return hipGetLastError();
   }
   const bf16_t* rb = static_cast<const bf16_t*>(res);
-#define KDL_APPLY(R, S, MO)                                                                              \
+#define BN_LAUNCH_APPLY(R, S, MO)                                                                              \
   hipLaunchKernelGGL((bn_fwd_apply_kernel<bf16_t, 8, R, S, MO>), grid, dim3(kBlock), 0, s, xb, rb, yb, mbits, \
                      coef, M, C, tl.TPR, tl.RPI)
-  if (relu && rb && mbits) KDL_APPLY(true, true, true);
-  else if (relu && rb) KDL_APPLY(true, true, false);
-  else if (relu) KDL_APPLY(true, false, false);
-  else if (rb) KDL_APPLY(false, true, false);
-  else KDL_APPLY(false, false, false);
-#undef KDL_APPLY
+  if (relu && rb && mbits) BN_LAUNCH_APPLY(true, true, true);
+  else if (relu && rb) BN_LAUNCH_APPLY(true, true, false);
+  else if (relu) BN_LAUNCH_APPLY(true, false, false);
+  else if (rb) BN_LAUNCH_APPLY(false, true, false);
+  else BN_LAUNCH_APPLY(false, false, false);
+#undef BN_LAUNCH_APPLY
   return hipGetLastError();
 }
 
@@ -1110,7 +1110,7 @@ hipError_t bn_stage_bwd_reduce(const void* dy, const void* x, const void* gamma,
                                hipStream_t s) {
   if (M <= 0 || C % 8) return hipErrorInvalidValue;
   ReducePlan rp = plan_reduce(M, C, 8);
-  KDL_DISPATCH_PT(pdtype, {
+  BN_DISPATCH_PT(pdtype, {
     const PT* g = static_cast<const PT*>(gamma);
     const PT* b = static_cast<const PT*>(beta);
     if (relu_mask_x)
@@ -1132,7 +1132,7 @@ hipError_t bn_stage_bwd_apply_maskx(const void* dy, const void* x, const void* g
   const Tiling tl = make_tiling(C, 8);
   dim3 grid(apply_gx(M, tl), tl.gy);
   const float* coef = ws_bcoef(const_cast<float*>(ws), C);
-  KDL_DISPATCH_PT(pdtype, {
+  BN_DISPATCH_PT(pdtype, {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, PT, 8, kMaskX, false>), grid, dim3(kBlock), 0, s,
                        static_cast<const bf16_t*>(dy), nullptr, nullptr, static_cast<const bf16_t*>(x),
                        static_cast<const PT*>(gamma), static_cast<const PT*>(beta), mean, invstd, coef,
@@ -1144,7 +1144,7 @@ hipError_t bn_stage_bwd_apply_maskx(const void* dy, const void* x, const void* g
 hipError_t bn_stage_bwd_finalize(float* ws, int64_t M, int C, const void* gamma, const float* mean,
                                  const float* invstd, void* dgamma, void* dbeta, int pdtype, bool training,
                                  hipStream_t s) {
-  KDL_DISPATCH_PT(pdtype, {
+  BN_DISPATCH_PT(pdtype, {
     hipLaunchKernelGGL((bn_bwd_finalize_kernel<PT>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                        ws_acc_bwd(ws, C), C, static_cast<float>(M), static_cast<const PT*>(gamma), mean, invstd,
                        training, static_cast<PT*>(dgamma), static_cast<PT*>(dbeta), ws_bcoef(ws, C));

@@ -8,7 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define KDL_CHECK_HIP(expr)                                                        \
+#define RETURN_IF_HIP_ERR(expr)                                                        \
   do {                                                                            \
     hipError_t _e = (expr);                                                       \
     if (_e != hipSuccess) return _e;                                              \

@@ -620,7 +620,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t s) {
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = p.N / BN;
   // persistent blocks: one round of the resident capacity (256 CUs x MINB), nblk % 8 == 0
-  // (1 round measured +2.3% per ResNet-50 step over 2; KDL_GEMM_ROUNDS overrides)
+  // (1 round measured +2.3% per ResNet-50 step over 2; KDL_TUNE gemm_rounds overrides)
   static const int rounds = tune_int("gemm_rounds", 1);
   const int target = 256 * MINB * rounds;
   int GM = (target + tiles_n - 1) / tiles_n;
@@ -902,19 +902,19 @@ template <int TN_, int TK_>
 void launch_wgrad(dim3 grid, hipStream_t s, const bf16_t* g, const bf16_t* x, const float* pro, float* dw32, int M,
                   int N, int K, int Hout, int Wout, int Hin, int Win, int stride, int rps, int tiles_k, int mode,
                   int cin) {
-#define KDL_WG(P, G)                                                                                             \
+#define WG_LAUNCH(P, G)                                                                                             \
   hipLaunchKernelGGL((wgrad1x1_kernel<TN_, TK_, P, G>), grid, dim3(kThreads), 0, s, g, x, pro, dw32, M, N, K, Hout, \
                      Wout, Hin, Win, stride, rps, tiles_k, cin)
   if (pro) {
-    if (mode == G_CONV3) KDL_WG(true, G_CONV3);
-    else if (mode == G_STRIDED) KDL_WG(true, G_STRIDED);
-    else KDL_WG(true, G_DENSE);
+    if (mode == G_CONV3) WG_LAUNCH(true, G_CONV3);
+    else if (mode == G_STRIDED) WG_LAUNCH(true, G_STRIDED);
+    else WG_LAUNCH(true, G_DENSE);
   } else {
-    if (mode == G_CONV3) KDL_WG(false, G_CONV3);
-    else if (mode == G_STRIDED) KDL_WG(false, G_STRIDED);
-    else KDL_WG(false, G_DENSE);
+    if (mode == G_CONV3) WG_LAUNCH(false, G_CONV3);
+    else if (mode == G_STRIDED) WG_LAUNCH(false, G_STRIDED);
+    else WG_LAUNCH(false, G_DENSE);
   }
-#undef KDL_WG
+#undef WG_LAUNCH
 }
 }  // namespace
 
@@ -923,7 +923,7 @@ namespace {
 // the columns alone would leave the chip idle (chunk partials first).
 hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t* dW, hipStream_t s,
                         int layout = 0) {
-  // timing-only (KDL_PRICE_WGRAD_REDUCE=0): skip the slab reduce to price its
+  // timing-only (KDL_TUNE price_wgrad_reduce=0): skip the slab reduce to price its
   // cost in the two-stream step (weight gradients are then garbage)
   static const bool skip = tune_int("price_wgrad_reduce", 1) == 0;
   if (skip) return hipSuccess;
@@ -1002,7 +1002,7 @@ hipError_t wgrad_impl(const void* G, const void* A, const float* pro_coef, float
     else if (tn == 128) launch_wgrad<128, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
     else if (tk == 128) launch_wgrad<64, 128>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
     else launch_wgrad<64, 64>(grid, s, g, x, pro_coef, dw32, M, N, K, Hout, Wout, Hin, Win, stride, rps, tiles_k, mode, cin);
-    KDL_CHECK_HIP(hipGetLastError());
+    RETURN_IF_HIP_ERR(hipGetLastError());
   }
   return wgrad_reduce(dw32, static_cast<int64_t>(N) * K, nsplit, scale, static_cast<bf16_t*>(dW), s);
 }

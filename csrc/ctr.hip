@@ -775,25 +775,25 @@ hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bi
   const float* b32 = bias_bf16 ? nullptr : static_cast<const float*>(bias);
   const bf16_t* b16 = bias_bf16 ? static_cast<const bf16_t*>(bias) : nullptr;
   const int cfg = ctr_tile_for(M, N);
-#define KDL_GBA(R, TM, TN, T)                                                                                \
+#define CTR_LAUNCH_GBA(R, TM, TN, T)                                                                                \
   do {                                                                                                       \
     const int tn = (N + TN - 1) / TN, tm = (M + TM - 1) / TM;                                                \
     hipLaunchKernelGGL((gemm_bias_act_kernel<R, TM, TN, T>), dim3(tn * tm), dim3(kThreads), 0, s, a, b, b32, b16, \
                        c, M, N, K, tn);                                                                      \
   } while (0)
-#define KDL_GBA_T(R, T)                 \
-  if (cfg == 0) KDL_GBA(R, 128, 128, T); \
-  else if (cfg == 1) KDL_GBA(R, 128, 64, T); \
-  else KDL_GBA(R, 64, 64, T)
+#define CTR_LAUNCH_GBA_T(R, T)                 \
+  if (cfg == 0) CTR_LAUNCH_GBA(R, 128, 128, T); \
+  else if (cfg == 1) CTR_LAUNCH_GBA(R, 128, 64, T); \
+  else CTR_LAUNCH_GBA(R, 64, 64, T)
   if (relu) {
-    if (b_kn) { KDL_GBA_T(true, true); }
-    else { KDL_GBA_T(true, false); }
+    if (b_kn) { CTR_LAUNCH_GBA_T(true, true); }
+    else { CTR_LAUNCH_GBA_T(true, false); }
   } else {
-    if (b_kn) { KDL_GBA_T(false, true); }
-    else { KDL_GBA_T(false, false); }
+    if (b_kn) { CTR_LAUNCH_GBA_T(false, true); }
+    else { CTR_LAUNCH_GBA_T(false, false); }
   }
-#undef KDL_GBA_T
-#undef KDL_GBA
+#undef CTR_LAUNCH_GBA_T
+#undef CTR_LAUNCH_GBA
   return hipGetLastError();
 }
 
@@ -878,17 +878,17 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
   // (mF = 0 when j * F can reach 2^32: the kernel divides in 64 bits instead)
   const bool fast = static_cast<uint64_t>(nrows) * static_cast<uint64_t>(F) < (uint64_t(1) << 32);
   const uint32_t mF = fast ? static_cast<uint32_t>(((uint64_t(1) << 32) + F - 1) / F) : 0u;
-#define KDL_SEGRED(T, V)                                                                                      \
+#define CTR_LAUNCH_SEGRED(T, V)                                                                                      \
   hipLaunchKernelGGL((segment_reduce_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, mF, \
                      ld, col0, order, seg, U, D, lg, out, ucount, out_row, out_lim)
   if (dtype == 1) {
-    if (v4) KDL_SEGRED(bf16_t, true);
-    else KDL_SEGRED(bf16_t, false);
+    if (v4) CTR_LAUNCH_SEGRED(bf16_t, true);
+    else CTR_LAUNCH_SEGRED(bf16_t, false);
   } else {
-    if (v4) KDL_SEGRED(float, true);
-    else KDL_SEGRED(float, false);
+    if (v4) CTR_LAUNCH_SEGRED(float, true);
+    else CTR_LAUNCH_SEGRED(float, false);
   }
-#undef KDL_SEGRED
+#undef CTR_LAUNCH_SEGRED
   return hipGetLastError();
 }
 
@@ -1359,7 +1359,7 @@ int dedup_table_slots(int n) {
 hipError_t dedup_ids(const int64_t* ids, int n, void* keys, int T, int* slot_of, int* slot_uid, int* bsum,
                      int64_t* uniq, int64_t* inv, int* count, int* sizes, hipStream_t s) {
   if (n <= 0 || T < 2 * n || (T & (T - 1)) || T % kChunk) return hipErrorInvalidValue;
-  KDL_CHECK_HIP(hipMemsetAsync(sizes, 0, static_cast<size_t>(n + 1) * sizeof(int), s));
+  RETURN_IF_HIP_ERR(hipMemsetAsync(sizes, 0, static_cast<size_t>(n + 1) * sizeof(int), s));
   auto* k = static_cast<unsigned long long*>(keys);
   hipLaunchKernelGGL(dedup_insert_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ids, n, k,
                      static_cast<uint32_t>(T - 1), slot_of);

@@ -466,7 +466,7 @@ hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* 
   const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(float);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once
   if (!attr_set) {
-    KDL_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_kernel),
+    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_kernel),
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       static_cast<int>(kFTile * 256 * 2 * sizeof(float))));
     attr_set = true;
@@ -495,7 +495,7 @@ static hipError_t hist_lds_attr() {
   static bool attr_set = false;
   if (!attr_set) {
     const int bytes = static_cast<int>(kFTile * 256 * 2 * sizeof(float));
-    KDL_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<4>),
+    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<4>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
     attr_set = true;
   }
@@ -508,7 +508,7 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
   if (nb <= 0 || F <= 0 || max_chunks <= 0) return hipSuccess;
   hipLaunchKernelGGL(hist_plan_kernel, dim3(1), dim3(64), 0, s, blo, bhi, nb, rpb, chunk_off);
   const int fp = hist_fp(F);
-  KDL_CHECK_HIP(hist_lds_attr());
+  RETURN_IF_HIP_ERR(hist_lds_attr());
   dim3 grid(max_chunks, (F + fp - 1) / fp);
   const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(float);
   hipLaunchKernelGGL((hist_build_wq_kernel<4>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows,

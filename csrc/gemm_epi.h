@@ -73,7 +73,7 @@ struct GemmParams {
   const bf16_t* ex2;    // RESBITS: optional second BN input (downsample BN)
   const float* emean2;
   float* acc2;          // its replicas [kRep][2N]
-  int price_drop;       // timing-only builds (KDL_IGEMM_PRICE): bit 0 drops A's loads, bit 1 B's
+  int price_drop;       // timing-only builds (KDL_TUNE igemm_price): bit 0 drops A's loads, bit 1 B's
   // G_DGRAD2: A = dy [Nb, Hin, Win, Cin] (Hin x Win = each class's pixel grid),
   // C = dx [Nb, Hout = 2 Hin (or 2 Hin - 1), Wout = 2 Win (or 2 Win - 1), N]; class c = 2 py + px owns the
   // dx pixels (2i + py, 2j + px).  mc = Nb Hin Win rows per class, padded to

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
 
   // buffer resources (wave-uniform: built from kernel arguments only)
   const int lda = TAPS ? p.Cin : K;
-  // (a zero-record descriptor drops that operand's loads: KDL_IGEMM_PRICE timing builds)
+  // (a zero-record descriptor drops that operand's loads: KDL_TUNE igemm_price timing builds)
   const int bytesA = (p.price_drop & 1) ? 0 : static_cast<int>(p.a_rows * lda * 2);
   const int bytesB = (p.price_drop & 2) ? 0 : static_cast<int>(static_cast<int64_t>(p.N) * K * 2);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), (short)0, bytesA,
@@ -351,7 +351,7 @@ hipError_t launch(const GemmParams& p, hipStream_t s) {
   }
   const int tiles_m = (q.M + BM - 1) / BM;
   const int tiles_n = q.N / BN;
-  // one round of resident blocks (KDL_IGEMM_ROUNDS > 1: that many rounds -- shorter
+  // one round of resident blocks (KDL_TUNE igemm_rounds > 1: that many rounds -- shorter
   // per-block tile lists, for the two-stream step's contention; A/B knob)
   static const int rounds = [] { const int v = tune_int("igemm_rounds", 1); return v < 1 ? 1 : v; }();
   const int target = 256 * BPC * rounds;

@@ -362,6 +362,6 @@ int gemm_core_mode();
 void set_gemm_core_mode(int m);
 // force an LDS-DMA tile config (-1 = by shape; csrc/igemm.hip igemm_pick)
 void set_igemm_cfg(int cfg);
-void set_halo3x3(int on);  // 0: every 3x3 on the implicit GEMM (A/B switch; KDL_HALO)
+void set_halo3x3(int on);  // 0: every 3x3 on the implicit GEMM (A/B switch; KDL_TUNE halo=0)
 
 }  // namespace kdl

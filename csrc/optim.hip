@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void cast_copy_kernel(const S* __restrict__ sr
 }  // namespace
 
 // dtype codes: 0 = f32, 1 = bf16
-#define KDL_DISPATCH2(gd, pd, ...)                                               \
+#define OPT_DISPATCH2(gd, pd, ...)                                               \
   do {                                                                          \
     if ((gd) == 1 && (pd) == 1) { using GT = bf16_t; using PT = bf16_t; __VA_ARGS__; } \
     else if ((gd) == 1) { using GT = bf16_t; using PT = float; __VA_ARGS__; }   \
@@ -153,7 +153,7 @@ hipError_t fused_sgd(const OptChunk* chunks, int nchunks, float* master, float* 
                      const void* grad, void* param, int gdtype, int pdtype, const OptHyper& h,
                      hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-  KDL_DISPATCH2(gdtype, pdtype,
+  OPT_DISPATCH2(gdtype, pdtype,
                 hipLaunchKernelGGL((sgd_chunk_kernel<GT, PT>), dim3(nchunks), dim3(256), 0, s,
                                    chunks, master, mom, static_cast<const GT*>(grad),
                                    static_cast<PT*>(param), h));
@@ -164,7 +164,7 @@ hipError_t fused_adam(const OptChunk* chunks, int nchunks, float* master, float*
                       const void* grad, void* param, int gdtype, int pdtype, const OptHyper& h,
                       hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-  KDL_DISPATCH2(gdtype, pdtype,
+  OPT_DISPATCH2(gdtype, pdtype,
                 hipLaunchKernelGGL((adam_chunk_kernel<GT, PT>), dim3(nchunks), dim3(256), 0, s,
                                    chunks, master, m1, m2, static_cast<const GT*>(grad),
                                    static_cast<PT*>(param), h));
@@ -187,7 +187,7 @@ hipError_t cast_copy(const void* src, int sdtype, void* dst, int ddtype, int64_t
   if (n <= 0) return hipSuccess;
   const int64_t n8 = n / 8;  // callers pass multiples of 8 (flat buffers are padded)
   const int grid = mem_bound_grid(n8, 256);
-  KDL_DISPATCH2(sdtype, ddtype,
+  OPT_DISPATCH2(sdtype, ddtype,
                 hipLaunchKernelGGL((cast_copy_kernel<GT, PT>), dim3(grid), dim3(256), 0, s,
                                    static_cast<const GT*>(src), static_cast<PT*>(dst), n8));
   return hipGetLastError();

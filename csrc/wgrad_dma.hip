@@ -292,29 +292,29 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
 
 template <int TN_, int TK_, int WN = 2, int WK = 2>
 void launch(const WgParams& p, int grid, hipStream_t s) {
-#define KDL_WGD(G, P) \
+#define WGD_LAUNCH(G, P) \
   hipLaunchKernelGGL((wgrad_dma_kernel<TN_, TK_, G, P, WN, WK>), dim3(grid), dim3(64 * WN * WK), 0, s, p)
   if (p.pro) {
-    if (p.mode == G_CONV3) KDL_WGD(G_CONV3, true);
-    else if (p.mode == G_STRIDED) KDL_WGD(G_STRIDED, true);
-    else KDL_WGD(G_DENSE, true);
+    if (p.mode == G_CONV3) WGD_LAUNCH(G_CONV3, true);
+    else if (p.mode == G_STRIDED) WGD_LAUNCH(G_STRIDED, true);
+    else WGD_LAUNCH(G_DENSE, true);
   } else {
-    if (p.mode == G_CONV3) KDL_WGD(G_CONV3, false);
-    else if (p.mode == G_STRIDED) KDL_WGD(G_STRIDED, false);
-    else KDL_WGD(G_DENSE, false);
+    if (p.mode == G_CONV3) WGD_LAUNCH(G_CONV3, false);
+    else if (p.mode == G_STRIDED) WGD_LAUNCH(G_STRIDED, false);
+    else WGD_LAUNCH(G_DENSE, false);
   }
-#undef KDL_WGD
+#undef WGD_LAUNCH
 }
 
 // G prologue (BWDG): 1x1 weight gradients only (dense or strided A rows)
 template <int TN_, int TK_, int WN, int WK>
 void launch_bwdg(const WgParams& p, int grid, hipStream_t s) {
-#define KDL_WGB(G, P) \
+#define WGD_LAUNCH_B(G, P) \
   hipLaunchKernelGGL((wgrad_dma_kernel<TN_, TK_, G, P, WN, WK, true>), dim3(grid), dim3(64 * WN * WK), 0, s, p)
-  if (p.mode == G_STRIDED) KDL_WGB(G_STRIDED, false);  // (strided rows: the downsample conv, no A prologue)
-  else if (p.pro) KDL_WGB(G_DENSE, true);               // conv3: B2 + ReLU recomputed on A as well
-  else KDL_WGB(G_DENSE, false);
-#undef KDL_WGB
+  if (p.mode == G_STRIDED) WGD_LAUNCH_B(G_STRIDED, false);  // (strided rows: the downsample conv, no A prologue)
+  else if (p.pro) WGD_LAUNCH_B(G_DENSE, true);               // conv3: B2 + ReLU recomputed on A as well
+  else WGD_LAUNCH_B(G_DENSE, false);
+#undef WGD_LAUNCH_B
 }
 
 }  // namespace

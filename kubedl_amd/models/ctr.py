@@ -262,7 +262,7 @@ class ShardedEmbedding:
         # to the host.  ``max_ids`` = the per-pull id bound every rank knows from
         # the job config (batch x fields).  By default cap = max_ids for the whole
         # run: exact, an overflow is impossible.  Adaptive capacity is opt-in
-        # (``slack`` / KDL_CTR_A2A_SLACK > 0): the header carries the sender's
+        # (``slack`` / KDL_TUNE ctr_a2a_slack > 0): the header carries the sender's
         # largest per-owner fill, so after the id exchange every rank holds the
         # same global max fill; LAG steps later (its pinned copy long landed)
         # every rank reads it and resizes ``cap`` by the same rule to slack x the
@@ -270,17 +270,18 @@ class ShardedEmbedding:
         # shifted within LAG steps) would drop the excess ids to a dump slot --
         # their rows read as zeros and their gradients are lost for that step --
         # so an overflow RAISES (the rank exits non-zero) unless lossy mode is
-        # asked for explicitly (KDL_CTR_A2A_STRICT=0: counted in
+        # asked for explicitly (KDL_TUNE ctr_a2a_strict=0: counted in
         # ``overflow_steps``, reported by ``finalize()``, capacity doubled).
         # ``force_fixed``: take this exchange at world 1 too (the one-GPU
         # rehearsal of the PS + worker path; RCCL all-to-alls on a 1-rank group).
         self.force_fixed = bool(force_fixed)
         self.max_ids = max_ids
         if max_ids is not None:
-            sl = slack if slack is not None else float(os.environ.get("KDL_CTR_A2A_SLACK", "0") or 0)
+            from kubedl_amd.utils.tune import tune
+            sl = slack if slack is not None else tune("ctr_a2a_slack", 0.0)
             self.slack = sl
             self.cap = max(int(max_ids), 1)
-            self.strict = os.environ.get("KDL_CTR_A2A_STRICT", "1") != "0"
+            self.strict = tune("ctr_a2a_strict", True)
             self._owner_rank = torch.tensor(self.owners, dtype=torch.int64, device=self.device)
             self._fills = collections.deque(maxlen=self.FILL_WINDOW)  # agreed max fills, oldest first
             self._pending = collections.deque()  # (cap used, pinned fill, event) per pull not yet read
@@ -358,9 +359,9 @@ class ShardedEmbedding:
                 self.overflow_steps += 1
                 if self.strict:
                     raise RuntimeError(f"CTR exchange overflow: {fill} ids for one owner > capacity {cap_used} "
-                                       f"(KDL_CTR_A2A_SLACK={self.slack}); that step's excess rows were dropped. "
-                                       f"Run with a larger slack, KDL_CTR_A2A_SLACK=0 (exact), or accept "
-                                       f"lossy steps with KDL_CTR_A2A_STRICT=0")
+                                       f"(ctr_a2a_slack={self.slack}); that step's excess rows were dropped. "
+                                       f"Run with a larger slack, KDL_TUNE ctr_a2a_slack=0 (exact), or accept "
+                                       f"lossy steps with KDL_TUNE ctr_a2a_strict=0")
             changed = True
         if not changed or self.slack <= 0 or drain:
             return

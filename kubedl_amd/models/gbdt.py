@@ -357,7 +357,6 @@ class HistGBDT:
         grower's workspaces; ``stats['boost_s']``: the boosting rounds alone (one
         synchronisation at each end, none inside)."""
         t0 = self._sync_time()
-        self._replayed = 0
         X = X.to(self.device)
         y = y.to(self.device)
         if self.cuts is None:
@@ -369,9 +368,7 @@ class HistGBDT:
         grower = self._device_grower(bins)
         t1 = self._sync_time()
         dev_trees = []
-        if self._graph_rounds(grower):
-            self._fit_graph(grower, pred, y, K, dev_trees, callback)
-        for it in range(len(dev_trees), self.p.n_estimators):
+        for it in range(self.p.n_estimators):
             g_all, h_all = self._grad_hess(pred, y)
             round_trees = []
             for k in range(K):
@@ -401,60 +398,9 @@ class HistGBDT:
                 host = torch.stack([torch.stack(r) for r in dev_trees]).cpu()
                 self.trees += [[self._heap_tree(host[i, k]) for k in range(K)] for i in range(len(dev_trees))]
             b, s = grower.stats()
-            if self._replayed:  # graph replays enqueue nothing on the host: count them per round
-                b += self._replayed * self._round_builds[0]
-                s += self._replayed * self._round_builds[1]
             self.stats["hist_builds"] += b
             self.stats["hist_subtracted"] += s
         return pred
-
-    # ------------------------------------------------------------ HIP-graph rounds
-    _replayed = 0
-    _round_builds = (0, 0)
-
-    def _graph_rounds(self, grower) -> bool:
-        """One boosting round is a fixed kernel sequence (~85 launches: gradients,
-        per-level split search, partition, histograms; every decision stays on the
-        device), so on one rank it is captured once as a HIP graph and replayed:
-        the round then costs its kernel time, not the host's launch rate.
-        Off by default (``KDL_GBDT_GRAPH=1`` turns it on): on a box that issues
-        launches fast enough the rounds are already kernel-bound -- 2M x 28,
-        depth 6: 349-351 rounds/s replayed vs 363 eager
-        (profiles/r02_gbdt_hist_sweep.txt)."""
-        return (grower is not None and self.device.type == "cuda" and _world() == 1
-                and self.p.n_estimators >= 3 and os.environ.get("KDL_GBDT_GRAPH", "0") == "1")
-
-    def _round(self, grower, pred, y, K):
-        g_all, h_all = self._grad_hess(pred, y)
-        outs = []
-        for k in range(K):
-            arr, leaf_val = self._grow_device(grower, g_all[:, k].contiguous(), h_all[:, k].contiguous())
-            pred[:, k] += leaf_val
-            outs.append(arr)
-        return outs
-
-    def _fit_graph(self, grower, pred, y, K, dev_trees, callback) -> None:
-        # round 0 eagerly (allocator warm-up, per-round build counts), then capture
-        dev_trees.append(self._round(grower, pred, y, K))
-        if callback is not None:
-            callback(0, pred)
-        b0 = grower.stats()
-        graph = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream(self.device)
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side):
-            with torch.cuda.graph(graph, stream=side):
-                static_out = self._round(grower, pred, y, K)
-        torch.cuda.current_stream(self.device).wait_stream(side)
-        b1 = grower.stats()
-        self._round_builds = (b1[0] - b0[0], b1[1] - b0[1])
-        self._replayed = self.p.n_estimators - 2  # the capture counted one round's builds
-        for it in range(1, self.p.n_estimators):
-            graph.replay()
-            dev_trees.append([a.clone() for a in static_out])  # the graph reuses its outputs
-            if callback is not None:
-                callback(it, pred)
-        self._graph = graph  # keep the graph's memory pool alive with the model
 
     def predict_margin(self, X: torch.Tensor) -> torch.Tensor:
         X = X.to(self.device).float()

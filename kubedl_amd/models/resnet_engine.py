@@ -746,8 +746,10 @@ class EngineOptions:
     res_pro_kmax: int = 512
     res_pro_down: bool = True
     res_pro_dual: bool = True
-    # bn1 + ReLU inside the 56x56 halo kernels: 1 forward + write-through, 2 also
-    # the weight gradient's halo, 0 apply pass
+    # bn1 + ReLU inside the 56x56 halo kernels: 1 forward + write-through, 0 apply
+    # pass (the weight gradient transforming its own halo as well, a1 never
+    # stored, measured slower -- 13,310-13,345 img/s, profiles/r03b_halo_pro_ab.txt
+    # -- and is not an engine option)
     halo_pro: int = 1
     # BN-backward apply fused into 1x1 data-gradient GEMMs (1 write-through, 2 both
     # operands, 0 own pass) up to this many channels; bn1 too (measured slower)
@@ -777,7 +779,7 @@ class ResNetEngine:
     called once that gradient is final (DP bucket launch)."""
 
     def __init__(self, model: ResNet, backend: str = "auto", grad_view=None, on_ready=None,
-                 options: EngineOptions | None = None):
+                 options: EngineOptions | None = None, side=None):
         self.model = model
         p = next(model.parameters())
         self.dev = p.device
@@ -842,8 +844,9 @@ class ResNetEngine:
         # bn1 + ReLU of the stride-1 56x56 3x3 convs applied inside the halo kernels,
         # which stage the input halo in LDS and transform it there (halo_pro):
         # 1 = the forward conv does, writing a1 = relu(B1(c1)) through for the weight
-        # gradient (no apply pass); 2 = the weight gradient transforms its halo too
-        # (a1 never written); 0 = apply pass
+        # gradient (no apply pass); 0 = apply pass
+        if o.halo_pro not in (0, 1):
+            raise ValueError(f"KDL_ENGINE halo_pro={o.halo_pro}: 0 (apply pass) or 1 (halo prologue)")
         self.halo_pro = o.halo_pro
         self.fuse_bwd = o.bn_bwd_fuse
         self.fuse_kmax = o.bn_bwd_fuse_kmax
@@ -851,7 +854,9 @@ class ResNetEngine:
         self.side = None
         if self.K.name == "hip" and o.side:
             from kubedl_amd.ops.streams import side_stream
-            self.side = side_stream(self.dev, o.side_prio)  # (ops/streams.py)
+            # (``side``: a stream the caller created -- and ran a kernel on -- before
+            # anything else claimed the hardware queues; ResNetTrainer does)
+            self.side = side if side is not None else side_stream(self.dev, o.side_prio)  # (ops/streams.py)
             # overlapped with the main stream, the 1x1 weight gradients gain from 256x256
             # tiles too (fewer, heavier side-stream blocks; csrc/conv1x1.hip wgrad_tiles)
             self.K.ext.set_wgrad_big(2)
@@ -1011,8 +1016,8 @@ class ResNetEngine:
             K.bn_finalize(st1, n * h * w, gemm_shift=True)
             if self._halo_pro_ok(c1, s):
                 # the conv applies B1 + ReLU to its input halo (csrc/halo3x3.hip) and
-                # writes a1 through (mode 1) or a1 is never stored (mode 2)
-                a1 = torch.empty_like(c1) if self.halo_pro == 1 else None
+                # writes a1 through for the weight gradient
+                a1 = torch.empty_like(c1)
                 c2 = K.conv3x3_fwd(c1, blk.conv2.weight, s, st2, pro=st1, aout=a1)
                 ho, wo = c2.shape[-2:]
                 K.bn_finalize(st2, n * ho * wo, gemm_shift=True)
@@ -1180,10 +1185,7 @@ class ResNetEngine:
             s = blk.conv2.stride[0]
             if s == 1:
                 with self._on_side(dc2):
-                    if a1 is None:  # a1 never stored: the halo weight gradient applies B1 + ReLU to c1
-                        self._wgrad3x3(dc2, c1, 1, blk.conv2.weight, pro=st1)
-                    else:
-                        self._wgrad3x3(dc2, a1, 1, blk.conv2.weight)
+                    self._wgrad3x3(dc2, a1, 1, blk.conv2.weight)
                 self.on_ready(blk.conv2.weight)
                 g1 = K.dgrad3x3_maskx(dc2, self._wd(blk.conv2), c1, st1)
                 n1, _, h1, w1 = c1.shape

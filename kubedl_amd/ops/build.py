@@ -71,7 +71,7 @@ def _compile(src: Path, flags, hdr_digest: str, force: bool, bdir: Path = BUILD)
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True, out: Path | None = None,
           defines: tuple = ()) -> Path:
-    """``out`` / ``defines``: an A/B variant of the extension (e.g. ``-DKDL_IGEMM_SPREAD=1`` into
+    """``out`` / ``defines``: an A/B variant of the extension (e.g. ``-DIGEMM_VARIANT=1`` into
     ``kubedl_amd/_C_alt.so``), loaded instead of ``_C.so`` with ``KDL_C_PATH`` (ops/_ext.py)."""
     out = Path(out) if out is not None else OUT
     bdir = BUILD if out == OUT else BUILD / out.stem  # a variant keeps its own objects

@@ -10,7 +10,7 @@ implicitly ordered against the other blocking streams of the process, and
 RCCL creates some.  So the trainer runs every step on a stream of its own and
 the engine's side stream is a second pool stream.
 
-``KDL_STREAMS`` selects the variant (A/B switch):
+``KDL_TUNE streams=`` selects the variant (A/B switch):
 
 * ``pool`` (default): pool streams (``torch.cuda.Stream``);
 * ``dedicated``: streams with an explicit full CU mask, which HIP always
@@ -30,7 +30,8 @@ _KEEP = []  # handles of dedicated streams (ExternalStream does not own them)
 
 
 def mode() -> str:
-    return os.environ.get("KDL_STREAMS", "pool")
+    from kubedl_amd.utils.tune import tune
+    return tune("streams", "pool")
 
 
 def compute_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
@@ -38,11 +39,12 @@ def compute_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     m = mode()
     if device.type != "cuda" or m == "null":
         return None
-    # the step's stream at high priority (KDL_MAIN_PRIO, default -1): the
+    # the step's stream at high priority (KDL_TUNE main_prio, default -1): the
     # dispatcher hands CUs to its critical-path kernels before the
     # weight-gradient side stream's (torch: lower number = higher priority);
     # measured 12,574-12,661 -> 12,740-12,751 img/s (profiles/r02_stream_priority_ab.txt)
-    return side_stream(device, int(os.environ.get("KDL_MAIN_PRIO", "-1")))
+    from kubedl_amd.utils.tune import tune
+    return side_stream(device, tune("main_prio", -1))
 
 
 def side_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:

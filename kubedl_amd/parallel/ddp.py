@@ -48,10 +48,11 @@ class Bucket:
 
 
 def reduce_fp32_wanted() -> bool:
-    """``KDL_DDP_REDUCE=fp32``: RCCL buckets of a bf16 gradient buffer are summed in
+    """``KDL_TUNE ddp_reduce=fp32``: RCCL buckets of a bf16 gradient buffer are summed in
     fp32 (2x the bytes on the links, one bf16 rounding at the end instead of one
     per ring step; tests/test_multigpu.py bounds the bf16 error at world 8)."""
-    return os.environ.get("KDL_DDP_REDUCE", "bf16").lower() == "fp32"
+    from kubedl_amd.utils.tune import tune
+    return tune("ddp_reduce", "bf16").lower() == "fp32"
 
 
 class FlatDDP:
@@ -64,14 +65,15 @@ class FlatDDP:
         self.space = space
         self.direct = direct
         self.world = world_size
-        # KDL_DDP_WORLD1=1: a world-1 job still buckets and all-reduces (RCCL's
+        # KDL_TUNE ddp_world1=1: a world-1 job still buckets and all-reduces (RCCL's
         # one-rank all-reduce) -- exercises the collective path the N-GPU job
         # takes; off by default (it is an identity).  RCCL's one-rank in-place
-        # all-reduce launches nothing, so KDL_DDP_WORLD1=copy issues each bucket
+        # all-reduce launches nothing, so ddp_world1=copy issues each bucket
         # as a one-rank all_gather into a scratch buffer instead: a bucket-sized
         # RCCL copy on the process group's own stream, event-joined like the
         # N-GPU collective (the stream / hardware-queue shape of world 8)
-        w1 = os.environ.get("KDL_DDP_WORLD1", "0")
+        from kubedl_amd.utils.tune import tune
+        w1 = tune("ddp_world1", "0")
         self.active = world_size > 1 or (w1 in ("1", "copy") and dist.is_initialized())
         self.world1_copy = world_size == 1 and w1 == "copy" and self.active
         self._w1_scratch = None

@@ -101,11 +101,12 @@ def init_from_env(device: str | None = None, timeout_s: float | None = None,
         os.environ.setdefault("MASTER_PORT", "23456")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        # lazy RCCL communicator (KDL_PG_EAGER=1: eager, bound at init): the
+        # lazy RCCL communicator (KDL_TUNE pg_eager=1: eager, bound at init): the
         # rendezvous through the TCP store is what init waits for; building
         # the communicator (~1.1 s of topology discovery even at world 1) is
         # deferred to the first collective instead of delaying rank readiness
-        if backend == "nccl" and os.environ.get("KDL_PG_EAGER", "0") == "1":
+        from kubedl_amd.utils.tune import tune
+        if backend == "nccl" and tune("pg_eager", False):
             kw["device_id"] = dev
         dist.init_process_group(**kw)
     return DistInfo(rank, world, local_rank, dev, backend)

@@ -7,7 +7,7 @@ through the process group (``all_gather_object``: a few hundred bytes, once)
 and maps the peers.  ``all_reduce_(lo, hi)`` then sums ``buf[lo:hi]`` over all
 ranks in place with one kernel on the current stream (csrc/p2p.hip:
 reduce-scatter + all-gather, every peer read concurrently over its own xGMI
-link; buckets up to ``KDL_P2P_ONESHOT_BYTES`` (256 KiB) take the one-shot
+link; buckets up to ``KDL_TUNE p2p_oneshot_bytes`` (256 KiB) take the one-shot
 kernel instead: every rank sums the whole bucket, two barriers).
 
 Why beside RCCL: on a fully connected 8-GPU MI355X node a ring moves each
@@ -18,7 +18,7 @@ for the small first/last buckets of a DP step.  RCCL stays the default
 transport when every rank is a GPU process on one node.
 
 Failure model: a peer that never arrives makes the kernel time out (bounded
-waits, ``KDL_P2P_TIMEOUT_S``, default 300 s like a process-group timeout:
+waits, ``KDL_TUNE p2p_timeout_s``, default 300 s like a process-group timeout:
 the clock starts at kernel start, so it must cover host-side skew between
 ranks such as a rank-0 checkpoint write) instead of hanging the GPU; the
 timeout sets a bit in a host-mapped word that ``check()`` raises on (callers
@@ -69,7 +69,8 @@ def single_node(group=None) -> bool:
 
 
 def default_timeout_s() -> float:
-    return float(os.environ.get("KDL_P2P_TIMEOUT_S", 300.0))
+    from kubedl_amd.utils.tune import tune
+    return tune("p2p_timeout_s", 300.0)
 
 
 class P2PError(RuntimeError):
@@ -95,7 +96,8 @@ class P2PAllReduce:
         self._ext = ext
         self.sig = ext.p2p_signal_alloc(self.dev)
         self._err_host, self._err_dev = ext.p2p_error_word()
-        oneshot = min(int(os.environ.get("KDL_P2P_ONESHOT_BYTES", 256 * 1024)), ext.p2p_oneshot_max_units() * 16)
+        from kubedl_amd.utils.tune import tune
+        oneshot = min(tune("p2p_oneshot_bytes", 256 * 1024), ext.p2p_oneshot_max_units() * 16)
         mine = (ext.ipc_handle(buf), ext.ipc_handle(self.sig), os.getpid(), oneshot)
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=group)

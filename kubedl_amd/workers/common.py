@@ -36,14 +36,15 @@ _PROGRESS_LAST = [0.0]  # monotonic time of the last progress write
 
 def report_progress(step: int, steps_per_sec: float | None = None, final: bool = False, **kw) -> None:
     """Write the step counter for the kubelet (``KDL_PROGRESS_FILE``).  Writes are
-    throttled to one per ``KDL_PROGRESS_MIN_S`` seconds (default 0.2): a file
+    throttled to one per ``KDL_TUNE progress_min_s`` seconds (default 0.2): a file
     write + rename costs tens of us of host time, ~10 % of a 0.47 ms CTR step
     when done every step.  The first call and ``final=True`` always write."""
     path = os.environ.get("KDL_PROGRESS_FILE")
     if not path:
         return
     now = time.monotonic()
-    min_s = float(os.environ.get("KDL_PROGRESS_MIN_S", "0.2") or 0)
+    from kubedl_amd.utils.tune import tune
+    min_s = tune("progress_min_s", 0.2)
     if not final and _PROGRESS_LAST[0] and now - _PROGRESS_LAST[0] < min_s:
         return
     _PROGRESS_LAST[0] = now

@@ -34,10 +34,11 @@ from kubedl_amd.parallel import dist as kdist
 from kubedl_amd.parallel.ddp import FlatDDP
 from kubedl_amd.utils.checkpoint import Checkpointer
 from kubedl_amd.utils.trace import StepLog, trace_range
+from kubedl_amd.utils.tune import tune
 from kubedl_amd.workers import common
 
 
-_LOSS_ALLREDUCE = os.environ.get("KDL_LOSS_ALLREDUCE", "1") != "0"
+_LOSS_ALLREDUCE = tune("loss_allreduce", True)
 
 
 class ResNetTrainer:
@@ -45,13 +46,40 @@ class ResNetTrainer:
                  num_classes: int = 1000, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 5e-5, tiny: bool = False,
                  bn_backend: str = "auto", bucket_cap_mb: float = 12.0, seed: int = 0,
-                 conv_benchmark: bool = False, engine: str = "auto"):
+                 conv_benchmark: bool = False, engine: str = "auto", on_streams_ready=None):
         """``engine``: "fused" runs the step through ``models.resnet_engine``
         (fused 1x1-conv GEMMs + staged BN, explicit backward); "autograd" runs
         the module under autograd; "auto" = fused on the GPU when the model's
-        channel counts fit the GEMM tiles (multiples of 64), else autograd."""
+        channel counts fit the GEMM tiles (multiples of 64), else autograd.
+
+        ``on_streams_ready``: called once the step's streams (compute + the
+        engine's weight-gradient side stream) exist and have run a kernel, i.e.
+        before the model is built -- the bench starts the RCCL communicator's
+        bootstrap there, on a helper thread, so it overlaps the weight init,
+        the workspaces and the first transposes instead of following them
+        (after the stream touch: RCCL's own streams must not claim the
+        hardware queues first, profiles/r03_stream_touch_ab.txt)."""
         self.info = info
         dev = info.device
+        if engine == "auto":
+            engine = "fused" if (dev.type == "cuda" and not tiny and bn_backend != "torch") else "autograd"
+        # the step runs on a non-blocking stream of its own, never the null
+        # stream: with an RCCL process group present the null stream loses the
+        # engine's side-stream overlap (-9 %, ops/streams.py); the caller's
+        # stream waits for it after each step
+        from kubedl_amd.ops.streams import compute_stream, side_stream
+        self.stream = compute_stream(dev)
+        side = None
+        eopts = None
+        if dev.type == "cuda" and engine == "fused":
+            from kubedl_amd.models.resnet_engine import EngineOptions
+            eopts = EngineOptions.from_env()
+            side = side_stream(dev, eopts.side_prio) if eopts.side else None
+        self._side = side
+        if dev.type == "cuda":
+            self.touch_streams()
+        if on_streams_ready is not None:
+            on_streams_ready(self.stream)
         if dev.type == "cuda":
             # MIOpen find (benchmark) vs immediate-mode heuristics: A/B'd in profiles/
             torch.backends.cudnn.benchmark = bool(conv_benchmark)
@@ -72,8 +100,6 @@ class ResNetTrainer:
         self.model = model
         self.dtype = dtype
         self.space = FlatParamSpace(model, dtype=dtype, device=dev)
-        if engine == "auto":
-            engine = "fused" if (dev.type == "cuda" and not tiny and bn_backend != "torch") else "autograd"
         self.engine_kind = engine
         self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb,
                            direct=(engine == "fused"))
@@ -81,7 +107,8 @@ class ResNetTrainer:
         if engine == "fused":
             from kubedl_amd.models.resnet_engine import ResNetEngine
             self.engine = ResNetEngine(model, backend="hip" if dev.type == "cuda" else "torch",
-                                       grad_view=self.space.grad_view, on_ready=self.ddp.ready)
+                                       grad_view=self.space.grad_view, on_ready=self.ddp.ready, options=eopts,
+                                       side=side)
             self.ddp.join_stream = self.engine.side
         self.opt = FusedSGD(self.space, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.opt.grad_scale = self.ddp.grad_scale
@@ -98,14 +125,6 @@ class ResNetTrainer:
         self._loss_work = None
         self._loss_sum = None
         self._loss_div = 1
-        # the step runs on a non-blocking stream of its own, never the null
-        # stream: with an RCCL process group present the null stream loses the
-        # engine's side-stream overlap (-9 %, ops/streams.py); the caller's
-        # stream waits for it after each step
-        from kubedl_amd.ops.streams import compute_stream
-        self.stream = compute_stream(dev)
-        if dev.type == "cuda":
-            self.touch_streams()
 
     def touch_streams(self) -> None:
         """One tiny kernel on each stream the step uses (compute, weight-gradient
@@ -115,7 +134,7 @@ class ResNetTrainer:
         per step untouched vs 19.28-19.44 touched (19.41 with the communicator
         built lazily inside step 1; the side stream's overlap is what is lost),
         profiles/r03_stream_touch_ab.txt."""
-        for s in (self.stream, getattr(self.engine, "side", None)):
+        for s in (self.stream, getattr(self, "_side", None)):
             if s is not None:
                 with torch.cuda.stream(s):
                     torch.zeros(1, device=self.info.device).add_(1)
@@ -127,50 +146,15 @@ class ResNetTrainer:
         caller = torch.cuda.current_stream(self.info.device)
         self.stream.wait_stream(caller)
         with torch.cuda.stream(self.stream):
-            loss = self._graph_step() if self._graph_mode() else self._step()
+            loss = self._step()
         caller.wait_stream(self.stream)
         return loss
-
-    # ------------------------------------------------------------ HIP graph replay
-    # KDL_HIP_GRAPH=1: after KDL_HIP_GRAPH_WARMUP eager steps (workspaces, weight
-    # transposes and kernel code objects in place) the whole step -- zero_grad,
-    # the engine's forward/backward on the main and side streams (event
-    # fork/join), the fused optimizer -- is captured once into a hipGraph and
-    # replayed: one host call per step instead of ~600 launches, and no launch
-    # gaps between the kernels.  Same work every step (static input batch and
-    # parameter/gradient storage); the loss all-reduce runs after the replay.
-    # World 1 only: DP gradient buckets are collectives issued from backward hooks.
-    def _graph_mode(self) -> bool:
-        if not hasattr(self, "_graph_state"):
-            on = (os.environ.get("KDL_HIP_GRAPH", "0") == "1" and self.engine is not None
-                  and self.info.device.type == "cuda" and not self.ddp.active)
-            self._graph_state = {"on": on, "eager": 0, "graph": None, "loss": None}
-        return self._graph_state["on"]
-
-    def _graph_step(self) -> torch.Tensor:
-        gs = self._graph_state
-        if gs["graph"] is None:
-            if gs["eager"] < int(os.environ.get("KDL_HIP_GRAPH_WARMUP", "2")):
-                gs["eager"] += 1
-                return self._step()
-            torch.cuda.synchronize(self.info.device)
-            g = torch.cuda.CUDAGraph()
-            # thread_local: the process group's watchdog thread keeps polling its
-            # events during the capture; in the default (global) mode that poll
-            # invalidates the capture (hipErrorStreamCaptureUnsupported)
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
-                loss = self._step_body()
-            gs["graph"], gs["loss"] = g, loss
-            self.opt.step_count -= 1  # the capture executed nothing; each replay is one step
-        gs["graph"].replay()
-        self.opt.step_count += 1
-        return self._finish_loss(gs["loss"])
 
     def _step(self) -> torch.Tensor:
         return self._finish_loss(self._step_body())
 
     def _step_body(self) -> torch.Tensor:
-        """The step's device work (what a hipGraph captures): returns the loss."""
+        """The step's device work: returns the loss."""
         self.space.zero_grad()
         with trace_range("forward_backward"):
             if self.engine is not None:
@@ -200,7 +184,7 @@ class ResNetTrainer:
 
     def loss(self) -> torch.Tensor:
         """The last step's loss averaged over ranks (waits for its all-reduce);
-        without the all-reduce (no process group, or KDL_LOSS_ALLREDUCE=0) this
+        without the all-reduce (no process group, or KDL_TUNE loss_allreduce=0) this
         rank's own loss -- divided only when the sum actually ran."""
         if self._loss_work is not None:
             self._loss_work.wait()
@@ -300,9 +284,9 @@ def run(args) -> dict:
 
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="ResNet-50 DP bf16 trainer (PyTorchJob worker)")
-    ap.add_argument("--steps", type=int, default=int(os.environ.get("KDL_STEPS", 20)))
-    ap.add_argument("--warmup", type=int, default=int(os.environ.get("KDL_WARMUP", 5)))
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("KDL_BATCH", 256)))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--tiny", action="store_true", help="tiny ResNet (tests)")
     ap.add_argument("--cpu", action="store_true")

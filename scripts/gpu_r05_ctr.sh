@@ -13,7 +13,7 @@ tail -1 gpurun_out/r05/ctr_tests.log
 for i in 1 2; do
   for ex in fixed slack auto; do
     a=$ex; s=0; [ $ex = slack ] && { a=fixed; s=1.5; }
-    KDL_CTR_A2A_SLACK=$s timeout -k 10 240 python -u -m kubedl_amd.workers.xdl_ctr --steps 2000 --warmup 20 --exchange $a > gpurun_out/r05/ctr_$ex$i.log 2>&1 || exit $?
+    KDL_TUNE=ctr_a2a_slack=$s timeout -k 10 240 python -u -m kubedl_amd.workers.xdl_ctr --steps 2000 --warmup 20 --exchange $a > gpurun_out/r05/ctr_$ex$i.log 2>&1 || exit $?
     tail -1 gpurun_out/r05/ctr_$ex$i.log
   done
 done

@@ -151,9 +151,9 @@ def _exchange_bytes_worker(rank, world, port, out, slack, strict):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     # lossy mode is an explicit opt-in (STRICT=0); strict is the default
     if strict:
-        os.environ.pop("KDL_CTR_A2A_STRICT", None)
+        os.environ.pop("KDL_TUNE", None)
     else:
-        os.environ["KDL_CTR_A2A_STRICT"] = "0"
+        os.environ["KDL_TUNE"] = "ctr_a2a_strict=0"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dim, n, vocab = 8, 2048, 1 << 22
     fixed = ShardedEmbedding(vocab, dim, list(range(world)), rank, world, "cpu", lr=0.1, max_ids=n, slack=slack)
@@ -225,7 +225,7 @@ def test_ctr_exchange_default_is_exact():
 def test_ctr_exchange_overflow_counted_and_capacity_grows():
     """A burst above the agreed capacity (every id owned by one rank) raises on
     every rank by default (no silent loss); in the explicit lossy
-    mode (KDL_CTR_A2A_STRICT=0) it is counted on every rank (read LAG pulls
+    mode (KDL_TUNE ctr_a2a_strict=0) it is counted on every rank (read LAG pulls
     later, or by finalize) and the capacity grows."""
     out = _run_exchange(0.9)
     for r in range(4):

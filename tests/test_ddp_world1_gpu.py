@@ -1,5 +1,5 @@
 """World-1 RCCL all-reduce through the engine's direct-mode DDP on a real
-MI355X (``KDL_DDP_WORLD1=1``): a one-rank "nccl" (= RCCL) process group, the
+MI355X (``KDL_TUNE ddp_world1=1``): a one-rank "nccl" (= RCCL) process group, the
 gradient buckets launched from inside the fused backward and all-reduced by
 RCCL exactly as on N GPUs -- the result must equal the step without DDP
 (a one-rank sum is the identity, scale 1)."""
@@ -25,7 +25,7 @@ dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cu
 info = DistInfo(0, 1, 0, torch.device("cuda", 0), "nccl")
 out = []
 for world1 in ("1", "0"):
-    os.environ["KDL_DDP_WORLD1"] = world1
+    os.environ["KDL_TUNE"] = f"ddp_world1={world1}"
     tr = ResNetTrainer(info, batch=8, image=64, num_classes=10, bn_backend="hip", engine="fused",
                        bucket_cap_mb=2.0, seed=0)
     assert tr.ddp.active == (world1 == "1") and (world1 == "0" or len(tr.ddp.buckets) > 1)

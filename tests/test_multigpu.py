@@ -10,7 +10,7 @@ itself unless ``torch.cuda.device_count()`` covers its world size, so the
 1-GPU box reports skips and an 8-GPU node runs all of them unchanged.
 
 The last test is the CPU (gloo, 8 ranks) bound on bf16 gradient sums that
-motivates ``KDL_DDP_REDUCE=fp32``.
+motivates ``KDL_TUNE ddp_reduce=fp32``.
 """
 import os
 import socket
@@ -67,7 +67,7 @@ def _init(rank, world, port, backend="nccl"):
     from kubedl_amd.runtime.gpu_env import rank_gpu_env
     os.environ.update(rank_gpu_env([str(rank)], [str(r) for r in range(world)]))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      KDL_DIST_BACKEND=backend, KDL_PG_EAGER="1")
+                      KDL_DIST_BACKEND=backend, KDL_TUNE="pg_eager=1")
     info = kdist.init_from_env()
     assert info.device == torch.device("cuda", 0), info
     assert os.environ["HIP_VISIBLE_DEVICES"].split(",")[0] == str(rank)
@@ -411,7 +411,7 @@ def _bf16_sum_worker(rank, world, port, q, n):
 def test_bf16_gradient_sum_error_bound_world8_cpu():
     """Summing bf16 gradients in bf16 across 8 ranks rounds at every step: the
     error is bounded by world * ulp(max |sum|) and is measurably larger on
-    average than an fp32 sum rounded once -- the case for KDL_DDP_REDUCE=fp32."""
+    average than an fp32 sum rounded once -- the case for KDL_TUNE ddp_reduce=fp32."""
     world = 8
     res = _spawn_cpu(_bf16_sum_worker, world, 1 << 16)
     for _, m16, m32, a16, a32, scale in res:
@@ -437,9 +437,9 @@ def _spawn_cpu(target, world, *args, timeout=240):
 
 def test_ddp_fp32_reduce_option_cpu(monkeypatch):
     from kubedl_amd.parallel import ddp
-    monkeypatch.delenv("KDL_DDP_REDUCE", raising=False)
+    monkeypatch.delenv("KDL_TUNE", raising=False)
     assert not ddp.reduce_fp32_wanted()
-    monkeypatch.setenv("KDL_DDP_REDUCE", "fp32")
+    monkeypatch.setenv("KDL_TUNE", "ddp_reduce=fp32")
     assert ddp.reduce_fp32_wanted()
 
 
@@ -447,7 +447,7 @@ def _ddp_fp32_worker(rank, world, port, q):
     import torch.distributed as dist
     from kubedl_amd.ops.optim import FlatParamSpace
     from kubedl_amd.parallel.ddp import FlatDDP
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KDL_DDP_REDUCE="fp32")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KDL_TUNE="ddp_reduce=fp32")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     m = torch.nn.Sequential(torch.nn.Linear(64, 32), torch.nn.Linear(32, 8))

@@ -366,9 +366,26 @@ def test_engine_options_from_one_variable(monkeypatch):
     from kubedl_amd.models.resnet_engine import EngineOptions
     monkeypatch.delenv("KDL_ENGINE", raising=False)
     assert EngineOptions.from_env() == EngineOptions()
-    monkeypatch.setenv("KDL_ENGINE", "side=0, res_pro_kmax=256,bn_fin=kernel,halo_pro=2")
+    monkeypatch.setenv("KDL_ENGINE", "side=0, res_pro_kmax=256,bn_fin=kernel,halo_pro=0")
     o = EngineOptions.from_env()
-    assert (o.side, o.res_pro_kmax, o.bn_fin, o.halo_pro) == (False, 256, "kernel", 2)
+    assert (o.side, o.res_pro_kmax, o.bn_fin, o.halo_pro) == (False, 256, "kernel", 0)
     monkeypatch.setenv("KDL_ENGINE", "no_such_knob=1")
     with pytest.raises(ValueError, match="unknown option"):
         EngineOptions.from_env()
+
+
+def test_knob_surface_stays_small():
+    """A/B switches live in KDL_TUNE / KDL_ENGINE; every other
+    KDL_* name in the package and the native sources is part of the runtime
+    contract (pod env, rendezvous, paths) -- fewer than 40 distinct names."""
+    import pathlib
+    import re
+    root = pathlib.Path(__file__).resolve().parents[1]
+    names = set()
+    for sub, pats in (("kubedl_amd", ("*.py",)), ("csrc", ("*.hip", "*.cpp", "*.h"))):
+        for pat in pats:
+            for f in (root / sub).rglob(pat):
+                names |= set(re.findall(r"KDL_[A-Z0-9_]+", f.read_text(errors="ignore")))
+    assert len(names) < 40, sorted(names)
+    for gone in ("KDL_HIP_GRAPH", "KDL_GBDT_GRAPH", "KDL_STREAMS", "KDL_MAIN_PRIO", "KDL_DDP_WORLD1"):
+        assert gone not in names

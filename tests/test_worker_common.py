@@ -7,7 +7,7 @@ from kubedl_amd.workers import common
 def test_progress_writes_are_throttled_but_first_and_final_land(tmp_path, monkeypatch):
     path = tmp_path / "progress.0"
     monkeypatch.setenv("KDL_PROGRESS_FILE", str(path))
-    monkeypatch.setenv("KDL_PROGRESS_MIN_S", "30")
+    monkeypatch.setenv("KDL_TUNE", "progress_min_s=30")
     monkeypatch.setattr(common, "_PROGRESS_LAST", [0.0])
     common.report_progress(1)
     assert json.loads(path.read_text())["step"] == 1
@@ -21,7 +21,7 @@ def test_progress_writes_are_throttled_but_first_and_final_land(tmp_path, monkey
 def test_progress_every_step_without_throttle(tmp_path, monkeypatch):
     path = tmp_path / "progress.0"
     monkeypatch.setenv("KDL_PROGRESS_FILE", str(path))
-    monkeypatch.setenv("KDL_PROGRESS_MIN_S", "0")
+    monkeypatch.setenv("KDL_TUNE", "progress_min_s=0")
     monkeypatch.setattr(common, "_PROGRESS_LAST", [0.0])
     for s in range(1, 4):
         common.report_progress(s, 2.5)
