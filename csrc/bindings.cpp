@@ -419,6 +419,20 @@ void p2p_allreduce(const std::vector<int64_t>& bufs, const std::vector<int64_t>&
 }
 
 // ------------------------------------------------------------------ GBDT
+std::vector<at::Tensor> gbdt_grad_hess(const at::Tensor& pred, const at::Tensor& y, int64_t obj) {
+  TORCH_CHECK(pred.is_cuda() && pred.scalar_type() == at::kFloat && pred.dim() == 2 && pred.is_contiguous(),
+              "gbdt_grad_hess: pred fp32 [n, K] contiguous");
+  TORCH_CHECK(y.scalar_type() == at::kFloat && y.is_contiguous() && y.numel() == pred.size(0),
+              "gbdt_grad_hess: y fp32 [n]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(pred.device());
+  auto g = at::empty_like(pred), h = at::empty_like(pred);
+  check_hip(kdl::gbdt_grad_hess(pred.data_ptr<float>(), y.data_ptr<float>(), pred.size(0),
+                                static_cast<int>(pred.size(1)), static_cast<int>(obj), g.data_ptr<float>(),
+                                h.data_ptr<float>(), cur_stream()),
+            "gbdt_grad_hess");
+  return {g, h};
+}
+
 void gbdt_hist(const at::Tensor& bins, const at::Tensor& grad, const at::Tensor& hess, int64_t gh_stride,
                const at::Tensor& rows, const at::Tensor& seg, int64_t max_rows_per_node, int64_t num_bins,
                at::Tensor hist) {
@@ -1595,6 +1609,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_grads", &pack_grads, "multi-tensor gather of gradient tensors into a flat buffer");
   m.def("pack_grads_ptrs", &pack_grads_ptrs, "pack_grads with the source pointers as kernel arguments");
   m.attr("pack_arg_ptrs") = kdl::kPackArgPtrs;
+  m.def("gbdt_grad_hess", &gbdt_grad_hess, "boosting round gradient + hessian in one launch (0 reg, 1 logistic, 2 softmax)");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");

@@ -41,6 +41,7 @@
 // distributed part here is an RCCL all-reduce of the level's histograms.
 #include "common.h"
 #include "kdl_api.h"
+#include "tune.h"
 
 namespace kdl {
 namespace {
@@ -208,13 +209,28 @@ __global__ __launch_bounds__(256) void route_rows_kernel(
 // prefix of ceil(size / rpb), chunk_off[nb] = total).  Each wave keeps UNROLL
 // row slots in flight (row ids, g/h and bin codes loaded before any LDS
 // atomic) so the dependent global loads overlap.
+// Quantised gradients (XGBoost's GPU-hist idea, here for the LDS rate): float
+// LDS atomics are the slow path on gfx950 -- the same round with the h
+// ds_add_f32 dropped ran 2.9x faster, and with both adds as ds_add_u32 as fast
+// as with no atomics at all (383 -> 1446 rounds/s, KDL_TUNE-priced variants,
+// profiles/r05_gbdt_price.txt).  So each block accumulates fixed-point
+// integers: q = rint(g * sg) with sg = 2^30 / (rpb * max|g|) -- a block sums
+// at most rpb rows, so |sum| <= 2^30 never overflows, and a row's rounding
+// error is <= 2^-31 rpb max|g| (~1e-6 max|g| at 2048 rows per chunk).  The
+// block's exact integer sums are converted back (/ sg) when flushed into the
+// node's fp32 histogram.  ``gh_max`` = {max |g|, max h} of the tree's rows
+// (gbdt_gh_absmax).
+constexpr float kQuantRange = 1073741824.f;  // 2^30
+
 template <int UNROLL>
 __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
     const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
     int64_t gh_stride, const int32_t* __restrict__ rows, const int32_t* __restrict__ blo,
     const int32_t* __restrict__ bhi, const int32_t* __restrict__ chunk_off, int nb, int F, int B, int rpb, int fp,
-    float* __restrict__ hist) {
-  extern __shared__ float lds[];  // [fp][B][2]
+    const float* __restrict__ gh_max, float* __restrict__ hist) {
+  // LDS: two int planes, g [fp][B] then h [fp][B]
+  extern __shared__ int qlds[];
+  int* qh_pl = qlds + fp * B;
   const int c = blockIdx.x;
   if (c >= chunk_off[nb]) return;  // block-uniform
   int a = 0, z = nb;               // last j with chunk_off[j] <= c
@@ -228,7 +244,10 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
   const int f0 = blockIdx.y * fp;
   const int nf = (F - f0) < fp ? (F - f0) : fp;
   const int t = threadIdx.x;
-  for (int i = t; i < nf * B * 2; i += kHistBlock) lds[i] = 0.f;
+  const float mg = gh_max[0], mh = gh_max[1];
+  const float sg = mg > 0.f ? kQuantRange / (static_cast<float>(rpb) * mg) : 0.f;
+  const float sh = mh > 0.f ? kQuantRange / (static_cast<float>(rpb) * mh) : 0.f;
+  for (int i = t; i < 2 * fp * B; i += kHistBlock) qlds[i] = 0;
   __syncthreads();
   const int lane = t & 63, wave = t >> 6;
   const int rpw = 64 / fp;
@@ -254,17 +273,45 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       if (row[u] >= 0 && fl < nf) {
-        float* p = lds + (fl * B + b[u]) * 2;
-        atomicAdd(p, g[u]);
-        atomicAdd(p + 1, h[u]);
+        const int e = fl * B + b[u];
+        atomicAdd(qlds + e, __float2int_rn(g[u] * sg));
+        atomicAdd(qh_pl + e, __float2int_rn(h[u] * sh));
       }
     }
   }
   __syncthreads();
   float* out = hist + (static_cast<int64_t>(j) * F + f0) * B * 2;
-  for (int i = t; i < nf * B * 2; i += kHistBlock) {
-    const float v = lds[i];
-    if (v != 0.f) __hip_atomic_fetch_add(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float ig = sg > 0.f ? 1.f / sg : 0.f, ih = sh > 0.f ? 1.f / sh : 0.f;
+  for (int i = t; i < nf * B; i += kHistBlock) {
+    const int vg = qlds[i], vh = qh_pl[i];
+    if (vg != 0) __hip_atomic_fetch_add(out + 2 * i, static_cast<float>(vg) * ig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (vh != 0) __hip_atomic_fetch_add(out + 2 * i + 1, static_cast<float>(vh) * ih, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// {max |g|, max h} over n rows into out[2] (zeroed by the caller): a block max,
+// then one integer atomicMax per value (non-negative floats order as their bits)
+__global__ __launch_bounds__(256) void gh_absmax_kernel(const float* __restrict__ g, const float* __restrict__ h,
+                                                        int n, unsigned* __restrict__ out) {
+  float mg = 0.f, mh = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    mg = fmaxf(mg, fabsf(g[i]));
+    mh = fmaxf(mh, fabsf(h[i]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmaxf(mg, __shfl_xor(mg, o));
+    mh = fmaxf(mh, __shfl_xor(mh, o));
+  }
+  __shared__ float sm[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { sm[0][w] = mg; sm[1][w] = mh; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mg = fmaxf(fmaxf(sm[0][0], sm[0][1]), fmaxf(sm[0][2], sm[0][3]));
+    mh = fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3]));
+    atomicMax(out, __float_as_uint(mg));
+    atomicMax(out + 1, __float_as_uint(mh));
   }
 }
 
@@ -451,7 +498,52 @@ __global__ __launch_bounds__(256) void quantise_kernel(const float* __restrict__
   out[e] = static_cast<uint8_t>(a < max_code ? a : max_code);
 }
 
+// Gradient / hessian of a boosting round in one pass over (pred, y):
+//   obj 0 reg:squarederror   g = p - y,            h = 1
+//   obj 1 binary:logistic    s = 1 / (1 + e^-p),   g = s - y,     h = max(s (1 - s), 1e-16)
+//   obj 2 multi:softprob     s = softmax_k(p),     g = s - [y == k], h = max(2 s (1 - s), 1e-16)
+// pred / g / h are [n, K] row-major (K = 1 except multi); one thread per row.
+// The same fp32 expressions as the torch composition (models/gbdt.py) -- one
+// launch instead of ~5 elementwise kernels per round.
+__global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict__ pred, const float* __restrict__ y,
+                                                        int64_t n, int K, int obj, float* __restrict__ g,
+                                                        float* __restrict__ h) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float yi = y[i];
+  if (obj == 0) {
+    for (int k = 0; k < K; ++k) {
+      g[i * K + k] = pred[i * K + k] - yi;
+      h[i * K + k] = 1.f;
+    }
+  } else if (obj == 1) {
+    const float s = 1.f / (1.f + expf(-pred[i]));
+    g[i] = s - yi;
+    h[i] = fmaxf(s * (1.f - s), 1e-16f);
+  } else {
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, pred[i * K + k]);
+    float z = 0.f;
+    for (int k = 0; k < K; ++k) z += expf(pred[i * K + k] - mx);
+    const int cls = static_cast<int>(yi);
+    for (int k = 0; k < K; ++k) {
+      const float s = expf(pred[i * K + k] - mx) / z;
+      g[i * K + k] = s - (k == cls ? 1.f : 0.f);
+      h[i * K + k] = fmaxf(2.f * s * (1.f - s), 1e-16f);
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t gbdt_grad_hess(const float* pred, const float* y, int64_t n, int K, int obj, float* g, float* h,
+                          hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (obj < 0 || obj > 2 || K < 1 || (obj == 1 && K != 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(grad_hess_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, pred, y, n, K,
+                     obj, g, h);
+  return hipGetLastError();
+}
 
 hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                            const int32_t* rows, const int32_t* seg, int num_nodes, int max_rows_per_node,
@@ -502,17 +594,26 @@ static hipError_t hist_lds_attr() {
   return hipSuccess;
 }
 
+hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* out, hipStream_t s) {
+  RETURN_IF_HIP_ERR(hipMemsetAsync(out, 0, 2 * sizeof(float), s));
+  if (n <= 0) return hipSuccess;
+  int blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(gh_absmax_kernel, dim3(blocks), dim3(256), 0, s, grad, hess, n, reinterpret_cast<unsigned*>(out));
+  return hipGetLastError();
+}
+
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
-                        int max_chunks, int rpb, int F, int B, float* hist, hipStream_t s) {
+                        int max_chunks, int rpb, int F, int B, const float* gh_max, float* hist, hipStream_t s) {
   if (nb <= 0 || F <= 0 || max_chunks <= 0) return hipSuccess;
   hipLaunchKernelGGL(hist_plan_kernel, dim3(1), dim3(64), 0, s, blo, bhi, nb, rpb, chunk_off);
   const int fp = hist_fp(F);
   RETURN_IF_HIP_ERR(hist_lds_attr());
   dim3 grid(max_chunks, (F + fp - 1) / fp);
-  const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(float);
+  const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(int);
   hipLaunchKernelGGL((hist_build_wq_kernel<4>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows,
-                     blo, bhi, chunk_off, nb, F, B, rpb, fp, hist);
+                     blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist);
   return hipGetLastError();
 }
 

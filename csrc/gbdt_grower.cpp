@@ -54,12 +54,11 @@ class GbdtGrower {
     gamma_ = static_cast<float>(gamma);
     lr_ = static_cast<float>(lr);
     mcw_ = static_cast<float>(min_child_weight);
-    // rows per histogram chunk: ~1000-2000 chunks over the root level, 256..2048.
-    // Measured at 2M x 28 (profiles/r02_gbdt_hist_sweep.txt): 1024 beats longer
-    // chunks (fewer flushes: 2048 +7 %, 4096 +32 %, 8192 2.3x the histogram time);
-    // deeper unrolling, a bank-spread LDS image and a branch-free body were all
-    // neutral or slower -- the LDS float-atomic rate bounds the build.
-    // KDL_TUNE gbdt_rpb overrides.
+    // rows per histogram chunk: ~1000-2000 chunks over the root level, 256..2048
+    // (also the quantisation's per-block row bound, csrc/gbdt.hip).  Measured at
+    // 2M x 28 with float LDS atomics (profiles/r02_gbdt_hist_sweep.txt): 1024 beat
+    // longer chunks; the float-atomic rate bounded the build then -- the integer
+    // planes (round 5) removed that bound.  KDL_TUNE gbdt_rpb overrides.
     const int64_t target = std::max(0, kdl::tune_int("gbdt_rpb", 0));
     rpb_ = 256;
     if (target > 0) {
@@ -103,6 +102,7 @@ class GbdtGrower {
     bhi_ = at::zeros({std::max<int64_t>(maxL / 2, 1)}, io);
     chunk_off_ = at::zeros({std::max<int64_t>(maxL / 2, 1) + 1}, io);
     root_lo_hi_ = at::tensor({0, N_}, io.device(at::kCPU)).to(bins.device());
+    gh_max_ = at::zeros({2}, fo);
   }
 
   // Reset the per-tree state and build the root histogram (returned: the
@@ -126,9 +126,12 @@ class GbdtGrower {
     hi_[0].fill_(N_);
     auto root = hist_cur_.narrow(0, 0, 1);
     root.zero_();
+    // the tree's fixed-point scale of the quantised histogram sums (csrc/gbdt.hip)
+    ck(kdl::gbdt_gh_absmax(fp(grad_), fp(hess_), N_, fp(gh_max_), stream()), "gbdt_gh_absmax");
     const int max_chunks = (N_ + rpb_ - 1) / rpb_ + 1;
     ck(kdl::gbdt_hist_wq(bins_.data_ptr<uint8_t>(), fp(grad_), fp(hess_), 1, ip(rows_), ip(root_lo_hi_),
-                         ip(root_lo_hi_) + 1, ip(chunk_off_), 1, max_chunks, rpb_, F_, B_, fp(root), stream()),
+                         ip(root_lo_hi_) + 1, ip(chunk_off_), 1, max_chunks, rpb_, F_, B_, fp(gh_max_), fp(root),
+                         stream()),
        "gbdt_hist_wq(root)");
     builds_ += 1;
     return root;
@@ -178,7 +181,7 @@ class GbdtGrower {
     built.zero_();
     const int max_chunks = (N_ + rpb_ - 1) / rpb_ + L;
     ck(kdl::gbdt_hist_wq(bins_.data_ptr<uint8_t>(), fp(grad_), fp(hess_), 1, ip(rows_), ip(blo_), ip(bhi_),
-                         ip(chunk_off_), L, max_chunks, rpb_, F_, B_, fp(built), stream()),
+                         ip(chunk_off_), L, max_chunks, rpb_, F_, B_, fp(gh_max_), fp(built), stream()),
        "gbdt_hist_wq");
     builds_ += L;
     return built;
@@ -221,7 +224,7 @@ class GbdtGrower {
   at::Tensor iota_, rows_, rows_next_, node_of_row_, flag_, sc_, root_lo_hi_;
   std::vector<at::Tensor> lo_, hi_, exists_;
   at::Tensor split_, gain_, sbin_, gl_, hl_, tot_, feat_, tbin_, thr_, val_;
-  at::Tensor hist_cur_, hist_next_, built_, cnt_, build_child_, blo_, bhi_, chunk_off_;
+  at::Tensor hist_cur_, hist_next_, built_, cnt_, build_child_, blo_, bhi_, chunk_off_, gh_max_;
 };
 
 at::Tensor gbdt_quantise(const at::Tensor& X, const at::Tensor& cuts, int64_t num_bins) {

@@ -143,6 +143,10 @@ int p2p_oneshot_max_units();
 hipError_t p2p_allreduce(const P2PArgs& a, bool bf16, bool oneshot, hipStream_t s);
 
 // ---- gbdt.hip (histogram GBDT for the XGBoostJob worker)
+// one boosting round's gradient / hessian (obj 0 reg:squarederror, 1 binary:logistic,
+// 2 multi:softprob; pred / g / h [n, K] fp32, y [n] fp32 labels / class ids)
+hipError_t gbdt_grad_hess(const float* pred, const float* y, int64_t n, int K, int obj, float* g, float* h,
+                          hipStream_t s);
 hipError_t gbdt_hist_build(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                            const int32_t* rows, const int32_t* seg, int num_nodes, int max_rows_per_node,
                            int F, int B, float* hist, hipStream_t s);
@@ -150,9 +154,12 @@ hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float
                            float min_child_weight, float* best_gain, int32_t* best_bin, float* best_gl,
                            float* best_hl, float* node_tot, hipStream_t s);
 // device-resident growth (see gbdt.hip header)
+// gh_max: {max |g|, max h} of the rows (gbdt_gh_absmax): the fixed-point scale
+// of the quantised per-block sums
+hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* out, hipStream_t s);
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
-                        int max_chunks, int rpb, int F, int B, float* hist, hipStream_t s);
+                        int max_chunks, int rpb, int F, int B, const float* gh_max, float* hist, hipStream_t s);
 hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot, const float* cuts,
                        const int32_t* exists, int L, int F, int ncut, int h0, int can_split, float lambda,
                        float gamma, float lr, int32_t* t_feat, int32_t* t_bin, float* t_thr, float* t_val,

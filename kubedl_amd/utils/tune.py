@@ -13,6 +13,7 @@ streams             pool        step streams: pool | dedicated | null (ops/strea
 main_prio           -1          HIP priority of the step's compute stream
 loss_allreduce      1           sum the step loss over ranks (RCCL) every step
 comm_probe          1           time the first collective (RCCL bootstrap) apart
+comm_overlap        1           run that bootstrap on a helper thread during the model build
 world1_pg           1           build a one-rank process group at world 1
 pg_eager            0           bind the RCCL communicator at init_process_group
 ddp_world1          0           world-1 DDP rehearsal: 0 | 1 | copy (parallel/ddp.py)

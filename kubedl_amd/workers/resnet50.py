@@ -67,8 +67,13 @@ class ResNetTrainer:
         # stream: with an RCCL process group present the null stream loses the
         # engine's side-stream overlap (-9 %, ops/streams.py); the caller's
         # stream waits for it after each step
+        # Hardware-queue order as the measured step had it: the null stream (the
+        # weight init's) first, then the weight-gradient side stream, then the
+        # compute stream, all before RCCL creates its own streams
+        # (profiles/r03_stream_touch_ab.txt, profiles/r05_comm_overlap_ab.jsonl)
         from kubedl_amd.ops.streams import compute_stream, side_stream
-        self.stream = compute_stream(dev)
+        if dev.type == "cuda":
+            torch.zeros(1, device=dev).add_(1)
         side = None
         eopts = None
         if dev.type == "cuda" and engine == "fused":
@@ -76,6 +81,10 @@ class ResNetTrainer:
             eopts = EngineOptions.from_env()
             side = side_stream(dev, eopts.side_prio) if eopts.side else None
         self._side = side
+        if side is not None:
+            with torch.cuda.stream(side):
+                torch.zeros(1, device=dev).add_(1)
+        self.stream = compute_stream(dev)
         if dev.type == "cuda":
             self.touch_streams()
         if on_streams_ready is not None:

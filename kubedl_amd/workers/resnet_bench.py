@@ -90,7 +90,11 @@ def run(args, launcher: str) -> int:
     threads = []
 
     def start_comm(stream):
-        if not tune("comm_probe", True):
+        # world 1 only: at N > 1 the trainer's own first collective (the DDP
+        # parameter broadcast, FlatDDP.__init__) would race the probe's from
+        # another thread, and collectives must reach RCCL in the same order on
+        # every rank; there the broadcast bootstraps the communicator
+        if info.world_size != 1 or not tune("comm_probe", True) or not tune("comm_overlap", True):
             return
         import threading
 
@@ -111,6 +115,8 @@ def run(args, launcher: str) -> int:
         th.join()
     if "err" in comm:
         raise comm["err"]
+    if not threads and tune("comm_probe", True):  # comm_overlap=0: bootstrap after the model build
+        comm["s"] = kdist.first_collective(info, getattr(trainer, "stream", None))
     sync(info)
     t_model = time.time()
     comm_init_s = comm["s"]
@@ -195,6 +201,11 @@ def run(args, launcher: str) -> int:
             "first_step_s": round(t_first_step - T_PROC_START, 3) if t_first_step else None,
             "t_first_step_unix": round(t_first_step, 3) if t_first_step else None,
             "host_issue_ms_per_step": round(host / args.steps * 1e3, 3),
+            # rank 0's start-up phases (s): imports, process group, model build,
+            # then what was left of the communicator bootstrap after the build
+            "startup": {"imports": round(t_import - T_PROC_START, 3), "process_group": round(t_pg - t_import, 3),
+                        "model": round(t_built - t_pg, 3), "comm_wait": round(t_model - t_built, 3),
+                        "comm_overlap": bool(threads)},
             "final_loss": round(loss, 4),
             # DP gradient buckets: plan + the all-reduce time the step's compute
             # stream waited for (the rest overlapped the backward)

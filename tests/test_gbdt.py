@@ -219,3 +219,23 @@ def test_gpu_device_grower_two_ranks_agree():
         p.join(120)
         assert p.exitcode == 0
     assert out[0] == out[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("objective,K", [("binary:logistic", 1), ("reg:squarederror", 1), ("multi:softprob", 4)])
+def test_gpu_grad_hess_kernel_matches_torch(objective, K):
+    """csrc/gbdt.hip grad_hess_kernel (one launch per round) against the torch
+    composition it replaces (fp32; expf vs torch's exp may differ by an ulp)."""
+    kw = dict(objective=objective)
+    if K > 1:
+        kw["num_class"] = K
+    m = HistGBDT(GBDTParams(**kw), "cuda")
+    torch.manual_seed(0)
+    n = 100003
+    pred = torch.randn(n, K, device="cuda") * 4
+    y = torch.randint(0, K, (n,), device="cuda") if K > 1 else (torch.rand(n, device="cuda") > 0.5).float()
+    g, h = m._grad_hess(pred, y)
+    m.use_hip = False
+    g_ref, h_ref = m._grad_hess(pred, y)
+    torch.testing.assert_close(g, g_ref, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(h, h_ref, atol=1e-6, rtol=1e-5)
