@@ -527,15 +527,18 @@ at::Tensor gemm_bias_act(const at::Tensor& a, const at::Tensor& w, const c10::op
   return c;
 }
 
-// per-device ticket counters of the in-launch reductions (zeroed once; every
-// kernel re-arms its own): slot 0 = head_bce_fwd, 1 = head_bce_bwd, 64.. = relu_bwd_dbias
+// ticket counters of the in-launch reductions (zeroed once; every kernel re-arms
+// its own): slot 0 = head_bce_fwd, 1 = head_bce_bwd, 64.. = relu_bwd_dbias.  One
+// set per (device, stream): launches on ONE stream are ordered, so they may share
+// a counter; two streams running the same kernel at once must not (a block would
+// count the other launch's arrivals and reduce partials that are not ready).
 static at::Tensor ticket_counters(const at::Tensor& like, int64_t base) {
   static std::mutex mu;
-  static std::map<int, at::Tensor> cache;
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> cache;
   std::lock_guard<std::mutex> lk(mu);
-  const int dev = like.get_device();
-  auto it = cache.find(dev);
-  if (it == cache.end()) it = cache.insert_or_assign(dev, at::zeros({1 << 14}, like.options().dtype(at::kInt))).first;
+  const auto key = std::make_pair(static_cast<int>(like.get_device()), cur_stream());
+  auto it = cache.find(key);
+  if (it == cache.end()) it = cache.insert_or_assign(key, at::zeros({1 << 14}, like.options().dtype(at::kInt))).first;
   return it->second.narrow(0, base, (1 << 14) - base);
 }
 

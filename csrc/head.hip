@@ -240,11 +240,16 @@ __global__ __launch_bounds__(256) void head_ce_kernel(const float* __restrict__ 
   float se = 0.f;
   for (int l = t; l < L; l += 256) se += __expf(z[l] - mx);
   se = block_reduce(se, red, false);
-  const int yn = static_cast<int>(y[n]);
-  if (t == 0) lrow[n] = __logf(se) + mx - z[yn];
+  const int64_t y64 = y[n];
+  // a label outside [0, L) (e.g. an ignore_index of -100) never indexes z: its
+  // row's loss is NaN -- the step's mean loss turns NaN, loudly, as the
+  // autograd head would have raised -- and its gradient row is zero
+  const bool ok = y64 >= 0 && y64 < L;
+  const int yn = ok ? static_cast<int>(y64) : -1;
+  if (t == 0) lrow[n] = ok ? __logf(se) + mx - z[yn] : __int_as_float(0x7fc00000);
   const float rse = 1.f / se;
   for (int l = t; l < Lp; l += 256) {  // dl rows padded to Lp (16-B rows for the backward's loads)
-    const float g = l < L ? (__expf(z[l] - mx) * rse - (l == yn ? 1.f : 0.f)) * inv_n : 0.f;
+    const float g = (l < L && ok) ? (__expf(z[l] - mx) * rse - (l == yn ? 1.f : 0.f)) * inv_n : 0.f;
     const bf16_t gb = f32_to_bf16(g);
     dl[static_cast<int64_t>(n) * Lp + l] = gb;
     if (l < L) dlT[static_cast<int64_t>(l) * Nb + n] = gb;

@@ -159,7 +159,7 @@ class Manager:
             self.allocator = GPUAllocator(inv)
             self.scheduler = NodeScheduler(self.store, self.allocator, starvation_s=self.opts.starvation_s,
                                            metrics=self.metrics)
-            self.kubelet = Kubelet(self.store, os.path.join(self.opts.home, "node"))
+            self.kubelet = Kubelet(self.store, os.path.join(self.opts.home, "node"), gpus=inv.count)
             self.scheduler.holder = self.kubelet.holds
             self.kubelet.on_worker_done = self.scheduler.wake
         # persistence (controllers/persist)

@@ -182,27 +182,34 @@ class DeviceDedup:
 
     def __init__(self, device):
         self.device = torch.device(device)
-        self._ws = {}
+        self._ws = None   # ONE workspace, sized for the largest n seen (one per n leaked)
+        self._ws_n = 0
         self._ar = {}
 
     def _buffers(self, n: int):
-        ws = self._ws.get(n)
-        if ws is None:
+        """The workspace for n ids: views of the one held for the largest n so far
+        (a bigger hash table serves a smaller n; it is left clean by every call)."""
+        if self._ws is None or n > self._ws_n:
             ext = _ext.load()
             T = ext.dedup_table_slots(n)
             i32 = dict(dtype=torch.int32, device=self.device)
             i64 = dict(dtype=torch.int64, device=self.device)
-            ws = dict(keys=torch.full((T,), -1, **i64), slot_of=torch.empty(n, **i32),
-                      slot_uid=torch.empty(T, **i32), bsum=torch.empty(T // 1024 + (n + 1) // 1024 + 2, **i32),
-                      sizes=torch.empty(n + 1, **i32), cursor=torch.empty(n + 1, **i32))
-            self._ws[n] = ws
-        return ws
+            self._ws = dict(keys=torch.full((T,), -1, **i64), slot_of=torch.empty(n, **i32),
+                            slot_uid=torch.empty(T, **i32), bsum=torch.empty(T // 1024 + (n + 1) // 1024 + 2, **i32),
+                            sizes=torch.empty(n + 1, **i32), cursor=torch.empty(n + 1, **i32))
+            self._ws_n = n
+        ws = self._ws
+        if n == self._ws_n:
+            return ws
+        return dict(keys=ws["keys"], slot_uid=ws["slot_uid"], bsum=ws["bsum"], slot_of=ws["slot_of"][:n],
+                    sizes=ws["sizes"][: n + 1], cursor=ws["cursor"][: n + 1])
 
     def arange(self, n: int):
         """(order, seg) of n distinct segments of one row each (a push of the
         pull's already-unique ids)."""
         a = self._ar.get(n)
         if a is None:
+            self._ar.clear()  # one size at a time (the batch's id count)
             a = self._ar[n] = (torch.arange(n, device=self.device), torch.arange(n + 1, device=self.device))
         return a
 

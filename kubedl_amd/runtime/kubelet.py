@@ -393,6 +393,17 @@ class PodWorker(threading.Thread):
         finally:
             self.k._worker_done(self)
 
+    def _wait_node_warm(self, timeout: float = 60.0) -> None:
+        """A pod placed on the node warm-up's GPU starts after the warm-up's
+        throw-away communicator is gone (it would share the device with it)."""
+        z, g = self.k.zygote, self.k.warm_gpu
+        if z is None or g is None or str(g) not in self.gpus or z.prefetched.is_set():
+            return
+        t_end = time.monotonic() + timeout
+        while not z.prefetched.is_set() and time.monotonic() < t_end:
+            if self.deleted.wait(self.k.poll_interval * 5):
+                return
+
     def _wait_peers_gone(self) -> None:
         """Gang teardown barrier: wait (bounded) until no other pod of this job
         is still terminating."""
@@ -403,6 +414,7 @@ class PodWorker(threading.Thread):
 
     def _run(self) -> None:
         self._wait_peers_gone()
+        self._wait_node_warm()
         if self.deleted.is_set():
             return
         os.makedirs(os.path.join(self.sandbox, "logs"), exist_ok=True)
@@ -622,7 +634,12 @@ class ServiceResolver:
 class Kubelet:
     def __init__(self, store: Store, root: str, node_name: str = "localhost",
                  poll_interval: float = 0.01, default_grace: float = 5.0,
-                 backoff_base: float = 1.0, backoff_max: float = 30.0, zygote: Optional[bool] = None):
+                 backoff_base: float = 1.0, backoff_max: float = 30.0, zygote: Optional[bool] = None,
+                 gpus: Optional[int] = None):
+        """``gpus``: the node's GPU inventory size (None: unknown, warm-up on GPU
+        0); the node warm-up runs on its LAST GPU -- the allocator hands GPUs
+        out from 0 -- and a pod bound to that GPU waits for the warm-up to end
+        before its containers start (``warm_gpu``)."""
         self.store = store
         self.root = root
         self.node = node_name
@@ -640,7 +657,9 @@ class Kubelet:
         self._cancel = None
         if zygote is None:
             zygote = os.environ.get("KDL_ZYGOTE", "1") != "0"
-        self.zygote = zygote_mod.ZygoteClient(root, self.native) if (zygote and self.native is not None) else None
+        self.warm_gpu = (gpus - 1 if gpus > 0 else None) if gpus is not None else 0
+        self.zygote = zygote_mod.ZygoteClient(root, self.native, warm_gpu=self.warm_gpu) \
+            if (zygote and self.native is not None) else None
 
     def backoff(self, n: int) -> float:
         return min(self.backoff_base * (2 ** max(0, n - 1)), self.backoff_max)

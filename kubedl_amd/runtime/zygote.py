@@ -211,26 +211,48 @@ def prefetch_files(paths: List[str], chunk: int = 8 << 20) -> int:
     return n
 
 
-def warm_node(env: dict, timeout: float = 180.0) -> dict:
+def warm_node(env: dict, timeout: float = 180.0, gpu: Optional[int] = None, procs: Optional[list] = None) -> dict:
     """Run runtime/node_warm.py in a child process (one world-1 RCCL
-    communicator on the first visible GPU) and return its JSON result."""
+    communicator on GPU ``gpu`` of the node's inventory) and return its JSON
+    result.  ``procs``: the live child is appended while it runs (the kubelet
+    kills it when it stops)."""
     import subprocess
     t0 = time.time()
+    env = dict(env or os.environ)
+    if gpu is not None:
+        env["HIP_VISIBLE_DEVICES"] = str(gpu)  # the warm-up's one GPU, from the inventory
     try:
-        p = subprocess.run([sys.executable, "-m", "kubedl_amd.runtime.node_warm"], env=env or None,
-                           capture_output=True, text=True, timeout=timeout)
-        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-        res = json.loads(lines[-1]) if lines else {"warm": False, "error": (p.stderr or "")[-300:]}
-    except (OSError, subprocess.TimeoutExpired, ValueError) as e:
+        p = subprocess.Popen([sys.executable, "-m", "kubedl_amd.runtime.node_warm"], env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+        if procs is not None:
+            procs.append(p)
+        try:
+            out, err = p.communicate(timeout=timeout)
+        finally:
+            if procs is not None and p in procs:
+                procs.remove(p)
+        lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+        res = json.loads(lines[-1]) if lines else {"warm": False, "error": (err or "")[-300:]}
+    except subprocess.TimeoutExpired as e:
+        p.kill()
+        p.wait()
+        res = {"warm": False, "error": f"TimeoutExpired: {e}"}
+    except (OSError, ValueError) as e:
         res = {"warm": False, "error": f"{type(e).__name__}: {e}"}
     res["wall_s"] = round(time.time() - t0, 3)
+    if gpu is not None:
+        res["gpu"] = gpu
     return res
 
 
 class ZygoteClient:
     """Kubelet side: start the zygote lazily and ask it for rank processes."""
 
-    def __init__(self, root: str, native):
+    def __init__(self, root: str, native, warm_gpu: Optional[int] = None):
+        """``warm_gpu``: the inventory GPU the node warm-up may use (None: no
+        warm-up -- a node without GPUs in its inventory)."""
+        self.warm_gpu = warm_gpu
+        self._warm_procs: list = []
         self.sock = os.path.join(root, "zygote.sock")
         self.log = os.path.join(root, "zygote.log")
         self.native = native
@@ -261,8 +283,9 @@ class ZygoteClient:
         try:
             prefetch_files(device_library_paths())
             self.prefetch_s = time.time() - t0
-            if os.environ.get("KDL_NODE_WARM", "1") != "0" and os.path.exists("/dev/kfd"):
-                self.warm = warm_node(self._env)
+            if (os.environ.get("KDL_NODE_WARM", "1") != "0" and os.path.exists("/dev/kfd")
+                    and self.warm_gpu is not None):
+                self.warm = warm_node(self._env, gpu=self.warm_gpu, procs=self._warm_procs)
         finally:
             if self.prefetch_s is None:
                 self.prefetch_s = time.time() - t0
@@ -305,6 +328,12 @@ class ZygoteClient:
         return int(r["pid"]) if "pid" in r else None
 
     def stop(self) -> None:
+        for p in list(self._warm_procs):  # a warm-up still running: it must not outlive the node runtime
+            try:
+                p.kill()
+                p.wait(timeout=5)
+            except Exception:
+                pass
         if self.pid is not None:
             try:
                 self.native.kill_group(self.pid, 9)

@@ -14,13 +14,16 @@ def _ext():
     return _ext.load()
 
 
-def _run(n, c, L, hw, seed):
+def _run(n, c, L, hw, seed, bad_label=None):
     ext = _ext()
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = torch.randn(n, hw, hw, c, device="cuda", generator=g).relu().bfloat16().permute(0, 3, 1, 2)
     w = (torch.randn(L, c, device="cuda", generator=g) * 0.05).bfloat16()
     b = (torch.randn(L, device="cuda", generator=g) * 0.1).bfloat16()
     y = torch.randint(0, L, (n,), device="cuda", generator=g)
+    if bad_label is not None:
+        y[1] = bad_label
+        return _bad(ext, n, c, L, x, w, b, y)
     s1, s2 = ext.head_splits(n, c, L)
     bf = dict(dtype=torch.bfloat16, device="cuda")
     feat, dl, dlT = torch.empty(n, c, **bf), torch.empty(n, ext.head_lpad(L), **bf), torch.empty(L, n, **bf)
@@ -60,3 +63,27 @@ def test_head_deterministic():
     a, b = _run(256, 2048, 1000, 7, 3), _run(256, 2048, 1000, 7, 3)
     for k in ("loss", "dfeat", "dw", "db"):
         assert torch.equal(a[k][0], b[k][0]), k
+
+
+def _bad(ext, n, c, L, x, w, b, y):
+    s1, s2 = ext.head_splits(n, c, L)
+    bf = dict(dtype=torch.bfloat16, device="cuda")
+    feat, dl, dlT = torch.empty(n, c, **bf), torch.empty(n, ext.head_lpad(L), **bf), torch.empty(L, n, **bf)
+    part1, part2 = torch.empty(s1 * n * L, device="cuda"), torch.empty(s2 * n * c, device="cuda")
+    lrow, loss = torch.empty(n, device="cuda"), torch.empty(1, device="cuda")
+    dfeat, dw, db = torch.empty(n, c, **bf), torch.empty(L, c, **bf), torch.empty(L, **bf)
+    ext.head_forward(x, w, b, y, feat, part1, lrow, dl, dlT)
+    ext.head_backward(feat, w, dl, dlT, part2, dfeat, dw, db, lrow, loss)
+    torch.cuda.synchronize()
+    return lrow, loss, dl
+
+
+@pytest.mark.parametrize("bad", [-100, 10, 1 << 40])
+def test_head_out_of_range_label_is_nan_not_a_wild_read(bad):
+    """a label outside [0, L) (the ignore_index -100, or L itself)
+    never indexes past the logits: that row's loss is NaN (the step's loss turns
+    NaN, loudly) and its gradient row is zero; the other rows are untouched."""
+    lrow, loss, dl = _run(8, 64, 10, 2, 5, bad_label=bad)
+    assert torch.isnan(lrow[1]) and torch.isnan(loss[0])
+    assert not torch.isnan(lrow[torch.arange(8, device="cuda") != 1]).any()
+    assert not dl[1].float().any()

@@ -45,3 +45,14 @@ def test_node_warm_child_reports_json():
     res = warm_node(dict(os.environ), timeout=120)
     assert "warm_s" in res and "wall_s" in res, res
     assert res["warm"] is False and res.get("reason") == "no GPU", res
+
+
+def test_node_warm_gpu_comes_from_the_inventory(tmp_path):
+    """the node warm-up runs on a GPU of the node's inventory (its
+    last one: the allocator hands GPUs out from 0), not on whatever is physical
+    GPU 0, and a node without GPUs has no warm-up at all."""
+    from kubedl_amd.runtime.kubelet import Kubelet
+    from kubedl_amd.store import Store
+    assert Kubelet(Store(), str(tmp_path / "a"), zygote=False, gpus=0).warm_gpu is None
+    assert Kubelet(Store(), str(tmp_path / "b"), zygote=False, gpus=8).warm_gpu == 7
+    assert Kubelet(Store(), str(tmp_path / "c"), zygote=False, gpus=1).warm_gpu == 0
