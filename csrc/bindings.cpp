@@ -1363,6 +1363,34 @@ void conv1x1_wgrad(const at::Tensor& G, const at::Tensor& A, const c10::optional
             "conv1x1_wgrad");
 }
 
+// Gram fold (csrc/conv1x1.hip): Q | s of relu(B(X)) into ws, then the folded bf16 dW
+int64_t conv1x1_gram_floats(int64_t M, int64_t K) {
+  return static_cast<int64_t>(kdl::conv1x1_gram_splits(static_cast<int>(M), static_cast<int>(K))) * (K * K + K);
+}
+
+void conv1x1_gram(const at::Tensor& X, const at::Tensor& pro, at::Tensor ws, int64_t M, int64_t K) {
+  need_bf16(X, M * K, "conv1x1_gram X");
+  need_opt_f32(pro, 2 * K, "conv1x1_gram pro");
+  need_opt_f32(ws, conv1x1_gram_floats(M, K), "conv1x1_gram ws");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check_hip(kdl::conv1x1_gram(X.data_ptr(), pro.data_ptr<float>(), ws.data_ptr<float>(), static_cast<int>(M),
+                              static_cast<int>(K), cur_stream()),
+            "conv1x1_gram");
+}
+
+void gram_fold(const at::Tensor& Gm, const at::Tensor& QS, const at::Tensor& W, const at::Tensor& bcoef, at::Tensor out,
+               int64_t N, int64_t K) {
+  need_opt_f32(Gm, N * K, "gram_fold G");
+  need_opt_f32(QS, K * K + K, "gram_fold Q|s");
+  need_opt_f32(bcoef, 3 * N, "gram_fold bcoef");
+  need_bf16(W, N * K, "gram_fold W");
+  need_bf16(out, N * K, "gram_fold out");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  check_hip(kdl::gram_fold(Gm.data_ptr<float>(), QS.data_ptr<float>(), W.data_ptr(), bcoef.data_ptr<float>(),
+                           static_cast<int>(N), static_cast<int>(K), out.data_ptr(), cur_stream()),
+            "gram_fold");
+}
+
 // fixed-order sum of nsplit fp32 [nk] slabs into the first (fp32, in place)
 void slab_reduce_f32(at::Tensor slabs, int64_t nk, int64_t nsplit) {
   TORCH_CHECK(nk % 4 == 0 && nsplit >= 1, "slab_reduce_f32: nk % 4 == 0");
@@ -1638,6 +1666,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("dedup_csr", &dedup_csr, "sync-free id de-duplication (uniq/inv/count on the device) + optional CSR of the inverse");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");
   m.def("set_stem_drop", &kdl::set_stem_drop, "timing-only: skip the stem kernel's MFMAs (1), epilogue (2), input (4)");
+  m.def("conv1x1_gram_floats", &conv1x1_gram_floats, "workspace floats of conv1x1_gram(M, K)");
+  m.def("conv1x1_gram", &conv1x1_gram, "Q = a^T a | s = 1^T a of a = relu(X*scale+shift) (fp32, into ws[:K*K+K])");
+  m.def("gram_fold", &gram_fold, "dW = diag(k) G + diag(c1) W Q + c0 s^T -> bf16 (BN-backward weight gradient, dc never stored)");
   m.def("slab_reduce_f32", &slab_reduce_f32, "fixed-order fp32 sum of slabs into the first");
   m.def("bn_bwd_pro_arm", &bn_bwd_pro_arm, "fuse this BN's backward apply (input x, workspace ws) into the next conv1x1_gemm's A (or conv1x1_wgrad's G) staging; optional write-through tensor");
   m.def("bn_fin_arm", &bn_fin_arm, "fold the BN finalize of this workspace (C channels, M elements) into the next conv GEMM launch");

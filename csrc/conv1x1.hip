@@ -402,11 +402,17 @@ __device__ __forceinline__ void transpose8x8(const uint4 (&in)[8], uint4 (&out)[
   }
 }
 
-template <int TN_, int TK_, bool PRO, int GATHER>
+// GPRO: G gets the same BN + ReLU prologue as A (coefficients [scale(N) |
+// shift(N)] of pro_coef: the Gram matrix relu(B(X))^T relu(B(X)) when G = A = X,
+// N = K).  COLSUM: the blocks of output-tile row 0 also write the column sums of
+// the staged A' (as the bf16 values the MFMAs see) behind each split's [N][K]
+// slab, i.e. slabs of N * K + K floats.
+template <int TN_, int TK_, bool PRO, int GATHER, bool GPRO = false, bool COLSUM = false>
 __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
     const bf16_t* __restrict__ G, const bf16_t* __restrict__ A, const float* __restrict__ pro_coef,
     float* __restrict__ dw32, int M, int N, int K, int Hout, int Wout, int Hin, int Win, int stride,
     int rows_per_split, int tiles_k, int cin) {
+  static_assert(!GPRO || (PRO && GATHER == G_DENSE), "the G prologue serves the dense Gram matrix");
   // [2 buffers][G^T tile TN_ x LDW | A^T tile TK_ x LDW]
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (TN_ + TK_) * LDW];
   constexpr int kBuf = (TN_ + TK_) * LDW;
@@ -448,6 +454,14 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) { psc[j] = pro_coef[col0 + j]; psf[j] = pro_coef[kcoef + col0 + j]; }
   }
+  if (GPRO && !isA && stager) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { psc[j] = pro_coef[col0 + j]; psf[j] = pro_coef[N + col0 + j]; }
+  }
+  float csum[8];  // COLSUM: this A-stager's column sums over its staged rows
+#pragma unroll
+  for (int j = 0; j < 8; ++j) csum[j] = 0.f;
+  (void)csum;
   uint4 rr[8];
   uint32_t rok = 0xffu;  // 3x3: rows of the staged set whose tap lies inside the image
   (void)tr3; (void)tq3;
@@ -482,7 +496,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const bool ok = m0 + mg * 8 + r < mend && ((rok >> r) & 1u);  // tail rows / padding taps stage as zero
-      if (PRO && isA) {
+      if ((PRO && isA) || (GPRO && !isA)) {
         float f[8];
         unpack8(rr[r], f);
 #pragma unroll
@@ -493,6 +507,12 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
         rr[r] = pack8(f);
       }
       if (!ok) rr[r] = make_uint4(0, 0, 0, 0);
+      if (COLSUM && isA) {
+        float f[8];
+        unpack8(rr[r], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) csum[j] += f[j];
+      }
     }
     uint4 tr[8];
     transpose8x8(rr, tr);
@@ -546,7 +566,22 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
   // fp32 atomics into one [N][K] buffer were capped at ~1.3 TB/s of added bytes
   // (MI355X_MICROARCH.md "Global float atomics") -- 16 splits x 4 MiB at the
   // 7x7 stage was half the kernel's time -- and the result is deterministic.
-  float* slab = dw32 + static_cast<int64_t>(split) * N * K;
+  float* slab = dw32 + static_cast<int64_t>(split) * (static_cast<int64_t>(N) * K + (COLSUM ? K : 0));
+  if constexpr (COLSUM) {
+    // fold the 8 row groups of each column chunk (the loop's last barrier freed lds)
+    float* cs = reinterpret_cast<float*>(lds);  // [8 (mg)][TK_]
+    if (stager && isA) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[mg * TK_ + cc + j] = csum[j];
+    }
+    __syncthreads();
+    if (tn == 0 && t < TK_) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) v += cs[g * TK_ + t];
+      slab[static_cast<int64_t>(N) * K + k0 + t] = v;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -947,7 +982,247 @@ hipError_t wgrad_reduce(float* dw32, int64_t nk, int nsplit, float scale, bf16_t
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ Gram fold of a BN-backward weight gradient
+// The weight gradient of a 1x1 conv whose output c = W a feeds a BN with
+// backward coefficients (k, c1, c0) -- dc = k g + c1 c + c0 -- is
+//   dW = dc^T a = diag(k) (g^T a) + diag(c1) W (a^T a) + c0 (1^T a)
+// so dc never has to be materialised: G = g^T a on the weight-gradient kernel,
+// Q = a^T a and s = 1^T a (a = relu(B(X)), the conv's prologued input) on the
+// Gram kernel below, and this fold, all in fp32 (models/resnet_engine.py
+// bn_bwd_fuse 3; the BN-backward apply's write-through of dc -- a 4C-channel
+// tensor -- disappears from the data gradient).
+// W Q is a small fp32 GEMM (N x K x K): 64 x 64 output tiles, 4 x 4 per thread,
+// j in chunks of 16 staged through LDS (a per-output K-long dependent-load loop
+// took 40 us at N = 256, K = 64).  N, K multiples of 64.
+constexpr int kFoldJ = 16;
+__global__ __launch_bounds__(256) void gram_fold_kernel(const float* __restrict__ Gm, const float* __restrict__ QS,
+                                                        const bf16_t* __restrict__ W, const float* __restrict__ bcoef,
+                                                        int N, int K, bf16_t* __restrict__ out) {
+  __shared__ float Ws[kFoldJ][64 + 4];  // [j][n]
+  __shared__ __attribute__((aligned(16))) float Qs[kFoldJ][64];  // [j][k]
+  const int n0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
+  const int t = threadIdx.x, tn = (t >> 4) * 4, tk = (t & 15) * 4;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[i][q] = 0.f;
+  const int wr = t >> 2, wc = (t & 3) * 4;   // W: row n0 + wr, j0 + wc .. +3
+  const int qr = t >> 4, qc = (t & 15) * 4;  // Q: row j0 + qr, k0 + qc .. +3
+  for (int j0 = 0; j0 < K; j0 += kFoldJ) {
+    const bf16_t* w = W + static_cast<int64_t>(n0 + wr) * K + j0 + wc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Ws[wc + q][wr] = bf16_to_f32(w[q]);
+    *reinterpret_cast<float4*>(&Qs[qr][qc]) =
+        *reinterpret_cast<const float4*>(QS + static_cast<int64_t>(j0 + qr) * K + k0 + qc);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kFoldJ; ++j) {
+      const float4 b = *reinterpret_cast<const float4*>(&Qs[j][tk]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float a = Ws[j][tn + i];
+        acc[i][0] = fmaf(a, b.x, acc[i][0]);
+        acc[i][1] = fmaf(a, b.y, acc[i][1]);
+        acc[i][2] = fmaf(a, b.z, acc[i][2]);
+        acc[i][3] = fmaf(a, b.w, acc[i][3]);
+      }
+    }
+    __syncthreads();
+  }
+  const float* colsum = QS + static_cast<int64_t>(K) * K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + tn + i;
+    const float kc = bcoef[n], c1 = bcoef[N + n], c0 = bcoef[2 * N + n];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 + tk + q;
+      const int64_t idx = static_cast<int64_t>(n) * K + k;
+      out[idx] = f32_to_bf16(kc * Gm[idx] + c1 * acc[i][q] + c0 * colsum[k]);
+    }
+  }
+}
+
+// Q = a^T a and s = 1^T a of a dense [M][T] operand (T = K = 64 or 128: one
+// output tile, on the diagonal): each staged row feeds BOTH MFMA operands, and
+// all 256 threads stage (one 8-row x 8-channel unit each per R-row step, R = 256
+// x 64 / T) -- the generic weight-gradient kernel staged the same rows twice
+// from half its threads and sat latency-bound at ~0.5 TB/s.  A block's rows are
+// its own contiguous range (nothing to share through an XCD's L2).
+template <int T>
+__global__ __launch_bounds__(kThreads, 2) void gram_kernel(const bf16_t* __restrict__ X,
+                                                           const float* __restrict__ pro, float* __restrict__ ws,
+                                                           int M, int rows_per_split) {
+  constexpr int R = kThreads * 64 / T;  // rows per step
+  constexpr int LDR = R + 8;
+  constexpr int kBuf = T * LDR;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kBuf];
+  constexpr int WT = T / 2, F = WT / 32;  // 2 x 2 waves
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int split = blockIdx.x;
+  const int mbeg = split * rows_per_split;
+  const int mend = min(M, mbeg + rows_per_split);
+  constexpr int cpr = T / 8;
+  const int mg = t / cpr, cc = (t % cpr) * 8;
+  float psc[8], psf[8], csum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    psc[j] = pro[cc + j];
+    psf[j] = pro[T + cc + j];
+    csum[j] = 0.f;
+  }
+  uint4 rr[8];
+  auto gload = [&](int m0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int m1 = m0 + mg * 8 + r;
+      rr[r] = ld16(X + static_cast<int64_t>(m1 < mend ? m1 : mbeg) * T + cc);
+    }
+  };
+  auto swrite = [&](int buf, int m0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float f[8];
+      unpack8(rr[r], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float o = fmaf(f[j], psc[j], psf[j]);
+        f[j] = o > 0.f ? o : 0.f;
+      }
+      rr[r] = m0 + mg * 8 + r < mend ? pack8(f) : make_uint4(0, 0, 0, 0);
+      unpack8(rr[r], f);  // the bf16 values the MFMAs see
+#pragma unroll
+      for (int j = 0; j < 8; ++j) csum[j] += f[j];
+    }
+    uint4 tr[8];
+    transpose8x8(rr, tr);
+    bf16_t* S = lds + buf * kBuf;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) *reinterpret_cast<uint4*>(&S[(cc + c) * LDR + mg * 8]) = tr[c];
+  };
+  const int wn0 = (wave >> 1) * WT, wk0 = (wave & 1) * WT;
+  const int fr = lane & 31, fh = lane >> 5;
+  f32x16_t acc[F][F];
+#pragma unroll
+  for (int i = 0; i < F; ++i)
+#pragma unroll
+    for (int j = 0; j < F; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  int cur = 0;
+  if (mbeg < mend) {
+    gload(mbeg);
+    swrite(0, mbeg);
+  }
+  __syncthreads();
+  for (int m0 = mbeg; m0 < mend; m0 += R) {
+    const bool more = m0 + R < mend;
+    if (more) gload(m0 + R);
+    const bf16_t* S = lds + cur * kBuf;
+#pragma unroll
+    for (int s = 0; s < R / 16; ++s) {
+      bf16x8_t gf[F], af[F];
+#pragma unroll
+      for (int i = 0; i < F; ++i) {
+        gf[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&S[(wn0 + i * 32 + fr) * LDR + s * 16 + fh * 8]));
+        af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&S[(wk0 + i * 32 + fr) * LDR + s * 16 + fh * 8]));
+      }
+#pragma unroll
+      for (int i = 0; i < F; ++i)
+#pragma unroll
+        for (int j = 0; j < F; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[i], af[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) swrite(cur ^ 1, m0 + R);
+    __syncthreads();
+    cur ^= 1;
+  }
+  float* slab = ws + static_cast<int64_t>(split) * (T * T + T);
+  // column sums: fold the R/8 row groups through LDS (the loop's last barrier freed it)
+  float* cs = reinterpret_cast<float*>(lds);  // [R / 8][T]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[mg * T + cc + j] = csum[j];
+  __syncthreads();
+  if (t < T) {
+    float v = 0.f;
+    for (int g = 0; g < R / 8; ++g) v += cs[g * T + t];
+    slab[T * T + t] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < F; ++i)
+#pragma unroll
+    for (int j = 0; j < F; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = wn0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const int k = wk0 + j * 32 + fr;
+        __builtin_nontemporal_store(acc[i][j][r], slab + n * T + k);
+      }
+}
+
+int gram_tile(int K) { return K % 128 == 0 ? 128 : 64; }
+bool gram_dedicated(int K) { return K == 64 || K == 128; }
+
 }  // namespace
+
+int conv1x1_gram_splits(int M, int K) {
+  if (gram_dedicated(K)) {
+    // ~2 blocks per CU at K = 64; half that at 128, whose 66 KB slabs would
+    // otherwise rival the operand's own bytes (KDL_TUNE gram_blocks)
+    static const int target = tune_int("gram_blocks", 512);
+    const int R = kThreads * 64 / K;
+    int splits = K == 64 ? target : target / 2;
+    const int max_splits = (M + R - 1) / R;
+    if (splits > max_splits) splits = max_splits;
+    return splits < 1 ? 1 : splits;
+  }
+  const int t = gram_tile(K), tiles = (K / t) * (K / t);
+  int splits = tune_int("wgrad_blocks", 384) / 2 / tiles;  // half the weight-gradient block target
+  const int max_splits = (M + WMK - 1) / WMK;
+  if (splits > max_splits) splits = max_splits;
+  return splits < 1 ? 1 : splits;
+}
+
+hipError_t conv1x1_gram(const void* X, const float* pro, float* ws, int M, int K, hipStream_t s) {
+  if (K % 64 || M <= 0 || K > 512 || !pro) return hipErrorInvalidValue;
+  const bf16_t* x = static_cast<const bf16_t*>(X);
+  if (gram_dedicated(K)) {
+    const int R = kThreads * 64 / K;
+    const int splits = conv1x1_gram_splits(M, K);
+    int rps = (M + splits - 1) / splits;
+    rps = (rps + R - 1) / R * R;
+    const int nsplit = (M + rps - 1) / rps;
+    if (K == 64)
+      hipLaunchKernelGGL(gram_kernel<64>, dim3(nsplit), dim3(kThreads), 0, s, x, pro, ws, M, rps);
+    else
+      hipLaunchKernelGGL(gram_kernel<128>, dim3(nsplit), dim3(kThreads), 0, s, x, pro, ws, M, rps);
+    RETURN_IF_HIP_ERR(hipGetLastError());
+    return wgrad_reduce(ws, static_cast<int64_t>(K) * K + K, nsplit, 1.f, nullptr, s);
+  }
+  const int t = gram_tile(K), tiles_k = K / t;
+  const int splits = conv1x1_gram_splits(M, K);
+  int rps = (M + splits - 1) / splits;
+  rps = (rps + WMK - 1) / WMK * WMK;
+  const int nsplit = (M + rps - 1) / rps;
+  dim3 grid(nsplit * tiles_k * tiles_k);
+  if (t == 128)
+    hipLaunchKernelGGL((wgrad1x1_kernel<128, 128, true, G_DENSE, true, true>), grid, dim3(kThreads), 0, s, x, x, pro,
+                       ws, M, K, K, 0, 0, 0, 0, 1, rps, tiles_k, K);
+  else
+    hipLaunchKernelGGL((wgrad1x1_kernel<64, 64, true, G_DENSE, true, true>), grid, dim3(kThreads), 0, s, x, x, pro,
+                       ws, M, K, K, 0, 0, 0, 0, 1, rps, tiles_k, K);
+  RETURN_IF_HIP_ERR(hipGetLastError());
+  return wgrad_reduce(ws, static_cast<int64_t>(K) * K + K, nsplit, 1.f, nullptr, s);  // fp32, in slab 0
+}
+
+hipError_t gram_fold(const float* Gm, const float* QS, const void* W, const float* bcoef, int N, int K, void* out,
+                     hipStream_t s) {
+  if (N <= 0 || K <= 0 || N % 64 || K % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gram_fold_kernel, dim3(K / 64, N / 64), dim3(256), 0, s, Gm, QS,
+                     static_cast<const bf16_t*>(W), bcoef, N, K, static_cast<bf16_t*>(out));
+  return hipGetLastError();
+}
 
 hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s,
                              int layout) {

@@ -333,6 +333,15 @@ hipError_t head_backward(const void* feat, const void* w, const void* dl, const 
                          hipStream_t s);
 // fixed-order sum of nsplit fp32 [nk] slabs into bf16 (scaled), csrc/conv1x1.hip;
 // layout 1: the stem's [64][224] K order written out as [64][3][7][7]
+// Gram fold of a BN-backward weight gradient (csrc/conv1x1.hip): Q = a^T a and
+// s = 1^T a of a = relu(X * scale + shift) (pro = [scale | shift], X [M, K] bf16)
+// into ws[0 : K * K + K] (fp32; ws holds conv1x1_gram_splits(M, K) * (K * K + K)
+// floats), and dW = diag(k) Gm + diag(c1) W Q + c0 s^T -> bf16 out [N, K]
+// (bcoef = [k | c1 | c0], Gm = g^T a fp32 [N, K], W the conv weight [N, K] bf16)
+int conv1x1_gram_splits(int M, int K);
+hipError_t conv1x1_gram(const void* X, const float* pro, float* ws, int M, int K, hipStream_t s);
+hipError_t gram_fold(const float* Gm, const float* QS, const void* W, const float* bcoef, int N, int K, void* out,
+                     hipStream_t s);
 hipError_t wgrad_slab_reduce(float* dw32, int64_t nk, int nsplit, float scale, void* dW, hipStream_t s,
                              int layout = 0);
 void set_stem_drop(int bits);  // timing-only: skip the stem's MFMAs (1), epilogue (2), input staging (4)

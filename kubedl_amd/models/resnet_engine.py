@@ -403,6 +403,24 @@ class HipKernels:
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
                                M, cout, cin, ho, wo, h, w, stride)
 
+    def wgrad_gram(self, g, x2, st2: BNState, st3: BNState, w3, dW):
+        """conv3's weight gradient with BN3's backward apply folded in (csrc/conv1x1.hip
+        Gram fold): dW3 = diag(k) g^T a2 + diag(c1) W3 (a2^T a2) + c0 (1^T a2), a2 =
+        relu(B2(c2)) -- dc3 is never materialised.  G on the weight-gradient kernel
+        (fp32, left in its slab workspace), Q | s on the Gram kernel, then the fold."""
+        n, cout, ho, wo = g.shape
+        _, cin, h, w = x2.shape
+        M = n * ho * wo
+        key = (M, cout, cin)
+        need = self.ext.conv1x1_wgrad_splits(M, cout, cin) * cout * cin
+        dw32 = self._dw32.get(key)
+        if dw32 is None or dw32.numel() < need:
+            dw32 = self._dw32[key] = torch.empty(need, device=g.device)
+        self.ext.conv1x1_wgrad(g, x2, self.fcoef(st2), dw32, None, 1.0, M, cout, cin, ho, wo, h, w, 1)
+        qs = self._ws32(("gram", M, cin), self.ext.conv1x1_gram_floats(M, cin))
+        self.ext.conv1x1_gram(x2, self.fcoef(st2), qs, M, cin)
+        self.ext.gram_fold(dw32, qs, w3.view(cout, cin), self.bcoef(st3), dW.view(cout, cin), cout, cin)
+
     def wgrad3x3(self, g, x, stride, dW, pro: BNState | None = None):
         """3x3 pad-1 weight gradient straight into ``dW`` (channels_last = OHWI):
         the 56x56 stage's input halo kernel (csrc/halo3x3.hip) or the LDS-DMA
@@ -704,6 +722,15 @@ class TorchKernels:
         a = _rows(a[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last))
         dW.copy_((_rows(g.float()).t() @ a).view_as(dW))
 
+    def wgrad_gram(self, g, x2, st2, st3, w3, dW):
+        """The Gram fold's algebra in fp32 (HipKernels.wgrad_gram)."""
+        a = _rows(self._pro(x2, st2).contiguous(memory_format=torch.channels_last))
+        G = _rows(g.float().contiguous(memory_format=torch.channels_last)).t() @ a
+        Q = a.t() @ a
+        k, c1, c0 = st3.bcoef
+        W = w3.float().view(w3.shape[0], -1)
+        dW.copy_((k[:, None] * G + c1[:, None] * (W @ Q) + c0[:, None] * a.sum(0)[None, :]).view_as(dW))
+
     def wgrad3x3(self, g, x, stride, dW, pro=None):
         a = self._pro(x, pro) if pro is not None else x.float()
         dW.copy_(torch.nn.grad.conv2d_weight(a, tuple(dW.shape), g.float(), stride=stride, padding=1))
@@ -752,8 +779,10 @@ class EngineOptions:
     # -- and is not an engine option)
     halo_pro: int = 1
     # BN-backward apply fused into 1x1 data-gradient GEMMs (1 write-through, 2 both
-    # operands, 0 own pass) up to this many channels; bn1 too (measured slower)
-    bn_bwd_fuse: int = 1
+    # operands, 3 = bn3: dgrad prologue without write-through + the Gram-fold weight
+    # gradient, dc3 never stored; 0 own pass) up to this many channels; bn1 too
+    # (measured slower)
+    bn_bwd_fuse: int = 3
     bn_bwd_fuse_kmax: int = 512
     bn_bwd_fuse_bn1: bool = False
 
@@ -825,7 +854,12 @@ class ResNetEngine:
         # (stage 1: 390 -> 287 us, down 371 -> 258; stage 2: 192 -> 157); it loses on
         # conv1's dgrad (N = 4C output tiles each re-transform the A tile) and at
         # K >= 1024 (the register-staged loop vs the LDS-DMA one: 88 -> 138 us); the
-        # G prologue (mode 2) loses to reading the written-through tensor (106 -> 354 us)
+        # G prologue (mode 2) loses to reading the written-through tensor (106 -> 354 us).
+        # Mode 3 (default): mode 1 for every BN except a block's bn3, whose conv3
+        # weight gradient is the Gram fold diag(k) g^T a2 + diag(c1) W3 (a2^T a2) +
+        # c0 1^T a2 (HipKernels.wgrad_gram) -- dc3, a 4C-channel tensor, is neither
+        # written by the dgrad nor read by the wgrad: 13,841 -> 13,900-13,960 img/s,
+        # main-stream busy 18.21 -> 17.80 ms/step (profiles/r05_gram_fold_ab.txt).
         # downsample branch conv of the forward on the side stream (down_side = False: in
         # line): 13,333-13,347 vs 13,252-13,279 img/s, profiles/r03b_fwd_down_side_ab.txt
         self.down_side = o.down_side
@@ -1113,10 +1147,16 @@ class ResNetEngine:
             return 0
         return self.fuse_bwd if C <= self.fuse_kmax else 0
 
-    def _bn_bwd_operand(self, g, x, st, bn1: bool = False):
+    def _bn_bwd_operand(self, g, x, st, bn1: bool = False, gram: bool = False):
         """(dgrad A, dgrad bpro, wgrad G, wgrad gbpro) for the BN-backward apply
-        dc = k g + c1 x + c0 of BN ``st`` (input ``x``) per ``_fuse_mode``."""
+        dc = k g + c1 x + c0 of BN ``st`` (input ``x``) per ``_fuse_mode``; wgrad
+        gbpro "gram": the weight gradient folds the apply in (``gram``: a block's
+        bn3, whose conv3 input is B2's prologued c2 -- HipKernels.wgrad_gram)."""
         mode = self._fuse_mode(x.shape[1], bn1)
+        if mode == 3 and gram:
+            return g, (x, st, None), g, "gram"
+        if mode == 3:
+            mode = 1
         if mode == 0:
             dc, _ = self.K.bn_bwd_apply(g, x, st)
             return dc, None, dc, None
@@ -1128,7 +1168,7 @@ class ResNetEngine:
     @staticmethod
     def _side_of(op):
         """Tensors a weight gradient on ``op`` reads (side-stream lifetime)."""
-        return (op[2],) if op[3] is None else (op[2], op[3][0])
+        return (op[2],) if op[3] is None or isinstance(op[3], str) else (op[2], op[3][0])
 
     def _bn_grads(self, st):
         return self._g(st.mod.weight), self._g(st.mod.bias)
@@ -1169,12 +1209,15 @@ class ResNetEngine:
                 dc3, dcd = K.bn_bwd_apply(g, c3, st3, cd, std_)  # one pass for both branches
                 op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
             else:
-                op3 = self._bn_bwd_operand(g, c3, st3)
+                op3 = self._bn_bwd_operand(g, c3, st3, gram=True)
                 opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
             # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
             g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
             with self._on_side(*self._side_of(op3)):
-                K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
+                if op3[3] == "gram":
+                    K.wgrad_gram(g, c2, st2, st3, blk.conv3.weight, self._g(blk.conv3.weight))
+                else:
+                    K.wgrad(op3[2], c2, 1, st2, self._g(blk.conv3.weight), gbpro=op3[3])
             self.on_ready(blk.conv3.weight)
             K.bn_bwd_finalize(st2, Mo, *self._bn_grads(st2))
             self._bn_ready(st2)

@@ -389,3 +389,88 @@ def test_knob_surface_stays_small():
     assert len(names) < 40, sorted(names)
     for gone in ("KDL_HIP_GRAPH", "KDL_GBDT_GRAPH", "KDL_STREAMS", "KDL_MAIN_PRIO", "KDL_DDP_WORLD1"):
         assert gone not in names
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("layers,width", [((1, 1, 1, 1), 8), ((2, 1, 1, 2), 16)])
+def test_engine_gram_fold_matches_autograd_fp32(layers, width, mode, monkeypatch):
+    """bn_bwd_fuse=3 (default): conv3's weight gradient as diag(k) g^T a2 +
+    diag(c1) W3 (a2^T a2) + c0 (1^T a2) -- dc3 never materialised -- is the same
+    gradient, exactly in fp32 (the algebra of HipKernels.wgrad_gram); 1: the
+    written-through dc3."""
+    import kubedl_amd.models.resnet_engine as RE
+    monkeypatch.setattr(RE, "_bfr", lambda t: t.float())
+    monkeypatch.setenv("KDL_ENGINE", f"bn_bwd_fuse={mode}")
+    torch.manual_seed(1)
+    model = ResNet(layers, num_classes=10, width=width)
+    with torch.no_grad():
+        for m in model.modules():
+            if hasattr(m, "running_mean"):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    ref = copy.deepcopy(model)
+    ref.set_bn_backend("torch")
+    x = torch.randn(4, 3, 64, 64)
+    y = torch.randint(0, 10, (4,))
+    eng = RE.ResNetEngine(model, backend="torch")
+    assert eng.fuse_bwd == mode
+    loss = eng.forward_backward(x, y)
+    rloss = _ref_step(ref, x, y)
+    torch.testing.assert_close(loss, rloss, atol=1e-5, rtol=1e-5)
+    for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-4 * (q.grad.abs().max().item() + 1e-6), rtol=1e-3,
+                                   msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [32, 256])
+def test_engine_hip_write_through_full_resnet50_matches_fp32_truth(batch, monkeypatch):
+    """bn_bwd_fuse=1 -- conv3's weight gradient from the written-through dc3
+    instead of the default Gram fold (csrc/conv1x1.hip conv1x1_gram + gram_fold)
+    -- on the benchmarked shape, against fp32 truth with the default's budget."""
+    monkeypatch.setenv("KDL_ENGINE", "bn_bwd_fuse=1")
+    model, ref, x, y = _setup((3, 4, 6, 3), 64, "cuda", 224, batch, classes=1000)
+    truth, tloss = _truth_of(ref, x, y)
+    eng = ResNetEngine(model, backend="hip")
+    assert eng.fuse_bwd == 1
+    loss = eng.forward_backward(x, y)
+    _ref_step(ref, x, y)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss, tloss, atol=2e-2, rtol=2e-2)
+    _vs_truth_strict(model, ref, truth)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K", [(802816, 64), (200704, 128), (1000, 64), (4160, 128)])
+def test_conv1x1_gram_matches_fp32(M, K):
+    """Q = a^T a and s = 1^T a of a = bf16(relu(x * scale + shift)) (the conv3
+    prologue's operand) against fp32 torch, including M tails."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    pro = torch.cat([torch.rand(K, device="cuda", generator=g) + 0.5, torch.randn(K, device="cuda", generator=g) * 0.3])
+    ws = torch.empty(ext.conv1x1_gram_floats(M, K), device="cuda")
+    ext.conv1x1_gram(x, pro, ws, M, K)
+    a = (x.float() * pro[:K] + pro[K:]).relu().bfloat16().float()
+    Q, s = a.t() @ a, a.sum(0)
+    torch.testing.assert_close(ws[: K * K].view(K, K), Q, atol=1e-3 * Q.abs().max().item(), rtol=1e-4)
+    torch.testing.assert_close(ws[K * K: K * K + K], s, atol=1e-3 * s.abs().max().item(), rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,K", [(256, 64), (512, 128), (2048, 512)])
+def test_gram_fold_matches_fp32(N, K):
+    """gram_fold: k G + c1 (W Q) + c0 s per output row, against fp32 torch."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    G = torch.randn(N, K, device="cuda", generator=g)
+    QS = torch.randn(K * K + K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    bc = torch.randn(3 * N, device="cuda", generator=g)
+    out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+    ext.gram_fold(G, QS, W, bc, out, N, K)
+    Q, s = QS[: K * K].view(K, K), QS[K * K:]
+    ref = bc[:N, None] * G + bc[N: 2 * N, None] * (W.float() @ Q) + bc[2 * N:, None] * s[None]
+    torch.testing.assert_close(out.float(), ref, atol=2e-2 * ref.abs().max().item(), rtol=1e-2)
