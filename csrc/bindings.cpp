@@ -750,6 +750,33 @@ void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at:
             "segment_adagrad");
 }
 
+// owner update of a fixed exchange (csrc/ctr.hip a2a_stamp + a2a_adagrad): no
+// de-duplication pass; slotmap int64 [nrows * W] kept by the caller (zero
+// initially), call = 1, 2, ... per update
+void a2a_owner_update(const at::Tensor& grads, const at::Tensor& local, int64_t cap, int64_t W, at::Tensor slotmap,
+                      int64_t call, at::Tensor table, at::Tensor accum, double lr, double eps, double scale) {
+  TORCH_CHECK(grads.is_cuda() && grads.scalar_type() == at::kFloat && grads.is_contiguous() && grads.dim() == 2,
+              "a2a_owner_update: fp32 grads [S, D]");
+  const int64_t S = grads.size(0), D = grads.size(1);
+  TORCH_CHECK(local.scalar_type() == at::kLong && local.is_contiguous() && local.numel() == S,
+              "a2a_owner_update: int64 local [S]");
+  TORCH_CHECK(W >= 1 && cap >= 1 && S == W * cap && S < (int64_t(1) << 31), "a2a_owner_update: S = W * cap < 2^31");
+  TORCH_CHECK(table.scalar_type() == at::kFloat && accum.scalar_type() == at::kFloat && table.is_contiguous() &&
+                  accum.is_contiguous() && table.sizes() == accum.sizes() && table.dim() == 2 && table.size(1) == D,
+              "a2a_owner_update: fp32 table/accum [nrows, D]");
+  const int64_t nrows = table.size(0);
+  TORCH_CHECK(slotmap.scalar_type() == at::kLong && slotmap.is_contiguous() && slotmap.numel() >= nrows * W,
+              "a2a_owner_update: slotmap int64 [nrows * W]");
+  TORCH_CHECK(call >= 1 && call < (int64_t(1) << 31), "a2a_owner_update: call in [1, 2^31)");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  check_hip(kdl::a2a_owner_update(grads.data_ptr<float>(), local.data_ptr<int64_t>(), static_cast<int>(S),
+                                  static_cast<int>(cap), static_cast<int>(W), static_cast<int>(D), nrows,
+                                  slotmap.data_ptr<int64_t>(), call, table.data_ptr<float>(),
+                                  accum.data_ptr<float>(), static_cast<float>(lr), static_cast<float>(eps),
+                                  static_cast<float>(scale), cur_stream()),
+            "a2a_owner_update");
+}
+
 int64_t dedup_table_slots(int64_t n) { return kdl::dedup_table_slots(static_cast<int>(n)); }
 
 // the CSR half of dedup_csr, later in the step (sizes from that dedup_csr call;
@@ -1657,6 +1684,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("col0"), py::arg("D"), py::arg("order"), py::arg("seg"), py::arg("ucount") = py::none(),
         py::arg("out_rows") = py::none(), py::arg("out") = py::none());
   m.def("a2a_route", &a2a_route, "fixed-capacity exchange: per-owner send blocks + header + rslot of unique ids");
+  m.def("a2a_owner_update", &a2a_owner_update, "owner Adagrad update of a fixed exchange without de-duplication");
   m.def("a2a_serve", &a2a_serve, "owner side of the fixed exchange: requested rows + local row ids",
         py::arg("table"), py::arg("req"), py::arg("n_own"), py::arg("rows_bf16") = false);
   m.def("embed_gather_cast", &embed_gather_cast, "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input");

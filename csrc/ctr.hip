@@ -545,6 +545,73 @@ __global__ __launch_bounds__(256) void segment_adagrad_kernel(const float* __res
   }
 }
 
+// Owner side of a fixed exchange without a de-duplication pass.  The received
+// gradient blocks are W senders x cap slots (slot s = w * cap + k, local row
+// local[s], padding < 0), and a sender routes each of its UNIQUE ids once, so a
+// row repeats only across senders.  Each slot stamps slotmap[row * W + w] =
+// (call << 32) | s -- one plain store, no atomics, nothing to clear: an entry
+// is live only while its stamp equals the current call.
+__global__ __launch_bounds__(256) void a2a_stamp_kernel(const int64_t* __restrict__ local, int S, int cap, int W,
+                                                        int64_t nrows, int64_t* __restrict__ slotmap, int64_t call) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= S) return;
+  const int64_t r = local[s];
+  if (r < 0 || r >= nrows) return;
+  slotmap[r * W + s / cap] = (call << 32) | static_cast<int64_t>(s);
+}
+
+// One lane group per slot; the row's leader is its lowest stamping sender.  It
+// sums the row's live senders' gradient rows in sender (= slot) order --
+// bitwise segment_adagrad's position order -- and applies Adagrad in place.
+template <bool V4>
+__global__ __launch_bounds__(256) void a2a_adagrad_kernel(const float* __restrict__ grads,
+                                                          const int64_t* __restrict__ local, int S, int cap, int D,
+                                                          int lg, int W, int64_t nrows,
+                                                          const int64_t* __restrict__ slotmap, int64_t call,
+                                                          float* __restrict__ table, float* __restrict__ accum,
+                                                          float lr, float eps, float scale) {
+  const int s = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
+  if (s >= S) return;
+  const int64_t row = local[s];
+  if (row < 0 || row >= nrows) return;
+  const int w0 = s / cap;
+  const int64_t* sm = slotmap + row * W;
+  for (int w = 0; w < w0; ++w)
+    if ((sm[w] >> 32) == call) return;  // a lower sender holds this row: it updates it
+  float* wt = table + row * static_cast<int64_t>(D);
+  float* a = accum + row * static_cast<int64_t>(D);
+  for (int c = gl * 4; c < D; c += 4 << lg) {
+    const int n = D - c < 4 ? D - c : 4;
+    float wv[4], av[4], g[4] = {0.f, 0.f, 0.f, 0.f};
+    ld4<float, V4>(wt + c, n, wv);
+    ld4<float, V4>(a + c, n, av);
+    for (int w = w0; w < W; ++w) {
+      const int64_t e = w == w0 ? ((call << 32) | s) : sm[w];
+      if ((e >> 32) != call) continue;
+      float v[4];
+      ld4<float, V4>(grads + (e & 0xffffffffll) * D + c, n, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = g[k] * scale;
+      av[k] += gk * gk;
+      wv[k] -= lr * gk / (sqrtf(av[k]) + eps);
+    }
+    if (V4) {
+      *reinterpret_cast<float4*>(a + c) = make_float4(av[0], av[1], av[2], av[3]);
+      *reinterpret_cast<float4*>(wt + c) = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    } else {
+      for (int k = 0; k < n; ++k) {
+        a[c + k] = av[k];
+        wt[c + k] = wv[k];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- logit head + BCE
 // 8 rows per wave (32 per block): logit = x[m,:] . w + b; loss_m = softplus(l) - y l;
 // dlogit_m = sigmoid(l) - y.  Each block writes the sum of its rows' losses
@@ -906,6 +973,25 @@ hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64
   else
     hipLaunchKernelGGL(segment_adagrad_kernel<false>, grid, dim3(256), 0, s, grads, order, seg, rows_local, U, D, lg,
                        table, accum, lr, eps, scale, ucount, nrows);
+  return hipGetLastError();
+}
+
+hipError_t a2a_owner_update(const float* grads, const int64_t* local, int S, int cap, int W, int D, int64_t nrows,
+                            int64_t* slotmap, int64_t call, float* table, float* accum, float lr, float eps,
+                            float scale, hipStream_t s) {
+  if (S <= 0 || cap <= 0 || W < 1 || call < 1 || call >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(a2a_stamp_kernel, dim3((S + 255) / 256), dim3(256), 0, s, local, S, cap, W, nrows, slotmap, call);
+  RETURN_IF_HIP_ERR(hipGetLastError());
+  const int lg = seg_lanes_log2(D);
+  dim3 grid(static_cast<unsigned>((static_cast<int64_t>(S) << lg) + 255) / 256);
+  const bool v4 = D % 4 == 0 && reinterpret_cast<uintptr_t>(grads) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(table) % 16 == 0 && reinterpret_cast<uintptr_t>(accum) % 16 == 0;
+  if (v4)
+    hipLaunchKernelGGL(a2a_adagrad_kernel<true>, grid, dim3(256), 0, s, grads, local, S, cap, D, lg, W, nrows,
+                       slotmap, call, table, accum, lr, eps, scale);
+  else
+    hipLaunchKernelGGL(a2a_adagrad_kernel<false>, grid, dim3(256), 0, s, grads, local, S, cap, D, lg, W, nrows,
+                       slotmap, call, table, accum, lr, eps, scale);
   return hipGetLastError();
 }
 

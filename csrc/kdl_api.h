@@ -226,6 +226,12 @@ hipError_t a2a_route(const int64_t* uniq, const int* count, int n, const int64_t
 // local [n] = req / n_own or -2 - r
 hipError_t a2a_serve(const float* table, const int64_t* req, int n, int n_own, int D, void* rows, bool rows_bf16,
                      int64_t* local, hipStream_t s);
+// owner update of a fixed exchange without de-duplication: grads [S = W * cap, D]
+// fp32 with local rows local [S] (< 0 padding); slotmap [nrows * W] int64
+// persistent (zero initially), call = 1, 2, ... (< 2^31) one per call
+hipError_t a2a_owner_update(const float* grads, const int64_t* local, int S, int cap, int W, int D, int64_t nrows,
+                            int64_t* slotmap, int64_t call, float* table, float* accum, float lr, float eps,
+                            float scale, hipStream_t s);
 // rows_local outside [0, nrows) are skipped (exchange padding sentinels)
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
                            int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,

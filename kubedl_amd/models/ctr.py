@@ -425,16 +425,21 @@ class ShardedEmbedding:
         recv = torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
         dist.all_to_all_single(recv, send[: W * (cap + 1)], group=self.group)  # equal splits: no size exchange
         rv = recv.view(W, cap + 1)
-        fill = rv[:, cap].max().reshape(1)  # the global max fill: identical on every rank
         req = rv[:, :cap].reshape(-1)       # ids asked of me, -1 = padding
-        if dev.type == "cuda":
-            host = torch.empty(1, dtype=torch.int64, pin_memory=True)
-            host.copy_(fill, non_blocking=True)
-            evt = torch.cuda.Event()
-            evt.record()
-        else:
-            host, evt = fill.clone(), None
-        self._pending.append((cap, host, evt))
+        if self.slack > 0 or cap < self.max_ids:
+            # adaptive capacity: the global max fill (identical on every rank) is
+            # read LAG pulls later.  At the exact capacity (cap = max_ids >= n,
+            # checked above) no block can overflow and nothing adapts: no fill
+            # reduction, no device->host copy, no event to wait on
+            fill = rv[:, cap].max().reshape(1)
+            if dev.type == "cuda":
+                host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+                host.copy_(fill, non_blocking=True)
+                evt = torch.cuda.Event()
+                evt.record()
+            else:
+                host, evt = fill.clone(), None
+            self._pending.append((cap, host, evt))
         local = None
         if self.is_owner and self.use_hip:
             # csrc/ctr.hip a2a_serve: requested rows (padding rows zero) + every
@@ -492,7 +497,24 @@ class ShardedEmbedding:
                 # one-row segments that the update skips -- never one giant segment
                 pad = -2 - torch.arange(req.numel(), device=dev)
                 local = torch.where(req >= 0, req // self.n_own, pad)
-            self._apply_updates_dev(local, grecv, scale)
+            if self.use_hip and self.dedup is not None:
+                self._owner_update(local, grecv, cap, scale)
+            else:
+                self._apply_updates_dev(local, grecv, scale)
+
+    def _owner_update(self, local: torch.Tensor, grecv: torch.Tensor, cap: int, scale: float) -> None:
+        """Owner update without a de-duplication pass (csrc/ctr.hip a2a_owner_update):
+        each sender routes a row once, so duplicates are only across senders --
+        a per-row, per-sender slot stamp (no atomics) replaces the hash dedup +
+        CSR sort of the W * cap received slots; each row's lowest sender sums
+        the row in slot order (bitwise the segment_adagrad result)."""
+        W = self.world
+        if getattr(self, "_slotmap", None) is None or self._calls >= (1 << 31) - 1:
+            self._slotmap = torch.zeros(self.table.shape[0] * W, dtype=torch.int64, device=self.device)
+            self._calls = 0
+        self._calls += 1
+        _ext.load().a2a_owner_update(grecv, local, cap, W, self._slotmap, self._calls, self.table, self.accum,
+                                     self.lr, self.eps, scale)
 
     def _apply_updates_dev(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:
         """Owner update with the duplicate-sum on the device (no size to the host):
@@ -619,6 +641,17 @@ class CTRModel:
                 p.data = p.data.to(dtype)
         self.field_off = (torch.arange(n_fields, device=self.device) * vocab_per_field)[None, :]
 
+    def _csr_of(self, inv: torch.Tensor, count: torch.Tensor):
+        # positions ascending per unique id: the argsort path's summation order;
+        # live count on the device
+        dd = self.emb.dedup
+        n = inv.numel()
+        ws = dd._buffers(n)
+        seg = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        order = torch.empty(n, dtype=torch.int64, device=self.device)
+        _ext.load().csr_from_inverse_only(inv, ws["sizes"], count, ws["bsum"], ws["cursor"], seg, order)
+        return seg, order
+
     def build_input(self, ids: torch.Tensor, dense: torch.Tensor):
         B = ids.shape[0]
         gids = (ids + self.field_off).reshape(-1)
@@ -646,14 +679,7 @@ class CTRModel:
         kind = ctx[0] if ctx is not None and isinstance(ctx[0], str) else None
         count = ctx[2] if kind == "dev" else ctx[3] if kind == "fixed" else None
         if kind is not None and self.emb.dedup is not None and inv.numel() > 0:
-            # CSR of the inverse on the device (positions ascending per unique id:
-            # the same summation order as the argsort path), live count on the device
-            dd = self.emb.dedup
-            n = inv.numel()
-            ws = dd._buffers(n)
-            seg = torch.empty(n + 1, dtype=torch.int64, device=self.device)
-            order = torch.empty(n, dtype=torch.int64, device=self.device)
-            _ext.load().csr_from_inverse_only(inv, ws["sizes"], count, ws["bsum"], ws["cursor"], seg, order)
+            seg, order = self._csr_of(inv, count)
             if kind == "fixed":
                 # each unique id's summed gradient row lands in its exchange slot
                 # (rslot) of the send buffer: no [U, D] intermediate, no scatter

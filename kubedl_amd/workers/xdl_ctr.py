@@ -160,6 +160,8 @@ def main(argv=None) -> int:
         opt.step()
         losses.append(loss.detach())
         common.report_progress(it + 1, final=it + 1 == total)
+    # host time to issue the timed steps (no sync inside the loop): ~dt when host-bound
+    issue = time.perf_counter() - t0 if t0 is not None else 0.0
     if use_gpu:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0 if t0 is not None else 0.0
@@ -174,6 +176,7 @@ def main(argv=None) -> int:
         print(json.dumps({"rank": rank, "world_size": world, "ps": n_ps, "workers": len(workers),
                           "steps": args.steps, "batch_per_worker": args.batch, "seconds": dt,
                           "steps_per_sec": args.steps / dt if dt > 0 else 0.0,
+                          "host_issue_ms_per_step": round(issue / max(args.steps, 1) * 1e3, 4),
                           "samples_per_sec": args.steps * args.batch * len(workers) / dt if dt > 0 else 0.0,
                           "loss_first": first, "loss_last": last, "device": str(device),
                           "hip_kernels": emb.use_hip, "exchange": "fixed" if emb._fixed() else "sync-free",

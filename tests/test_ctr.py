@@ -717,6 +717,40 @@ def test_a2a_serve_and_mapped_segment_reduce():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("W,cap,nrows,D", [(5, 300, 700, 64), (1, 1000, 5000, 64), (64, 8, 200, 16), (3, 50, 40, 12)])
+def test_a2a_owner_update_matches_dedup_segment_adagrad(W, cap, nrows, D):
+    """a2a_owner_update (per-row sender stamps, no dedup pass) gives bitwise the
+    table and Adagrad state of the hash dedup + CSR + segment_adagrad path, with
+    rows repeated across senders, padding sentinels, and three calls in a row
+    (stale stamps of earlier calls must not count)."""
+    from kubedl_amd.models.ctr import DeviceDedup
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g = torch.Generator(device="cuda").manual_seed(W * 1000 + cap)
+    table0 = torch.randn(nrows, D, device="cuda", generator=g)
+    accum0 = torch.rand(nrows, D, device="cuda", generator=g)
+    t1, a1 = table0.clone(), accum0.clone()
+    t2, a2 = table0.clone(), accum0.clone()
+    slotmap = torch.zeros(nrows * W, dtype=torch.int64, device="cuda")
+    dd = DeviceDedup("cuda")
+    for call in range(1, 4):
+        # each sender: distinct rows (a sender routes an id once), then padding
+        blocks = []
+        for w in range(W):
+            k = int(torch.randint(0, min(cap, nrows) + 1, (1,), generator=g, device="cuda"))
+            rows = torch.randperm(nrows, device="cuda", generator=g)[:k]
+            pad = -2 - torch.arange(w * cap + k, (w + 1) * cap, device="cuda")
+            blocks.append(torch.cat([rows, pad]))
+        local = torch.cat(blocks)
+        grads = torch.randn(W * cap, D, device="cuda", generator=g)
+        ext.a2a_owner_update(grads, local, cap, W, slotmap, call, t1, a1, 0.05, 1e-8, 0.5)
+        uniq, inv, count, seg, order = dd(local, csr=True)
+        ext.segment_adagrad(grads, order, seg, uniq, t2, a2, 0.05, 1e-8, 0.5, count)
+        torch.cuda.synchronize()
+        assert torch.equal(t1, t2) and torch.equal(a1, a2), call
+
+
+@pytest.mark.gpu
 def test_ctr_fixed_exchange_world1_rehearsal_bit_exact():
     """The world-1 rehearsal of the PS + worker exchange (force_fixed, one owner,
     RCCL all-to-alls on a 1-rank group) trains to the same table, Adagrad state
