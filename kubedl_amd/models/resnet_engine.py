@@ -121,6 +121,7 @@ class HipKernels:
         self.ext = _ext.load()
         self.dev = dev
         self._dw32 = {}
+        self._ident = {}  # identity prologue coefficients [ones | zeros] per channel count
         # BN finalize folded into the producing conv GEMM's last arriving blocks
         # (csrc/bn_fin.h; EngineOptions.bn_fin = "kernel": separate finalize
         # launches).  Round 2 measured it neutral while its inlined tail made every
@@ -403,10 +404,12 @@ class HipKernels:
         self.ext.conv1x1_wgrad(g, x, self.fcoef(pro) if pro is not None else None, dw32, dW.view(cout, cin), 1.0,
                                M, cout, cin, ho, wo, h, w, stride)
 
-    def wgrad_gram(self, g, x2, st2: BNState, st3: BNState, w3, dW):
-        """conv3's weight gradient with BN3's backward apply folded in (csrc/conv1x1.hip
-        Gram fold): dW3 = diag(k) g^T a2 + diag(c1) W3 (a2^T a2) + c0 (1^T a2), a2 =
-        relu(B2(c2)) -- dc3 is never materialised.  G on the weight-gradient kernel
+    def wgrad_gram(self, g, x2, st2: BNState | None, st3: BNState, w3, dW):
+        """A 1x1 conv's weight gradient with its output BN's backward apply folded in
+        (csrc/conv1x1.hip Gram fold): dW = diag(k) g^T a + diag(c1) W (a^T a) + c0 (1^T a),
+        a = relu(B2(x2)) (conv3) or x2 itself when ``st2`` is None (a stride-1
+        downsample conv: its input is a block output, already >= 0) -- the BN's
+        input gradient is never materialised.  G on the weight-gradient kernel
         (fp32, left in its slab workspace), Q | s on the Gram kernel, then the fold."""
         n, cout, ho, wo = g.shape
         _, cin, h, w = x2.shape
@@ -416,9 +419,14 @@ class HipKernels:
         dw32 = self._dw32.get(key)
         if dw32 is None or dw32.numel() < need:
             dw32 = self._dw32[key] = torch.empty(need, device=g.device)
-        self.ext.conv1x1_wgrad(g, x2, self.fcoef(st2), dw32, None, 1.0, M, cout, cin, ho, wo, h, w, 1)
+        pro = self.fcoef(st2) if st2 is not None else None
+        self.ext.conv1x1_wgrad(g, x2, pro, dw32, None, 1.0, M, cout, cin, ho, wo, h, w, 1)
+        if pro is None:  # relu(x * 1 + 0) = x for the non-negative block output
+            pro = self._ident.get(cin)
+            if pro is None:
+                pro = self._ident[cin] = torch.cat([torch.ones(cin, device=g.device), torch.zeros(cin, device=g.device)])
         qs = self._ws32(("gram", M, cin), self.ext.conv1x1_gram_floats(M, cin))
-        self.ext.conv1x1_gram(x2, self.fcoef(st2), qs, M, cin)
+        self.ext.conv1x1_gram(x2, pro, qs, M, cin)
         self.ext.gram_fold(dw32, qs, w3.view(cout, cin), self.bcoef(st3), dW.view(cout, cin), cout, cin)
 
     def wgrad3x3(self, g, x, stride, dW, pro: BNState | None = None):
@@ -724,7 +732,7 @@ class TorchKernels:
 
     def wgrad_gram(self, g, x2, st2, st3, w3, dW):
         """The Gram fold's algebra in fp32 (HipKernels.wgrad_gram)."""
-        a = _rows(self._pro(x2, st2).contiguous(memory_format=torch.channels_last))
+        a = _rows((self._pro(x2, st2) if st2 is not None else x2.float()).contiguous(memory_format=torch.channels_last))
         G = _rows(g.float().contiguous(memory_format=torch.channels_last)).t() @ a
         Q = a.t() @ a
         k, c1, c0 = st3.bcoef
@@ -1210,7 +1218,12 @@ class ResNetEngine:
                 op3, opd = (dc3, None, dc3, None), (dcd, None, dcd, None)
             else:
                 op3 = self._bn_bwd_operand(g, c3, st3, gram=True)
-                opd = self._bn_bwd_operand(g, cd, std_) if std_ is not None else None
+                # a stride-1 downsample conv's input is dense: its weight gradient
+                # takes the Gram fold too (the dedicated Gram kernel: 64 / 128 channels)
+                # (13,910-13,933 vs 13,848-13,872 img/s, profiles/r05_gram_fold_ab.txt)
+                dgram = (std_ is not None and blk.down_conv.stride[0] == 1
+                         and (blk.down_conv.in_channels in (64, 128) or K.name != "hip"))
+                opd = self._bn_bwd_operand(g, cd, std_, gram=dgram) if std_ is not None else None
             # conv3: dgrad with B2+ReLU mask and B2 sums fused; wgrad with B2+ReLU recomputed
             g2 = K.dgrad_maskx(op3[0], self._wt(blk.conv3), c2, st2, bpro=op3[1])
             with self._on_side(*self._side_of(op3)):
@@ -1265,7 +1278,9 @@ class ResNetEngine:
                 g_prev = K.dgrad_res(op1[0], self._wt(blk.conv1), eres, res_stride, None, bpro=op1[1])
             with self._on_side(*self._side_of(op1), *(self._side_of(opd) if opd is not None else ())):
                 K.wgrad(op1[2], cur_in, 1, None, self._g(blk.conv1.weight), gbpro=op1[3])
-                if blk.down_conv is not None:
+                if blk.down_conv is not None and opd[3] == "gram":
+                    K.wgrad_gram(g, cur_in, None, std_, blk.down_conv.weight, self._g(blk.down_conv.weight))
+                elif blk.down_conv is not None:
                     K.wgrad(opd[2], cur_in, blk.down_conv.stride[0], None, self._g(blk.down_conv.weight),
                             gbpro=opd[3])
             self.on_ready(blk.conv1.weight)
