@@ -84,11 +84,21 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   static_assert((PRO != PRO_BWD && PRO != PRO_RES && PRO != PRO_RES2) || GATHER == G_DENSE,
                 "the two-input prologues read dense rows");
   constexpr bool TWO_IN = PRO == PRO_BWD || PRO == PRO_RES || PRO == PRO_RES2;  // A and a second row operand bx
-  // [2 buffers][BM + BN rows][LDK]; after the K loop one buffer doubles as the
-  // [BM][BN + 8] output tile and finally as the reduction scratch.
-  constexpr int LDK = KBK + 8;  // padded LDS row (bf16): 16-B slot stride odd -> conflict-free fragment reads
+  // [2 buffers][BM + BN rows][KBK]; after the K loop one buffer doubles as the
+  // [BM][BN + 8] output tile and finally as the reduction scratch.  Buffers are
+  // spaced as padded rows (LDK) so that output tile fits one of them as before.
+  constexpr int LDK = KBK + 8;
   constexpr int CPRK = KBK / 8; // 16-B chunks per staged row
   constexpr int kBuf = (BM + BN) * LDK;
+  // Staged rows are unpadded with the 16-B chunk index XORed by (row / RG): the
+  // 16 lanes of one staging store (RG rows x CPRK chunks) and the 16 rows of one
+  // MFMA fragment read both land on distinct bank groups.  The padded layout
+  // (row stride KBK + 8) left the stores 2-way conflicted: the 32-deep-K conv3
+  // forward ran 131 % LDS conflict cycles per LDS cycle, 57 % swizzled, and the
+  // step 13,761-13,793 -> 13,810-13,879 img/s (profiles/r05_gemm_swizzle_ab.txt).
+  constexpr int RG = 16 / CPRK;
+  constexpr int ldk = KBK;
+  auto soff = [](int row, int chunk) { return row * KBK + ((chunk ^ ((row / RG) & (CPRK - 1))) << 3); };
   // PRO_BWD: the backward coefficients k | c1 | c0 of every K channel, staged
   // once per block behind the operand buffers (one __shared__ array: a second
   // one can make hipcc drain the pipeline, cdna_hip_programming.md §5 item 4a)
@@ -222,7 +232,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
   };
   auto swrite = [&](int buf) {
     bf16_t* As = lds + buf * kBuf;
-    bf16_t* Bs = As + BM * LDK;
+    bf16_t* Bs = As + BM * ldk;
     float bk[8], bc1[8], bc0[8], bd[8];  // PRO_BWD / RES / RES2: this thread's 8 channels of the staged K-step
     (void)bk; (void)bc1; (void)bc0; (void)bd;
     if constexpr (TWO_IN) {
@@ -287,12 +297,12 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       if constexpr (GATHER == G_CONV3) {
         if (!((ra_ok >> i) & 1u)) v = make_uint4(0, 0, 0, 0);  // zero padding (after BN+ReLU)
       }
-      *reinterpret_cast<uint4*>(&As[a_row[i] * LDK + a_kc[i]]) = v;
+      *reinterpret_cast<uint4*>(&As[soff(a_row[i], a_kc[i] >> 3)]) = v;
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int c = t + i * kThreads;
-      *reinterpret_cast<uint4*>(&Bs[(c / CPRK) * LDK + (c % CPRK) * 8]) = rb[i];
+      *reinterpret_cast<uint4*>(&Bs[soff(c / CPRK, c % CPRK)]) = rb[i];
     }
   };
 
@@ -315,16 +325,16 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm1x1_kernel(GemmParams p, i
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
     // one staged K-step's fragments + MFMAs into ``a``
     auto mma = [&](const bf16_t* As, f32x16_t (&a)[TN][TM]) {
-      const bf16_t* Bs = As + BM * LDK;
+      const bf16_t* Bs = As + BM * ldk;
 #pragma unroll
       for (int s = 0; s < KBK / 16; ++s) {
         bf16x8_t wf[TN], xf[TM];
 #pragma unroll
         for (int i = 0; i < TN; ++i)
-          wf[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&Bs[(wn0 + i * 32 + fr) * LDK + s * 16 + fh * 8]));
+          wf[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&Bs[soff(wn0 + i * 32 + fr, s * 2 + fh)]));
 #pragma unroll
         for (int j = 0; j < TM; ++j)
-          xf[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&As[(wm0 + j * 32 + fr) * LDK + s * 16 + fh * 8]));
+          xf[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&As[soff(wm0 + j * 32 + fr, s * 2 + fh)]));
 #pragma unroll
         for (int i = 0; i < TN; ++i)
 #pragma unroll
