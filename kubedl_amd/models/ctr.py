@@ -53,30 +53,37 @@ class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        ext = _ext.load()
-        dy = dy.contiguous()
-        # db straight in the parameter dtype (bf16): no zero-fill, no conversion launch
-        dz, db = ext.relu_bwd_dbias(dy, y if ctx.relu else None, w.dtype == torch.bfloat16)
-        fout, fin = w.shape
-        # dx = dz . W on the same MFMA kernel as the forward, W read as [K, N]
-        # (transposed LDS reads: no per-step W^T copy)
-        if fin % 8 == 0:
-            dx = ext.gemm_bias_act(dz, w.contiguous(), None, False, True)
-        else:
-            dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
-        if fout % 64 == 0 and fin % 64 == 0:
-            # dW = dz^T x: the reduction over the batch is the weight-gradient
-            # form of csrc/wgrad_dma.hip (both operands row-major, LDS-DMA +
-            # transposed LDS reads; split-batch fp32 slabs, fixed-order reduce)
-            B = x.shape[0]
-            ws = _wgrad_workspace(ext, B, fout, fin, x.device)
-            dw = torch.empty(fout, fin, dtype=w.dtype, device=w.device)
-            # solo: no weight-gradient side stream here, so the split count
-            # that fills the chip (not the ResNet engine's two-stream one)
-            ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1, True)
-        else:
-            dw = (dz.t() @ x).to(w.dtype)
-        return dx, dw, ((db if db.dtype == w.dtype else db.to(w.dtype)) if ctx.has_b else None), None
+        dx, dw, db = _linear_bwd(dy, x, w, y, ctx.relu, ctx.has_b)
+        return dx, dw, db, None
+
+
+def _linear_bwd(dy, x, w, y, relu: bool, has_b: bool):
+    """(dx, dW, db) of y = act(x W^T + b) on the kdl kernels (the backward of
+    _FusedLinearFn and of DenseTower.train_step)."""
+    ext = _ext.load()
+    dy = dy.contiguous()
+    # db straight in the parameter dtype (bf16): no zero-fill, no conversion launch
+    dz, db = ext.relu_bwd_dbias(dy, y if relu else None, w.dtype == torch.bfloat16)
+    fout, fin = w.shape
+    # dx = dz . W on the same MFMA kernel as the forward, W read as [K, N]
+    # (transposed LDS reads: no per-step W^T copy)
+    if fin % 8 == 0:
+        dx = ext.gemm_bias_act(dz, w.contiguous(), None, False, True)
+    else:
+        dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
+    if fout % 64 == 0 and fin % 64 == 0:
+        # dW = dz^T x: the reduction over the batch is the weight-gradient
+        # form of csrc/wgrad_dma.hip (both operands row-major, LDS-DMA +
+        # transposed LDS reads; split-batch fp32 slabs, fixed-order reduce)
+        B = x.shape[0]
+        ws = _wgrad_workspace(ext, B, fout, fin, x.device)
+        dw = torch.empty(fout, fin, dtype=w.dtype, device=w.device)
+        # solo: no weight-gradient side stream here, so the split count
+        # that fills the chip (not the ResNet engine's two-stream one)
+        ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1, True)
+    else:
+        dw = (dz.t() @ x).to(w.dtype)
+    return dx, dw, ((db if db.dtype == w.dtype else db.to(w.dtype)) if has_b else None)
 
 
 _WS = {}
@@ -105,12 +112,8 @@ class _HeadBCEFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, y):
-        ext = _ext.load()
         x = x.contiguous()
-        bb = b.reshape(1) if b.dtype in (torch.bfloat16, torch.float32) else b.float().reshape(1)
-        # the kernel's last block folds the per-block losses into the mean (no reduce launch)
-        logit, dlogit, _part, loss = ext.head_bce_fwd(x, w.reshape(-1).contiguous(), bb.contiguous(),
-                                                      y.float().contiguous())
+        loss, logit, dlogit = _head_fwd(x, w, b, y)
         ctx.save_for_backward(x, w, dlogit)
         ctx.b_dtype = b.dtype
         ctx.mark_non_differentiable(logit)
@@ -119,14 +122,28 @@ class _HeadBCEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss, _glogit):
         x, w, dlogit = ctx.saved_tensors
-        ext = _ext.load()
-        # dW / db summed over the per-block partials in a fixed order by the kernel's
-        # last block (deterministic), already bf16
-        dx, dw, db, _dwp, _dbp = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0],
-                                                  gloss.float().reshape(1).contiguous())
-        dw = dw.reshape(w.shape) if w.dtype == dw.dtype else dw.to(w.dtype).reshape(w.shape)
-        db = db if ctx.b_dtype == db.dtype else db.to(ctx.b_dtype)
+        dx, dw, db = _head_bwd(x, w, ctx.b_dtype, dlogit, gloss.float().reshape(1).contiguous())
         return dx, dw, db, None
+
+
+def _head_fwd(x, w, b, y):
+    """(mean loss [1], logits, dloss/dlogit) of the fused logit head + BCE."""
+    ext = _ext.load()
+    bb = b.reshape(1) if b.dtype in (torch.bfloat16, torch.float32) else b.float().reshape(1)
+    # the kernel's last block folds the per-block losses into the mean (no reduce launch)
+    logit, dlogit, _part, loss = ext.head_bce_fwd(x, w.reshape(-1).contiguous(), bb.contiguous(),
+                                                  y.float().contiguous())
+    return loss, logit, dlogit
+
+
+def _head_bwd(x, w, b_dtype, dlogit, gloss):
+    ext = _ext.load()
+    # dW / db summed over the per-block partials in a fixed order by the kernel's
+    # last block (deterministic), already bf16
+    dx, dw, db, _dwp, _dbp = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0], gloss)
+    dw = dw.reshape(w.shape) if w.dtype == dw.dtype else dw.to(w.dtype).reshape(w.shape)
+    db = db if b_dtype == db.dtype else db.to(b_dtype)
+    return dx, dw, db
 
 
 def head_bce(x, w, b, y):
@@ -162,6 +179,40 @@ class DenseTower(nn.Module):
         for l in self.layers:
             x = l(x)
         return self.head(x).float().squeeze(-1)
+
+    def fused_ok(self, x) -> bool:
+        return (x.is_cuda and _ext.available() and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0
+                and all(l.weight.dtype == torch.bfloat16 for l in self.layers))
+
+    @torch.no_grad()
+    def train_step(self, x, y, on_ready=None):
+        """Forward + backward of the tower without the autograd engine: the same
+        kernels as ``loss`` + ``backward`` (_FusedLinearFn, _HeadBCEFn) called in
+        order -- bitwise the same loss and gradients (tests/test_ctr.py), a
+        fraction of the host time of a 4-node autograd graph in a ~0.4 ms step.
+        Parameter gradients are assigned to ``.grad`` (``on_ready(p)`` after each,
+        e.g. FlatDDP.ready); returns (loss, dL/dx)."""
+        acts = [x.contiguous()]
+        for l in self.layers:
+            acts.append(_ext.load().gemm_bias_act(acts[-1], l.weight.contiguous(), l.bias, bool(l.relu)))
+        hw, hb = self.head.weight, self.head.bias
+        loss, _logit, dlogit = _head_fwd(acts[-1], hw, hb, y)
+        one = getattr(self, "_one", None)
+        if one is None or one.device != x.device:
+            one = self._one = torch.ones(1, device=x.device)
+        dy, dw, db = _head_bwd(acts[-1], hw, hb.dtype, dlogit, one)
+        for p, g in ((hw, dw), (hb, db)):
+            p.grad = g
+            if on_ready is not None:
+                on_ready(p)
+        for i in range(len(self.layers) - 1, -1, -1):
+            l = self.layers[i]
+            dy, dw, db = _linear_bwd(dy, acts[i], l.weight, acts[i + 1], l.relu, True)
+            for p, g in ((l.weight, dw), (l.bias, db)):
+                p.grad = g
+                if on_ready is not None:
+                    on_ready(p)
+        return loss.view(()), dy
 
     def loss(self, x, y):
         """Training step forward: (mean BCE loss, logits); the head runs fused

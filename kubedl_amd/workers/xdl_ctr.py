@@ -152,10 +152,14 @@ def main(argv=None) -> int:
         ids, dense, y = batches[it % len(batches)]
         space.zero_grad()
         x, inv, U = model.build_input(ids, dense)
-        x.requires_grad_(True)
-        loss, _logit = model.tower.loss(x, y)
-        loss.backward()
-        model.push_grads(x.grad, inv, U, scale=1.0 / len(workers))
+        if model.tower.fused_ok(x):  # explicit forward + backward (no autograd graph)
+            loss, xgrad = model.tower.train_step(x, y, on_ready=ddp.ready if ddp.active else None)
+        else:
+            x.requires_grad_(True)
+            loss, _logit = model.tower.loss(x, y)
+            loss.backward()
+            xgrad = x.grad
+        model.push_grads(xgrad, inv, U, scale=1.0 / len(workers))
         ddp.finish()
         opt.step()
         losses.append(loss.detach())

@@ -751,6 +751,34 @@ def test_a2a_owner_update_matches_dedup_segment_adagrad(W, cap, nrows, D):
 
 
 @pytest.mark.gpu
+def test_tower_train_step_matches_autograd_bitwise():
+    """DenseTower.train_step (the kernels called in order, no autograd graph) gives
+    bitwise the loss, input gradient and parameter gradients of loss() + backward()."""
+    import copy
+    from kubedl_amd.models.ctr import DenseTower
+    torch.manual_seed(5)
+    t1 = DenseTower(1728, (1024, 512, 256)).cuda()
+    with torch.no_grad():
+        for p in t1.parameters():
+            p.data = p.data.bfloat16()
+    t2 = copy.deepcopy(t1)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.randn(4096, 1728, device="cuda", generator=g).bfloat16()
+    y = torch.randint(0, 2, (4096,), device="cuda", generator=g).float()
+    xa = x.clone().requires_grad_(True)
+    la, _ = t1.loss(xa, y)
+    la.backward()
+    seen = []
+    assert t2.fused_ok(x)
+    lb, dxb = t2.train_step(x, y, on_ready=seen.append)
+    torch.cuda.synchronize()
+    assert torch.equal(la.detach(), lb) and torch.equal(xa.grad, dxb)
+    for (n, p), q in zip(t1.named_parameters(), t2.parameters()):
+        assert torch.equal(p.grad, q.grad), n
+    assert len(seen) == len(list(t2.parameters()))
+
+
+@pytest.mark.gpu
 def test_ctr_fixed_exchange_world1_rehearsal_bit_exact():
     """The world-1 rehearsal of the PS + worker exchange (force_fixed, one owner,
     RCCL all-to-alls on a 1-rank group) trains to the same table, Adagrad state
