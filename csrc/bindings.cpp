@@ -715,7 +715,8 @@ void a2a_route(const at::Tensor& uniq, const c10::optional<at::Tensor>& count, c
 }
 
 // owner side: (rows [n, D] fp32, local [n] int64) for the requested ids req [n]
-std::vector<at::Tensor> a2a_serve(const at::Tensor& table, const at::Tensor& req, int64_t n_own, bool rows_bf16) {
+std::vector<at::Tensor> a2a_serve(const at::Tensor& table, const at::Tensor& req, int64_t n_own, bool rows_bf16,
+                                  const c10::optional<at::Tensor>& slotmap, int64_t call, int64_t cap, int64_t W) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous() && table.scalar_type() == at::kFloat &&
                   table.size(1) % 4 == 0 && reinterpret_cast<uintptr_t>(table.data_ptr()) % 16 == 0,
               "a2a_serve: fp32 table [V, D], D % 4 == 0");
@@ -724,9 +725,17 @@ std::vector<at::Tensor> a2a_serve(const at::Tensor& table, const at::Tensor& req
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto rows = at::empty({n, D}, table.options().dtype(rows_bf16 ? at::kBFloat16 : at::kFloat));
   auto local = at::empty({n}, req.options());
+  int64_t* sm = nullptr;
+  if (slotmap.has_value()) {
+    TORCH_CHECK(slotmap->scalar_type() == at::kLong && slotmap->is_contiguous() &&
+                    slotmap->numel() >= table.size(0) * W && W >= 1 && cap >= 1 && n == W * cap,
+                "a2a_serve: slotmap int64 [nrows * W], n = W * cap");
+    sm = slotmap->data_ptr<int64_t>();
+  }
   check_hip(kdl::a2a_serve(table.data_ptr<float>(), req.data_ptr<int64_t>(), static_cast<int>(n),
                            static_cast<int>(n_own), static_cast<int>(D), rows.data_ptr(), rows_bf16,
-                           local.data_ptr<int64_t>(), cur_stream()),
+                           local.data_ptr<int64_t>(), cur_stream(), sm, call, static_cast<int>(cap),
+                           static_cast<int>(W), table.size(0)),
             "a2a_serve");
   return {rows, local};
 }
@@ -754,7 +763,8 @@ void segment_adagrad(const at::Tensor& grads, const at::Tensor& order, const at:
 // de-duplication pass; slotmap int64 [nrows * W] kept by the caller (zero
 // initially), call = 1, 2, ... per update
 void a2a_owner_update(const at::Tensor& grads, const at::Tensor& local, int64_t cap, int64_t W, at::Tensor slotmap,
-                      int64_t call, at::Tensor table, at::Tensor accum, double lr, double eps, double scale) {
+                      int64_t call, at::Tensor table, at::Tensor accum, double lr, double eps, double scale,
+                      bool stamped) {
   TORCH_CHECK(grads.is_cuda() && grads.scalar_type() == at::kFloat && grads.is_contiguous() && grads.dim() == 2,
               "a2a_owner_update: fp32 grads [S, D]");
   const int64_t S = grads.size(0), D = grads.size(1);
@@ -773,7 +783,7 @@ void a2a_owner_update(const at::Tensor& grads, const at::Tensor& local, int64_t 
                                   static_cast<int>(cap), static_cast<int>(W), static_cast<int>(D), nrows,
                                   slotmap.data_ptr<int64_t>(), call, table.data_ptr<float>(),
                                   accum.data_ptr<float>(), static_cast<float>(lr), static_cast<float>(eps),
-                                  static_cast<float>(scale), cur_stream()),
+                                  static_cast<float>(scale), cur_stream(), stamped),
             "a2a_owner_update");
 }
 
@@ -1684,9 +1694,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("col0"), py::arg("D"), py::arg("order"), py::arg("seg"), py::arg("ucount") = py::none(),
         py::arg("out_rows") = py::none(), py::arg("out") = py::none());
   m.def("a2a_route", &a2a_route, "fixed-capacity exchange: per-owner send blocks + header + rslot of unique ids");
-  m.def("a2a_owner_update", &a2a_owner_update, "owner Adagrad update of a fixed exchange without de-duplication");
-  m.def("a2a_serve", &a2a_serve, "owner side of the fixed exchange: requested rows + local row ids",
-        py::arg("table"), py::arg("req"), py::arg("n_own"), py::arg("rows_bf16") = false);
+  m.def("a2a_owner_update", &a2a_owner_update, "owner Adagrad update of a fixed exchange without de-duplication",
+        py::arg("grads"), py::arg("local"), py::arg("cap"), py::arg("W"), py::arg("slotmap"), py::arg("call"),
+        py::arg("table"), py::arg("accum"), py::arg("lr"), py::arg("eps"), py::arg("scale"),
+        py::arg("stamped") = false);
+  m.def("a2a_serve", &a2a_serve, "owner side of the fixed exchange: requested rows + local row ids (+ the owner "
+        "update's slot stamps)",
+        py::arg("table"), py::arg("req"), py::arg("n_own"), py::arg("rows_bf16") = false,
+        py::arg("slotmap") = py::none(), py::arg("call") = 0, py::arg("cap") = 0, py::arg("W") = 0);
   m.def("embed_gather_cast", &embed_gather_cast, "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("dedup_table_slots", &dedup_table_slots, "hash-table slots dedup_csr needs for n ids");

@@ -978,10 +978,13 @@ hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64
 
 hipError_t a2a_owner_update(const float* grads, const int64_t* local, int S, int cap, int W, int D, int64_t nrows,
                             int64_t* slotmap, int64_t call, float* table, float* accum, float lr, float eps,
-                            float scale, hipStream_t s) {
+                            float scale, hipStream_t s, bool stamped) {
   if (S <= 0 || cap <= 0 || W < 1 || call < 1 || call >= (int64_t(1) << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(a2a_stamp_kernel, dim3((S + 255) / 256), dim3(256), 0, s, local, S, cap, W, nrows, slotmap, call);
-  RETURN_IF_HIP_ERR(hipGetLastError());
+  if (!stamped) {
+    hipLaunchKernelGGL(a2a_stamp_kernel, dim3((S + 255) / 256), dim3(256), 0, s, local, S, cap, W, nrows, slotmap,
+                       call);
+    RETURN_IF_HIP_ERR(hipGetLastError());
+  }
   const int lg = seg_lanes_log2(D);
   dim3 grid(static_cast<unsigned>((static_cast<int64_t>(S) << lg) + 255) / 256);
   const bool v4 = D % 4 == 0 && reinterpret_cast<uintptr_t>(grads) % 16 == 0 &&
@@ -1387,13 +1390,19 @@ __global__ __launch_bounds__(256) void a2a_route_kernel(const int64_t* __restric
 template <typename T>
 __global__ __launch_bounds__(256) void a2a_serve_kernel(const float* __restrict__ table, const int64_t* __restrict__ req,
                                                         int n, int n_own, int D, int lg, T* __restrict__ rows,
-                                                        int64_t* __restrict__ local) {
+                                                        int64_t* __restrict__ local, int64_t* __restrict__ slotmap,
+                                                        int64_t call, int cap, int W, int64_t nrows) {
   const int r = (blockIdx.x * 256 + threadIdx.x) >> lg;
   const int gl = threadIdx.x & ((1 << lg) - 1);
   if (r >= n) return;
   const int64_t id = req[r];
   const int64_t row = id >= 0 ? id / n_own : -2 - static_cast<int64_t>(r);
-  if (gl == 0) local[r] = row;
+  if (gl == 0) {
+    local[r] = row;
+    // the push's owner update stamp (a2a_stamp_kernel's store), here while the
+    // slot's row is at hand: one launch less per step
+    if (slotmap != nullptr && row >= 0 && row < nrows) slotmap[row * W + r / cap] = (call << 32) | r;
+  }
   T* dst = rows + static_cast<int64_t>(r) * D;
   const float* src = table + (row >= 0 ? row : 0) * static_cast<int64_t>(D);
   for (int c = gl * 4; c < D; c += 4 << lg) {
@@ -1422,17 +1431,19 @@ hipError_t a2a_route(const int64_t* uniq, const int* count, int n, const int64_t
 int a2a_route_blocks(int n) { return n > 0 ? (n + 255) / 256 : 1; }
 
 hipError_t a2a_serve(const float* table, const int64_t* req, int n, int n_own, int D, void* rows, bool rows_bf16,
-                     int64_t* local, hipStream_t s) {
+                     int64_t* local, hipStream_t s, int64_t* slotmap, int64_t call, int cap, int W, int64_t nrows) {
   if (n <= 0) return hipSuccess;
   if (D % 4 || n_own < 1) return hipErrorInvalidValue;
+  if (slotmap != nullptr && (cap < 1 || W < 1 || n != W * cap || call < 1 || call >= (int64_t(1) << 31)))
+    return hipErrorInvalidValue;
   const int lg = seg_lanes_log2(D);
   dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(n) << lg) + 255) / 256));
   if (rows_bf16)
     hipLaunchKernelGGL(a2a_serve_kernel<bf16_t>, grid, dim3(256), 0, s, table, req, n, n_own, D, lg,
-                       static_cast<bf16_t*>(rows), local);
+                       static_cast<bf16_t*>(rows), local, slotmap, call, cap, W, nrows);
   else
     hipLaunchKernelGGL(a2a_serve_kernel<float>, grid, dim3(256), 0, s, table, req, n, n_own, D, lg,
-                       static_cast<float*>(rows), local);
+                       static_cast<float*>(rows), local, slotmap, call, cap, W, nrows);
   return hipGetLastError();
 }
 

@@ -224,14 +224,17 @@ hipError_t a2a_route(const int64_t* uniq, const int* count, int n, const int64_t
                      int cap, int* cnt, int64_t* send, int64_t* rslot, hipStream_t s);
 // owner side: rows [n, D] = table[req / n_own] (zero for req < 0; fp32 or bf16),
 // local [n] = req / n_own or -2 - r
+// slotmap != nullptr: also stamp slotmap[local * W + slot / cap] = (call << 32) | slot
+// (the owner update's stamps, a2a_owner_update(..., stamped = true); n = W * cap)
 hipError_t a2a_serve(const float* table, const int64_t* req, int n, int n_own, int D, void* rows, bool rows_bf16,
-                     int64_t* local, hipStream_t s);
+                     int64_t* local, hipStream_t s, int64_t* slotmap = nullptr, int64_t call = 0, int cap = 0,
+                     int W = 0, int64_t nrows = 0);
 // owner update of a fixed exchange without de-duplication: grads [S = W * cap, D]
 // fp32 with local rows local [S] (< 0 padding); slotmap [nrows * W] int64
 // persistent (zero initially), call = 1, 2, ... (< 2^31) one per call
 hipError_t a2a_owner_update(const float* grads, const int64_t* local, int S, int cap, int W, int D, int64_t nrows,
                             int64_t* slotmap, int64_t call, float* table, float* accum, float lr, float eps,
-                            float scale, hipStream_t s);
+                            float scale, hipStream_t s, bool stamped = false);  // stamped: by a2a_serve
 // rows_local outside [0, nrows) are skipped (exchange padding sentinels)
 hipError_t segment_adagrad(const float* grads, const int64_t* order, const int64_t* seg, const int64_t* rows_local,
                            int U, int D, int64_t nrows, float* table, float* accum, float lr, float eps, float scale,

@@ -456,8 +456,8 @@ class ShardedEmbedding:
             # csrc/ctr.hip a2a_route: a block-stable counting sort of the unique ids
             # by owner straight into the send blocks, padding and headers written by
             # the same launch; no one-hot [n, W + 1], no fill of the send buffer
-            send = torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
-            rslot = torch.empty(n, dtype=torch.int64, device=dev)
+            send = self._buf("send", (W * (cap + 1),), torch.int64)
+            rslot = self._buf("rslot", (n,), torch.int64)
             _ext.load().a2a_route(uniq, count if n else None, self._owner_rank, W, cap, send, rslot)
         else:
             send = torch.full((W * (cap + 1) + 1,), -1, dtype=torch.int64, device=dev)
@@ -473,7 +473,8 @@ class ShardedEmbedding:
             else:
                 rslot = torch.empty(0, dtype=torch.int64, device=dev)
                 send[cap: W * (cap + 1): cap + 1] = 0
-        recv = torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
+        recv = self._buf("recv", (W * (cap + 1),), torch.int64) if self.use_hip else \
+            torch.empty(W * (cap + 1), dtype=torch.int64, device=dev)
         dist.all_to_all_single(recv, send[: W * (cap + 1)], group=self.group)  # equal splits: no size exchange
         rv = recv.view(W, cap + 1)
         req = rv[:, :cap].reshape(-1)       # ids asked of me, -1 = padding
@@ -491,11 +492,13 @@ class ShardedEmbedding:
             else:
                 host, evt = fill.clone(), None
             self._pending.append((cap, host, evt))
-        local = None
+        local, call = None, 0
         if self.is_owner and self.use_hip:
             # csrc/ctr.hip a2a_serve: requested rows (padding rows zero) + every
             # slot's local row for the push (padding -> distinct negative sentinels)
-            rows, local = _ext.load().a2a_serve(self.table, req, self.n_own, rows_bf16)
+            # + the push's owner-update stamps (_owner_update)
+            slotmap, call = self._stamp_call()
+            rows, local = _ext.load().a2a_serve(self.table, req, self.n_own, rows_bf16, slotmap, call, cap, W)
         elif self.is_owner:
             rows = self._local_gather(torch.where(req >= 0, req // self.n_own, torch.zeros_like(req)))
         elif self.use_hip:  # no id is routed to a non-owner: never read
@@ -505,8 +508,18 @@ class ShardedEmbedding:
         got = self._got_buffer(W * cap, rows.dtype)
         dist.all_to_all_single(got[: W * cap], rows.contiguous(), group=self.group)
         self.exchange_bytes += W * (cap + 1) * 8 + W * cap * self.dim * rows.element_size()
-        self._ctx = ("fixed", rslot, req, count, cap, local)
+        self._ctx = ("fixed", rslot, req, count, cap, local, call)
         return got, rslot, inv
+
+    def _buf(self, name: str, shape, dtype) -> torch.Tensor:
+        """A per-step exchange buffer kept across steps (the HIP path: five fewer
+        allocations per step; reuse is ordered -- every collective that reads or
+        writes one is joined by the compute stream before the next step's writes)."""
+        bufs = self.__dict__.setdefault("_bufs", {})
+        b = bufs.get(name)
+        if b is None or b.shape != torch.Size(shape) or b.dtype != dtype:
+            b = bufs[name] = torch.empty(shape, dtype=dtype, device=self.device)
+        return b
 
     def _got_buffer(self, rows: int, dtype) -> torch.Tensor:
         """[rows + 1, dim] receive buffer of the row exchange; row ``rows`` is the
@@ -524,7 +537,7 @@ class ShardedEmbedding:
         row past the exchange for ids that did not fit."""
         rows = self.world * self._ctx[4] + (1 if dump_row else 0)
         if self.use_hip:
-            return torch.empty(rows, self.dim, device=self.device)
+            return self._buf("gsend", (rows, self.dim), torch.float32)
         return torch.zeros(rows, self.dim, device=self.device)
 
     def _push_fixed(self, grad_unique: torch.Tensor, scale: float) -> None:
@@ -537,9 +550,10 @@ class ShardedEmbedding:
     def push_send(self, gsend: torch.Tensor, scale: float) -> None:
         """Exchange a filled gradient send buffer of the last fixed pull and apply
         the owner update."""
-        _, _, req, _, cap, local = self._ctx
+        _, _, req, _, cap, local, call = self._ctx
         W, dev = self.world, self.device
-        grecv = torch.empty(W * cap, self.dim, device=dev)
+        grecv = self._buf("grecv", (W * cap, self.dim), torch.float32) if self.use_hip else \
+            torch.empty(W * cap, self.dim, device=dev)
         dist.all_to_all_single(grecv, gsend[: W * cap], group=self.group)
         self.exchange_bytes += W * cap * self.dim * 4
         if self.is_owner:
@@ -549,23 +563,31 @@ class ShardedEmbedding:
                 pad = -2 - torch.arange(req.numel(), device=dev)
                 local = torch.where(req >= 0, req // self.n_own, pad)
             if self.use_hip and self.dedup is not None:
-                self._owner_update(local, grecv, cap, scale)
+                self._owner_update(local, grecv, cap, scale, call)
             else:
                 self._apply_updates_dev(local, grecv, scale)
 
-    def _owner_update(self, local: torch.Tensor, grecv: torch.Tensor, cap: int, scale: float) -> None:
-        """Owner update without a de-duplication pass (csrc/ctr.hip a2a_owner_update):
-        each sender routes a row once, so duplicates are only across senders --
-        a per-row, per-sender slot stamp (no atomics) replaces the hash dedup +
-        CSR sort of the W * cap received slots; each row's lowest sender sums
-        the row in slot order (bitwise the segment_adagrad result)."""
-        W = self.world
+    def _stamp_call(self):
+        """(slot map, call id) of the next owner update: the map is persistent
+        (zeros), the id grows by one per pull (entries of earlier calls are stale)."""
         if getattr(self, "_slotmap", None) is None or self._calls >= (1 << 31) - 1:
-            self._slotmap = torch.zeros(self.table.shape[0] * W, dtype=torch.int64, device=self.device)
+            self._slotmap = torch.zeros(self.table.shape[0] * self.world, dtype=torch.int64, device=self.device)
             self._calls = 0
         self._calls += 1
-        _ext.load().a2a_owner_update(grecv, local, cap, W, self._slotmap, self._calls, self.table, self.accum,
-                                     self.lr, self.eps, scale)
+        return self._slotmap, self._calls
+
+    def _owner_update(self, local: torch.Tensor, grecv: torch.Tensor, cap: int, scale: float, call: int = 0) -> None:
+        """Owner update without a de-duplication pass (csrc/ctr.hip a2a_owner_update):
+        each sender routes a row once, so duplicates are only across senders --
+        a per-row, per-sender slot stamp (no atomics; written by the pull's
+        a2a_serve when ``call`` is its id) replaces the hash dedup + CSR sort of
+        the W * cap received slots; each row's lowest sender sums the row in slot
+        order (bitwise the segment_adagrad result)."""
+        stamped = call > 0
+        if not stamped:
+            _, call = self._stamp_call()
+        _ext.load().a2a_owner_update(grecv, local, cap, self.world, self._slotmap, call, self.table, self.accum,
+                                     self.lr, self.eps, scale, stamped)
 
     def _apply_updates_dev(self, ids_local: torch.Tensor, grads: torch.Tensor, scale: float) -> None:
         """Owner update with the duplicate-sum on the device (no size to the host):

@@ -751,6 +751,37 @@ def test_a2a_owner_update_matches_dedup_segment_adagrad(W, cap, nrows, D):
 
 
 @pytest.mark.gpu
+def test_a2a_serve_stamps_match_owner_update_stamps():
+    """The pull's a2a_serve stamps the owner update's slot map (stamped=True skips
+    the update's own stamp launch): bitwise the dedup + CSR + segment_adagrad
+    result, over calls whose rows repeat across senders."""
+    from kubedl_amd.models.ctr import DeviceDedup
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    W, cap, nrows, D = 4, 200, 500, 64
+    g = torch.Generator(device="cuda").manual_seed(11)
+    t1 = torch.randn(nrows, D, device="cuda", generator=g)
+    a1 = torch.rand(nrows, D, device="cuda", generator=g)
+    t2, a2 = t1.clone(), a1.clone()
+    slotmap = torch.zeros(nrows * W, dtype=torch.int64, device="cuda")
+    dd = DeviceDedup("cuda")
+    for call in range(1, 4):
+        req = []
+        for w in range(W):
+            k = int(torch.randint(0, cap + 1, (1,), generator=g, device="cuda"))
+            req.append(torch.cat([torch.randperm(nrows, device="cuda", generator=g)[:k],
+                                  torch.full((cap - k,), -1, dtype=torch.int64, device="cuda")]))
+        req = torch.cat(req)
+        _rows, local = ext.a2a_serve(t1, req, 1, False, slotmap, call, cap, W)
+        grads = torch.randn(W * cap, D, device="cuda", generator=g)
+        ext.a2a_owner_update(grads, local, cap, W, slotmap, call, t1, a1, 0.05, 1e-8, 0.5, True)
+        uniq, inv, count, seg, order = dd(local, csr=True)
+        ext.segment_adagrad(grads, order, seg, uniq, t2, a2, 0.05, 1e-8, 0.5, count)
+        torch.cuda.synchronize()
+        assert torch.equal(t1, t2) and torch.equal(a1, a2), call
+
+
+@pytest.mark.gpu
 def test_tower_train_step_matches_autograd_bitwise():
     """DenseTower.train_step (the kernels called in order, no autograd graph) gives
     bitwise the loss, input gradient and parameter gradients of loss() + backward()."""
