@@ -534,6 +534,56 @@ __global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict_
   }
 }
 
+// A tree's state reset in one launch (was eight torch fills / copies per tree):
+// rows = iota, every row at the root, empty heap arrays, the root's bounds and
+// zeroed root histogram.
+__global__ __launch_bounds__(256) void tree_init_kernel(int32_t* __restrict__ rows, int32_t* __restrict__ node_of_row,
+                                                        int N, int32_t* __restrict__ feat, int32_t* __restrict__ tbin,
+                                                        float* __restrict__ thr, float* __restrict__ val, int heap,
+                                                        int32_t* __restrict__ exists0, int32_t* __restrict__ lo0,
+                                                        int32_t* __restrict__ hi0, float* __restrict__ root,
+                                                        int root_n) {
+  const int stride = gridDim.x * 256;
+  const int t0 = blockIdx.x * 256 + threadIdx.x;
+  for (int i = t0; i < N; i += stride) {
+    rows[i] = i;
+    node_of_row[i] = 0;
+  }
+  for (int i = t0; i < heap; i += stride) {
+    feat[i] = -1;
+    tbin[i] = -1;
+    thr[i] = 0.f;
+    val[i] = 0.f;
+  }
+  for (int i = t0; i < root_n; i += stride) root[i] = 0.f;
+  if (t0 == 0) {
+    exists0[0] = 1;
+    lo0[0] = 0;
+    hi0[0] = N;
+  }
+}
+
+// pred[r * ld + k] += val[node_of_row[r]] (the tree's leaf values into the margins)
+__global__ __launch_bounds__(256) void leaf_add_kernel(float* __restrict__ pred, int ld, int k,
+                                                       const float* __restrict__ val,
+                                                       const int32_t* __restrict__ node_of_row, int N) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < N) pred[static_cast<int64_t>(r) * ld + k] += val[node_of_row[r]];
+}
+
+// [4, heap] fp32 (feature, split bin, threshold, value) of the current tree
+__global__ __launch_bounds__(256) void heap_pack_kernel(const int32_t* __restrict__ feat,
+                                                        const int32_t* __restrict__ tbin,
+                                                        const float* __restrict__ thr, const float* __restrict__ val,
+                                                        int heap, float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= heap) return;
+  out[i] = static_cast<float>(feat[i]);
+  out[heap + i] = static_cast<float>(tbin[i]);
+  out[2 * heap + i] = thr[i];
+  out[3 * heap + i] = val[i];
+}
+
 }  // namespace
 
 hipError_t gbdt_grad_hess(const float* pred, const float* y, int64_t n, int K, int obj, float* g, float* h,
@@ -688,6 +738,35 @@ hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(route_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bins, rows, row_node,
                      split_feat, split_bin, F, n, go_right);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_of_row, int N, int32_t* feat, int32_t* tbin, float* thr,
+                          float* val, int heap, int32_t* exists0, int32_t* lo0, int32_t* hi0, float* root, int root_n,
+                          hipStream_t s) {
+  if (N < 0 || heap < 0 || root_n < 0) return hipErrorInvalidValue;
+  int m = N > heap ? N : heap;
+  if (root_n > m) m = root_n;
+  int blocks = (m + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(tree_init_kernel, dim3(blocks), dim3(256), 0, s, rows, node_of_row, N, feat, tbin, thr, val, heap,
+                     exists0, lo0, hi0, root, root_n);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int32_t* node_of_row, int N,
+                         hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  if (ld < 1 || k < 0 || k >= ld) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(leaf_add_kernel, dim3((N + 255) / 256), dim3(256), 0, s, pred, ld, k, val, node_of_row, N);
+  return hipGetLastError();
+}
+
+hipError_t gbdt_heap_pack(const int32_t* feat, const int32_t* tbin, const float* thr, const float* val, int heap,
+                          float* out, hipStream_t s) {
+  if (heap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(heap_pack_kernel, dim3((heap + 255) / 256), dim3(256), 0, s, feat, tbin, thr, val, heap, out);
   return hipGetLastError();
 }
 

@@ -115,17 +115,11 @@ class GbdtGrower {
     const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
     grad_ = grad;
     hess_ = hess;
-    rows_.copy_(iota_);
-    node_of_row_.zero_();
-    feat_.fill_(-1);
-    tbin_.fill_(-1);
-    thr_.zero_();
-    val_.zero_();
-    exists_[0].fill_(1);
-    lo_[0].zero_();
-    hi_[0].fill_(N_);
     auto root = hist_cur_.narrow(0, 0, 1);
-    root.zero_();
+    ck(kdl::gbdt_tree_init(ip(rows_), ip(node_of_row_), N_, ip(feat_), ip(tbin_), fp(thr_), fp(val_),
+                           static_cast<int>(feat_.numel()), ip(exists_[0]), ip(lo_[0]), ip(hi_[0]), fp(root),
+                           static_cast<int>(root.numel()), stream()),
+       "gbdt_tree_init");
     // the tree's fixed-point scale of the quantised histogram sums (csrc/gbdt.hip)
     ck(kdl::gbdt_gh_absmax(fp(grad_), fp(hess_), N_, fp(gh_max_), stream()), "gbdt_gh_absmax");
     const int max_chunks = (N_ + rpb_ - 1) / rpb_ + 1;
@@ -211,6 +205,25 @@ class GbdtGrower {
   }
 
   at::Tensor node_of_row() const { return node_of_row_; }
+  // pred[:, k] += leaf value of each row (pred [N, K] fp32 contiguous)
+  void add_leaf(at::Tensor pred, int64_t k) {
+    TORCH_CHECK(pred.is_cuda() && pred.scalar_type() == at::kFloat && pred.is_contiguous() && pred.dim() == 2 &&
+                    pred.size(0) == N_ && k >= 0 && k < pred.size(1),
+                "GbdtGrower.add_leaf: pred [N, K] fp32 contiguous, 0 <= k < K");
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
+    ck(kdl::gbdt_leaf_add(fp(pred), static_cast<int>(pred.size(1)), static_cast<int>(k), fp(val_), ip(node_of_row_),
+                          N_, stream()),
+       "gbdt_leaf_add");
+  }
+  // the current tree's heap arrays as one [4, heap] fp32 tensor (feature, split bin, threshold, value)
+  at::Tensor heap_packed() const {
+    const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
+    const int64_t heap = feat_.numel();
+    auto out = at::empty({4, heap}, thr_.options());
+    ck(kdl::gbdt_heap_pack(ip(feat_), ip(tbin_), fp(thr_), fp(val_), static_cast<int>(heap), fp(out), stream()),
+       "gbdt_heap_pack");
+    return out;
+  }
   // (feature, split_bin, threshold, value) heap arrays of the current tree
   std::vector<at::Tensor> tree() const { return {feat_, tbin_, thr_, val_}; }
   std::vector<int64_t> stats() const { return {builds_, subtracted_}; }
@@ -255,6 +268,8 @@ void register_gbdt(pybind11::module& m) {
       .def("level_c", &GbdtGrower::level_c)
       .def("grow_local", &GbdtGrower::grow_local)
       .def("node_of_row", &GbdtGrower::node_of_row)
+      .def("add_leaf", &GbdtGrower::add_leaf)
+      .def("heap_packed", &GbdtGrower::heap_packed)
       .def("tree", &GbdtGrower::tree)
       .def("stats", &GbdtGrower::stats)
       .def("rows_per_chunk", &GbdtGrower::rows_per_chunk);

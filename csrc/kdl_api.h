@@ -157,6 +157,16 @@ hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float
 // gh_max: {max |g|, max h} of the rows (gbdt_gh_absmax): the fixed-point scale
 // of the quantised per-block sums
 hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* out, hipStream_t s);
+// a tree's state reset (rows = iota, node_of_row = 0, heap arrays -1 / 0, root bounds, root histogram)
+hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_of_row, int N, int32_t* feat, int32_t* tbin, float* thr,
+                          float* val, int heap, int32_t* exists0, int32_t* lo0, int32_t* hi0, float* root, int root_n,
+                          hipStream_t s);
+// pred[r * ld + k] += val[node_of_row[r]]
+hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int32_t* node_of_row, int N,
+                         hipStream_t s);
+// out [4, heap] fp32 = (feat, tbin, thr, val)
+hipError_t gbdt_heap_pack(const int32_t* feat, const int32_t* tbin, const float* thr, const float* val, int heap,
+                          float* out, hipStream_t s);
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
                         int max_chunks, int rpb, int F, int B, const float* gh_max, float* hist, hipStream_t s);

@@ -146,6 +146,30 @@ class HistGBDT:
         w = (pos - lo.double()).float()
         self.cuts = (srt[:, lo] * (1 - w) + srt[:, hi] * w).contiguous()  # [F, B-1]
 
+    def host_cuts(self, X: torch.Tensor, sample: int = 65536, seed: int = 0) -> torch.Tensor:
+        """``fit_cuts`` on a host copy of X, bitwise the same cuts: the same
+        systematic sample, the same order statistics (``numpy.partition`` puts each
+        needed rank exactly where a full sort would), the same float32 lerp.  On a
+        fresh GPU process the device version's first calls load torch's sort and
+        elementwise code objects (0.1-0.6 s, ``scripts/cuts_probe.py``); this one
+        loads nothing and runs beside the host->device copy (``fit``)."""
+        import numpy as np
+        B = self.p.max_bin
+        n = X.shape[0]
+        k = min(sample, n)
+        off = (seed * 7919 + 17) % max(n // k, 1)
+        idx = np.minimum((np.arange(k, dtype=np.int64) * n) // k + off, n - 1)
+        samp = np.ascontiguousarray(X.numpy()[idx].astype(np.float32, copy=False))  # [k, F]
+        q = torch.linspace(0, 1, B + 1, dtype=torch.float64)[1:-1]
+        pos = q * (k - 1)
+        lo, hi = pos.floor().long(), pos.ceil().long()
+        w = (pos - lo.double()).float()
+        kth = np.unique(np.concatenate([lo.numpy(), hi.numpy()]))
+        part = np.partition(samp, kth, axis=0)
+        a = torch.from_numpy(np.ascontiguousarray(part[lo.numpy()].T))  # [F, B-1]
+        b = torch.from_numpy(np.ascontiguousarray(part[hi.numpy()].T))
+        return (a * (1 - w) + b * w).contiguous()
+
     def quantise(self, X: torch.Tensor) -> torch.Tensor:
         if self.use_hip and X.is_cuda:
             return _ext.load().gbdt_quantise(X, self.cuts, self.p.max_bin)
@@ -338,7 +362,8 @@ class HistGBDT:
                                       p.learning_rate, p.min_child_weight)
 
     def _grow_device(self, gr, g, h):
-        """One tree on the GPU; returns (heap arrays, per-row leaf value)."""
+        """One tree on the GPU; returns its [4, heap] arrays (feature, split bin,
+        threshold, value)."""
         D = self.p.max_depth
         if _world() == 1:
             gr.grow_local(g, h)
@@ -350,8 +375,7 @@ class HistGBDT:
                     _allreduce_(cnt)                    # global child counts -> same smaller child on all ranks
                     _allreduce_(gr.level_b(d, True))    # the built children's histograms
                     gr.level_c(d)
-        feat, tbin, thr, val = gr.tree()
-        return torch.stack([feat.float(), tbin.float(), thr, val]), val[gr.node_of_row().long()]
+        return gr.heap_packed()  # [4, heap] in one launch (the leaf values go in by add_leaf)
 
     @staticmethod
     def _heap_tree(arr) -> Tree:
@@ -376,10 +400,30 @@ class HistGBDT:
         grower's workspaces; ``stats['boost_s']``: the boosting rounds alone (one
         synchronisation at each end, none inside)."""
         t0 = self._sync_time()
+        host_cuts = {}
+        th = None
+        if (self.cuts is None and X.device.type == "cpu" and self.device.type == "cuda" and _world() == 1
+                and X.dim() == 2 and X.dtype in (torch.float32, torch.float64)):
+            # the cuts from the host copy, beside the host->device copy (numpy and
+            # the copy release the GIL)
+            import threading
+
+            def run():
+                try:
+                    host_cuts["c"] = self.host_cuts(X)
+                except BaseException as e:  # re-raised below
+                    host_cuts["e"] = e
+            th = threading.Thread(target=run, name="gbdt-cuts", daemon=True)
+            th.start()
         X = X.to(self.device)
         y = y.to(self.device)
         ta = self._sync_time()
-        if self.cuts is None:
+        if th is not None:
+            th.join()
+            if "e" in host_cuts:
+                raise host_cuts["e"]
+            self.cuts = host_cuts["c"].to(self.device)
+        elif self.cuts is None:
             self.fit_cuts(X)
         tb = self._sync_time()
         bins = self.quantise(X).contiguous()
@@ -400,9 +444,8 @@ class HistGBDT:
                 g = g_all[:, k].contiguous()
                 h = h_all[:, k].contiguous()
                 if grower is not None:
-                    arr, leaf_val = self._grow_device(grower, g, h)
-                    pred[:, k] += leaf_val
-                    round_trees.append(arr)
+                    round_trees.append(self._grow_device(grower, g, h))
+                    grower.add_leaf(pred, k)  # pred[:, k] += the rows' leaf values, one launch
                     continue
                 tree, leaf = self._grow(bins, g, h, n)
                 vals = torch.tensor(tree.value, dtype=torch.float32, device=self.device)

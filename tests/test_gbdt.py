@@ -239,3 +239,16 @@ def test_gpu_grad_hess_kernel_matches_torch(objective, K):
     g_ref, h_ref = m._grad_hess(pred, y)
     torch.testing.assert_close(g, g_ref, atol=1e-6, rtol=1e-5)
     torch.testing.assert_close(h, h_ref, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("n,F,B", [(200000, 28, 256), (1000, 5, 16), (70000, 3, 64)])
+def test_host_cuts_bitwise_equal_fit_cuts(n, F, B):
+    """HistGBDT.host_cuts (numpy partition on the host copy, run beside the
+    host->device copy) gives bitwise the cuts of fit_cuts (sort + lerp)."""
+    from kubedl_amd.models.gbdt import GBDTParams, HistGBDT
+    g = torch.Generator().manual_seed(n)
+    X = torch.randn(n, F, generator=g)
+    X[::97, 0] = 0.0  # ties
+    m = HistGBDT(GBDTParams(max_bin=B), device="cpu")
+    m.fit_cuts(X)
+    assert torch.equal(m.cuts, m.host_cuts(X))
