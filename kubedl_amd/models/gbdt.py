@@ -159,7 +159,7 @@ class HistGBDT:
         k = min(sample, n)
         off = (seed * 7919 + 17) % max(n // k, 1)
         idx = np.minimum((np.arange(k, dtype=np.int64) * n) // k + off, n - 1)
-        samp = np.ascontiguousarray(X.numpy()[idx].astype(np.float32, copy=False))  # [k, F]
+        samp = np.ascontiguousarray(X.detach().numpy()[idx].astype(np.float32, copy=False))  # [k, F]
         q = torch.linspace(0, 1, B + 1, dtype=torch.float64)[1:-1]
         pos = q * (k - 1)
         lo, hi = pos.floor().long(), pos.ceil().long()
