@@ -1032,9 +1032,14 @@ __device__ __forceinline__ uint32_t hash64(uint64_t x) {
 
 __global__ __launch_bounds__(256) void dedup_insert_kernel(const int64_t* __restrict__ ids, int n,
                                                            unsigned long long* __restrict__ keys, uint32_t mask,
-                                                           int* __restrict__ slot_of) {
+                                                           int* __restrict__ slot_of, int* __restrict__ sizes) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
+  // the segment sizes counted by dedup_inverse_kernel (a later launch) start
+  // at zero: cleared here rather than by a runtime memset, so a captured
+  // step holds kernel nodes only (docs/perf_notes.md, the CTR hipGraph fault)
+  sizes[i] = 0;
+  if (i == 0) sizes[n] = 0;
   const unsigned long long id = static_cast<unsigned long long>(ids[i]);
   uint32_t h = hash64(id) & mask;
   // T >= 2n: at most n keys, so a free or matching slot exists within T probes
@@ -1456,10 +1461,9 @@ int dedup_table_slots(int n) {
 hipError_t dedup_ids(const int64_t* ids, int n, void* keys, int T, int* slot_of, int* slot_uid, int* bsum,
                      int64_t* uniq, int64_t* inv, int* count, int* sizes, hipStream_t s) {
   if (n <= 0 || T < 2 * n || (T & (T - 1)) || T % kChunk) return hipErrorInvalidValue;
-  RETURN_IF_HIP_ERR(hipMemsetAsync(sizes, 0, static_cast<size_t>(n + 1) * sizeof(int), s));
   auto* k = static_cast<unsigned long long*>(keys);
   hipLaunchKernelGGL(dedup_insert_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ids, n, k,
-                     static_cast<uint32_t>(T - 1), slot_of);
+                     static_cast<uint32_t>(T - 1), slot_of, sizes);
   const int nb = T / kChunk;
   hipLaunchKernelGGL(chunk_count_kernel, dim3(nb), dim3(256), 0, s, k, static_cast<const int*>(nullptr), T, 0, bsum);
   hipLaunchKernelGGL(dedup_assign_kernel, dim3(nb), dim3(256), 0, s, k, T, bsum, slot_uid, uniq, count);

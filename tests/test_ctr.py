@@ -477,6 +477,35 @@ def test_fused_pull_builds_the_same_input():
     assert torch.equal(x1, ref)
 
 
+def test_ctr_launchers_issue_kernels_only():
+    """The CTR step's native launchers enqueue kernels only: a captured step with
+    a memset node faulted under back-to-back hipGraph replays (the node is not
+    held behind the previous launch's kernels; docs/perf_notes.md, Round 5)."""
+    src = open(os.path.join(os.path.dirname(__file__), "..", "csrc", "ctr.hip")).read()
+    for call in ("hipMemsetAsync", "hipMemcpyAsync", "hipMemset(", "hipMemcpy("):
+        assert call not in src, f"csrc/ctr.hip issues {call}: clear / copy inside a kernel instead"
+
+
+@pytest.mark.gpu
+def test_ctr_step_graph_replay_matches_eager():
+    """The world-1 CTR step captured with torch.cuda.graph replays bitwise equal
+    to the same step run eagerly (losses, embedding table, parameters), with a
+    host sync after every replay (scripts/ctr_graph_probe.py, stage ``fused``)."""
+    import argparse
+    import importlib.util
+    path = os.path.join(os.path.dirname(__file__), "..", "scripts", "ctr_graph_probe.py")
+    spec = importlib.util.spec_from_file_location("ctr_graph_probe", path)
+    probe = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(probe)
+    args = argparse.Namespace(batch=512, fields=8, vocab=3000, dim=32, dense=16, hidden=(256, 128))
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev).manual_seed(5)
+    w_true = (torch.randn(4096, generator=torch.Generator().manual_seed(7)) * 0.5).to(dev)
+    from kubedl_amd.workers.xdl_ctr import synth_batch
+    batches = [synth_batch(args.batch, args.fields, args.vocab, args.dense, gen, w_true) for _ in range(8)]
+    assert probe.stage_step(dev, args, batches, 4, autograd=False, ring=False)
+
+
 @pytest.mark.gpu
 def test_ctr_worker_trains_on_gpu():
     from kubedl_amd.workers.xdl_ctr import main
