@@ -422,8 +422,8 @@ __device__ __forceinline__ void ld4(const T* p, int n, float (&o)[4]) {
 // rows + b*ld + col0 + f*D (the layout embed_gather wrote).  Rows order[j]
 // are summed per segment [seg[u], seg[u+1]), in j order, by a group of G =
 // 2^lg lanes (G*4 >= D when D <= 256: a wave per segment left 48 of 64 lanes
-// idle at D = 64), two rows' loads in flight per step.  (Four segments per
-// group in lock step measured slower: 63 vs 33 us at batch 4096.)
+// idle at D = 64), kSegFly rows' loads in flight per step on long segments.
+// (Four segments per group in lock step measured slower: 63 vs 33 us at batch 4096.)
 // j / F as umulhi(j, mF), mF = ceil(2^32 / F): exact while j * F < 2^32 (host
 // check; mF = 0 selects the 64-bit division) -- no 64-bit division sequence per row.
 // ``ucount`` (optional): the live segment count on the device (U is then the
@@ -444,6 +444,8 @@ __device__ __forceinline__ void seg_row(const T* rows, int64_t jj, uint32_t F, u
   ld4<T, V4>(rows + bi * ld + col0 + f * D + c, n, v);
 }
 
+constexpr int kSegFly = 8;  // rows in flight per lane group on a long segment
+
 template <typename T, bool V4>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, uint32_t mF, int ld,
                                                              int col0, const int64_t* __restrict__ order,
@@ -462,6 +464,21 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict
     const int n = D - c < 4 ? D - c : 4;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     int64_t j = s0;
+    // hot ids: a long segment is a serial chain (index load -> row load ->
+    // add), and the longest one sets the launch's time -- keep kSegFly rows'
+    // loads in flight, then add them in j order (the same sums, bit for bit)
+    for (; j + kSegFly <= s1; j += kSegFly) {
+      int64_t jj[kSegFly];
+      float v[kSegFly][4];
+#pragma unroll
+      for (int r = 0; r < kSegFly; ++r) jj[r] = order[j + r];
+#pragma unroll
+      for (int r = 0; r < kSegFly; ++r) seg_row<T, V4>(rows, jj[r], F, mF, ld, col0, D, c, n, v[r]);
+#pragma unroll
+      for (int r = 0; r < kSegFly; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += v[r][k];
+    }
     for (; j + 1 < s1; j += 2) {
       const int64_t j0 = order[j], j1 = order[j + 1];
       float v0[4], v1[4];
