@@ -693,6 +693,34 @@ at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64
   return out;
 }
 
+// sync-free one-owner push in one launch: the per-id gradient sums of rows
+// (segment_reduce) applied by Adagrad to table/accum rows rows_local[u]
+void segment_reduce_adagrad(const at::Tensor& rows, int64_t F, int64_t col0, int64_t D, const at::Tensor& order,
+                            const at::Tensor& seg, const c10::optional<at::Tensor>& ucount, const at::Tensor& rows_local,
+                            at::Tensor table, at::Tensor accum, double lr, double eps, double scale) {
+  TORCH_CHECK(rows.is_cuda() && rows.dim() == 2 && rows.stride(1) == 1, "segment_reduce_adagrad: rows [B, ld]");
+  TORCH_CHECK(order.scalar_type() == at::kLong && seg.scalar_type() == at::kLong && order.is_contiguous() &&
+                  seg.is_contiguous(),
+              "segment_reduce_adagrad: int64 order/seg");
+  TORCH_CHECK(order.numel() == rows.size(0) * F && col0 + F * D <= rows.size(1), "segment_reduce_adagrad: shapes");
+  const int64_t U = seg.numel() - 1;
+  TORCH_CHECK(rows_local.scalar_type() == at::kLong && rows_local.is_contiguous() && rows_local.numel() >= U,
+              "segment_reduce_adagrad: int64 rows_local [U]");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kFloat && table.is_contiguous() && table.dim() == 2 &&
+                  table.size(1) == D && accum.sizes() == table.sizes() && accum.scalar_type() == at::kFloat &&
+                  accum.is_contiguous(),
+              "segment_reduce_adagrad: fp32 table / accum [rows, D]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(rows.device());
+  check_hip(kdl::segment_reduce_adagrad(rows.data_ptr(), dtype_code(rows), static_cast<int>(F),
+                                        static_cast<int>(rows.stride(0)), static_cast<int>(col0),
+                                        order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(), static_cast<int>(U),
+                                        static_cast<int>(D), opt_count(ucount), order.numel(),
+                                        rows_local.data_ptr<int64_t>(), table.size(0), table.data_ptr<float>(),
+                                        accum.data_ptr<float>(), static_cast<float>(lr), static_cast<float>(eps),
+                                        static_cast<float>(scale), cur_stream()),
+            "segment_reduce_adagrad");
+}
+
 // Fixed-capacity exchange routing (csrc/ctr.hip a2a_route): send [W * (cap + 1)]
 // int64 and rslot [n] int64 are written; count: int32 [1] live ids (or None = n)
 void a2a_route(const at::Tensor& uniq, const c10::optional<at::Tensor>& count, const at::Tensor& owner_rank,
@@ -1705,6 +1733,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_gather_cast", &embed_gather_cast, "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input");
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("dedup_table_slots", &dedup_table_slots, "hash-table slots dedup_csr needs for n ids");
+  m.def("segment_reduce_adagrad", &segment_reduce_adagrad,
+        "one-owner sync-free push: per-id gradient sums (segment_reduce) applied by Adagrad in the same launch");
   m.def("csr_from_inverse_only", &csr_from_inverse_only, "CSR (seg, order) of a dedup_csr inverse, positions ascending per id");
   m.def("dedup_csr", &dedup_csr, "sync-free id de-duplication (uniq/inv/count on the device) + optional CSR of the inverse");
   m.def("conv1x1_gemm", &conv1x1_gemm, "1x1 conv / dgrad as MFMA GEMM with fused BN prologue/epilogue");

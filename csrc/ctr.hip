@@ -446,6 +446,44 @@ __device__ __forceinline__ void seg_row(const T* rows, int64_t jj, uint32_t F, u
 
 constexpr int kSegFly = 8;  // rows in flight per lane group on a long segment
 
+// Sum of the rows order[s0 .. s1) of one segment, columns [c, c + n), in j
+// order.  Hot ids: a long segment is a serial chain (index load -> row load ->
+// add), and the longest one sets the launch's time -- keep kSegFly rows' loads
+// in flight, then add them in j order (the same sums, bit for bit).
+template <typename T, bool V4>
+__device__ __forceinline__ void seg_sum(const T* rows, const int64_t* order, int64_t s0, int64_t s1, uint32_t F,
+                                        uint32_t mF, int ld, int col0, int D, int c, int n, float (&a)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a[k] = 0.f;
+  int64_t j = s0;
+  for (; j + kSegFly <= s1; j += kSegFly) {
+    int64_t jj[kSegFly];
+    float v[kSegFly][4];
+#pragma unroll
+    for (int r = 0; r < kSegFly; ++r) jj[r] = order[j + r];
+#pragma unroll
+    for (int r = 0; r < kSegFly; ++r) seg_row<T, V4>(rows, jj[r], F, mF, ld, col0, D, c, n, v[r]);
+#pragma unroll
+    for (int r = 0; r < kSegFly; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += v[r][k];
+  }
+  for (; j + 1 < s1; j += 2) {
+    const int64_t j0 = order[j], j1 = order[j + 1];
+    float v0[4], v1[4];
+    seg_row<T, V4>(rows, j0, F, mF, ld, col0, D, c, n, v0);
+    seg_row<T, V4>(rows, j1, F, mF, ld, col0, D, c, n, v1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = (a[k] + v0[k]) + v1[k];
+  }
+  if (j < s1) {
+    float v0[4];
+    seg_row<T, V4>(rows, order[j], F, mF, ld, col0, D, c, n, v0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += v0[k];
+  }
+}
+
 template <typename T, bool V4>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ rows, int F, uint32_t mF, int ld,
                                                              int col0, const int64_t* __restrict__ order,
@@ -462,42 +500,56 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict
   const int64_t s0 = seg[u], s1 = seg[u + 1];
   for (int c = gl * 4; c < D; c += 4 << lg) {
     const int n = D - c < 4 ? D - c : 4;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    int64_t j = s0;
-    // hot ids: a long segment is a serial chain (index load -> row load ->
-    // add), and the longest one sets the launch's time -- keep kSegFly rows'
-    // loads in flight, then add them in j order (the same sums, bit for bit)
-    for (; j + kSegFly <= s1; j += kSegFly) {
-      int64_t jj[kSegFly];
-      float v[kSegFly][4];
-#pragma unroll
-      for (int r = 0; r < kSegFly; ++r) jj[r] = order[j + r];
-#pragma unroll
-      for (int r = 0; r < kSegFly; ++r) seg_row<T, V4>(rows, jj[r], F, mF, ld, col0, D, c, n, v[r]);
-#pragma unroll
-      for (int r = 0; r < kSegFly; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) a[k] += v[r][k];
-    }
-    for (; j + 1 < s1; j += 2) {
-      const int64_t j0 = order[j], j1 = order[j + 1];
-      float v0[4], v1[4];
-      seg_row<T, V4>(rows, j0, F, mF, ld, col0, D, c, n, v0);
-      seg_row<T, V4>(rows, j1, F, mF, ld, col0, D, c, n, v1);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = (a[k] + v0[k]) + v1[k];
-    }
-    if (j < s1) {
-      float v0[4];
-      seg_row<T, V4>(rows, order[j], F, mF, ld, col0, D, c, n, v0);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] += v0[k];
-    }
+    float a[4];
+    seg_sum<T, V4>(rows, order, s0, s1, F, mF, ld, col0, D, c, n, a);
     float* o = out + orow * D + c;
     if (V4) {
       *reinterpret_cast<float4*>(o) = make_float4(a[0], a[1], a[2], a[3]);
     } else {
       for (int k = 0; k < n; ++k) o[k] = a[k];
+    }
+  }
+}
+
+// One owner, sync-free push (world 1): segment u's summed gradient is applied
+// straight to table row rows_local[u] -- segment_reduce_kernel followed by a
+// one-row-per-segment segment_adagrad_kernel, without the [U, D] fp32 rows
+// between them (written once, read once) or the second launch.  Same
+// arithmetic in the same order: bitwise those two launches.
+template <typename T, bool V4>
+__global__ __launch_bounds__(256) void segment_reduce_adagrad_kernel(
+    const T* __restrict__ rows, int F, uint32_t mF, int ld, int col0, const int64_t* __restrict__ order,
+    const int64_t* __restrict__ seg, int U, int D, int lg, const int* __restrict__ ucount,
+    const int64_t* __restrict__ rows_local, int64_t nrows, float* __restrict__ table, float* __restrict__ accum,
+    float lr, float eps, float scale) {
+  const int u = (blockIdx.x * 256 + threadIdx.x) >> lg;
+  const int gl = threadIdx.x & ((1 << lg) - 1);
+  if (u >= (ucount ? *ucount : U)) return;
+  const int64_t row = rows_local[u];
+  if (row < 0 || row >= nrows) return;
+  const int64_t s0 = seg[u], s1 = seg[u + 1];
+  float* w = table + row * static_cast<int64_t>(D);
+  float* ac = accum + row * static_cast<int64_t>(D);
+  for (int c = gl * 4; c < D; c += 4 << lg) {
+    const int n = D - c < 4 ? D - c : 4;
+    float wv[4], av[4], a[4];
+    ld4<float, V4>(w + c, n, wv);  // issued before the gradient rows
+    ld4<float, V4>(ac + c, n, av);
+    seg_sum<T, V4>(rows, order, s0, s1, F, mF, ld, col0, D, c, n, a);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = (0.f + a[k]) * scale;  // segment_adagrad's one-row sum: 0 + g
+      av[k] += gk * gk;
+      wv[k] -= lr * gk / (sqrtf(av[k]) + eps);
+    }
+    if (V4) {
+      *reinterpret_cast<float4*>(ac + c) = make_float4(av[0], av[1], av[2], av[3]);
+      *reinterpret_cast<float4*>(w + c) = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    } else {
+      for (int k = 0; k < n; ++k) {
+        ac[c + k] = av[k];
+        w[c + k] = wv[k];
+      }
     }
   }
 }
@@ -973,6 +1025,32 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
     else CTR_LAUNCH_SEGRED(float, false);
   }
 #undef CTR_LAUNCH_SEGRED
+  return hipGetLastError();
+}
+
+hipError_t segment_reduce_adagrad(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
+                                  const int64_t* seg, int U, int D, const int* ucount, int64_t nrows_in,
+                                  const int64_t* rows_local, int64_t nrows, float* table, float* accum, float lr,
+                                  float eps, float scale, hipStream_t s) {
+  if (U <= 0 || nrows_in <= 0) return hipSuccess;
+  const int lg = seg_lanes_log2(D);
+  dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(U) << lg) + 255) / 256));
+  const size_t esz = dtype == 1 ? 2 : 4;
+  const bool v4 = D % 4 == 0 && ld % 4 == 0 && col0 % 4 == 0 && reinterpret_cast<uintptr_t>(rows) % (4 * esz) == 0 &&
+                  reinterpret_cast<uintptr_t>(table) % 16 == 0 && reinterpret_cast<uintptr_t>(accum) % 16 == 0;
+  const bool fast = static_cast<uint64_t>(nrows_in) * static_cast<uint64_t>(F) < (uint64_t(1) << 32);
+  const uint32_t mF = fast ? static_cast<uint32_t>(((uint64_t(1) << 32) + F - 1) / F) : 0u;
+#define CTR_LAUNCH_SRA(T, V)                                                                                       \
+  hipLaunchKernelGGL((segment_reduce_adagrad_kernel<T, V>), grid, dim3(256), 0, s, static_cast<const T*>(rows), F, \
+                     mF, ld, col0, order, seg, U, D, lg, ucount, rows_local, nrows, table, accum, lr, eps, scale)
+  if (dtype == 1) {
+    if (v4) CTR_LAUNCH_SRA(bf16_t, true);
+    else CTR_LAUNCH_SRA(bf16_t, false);
+  } else {
+    if (v4) CTR_LAUNCH_SRA(float, true);
+    else CTR_LAUNCH_SRA(float, false);
+  }
+#undef CTR_LAUNCH_SRA
   return hipGetLastError();
 }
 

@@ -224,6 +224,12 @@ hipError_t segment_reduce(const void* rows, int dtype, int F, int ld, int col0, 
                           const int64_t* seg, int U, int D, float* out, hipStream_t s, const int* ucount,
                           int64_t nrows,  // nrows = order's length (B * F)
                           const int64_t* out_row = nullptr, int64_t out_lim = 0);  // out row of segment u (< out_lim)
+// segment_reduce + a one-row-per-segment segment_adagrad in one launch: segment
+// u's sum updates table/accum row rows_local[u] (rows outside [0, nrows) skipped)
+hipError_t segment_reduce_adagrad(const void* rows, int dtype, int F, int ld, int col0, const int64_t* order,
+                                  const int64_t* seg, int U, int D, const int* ucount, int64_t nrows_in,
+                                  const int64_t* rows_local, int64_t nrows, float* table, float* accum, float lr,
+                                  float eps, float scale, hipStream_t s);
 // Fixed-capacity embedding exchange (models/ctr.py _pull_fixed / _push_fixed):
 // route n unique ids (first *count live) to W destination blocks of cap + 1
 // slots (send [W * (cap + 1)]: ids, -1 padding, header = the largest fill) and

@@ -687,6 +687,22 @@ class ShardedEmbedding:
         if self.is_owner:
             self._apply_updates(req // self.n_own, g_recv, scale)
 
+    def push_rows(self, rows: torch.Tensor, F: int, col0: int, order: torch.Tensor, seg: torch.Tensor,
+                  scale: float = 1.0) -> bool:
+        """Sync-free one-owner push straight from the activation-gradient rows
+        (row j = b*F + f at ``rows[b, col0 + f*dim:]``): each unique id's rows
+        order[seg[u]:seg[u+1]] are summed and applied by Adagrad in one launch
+        (csrc/ctr.hip ``segment_reduce_adagrad``: bitwise ``segment_reduce`` +
+        ``push``, without the [U, dim] fp32 sums between them).  Returns False
+        when the last pull was not the sync-free kind (then use ``push``)."""
+        ctx = self._ctx
+        if ctx is None or not isinstance(ctx[0], str) or ctx[0] != "dev" or not self.use_hip:
+            return False
+        _, uniq, count = ctx
+        _ext.load().segment_reduce_adagrad(rows, F, col0, self.dim, order, seg, count, uniq, self.table, self.accum,
+                                           self.lr, self.eps, scale)
+        return True
+
     def participate(self) -> None:
         """An owner without a batch of its own (PS rank) serves one pull+push round."""
         empty = torch.empty(0, dtype=torch.int64, device=self.device)
@@ -759,6 +775,8 @@ class CTRModel:
                 gsend = self.emb.fixed_send_buffer()
                 _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg, count, ctx[1], gsend)
                 self.emb.push_send(gsend, scale)
+                return
+            if kind == "dev" and self.emb.push_rows(xgrad, self.F, 0, order, seg, scale):
                 return
             g_u = _ext.load().segment_reduce(xgrad, self.F, 0, self.D, order, seg, count)
             self.emb.push(g_u, scale)

@@ -477,6 +477,34 @@ def test_fused_pull_builds_the_same_input():
     assert torch.equal(x1, ref)
 
 
+@pytest.mark.gpu
+def test_segment_reduce_adagrad_matches_two_launches():
+    """The one-launch sync-free push (segment sums applied by Adagrad) updates
+    table and accumulator bitwise like segment_reduce + push, hot ids included
+    (segments longer than the kernel's rows in flight)."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(3)
+    B, F, D, V = 512, 8, 64, 3000
+    ids = (V * torch.rand(B * F, generator=g, device=dev).pow(3)).long().clamp_(max=V - 1)
+    ids[::5] = 7  # one id with ~800 positions
+    rows = torch.randn(B, F * D + 16, generator=g, device=dev).to(torch.bfloat16)
+    tables = []
+    for fused in (False, True):
+        emb = ShardedEmbedding(V, D, [0], 0, 1, dev, lr=0.05)
+        for step in range(3):
+            uniq, inv, count, seg, order = emb.dedup(ids, csr=True)
+            emb._ctx = ("dev", uniq, count)
+            if fused:
+                assert emb.push_rows(rows, F, 0, order, seg, 0.5)
+            else:
+                emb.push(ext.segment_reduce(rows, F, 0, D, order, seg, count), 0.5)
+        tables.append((emb.table.clone(), emb.accum.clone()))
+    assert torch.equal(tables[0][0], tables[1][0]) and torch.equal(tables[0][1], tables[1][1])
+    assert not torch.equal(tables[0][0], ShardedEmbedding(V, D, [0], 0, 1, dev, lr=0.05).table)
+
+
 def test_ctr_launchers_issue_kernels_only():
     """The CTR step's native launchers enqueue kernels only: a captured step with
     a memset node faulted under back-to-back hipGraph replays (the node is not
