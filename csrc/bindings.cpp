@@ -664,8 +664,8 @@ at::Tensor segment_reduce(const at::Tensor& rows, int64_t F, int64_t col0, int64
                           const c10::optional<at::Tensor>& out_rows, const c10::optional<at::Tensor>& out_opt) {
   TORCH_CHECK(rows.is_cuda() && rows.dim() == 2 && rows.stride(1) == 1, "segment_reduce: rows [B, ld]");
   TORCH_CHECK(order.scalar_type() == at::kLong && seg.scalar_type() == at::kLong && order.is_contiguous() &&
-                  seg.is_contiguous(),
-              "segment_reduce: int64 order/seg");
+                  seg.is_contiguous() && order.device() == rows.device() && seg.device() == rows.device(),
+              "segment_reduce: int64 order/seg on rows' device");
   TORCH_CHECK(order.numel() == rows.size(0) * F && col0 + F * D <= rows.size(1), "segment_reduce: shapes");
   const int64_t U = seg.numel() - 1;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(rows.device());
@@ -700,13 +700,14 @@ void segment_reduce_adagrad(const at::Tensor& rows, int64_t F, int64_t col0, int
                             at::Tensor table, at::Tensor accum, double lr, double eps, double scale) {
   TORCH_CHECK(rows.is_cuda() && rows.dim() == 2 && rows.stride(1) == 1, "segment_reduce_adagrad: rows [B, ld]");
   TORCH_CHECK(order.scalar_type() == at::kLong && seg.scalar_type() == at::kLong && order.is_contiguous() &&
-                  seg.is_contiguous(),
-              "segment_reduce_adagrad: int64 order/seg");
+                  seg.is_contiguous() && order.device() == rows.device() && seg.device() == rows.device(),
+              "segment_reduce_adagrad: int64 order/seg on rows' device");
   TORCH_CHECK(order.numel() == rows.size(0) * F && col0 + F * D <= rows.size(1), "segment_reduce_adagrad: shapes");
   const int64_t U = seg.numel() - 1;
-  TORCH_CHECK(rows_local.scalar_type() == at::kLong && rows_local.is_contiguous() && rows_local.numel() >= U,
-              "segment_reduce_adagrad: int64 rows_local [U]");
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kFloat && table.is_contiguous() && table.dim() == 2 &&
+  TORCH_CHECK(rows_local.scalar_type() == at::kLong && rows_local.is_contiguous() && rows_local.numel() >= U &&
+                  rows_local.device() == rows.device(),
+              "segment_reduce_adagrad: int64 rows_local [U] on rows' device");
+  TORCH_CHECK(table.device() == rows.device() && accum.device() == rows.device() && table.scalar_type() == at::kFloat && table.is_contiguous() && table.dim() == 2 &&
                   table.size(1) == D && accum.sizes() == table.sizes() && accum.scalar_type() == at::kFloat &&
                   accum.is_contiguous(),
               "segment_reduce_adagrad: fp32 table / accum [rows, D]");
