@@ -444,7 +444,7 @@ __device__ __forceinline__ void seg_row(const T* rows, int64_t jj, uint32_t F, u
   ld4<T, V4>(rows + bi * ld + col0 + f * D + c, n, v);
 }
 
-constexpr int kSegFly = 8;  // rows in flight per lane group on a long segment
+constexpr int kSegFly = 8;  // rows in flight per lane group on a long segment (16: 39.9 vs 34.5 us)
 
 // Sum of the rows order[s0 .. s1) of one segment, columns [c, c + n), in j
 // order.  Hot ids: a long segment is a serial chain (index load -> row load ->
