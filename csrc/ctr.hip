@@ -1496,12 +1496,15 @@ __global__ __launch_bounds__(256) void a2a_serve_kernel(const float* __restrict_
   const int gl = threadIdx.x & ((1 << lg) - 1);
   if (r >= n) return;
   const int64_t id = req[r];
-  const int64_t row = id >= 0 ? id / n_own : -2 - static_cast<int64_t>(r);
+  // an id past this owner's shard (a sender's id at or beyond the vocab) is
+  // served like padding -- a zero row, a negative local the update skips --
+  // never read out of the table's bounds
+  const int64_t row = (id >= 0 && id / n_own < nrows) ? id / n_own : -2 - static_cast<int64_t>(r);
   if (gl == 0) {
     local[r] = row;
     // the push's owner update stamp (a2a_stamp_kernel's store), here while the
     // slot's row is at hand: one launch less per step
-    if (slotmap != nullptr && row >= 0 && row < nrows) slotmap[row * W + r / cap] = (call << 32) | r;
+    if (slotmap != nullptr && row >= 0) slotmap[row * W + r / cap] = (call << 32) | r;
   }
   T* dst = rows + static_cast<int64_t>(r) * D;
   const float* src = table + (row >= 0 ? row : 0) * static_cast<int64_t>(D);

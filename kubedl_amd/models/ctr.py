@@ -295,8 +295,13 @@ class ShardedEmbedding:
 
     def __init__(self, vocab: int, dim: int, owners: List[int], rank: int, world: int, device,
                  group=None, lr: float = 0.05, eps: float = 1e-8, init_std: float = 0.01, seed: int = 0,
-                 max_ids: Optional[int] = None, slack: Optional[float] = None, force_fixed: bool = False):
+                 max_ids: Optional[int] = None, slack: Optional[float] = None, force_fixed: bool = False,
+                 rows_bf16: bool = False):
         self.vocab, self.dim = vocab, dim
+        # the fixed exchange's row dtype: ONE value per embedding, the same on
+        # every rank (the job config), so the row all-to-all's byte counts match
+        # between a worker's pull_into / pull and a PS rank's participate()
+        self.rows_bf16 = bool(rows_bf16)
         self.owners = list(owners)
         self.n_own = len(owners)
         self.rank, self.world = rank, world
@@ -439,11 +444,13 @@ class ShardedEmbedding:
                     "exchange_bytes": self.exchange_bytes}
         return {}
 
-    def _pull_fixed(self, ids: torch.Tensor, rows_bf16: bool = False):
+    def _pull_fixed(self, ids: torch.Tensor):
         """The fixed-capacity exchange of a pull -> (received rows [W * cap + 1, dim]
-        (the last row zero), rslot [n], inverse [n]).  ``rows_bf16``: the rows
+        (the last row zero), rslot [n], inverse [n]).  ``self.rows_bf16``: the rows
         travel as bf16 (the caller casts them to the bf16 tower input anyway:
-        the owner rounds once, bit-identical, half the bytes)."""
+        the owner rounds once, bit-identical, half the bytes) -- fixed at
+        construction, so every rank of the exchange sends and receives one dtype."""
+        rows_bf16 = self.rows_bf16
         self._agree()
         W, cap, dev = self.world, self.cap, self.device
         n = ids.numel()
@@ -500,11 +507,17 @@ class ShardedEmbedding:
             slotmap, call = self._stamp_call()
             rows, local = _ext.load().a2a_serve(self.table, req, self.n_own, rows_bf16, slotmap, call, cap, W)
         elif self.is_owner:
-            rows = self._local_gather(torch.where(req >= 0, req // self.n_own, torch.zeros_like(req)))
+            lrow = torch.where(req >= 0, req // self.n_own, torch.zeros_like(req))
+            ok = (req >= 0) & (lrow < self.table.shape[0])  # ids past the shard read as zero rows
+            rows = self._local_gather(torch.where(ok, lrow, torch.zeros_like(lrow)))
+            rows = torch.where(ok[:, None], rows, torch.zeros_like(rows))
+            if rows_bf16:
+                rows = rows.to(torch.bfloat16)
         elif self.use_hip:  # no id is routed to a non-owner: never read
             rows = torch.empty(W * cap, self.dim, device=dev, dtype=torch.bfloat16 if rows_bf16 else torch.float32)
         else:
-            rows = torch.zeros(W * cap, self.dim, device=dev)
+            rows = torch.zeros(W * cap, self.dim, device=dev,
+                               dtype=torch.bfloat16 if rows_bf16 else torch.float32)
         got = self._got_buffer(W * cap, rows.dtype)
         dist.all_to_all_single(got[: W * cap], rows.contiguous(), group=self.group)
         self.exchange_bytes += W * (cap + 1) * 8 + W * cap * self.dim * rows.element_size()
@@ -560,8 +573,10 @@ class ShardedEmbedding:
             if local is None:
                 # padding slots (id -1, zero gradient) become DISTINCT negative rows:
                 # one-row segments that the update skips -- never one giant segment
+                # (so do ids past the shard: served as zero rows, never updated)
                 pad = -2 - torch.arange(req.numel(), device=dev)
-                local = torch.where(req >= 0, req // self.n_own, pad)
+                lrow = req // self.n_own
+                local = torch.where((req >= 0) & (lrow < self.table.shape[0]), lrow, pad)
             if self.use_hip and self.dedup is not None:
                 self._owner_update(local, grecv, cap, scale, call)
             else:
@@ -614,7 +629,7 @@ class ShardedEmbedding:
         if self._fixed():
             # fixed exchange: the received rows go straight into the bf16 input
             # through rslot (dump slots read the zero row)
-            got, rslot, inv = self._pull_fixed(ids, rows_bf16=True)
+            got, rslot, inv = self._pull_fixed(ids)
             _ext.load().embed_gather_cast(got, rslot, inv, F, out, col0)
             return inv
         if not self._sync_free(ids):
@@ -703,11 +718,14 @@ class ShardedEmbedding:
                                            self.lr, self.eps, scale)
         return True
 
-    def participate(self) -> None:
-        """An owner without a batch of its own (PS rank) serves one pull+push round."""
+    def participate(self, scale: float = 1.0) -> None:
+        """An owner without a batch of its own (PS rank) serves one pull+push round.
+        ``scale``: the gradient scale the workers push with (the owner applies
+        it to every received row), e.g. 1 / n_workers -- the same value on
+        every rank of the job."""
         empty = torch.empty(0, dtype=torch.int64, device=self.device)
         self.pull(empty)
-        self.push(torch.empty(0, self.dim, device=self.device))
+        self.push(torch.empty(0, self.dim, device=self.device), scale)
 
 
 # ---------------------------------------------------------------- model

@@ -118,11 +118,11 @@ def main(argv=None) -> int:
     # equal all-to-all splits and no per-step size round trip to the host
     emb = ShardedEmbedding(args.fields * args.vocab, args.dim, owners, rank, world, device,
                            group=None, lr=args.emb_lr, max_ids=args.batch * args.fields,
-                           force_fixed=args.exchange == "fixed")
+                           force_fixed=args.exchange == "fixed", rows_bf16=True)
     total = args.warmup + args.steps
     if not is_worker:  # PS: serve pull/push rounds
         for _ in range(total):
-            emb.participate()
+            emb.participate(scale=1.0 / len(workers))  # the workers' push scale
         emb.finalize()
         dist.barrier()
         dist.destroy_process_group()

@@ -235,6 +235,96 @@ def test_ctr_exchange_overflow_counted_and_capacity_grows():
     assert all("CTR exchange overflow" in out.get(f"error{r}", "") for r in range(4)), out
 
 
+def _ps_worker_ctr(rank, world, port, out):
+    """world 2: rank 0 is a PS (owner, no batch: participate()), rank 1 a worker
+    (build_input / push_grads).  world 1: one rank in both roles (the
+    rehearsal).  Every rank takes the job's one exchange row dtype (bf16)."""
+    import torch.distributed as dist
+    from kubedl_amd.models.ctr import CTRModel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, F, V, D = 16, 6, 50, 8
+    emb = ShardedEmbedding(F * V, D, [0], rank, world, "cpu", lr=0.1, max_ids=B * F, force_fixed=True,
+                           rows_bf16=True)
+    steps = 3
+    if world == 2 and rank == 0:
+        for _ in range(steps):
+            emb.participate(scale=0.5)  # the worker's push scale
+        emb.finalize()
+        out["table"] = emb.table.clone()
+        dist.destroy_process_group()
+        return
+    torch.manual_seed(0)
+    model = CTRModel(F, V, D, 5, (64, 32), emb, "cpu", dtype=torch.float32)
+    g = torch.Generator().manual_seed(10)
+    losses = []
+    for _ in range(steps):
+        ids = torch.randint(0, V, (B, F), generator=g)
+        ids[:, 0] = 3
+        dense, y = torch.randn(B, 5, generator=g), torch.randint(0, 2, (B,), generator=g).float()
+        x, inv, U = model.build_input(ids, dense)
+        x.requires_grad_(True)
+        loss, _ = model.tower.loss(x, y)
+        loss.backward()
+        model.push_grads(x.grad, inv, U, scale=0.5)
+        losses.append(float(loss))
+    emb.finalize()
+    out["losses"] = losses
+    if world == 1:
+        out["table"] = emb.table.clone()
+    dist.destroy_process_group()
+
+
+def _run_ps_ctr(world):
+    port = _port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_ps_worker_ctr, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    return dict(out)
+
+
+def test_ps_plus_worker_ctr_exchange_one_row_dtype():
+    """a PS rank (participate(): an empty pull) and a worker
+    (build_input -> the bf16 fixed exchange) must send one row dtype, or the
+    row all-to-all's byte counts differ.  Scheduler-less 1 PS + 1 worker over
+    gloo trains three steps; the PS's table and the worker's losses equal the
+    one-rank rehearsal's (same owner, same ids, same bf16 rows) exactly --
+    which also needs the PS to apply the workers' push scale (participate(scale))."""
+    ref = _run_ps_ctr(1)
+    got = _run_ps_ctr(2)
+    assert got["losses"] == ref["losses"]
+    assert torch.equal(got["table"], ref["table"])
+    assert not torch.equal(ref["table"], ShardedEmbedding(6 * 50, 8, [0], 0, 1, "cpu").table)  # it trained
+
+
+def test_fixed_exchange_serves_out_of_range_ids_as_zero_rows():
+    """an id past the owner's shard (>= vocab) is served as a
+    zero row and skipped by the update, never read out of bounds (CPU path; the
+    GPU kernel's twin is test_a2a_serve_out_of_range_gpu)."""
+    import torch.distributed as dist
+    port = _port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        emb = ShardedEmbedding(40, 4, [0], 0, 1, "cpu", lr=0.1, max_ids=8, force_fixed=True)
+        t0 = emb.table.clone()
+        ids = torch.tensor([1, 39, 40, 1000])
+        rows, inv = emb.pull(ids)
+        torch.testing.assert_close(rows[inv][:2], t0[[1, 39]])
+        assert torch.count_nonzero(rows[inv][2:]) == 0
+        emb.push(torch.ones(rows.shape[0], 4))
+        assert emb.table.shape == t0.shape and torch.isfinite(emb.table).all()
+        assert not torch.equal(emb.table[1], t0[1]) and not torch.equal(emb.table[39], t0[39])
+    finally:
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------- GPU kernels
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 72), (4096, 1024, 1680), (1, 128, 64)])
@@ -771,6 +861,28 @@ def test_a2a_serve_and_mapped_segment_reduce():
     written = torch.zeros(60, dtype=torch.bool, device="cuda")
     written[out_rows[keep]] = True
     assert bool(out[~written].isnan().all())
+
+
+@pytest.mark.gpu
+def test_a2a_serve_out_of_range_gpu():
+    """ids past the owner's shard (a sender's id >= vocab) are
+    served like padding -- zero rows, a distinct negative local, no stamp --
+    never read out of the table's bounds."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    table = torch.randn(100, 64, device="cuda")
+    W, cap = 2, 4
+    req = torch.tensor([0, 199, 200, 10_000_000, -1, 7, 1 << 40, 3], device="cuda")
+    slotmap = torch.zeros(100 * W, dtype=torch.int64, device="cuda")
+    rows, local = ext.a2a_serve(table, req, 2, False, slotmap, 1, cap, W)
+    torch.cuda.synchronize()
+    bad = torch.tensor([False, False, True, True, True, False, True, False], device="cuda")
+    want_local = torch.where(bad, -2 - torch.arange(8, device="cuda"), req // 2)
+    assert torch.equal(local, want_local)
+    assert torch.equal(rows[~bad], table[req[~bad] // 2])
+    assert torch.count_nonzero(rows[bad]) == 0
+    stamped = (slotmap != 0).nonzero().flatten()
+    assert stamped.numel() == 4 and bool((stamped // W < 100).all())
 
 
 @pytest.mark.gpu
