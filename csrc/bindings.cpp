@@ -458,6 +458,37 @@ void gbdt_hist(const at::Tensor& bins, const at::Tensor& grad, const at::Tensor&
             "gbdt_hist_build");
 }
 
+// The device grower's quantised histogram (gbdt_hist_wq) over nodes = consecutive
+// row ranges seg[j]..seg[j+1] of ``rows``, with the grower's fixed-point scale
+// from {max |g|, max h} of all rows: [nodes, F, B, 2] fp32 (a test hook: the
+// grower calls the launcher natively).
+at::Tensor gbdt_hist_quant(const at::Tensor& bins, const at::Tensor& grad, const at::Tensor& hess,
+                           const at::Tensor& rows, const at::Tensor& seg, int64_t num_bins, int64_t rpb) {
+  TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.dim() == 2 && bins.is_contiguous(),
+              "gbdt_hist_quant: contiguous uint8 bins [N, F]");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && hess.scalar_type() == at::kFloat && grad.is_contiguous() &&
+                  hess.is_contiguous() && grad.numel() == bins.size(0) && hess.numel() == grad.numel(),
+              "gbdt_hist_quant: fp32 g/h [N]");
+  TORCH_CHECK(rows.scalar_type() == at::kInt && seg.scalar_type() == at::kInt && rows.is_contiguous() &&
+                  seg.is_contiguous() && seg.numel() >= 2, "gbdt_hist_quant: int32 rows / seg");
+  TORCH_CHECK(num_bins >= 2 && num_bins <= 256 && rpb >= 64 && rpb <= 4096, "gbdt_hist_quant: bins / rpb");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
+  const int64_t nb = seg.numel() - 1, F = bins.size(1), N = bins.size(0);
+  auto ghmax = at::empty({2}, grad.options());
+  auto hist = at::zeros({nb, F, num_bins, 2}, grad.options());
+  auto blo = seg.slice(0, 0, nb).contiguous(), bhi = seg.slice(0, 1, nb + 1).contiguous();
+  auto chunk_off = at::empty({nb + 1}, seg.options());
+  check_hip(kdl::gbdt_gh_absmax(grad.data_ptr<float>(), hess.data_ptr<float>(), static_cast<int>(N),
+                                ghmax.data_ptr<float>(), cur_stream()), "gbdt_gh_absmax");
+  const int max_chunks = static_cast<int>((N + rpb - 1) / rpb + nb);
+  check_hip(kdl::gbdt_hist_wq(bins.data_ptr<uint8_t>(), grad.data_ptr<float>(), hess.data_ptr<float>(), 1,
+                              rows.data_ptr<int32_t>(), blo.data_ptr<int32_t>(), bhi.data_ptr<int32_t>(),
+                              chunk_off.data_ptr<int32_t>(), static_cast<int>(nb), max_chunks, static_cast<int>(rpb),
+                              static_cast<int>(F), static_cast<int>(num_bins), ghmax.data_ptr<float>(),
+                              hist.data_ptr<float>(), cur_stream()), "gbdt_hist_wq");
+  return hist;
+}
+
 std::vector<at::Tensor> gbdt_split(const at::Tensor& hist, double lambda, double min_child_weight) {
   TORCH_CHECK(hist.is_cuda() && hist.dim() == 4 && hist.size(3) == 2 && hist.is_contiguous() &&
                   hist.scalar_type() == at::kFloat,
@@ -1708,6 +1739,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("pack_arg_ptrs") = kdl::kPackArgPtrs;
   m.def("gbdt_grad_hess", &gbdt_grad_hess, "boosting round gradient + hessian in one launch (0 reg, 1 logistic, 2 softmax)");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
+  m.def("gbdt_hist_quant", &gbdt_hist_quant, "the device grower's quantised (fixed-point) histograms (test hook)");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
   m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b) (trans_w: A W, W [K, N])",

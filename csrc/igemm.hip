@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "common.h"
 #include "gemm_epi.h"
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   constexpr int WTM = BM / WM, WTN = BN / WN;
   static_assert(WTM % 32 == 0 && WTN % 32 == 0, "wave tile = whole 32x32 MFMA blocks");
   constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int NMF = 4 * TN * TM;  // MFMAs per wave per K-step
   using Epi = Epilogue<BM, BN, NT, EPI, GATHER>;
   constexpr bool TAPS = GATHER == G_CONV3 || GATHER == G_DGRAD2;
   constexpr int LDC = Epi::LDC;
@@ -131,130 +133,129 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
   // (a zero-record descriptor drops that operand's loads: KDL_TUNE igemm_price timing builds)
   const int bytesA = (p.price_drop & 1) ? 0 : static_cast<int>(p.a_rows * lda * 2);
   const int bytesB = (p.price_drop & 2) ? 0 : static_cast<int>(static_cast<int64_t>(p.N) * K * 2);
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), (short)0, bytesA,
-                                                                      0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.B), (short)0, bytesB,
-                                                                      0x00020000);
-  i32x4_t wA{}, wB{};
-  if constexpr (STAGES == 3) {
-    wA = rsrc_words(p.A, static_cast<uint32_t>(bytesA));
-    wB = rsrc_words(p.B, static_cast<uint32_t>(bytesB));
-  }
-  auto dma = [&](bool is_a, lds_void_t* dst, uint32_t voff, uint32_t soff) {
-    if constexpr (STAGES == 3) dma16_asm(is_a ? wA : wB, dst, voff, soff);
-    else dma16(is_a ? rA : rB, dst, voff, soff);
-  };
+  const i32x4_t wA = rsrc_words(p.A, static_cast<uint32_t>(bytesA));
+  const i32x4_t wB = rsrc_words(p.B, static_cast<uint32_t>(bytesB));
 
-  // per DMA instruction i of this wave: operand row (within its A or B region)
-  // and the logical 16-B chunk this lane fetches (source-side swizzle)
+  // Per DMA piece i of this wave (1 KiB: 8 operand rows x 8 16-B chunks, the
+  // lane's chunk swizzled at the SOURCE): a byte offset base and an INVERTED
+  // validity mask, so that every piece of every gather is issued as
+  //   voffset = (base + delta) | (((inv >> bit) & 1) << 31),  soffset = soff
+  // with wave-uniform (delta, bit, soff) per K-step: bit 31 puts an invalid
+  // row past num_records (< 2^31) and the hardware returns zeros.  3x3 taps:
+  // bit 3r + s of the mask is tap (r, s); delta = ((r Win + s) Cin + kc0) * 2
+  // from the row's (ih0, iw0) pixel.  Dense / strided A rows and B rows: one
+  // bit (row < M, or always), delta 0, the K column in soffset.  No per-piece
+  // branch and no per-piece integer division in the main loop.
   const int lrow = lane >> 3;
-  uint32_t voff[IPW];
-  int crow[IPW];    // conv3 / dgrad2: image base row (n * Hin * Win) or -1 for rows >= M
+  int pbase[IPW];
+  uint32_t pinv[IPW];
+  bool pisA[IPW];  // wave-uniform
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int g = wave * IPW + i;
+    pisA[i] = g < BM / 8;
+    if (!pisA[i]) {  // B (weights): row n0 + r, chunk c
+      const int r = 8 * (g - BM / 8) + lrow;
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      pbase[i] = ((n0 + r) * K + 8 * c) * 2;
+      pinv[i] = 0;
+    }
+  }
   // G_DGRAD2 (per tile, wave-uniform): sub-pixel class (py, px), its taps per
   // row-of-taps (ns) and its first K column in the class-major weight matrix
   int py = 0, px = 0, ns = 1, koff = 0;
   (void)py; (void)px; (void)ns; (void)koff;
-  int cih[IPW], ciw[IPW];
-  (void)crow; (void)cih; (void)ciw;
-#pragma unroll
-  for (int i = 0; i < IPW; ++i) {
-    const int g = wave * IPW + i;
-    if (g >= BM / 8) {  // B (weights): row n0 + r, chunk c
-      const int r = 8 * (g - BM / 8) + lrow;
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      voff[i] = static_cast<uint32_t>(((n0 + r) * K + 8 * c) * 2);
-    }
-  }
 
   auto setup_rows = [&](int tm) {
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
+      if (!pisA[i]) continue;
       const int g = wave * IPW + i;
-      if (g < BM / 8) {
-        const int r = 8 * g + lrow;
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        const int m = tm * BM + r;
+      const int r = 8 * g + lrow;
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int m = tm * BM + r;
+      if constexpr (TAPS) {
+        bool live;
+        int crow, ih0, iw0;
         if constexpr (GATHER == G_DGRAD2) {
           const int cls = tm / (p.mc_pad / BM);
           const int mc = m - cls * p.mc_pad;  // row within the class
-          if (mc < p.mc) {
-            const int hw = p.Hin * p.Win;
-            const int nimg = mc / hw, rem = mc - nimg * hw;
-            const int oi = rem / p.Win;
-            crow[i] = nimg * hw;
-            cih[i] = oi;
-            ciw[i] = rem - oi * p.Win;
-          } else {
-            crow[i] = -1;
-            cih[i] = 0;
-            ciw[i] = 0;
-          }
-          voff[i] = static_cast<uint32_t>(8 * c * 2);
-        } else if constexpr (GATHER == G_CONV3) {
-          if (m < M) {
-            const int hw = p.Hout * p.Wout;
-            const int nimg = m / hw, rem = m - nimg * hw;
-            const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
-            crow[i] = nimg * p.Hin * p.Win;
-            cih[i] = oh * p.stride - 1;
-            ciw[i] = ow * p.stride - 1;
-          } else {
-            crow[i] = -1;
-            cih[i] = 0;
-            ciw[i] = 0;
-          }
-          voff[i] = static_cast<uint32_t>(8 * c * 2);  // chunk byte offset; the row part is per tap
+          live = mc < p.mc;
+          const int hw = p.Hin * p.Win;
+          const int nimg = mc / hw, rem = mc - nimg * hw;
+          crow = nimg * hw;
+          ih0 = rem / p.Win;
+          iw0 = rem - ih0 * p.Win;
         } else {
-          int64_t src = m;
-          if constexpr (GATHER == G_STRIDED) {
-            const int hw = p.Hout * p.Wout;
-            const int nimg = m / hw, rem = m - nimg * hw;
-            const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
-            src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
-          }
-          voff[i] = m < M ? static_cast<uint32_t>((src * K + 8 * c) * 2) : kOOB;
+          live = m < M;
+          const int hw = p.Hout * p.Wout;
+          const int nimg = m / hw, rem = m - nimg * hw;
+          const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
+          crow = nimg * p.Hin * p.Win;
+          ih0 = oh * p.stride - 1;
+          iw0 = ow * p.stride - 1;
         }
+        uint32_t valid = 0;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+          for (int ss = 0; ss < 3; ++ss) {
+            const bool ok = static_cast<unsigned>(ih0 + rr) < static_cast<unsigned>(p.Hin) &&
+                            static_cast<unsigned>(iw0 + ss) < static_cast<unsigned>(p.Win);
+            valid |= (ok ? 1u : 0u) << (3 * rr + ss);
+          }
+        pinv[i] = live ? ~valid : ~0u;
+        pbase[i] = live ? ((crow + ih0 * p.Win + iw0) * p.Cin + 8 * c) * 2 : 0;
+      } else {
+        int64_t src = m;
+        if constexpr (GATHER == G_STRIDED) {
+          const int hw = p.Hout * p.Wout;
+          const int nimg = m / hw, rem = m - nimg * hw;
+          const int oh = rem / p.Wout, ow = rem - oh * p.Wout;
+          src = (static_cast<int64_t>(nimg) * p.Hin + oh * p.stride) * p.Win + ow * p.stride;
+        }
+        pinv[i] = m < M ? 0u : ~0u;
+        pbase[i] = m < M ? static_cast<int>((src * K + 8 * c) * 2) : 0;
       }
     }
   };
 
-  auto issue = [&](int kt, int stage) {
+  // wave-uniform per K-step: (delta, bit, soffset) of its A pieces and the
+  // soffset of its B pieces
+  struct KStep { int delta; int bit; uint32_t soffA, soffB; };
+  auto kstep_of = [&](int kt) {
+    KStep s;
     const int k0 = kt * IBK;
-    char* base = lds + stage * STAGE;
-    int tap = 0, kc0 = k0, r3 = 0, q3 = 0;
-    (void)tap; (void)r3; (void)q3;
-    if constexpr (GATHER == G_DGRAD2) {
-      // class tap (ri, si): dy pixel offset (di, dj) = (py && ri == 0, px && si == 0)
-      tap = k0 / p.Cin;
-      kc0 = k0 - tap * p.Cin;
-      const int ri = tap / ns, si = tap - ri * ns;
-      r3 = (py && ri == 0) ? 1 : 0;
-      q3 = (px && si == 0) ? 1 : 0;
-    } else if constexpr (GATHER == G_CONV3) {
-      tap = k0 / p.Cin;  // a 64-deep K-step never straddles taps (Cin % 64 == 0)
-      kc0 = k0 - tap * p.Cin;
-      r3 = tap / 3;
-      q3 = tap - 3 * r3;
-    }
-#pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int g = wave * IPW + i;
-      lds_void_t* dst = (lds_void_t*)(base + g * 1024);
-      if (g < BM / 8) {
-        if constexpr (TAPS) {
-          const int ih = cih[i] + r3, iw = ciw[i] + q3;
-          const bool ok = crow[i] >= 0 && static_cast<unsigned>(ih) < static_cast<unsigned>(p.Hin) &&
-                          static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win);
-          const uint32_t off = ok ? static_cast<uint32_t>(((crow[i] + ih * p.Win + iw) * p.Cin + kc0) * 2) + voff[i]
-                                  : kOOB;
-          dma(true, dst, off, 0);
-        } else {
-          dma(true, dst, voff[i], k0 * 2);
-        }
+    s.delta = 0;
+    s.bit = 0;
+    s.soffA = static_cast<uint32_t>(k0 * 2);
+    s.soffB = static_cast<uint32_t>((koff + k0) * 2);
+    if constexpr (TAPS) {
+      const int tap = k0 / p.Cin;  // a 64-deep K-step never straddles taps (Cin % 64 == 0)
+      const int kc0 = k0 - tap * p.Cin;
+      int r3, q3;
+      if constexpr (GATHER == G_DGRAD2) {
+        // class tap (ri, si): dy pixel offset (di, dj) = (py && ri == 0, px && si == 0)
+        const int ri = tap / ns, si = tap - ri * ns;
+        r3 = (py && ri == 0) ? 1 : 0;
+        q3 = (px && si == 0) ? 1 : 0;
       } else {
-        dma(false, dst, voff[i], (koff + k0) * 2);
+        r3 = tap / 3;
+        q3 = tap - 3 * r3;
       }
+      s.delta = ((r3 * p.Win + q3) * p.Cin + kc0) * 2;
+      s.bit = 3 * r3 + q3;
+      s.soffA = 0;
     }
+    return s;
+  };
+  auto piece = [&](int i, const KStep& s, int stage) {
+    const int g = wave * IPW + i;
+    lds_void_t* dst = (lds_void_t*)(lds + stage * STAGE + g * 1024);
+    const int delta = pisA[i] ? s.delta : 0;
+    const int bit = pisA[i] ? s.bit : 0;
+    const uint32_t off = static_cast<uint32_t>(pbase[i] + delta) | (((pinv[i] >> bit) & 1u) << 31);
+    dma16_asm(pisA[i] ? wA : wB, dst, off, pisA[i] ? s.soffA : s.soffB);
   };
 
   // fragment byte offsets within a row: logical chunk 2s + fh, swizzled by the
@@ -283,31 +284,74 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x16_t{};
-    auto compute = [&](const char* As) {
+    auto frags = [&](const char* As, int s, bf16x8_t (&wf)[TN], bf16x8_t (&xf)[TM]) {
       const char* Bs = As + SA;
 #pragma unroll
+      for (int i = 0; i < TN; ++i)
+        wf[i] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + i * 32 + fr) * 128 + xo[s]);
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        xf[j] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + j * 32 + fr) * 128 + xo[s]);
+    };
+    // One K-step of MFMAs on stage `As`, fragments double-buffered (substep
+    // s + 1's reads issued before substep s's MFMAs); with ISSUE, the next
+    // K-step's DMA pieces are spread over the first half of the MFMAs (one
+    // piece per MFMA gap at most), so their issue cost runs in the MFMA
+    // shadow instead of in a burst after the barrier, and each lands about
+    // half a K-step before the barrier that publishes it.
+    auto compute = [&](const char* As, auto issue_tag, const KStep& ks, int nstage) {
+      constexpr bool ISSUE = decltype(issue_tag)::value;
+      constexpr int SPAN = NMF / 2 > IPW ? NMF / 2 : (NMF > IPW ? IPW : NMF);
+      bf16x8_t wf[2][TN], xf[2][TM];
+      frags(As, 0, wf[0], xf[0]);
+      int done = 0;
+      (void)done;
+#pragma unroll
       for (int s = 0; s < 4; ++s) {
-        bf16x8_t wf[TN], xf[TM];
+        if (s < 3) frags(As, s + 1, wf[(s + 1) & 1], xf[(s + 1) & 1]);
+        // pin the prefetch ahead of this substep's MFMAs (the scheduler would
+        // otherwise sink the reads next to their first use and expose the LDS
+        // latency four times per K-step)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < TN; ++i)
-          wf[i] = *reinterpret_cast<const bf16x8_t*>(Bs + (wn0 + i * 32 + fr) * 128 + xo[s]);
 #pragma unroll
-        for (int j = 0; j < TM; ++j)
-          xf[j] = *reinterpret_cast<const bf16x8_t*>(As + (wm0 + j * 32 + fr) * 128 + xo[s]);
+          for (int j = 0; j < TM; ++j) {
+            const int mi = (s * TN + i) * TM + j;  // MFMA index within the K-step
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][i], xf[s & 1][j], acc[i][j], 0, 0, 0);
+            if constexpr (ISSUE) {
+              // pieces [mi * IPW / SPAN, (mi + 1) * IPW / SPAN) after MFMA mi (mi < SPAN)
 #pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int j = 0; j < TM; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+              for (int pi = 0; pi < IPW; ++pi)
+                if (pi * SPAN / IPW == mi) piece(pi, ks, nstage);
+            }
+          }
       }
     };
+    using yes = std::integral_constant<bool, true>;
+    using no = std::integral_constant<bool, false>;
     if constexpr (STAGES == 2) {
-      issue(0, 0);
-      for (int kt = 0; kt < nk; ++kt) {
-        __syncthreads();  // stage kt landed (every wave's vmcnt(0) + barrier); stage kt+1 free
-        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-        compute(lds + (kt & 1) * STAGE);
+      {
+        const KStep k0s = kstep_of(0);
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) piece(i, k0s, 0);
       }
+      // stage kt landed (every wave's vmcnt(0) + barrier); every wave's
+      // fragment reads of stage kt - 1 retired: stage kt + 1 is free.  The
+      // last K-step is peeled (no DMA): one loop body, so the accumulators
+      // keep their registers (an if/else of two bodies copies them per step).
+      auto publish = [] {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      };
+      int kt = 0;
+      for (; kt + 1 < nk; ++kt) {
+        publish();
+        compute(lds + (kt & 1) * STAGE, yes{}, kstep_of(kt + 1), (kt + 1) & 1);
+      }
+      publish();
+      compute(lds + (kt & 1) * STAGE, no{}, KStep{}, 0);
     } else {
       // three stages, two K-steps of DMA in flight across each barrier: a
       // counted vmcnt retires stage kt only (the IPW loads of stage kt+1 stay
@@ -315,8 +359,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
       // would drain vmcnt to 0), then stage kt+2 is issued into the buffer
       // every wave finished reading in step kt-1 (its ds_reads retired by the
       // lgkmcnt(0) before this barrier).
-      issue(0, 0);
-      if (nk > 1) issue(1, 1);
+      {
+        const KStep a = kstep_of(0);
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) piece(i, a, 0);
+      }
+      if (nk > 1) {
+        const KStep a = kstep_of(1);
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) piece(i, a, 1);
+      }
       int cur = 0;
       for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk)
@@ -326,8 +378,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + 2 < nk) issue(kt + 2, cur == 0 ? 2 : cur - 1);
-        compute(lds + cur * STAGE);
+        if (kt + 2 < nk) {
+          const KStep a = kstep_of(kt + 2);
+          const int st = cur == 0 ? 2 : cur - 1;
+#pragma unroll
+          for (int i = 0; i < IPW; ++i) piece(i, a, st);
+        }
+        compute(lds + cur * STAGE, no{}, KStep{}, 0);
         cur = cur == 2 ? 0 : cur + 1;
       }
     }

@@ -88,6 +88,19 @@ def main(args) -> int:
             uid = job["metadata"]["uid"]
             created = c.to_epoch(job["metadata"]["creationTimestamp"])
             res = _last_json(mgr.kubelet.log_path("default", f"{n}-master-0")) or {}
+            if c.last_condition_type(st) != "Succeeded":
+                # a diagnosable tail per rank: which rank died, and how
+                print(f"[bench_launch] job {n} ended {c.last_condition_type(st)!r}; rank logs:", file=sys.stderr)
+                for p in mgr.store.list("Pod", "default"):
+                    pn = p["metadata"]["name"]
+                    if not pn.startswith(n + "-"):
+                        continue
+                    lp = mgr.kubelet.log_path("default", pn)
+                    tail = ""
+                    if lp and os.path.exists(lp):
+                        with open(lp, errors="replace") as f:
+                            tail = "".join(f.readlines()[-30:])
+                    print(f"---- {pn} ----\n{tail}", file=sys.stderr, flush=True)
             out["jobs"].append({
                 "name": n, "state": c.last_condition_type(st), "ranks": args.gpus,
                 "first_pod_launch_delay_s": mgr.metrics.observed["first"].get(uid),

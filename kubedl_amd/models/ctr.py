@@ -584,8 +584,20 @@ class ShardedEmbedding:
 
     def _stamp_call(self):
         """(slot map, call id) of the next owner update: the map is persistent
-        (zeros), the id grows by one per pull (entries of earlier calls are stale)."""
+        (zeros), the id grows by one per pull (entries of earlier calls are stale).
+
+        Memory: the map is int64 [owned rows x world] -- 8 W bytes per owned row
+        for the whole run (W = 8: 64 B per row, the size of a D = 8 fp32 row
+        plus its Adagrad state; the CTR config's D = 64 rows take 512 B).  It is
+        checked against the device's free memory when first allocated."""
         if getattr(self, "_slotmap", None) is None or self._calls >= (1 << 31) - 1:
+            need = self.table.shape[0] * self.world * 8
+            if self.device.type == "cuda":
+                free, _total = torch.cuda.mem_get_info(self.device)
+                if need > free // 2:
+                    raise MemoryError(f"CTR owner-update slot map needs {need / 2**30:.2f} GiB "
+                                      f"({self.table.shape[0]} owned rows x {self.world} ranks x 8 B), more than "
+                                      f"half of the {free / 2**30:.2f} GiB free: shard the table over more owners")
             self._slotmap = torch.zeros(self.table.shape[0] * self.world, dtype=torch.int64, device=self.device)
             self._calls = 0
         self._calls += 1

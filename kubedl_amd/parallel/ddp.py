@@ -94,6 +94,8 @@ class FlatDDP:
         self.join_stream = None
         if self.active:
             if broadcast_from is not None and world_size > 1:
+                from kubedl_amd.parallel.dist import wait_node_warm
+                wait_node_warm()  # (no-op unless this is the rank's first communicator build)
                 with torch.no_grad():
                     dist.broadcast(space.param, broadcast_from, group=process_group)
                     space.sync_master_from_params()

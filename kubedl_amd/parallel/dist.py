@@ -77,6 +77,8 @@ def init_from_env(device: str | None = None, timeout_s: float | None = None,
     """``world1_group``: also build a (one-rank) process group at WORLD_SIZE=1,
     so a single-GPU job still runs its collectives through RCCL (SURVEY.md
     §7.2 step 5).  ``timeout_s`` defaults to ``KDL_PG_TIMEOUT_S`` (600 s)."""
+    from kubedl_amd.utils.tune import warn_retired_env
+    warn_retired_env()
     if timeout_s is None:
         timeout_s = float(os.environ.get("KDL_PG_TIMEOUT_S", 600))
     rank = env_int("RANK", 0)
@@ -112,6 +114,48 @@ def init_from_env(device: str | None = None, timeout_s: float | None = None,
     return DistInfo(rank, world, local_rank, dev, backend)
 
 
+_NODE_WARM_WAITED = [None]  # seconds waited (None: not yet asked)
+
+
+def wait_node_warm(timeout_s: float = 60.0) -> float:
+    """Wait until the node warm-up (runtime/node_warm.py) has released its lock
+    (``KDL_NODE_WARM_LOCK``, held exclusively by the node runtime while the
+    throw-away communicator fills the code-object cache).  Called AFTER the
+    rank signalled Ready and before its first communicator build, so the
+    launch delay never includes the warm-up and no rank
+    builds a communicator beside it.  Idempotent; returns the seconds waited."""
+    if _NODE_WARM_WAITED[0] is not None:
+        return 0.0
+    import fcntl
+    import time
+    path = os.environ.get("KDL_NODE_WARM_LOCK")
+    t0 = time.monotonic()
+    if path and os.path.exists(path):
+        try:
+            fd = os.open(path, os.O_RDONLY | os.O_CLOEXEC)
+        except OSError:
+            fd = None
+        if fd is not None:
+            try:
+                while True:
+                    try:
+                        fcntl.flock(fd, fcntl.LOCK_SH | fcntl.LOCK_NB)
+                        fcntl.flock(fd, fcntl.LOCK_UN)
+                        break
+                    except BlockingIOError:
+                        if time.monotonic() - t0 > timeout_s:  # best effort: a job still runs cold
+                            break
+                        time.sleep(0.01)
+            finally:
+                os.close(fd)
+    _NODE_WARM_WAITED[0] = time.monotonic() - t0
+    if _NODE_WARM_WAITED[0] > 0.05:
+        import sys
+        print(f"[kdl] waited {_NODE_WARM_WAITED[0]:.2f}s for the node warm-up before the first communicator",
+              file=sys.stderr, flush=True)
+    return _NODE_WARM_WAITED[0]
+
+
 def barrier(info: DistInfo) -> None:
     if info.world_size > 1:
         if info.backend == "nccl":
@@ -137,6 +181,7 @@ def first_collective(info: DistInfo, stream=None) -> float:
     import time
     if not dist.is_initialized():
         return 0.0
+    wait_node_warm()
     ctx = torch.cuda.stream(stream) if (stream is not None and info.device.type == "cuda") \
         else contextlib.nullcontext()
     with ctx:

@@ -182,21 +182,69 @@ class _StreamHandle:
 
 class P2PTransport:
     """Async launcher for ``FlatDDP``: runs ``P2PAllReduce`` on a side stream
-    after the gradients produced so far on the compute stream."""
+    after the gradients produced so far on the compute stream.
+
+    Self-check: the kernel has only run with two ranks
+    sharing one GPU, so its FIRST bucket is reduced twice -- through the
+    process group (RCCL on a node) on an fp32 copy, and through the P2P
+    kernel -- and compared before training consumes it.  A mismatch on any
+    rank (agreed by a MAX all-reduce, so every rank raises together) raises
+    ``P2PError``: a cross-device coherence bug stops the job instead of
+    silently corrupting its gradients."""
+
+    # test hook: this rank perturbs its own bucket after the reference copy --
+    # what its peers would read through a stale or incoherent mapping
+    inject_corrupt_rank: int | None = None
 
     def __init__(self, buf: torch.Tensor, group=None):
         self.ar = P2PAllReduce(buf, group)
+        self.group = group
         self.stream = torch.cuda.Stream(device=buf.device)
+        self.verified = False
+        self.self_check_max_err: float | None = None
 
     def launch(self, lo: int, hi: int) -> _StreamHandle:
         ready = torch.cuda.Event()
         ready.record()
         self.stream.wait_event(ready)
+        if not self.verified:
+            self._self_check(lo, hi)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+            return _StreamHandle(done)
         with torch.cuda.stream(self.stream):
             self.ar.all_reduce_(lo, hi)
             done = torch.cuda.Event()
             done.record()
         return _StreamHandle(done)
+
+    def _self_check(self, lo: int, hi: int) -> None:
+        buf = self.ar.buf
+        with torch.cuda.stream(self.stream):
+            ref = buf[lo:hi].float()
+            dist.all_reduce(ref, group=self.group)  # ordered before the kernel on this stream
+            if self.inject_corrupt_rank is not None and self.inject_corrupt_rank == self.ar.rank:
+                buf[lo:hi].add_(1.0)
+            self.ar.all_reduce_(lo, hi)
+        self.stream.synchronize()
+        self.ar.check()
+        with torch.cuda.stream(self.stream):
+            want = ref.to(buf.dtype).float()  # the kernel rounds its fp32 sum once
+            got = buf[lo:hi].float()
+            err = (got - want).abs()
+            # bf16: one rounding of two fp32 sums taken in different orders may
+            # land one ulp apart; fp32: summation-order noise only
+            rel = 2.0 ** -7 if buf.dtype == torch.bfloat16 else 1e-5
+            tol = rel * want.abs() + 1e-6 * float(want.abs().max()) + 1e-30
+            bad = torch.tensor([float((err > tol).any())], device=buf.device)
+            self.self_check_max_err = float(err.max())
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=self.group)
+        self.stream.synchronize()
+        if float(bad.item()) > 0:
+            raise P2PError(f"p2p self-check: the P2P all-reduce of bucket [{lo}, {hi}) differs from the "
+                           f"process group's on at least one rank (max |diff| here {self.self_check_max_err:.3g}); "
+                           f"refusing to train on it -- run with KDL_ALLREDUCE=rccl")
+        self.verified = True
 
     def check(self) -> None:
         self.ar.check()

@@ -240,6 +240,12 @@ class PodWorker(threading.Thread):
         ready = os.path.join(self.sandbox, f"ready.{cidx}")
         env["KDL_READY_FILE"] = ready
         env["KDL_PROGRESS_FILE"] = os.path.join(self.sandbox, f"progress.{cidx}")
+        # the node warm-up's lock: a rank waits on it after its Ready, before its
+        # first communicator build (parallel/dist.py wait_node_warm) -- pods are
+        # never held back from starting by the warm-up
+        z = self.k.zygote
+        if z is not None and z.warm_gpu is not None:
+            env["KDL_NODE_WARM_LOCK"] = z.warm_lock
         return env, ready
 
     # ------------------------------------------------------------ process control
@@ -393,17 +399,6 @@ class PodWorker(threading.Thread):
         finally:
             self.k._worker_done(self)
 
-    def _wait_node_warm(self, timeout: float = 60.0) -> None:
-        """A pod placed on the node warm-up's GPU starts after the warm-up's
-        throw-away communicator is gone (it would share the device with it)."""
-        z, g = self.k.zygote, self.k.warm_gpu
-        if z is None or g is None or str(g) not in self.gpus or z.prefetched.is_set():
-            return
-        t_end = time.monotonic() + timeout
-        while not z.prefetched.is_set() and time.monotonic() < t_end:
-            if self.deleted.wait(self.k.poll_interval * 5):
-                return
-
     def _wait_peers_gone(self) -> None:
         """Gang teardown barrier: wait (bounded) until no other pod of this job
         is still terminating."""
@@ -414,7 +409,6 @@ class PodWorker(threading.Thread):
 
     def _run(self) -> None:
         self._wait_peers_gone()
-        self._wait_node_warm()
         if self.deleted.is_set():
             return
         os.makedirs(os.path.join(self.sandbox, "logs"), exist_ok=True)
@@ -638,8 +632,9 @@ class Kubelet:
                  gpus: Optional[int] = None):
         """``gpus``: the node's GPU inventory size (None: unknown, warm-up on GPU
         0); the node warm-up runs on its LAST GPU -- the allocator hands GPUs
-        out from 0 -- and a pod bound to that GPU waits for the warm-up to end
-        before its containers start (``warm_gpu``)."""
+        out from 0 (``warm_gpu``).  No pod waits for it to start: every rank
+        gets ``KDL_NODE_WARM_LOCK`` and waits on it after its Ready, before
+        its first communicator build."""
         self.store = store
         self.root = root
         self.node = node_name

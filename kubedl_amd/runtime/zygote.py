@@ -263,6 +263,10 @@ class ZygoteClient:
         self.prefetch_s: Optional[float] = None
         self.warm: Optional[dict] = None
         self._env: dict = {}
+        # held exclusively while the warm-up runs: ranks wait on it (shared)
+        # before their first communicator build, after their Ready
+        self.warm_lock = os.path.join(root, "node_warm.lock")
+        self._warm_fd: Optional[int] = None
 
     def start(self, env: dict) -> None:
         with self._lock:
@@ -275,20 +279,40 @@ class ZygoteClient:
             argv = [sys.executable, "-u", "-m", "kubedl_amd.runtime.zygote", self.sock]
             self.pid = self.native.spawn(argv, [f"{k}={v}" for k, v in env.items()], None, self.log, self.log)
             self._env = env
+            mode = os.environ.get("KDL_NODE_WARM", "1")  # 0 off; force: without /dev/kfd too (tests)
+            if mode != "0" and (mode == "force" or os.path.exists("/dev/kfd")) and self.warm_gpu is not None:
+                self._hold_warm_lock()
         threading.Thread(target=self._wait_ready, daemon=True).start()
         threading.Thread(target=self._prefetch, daemon=True).start()
+
+    def _hold_warm_lock(self) -> None:
+        """Take the warm-up lock before any pod can start (synchronously in
+        start()), so a rank started right after the node runtime sees it held."""
+        import fcntl
+        fd = os.open(self.warm_lock, os.O_RDWR | os.O_CREAT | os.O_CLOEXEC, 0o644)
+        fcntl.flock(fd, fcntl.LOCK_EX)
+        self._warm_fd = fd
+
+    def _release_warm_lock(self) -> None:
+        import fcntl
+        fd, self._warm_fd = self._warm_fd, None
+        if fd is not None:
+            try:
+                fcntl.flock(fd, fcntl.LOCK_UN)
+            finally:
+                os.close(fd)
 
     def _prefetch(self) -> None:
         t0 = time.time()
         try:
             prefetch_files(device_library_paths())
             self.prefetch_s = time.time() - t0
-            if (os.environ.get("KDL_NODE_WARM", "1") != "0" and os.path.exists("/dev/kfd")
-                    and self.warm_gpu is not None):
+            if self._warm_fd is not None:
                 self.warm = warm_node(self._env, gpu=self.warm_gpu, procs=self._warm_procs)
         finally:
             if self.prefetch_s is None:
                 self.prefetch_s = time.time() - t0
+            self._release_warm_lock()
             self.prefetched.set()
 
     def _wait_ready(self, timeout: float = 300.0) -> None:
@@ -334,6 +358,7 @@ class ZygoteClient:
                 p.wait(timeout=5)
             except Exception:
                 pass
+        self._release_warm_lock()
         if self.pid is not None:
             try:
                 self.native.kill_group(self.pid, 9)

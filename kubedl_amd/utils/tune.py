@@ -33,6 +33,33 @@ from typing import Callable, Optional, TypeVar
 T = TypeVar("T")
 
 
+# stand-alone variables of earlier rounds, now KDL_TUNE keys: setting one does
+# nothing, so it is reported once instead of silently ignored
+RETIRED_ENV = {
+    "KDL_STREAMS": "streams", "KDL_MAIN_PRIO": "main_prio", "KDL_DDP_WORLD1": "ddp_world1",
+    "KDL_DDP_REDUCE": "ddp_reduce", "KDL_P2P_TIMEOUT_S": "p2p_timeout_s",
+    "KDL_P2P_ONESHOT_BYTES": "p2p_oneshot_bytes", "KDL_PG_EAGER": "pg_eager",
+    "KDL_PROGRESS_MIN_S": "progress_min_s", "KDL_CTR_A2A_SLACK": "ctr_a2a_slack",
+    "KDL_CTR_A2A_STRICT": "ctr_a2a_strict", "KDL_WORLD1_PG": "world1_pg",
+    "KDL_LOSS_ALLREDUCE": "loss_allreduce", "KDL_COMM_PROBE": "comm_probe",
+    "KDL_COMM_OVERLAP": "comm_overlap",
+}
+_WARNED = [False]
+
+
+def warn_retired_env(stream=None) -> list:
+    """Print one line per retired ``KDL_*`` variable set in the environment,
+    naming the KDL_TUNE key that replaced it (once per process)."""
+    import sys
+    found = [k for k in RETIRED_ENV if k in os.environ]
+    if found and not _WARNED[0]:
+        _WARNED[0] = True
+        for k in found:
+            print(f"[kdl] warning: {k} is retired and ignored; use KDL_TUNE=\"{RETIRED_ENV[k]}="
+                  f"{os.environ[k]}\"", file=stream or sys.stderr, flush=True)
+    return found
+
+
 def tune_find(name: str) -> Optional[str]:
     """The raw value of ``name`` in KDL_TUNE, or None when the key is absent."""
     spec = os.environ.get("KDL_TUNE", "")

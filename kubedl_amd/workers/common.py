@@ -18,17 +18,24 @@ import sys
 import time
 
 
-def signal_ready(extra: dict | None = None) -> None:
+def signal_ready(extra: dict | None = None, wait_warm: bool = True) -> None:
+    """Report Ready; then (``wait_warm``) wait for the node warm-up's lock
+    (parallel/dist.py ``wait_node_warm``) before the caller's first
+    collective -- AFTER Ready, so the launch delay never includes it.  Callers
+    that overlap the wait with other start-up work pass False and wait at
+    their first collective instead (dist.first_collective, FlatDDP)."""
     path = os.environ.get("KDL_READY_FILE")
-    if not path:
-        return
-    payload = {"ready_time": time.time(), "pid": os.getpid()}
-    if extra:
-        payload.update(extra)
-    tmp = path + ".tmp"
-    with open(tmp, "w") as f:
-        json.dump(payload, f)
-    os.replace(tmp, path)
+    if path:
+        payload = {"ready_time": time.time(), "pid": os.getpid()}
+        if extra:
+            payload.update(extra)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(payload, f)
+        os.replace(tmp, path)
+    if wait_warm and os.environ.get("KDL_NODE_WARM_LOCK"):
+        from kubedl_amd.parallel.dist import wait_node_warm
+        wait_node_warm()
 
 
 _PROGRESS_LAST = [0.0]  # monotonic time of the last progress write

@@ -46,11 +46,17 @@ class ResNetTrainer:
                  num_classes: int = 1000, dtype: torch.dtype = torch.bfloat16, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 5e-5, tiny: bool = False,
                  bn_backend: str = "auto", bucket_cap_mb: float = 12.0, seed: int = 0,
-                 conv_benchmark: bool = False, engine: str = "auto", on_streams_ready=None):
+                 conv_benchmark: bool = False, engine: str = "auto", on_streams_ready=None,
+                 before_collectives=None):
         """``engine``: "fused" runs the step through ``models.resnet_engine``
         (fused 1x1-conv GEMMs + staged BN, explicit backward); "autograd" runs
         the module under autograd; "auto" = fused on the GPU when the model's
         channel counts fit the GEMM tiles (multiples of 64), else autograd.
+
+        ``before_collectives``: called right before the trainer's first
+        collective (the DDP parameter broadcast at world > 1), after the model
+        is built -- a caller that bootstraps the communicator on a helper
+        thread joins it here, so every rank's collectives reach RCCL in one order.
 
         ``on_streams_ready``: called once the step's streams (compute + the
         engine's weight-gradient side stream) exist and have run a kernel, i.e.
@@ -110,6 +116,8 @@ class ResNetTrainer:
         self.dtype = dtype
         self.space = FlatParamSpace(model, dtype=dtype, device=dev)
         self.engine_kind = engine
+        if before_collectives is not None:
+            before_collectives()
         self.ddp = FlatDDP(self.space, info.world_size, bucket_cap_mb=bucket_cap_mb,
                            direct=(engine == "fused"))
         self.engine = None

@@ -10,7 +10,7 @@ Rank 0 prints one JSON line per (dtype, size) -- microseconds (MAX over ranks)
 and bus bandwidth 2(W-1)/W * bytes / time for ``p2p1`` (one-shot), ``p2p2``
 (two-shot) and ``rccl`` -- then one summary line per dtype with the measured
 crossovers: the largest size where one-shot beats two-shot (the value for
-``KDL_P2P_ONESHOT_BYTES``) and the sizes where P2P beats RCCL (where
+``KDL_TUNE p2p_oneshot_bytes``) and the sizes where P2P beats RCCL (where
 ``KDL_ALLREDUCE=p2p`` pays).  Env: ``P2P_SIZES`` (bytes, comma list),
 ``P2P_DTYPES`` (bfloat16,float32), ``P2P_ITERS``.
 """

@@ -11,8 +11,8 @@ run() {  # name env...
   echo "$name $(grep -o '"value": [0-9.]*' gpurun_out/ab_$name.log)"
 }
 for r in 1 2; do
-run G_pg_ded_$r KDL_WORLD1_PG=1 KDL_STREAMS=dedicated
-run H_pg_pool_$r KDL_WORLD1_PG=1 KDL_STREAMS=pool
-run I_nopg_ded_$r KDL_WORLD1_PG=0 KDL_STREAMS=dedicated
-run J_pg_ded_noar_$r KDL_WORLD1_PG=1 KDL_STREAMS=dedicated KDL_LOSS_ALLREDUCE=0
+run G_pg_ded_$r KDL_TUNE=world1_pg=1,streams=dedicated
+run H_pg_pool_$r KDL_TUNE=world1_pg=1,streams=pool
+run I_nopg_ded_$r KDL_TUNE=world1_pg=0,streams=dedicated
+run J_pg_ded_noar_$r KDL_TUNE=world1_pg=1,streams=dedicated,loss_allreduce=0
 done

@@ -4,7 +4,10 @@ b256 stage 2-4 shapes: which tile / pipeline depth wins, alone on the GPU.
 
 cfg: 0 = 256x256 (8 waves, 2 LDS stages), 1 = 256x128 (8 waves), 2 = 128x128
 (4 waves, 2 blocks/CU), 3 = 256x64, 4 = 256x128 with three LDS stages (two
-K-steps of DMA in flight: counted vmcnt + raw barrier).  Prints one JSON line per
+K-steps of DMA in flight: counted vmcnt + raw barrier), 5 = 256x256 (4 waves of
+128x128, accumulators in AGPRs), 6 = 512x128 (4 waves of 128x128), 7 = 256x128
+(4 waves of 128x64).  The last line per shape is hipBLASLt (torch.matmul) on the
+dense GEMM of the same M x N x K: a yardstick only.  Prints one JSON line per
 (shape, epilogue, cfg): mean us over 30 launches, TF/s.
 """
 import json
@@ -26,6 +29,9 @@ def nhwc(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+CFGS = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 3, 4, 5, 6, 7]
+
+
 def main() -> int:
     ext = _ext.load()
     torch.manual_seed(0)
@@ -37,8 +43,8 @@ def main() -> int:
         acc = torch.zeros(32 * 2 * c, device="cuda")
         flop = 2.0 * nb * h * h * c * 9 * c
         for epi in (0, 1):
-            for cfg in (0, 1, 2, 3, 4):
-                if cfg == 0 and c % 256:
+            for cfg in CFGS:
+                if cfg in (0, 5) and c % 256:
                     continue
                 ext.set_igemm_cfg(cfg)
                 args = (x, w, y, nb, h, h, c, c, 1, None, epi, shift if epi else None, acc if epi else None,
@@ -56,6 +62,22 @@ def main() -> int:
                 print(json.dumps({"shape": name, "epi": epi, "cfg": cfg, "us": round(us, 1),
                                   "tflops": round(flop / us / 1e6, 1)}), flush=True)
         ext.set_igemm_cfg(-1)
+        # yardstick only (never in the step): hipBLASLt on the dense GEMM of the same M x N x K
+        m, k = nb * h * h, 9 * c
+        a = torch.randn(m, k, device="cuda").bfloat16()
+        b = torch.randn(k, c, device="cuda").bfloat16()
+        for _ in range(3):
+            torch.matmul(a, b)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(30):
+            torch.matmul(a, b)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / 30
+        print(json.dumps({"shape": name, "hipblaslt_dense": True, "M": m, "N": c, "K": k, "us": round(us, 1),
+                          "tflops": round(flop / us / 1e6, 1)}), flush=True)
     return 0
 
 

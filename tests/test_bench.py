@@ -88,6 +88,11 @@ def test_bench_job_path_n_ranks_cpu(n):
     assert line["first_pod_launch_delay_s"] is not None and line["all_pods_launch_delay_s"] is not None
     assert line["all_pods_launch_delay_s"] >= line["first_pod_launch_delay_s"] > 0
     assert line["job_wall_s"] >= line["all_pods_launch_delay_s"]
+    # the communicator bootstrap runs beside the model build at
+    # world N too, joined before the DDP broadcast (the trainer's first collective)
+    st = line["startup"]
+    assert st["comm_overlap"] is True and st["comm_joined_at"] is not None, st
+    assert line["comm_init_s"] > 0
 
 
 def test_bench_direct_path_cpu():

@@ -190,3 +190,44 @@ def test_engine_ddp_p2p_transport_gpu():
     # bf16 gradient sums: the p2p kernel rounds once from fp32, gloo per hop
     torch.testing.assert_close(gp0, gg0, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(mp0, mg0, atol=2e-3, rtol=2e-3)
+
+
+def _selfcheck_worker(rank, world, port, q, corrupt):
+    import torch.distributed as dist
+    from kubedl_amd.parallel.p2p import P2PError, P2PTransport
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1 << 16
+    g = torch.Generator().manual_seed(rank)
+    buf = (torch.randn(n, generator=g) * 1e-2).to(torch.bfloat16).to("cuda:0")
+    P2PTransport.inject_corrupt_rank = 1 if corrupt else None
+    tr = P2PTransport(buf)
+    raised, msg = False, ""
+    try:
+        tr.launch(0, n).wait()
+        torch.cuda.synchronize()
+        tr.launch(0, 4096).wait()  # verified: the plain path
+        torch.cuda.synchronize()
+    except P2PError as e:
+        raised, msg = True, str(e)
+    q.put((rank, raised, tr.verified, tr.self_check_max_err, msg))
+    tr.ar.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_p2p_transport_self_check_gpu(corrupt):
+    """the transport's first bucket goes through both the
+    process group and the P2P kernel and is compared.  A clean pair passes
+    (one-ulp bf16 agreement) and the transport switches to the plain path; a
+    peer buffer corrupted between the two (rank 1 perturbs its bucket after the
+    reference copy) makes EVERY rank raise P2PError instead of training on it."""
+    res = _spawn(_selfcheck_worker, 2, corrupt, timeout=120)
+    for rank, raised, verified, err, msg in res:
+        if corrupt:
+            assert raised and not verified and "self-check" in msg, (rank, msg)
+        else:
+            assert not raised and verified, (rank, msg)
+            assert err is not None and err <= 2 ** -7 * 0.1, err

@@ -386,9 +386,29 @@ def test_knob_surface_stays_small():
         for pat in pats:
             for f in (root / sub).rglob(pat):
                 names |= set(re.findall(r"KDL_[A-Z0-9_]+", f.read_text(errors="ignore")))
+    # the retired names are listed once, only to warn about them (utils/tune.py RETIRED_ENV)
+    from kubedl_amd.utils.tune import RETIRED_ENV, warn_retired_env
+    names -= set(RETIRED_ENV)
     assert len(names) < 40, sorted(names)
     for gone in ("KDL_HIP_GRAPH", "KDL_GBDT_GRAPH", "KDL_STREAMS", "KDL_MAIN_PRIO", "KDL_DDP_WORLD1"):
         assert gone not in names
+    # a retired variable is reported (once), naming its KDL_TUNE key
+    import io
+    import kubedl_amd.utils.tune as tmod
+    tmod._WARNED[0] = False
+    buf = io.StringIO()
+    import os as _os
+    old = _os.environ.get("KDL_STREAMS")
+    _os.environ["KDL_STREAMS"] = "dedicated"
+    try:
+        assert warn_retired_env(buf) == ["KDL_STREAMS"]
+        assert 'KDL_TUNE="streams=dedicated"' in buf.getvalue()
+        assert warn_retired_env(buf) == ["KDL_STREAMS"] and buf.getvalue().count("retired") == 1
+    finally:
+        if old is None:
+            _os.environ.pop("KDL_STREAMS")
+        else:
+            _os.environ["KDL_STREAMS"] = old
 
 
 @pytest.mark.parametrize("mode", [1, 3])
