@@ -44,6 +44,7 @@
 #include "common.h"
 #include "gemm_epi.h"
 #include "kdl_api.h"
+#include "lds_dma.h"
 #include "tune.h"
 
 namespace kdl {
@@ -51,51 +52,16 @@ namespace {
 
 using namespace gemm;
 
-typedef __attribute__((address_space(3))) void lds_void_t;
+using lds_dma::lds_void_t;
+using lds_dma::i32x4_t;
+using lds_dma::kOOB;
+using lds_dma::rsrc_words;
+using lds_dma::dma16;
+using lds_dma::publish_stage;
 
-constexpr int IBK = 64;                 // K per stage (one 128-B LDS row per operand row)
-constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load returns zeros
+constexpr int IBK = 64;  // K per stage (one 128-B LDS row per operand row)
 
 template <int A, int B> struct cmax { static constexpr int v = A > B ? A : B; };
-
-typedef __attribute__((ext_vector_type(4))) int i32x4_t;
-
-// Raw buffer resource words (what __builtin_amdgcn_make_buffer_rsrc builds):
-// 48-bit base, stride 0, num_records bytes, raw-buffer flags.
-__device__ __forceinline__ i32x4_t rsrc_words(const void* base, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  i32x4_t r;
-  r.x = __builtin_amdgcn_readfirstlane(static_cast<int>(a & 0xffffffffu));
-  r.y = __builtin_amdgcn_readfirstlane(static_cast<int>((a >> 32) & 0xffffu));
-  r.z = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
-  r.w = 0x00020000;
-  return r;
-}
-
-// The same 16-B-per-lane LDS-DMA as dma16, issued from inline asm so the
-// compiler does not see an LDS write: hipcc otherwise inserts its own
-// vmcnt wait before the first ds_read of a step, retiring the NEWER stage a
-// step early (guide: "three .s-level traps", item b).  The caller's counted
-// s_waitcnt vmcnt + barrier is then the only ordering, by construction.
-__device__ __forceinline__ void dma16_asm(i32x4_t r, lds_void_t* dst, uint32_t voff, uint32_t soff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst)));
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               :
-               : "s"(m0), "v"(voff), "s"(r), "s"(soff)
-               : "memory", "m0");
-#endif
-}
-
-// One 16-byte-per-lane LDS-DMA load (1 KiB per wave at dst + 16 * lane).  The
-// builtin exists only for the device pass; referenced in the host pass it
-// makes clang drop the kernel's host stub, hence the pass guard.
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff, uint32_t soff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
-#endif
-}
 
 template <int BM, int BN, int WM, int WN, int GATHER, int EPI, int MINB, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p, int GM, int tiles_m, int tiles_n) {
@@ -255,7 +221,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
     const int delta = pisA[i] ? s.delta : 0;
     const int bit = pisA[i] ? s.bit : 0;
     const uint32_t off = static_cast<uint32_t>(pbase[i] + delta) | (((pinv[i] >> bit) & 1u) << 31);
-    dma16_asm(pisA[i] ? wA : wB, dst, off, pisA[i] ? s.soffA : s.soffB);
+    dma16(pisA[i] ? wA : wB, dst, off, pisA[i] ? s.soffA : s.soffB);
   };
 
   // fragment byte offsets within a row: logical chunk 2s + fh, swizzled by the
@@ -340,17 +306,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void igemm_kernel(GemmParams p,
       // fragment reads of stage kt - 1 retired: stage kt + 1 is free.  The
       // last K-step is peeled (no DMA): one loop body, so the accumulators
       // keep their registers (an if/else of two bodies copies them per step).
-      auto publish = [] {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      };
       int kt = 0;
       for (; kt + 1 < nk; ++kt) {
-        publish();
+        publish_stage();
         compute(lds + (kt & 1) * STAGE, yes{}, kstep_of(kt + 1), (kt + 1) & 1);
       }
-      publish();
+      publish_stage();
       compute(lds + (kt & 1) * STAGE, no{}, KStep{}, 0);
     } else {
       // three stages, two K-steps of DMA in flight across each barrier: a

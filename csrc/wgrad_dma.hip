@@ -30,26 +30,27 @@
 #include "common.h"
 #include "gemm_epi.h"
 #include "kdl_api.h"
+#include "lds_dma.h"
+
+#include <type_traits>
 
 namespace kdl {
 namespace gemm {
 namespace {
 
-typedef __attribute__((address_space(3))) void lds_void_t;
+using lds_dma::dma16;
+using lds_dma::i32x4_t;
+using lds_dma::kOOB;
+using lds_dma::lds_void_t;
+using lds_dma::publish_stage;
+using lds_dma::rsrc_words;
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
 
-constexpr int MK = 64;                  // rows (m) per stage
-constexpr uint32_t kOOB = 0x80000000u;  // voffset past every buffer: the load returns zeros
+constexpr int MK = 64;  // rows (m) per stage
 
-// device-pass guards: referenced in the host pass these builtins make clang
-// drop the kernel's host stub (csrc/igemm.hip dma16)
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff, uint32_t soff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
-#endif
-}
-
+// (device-pass guard: referenced in the host pass this builtin makes clang
+// drop the kernel's host stub)
 __device__ __forceinline__ v4s_t tr_read(const char* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(p));
@@ -104,65 +105,57 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
   const int lda = GATHER == G_CONV3 ? p.cin : p.K;
   const int acol0 = GATHER == G_CONV3 ? kin0 : k0;
 
-  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(p.G), (short)0, static_cast<int>(static_cast<int64_t>(p.M) * p.N * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(p.A), (short)0, static_cast<int>(p.a_rows * lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(BWDG ? p.gx : p.G), (short)0, static_cast<int>(static_cast<int64_t>(p.M) * p.N * 2),
-      0x00020000);
+  const i32x4_t wG = rsrc_words(p.G, static_cast<uint32_t>(static_cast<int64_t>(p.M) * p.N * 2));
+  const i32x4_t wA = rsrc_words(p.A, static_cast<uint32_t>(p.a_rows * lda * 2));
+  const i32x4_t wX = rsrc_words(BWDG ? p.gx : p.G, static_cast<uint32_t>(static_cast<int64_t>(p.M) * p.N * 2));
 
-  // DMA instruction i of this wave: panel (G panels first, then A), 8-row group
+  // DMA piece i of this wave: panel kind (0 G, 1 A, 2 gx -- wave-uniform), the
+  // lane's row within the 64-row step and its 16-B chunk's byte offset in the row
   const int lrow = lane >> 3;
-  uint32_t gcol[IPW];  // byte offset of this lane's 16-B chunk within its row
+  uint32_t gcol[IPW];
+  int prow[IPW], pkind[IPW];
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int g = wave * IPW + i;
     const int panel = g / (MK / 8), r = 8 * (g % (MK / 8)) + lrow;
     const int c = (lane & 7) ^ (((r >> 1) & 1) * 4);
+    prow[i] = r;
+    pkind[i] = panel < PN ? 0 : panel < PN + PK ? 1 : 2;
     gcol[i] = panel < PN        ? static_cast<uint32_t>((n0 + 64 * panel + 8 * c) * 2)
               : panel < PN + PK ? static_cast<uint32_t>((acol0 + 64 * (panel - PN) + 8 * c) * 2)
                                 : static_cast<uint32_t>((n0 + 64 * (panel - PN - PK) + 8 * c) * 2);
   }
 
-  auto issue = [&](int m0, int stage) {
-    char* base = lds + stage * STAGE;
-#pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int g = wave * IPW + i;
-      const int panel = g / (MK / 8), r = 8 * (g % (MK / 8)) + lrow;
-      lds_void_t* dst = (lds_void_t*)(base + g * 1024);
-      const int m = m0 + r;
-      // rows past M: an explicit out-of-range voffset (the range check covers
-      // the VGPR offset; soffset stays 0)
-      if (panel < PN) {
-        dma16(rG, dst, m < p.M ? static_cast<uint32_t>(m * p.N * 2) + gcol[i] : kOOB, 0);
-      } else if (BWDG && panel >= PN + PK) {
-        dma16(rX, dst, m < p.M ? static_cast<uint32_t>(m * p.N * 2) + gcol[i] : kOOB, 0);
-      } else if constexpr (GATHER == G_DENSE) {
-        dma16(rA, dst, m < p.M ? static_cast<uint32_t>(m * p.K * 2) + gcol[i] : kOOB, 0);
-      } else {
-        uint32_t off = kOOB;
-        if (m < p.M) {
-          const int hw = p.Hout * p.Wout;
-          const int nimg = static_cast<int>(__umulhi(static_cast<uint32_t>(m), p.mg_hw));
-          const int rem = m - nimg * hw;
-          const int oh = static_cast<int>(__umulhi(static_cast<uint32_t>(rem), p.mg_w));
-          const int ow = rem - oh * p.Wout;
-          if constexpr (GATHER == G_STRIDED) {
-            off = static_cast<uint32_t>(((nimg * p.Hin + oh * p.stride) * p.Win + ow * p.stride) * lda * 2) + gcol[i];
-          } else {
-            const int ih = oh * p.stride + tr3 - 1, iw = ow * p.stride + tq3 - 1;
-            if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.Hin) &&
-                static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win))
-              off = static_cast<uint32_t>(((nimg * p.Hin + ih) * p.Win + iw) * lda * 2) + gcol[i];
-          }
+  // one piece of the step at rows m0.. into `stage` (rows past M: an explicit
+  // out-of-range voffset -- the range check covers the VGPR offset)
+  auto piece = [&](int i, int m0, int stage) {
+    const int g = wave * IPW + i;
+    lds_void_t* dst = (lds_void_t*)(lds + stage * STAGE + g * 1024);
+    const int m = m0 + prow[i];
+    if (pkind[i] != 1) {
+      dma16(pkind[i] == 0 ? wG : wX, dst, m < p.M ? static_cast<uint32_t>(m * p.N * 2) + gcol[i] : kOOB, 0);
+    } else if constexpr (GATHER == G_DENSE) {
+      dma16(wA, dst, m < p.M ? static_cast<uint32_t>(m * p.K * 2) + gcol[i] : kOOB, 0);
+    } else {
+      uint32_t off = kOOB;
+      if (m < p.M) {
+        const int hw = p.Hout * p.Wout;
+        const int nimg = static_cast<int>(__umulhi(static_cast<uint32_t>(m), p.mg_hw));
+        const int rem = m - nimg * hw;
+        const int oh = static_cast<int>(__umulhi(static_cast<uint32_t>(rem), p.mg_w));
+        const int ow = rem - oh * p.Wout;
+        if constexpr (GATHER == G_STRIDED) {
+          off = static_cast<uint32_t>(((nimg * p.Hin + oh * p.stride) * p.Win + ow * p.stride) * lda * 2) + gcol[i];
+        } else {
+          const int ih = oh * p.stride + tr3 - 1, iw = ow * p.stride + tq3 - 1;
+          if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.Hin) &&
+              static_cast<unsigned>(iw) < static_cast<unsigned>(p.Win))
+            off = static_cast<uint32_t>(((nimg * p.Hin + ih) * p.Win + iw) * lda * 2) + gcol[i];
         }
-        dma16(rA, dst, off, 0);
       }
+      dma16(wA, dst, off, 0);
     }
   };
-
   // transposed fragment reads: lane (group g = lane >> 4, q = (lane & 15) >> 2,
   // pp = lane & 3) reads rows 16s + 8(g >> 1) + q (+4) at column
   // 16(g & 1) + 4pp of its 32-column fragment
@@ -220,59 +213,109 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
 #pragma unroll
     for (int j = 0; j < TK; ++j) acc[i][j] = f32x16_t{};
 
-  if (mbeg < mend) issue(mbeg, 0);
-  int st = 0;
-  for (int m0 = mbeg; m0 < mend; m0 += MK) {
-    __syncthreads();  // stage st landed everywhere; the other stage is free
-    if (m0 + MK < mend) issue(m0 + MK, st ^ 1);
-    const char* S = lds + st * STAGE;
-    const bool tail = (PRO || BWDG) && m0 + MK > mend;  // rows past the range: zero after the prologue
+  // One 64-row step on stage S: raw fragments double-buffered (substep s + 1's
+  // transposed reads issued before substep s's MFMAs, its prologue applied at
+  // the top of substep s + 1), and with ISSUE the next step's DMA pieces spread
+  // over the first half of the MFMAs -- their address math and issue run in the
+  // MFMA shadow, not in a burst after the barrier (csrc/igemm.hip, round 6).
+  constexpr int NMF = 4 * TN * TK;
+  // spread the pieces only where there are at least two MFMAs per piece; the
+  // small, bandwidth-bound tiles (64-wide at K or N = 64: 8 MFMAs per wave
+  // for 6 pieces) keep the burst right after the barrier -- spreading their
+  // loads cost 8-14 % there (profiles/r06_wgrad_probe.txt)
+  constexpr int SPAN = NMF < 2 * IPW ? 1 : (NMF / 2 > IPW ? NMF / 2 : IPW);
+  auto raw = [&](const char* S, int s, bf16x8_t (&gf)[TN], bf16x8_t (&xf)[TN], bf16x8_t (&af)[TK]) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8_t gf[TN], af[TK];
+    for (int i = 0; i < TN; ++i) {
+      const char* b = S + goff[i] + s * 16 * 128;
+      gf[i] = frag8(tr_read(b), tr_read(b + 4 * 128));
+      if constexpr (BWDG) {
+        const char* bx = b + (PN + PK) * PANEL;
+        xf[i] = frag8(tr_read(bx), tr_read(bx + 4 * 128));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TK; ++j) {
+      const char* b = S + aoff[j] + s * 16 * 128;
+      af[j] = frag8(tr_read(b), tr_read(b + 4 * 128));
+    }
+  };
+  auto prologue = [&](int m0, int s, bool tail, bf16x8_t (&gf)[TN], const bf16x8_t (&xf)[TN], bf16x8_t (&af)[TK]) {
+    (void)m0; (void)s; (void)tail; (void)gf; (void)xf; (void)af;
+    const int mrow = m0 + 16 * s + 8 * (lane >> 5);
+    (void)mrow;
+    if constexpr (BWDG) {
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
-        const char* b = S + goff[i] + s * 16 * 128;
-        gf[i] = frag8(tr_read(b), tr_read(b + 4 * 128));
-        if constexpr (BWDG) {
-          const char* bx = b + (PN + PK) * PANEL;
-          const bf16x8_t xf = frag8(tr_read(bx), tr_read(bx + 4 * 128));
-          float f[8], x[8];
-          unpack8(__builtin_bit_cast(uint4, gf[i]), f);
-          unpack8(__builtin_bit_cast(uint4, xf), x);
-          const int mrow = m0 + 16 * s + 8 * (lane >> 5);
+        float f[8], x[8];
+        unpack8(__builtin_bit_cast(uint4, gf[i]), f);
+        unpack8(__builtin_bit_cast(uint4, xf[i]), x);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float o = fmaf(gk[i], f[e], fmaf(gc1[i], x[e], gc0[i]));  // bn_bwd_apply_kernel's nesting
-            f[e] = (!tail || mrow + e < mend) ? o : 0.f;
-          }
-          gf[i] = __builtin_bit_cast(bf16x8_t, pack8(f));
+        for (int e = 0; e < 8; ++e) {
+          const float o = fmaf(gk[i], f[e], fmaf(gc1[i], x[e], gc0[i]));  // bn_bwd_apply_kernel's nesting
+          f[e] = (!tail || mrow + e < mend) ? o : 0.f;
         }
+        gf[i] = __builtin_bit_cast(bf16x8_t, pack8(f));
       }
+    }
+    if constexpr (PRO) {
 #pragma unroll
       for (int j = 0; j < TK; ++j) {
-        const char* b = S + aoff[j] + s * 16 * 128;
-        af[j] = frag8(tr_read(b), tr_read(b + 4 * 128));
-        if constexpr (PRO) {
-          const uint4 raw = __builtin_bit_cast(uint4, af[j]);
-          float f[8];
-          unpack8(raw, f);
-          const int mrow = m0 + 16 * s + 8 * (lane >> 5);
+        float f[8];
+        unpack8(__builtin_bit_cast(uint4, af[j]), f);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float o = fmaf(f[e], psc[j], psf[j]);
-            f[e] = (o > 0.f && (!tail || mrow + e < mend)) ? o : 0.f;
-          }
-          af[j] = __builtin_bit_cast(bf16x8_t, pack8(f));
+        for (int e = 0; e < 8; ++e) {
+          const float o = fmaf(f[e], psc[j], psf[j]);
+          f[e] = (o > 0.f && (!tail || mrow + e < mend)) ? o : 0.f;
         }
+        af[j] = __builtin_bit_cast(bf16x8_t, pack8(f));
       }
+    }
+  };
+  auto step = [&](const char* S, int m0, auto issue_tag, int next_stage) {
+    constexpr bool ISSUE = decltype(issue_tag)::value;
+    const bool tail = (PRO || BWDG) && m0 + MK > mend;  // rows past the range: zero after the prologue
+    bf16x8_t gf[2][TN], xf[2][TN], af[2][TK];
+    raw(S, 0, gf[0], xf[0], af[0]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      prologue(m0, s, tail, gf[s & 1], xf[s & 1], af[s & 1]);
+      if (s < 3) raw(S, s + 1, gf[(s + 1) & 1], xf[(s + 1) & 1], af[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
-        for (int j = 0; j < TK; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[i], af[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TK; ++j) {
+          const int mi = (s * TN + i) * TK + j;
+          if constexpr (ISSUE && SPAN == 1) {
+            if (mi == 0) {
+#pragma unroll
+              for (int pi = 0; pi < IPW; ++pi) piece(pi, m0 + MK, next_stage);
+            }
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[s & 1][i], af[s & 1][j], acc[i][j], 0, 0, 0);
+          if constexpr (ISSUE && SPAN > 1) {
+#pragma unroll
+            for (int pi = 0; pi < IPW; ++pi)
+              if (pi * SPAN / IPW == mi) piece(pi, m0 + MK, next_stage);
+          }
+        }
     }
-    st ^= 1;
+  };
+  using yes = std::integral_constant<bool, true>;
+  using no = std::integral_constant<bool, false>;
+  if (mbeg < mend) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) piece(i, mbeg, 0);
+    int st = 0, m0 = mbeg;
+    // the last step is peeled (no DMA): one loop body, the accumulators keep their registers
+    for (; m0 + MK < mend; m0 += MK) {
+      publish_stage();
+      step(lds + st * STAGE, m0, yes{}, st ^ 1);
+      st ^= 1;
+    }
+    publish_stage();
+    step(lds + st * STAGE, m0, no{}, 0);
   }
   // D[n][k]: column k = lane & 31, rows n = (r&3) + 8(r>>2) + 4(lane>>5); this
   // split's partial tile goes to its own fp32 slab (reduced in a fixed order)

@@ -14,6 +14,7 @@ main_prio           -1          HIP priority of the step's compute stream
 loss_allreduce      1           sum the step loss over ranks (RCCL) every step
 comm_probe          1           time the first collective (RCCL bootstrap) apart
 comm_overlap        1           run that bootstrap on a helper thread during the model build
+comm_defer_w1       1           world 1: build the communicator after the first step instead
 world1_pg           1           build a one-rank process group at world 1
 pg_eager            0           bind the RCCL communicator at init_process_group
 ddp_world1          0           world-1 DDP rehearsal: 0 | 1 | copy (parallel/ddp.py)

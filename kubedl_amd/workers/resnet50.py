@@ -140,6 +140,9 @@ class ResNetTrainer:
         self.batch = batch
         self.last_loss = None
         self._loss_work = None
+        # (world 1: the caller may build the communicator after the first step;
+        # until then the loss "sum" over the one rank is the loss itself)
+        self.defer_collectives = False
         self._loss_sum = None
         self._loss_div = 1
 
@@ -191,7 +194,7 @@ class ResNetTrainer:
         self.last_loss = loss  # this rank's loss (returned)
         self._loss_sum = loss
         self._loss_div = 1
-        if dist.is_initialized() and _LOSS_ALLREDUCE:
+        if dist.is_initialized() and _LOSS_ALLREDUCE and not self.defer_collectives:
             # the step's loss summed over ranks (reporting); at world 1 this is
             # the collective that keeps the RCCL path exercised in every step
             self._loss_sum = loss.clone()
