@@ -113,4 +113,11 @@ __host__ __forceinline__ int mem_bound_grid(int64_t work_items, int block, int c
   return static_cast<int>(g);
 }
 
+// Weight-gradient split slabs (fp32 partial tiles, summed by wgrad_reduce_kernel
+// right after): plain cacheable stores, so the reduce finds them in the
+// Infinity Cache -- nontemporal ones (streamed past the caches) measured
+// 0.3 % slower per ResNet-50 step, both of two interleaved rounds
+// (profiles/r06_slab_blocks_sweep.txt).
+__device__ __forceinline__ void slab_store(float* p, float v) { *p = v; }
+
 }  // namespace kdl

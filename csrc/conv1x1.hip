@@ -600,7 +600,7 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad1x1_kernel(
       for (int r = 0; r < 16; ++r) {
         const int n = n0 + wn0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
         const int k = k0 + wk0 + j * 32 + fr;
-        __builtin_nontemporal_store(acc[i][j][r], slab + static_cast<int64_t>(n) * K + k);
+        slab_store(slab + static_cast<int64_t>(n) * K + k, acc[i][j][r]);
       }
 }
 
@@ -628,8 +628,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(float* __restric
   if (i4 < nk) {
 #pragma unroll 4
     for (int sp = grp; sp < cnt; sp += kRedGroups) {
-      const f32x4_t v = __builtin_nontemporal_load(
-          reinterpret_cast<const f32x4_t*>(dw32 + static_cast<int64_t>(base + sp) * stride * nk + i4));
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(dw32 + static_cast<int64_t>(base + sp) * stride * nk + i4);
       a.x += v[0]; a.y += v[1]; a.z += v[2]; a.w += v[3];
     }
   }
@@ -1167,7 +1166,7 @@ __global__ __launch_bounds__(kThreads, 2) void gram_kernel(const bf16_t* __restr
       for (int r = 0; r < 16; ++r) {
         const int n = wn0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
         const int k = wk0 + j * 32 + fr;
-        __builtin_nontemporal_store(acc[i][j][r], slab + n * T + k);
+        slab_store(slab + n * T + k, acc[i][j][r]);
       }
 }
 

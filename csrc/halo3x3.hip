@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kWgNT, 1) void halo3x3_wgrad_kernel(const bf16_t* G
       for (int r = 0; r < 16; ++r) {
         const float v = acc[tap][r] + X[((pw * 9 + tap) * 16 + r) * 64 + lane];
         const int co = 32 * cob + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        __builtin_nontemporal_store(v, slab + co * 576 + tap * 64 + 32 * cib + fr);
+        slab_store(slab + co * 576 + tap * 64 + 32 * cib + fr, v);
       }
   }
 }

@@ -484,7 +484,7 @@ __global__ __launch_bounds__(kNT, 4) void stem_wgrad_kernel(const bf16_t* __rest
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * fh;
-      __builtin_nontemporal_store(acc[i][r], slab + co * kK + 32 * wave + fr);
+      slab_store(slab + co * kK + 32 * wave + fr, acc[i][r]);
     }
 }
 

@@ -329,7 +329,7 @@ __global__ __launch_bounds__(64 * WN * WK, (WN * WK == 4) ? 2 : 1) void wgrad_dm
       for (int r = 0; r < 16; ++r) {
         const int n = n0 + wn0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
         const int k = k0 + wk0 + j * 32 + fr;
-        __builtin_nontemporal_store(acc[i][j][r], slab + static_cast<int64_t>(n) * p.K + k);
+        slab_store(slab + static_cast<int64_t>(n) * p.K + k, acc[i][j][r]);
       }
 }
 
