@@ -639,6 +639,10 @@ static hipError_t hist_lds_attr() {
     const int bytes = static_cast<int>(kFTile * 256 * 2 * sizeof(float));
     RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<4>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<8>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_wq_kernel<16>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
     attr_set = true;
   }
   return hipSuccess;
@@ -662,8 +666,18 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
   RETURN_IF_HIP_ERR(hist_lds_attr());
   dim3 grid(max_chunks, (F + fp - 1) / fp);
   const size_t lds = static_cast<size_t>(fp) * B * 2 * sizeof(int);
-  hipLaunchKernelGGL((hist_build_wq_kernel<4>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows,
-                     blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist);
+  // row slots in flight per thread (KDL_TUNE gbdt_unroll: 4 | 8 | 16): the build waits on its
+  // dependent row -> bins / g / h loads (PMC: waves parked 58 % of their cycles at 4); 2M x 28,
+  // depth 6: 637-642 / 680-694 / 701-712 boosting rounds/s at 4 / 8 / 16, and 32 slots or 1024 /
+  // 4096 rows per chunk no better than 16 (profiles/r06_gbdt_unroll.txt)
+  static const int unroll = tune_int("gbdt_unroll", 16);
+#define KDL_HIST_WQ(U)                                                                                         \
+  hipLaunchKernelGGL((hist_build_wq_kernel<U>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows, \
+                     blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist)
+  if (unroll >= 16) KDL_HIST_WQ(16);
+  else if (unroll >= 8) KDL_HIST_WQ(8);
+  else KDL_HIST_WQ(4);
+#undef KDL_HIST_WQ
   return hipGetLastError();
 }
 

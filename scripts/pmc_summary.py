@@ -64,6 +64,7 @@ def main() -> int:
     ap.add_argument("root")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--kdl", action="store_true", help="only kdl:: kernels")
+    ap.add_argument("--steps", type=int, default=0, help="steps in the run: print per-step GB and TFLOP totals")
     a = ap.parse_args()
     passes = {}
     for p in ("P1", "P2", "P3"):
@@ -95,6 +96,8 @@ def main() -> int:
         lds = g.get("SQ_ACTIVE_INST_LDS", 0)
         hit, miss = g.get("TCC_HIT_sum", 0), g.get("TCC_MISS_sum", 0)
         rows.append(dict(
+            rd=2 * g.get("FETCH_SIZE", 0) * 1024, wr=g.get("WRITE_SIZE", 0) * 1024,
+            flop=g.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) * 1024,
             name=name, n=int(g["n"]), us=g["ns"] / g["n"] / 1e3, tot_ms=g["ns"] / 1e6,
             gbs=gbs, hbm=100 * gbs / 6300, tfs=tfs, mfma=100 * tfs / 2500,
             ldsc=(100 * g.get("SQ_LDS_BANK_CONFLICT", 0) / lds) if lds else 0.0,
@@ -109,6 +112,10 @@ def main() -> int:
               f"{r['gbs']:>6.0f} {r['hbm']:>5.1f} {r['tfs']:>6.0f} {r['mfma']:>5.1f} "
               f"{bound:>5} {r['ldsc']:>5.1f} {r['l2']:>5.1f}")
     print(f"total serialised kernel time {tot:.1f} ms over {sum(r['n'] for r in rows)} dispatches")
+    if a.steps:
+        rd, wr, fl = (sum(r[k] for r in rows) / a.steps for k in ("rd", "wr", "flop"))
+        print(f"per step ({a.steps} steps): read {rd / 1e9:.2f} GB + write {wr / 1e9:.2f} GB = {(rd + wr) / 1e9:.1f} GB; "
+              f"MFMA work {fl / 1e12:.3f} TFLOP")
     return 0
 
 
