@@ -21,9 +21,10 @@
 //
 // Device-resident tree growth (no host round trip inside a tree; the host only
 // enqueues a fixed kernel sequence per level):
-//   nodes live in heap order (level d = heap ids [2^d-1, 2^(d+1)-1)); each row
-//   carries its heap node id (``node_of_row``) and ``rows`` keeps rows grouped by
-//   node, node i of the level owning rows[lo[i] .. hi[i]).  Per level:
+//   nodes live in heap order (level d = heap ids [2^d-1, 2^(d+1)-1)); ``rows``
+//   keeps rows grouped by node, node i of the level owning rows[lo[i] .. hi[i]),
+//   and ``node_pos`` holds the heap node id of the row at each position (moved
+//   with the rows; the row-indexed ``node_of_row`` is written at the tree's end).  Per level:
 //   split_find -> gbdt_decide (argmax over features, leaf weight, tree arrays)
 //   -> gbdt_route_flags (1 = goes right) -> inclusive scan of the flags
 //   -> gbdt_partition (stable in-segment partition: left rows keep their
@@ -364,15 +365,18 @@ __global__ __launch_bounds__(256) void decide_kernel(
 }
 
 // flag[p] = 1 when the row at position p belongs to a splitting node of the
-// level and goes right.
+// level and goes right.  ``node_pos`` is POSITION-indexed (the heap node of the
+// row at position p, moved with the rows by partition_kernel): a coalesced read
+// where a row-indexed node id was a dependent random gather (both kernels are
+// latency-bound: waves parked ~90 % of their cycles, scripts/gpu_r06_gbdt_pmc.sh).
 __global__ __launch_bounds__(256) void route_flags_kernel(
-    const uint8_t* __restrict__ bins, const int32_t* __restrict__ rows, const int32_t* __restrict__ node_of_row,
+    const uint8_t* __restrict__ bins, const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos,
     const int32_t* __restrict__ split, const int32_t* __restrict__ t_feat, const int32_t* __restrict__ t_bin,
     int F, int n, int h0, int L, int32_t* __restrict__ flag) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= n) return;
   const int row = rows[p];
-  const int i = node_of_row[row] - h0;
+  const int i = node_pos[p] - h0;
   int r = 0;
   if (i >= 0 && i < L && split[i]) {
     const int h = h0 + i;
@@ -384,13 +388,14 @@ __global__ __launch_bounds__(256) void route_flags_kernel(
 // stable in-segment partition by flag (sc = inclusive scan of flag over all
 // positions): left rows first, then right rows, each in their old order.
 __global__ __launch_bounds__(256) void partition_kernel(
-    const int32_t* __restrict__ rows, int32_t* __restrict__ node_of_row, const int32_t* __restrict__ split,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ split,
     const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, const int32_t* __restrict__ flag,
-    const int32_t* __restrict__ sc, int n, int h0, int L, int32_t* __restrict__ rows_next) {
+    const int32_t* __restrict__ sc, int n, int h0, int L, int32_t* __restrict__ rows_next,
+    int32_t* __restrict__ node_pos_next) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= n) return;
   const int row = rows[p];
-  const int hn = node_of_row[row];
+  const int hn = node_pos[p];
   const int i = hn - h0;
   if (i >= 0 && i < L && split[i]) {
     const int s0 = lo[i], s1 = hi[i];
@@ -407,9 +412,10 @@ __global__ __launch_bounds__(256) void partition_kernel(
       child = 2 * hn + 1;
     }
     rows_next[np] = row;
-    node_of_row[row] = child;
+    node_pos_next[np] = child;
   } else {
     rows_next[p] = row;
+    node_pos_next[p] = hn;
   }
 }
 
@@ -537,7 +543,7 @@ __global__ __launch_bounds__(256) void grad_hess_kernel(const float* __restrict_
 // A tree's state reset in one launch (was eight torch fills / copies per tree):
 // rows = iota, every row at the root, empty heap arrays, the root's bounds and
 // zeroed root histogram.
-__global__ __launch_bounds__(256) void tree_init_kernel(int32_t* __restrict__ rows, int32_t* __restrict__ node_of_row,
+__global__ __launch_bounds__(256) void tree_init_kernel(int32_t* __restrict__ rows, int32_t* __restrict__ node_pos,
                                                         int N, int32_t* __restrict__ feat, int32_t* __restrict__ tbin,
                                                         float* __restrict__ thr, float* __restrict__ val, int heap,
                                                         int32_t* __restrict__ exists0, int32_t* __restrict__ lo0,
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(256) void tree_init_kernel(int32_t* __restrict__ ro
   const int t0 = blockIdx.x * 256 + threadIdx.x;
   for (int i = t0; i < N; i += stride) {
     rows[i] = i;
-    node_of_row[i] = 0;
+    node_pos[i] = 0;
   }
   for (int i = t0; i < heap; i += stride) {
     feat[i] = -1;
@@ -563,7 +569,17 @@ __global__ __launch_bounds__(256) void tree_init_kernel(int32_t* __restrict__ ro
   }
 }
 
-// pred[r * ld + k] += val[node_of_row[r]] (the tree's leaf values into the margins)
+// the row-indexed leaf of every row: node_of_row[rows[p]] = node_pos[p] (a
+// scatter of plain stores), then pred[r * ld + k] += val[node_of_row[r]] with
+// coalesced margins -- one position-ordered read-modify-write of pred measured
+// 50 us per tree against ~20 for the pair
+__global__ __launch_bounds__(256) void leaf_scatter_kernel(const int32_t* __restrict__ rows,
+                                                           const int32_t* __restrict__ node_pos, int N,
+                                                           int32_t* __restrict__ node_of_row) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p < N) node_of_row[rows[p]] = node_pos[p];
+}
+
 __global__ __launch_bounds__(256) void leaf_add_kernel(float* __restrict__ pred, int ld, int k,
                                                        const float* __restrict__ val,
                                                        const int32_t* __restrict__ node_of_row, int N) {
@@ -627,9 +643,14 @@ hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float
   return hipGetLastError();
 }
 
+// features per block of the quantised build (a power of two up to the wave
+// width); KDL_TUNE gbdt_ftile caps it below F: more, smaller blocks (LDS fp x B
+// x 8 bytes each, more resident per CU) at the price of re-reading each row's
+// index and g / h once per feature tile
 static int hist_fp(int F) {
+  static const int cap = [] { const int v = tune_int("gbdt_ftile", kFTile); return v < 1 ? 1 : v > kFTile ? kFTile : v; }();
   int fp = 1;
-  while (fp < F && fp < kFTile) fp <<= 1;
+  while (fp < F && fp < cap) fp <<= 1;
   return fp;
 }
 
@@ -691,21 +712,21 @@ hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot,
   return hipGetLastError();
 }
 
-hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_of_row,
+hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos,
                             const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
                             int L, int32_t* flag, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(route_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bins, rows, node_of_row, split,
+  hipLaunchKernelGGL(route_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bins, rows, node_pos, split,
                      t_feat, t_bin, F, n, h0, L, flag);
   return hipGetLastError();
 }
 
-hipError_t gbdt_partition(const int32_t* rows, int32_t* node_of_row, const int32_t* split, const int32_t* lo,
+hipError_t gbdt_partition(const int32_t* rows, const int32_t* node_pos, const int32_t* split, const int32_t* lo,
                           const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
-                          int32_t* rows_next, hipStream_t s) {
+                          int32_t* rows_next, int32_t* node_pos_next, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(partition_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, node_of_row, split, lo, hi,
-                     flag, sc, n, h0, L, rows_next);
+  hipLaunchKernelGGL(partition_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, node_pos, split, lo, hi,
+                     flag, sc, n, h0, L, rows_next, node_pos_next);
   return hipGetLastError();
 }
 
@@ -755,7 +776,7 @@ hipError_t gbdt_route_rows(const uint8_t* bins, const int32_t* rows, const int32
   return hipGetLastError();
 }
 
-hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_of_row, int N, int32_t* feat, int32_t* tbin, float* thr,
+hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_pos, int N, int32_t* feat, int32_t* tbin, float* thr,
                           float* val, int heap, int32_t* exists0, int32_t* lo0, int32_t* hi0, float* root, int root_n,
                           hipStream_t s) {
   if (N < 0 || heap < 0 || root_n < 0) return hipErrorInvalidValue;
@@ -764,15 +785,17 @@ hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_of_row, int N, int32_t* f
   int blocks = (m + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(tree_init_kernel, dim3(blocks), dim3(256), 0, s, rows, node_of_row, N, feat, tbin, thr, val, heap,
+  hipLaunchKernelGGL(tree_init_kernel, dim3(blocks), dim3(256), 0, s, rows, node_pos, N, feat, tbin, thr, val, heap,
                      exists0, lo0, hi0, root, root_n);
   return hipGetLastError();
 }
 
-hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int32_t* node_of_row, int N,
-                         hipStream_t s) {
+hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int32_t* rows, const int32_t* node_pos,
+                         int N, int32_t* node_of_row, hipStream_t s) {
   if (N <= 0) return hipSuccess;
   if (ld < 1 || k < 0 || k >= ld) return hipErrorInvalidValue;
+  if (node_of_row == nullptr) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(leaf_scatter_kernel, dim3((N + 255) / 256), dim3(256), 0, s, rows, node_pos, N, node_of_row);
   hipLaunchKernelGGL(leaf_add_kernel, dim3((N + 255) / 256), dim3(256), 0, s, pred, ld, k, val, node_of_row, N);
   return hipGetLastError();
 }

@@ -74,7 +74,9 @@ class GbdtGrower {
     iota_ = at::arange(N_, io);
     rows_ = at::empty({N_}, io);
     rows_next_ = at::empty({N_}, io);
-    node_of_row_ = at::empty({N_}, io);
+    node_of_row_ = at::zeros({N_}, io);
+    node_pos_ = at::empty({N_}, io);
+    node_pos_next_ = at::empty({N_}, io);
     flag_ = at::empty({N_}, io);
     sc_ = at::empty({N_}, io);
     for (int d = 0; d <= D_; ++d) {
@@ -116,7 +118,7 @@ class GbdtGrower {
     grad_ = grad;
     hess_ = hess;
     auto root = hist_cur_.narrow(0, 0, 1);
-    ck(kdl::gbdt_tree_init(ip(rows_), ip(node_of_row_), N_, ip(feat_), ip(tbin_), fp(thr_), fp(val_),
+    ck(kdl::gbdt_tree_init(ip(rows_), ip(node_pos_), N_, ip(feat_), ip(tbin_), fp(thr_), fp(val_),
                            static_cast<int>(feat_.numel()), ip(exists_[0]), ip(lo_[0]), ip(hi_[0]), fp(root),
                            static_cast<int>(root.numel()), stream()),
        "gbdt_tree_init");
@@ -147,14 +149,15 @@ class GbdtGrower {
                         last ? nullptr : ip(exists_[d + 1]), stream()),
        "gbdt_decide");
     if (last) return at::Tensor();
-    ck(kdl::gbdt_route_flags(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_of_row_), ip(split_), ip(feat_),
+    ck(kdl::gbdt_route_flags(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_pos_), ip(split_), ip(feat_),
                              ip(tbin_), F_, N_, h0, L, ip(flag_), stream()),
        "gbdt_route_flags");
     at::cumsum_out(sc_, flag_, 0, at::kInt);
-    ck(kdl::gbdt_partition(ip(rows_), ip(node_of_row_), ip(split_), ip(lo_[d]), ip(hi_[d]), ip(flag_), ip(sc_), N_,
-                           h0, L, ip(rows_next_), stream()),
+    ck(kdl::gbdt_partition(ip(rows_), ip(node_pos_), ip(split_), ip(lo_[d]), ip(hi_[d]), ip(flag_), ip(sc_), N_,
+                           h0, L, ip(rows_next_), ip(node_pos_next_), stream()),
        "gbdt_partition");
     std::swap(rows_, rows_next_);
+    std::swap(node_pos_, node_pos_next_);
     ck(kdl::gbdt_children(ip(split_), ip(lo_[d]), ip(hi_[d]), ip(sc_), L, ip(lo_[d + 1]), ip(hi_[d + 1]), fp(cnt_),
                           pick ? 1 : 0, ip(build_child_), ip(blo_), ip(bhi_), stream()),
        "gbdt_children");
@@ -204,6 +207,7 @@ class GbdtGrower {
     }
   }
 
+  // the row-indexed leaf of every row, as of the last add_leaf
   at::Tensor node_of_row() const { return node_of_row_; }
   // pred[:, k] += leaf value of each row (pred [N, K] fp32 contiguous)
   void add_leaf(at::Tensor pred, int64_t k) {
@@ -211,8 +215,8 @@ class GbdtGrower {
                     pred.size(0) == N_ && k >= 0 && k < pred.size(1),
                 "GbdtGrower.add_leaf: pred [N, K] fp32 contiguous, 0 <= k < K");
     const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins_.device());
-    ck(kdl::gbdt_leaf_add(fp(pred), static_cast<int>(pred.size(1)), static_cast<int>(k), fp(val_), ip(node_of_row_),
-                          N_, stream()),
+    ck(kdl::gbdt_leaf_add(fp(pred), static_cast<int>(pred.size(1)), static_cast<int>(k), fp(val_), ip(rows_),
+                          ip(node_pos_), N_, ip(node_of_row_), stream()),
        "gbdt_leaf_add");
   }
   // the current tree's heap arrays as one [4, heap] fp32 tensor (feature, split bin, threshold, value)
@@ -234,7 +238,7 @@ class GbdtGrower {
   int N_ = 0, F_ = 0, B_ = 0, D_ = 0, ncut_ = 0, rpb_ = 256;
   float lam_ = 1.f, gamma_ = 0.f, lr_ = 0.3f, mcw_ = 1.f;
   int64_t per_node_ = 0, builds_ = 0, subtracted_ = 0;
-  at::Tensor iota_, rows_, rows_next_, node_of_row_, flag_, sc_, root_lo_hi_;
+  at::Tensor iota_, rows_, rows_next_, node_of_row_, node_pos_, node_pos_next_, flag_, sc_, root_lo_hi_;
   std::vector<at::Tensor> lo_, hi_, exists_;
   at::Tensor split_, gain_, sbin_, gl_, hl_, tot_, feat_, tbin_, thr_, val_;
   at::Tensor hist_cur_, hist_next_, built_, cnt_, build_child_, blo_, bhi_, chunk_off_, gh_max_;

@@ -157,13 +157,13 @@ hipError_t gbdt_split_find(const float* hist, int num_nodes, int F, int B, float
 // gh_max: {max |g|, max h} of the rows (gbdt_gh_absmax): the fixed-point scale
 // of the quantised per-block sums
 hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* out, hipStream_t s);
-// a tree's state reset (rows = iota, node_of_row = 0, heap arrays -1 / 0, root bounds, root histogram)
-hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_of_row, int N, int32_t* feat, int32_t* tbin, float* thr,
+// a tree's state reset (rows = iota, node_pos = 0, heap arrays -1 / 0, root bounds, root histogram)
+hipError_t gbdt_tree_init(int32_t* rows, int32_t* node_pos, int N, int32_t* feat, int32_t* tbin, float* thr,
                           float* val, int heap, int32_t* exists0, int32_t* lo0, int32_t* hi0, float* root, int root_n,
                           hipStream_t s);
-// pred[r * ld + k] += val[node_of_row[r]]
-hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int32_t* node_of_row, int N,
-                         hipStream_t s);
+// node_of_row[rows[p]] = node_pos[p], then pred[r * ld + k] += val[node_of_row[r]]
+hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int32_t* rows, const int32_t* node_pos,
+                         int N, int32_t* node_of_row, hipStream_t s);
 // out [4, heap] fp32 = (feat, tbin, thr, val)
 hipError_t gbdt_heap_pack(const int32_t* feat, const int32_t* tbin, const float* thr, const float* val, int heap,
                           float* out, hipStream_t s);
@@ -174,12 +174,13 @@ hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot,
                        const int32_t* exists, int L, int F, int ncut, int h0, int can_split, float lambda,
                        float gamma, float lr, int32_t* t_feat, int32_t* t_bin, float* t_thr, float* t_val,
                        int32_t* split, int32_t* exists_next, hipStream_t s);
-hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_of_row,
+// node_pos: the heap node of the row at each POSITION (moved with the rows by gbdt_partition)
+hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos,
                             const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
                             int L, int32_t* flag, hipStream_t s);
-hipError_t gbdt_partition(const int32_t* rows, int32_t* node_of_row, const int32_t* split, const int32_t* lo,
+hipError_t gbdt_partition(const int32_t* rows, const int32_t* node_pos, const int32_t* split, const int32_t* lo,
                           const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
-                          int32_t* rows_next, hipStream_t s);
+                          int32_t* rows_next, int32_t* node_pos_next, hipStream_t s);
 hipError_t gbdt_children(const int32_t* split, const int32_t* lo, const int32_t* hi, const int32_t* sc, int L,
                          int32_t* lo_next, int32_t* hi_next, float* cnt, int pick, int32_t* build_child,
                          int32_t* blo, int32_t* bhi, hipStream_t s);
