@@ -593,6 +593,30 @@ std::vector<at::Tensor> relu_bwd_dbias(const at::Tensor& dy, const c10::optional
   return {dz, db};
 }
 
+// dz_prev = (dz W) * [y > 0], db_prev = sum_m dz_prev (bf16): the tower's data gradient through the
+// previous layer's ReLU with that layer's bias gradient, in one launch (replaces gemm + relu_bwd_dbias)
+std::vector<at::Tensor> gemm_dgrad_relu(const at::Tensor& dz, const at::Tensor& w, const at::Tensor& y) {
+  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  y.scalar_type() == at::kBFloat16, "gemm_dgrad_relu: bf16 GPU operands");
+  TORCH_CHECK(dz.dim() == 2 && w.dim() == 2 && dz.size(1) == w.size(0), "gemm_dgrad_relu: dz [M, K], W [K, N]");
+  TORCH_CHECK(dz.is_contiguous() && w.is_contiguous() && y.is_contiguous(), "gemm_dgrad_relu: contiguous operands");
+  const int64_t M = dz.size(0), N = w.size(1), K = dz.size(1);
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm_dgrad_relu: K % 8 == 0 and N % 8 == 0");
+  TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == N, "gemm_dgrad_relu: y [M, N]");
+  TORCH_CHECK((N + 63) / 64 <= (1 << 14) - 8192, "gemm_dgrad_relu: N too wide for the ticket slots");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(dz.device());
+  auto c = at::empty({M, N}, dz.options());
+  auto db = at::empty({N}, dz.options());
+  const int tm = kdl::gemm_dgrad_relu_tiles_m(static_cast<int>(M), static_cast<int>(N));
+  auto part = at::empty({tm, N}, dz.options().dtype(at::kFloat));
+  auto cnt = ticket_counters(dz, 8192);
+  check_hip(kdl::gemm_dgrad_relu(dz.data_ptr(), w.data_ptr(), y.data_ptr(), c.data_ptr(), part.data_ptr<float>(),
+                                 reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), db.data_ptr(), static_cast<int>(M),
+                                 static_cast<int>(N), static_cast<int>(K), cur_stream()),
+            "gemm_dgrad_relu");
+  return {c, db};
+}
+
 static void check_head(const at::Tensor& x, const at::Tensor& w, const char* who) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
               who, ": x bf16 [M,K] contiguous");
@@ -621,7 +645,7 @@ std::vector<at::Tensor> head_bce_fwd(const at::Tensor& x, const at::Tensor& w, c
 }
 
 std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& dlogit,
-                                     double scale, const c10::optional<at::Tensor>& gscale) {
+                                     double scale, const c10::optional<at::Tensor>& gscale, bool relu_x) {
   check_head(x, w, "head_bce_bwd");
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(dlogit.scalar_type() == at::kFloat && dlogit.numel() == M && dlogit.is_contiguous(),
@@ -636,12 +660,20 @@ std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, c
   auto dx = at::empty_like(x), dwp = at::empty({nb, K}, opt), dbp = at::empty({nb}, opt);
   auto dw = at::empty({K}, x.options()), db = at::empty({1}, x.options());  // bf16, summed in block order
   auto cnt = ticket_counters(x, 1);
+  // relu_x: x is a ReLU output; dx masked by x > 0 and dbx = its column sums (bf16 [K])
+  at::Tensor dbxp, dbx;
+  if (relu_x) {
+    dbxp = at::empty({nb, K}, opt);
+    dbx = at::empty({K}, x.options());
+  }
   check_hip(kdl::head_bce_bwd(x.data_ptr(), w.data_ptr(), dlogit.data_ptr<float>(), static_cast<float>(scale),
                               has_g ? gscale->data_ptr<float>() : nullptr, static_cast<int>(M), static_cast<int>(K),
                               dx.data_ptr(), dwp.data_ptr<float>(), dbp.data_ptr<float>(),
                               reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), dw.data_ptr(), db.data_ptr(),
-                              cur_stream()),
+                              cur_stream(), relu_x ? dbxp.data_ptr<float>() : nullptr,
+                              relu_x ? dbx.data_ptr() : nullptr),
             "head_bce_bwd");
+  if (relu_x) return {dx, dw, db, dwp, dbp, dbx};
   return {dx, dw, db, dwp, dbp};
 }
 
@@ -1740,16 +1772,23 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_grad_hess", &gbdt_grad_hess, "boosting round gradient + hessian in one launch (0 reg, 1 logistic, 2 softmax)");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_hist_quant", &gbdt_hist_quant, "the device grower's quantised (fixed-point) histograms (test hook)");
+  m.def("set_gbdt_hist_rows", &kdl::set_gbdt_hist_rows, "quantised hist kernel: 0 slot, 4 / 8 row-per-lane (rows in flight), -2 KDL_TUNE");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");
   m.def("gemm_bias_act", &gemm_bias_act, "MFMA bf16 GEMM C = act(A W^T + b) (trans_w: A W, W [K, N])",
         py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("trans_w") = false);
   m.def("set_ctr_tile", &kdl::set_ctr_tile, "gemm_bias_act tile: -1 by shape, 0/1/2 = 128x128 / 128x64 / 64x64");
   m.def("ctr_tile_for", &kdl::ctr_tile_for, "the gemm_bias_act tile picked for an M x N output");
+  m.def("set_ctr_igemm", &kdl::set_ctr_igemm, "forward gemm_bias_act on igemm: mode 0 off / 1 by tile count / 2 always; cfg -1 by shape",
+        py::arg("mode"), py::arg("cfg") = -1);
+  m.def("ctr_igemm_cfg_for", &kdl::ctr_igemm_cfg_for, "igemm cfg serving a forward M x N x K gemm_bias_act (-1: none)");
+  m.def("gemm_dgrad_relu", &gemm_dgrad_relu, "(dz W) * [y > 0] and its column sums (bf16): data gradient through a ReLU + bias gradient, one launch");
   m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient (deterministic; bf16 or fp32)",
         py::arg("dy"), py::arg("y"), py::arg("db_bf16") = false);
   m.def("head_bce_fwd", &head_bce_fwd, "1-wide logit layer + sigmoid BCE: (logit, dlogit, per-block loss sums)");
-  m.def("head_bce_bwd", &head_bce_bwd, "logit layer backward: (dx, per-block dw partials, per-block db partials)");
+  m.def("head_bce_bwd", &head_bce_bwd,
+        "logit layer backward: (dx, dw, db, per-block dw partials, per-block db partials[, dbx: relu_x])",
+        py::arg("x"), py::arg("w"), py::arg("dlogit"), py::arg("scale"), py::arg("gscale"), py::arg("relu_x") = false);
   m.def("embed_gather", &embed_gather, "embedding row gather into a [B, ld] activation");
   m.def("segment_reduce", &segment_reduce, "sorted segment sum of gradient rows", py::arg("rows"), py::arg("F"),
         py::arg("col0"), py::arg("D"), py::arg("order"), py::arg("seg"), py::arg("ucount") = py::none(),

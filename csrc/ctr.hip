@@ -27,6 +27,7 @@
 //   dx = dlogit * w and per-block fp32 partials of dw / db (reduced in fixed
 //   order by the caller) -- no vendor GEMM for the N=1 layer.
 #include "common.h"
+#include "gemm_epi.h"
 #include "kdl_api.h"
 #include "tune.h"
 
@@ -52,6 +53,21 @@ constexpr int BK = 64;
 constexpr int LDA = BK + 8;  // padded LDS row (bf16 elements)
 constexpr int kThreads = 256;
 
+// Sum of part[r * stride] for r in [0, n), in r order; 16 loads in flight per
+// round (one dependent load per partial made the last block's sum the
+// kernel's critical path: 64 partials x L2 latency)
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ part, int n, int64_t stride) {
+  float a = 0.f;
+  for (int r0 = 0; r0 < n; r0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = r0 + j < n ? part[static_cast<int64_t>(r0 + j) * stride] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a += v[j];
+  }
+  return a;
+}
+
 // BM_ x BN_ tile (128x128, 128x64 or 64x64): 4 waves as 2x2, each wave
 // (BM_/2) x (BN_/2) = I x J MFMA 32x32 blocks.  A 4096-row batch gives a
 // 128x128 tiling only 64-256 tiles on 256 CUs (one wave per SIMD, nothing to
@@ -64,10 +80,18 @@ constexpr int kThreads = 256;
 // ds_read_b64_tr_b16: a 32x32x16 B fragment (8 k of one n per lane) is two
 // transposed reads 4 rows apart.  Row stride 2*BN_ + 64 bytes = 64 or 192 mod 256:
 // the 4 rows of a read land on 4 distinct 16-bank quarters (conflict-free).
-template <bool RELU, int BM_, int BN_, bool BT>
+//
+// DM (data gradient through the previous layer's ReLU, BT only): C = bf16(acc)
+// masked by ymask > 0 (that layer's output), and that layer's bias gradient
+// db[n] = sum_m C[m, n] -- per-tile column sums into part[tile_m][N], the last
+// block of each column of tiles summing them in tile order (deterministic);
+// replaces a separate ReLU-backward + dbias pass over dy (relu_bwd_dbias).
+template <bool RELU, int BM_, int BN_, bool BT, bool DM = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, const float* __restrict__ bias32,
-    const bf16_t* __restrict__ bias16, bf16_t* __restrict__ C, int M, int N, int K, int tiles_n) {
+    const bf16_t* __restrict__ bias16, bf16_t* __restrict__ C, int M, int N, int K, int tiles_n,
+    const bf16_t* __restrict__ ymask = nullptr, float* __restrict__ part = nullptr, unsigned* __restrict__ cnt = nullptr,
+    bf16_t* __restrict__ db = nullptr) {
   constexpr int I = BM_ / 64, J = BN_ / 64;
   constexpr int SA = BM_ / 32, SB = BN_ / 32;  // 16-B chunks per thread per k-tile (rows x 8 chunks / 256)
   constexpr int SBT = BN_ + 32;                // BT: B image row (elements)
@@ -190,6 +214,58 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     __syncthreads();
   }
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  if constexpr (DM) {
+    __shared__ float dred[2][BN_];  // column sums of the two wave rows (wm halves)
+    __shared__ int last;
+    float cs[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int col = n0 + wn + j * 32 + fr;
+      cs[j] = 0.f;
+      bf16_t yv[I][16];
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          yv[i][r] = (row < M && col < N) ? ymask[static_cast<int64_t>(row) * N + col] : bf16_t(0);
+        }
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (row < M && col < N) {
+            const bf16_t v = bf16_to_f32(yv[i][r]) > 0.f ? f32_to_bf16(acc[i][j][r]) : bf16_t(0);
+            C[static_cast<int64_t>(row) * N + col] = v;
+            cs[j] += bf16_to_f32(v);
+          }
+        }
+      cs[j] += __shfl_xor(cs[j], 32, 64);  // lanes fr and fr + 32 hold the same column
+      if (fh == 0) dred[wave >> 1][wn + j * 32 + fr] = cs[j];
+    }
+    __syncthreads();
+    if (t < BN_ && n0 + t < N) part[static_cast<int64_t>(tile_m) * N + n0 + t] = dred[0][t] + dred[1][t];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(cnt + tile_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = tk == static_cast<unsigned>(tiles_m) - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!last) return;
+    if (t < BN_ && n0 + t < N) {
+      db[n0 + t] = f32_to_bf16(ordered_sum(part + n0 + t, tiles_m, N));  // tile order
+    }
+    if (t == 0) __hip_atomic_store(cnt + tile_n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int col = n0 + wn + j * 32 + fr;
@@ -224,21 +300,6 @@ __device__ __forceinline__ void u4_to_f8(const uint4 v, float (&o)[8]) {
 }
 __device__ __forceinline__ uint4 f8_to_u4(const float (&o)[8]) {
   return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
-}
-
-// Sum of part[r * stride] for r in [0, n), in r order; 16 loads in flight per
-// round (one dependent load per partial made the last block's sum the
-// kernel's critical path: 64 partials x L2 latency)
-__device__ __forceinline__ float ordered_sum(const float* __restrict__ part, int n, int64_t stride) {
-  float a = 0.f;
-  for (int r0 = 0; r0 < n; r0 += 16) {
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = r0 + j < n ? part[static_cast<int64_t>(r0 + j) * stride] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) a += v[j];
-  }
-  return a;
 }
 
 // Row-block partial column sums go to part[blockIdx.x][N]; the last block of a
@@ -771,6 +832,11 @@ __global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restr
 // block = 256 threads = 8 row lanes x 32 column groups of 8 (K <= 256 per
 // pass, looped for wider K); rows [blockIdx.x*rpb, +rpb).  dx = g*w (bf16),
 // dw partial[block, k] = sum g*x, db partial[block] = sum g; g = dlogit*scale.
+// MASK: x is the previous layer's ReLU output -- dx = g*w*[x > 0] (the gradient
+// into that layer's pre-activation) and that layer's bias gradient
+// dbx[k] = sum_m bf16(dx[m, k]) from per-block partials dbx_part (replaces a
+// relu_bwd_dbias pass over dx).
+template <bool MASK>
 __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ w,
                                                            const float* __restrict__ dlogit, float scale,
@@ -778,8 +844,10 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
                                                            int K, int rpb, bf16_t* __restrict__ dx,
                                                            float* __restrict__ dw_part, float* __restrict__ db_part,
                                                            unsigned* __restrict__ cnt, bf16_t* __restrict__ dw,
-                                                           bf16_t* __restrict__ db) {
+                                                           bf16_t* __restrict__ db, float* __restrict__ dbx_part,
+                                                           bf16_t* __restrict__ dbx) {
   __shared__ float red[8][257];
+  __shared__ float redx[MASK ? 8 : 1][MASK ? 256 : 1];
   __shared__ int last;
   if (gscale != nullptr) scale *= gscale[0];  // upstream gradient of the loss, read on the device
   const int rl = threadIdx.x >> 5, cg = threadIdx.x & 31;
@@ -789,9 +857,9 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
   for (int kb = 0; kb < K; kb += 256) {
     const int k = kb + cg * 8;
     const bool on = k < K;
-    float wv8[8], s[8];
+    float wv8[8], s[8], sx[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    for (int i = 0; i < 8; ++i) { s[i] = 0.f; sx[i] = 0.f; }
     if (on) Vec<bf16_t, 8>::load(w + k, wv8);
     for (int m = m0 + rl; m < m1; m += 8) {
       const float g = dlogit[m] * scale;
@@ -804,11 +872,19 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
       for (int i = 0; i < 8; ++i) {
         s[i] += g * xv[i];
         d[i] = g * wv8[i];
+        if constexpr (MASK) {
+          d[i] = xv[i] > 0.f ? bf16_to_f32(f32_to_bf16(d[i])) : 0.f;  // the stored (rounded) value
+          sx[i] += d[i];
+        }
       }
       Vec<bf16_t, 8>::store(dx + o, d);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) red[rl][cg * 8 + i] = s[i];
+    if constexpr (MASK) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) redx[rl][cg * 8 + i] = sx[i];
+    }
     if (kb == 0 && cg == 0) red[rl][256] = gsum;
     __syncthreads();
     // fixed-order sum over the 8 row lanes
@@ -818,6 +894,12 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
 #pragma unroll
       for (int r = 0; r < 8; ++r) t += red[r][c];
       dw_part[static_cast<int64_t>(blockIdx.x) * K + kb + c] = t;
+      if constexpr (MASK) {
+        float tx = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) tx += redx[r][c];
+        dbx_part[static_cast<int64_t>(blockIdx.x) * K + kb + c] = tx;
+      }
     }
     if (kb == 0 && threadIdx.x == 0) {
       float t = 0.f;
@@ -845,6 +927,7 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
   for (int k = threadIdx.x; k < K; k += 256) {
     const float t = ordered_sum(dw_part + k, static_cast<int>(gridDim.x), K);
     dw[k] = f32_to_bf16(t);
+    if constexpr (MASK) dbx[k] = f32_to_bf16(ordered_sum(dbx_part + k, static_cast<int>(gridDim.x), K));
   }
   if (threadIdx.x == 0) {
     const float t = ordered_sum(db_part, static_cast<int>(gridDim.x), 1);
@@ -875,13 +958,20 @@ int head_bce_bwd_blocks(int M) {
 
 hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
                         int K, void* dx, float* dw_part, float* db_part, unsigned* cnt, void* dw, void* db,
-                        hipStream_t s) {
+                        hipStream_t s, float* dbx_part, void* dbx) {
   if (M <= 0) return hipSuccess;
+  if ((dbx != nullptr) && (dw == nullptr || dbx_part == nullptr)) return hipErrorInvalidValue;
   const int nb = head_bce_bwd_blocks(M);
   const int rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(head_bce_bwd_kernel, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
-                     static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx), dw_part,
-                     db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db));
+  if (dbx != nullptr)
+    hipLaunchKernelGGL(head_bce_bwd_kernel<true>, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                       static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx),
+                       dw_part, db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), dbx_part,
+                       static_cast<bf16_t*>(dbx));
+  else
+    hipLaunchKernelGGL(head_bce_bwd_kernel<false>, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                       static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx),
+                       dw_part, db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -901,10 +991,48 @@ int ctr_tile_for(int M, int N) {
   return 2;
 }
 
+static int g_ctr_igemm = -2;  // -2: KDL_TUNE ctr_igemm; 0 off, 1 by tile count, 2 every K % 64 / N % 64 shape
+static int g_ctr_igemm_cfg = -2;
+
+void set_ctr_igemm(int mode, int cfg) { g_ctr_igemm = mode; g_ctr_igemm_cfg = cfg; }
+
+// The LDS-DMA implicit-GEMM main loop (csrc/igemm.hip, DMA issued in the MFMA
+// shadow) for the forward layers (B = [N, K]) with at least 128 128x128 tiles:
+// at batch 4096 the 1728 -> 1024 layer 32.6 -> 22.4 us and the 1024 -> 512 one
+// 14.2 -> 11.3 us against the register-staged kernel below; the 512 -> 256 layer
+// (64 tiles) stays there (7.0 vs 8.0 us; profiles/r06_ctr_igemm_probe.txt).
+// -1: not served.
+int ctr_igemm_cfg_for(int M, int N, int K) {
+  if (g_ctr_igemm == -2) g_ctr_igemm = tune_int("ctr_igemm", 1);
+  if (g_ctr_igemm_cfg == -2) g_ctr_igemm_cfg = tune_int("ctr_igemm_cfg", -1);
+  if (g_ctr_igemm <= 0 || K % 64 || N % 64 || M <= 0) return -1;
+  if (g_ctr_igemm_cfg >= 0) return g_ctr_igemm_cfg;
+  if (g_ctr_igemm == 2) return N % 128 == 0 ? 2 : 3;
+  const int64_t t128 = N % 128 == 0 ? static_cast<int64_t>((M + 127) / 128) * (N / 128) : 0;
+  return t128 >= 128 ? 2 : -1;
+}
+
 hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bias_bf16, void* C, int M, int N, int K,
                          bool relu, bool b_kn, hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (b_kn && N % 8) return hipErrorInvalidValue;  // 16-B chunks along N
+  if (!b_kn) {
+    const int icfg = ctr_igemm_cfg_for(M, N, K);
+    if (icfg >= 0) {
+      gemm::GemmParams p{};
+      p.A = static_cast<const bf16_t*>(A);
+      p.B = static_cast<const bf16_t*>(B);
+      p.C = static_cast<bf16_t*>(C);
+      p.M = M;
+      p.N = N;
+      p.K = K;
+      p.a_rows = M;
+      p.shift = bias_bf16 ? nullptr : static_cast<const float*>(bias);
+      p.bias16 = bias_bf16 ? static_cast<const bf16_t*>(bias) : nullptr;
+      const hipError_t e = gemm::igemm(p, relu ? gemm::EPI_BIAS_RELU : gemm::EPI_BIAS, gemm::G_DENSE, icfg, s);
+      if (e != hipErrorInvalidValue) return e;  // InvalidValue: a shape igemm does not take; the kernel below does
+    }
+  }
   auto a = static_cast<const bf16_t*>(A);
   auto b = static_cast<const bf16_t*>(B);
   auto c = static_cast<bf16_t*>(C);
@@ -931,6 +1059,34 @@ hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bi
 #undef CTR_LAUNCH_GBA_T
 #undef CTR_LAUNCH_GBA
   return hipGetLastError();
+}
+
+hipError_t gemm_dgrad_relu(const void* A, const void* B, const void* y, void* C, float* part, unsigned* cnt, void* db,
+                           int M, int N, int K, hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (N % 8) return hipErrorInvalidValue;  // B = W [K, N]: 16-B chunks along N
+  auto a = static_cast<const bf16_t*>(A);
+  auto b = static_cast<const bf16_t*>(B);
+  auto ym = static_cast<const bf16_t*>(y);
+  auto c = static_cast<bf16_t*>(C);
+  auto d = static_cast<bf16_t*>(db);
+  const int cfg = ctr_tile_for(M, N);
+#define CTR_LAUNCH_DM(TM, TN)                                                                                    \
+  do {                                                                                                           \
+    const int tn = (N + TN - 1) / TN, tm = (M + TM - 1) / TM;                                                    \
+    hipLaunchKernelGGL((gemm_bias_act_kernel<false, TM, TN, true, true>), dim3(tn * tm), dim3(kThreads), 0, s, a, b, \
+                       nullptr, nullptr, c, M, N, K, tn, ym, part, cnt, d);                                      \
+  } while (0)
+  if (cfg == 0) CTR_LAUNCH_DM(128, 128);
+  else if (cfg == 1) CTR_LAUNCH_DM(128, 64);
+  else CTR_LAUNCH_DM(64, 64);
+#undef CTR_LAUNCH_DM
+  return hipGetLastError();
+}
+
+int gemm_dgrad_relu_tiles_m(int M, int N) {
+  const int bm = ctr_tile_for(M, N) == 2 ? 64 : 128;
+  return (M + bm - 1) / bm;
 }
 
 int relu_bwd_dbias_rows(int M, int N) {

@@ -290,6 +290,88 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
   }
 }
 
+// Row-per-lane variant (F % 4 == 0): each lane owns whole rows -- its row
+// index, g / h quantised once per row, and the row's fp bin codes as NW = fp / 4
+// dword loads -- so a wave's memory instructions cover 64 rows x fp features;
+// the slot kernel above issues a row-index, g, h and a byte load per 64
+// (row, feature) pairs.  Same chunks, same fixed-point values, same integer
+// block sums (exact, so order-free): the flushed histogram equals the slot
+// kernel's up to the order of the fp32 flush atomics.  LDS holds nf = min(fp, F - f0)
+// feature planes (g [nf][B] then h [nf][B]).
+template <int U, int NW>
+__global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
+    const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
+    int64_t gh_stride, const int32_t* __restrict__ rows, const int32_t* __restrict__ blo,
+    const int32_t* __restrict__ bhi, const int32_t* __restrict__ chunk_off, int nb, int F, int B, int rpb, int fp,
+    const float* __restrict__ gh_max, float* __restrict__ hist, int flush) {
+  extern __shared__ int qlds[];
+  const int c = blockIdx.x;
+  if (c >= chunk_off[nb]) return;  // block-uniform
+  int a = 0, z = nb;
+  while (z - a > 1) {
+    const int m = (a + z) >> 1;
+    if (chunk_off[m] <= c) a = m; else z = m;
+  }
+  const int j = a;
+  const int r0 = blo[j] + (c - chunk_off[j]) * rpb;
+  const int r1 = (r0 + rpb) < bhi[j] ? (r0 + rpb) : bhi[j];
+  const int f0 = blockIdx.y * fp;
+  const int nf = (F - f0) < fp ? (F - f0) : fp;  // a multiple of 4 (F % 4 == 0, fp % 4 == 0)
+  int* qh_pl = qlds + nf * B;
+  const int t = threadIdx.x;
+  const float mg = gh_max[0], mh = gh_max[1];
+  const float sg = mg > 0.f ? kQuantRange / (static_cast<float>(rpb) * mg) : 0.f;
+  const float sh = mh > 0.f ? kQuantRange / (static_cast<float>(rpb) * mh) : 0.f;
+  for (int i = t; i < 2 * nf * B; i += kHistBlock) qlds[i] = 0;
+  __syncthreads();
+  const int nw = nf >> 2;
+  for (int base = r0 + t; base < r1; base += kHistBlock * U) {
+    int row[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = base + u * kHistBlock;
+      row[u] = r < r1 ? rows[r] : -1;
+    }
+    int qg[U], qh[U];
+    uint32_t w[U][NW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = row[u] >= 0 ? row[u] : 0;  // unconditional loads (row 0 for an idle slot)
+      qg[u] = __float2int_rn(grad[rr * gh_stride] * sg);
+      qh[u] = __float2int_rn(hess[rr * gh_stride] * sh);
+      const uint32_t* bw = reinterpret_cast<const uint32_t*>(bins + rr * F + f0);
+#pragma unroll
+      for (int k = 0; k < NW; ++k) w[u][k] = k < nw ? bw[k] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (row[u] < 0) continue;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        if (k >= nw) break;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = (4 * k + q) * B + ((w[u][k] >> (8 * q)) & 255u);
+          atomicAdd(qlds + e, qg[u]);
+          atomicAdd(qh_pl + e, qh[u]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (!flush) {  // timing only (KDL_TUNE gbdt_price_noflush): keep the sums alive, skip the atomics
+    if (t == 0 && qlds[0] == 0x7fffffff) hist[0] = 0.f;
+    return;
+  }
+  float* out = hist + (static_cast<int64_t>(j) * F + f0) * B * 2;
+  const float ig = sg > 0.f ? 1.f / sg : 0.f, ih = sh > 0.f ? 1.f / sh : 0.f;
+  for (int i = t; i < nf * B; i += kHistBlock) {
+    const int vg = qlds[i], vh = qh_pl[i];
+    if (vg != 0) __hip_atomic_fetch_add(out + 2 * i, static_cast<float>(vg) * ig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (vh != 0) __hip_atomic_fetch_add(out + 2 * i + 1, static_cast<float>(vh) * ih, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // {max |g|, max h} over n rows into out[2] (zeroed by the caller): a block max,
 // then one integer atomicMax per value (non-negative floats order as their bits)
 __global__ __launch_bounds__(256) void gh_absmax_kernel(const float* __restrict__ g, const float* __restrict__ h,
@@ -669,6 +751,18 @@ static hipError_t hist_lds_attr() {
   return hipSuccess;
 }
 
+template <int U, int NW>
+static hipError_t rows_lds_attr() {
+  static bool attr_set = false;
+  if (!attr_set) {
+    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_rows_kernel<U, NW>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          static_cast<int>(kFTile * 256 * 2 * sizeof(int))));
+    attr_set = true;
+  }
+  return hipSuccess;
+}
+
 hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* out, hipStream_t s) {
   RETURN_IF_HIP_ERR(hipMemsetAsync(out, 0, 2 * sizeof(float), s));
   if (n <= 0) return hipSuccess;
@@ -677,6 +771,9 @@ hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* ou
   hipLaunchKernelGGL(gh_absmax_kernel, dim3(blocks), dim3(256), 0, s, grad, hess, n, reinterpret_cast<unsigned*>(out));
   return hipGetLastError();
 }
+
+static int g_hist_rows = -2;  // -2: KDL_TUNE gbdt_hist_rows
+void set_gbdt_hist_rows(int u) { g_hist_rows = u; }
 
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
@@ -692,13 +789,38 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
   // depth 6: 637-642 / 680-694 / 701-712 boosting rounds/s at 4 / 8 / 16, and 32 slots or 1024 /
   // 4096 rows per chunk no better than 16 (profiles/r06_gbdt_unroll.txt)
   static const int unroll = tune_int("gbdt_unroll", 16);
-#define KDL_HIST_WQ(U)                                                                                         \
+  // row-per-lane build (KDL_TUNE gbdt_hist_rows: 0 = slot kernel only; else its rows in flight per lane, 4 | 8)
+  if (g_hist_rows == -2) g_hist_rows = tune_int("gbdt_hist_rows", 4);
+  const int rows_u = g_hist_rows;
+  static const bool noflush = tune_int("gbdt_price_noflush", 0) != 0;
+  if (rows_u > 0 && F % 4 == 0 && fp >= 4) {
+    const int nf0 = F < fp ? F : fp;  // the first (largest) tile's planes
+    const size_t lds_r = static_cast<size_t>(nf0) * B * 2 * sizeof(int);
+#define HIST_ROWS_LAUNCH(U, NW)                                                                                        \
+  RETURN_IF_HIP_ERR((rows_lds_attr<U, NW>()));                                                                        \
+  hipLaunchKernelGGL((hist_build_rows_kernel<U, NW>), grid, dim3(kHistBlock), lds_r, s, bins, grad, hess, gh_stride, \
+                     rows, blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist, noflush ? 0 : 1)
+#define HIST_ROWS_BY_U(U)                  \
+  switch (fp / 4) {                         \
+    case 1: HIST_ROWS_LAUNCH(U, 1); break;     \
+    case 2: HIST_ROWS_LAUNCH(U, 2); break;     \
+    case 4: HIST_ROWS_LAUNCH(U, 4); break;     \
+    case 8: HIST_ROWS_LAUNCH(U, 8); break;     \
+    default: HIST_ROWS_LAUNCH(U, 16); break;   \
+  }
+    if (rows_u >= 8) { HIST_ROWS_BY_U(8) }
+    else { HIST_ROWS_BY_U(4) }
+#undef HIST_ROWS_BY_U
+#undef HIST_ROWS_LAUNCH
+    return hipGetLastError();
+  }
+#define HIST_WQ_LAUNCH(U)                                                                                         \
   hipLaunchKernelGGL((hist_build_wq_kernel<U>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows, \
                      blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist)
-  if (unroll >= 16) KDL_HIST_WQ(16);
-  else if (unroll >= 8) KDL_HIST_WQ(8);
-  else KDL_HIST_WQ(4);
-#undef KDL_HIST_WQ
+  if (unroll >= 16) HIST_WQ_LAUNCH(16);
+  else if (unroll >= 8) HIST_WQ_LAUNCH(8);
+  else HIST_WQ_LAUNCH(4);
+#undef HIST_WQ_LAUNCH
   return hipGetLastError();
 }
 

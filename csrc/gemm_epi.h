@@ -16,6 +16,9 @@
 //            the previous block's packed ReLU bits, + bn3 (and downsample BN)
 //            backward sums
 //   RES      g = dgrad + d(identity), no mask (network stem)
+//   BIAS / BIAS_RELU  y = [relu](c + bias[n]) (the CTR tower's dense layers,
+//            csrc/ctr.hip gemm_bias_act; bias fp32 in ``shift`` or bf16 in
+//            ``bias16``; c is the bf16-rounded accumulator)
 // and after its last tile folds the per-thread sums in LDS and adds them to
 // the BN workspace replica of the block (one atomic per channel per block).
 #pragma once
@@ -33,7 +36,7 @@ typedef __attribute__((ext_vector_type(2))) float f2_t;
 
 constexpr int kRep = 32;  // replica count of the BN workspace (== bn_act.hip kReplicas)
 
-enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4 };
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_MASKX = 2, EPI_RESBITS = 3, EPI_RES = 4, EPI_BIAS = 5, EPI_BIAS_RELU = 6 };
 // A-row addressing: dense rows | stride-s 1x1 gather | 3x3 implicit GEMM (pad 1, stride s) |
 // data gradient of a stride-2 3x3 pad-1 conv as four sub-pixel class GEMMs (csrc/igemm.hip)
 // G_STEM (csrc/stem.hip): a tile is 2 output rows x 112 columns of one image
@@ -61,7 +64,8 @@ struct GemmParams {
   const float* bcoef2;    // PRO_RES2: the downsample BN's [2K] scale | shift (LDS after bcoef's [2K])
   bf16_t* aout;           // optional write-through of A' [M, K] (the blocks of output tile 0)
   // epilogue operands
-  const float* shift;   // STATS: [N]
+  const float* shift;   // STATS: [N]; BIAS: fp32 bias [N] (or null)
+  const bf16_t* bias16; // BIAS: bf16 bias [N] (when shift is null; both null: no bias)
   float* acc;           // STATS/MASKX/RESBITS: [kRep][2N]
   const bf16_t* ex;     // MASKX/RESBITS: BN input x [M, N]
   const float* emean;   // [N]
@@ -306,6 +310,16 @@ struct Epilogue {
         em[q] = ld2(p.emean, ch0 + 2 * q);
         if (p.ex2) em2[q] = ld2(p.emean2, ch0 + 2 * q);
       }
+    } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+      if (p.shift) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ea[q] = ld2(p.shift, ch0 + 2 * q);
+      } else if (p.bias16) {
+        f2_t b[4];
+        unpack4x2(ld16(p.bias16 + ch0), b);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ea[q] = b[q];
+      }
     }
   }
 
@@ -355,6 +369,14 @@ struct Epilogue {
               s1[q] += g;
               s2[q] = pfma(g, x[q] - em[q], s2[q]);
               o[q] = pack2(g);
+            }
+            out = make_uint4(o[0], o[1], o[2], o[3]);
+          } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              f2_t y = v[q] + ea[q];
+              if constexpr (EPI == EPI_BIAS_RELU) y = f2_t{y.x > 0.f ? y.x : 0.f, y.y > 0.f ? y.y : 0.f};
+              o[q] = pack2(y);
             }
             out = make_uint4(o[0], o[1], o[2], o[3]);
           } else if constexpr (LR) {  // RESBITS / RES: add d(identity), rounded to bf16

@@ -394,6 +394,8 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     switch (epi) {
       case EPI_RESBITS: return launch<BM, BN, WM, WN, GATHER, EPI_RESBITS, MINB, STAGES, BPC>(p, s);
       case EPI_RES: return launch<BM, BN, WM, WN, GATHER, EPI_RES, MINB, STAGES, BPC>(p, s);
+      case EPI_BIAS: return launch<BM, BN, WM, WN, GATHER, EPI_BIAS, MINB, STAGES, BPC>(p, s);
+      case EPI_BIAS_RELU: return launch<BM, BN, WM, WN, GATHER, EPI_BIAS_RELU, MINB, STAGES, BPC>(p, s);
     }
   }
   return hipErrorInvalidValue;

@@ -167,6 +167,9 @@ hipError_t gbdt_leaf_add(float* pred, int ld, int k, const float* val, const int
 // out [4, heap] fp32 = (feat, tbin, thr, val)
 hipError_t gbdt_heap_pack(const int32_t* feat, const int32_t* tbin, const float* thr, const float* val, int heap,
                           float* out, hipStream_t s);
+// quantised histogram build: 0 = slot kernel (a wave = 64 / fp rows x fp features), 4 | 8 = row-per-lane
+// kernel with that many rows in flight per lane (F % 4 == 0); -2 = KDL_TUNE gbdt_hist_rows
+void set_gbdt_hist_rows(int u);
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
                         int max_chunks, int rpb, int F, int B, const float* gh_max, float* hist, hipStream_t s);
@@ -200,9 +203,19 @@ hipError_t gemm_bias_act(const void* A, const void* B, const void* bias, bool bi
                          bool relu, bool b_kn, hipStream_t s);
 void set_ctr_tile(int t);  // -1 by shape, 0/1/2: 128x128 / 128x64 / 64x64 (csrc/ctr.hip)
 int ctr_tile_for(int M, int N);
+// forward gemm_bias_act on the LDS-DMA igemm loop: 0 off, 1 by tile count, 2 every
+// K % 64 / N % 64 shape; cfg -1 by shape (igemm tile configs 0-4)
+void set_ctr_igemm(int mode, int cfg);
+int ctr_igemm_cfg_for(int M, int N, int K);  // -1: the register-staged kernel
 // part: relu_bwd_dbias_parts(M, N) x [N] fp32 scratch; cnt: (N + 255) / 256 counters,
 // zero before the first call (the kernel re-arms them); db: [N] bf16 (db_bf16) or fp32
 int relu_bwd_dbias_parts(int M, int N);
+// C = (A W) masked by y > 0 (W [K, N]: the data gradient into the previous layer's ReLU output y),
+// db = column sums of C (bf16, deterministic); part: gemm_dgrad_relu_tiles_m(M, N) x [N] fp32
+// scratch; cnt: ceil(N / 64) zeroed ticket counters (re-armed by the kernel)
+int gemm_dgrad_relu_tiles_m(int M, int N);
+hipError_t gemm_dgrad_relu(const void* A, const void* B, const void* y, void* C, float* part, unsigned* cnt, void* db,
+                           int M, int N, int K, hipStream_t s);
 hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* part, unsigned* cnt, void* db, bool db_bf16,
                           int M, int N, hipStream_t s);
 // cnt: one ticket counter, zero before the first call (re-armed by the kernel);
@@ -214,7 +227,9 @@ int head_bce_bwd_blocks(int M);
 // dw / db (bf16 [K] / [1], optional): the partials summed in block order by the last block
 hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float scale, const float* gscale, int M,
                         int K, void* dx, float* dw_part, float* db_part, unsigned* cnt, void* dw, void* db,
-                        hipStream_t s);
+                        hipStream_t s, float* dbx_part = nullptr, void* dbx = nullptr);
+// dbx (bf16 [K], needs dw and dbx_part [blocks][K]): x is a ReLU output -- dx is masked by x > 0
+// and dbx = its column sums (the bias gradient of the layer that produced x)
 // out[b, col0 + f*D : +D] = bf16(table[uniq[inv[b*F + f]]]) (fp32 table, bf16 out)
 hipError_t embed_gather_cast(const void* table, bool table_bf16, const int64_t* uniq, const int64_t* inv, int n,
                              int F, int D, void* out, int ld_out, int col0, hipStream_t s);

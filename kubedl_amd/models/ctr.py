@@ -17,8 +17,11 @@ MI355X-first re-design:
   (``segment_reduce``) so only one row per unique id crosses xGMI.
 * **Dense tower on MFMA.**  ``FusedLinear`` runs forward as the hand-written
   ``gemm_bias_act`` kernel (v_mfma_f32_32x32x16_bf16, bias + ReLU fused in the
-  epilogue); backward fuses ReLU-mask + bias-gradient (``relu_bwd_dbias``),
-  runs dx on ``gemm_bias_act`` and dW on the LDS-DMA weight-gradient kernel
+  epilogue; the wide layers on the LDS-DMA igemm loop); backward fuses
+  ReLU-mask + bias-gradient (``relu_bwd_dbias``; opt-in: folded into the
+  launch that produces the gradient, ``head_bce_bwd`` relu_x /
+  ``gemm_dgrad_relu``), runs dx on ``gemm_bias_act`` and dW on the LDS-DMA
+  weight-gradient kernel
   (csrc/wgrad_dma.hip); the 1-wide logit layer is fused with the sigmoid-BCE
   loss (``head_bce_fwd/bwd``: a GEMV per row + loss + dlogit in one pass,
   dx / dw / db in one backward pass) -- no vendor GEMM in the step.
@@ -59,7 +62,8 @@ class _FusedLinearFn(torch.autograd.Function):
 
 def _linear_bwd(dy, x, w, y, relu: bool, has_b: bool):
     """(dx, dW, db) of y = act(x W^T + b) on the kdl kernels (the backward of
-    _FusedLinearFn and of DenseTower.train_step)."""
+    _FusedLinearFn; DenseTower.train_step fuses the ReLU backward and the bias
+    gradient into the producing launches instead, _tower_layer_bwd)."""
     ext = _ext.load()
     dy = dy.contiguous()
     # db straight in the parameter dtype (bf16): no zero-fill, no conversion launch
@@ -71,18 +75,7 @@ def _linear_bwd(dy, x, w, y, relu: bool, has_b: bool):
         dx = ext.gemm_bias_act(dz, w.contiguous(), None, False, True)
     else:
         dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
-    if fout % 64 == 0 and fin % 64 == 0:
-        # dW = dz^T x: the reduction over the batch is the weight-gradient
-        # form of csrc/wgrad_dma.hip (both operands row-major, LDS-DMA +
-        # transposed LDS reads; split-batch fp32 slabs, fixed-order reduce)
-        B = x.shape[0]
-        ws = _wgrad_workspace(ext, B, fout, fin, x.device)
-        dw = torch.empty(fout, fin, dtype=w.dtype, device=w.device)
-        # solo: no weight-gradient side stream here, so the split count
-        # that fills the chip (not the ResNet engine's two-stream one)
-        ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1, True)
-    else:
-        dw = (dz.t() @ x).to(w.dtype)
+    dw = _dw_of(ext, dz, x, w)
     return dx, dw, ((db if db.dtype == w.dtype else db.to(w.dtype)) if has_b else None)
 
 
@@ -136,14 +129,71 @@ def _head_fwd(x, w, b, y):
     return loss, logit, dlogit
 
 
-def _head_bwd(x, w, b_dtype, dlogit, gloss):
+def _head_bwd(x, w, b_dtype, dlogit, gloss, relu_x: bool = False):
+    """(dx, dW, db) of the logit head; ``relu_x`` (x is the last tower layer's
+    ReLU output): dx comes back masked by x > 0 -- that layer's pre-activation
+    gradient -- and a fourth value, that layer's bias gradient (bf16), is
+    summed in the same launch (no relu_bwd_dbias pass)."""
     ext = _ext.load()
     # dW / db summed over the per-block partials in a fixed order by the kernel's
     # last block (deterministic), already bf16
-    dx, dw, db, _dwp, _dbp = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0], gloss)
+    out = ext.head_bce_bwd(x, w.reshape(-1).contiguous(), dlogit, 1.0 / x.shape[0], gloss, relu_x)
+    dx, dw, db = out[0], out[1], out[2]
     dw = dw.reshape(w.shape) if w.dtype == dw.dtype else dw.to(w.dtype).reshape(w.shape)
     db = db if b_dtype == db.dtype else db.to(b_dtype)
+    if relu_x:
+        return dx, dw, db, out[5]
     return dx, dw, db
+
+
+_FUSED_RELU_BWD = []
+
+
+def _fused_relu_bwd() -> bool:
+    if not _FUSED_RELU_BWD:
+        from ..utils.tune import tune
+        # default off: each fused launch ends in a ticketed cross-block reduction
+        # whose agent release writes back the freshly stored gradient tile -- the
+        # 1024- / 512-wide data gradients ran 32.7 / 23.4 us against 14 / 7 us
+        # unfused + relu_bwd_dbias, and the step 10.94-10.96 vs 11.01-11.02 M
+        # samples/s (profiles/r06_ctr_fused_relu_bwd.txt)
+        _FUSED_RELU_BWD.append(bool(tune("ctr_fused_relu_bwd", 0)))
+    return _FUSED_RELU_BWD[0]
+
+
+def _tower_layer_bwd(dz, x, w, x_relu: bool):
+    """(dx, dW, dbx) of z = x W^T + b given dz = dL/dz.  ``x_relu`` (x is the
+    previous layer's ReLU output): dx comes back masked by x > 0 (that layer's
+    dz) with dbx = its column sums, that layer's bias gradient, from the same
+    launch (``gemm_dgrad_relu``); else dbx is None."""
+    ext = _ext.load()
+    fout, fin = w.shape
+    dbx = None
+    if fin % 8 == 0:
+        if x_relu:
+            dx, dbx = ext.gemm_dgrad_relu(dz, w.contiguous(), x)
+        else:
+            dx = ext.gemm_bias_act(dz, w.contiguous(), None, False, True)
+    else:
+        dx = ext.gemm_bias_act(dz, w.t().contiguous(), None, False)
+        if x_relu:
+            dx, dbx = ext.relu_bwd_dbias(dx, x, True)
+    return dx, _dw_of(ext, dz, x, w), dbx
+
+
+def _dw_of(ext, dz, x, w):
+    """dW = dz^T x: the reduction over the batch is the weight-gradient form of
+    csrc/wgrad_dma.hip (both operands row-major, LDS-DMA + transposed LDS reads;
+    split-batch fp32 slabs, fixed-order reduce); solo: no weight-gradient side
+    stream here, so the split count that fills the chip."""
+    fout, fin = w.shape
+    if fout % 64 == 0 and fin % 64 == 0:
+        B = x.shape[0]
+        ws = _wgrad_workspace(ext, B, fout, fin, x.device)
+        dw = torch.empty(fout, fin, dtype=w.dtype, device=w.device)
+        ext.conv1x1_wgrad(dz, x, None, ws, dw, 1.0, B, fout, fin, 0, 0, 0, 0, 1, True)
+        return dw
+    return (dz.t() @ x).to(w.dtype)
 
 
 def head_bce(x, w, b, y):
@@ -200,19 +250,47 @@ class DenseTower(nn.Module):
         one = getattr(self, "_one", None)
         if one is None or one.device != x.device:
             one = self._one = torch.ones(1, device=x.device)
-        dy, dw, db = _head_bwd(acts[-1], hw, hb.dtype, dlogit, one)
+        # KDL_TUNE ctr_fused_relu_bwd=1: every ReLU backward and bias gradient
+        # fused into the launch that produces the gradient (head backward, then
+        # each layer's data-gradient GEMM): dz is the pre-activation gradient of
+        # layer i, db its bias grad
+        if not _fused_relu_bwd():  # A/B: the separate relu_bwd_dbias pass per layer
+            dy, dw, db = _head_bwd(acts[-1], hw, hb.dtype, dlogit, one)
+            for p, g in ((hw, dw), (hb, db)):
+                p.grad = g
+                if on_ready is not None:
+                    on_ready(p)
+            for i in range(len(self.layers) - 1, -1, -1):
+                l = self.layers[i]
+                dy, dw, db = _linear_bwd(dy, acts[i], l.weight, acts[i + 1], l.relu, True)
+                for p, g in ((l.weight, dw), (l.bias, db)):
+                    p.grad = g
+                    if on_ready is not None:
+                        on_ready(p)
+            return loss.view(()), dy
+        last = self.layers[-1]
+        if last.relu:
+            dz, dw, db, db_z = _head_bwd(acts[-1], hw, hb.dtype, dlogit, one, relu_x=True)
+        else:
+            dz, dw, db = _head_bwd(acts[-1], hw, hb.dtype, dlogit, one)
+            db_z = None
         for p, g in ((hw, dw), (hb, db)):
             p.grad = g
             if on_ready is not None:
                 on_ready(p)
         for i in range(len(self.layers) - 1, -1, -1):
             l = self.layers[i]
-            dy, dw, db = _linear_bwd(dy, acts[i], l.weight, acts[i + 1], l.relu, True)
+            if db_z is None:  # a layer without ReLU: its bias gradient from dz itself
+                dz, db_z = _ext.load().relu_bwd_dbias(dz, None, True)
+            x_relu = i > 0 and self.layers[i - 1].relu
+            dx, dw, db_prev = _tower_layer_bwd(dz, acts[i], l.weight, x_relu)
+            db = db_z if db_z.dtype == l.bias.dtype else db_z.to(l.bias.dtype)
             for p, g in ((l.weight, dw), (l.bias, db)):
                 p.grad = g
                 if on_ready is not None:
                     on_ready(p)
-        return loss.view(()), dy
+            dz, db_z = dx, db_prev
+        return loss.view(()), dz
 
     def loss(self, x, y):
         """Training step forward: (mean BCE loss, logits); the head runs fused

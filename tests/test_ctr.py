@@ -371,6 +371,43 @@ def test_gemm_bias_act_matches_fp32(M, N, K, relu, tile):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 1728), (300, 256, 128), (1, 128, 64), (130, 64, 192)])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4])
+def test_gemm_bias_act_on_igemm_matches_fp32(M, N, K, cfg):
+    """The forward layers on the LDS-DMA igemm loop (BIAS / BIAS_RELU epilogues):
+    every tile config that takes N, fp32 / bf16 / no bias, ragged M."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(2)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5 + torch.arange(N, device="cuda")[:, None] * 1e-3).bfloat16()
+    b = torch.randn(N, device="cuda")
+    ext.set_ctr_igemm(2, cfg)
+    try:
+        outs = [(ext.gemm_bias_act(a, w, bias, relu), bias, relu)
+                for bias in (b, b.bfloat16(), None) for relu in (True, False)]
+    finally:
+        ext.set_ctr_igemm(-2, -2)
+    base = a.float() @ w.float().t()
+    for y, bias, relu in outs:
+        ref = base + (bias.float() if bias is not None else 0.0)
+        if relu:
+            ref = ref.relu()
+        torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_ctr_igemm_serves_the_wide_forward_layers_only():
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    ext.set_ctr_igemm(-2, -2)
+    assert ext.ctr_igemm_cfg_for(4096, 1024, 1728) == 2   # 256 tiles of 128x128
+    assert ext.ctr_igemm_cfg_for(4096, 512, 1024) == 2    # 128 tiles
+    assert ext.ctr_igemm_cfg_for(4096, 256, 512) == -1    # 64 tiles: the 64x64 register kernel
+    assert ext.ctr_igemm_cfg_for(4096, 1024, 1680) == -1  # K % 64
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 72), (4096, 1680, 1024), (1, 128, 64), (130, 72, 1000)])
 @pytest.mark.parametrize("tile", [0, 1, 2])
 def test_gemm_trans_w_matches_fp32(M, N, K, tile):
@@ -969,11 +1006,17 @@ def test_a2a_serve_stamps_match_owner_update_stamps():
 
 
 @pytest.mark.gpu
-def test_tower_train_step_matches_autograd_bitwise():
+@pytest.mark.parametrize("fused", [False, True])
+def test_tower_train_step_matches_autograd_bitwise(fused, monkeypatch):
     """DenseTower.train_step (the kernels called in order, no autograd graph) gives
-    bitwise the loss, input gradient and parameter gradients of loss() + backward()."""
+    bitwise the loss, input gradient and weight gradients of loss() + backward().
+    Its ReLU backward and bias gradients run inside the producing launches (head
+    backward, gemm_dgrad_relu): the masked gradients are the same bits, the bias
+    gradients the same sums in another fp32 order (within 2 bf16 ulp)."""
     import copy
+    from kubedl_amd.models import ctr
     from kubedl_amd.models.ctr import DenseTower
+    monkeypatch.setattr(ctr, "_FUSED_RELU_BWD", [fused])
     torch.manual_seed(5)
     t1 = DenseTower(1728, (1024, 512, 256)).cuda()
     with torch.no_grad():
@@ -992,8 +1035,58 @@ def test_tower_train_step_matches_autograd_bitwise():
     torch.cuda.synchronize()
     assert torch.equal(la.detach(), lb) and torch.equal(xa.grad, dxb)
     for (n, p), q in zip(t1.named_parameters(), t2.parameters()):
-        assert torch.equal(p.grad, q.grad), n
+        if fused and n.startswith("layers.") and n.endswith(".bias"):
+            a, b = p.grad.float(), q.grad.float()
+            torch.testing.assert_close(b, a, rtol=8e-3, atol=1e-3 * float(a.abs().max()))
+        else:
+            assert torch.equal(p.grad, q.grad), n
     assert len(seen) == len(list(t2.parameters()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,N", [(4096, 1024, 512), (4096, 512, 1024), (300, 64, 72), (1, 128, 64)])
+def test_gemm_dgrad_relu_matches_unfused(M, K, N):
+    """(dz W) masked by y > 0 and its column sums in one launch (every tile
+    config) == gemm_bias_act(trans_w) + relu_bwd_dbias: the same bits for the
+    gradient, the bias gradient within fp32 order (2 bf16 ulp)."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(3)
+    dz = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(K, N, device="cuda") / K ** 0.5).bfloat16()
+    y = torch.randn(M, N, device="cuda").relu().bfloat16()
+    for tile in (0, 1, 2):
+        ext.set_ctr_tile(tile)
+        try:
+            got, db = ext.gemm_dgrad_relu(dz, w, y)
+            dx = ext.gemm_bias_act(dz, w, None, False, True)
+            ref, dbr = ext.relu_bwd_dbias(dx, y, True)
+        finally:
+            ext.set_ctr_tile(-1)
+        assert torch.equal(got, ref), tile
+        exact = (ref.double().sum(0))
+        torch.testing.assert_close(db.double(), exact, rtol=8e-3, atol=1e-3 * float(exact.abs().max()) + 1e-6)
+        torch.testing.assert_close(dbr.double(), exact, rtol=8e-3, atol=1e-3 * float(exact.abs().max()) + 1e-6)
+    again, db2 = ext.gemm_dgrad_relu(dz, w, y)
+    assert torch.equal(again, got) and torch.equal(db2, db)  # deterministic (tickets re-armed)
+
+
+@pytest.mark.gpu
+def test_head_bwd_relu_mask_matches_unfused():
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(4)
+    M, K = 4096, 256
+    x = torch.randn(M, K, device="cuda").relu().bfloat16()
+    w = (torch.randn(K, device="cuda") / 16).bfloat16()
+    dlogit = torch.randn(M, device="cuda")
+    one = torch.ones(1, device="cuda")
+    dx, dw, db, *_ = ext.head_bce_bwd(x, w, dlogit, 1.0 / M, one)
+    dz_ref, dbx_ref = ext.relu_bwd_dbias(dx, x, True)
+    out = ext.head_bce_bwd(x, w, dlogit, 1.0 / M, one, True)
+    assert torch.equal(out[0], dz_ref) and torch.equal(out[1], dw) and torch.equal(out[2], db)
+    exact = dz_ref.double().sum(0)
+    torch.testing.assert_close(out[5].double(), exact, rtol=8e-3, atol=1e-3 * float(exact.abs().max()))
 
 
 @pytest.mark.gpu

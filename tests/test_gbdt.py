@@ -255,6 +255,40 @@ def test_host_cuts_bitwise_equal_fit_cuts(n, F, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("F", [28, 12, 64, 100, 7])
+def test_gpu_row_per_lane_hist_equals_slot_kernel(F):
+    """The row-per-lane build (dword bin loads, g / h quantised once per row)
+    sums the same fixed-point integers per block as the slot kernel: equal up to
+    the order of the fp32 flush atomics.  F = 7 (not a multiple of 4) runs the
+    slot kernel in both; F = 100 has a 36-feature second tile; F = 64 a 128 KiB
+    LDS tile."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g0 = torch.Generator().manual_seed(F)
+    N, B, rpb = 50_000, 256, 2048
+    bins = torch.randint(0, B, (N, F), generator=g0, dtype=torch.uint8)
+    bins[:, 0] = 3  # one hot bin: every lane of a wave adds to the same address
+    grad = torch.randn(N, generator=g0)
+    hess = torch.rand(N, generator=g0) * 0.25
+    rows = torch.randperm(N, generator=g0).int()
+    seg = torch.tensor([0, 777, 20_000, N], dtype=torch.int32)
+    args = (bins.cuda(), grad.cuda(), hess.cuda(), rows.cuda(), seg.cuda(), B, rpb)
+    try:
+        ext.set_gbdt_hist_rows(0)
+        slot = ext.gbdt_hist_quant(*args).cpu()
+        outs = []
+        for u in (4, 8):
+            ext.set_gbdt_hist_rows(u)
+            outs.append(ext.gbdt_hist_quant(*args).cpu())
+    finally:
+        ext.set_gbdt_hist_rows(-2)
+    for got in outs:
+        torch.testing.assert_close(got, slot, rtol=1e-5, atol=1e-5)
+    # and both are the histogram: counts of the hot bin
+    torch.testing.assert_close(outs[0][:, 0, 3, 1].double().sum(), hess.double().sum(), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
 def test_gpu_quantised_hist_tiny_and_skewed_hessians():
     """the device grower sums fixed-point integers per block (step =
     rpb * max / 2^30 per row).  With skewed gradients and hessians spanning
