@@ -298,27 +298,53 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
 // block sums (exact, so order-free): the flushed histogram equals the slot
 // kernel's up to the order of the fp32 flush atomics.  LDS holds nf = min(fp, F - f0)
 // feature planes (g [nf][B] then h [nf][B]).
+// The chunk plan (hist_plan_kernel's prefix of ceil(size / rpb) over the nb
+// built nodes) is computed by wave 0 of every block into LDS: no plan launch
+// per level (nb <= kPlanMax).
+constexpr int kPlanMax = 1024;
+
 template <int U, int NW>
 __global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
     const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
     int64_t gh_stride, const int32_t* __restrict__ rows, const int32_t* __restrict__ blo,
-    const int32_t* __restrict__ bhi, const int32_t* __restrict__ chunk_off, int nb, int F, int B, int rpb, int fp,
+    const int32_t* __restrict__ bhi, int nb, int F, int B, int rpb, int fp,
     const float* __restrict__ gh_max, float* __restrict__ hist, int flush) {
   extern __shared__ int qlds[];
+  __shared__ int s_off[kPlanMax + 1];
+  const int t = threadIdx.x;
+  if (t < 64) {  // wave 0: inclusive wave scans, 64 nodes at a time
+    int carry = 0;
+    if (t == 0) s_off[0] = 0;
+    for (int j0 = 0; j0 < nb; j0 += 64) {
+      const int jj = j0 + t;
+      int n = 0;
+      if (jj < nb) {
+        const int sz = bhi[jj] - blo[jj];
+        n = sz > 0 ? (sz + rpb - 1) / rpb : 0;
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(n, o, 64);
+        if (t >= o) n += u;
+      }
+      if (jj < nb) s_off[jj + 1] = carry + n;
+      carry += __shfl(n, 63, 64);
+    }
+  }
+  __syncthreads();
   const int c = blockIdx.x;
-  if (c >= chunk_off[nb]) return;  // block-uniform
+  if (c >= s_off[nb]) return;  // block-uniform
   int a = 0, z = nb;
   while (z - a > 1) {
     const int m = (a + z) >> 1;
-    if (chunk_off[m] <= c) a = m; else z = m;
+    if (s_off[m] <= c) a = m; else z = m;
   }
   const int j = a;
-  const int r0 = blo[j] + (c - chunk_off[j]) * rpb;
+  const int r0 = blo[j] + (c - s_off[j]) * rpb;
   const int r1 = (r0 + rpb) < bhi[j] ? (r0 + rpb) : bhi[j];
   const int f0 = blockIdx.y * fp;
   const int nf = (F - f0) < fp ? (F - f0) : fp;  // a multiple of 4 (F % 4 == 0, fp % 4 == 0)
   int* qh_pl = qlds + nf * B;
-  const int t = threadIdx.x;
   const float mg = gh_max[0], mh = gh_max[1];
   const float sg = mg > 0.f ? kQuantRange / (static_cast<float>(rpb) * mg) : 0.f;
   const float sh = mh > 0.f ? kQuantRange / (static_cast<float>(rpb) * mh) : 0.f;
@@ -374,10 +400,19 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
 
 // {max |g|, max h} over n rows into out[2] (zeroed by the caller): a block max,
 // then one integer atomicMax per value (non-negative floats order as their bits)
+// (n4 > 0: g and h 16-B aligned, read as float4 up to 4 n4, the tail as floats)
 __global__ __launch_bounds__(256) void gh_absmax_kernel(const float* __restrict__ g, const float* __restrict__ h,
-                                                        int n, unsigned* __restrict__ out) {
+                                                        int n, int n4, unsigned* __restrict__ out) {
   float mg = 0.f, mh = 0.f;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* h4 = reinterpret_cast<const float4*>(h);
+#pragma unroll 4
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+    const float4 a = g4[i], b = h4[i];
+    mg = fmaxf(mg, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+    mh = fmaxf(mh, fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
+  }
+  for (int i = 4 * n4 + blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     mg = fmaxf(mg, fabsf(g[i]));
     mh = fmaxf(mh, fabsf(h[i]));
   }
@@ -549,9 +584,12 @@ __global__ __launch_bounds__(256) void pick_small_kernel(const float* __restrict
 }
 
 // hist_next[build_child[i]] = built[i]; hist_next[sibling] = parent[i] - built[i]
-// (zero below a non-split parent).  float4 per thread over [L][F*B*2].
+// (zero below a non-split parent).  float4 per thread over [L][F*B*2].  built[i]
+// is zeroed once read: the next level's build accumulates into a zeroed buffer
+// without a fill launch (the grower's built_ starts zeroed; a complete tree's
+// last level leaves all of it zero).
 __global__ __launch_bounds__(256) void subtract_kernel(const float4* __restrict__ parent,
-                                                       const float4* __restrict__ built,
+                                                       float4* __restrict__ built,
                                                        const int32_t* __restrict__ split,
                                                        const int32_t* __restrict__ build_child, int L, int per_node4,
                                                        float4* __restrict__ next) {
@@ -561,6 +599,7 @@ __global__ __launch_bounds__(256) void subtract_kernel(const float4* __restrict_
   const int64_t k = e - static_cast<int64_t>(i) * per_node4;
   const int c = build_child[i];
   const float4 b = built[e];
+  built[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 sib = make_float4(0.f, 0.f, 0.f, 0.f);
   if (split[i]) {
     const float4 pa = parent[e];
@@ -766,9 +805,13 @@ static hipError_t rows_lds_attr() {
 hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* out, hipStream_t s) {
   RETURN_IF_HIP_ERR(hipMemsetAsync(out, 0, 2 * sizeof(float), s));
   if (n <= 0) return hipSuccess;
-  int blocks = (n + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(gh_absmax_kernel, dim3(blocks), dim3(256), 0, s, grad, hess, n, reinterpret_cast<unsigned*>(out));
+  // 128 blocks: each ends in two device-scope atomicMax on the same two words,
+  // which serialise (1024 blocks: 27 us for 2M rows, the atomics not the 16 MB read)
+  int blocks = (n + 1023) / 1024;
+  if (blocks > 128) blocks = 128;
+  const bool vec = ((reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(hess)) & 15) == 0;
+  hipLaunchKernelGGL(gh_absmax_kernel, dim3(blocks), dim3(256), 0, s, grad, hess, n, vec ? n / 4 : 0,
+                     reinterpret_cast<unsigned*>(out));
   return hipGetLastError();
 }
 
@@ -779,7 +822,6 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
                         int max_chunks, int rpb, int F, int B, const float* gh_max, float* hist, hipStream_t s) {
   if (nb <= 0 || F <= 0 || max_chunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hist_plan_kernel, dim3(1), dim3(64), 0, s, blo, bhi, nb, rpb, chunk_off);
   const int fp = hist_fp(F);
   RETURN_IF_HIP_ERR(hist_lds_attr());
   dim3 grid(max_chunks, (F + fp - 1) / fp);
@@ -793,13 +835,13 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
   if (g_hist_rows == -2) g_hist_rows = tune_int("gbdt_hist_rows", 4);
   const int rows_u = g_hist_rows;
   static const bool noflush = tune_int("gbdt_price_noflush", 0) != 0;
-  if (rows_u > 0 && F % 4 == 0 && fp >= 4) {
+  if (rows_u > 0 && F % 4 == 0 && fp >= 4 && nb <= kPlanMax) {
     const int nf0 = F < fp ? F : fp;  // the first (largest) tile's planes
     const size_t lds_r = static_cast<size_t>(nf0) * B * 2 * sizeof(int);
 #define HIST_ROWS_LAUNCH(U, NW)                                                                                        \
   RETURN_IF_HIP_ERR((rows_lds_attr<U, NW>()));                                                                        \
   hipLaunchKernelGGL((hist_build_rows_kernel<U, NW>), grid, dim3(kHistBlock), lds_r, s, bins, grad, hess, gh_stride, \
-                     rows, blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist, noflush ? 0 : 1)
+                     rows, blo, bhi, nb, F, B, rpb, fp, gh_max, hist, noflush ? 0 : 1)
 #define HIST_ROWS_BY_U(U)                  \
   switch (fp / 4) {                         \
     case 1: HIST_ROWS_LAUNCH(U, 1); break;     \
@@ -814,6 +856,7 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
 #undef HIST_ROWS_LAUNCH
     return hipGetLastError();
   }
+  hipLaunchKernelGGL(hist_plan_kernel, dim3(1), dim3(64), 0, s, blo, bhi, nb, rpb, chunk_off);
 #define HIST_WQ_LAUNCH(U)                                                                                         \
   hipLaunchKernelGGL((hist_build_wq_kernel<U>), grid, dim3(kHistBlock), lds, s, bins, grad, hess, gh_stride, rows, \
                      blo, bhi, chunk_off, nb, F, B, rpb, fp, gh_max, hist)
@@ -869,13 +912,13 @@ hipError_t gbdt_pick_small(const float* cnt, const int32_t* lo_next, const int32
   return hipGetLastError();
 }
 
-hipError_t gbdt_subtract(const float* parent, const float* built, const int32_t* split, const int32_t* build_child,
+hipError_t gbdt_subtract(const float* parent, float* built, const int32_t* split, const int32_t* build_child,
                          int L, int per_node, float* next, hipStream_t s) {
   if (L <= 0) return hipSuccess;
   const int per4 = per_node / 4;
   const int64_t n = static_cast<int64_t>(L) * per4;
   hipLaunchKernelGGL(subtract_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
-                     reinterpret_cast<const float4*>(parent), reinterpret_cast<const float4*>(built), split,
+                     reinterpret_cast<const float4*>(parent), reinterpret_cast<float4*>(built), split,
                      build_child, L, per4, reinterpret_cast<float4*>(next));
   return hipGetLastError();
 }

@@ -54,17 +54,20 @@ class GbdtGrower {
     gamma_ = static_cast<float>(gamma);
     lr_ = static_cast<float>(lr);
     mcw_ = static_cast<float>(min_child_weight);
-    // rows per histogram chunk: ~1000-2000 chunks over the root level, 256..2048
-    // (also the quantisation's per-block row bound, csrc/gbdt.hip).  Measured at
-    // 2M x 28 with float LDS atomics (profiles/r02_gbdt_hist_sweep.txt): 1024 beat
-    // longer chunks; the float-atomic rate bounded the build then -- the integer
-    // planes (round 5) removed that bound.  KDL_TUNE gbdt_rpb overrides.
+    // rows per histogram chunk (also the quantisation's per-block row bound,
+    // csrc/gbdt.hip): the smallest power of two giving <= 512 chunks over the
+    // root (two resident blocks per CU), 256..4096.  Every chunk's block ends in
+    // a 57 KB flush of agent-scope float atomics (2M x 28), paid per block: with
+    // the row-per-lane build the flush, not the LDS adds, bounds small chunks --
+    // 2M x 28, depth 6: 1024 / 2048 / 4096 / 8192 rows per chunk 578-793 /
+    // 941-946 / 1005-1007 / 934-939 boosting rounds/s (profiles/r06_gbdt_rpb.txt;
+    // the round-2 float-atomic build preferred 1024).  KDL_TUNE gbdt_rpb overrides.
     const int64_t target = std::max(0, kdl::tune_int("gbdt_rpb", 0));
     rpb_ = 256;
     if (target > 0) {
       rpb_ = static_cast<int>(target);
     } else {
-      while (rpb_ < 2048 && static_cast<int64_t>(rpb_) * 2 * 1024 <= N_) rpb_ *= 2;
+      while (rpb_ < 4096 && static_cast<int64_t>(rpb_) * 512 < N_) rpb_ *= 2;
     }
 
     const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
@@ -97,7 +100,8 @@ class GbdtGrower {
     per_node_ = static_cast<int64_t>(F_) * B_ * 2;
     hist_cur_ = at::empty({maxL, F_, B_, 2}, fo);
     hist_next_ = at::empty({maxL, F_, B_, 2}, fo);
-    built_ = at::empty({std::max<int64_t>(maxL / 2, 1), F_, B_, 2}, fo);
+    // zeroed here and by every level's subtract once read (no fill per level)
+    built_ = at::zeros({std::max<int64_t>(maxL / 2, 1), F_, B_, 2}, fo);
     cnt_ = at::zeros({maxL}, fo);
     build_child_ = at::zeros({std::max<int64_t>(maxL / 2, 1)}, io);
     blo_ = at::zeros({std::max<int64_t>(maxL / 2, 1)}, io);
@@ -174,8 +178,7 @@ class GbdtGrower {
       ck(kdl::gbdt_pick_small(fp(cnt_), ip(lo_[d + 1]), ip(hi_[d + 1]), L, ip(build_child_), ip(blo_), ip(bhi_),
                               stream()),
          "gbdt_pick_small");
-    auto built = built_.narrow(0, 0, L);
-    built.zero_();
+    auto built = built_.narrow(0, 0, L);  // zero: level_c's subtract cleared what the last build wrote
     const int max_chunks = (N_ + rpb_ - 1) / rpb_ + L;
     ck(kdl::gbdt_hist_wq(bins_.data_ptr<uint8_t>(), fp(grad_), fp(hess_), 1, ip(rows_), ip(blo_), ip(bhi_),
                          ip(chunk_off_), L, max_chunks, rpb_, F_, B_, fp(gh_max_), fp(built), stream()),

@@ -189,7 +189,7 @@ hipError_t gbdt_children(const int32_t* split, const int32_t* lo, const int32_t*
                          int32_t* blo, int32_t* bhi, hipStream_t s);
 hipError_t gbdt_pick_small(const float* cnt, const int32_t* lo_next, const int32_t* hi_next, int L,
                            int32_t* build_child, int32_t* blo, int32_t* bhi, hipStream_t s);
-hipError_t gbdt_subtract(const float* parent, const float* built, const int32_t* split, const int32_t* build_child,
+hipError_t gbdt_subtract(const float* parent, float* built, const int32_t* split, const int32_t* build_child,
                          int L, int per_node, float* next, hipStream_t s);
 hipError_t gbdt_quantise(const float* X, const float* cuts, int64_t n, int F, int ncut, int max_code, uint8_t* out,
                          hipStream_t s);

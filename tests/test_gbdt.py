@@ -289,7 +289,8 @@ def test_gpu_row_per_lane_hist_equals_slot_kernel(F):
 
 
 @pytest.mark.gpu
-def test_gpu_quantised_hist_tiny_and_skewed_hessians():
+@pytest.mark.parametrize("rpb", [2048, 4096])
+def test_gpu_quantised_hist_tiny_and_skewed_hessians(rpb):
     """the device grower sums fixed-point integers per block (step =
     rpb * max / 2^30 per row).  With skewed gradients and hessians spanning
     1e-9 .. 0.25 (confidently classified logistic rows next to uncertain ones)
@@ -298,7 +299,7 @@ def test_gpu_quantised_hist_tiny_and_skewed_hessians():
     from kubedl_amd.ops import _ext
     ext = _ext.load()
     g0 = torch.Generator().manual_seed(7)
-    N, F, B, rpb = 100_000, 8, 64, 2048
+    N, F, B = 100_000, 8, 64
     bins = torch.randint(0, B, (N, F), generator=g0, dtype=torch.uint8)
     grad = torch.randn(N, generator=g0) * 1e-3
     hot = torch.rand(N, generator=g0) < 0.01
