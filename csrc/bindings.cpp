@@ -678,7 +678,7 @@ std::vector<at::Tensor> head_bce_bwd(const at::Tensor& x, const at::Tensor& w, c
 }
 
 void embed_gather_cast(const at::Tensor& table, const at::Tensor& uniq, const at::Tensor& inv, int64_t F,
-                       at::Tensor out, int64_t col0) {
+                       at::Tensor out, int64_t col0, const c10::optional<at::Tensor>& dense, int64_t tail) {
   TORCH_CHECK(table.is_cuda() && table.dim() == 2 && table.is_contiguous() &&
                   (table.scalar_type() == at::kFloat || table.scalar_type() == at::kBFloat16),
               "embed_gather_cast: fp32 or bf16 table [V, D]");
@@ -692,11 +692,25 @@ void embed_gather_cast(const at::Tensor& table, const at::Tensor& uniq, const at
                   reinterpret_cast<uintptr_t>(table.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
               "embed_gather_cast: 16-byte rows (D, the out row stride and col0 multiples of 8)");
+  // tail: the next ``tail`` columns after the last field (dense fp32 [B, nd], then zeros) in the same launch
+  const bool has_d = dense.has_value() && dense->defined();
+  int64_t nd = 0;
+  if (tail > 0) {
+    TORCH_CHECK(tail % 8 == 0 && col0 + F * D + tail <= out.size(1), "embed_gather_cast: tail columns");
+    if (has_d) {
+      TORCH_CHECK(dense->is_cuda() && dense->scalar_type() == at::kFloat && dense->is_contiguous() && dense->dim() == 2 &&
+                      dense->size(0) == out.size(0) && dense->size(1) <= tail,
+                  "embed_gather_cast: dense fp32 [B, nd <= tail] contiguous");
+      nd = dense->size(1);
+    }
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   check_hip(kdl::embed_gather_cast(table.data_ptr(), table.scalar_type() == at::kBFloat16, uniq.data_ptr<int64_t>(),
                                    inv.data_ptr<int64_t>(),
                                    static_cast<int>(n), static_cast<int>(F), static_cast<int>(D), out.data_ptr(),
-                                   static_cast<int>(out.stride(0)), static_cast<int>(col0), cur_stream()),
+                                   static_cast<int>(out.stride(0)), static_cast<int>(col0), cur_stream(),
+                                   has_d && tail > 0 ? dense->data_ptr<float>() : nullptr, static_cast<int>(nd),
+                                   static_cast<int>(tail > 0 ? tail : 0)),
             "embed_gather_cast");
 }
 
@@ -1802,7 +1816,10 @@ PYBIND11_MODULE(_C, m) {
         "update's slot stamps)",
         py::arg("table"), py::arg("req"), py::arg("n_own"), py::arg("rows_bf16") = false,
         py::arg("slotmap") = py::none(), py::arg("call") = 0, py::arg("cap") = 0, py::arg("W") = 0);
-  m.def("embed_gather_cast", &embed_gather_cast, "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input");
+  m.def("embed_gather_cast", &embed_gather_cast,
+        "fused one-owner pull: bf16(table[uniq[inv]]) into the tower input (+ tail: dense columns, zero pad)",
+        py::arg("table"), py::arg("uniq"), py::arg("inv"), py::arg("F"), py::arg("out"), py::arg("col0"),
+        py::arg("dense") = py::none(), py::arg("tail") = 0);
   m.def("segment_adagrad", &segment_adagrad, "segment sum + fused sparse Adagrad on owned rows");
   m.def("dedup_table_slots", &dedup_table_slots, "hash-table slots dedup_csr needs for n ids");
   m.def("segment_reduce_adagrad", &segment_reduce_adagrad,

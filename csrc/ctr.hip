@@ -435,17 +435,33 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(const T* __restrict__
 // 16-B aligned rows (host-checked).  T = bf16: the rows are already bf16 (the
 // fixed exchange's received rows, rounded once by their owner): one 16-B copy.
 template <typename T>
+// tail > 0 (the CTR tower input): the last field's lane group of each row also
+// writes the row's next ``tail`` columns -- the nd dense features (fp32 ->
+// bf16) then zeros up to the padded width -- so the input is built in one
+// launch (no torch fill of the pad, no cast-copy of the dense block).
 __global__ __launch_bounds__(256) void embed_gather_cast_kernel(const T* __restrict__ table,
                                                                 const int64_t* __restrict__ uniq,
                                                                 const int64_t* __restrict__ inv, int n, int F, int D,
                                                                 bf16_t* __restrict__ out, int ld_out, int col0,
-                                                                int lg) {
+                                                                int lg, const float* __restrict__ dense = nullptr,
+                                                                int nd = 0, int tail = 0) {
   const int r = (blockIdx.x * 256 + threadIdx.x) >> lg;
   const int gl = threadIdx.x & ((1 << lg) - 1);
   if (r >= n) return;
   const T* src = table + uniq[inv[r]] * static_cast<int64_t>(D);
   const int b = r / F, f = r - b * F;
   bf16_t* dst = out + static_cast<int64_t>(b) * ld_out + col0 + static_cast<int64_t>(f) * D;
+  if (tail > 0 && f == F - 1) {
+    bf16_t* tdst = dst + D;
+    const float* dsrc = dense + static_cast<int64_t>(b) * nd;
+    for (int c = gl * 8; c < tail; c += 8 << lg) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = c + e < nd ? dsrc[c + e] : 0.f;
+      *reinterpret_cast<uint4*>(tdst + c) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                       pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+  }
   for (int c = gl * 8; c < D; c += 8 << lg) {
     if constexpr (sizeof(T) == 2) {
       *reinterpret_cast<uint4*>(dst + c) = *reinterpret_cast<const uint4*>(src + c);
@@ -1134,18 +1150,20 @@ hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n,
 }
 
 hipError_t embed_gather_cast(const void* table, bool table_bf16, const int64_t* uniq, const int64_t* inv, int n,
-                             int F, int D, void* out, int ld_out, int col0, hipStream_t s) {
+                             int F, int D, void* out, int ld_out, int col0, hipStream_t s, const float* dense, int nd,
+                             int tail) {
   if (n <= 0) return hipSuccess;
-  if (D % 8 || ld_out % 8 || col0 % 8) return hipErrorInvalidValue;
+  if (D % 8 || ld_out % 8 || col0 % 8 || tail % 8 || tail < 0 || nd > tail || (nd > 0 && dense == nullptr))
+    return hipErrorInvalidValue;
   int lg = 0;
   while (lg < 6 && (8 << lg) < D) ++lg;
   dim3 grid(static_cast<unsigned>(((static_cast<int64_t>(n) << lg) + 255) / 256));
   if (table_bf16)
     hipLaunchKernelGGL(embed_gather_cast_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(table),
-                       uniq, inv, n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg);
+                       uniq, inv, n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg, dense, nd, tail);
   else
     hipLaunchKernelGGL(embed_gather_cast_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(table), uniq,
-                       inv, n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg);
+                       inv, n, F, D, static_cast<bf16_t*>(out), ld_out, col0, lg, dense, nd, tail);
   return hipGetLastError();
 }
 

@@ -447,7 +447,8 @@ int igemm_pick(int M, int N, int K) {
   // 256x256 wins at N = 256 (fewest operand bytes per MFMA), 128x128 at two
   // blocks per CU elsewhere (more resident waves, more tiles to fill 256 CUs)
   (void)M; (void)K;
-  if (N == 256) return 0;
+  static const int n256 = tune_int("igemm_n256", 0);  // A/B: the tile of the N = 256 (stage-3) GEMMs
+  if (N == 256) return n256 >= 0 && n256 <= 4 ? n256 : 0;
   if (N % 128 == 0) return 2;
   return 3;
 }

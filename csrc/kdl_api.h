@@ -232,7 +232,8 @@ hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float
 // and dbx = its column sums (the bias gradient of the layer that produced x)
 // out[b, col0 + f*D : +D] = bf16(table[uniq[inv[b*F + f]]]) (fp32 table, bf16 out)
 hipError_t embed_gather_cast(const void* table, bool table_bf16, const int64_t* uniq, const int64_t* inv, int n,
-                             int F, int D, void* out, int ld_out, int col0, hipStream_t s);
+                             int F, int D, void* out, int ld_out, int col0, hipStream_t s,
+                             const float* dense = nullptr, int nd = 0, int tail = 0);
 hipError_t embed_gather(const void* table, int dtype, const int64_t* idx, int n, int F, int D, void* out, int ld_out,
                         int col0, hipStream_t s);
 // ucount (optional): the live segment count on the device; U is then a capacity

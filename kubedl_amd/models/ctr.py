@@ -708,11 +708,14 @@ class ShardedEmbedding:
         return (self.dedup is not None and ids.numel() > 0 and self.n_own == 1 and not self.force_fixed and
                 (self.world == 1 or self.group is None and not dist.is_initialized()))
 
-    def pull_into(self, ids: torch.Tensor, out: torch.Tensor, F: int, col0: int = 0) -> Optional[torch.Tensor]:
+    def pull_into(self, ids: torch.Tensor, out: torch.Tensor, F: int, col0: int = 0,
+                  dense: Optional[torch.Tensor] = None, tail: int = 0) -> Optional[torch.Tensor]:
         """One-owner sync-free pull written straight into the bf16 tower input:
         ``out[b, col0 + f*D : +D] = table[ids[b*F + f]]`` (csrc/ctr.hip
-        ``embed_gather_cast``: no fp32 [n, D] gather, no cast pass).  Returns the
-        inverse map, or None when this path does not apply (then use ``pull``)."""
+        ``embed_gather_cast``: no fp32 [n, D] gather, no cast pass).  ``tail``:
+        the same launch writes the ``tail`` columns after the last field --
+        ``dense`` (fp32 [B, nd]) cast to bf16, then zeros.  Returns the inverse
+        map, or None when this path does not apply (then use ``pull``)."""
         if not (out.dtype == torch.bfloat16 and self.table.dtype == torch.float32 and self.use_hip
                 and self.dim % 8 == 0 and out.stride(0) % 8 == 0 and col0 % 8 == 0 and ids.numel() > 0):
             return None
@@ -720,12 +723,12 @@ class ShardedEmbedding:
             # fixed exchange: the received rows go straight into the bf16 input
             # through rslot (dump slots read the zero row)
             got, rslot, inv = self._pull_fixed(ids)
-            _ext.load().embed_gather_cast(got, rslot, inv, F, out, col0)
+            _ext.load().embed_gather_cast(got, rslot, inv, F, out, col0, dense, tail)
             return inv
         if not self._sync_free(ids):
             return None
         uniq, inv, count, _, _ = self.dedup(ids, csr=False)
-        _ext.load().embed_gather_cast(self.table, uniq, inv, F, out, col0)
+        _ext.load().embed_gather_cast(self.table, uniq, inv, F, out, col0, dense, tail)
         self._ctx = ("dev", uniq, count)
         return inv
 
@@ -852,12 +855,20 @@ class CTRModel:
     def build_input(self, ids: torch.Tensor, dense: torch.Tensor):
         B = ids.shape[0]
         gids = (ids + self.field_off).reshape(-1)
-        # every column is written below except the pad [k_in, k_pad): zero only that
         x = torch.empty(B, self.k_pad, dtype=self.dtype, device=self.device)
+        tail = self.k_pad - self.F * self.D
+        fuse_tail = (dense.dtype == torch.float32 and dense.is_contiguous() and dense.dim() == 2
+                     and dense.shape[1] == self.nd and tail % 8 == 0)
+        # fused one-owner pull: table rows -> bf16 input directly; with the dense
+        # features and the zero pad written by the same launch
+        inv = self.emb.pull_into(gids, x, self.F, 0, dense if fuse_tail else None,
+                                 tail if fuse_tail else 0) if self.device.type == "cuda" else None
+        if inv is not None and fuse_tail:
+            return x, inv, gids.numel()
+        # every column is written below except the pad [k_in, k_pad): zero only that
         if self.k_pad > self.k_in:
             x[:, self.k_in:].zero_()
-        inv = self.emb.pull_into(gids, x, self.F, 0) if self.device.type == "cuda" else None
-        if inv is not None:  # fused one-owner pull: table rows -> bf16 input directly
+        if inv is not None:
             U = gids.numel()
         else:
             emb_u, inv = self.emb.pull(gids)

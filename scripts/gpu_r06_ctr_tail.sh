@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 6: the CTR tower input built in one launch (embedding rows + dense block + zero pad): CTR GPU tests, then
+# the sync-free and fixed CTR step x2.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/r06
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ctr.py -m gpu > gpurun_out/r06/ctrt_tests.log 2>&1 || { tail -30 gpurun_out/r06/ctrt_tests.log; exit 1; }
+tail -1 gpurun_out/r06/ctrt_tests.log
+for i in 1 2; do
+  for ex in auto fixed; do
+    timeout -k 10 200 python -u -m kubedl_amd.workers.xdl_ctr --steps 2000 --warmup 20 --exchange $ex > gpurun_out/r06/ctrt_${ex}_$i.log 2>&1 || { tail -20 gpurun_out/r06/ctrt_${ex}_$i.log; exit 1; }
+    python3 -c "import json;d=json.loads([l for l in open('gpurun_out/r06/ctrt_${ex}_$i.log') if l.startswith('{')][-1]);print('$ex run $i:', round(d['steps_per_sec'],1),'steps/s', round(d['samples_per_sec']/1e6,3),'M samples/s  host', d.get('host_issue_ms_per_step'),'ms/step  loss_last', d.get('loss_last'))"
+  done
+done

@@ -620,6 +620,10 @@ def test_fused_pull_builds_the_same_input():
     ref[:, : F * D] = emb_u.bfloat16()[inv2].reshape(B, F * D)
     ref[:, F * D: model.k_in] = dense.bfloat16()
     assert torch.equal(x1, ref)
+    # the dense block and the zero pad written by the gather launch (tail) ==
+    # the separate fill + cast-copy (taken for a non-contiguous dense block)
+    x3, _, _ = model.build_input(ids, dense.t().contiguous().t())
+    assert torch.equal(x3, ref)
 
 
 @pytest.mark.gpu
