@@ -502,6 +502,134 @@ __global__ __launch_bounds__(256) void route_flags_kernel(
   flag[p] = r;
 }
 
+// Route + inclusive scan of the flags in one launch (replaces route_flags_kernel
+// and a two-launch device scan): single-pass scan with decoupled look-back.
+// A block takes the next tile of kScanTile positions from a ticket (tiles are
+// handed out in start order, so a block only ever waits on tiles of blocks
+// that are already running), routes its 8 positions per thread with every
+// load issued first, scans the tile in registers / LDS, publishes its
+// aggregate, looks back over its predecessors' words 64 at a time (wave 0)
+// until one holds an inclusive prefix, and publishes its own.  A status word
+// is one 8-B agent-scope atomic: epoch (31 bits) | state (2: aggregate,
+// prefix) | value (31 bits) -- the payload travels in the flag word, and a
+// word of an earlier launch (older epoch) reads as not ready, so the array is
+// never reset.  A poll that does not become ready within kScanSpins (a
+// protocol bug, never expected) records a fault instead of hanging the GPU.
+constexpr int kScanItems = 8;
+constexpr int kScanTile = 256 * kScanItems;
+constexpr int kScanSpins = 1 << 22;
+
+__device__ __forceinline__ unsigned long long scan_word(uint32_t epoch, uint32_t state, uint32_t v) {
+  return (static_cast<unsigned long long>(epoch) << 33) | (static_cast<unsigned long long>(state) << 31) | v;
+}
+
+__global__ __launch_bounds__(256) void route_scan_kernel(
+    const uint8_t* __restrict__ bins, const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos,
+    const int32_t* __restrict__ split, const int32_t* __restrict__ t_feat, const int32_t* __restrict__ t_bin,
+    int F, int n, int h0, int L, int32_t* __restrict__ flag, int32_t* __restrict__ sc,
+    unsigned long long* __restrict__ status, unsigned* __restrict__ ticket, uint32_t epoch, int* __restrict__ fault) {
+  __shared__ int s_tile, s_excl;
+  __shared__ int s_wsum[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) s_tile = static_cast<int>(__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  const int tile = s_tile;
+  const int p0 = tile * kScanTile + t * kScanItems;
+  int row[kScanItems], hn[kScanItems];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int p = p0 + k;
+    row[k] = p < n ? rows[p] : 0;
+    hn[k] = p < n ? node_pos[p] : -1;
+  }
+  int f[kScanItems];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int i = hn[k] - h0;
+    f[k] = (i >= 0 && i < L && split[i]) ? 1 : 0;
+    if (f[k]) {
+      const int h = hn[k];
+      f[k] = bins[static_cast<int64_t>(row[k]) * F + t_feat[h]] > t_bin[h] ? 1 : 0;
+    }
+  }
+  int incl[kScanItems];
+  int run = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    run += f[k];
+    incl[k] = run;
+    if (p0 + k < n) flag[p0 + k] = f[k];
+  }
+  // block scan of the thread totals
+  int x = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(x, o, 64);
+    if (lane >= o) x += u;
+  }
+  if (lane == 63) s_wsum[w] = x;
+  __syncthreads();
+  int wexcl = 0, agg = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < w) wexcl += s_wsum[k];
+    agg += s_wsum[k];
+  }
+  const int texcl = wexcl + x - run;  // positions of earlier threads in this tile
+  if (w == 0) {
+    int excl = 0;
+    if (tile == 0) {
+      if (lane == 0)
+        __hip_atomic_store(status, scan_word(epoch, 2u, static_cast<uint32_t>(agg)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(status + tile, scan_word(epoch, 1u, static_cast<uint32_t>(agg)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int j = tile - 1;
+      bool bad = false;
+      while (true) {
+        const int jj = j - lane;
+        uint32_t state = 2u, val = 0u;  // past tile 0: a virtual zero prefix
+        if (jj >= 0) {
+          int spins = 0;
+          do {
+            const unsigned long long wd = __hip_atomic_load(status + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            state = static_cast<uint32_t>(wd >> 33) == epoch ? static_cast<uint32_t>((wd >> 31) & 3u) : 0u;
+            val = static_cast<uint32_t>(wd & 0x7fffffffu);
+          } while (state == 0u && ++spins < kScanSpins);
+          if (state == 0u) {
+            bad = true;
+            state = 2u;
+            val = 0u;
+          }
+        }
+        const unsigned long long pm = __ballot(state == 2u);
+        const int stop = pm ? __ffsll(static_cast<long long>(pm)) - 1 : 64;
+        int c = lane <= stop ? static_cast<int>(val) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        excl += c;
+        if (pm) break;
+        j -= 64;
+      }
+      if (__ballot(bad) && lane == 0) atomicAdd(fault, 1);
+      if (lane == 0)
+        __hip_atomic_store(status + tile, scan_word(epoch, 2u, static_cast<uint32_t>(excl + agg)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  const int base = s_excl + texcl;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (p0 + k < n) sc[p0 + k] = base + incl[k];
+  // every block has drawn its ticket once the last tile is handed out: re-arm
+  if (t == 0 && tile == static_cast<int>(gridDim.x) - 1)
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // stable in-segment partition by flag (sc = inclusive scan of flag over all
 // positions): left rows first, then right rows, each in their old order.
 __global__ __launch_bounds__(256) void partition_kernel(
@@ -883,6 +1011,19 @@ hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int3
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(route_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bins, rows, node_pos, split,
                      t_feat, t_bin, F, n, h0, L, flag);
+  return hipGetLastError();
+}
+
+int gbdt_route_scan_tiles(int n) { return (n + kScanTile - 1) / kScanTile; }
+
+hipError_t gbdt_route_scan(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos, const int32_t* split,
+                           const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0, int L, int32_t* flag,
+                           int32_t* sc, unsigned long long* status, unsigned* ticket, uint32_t epoch, int* fault,
+                           hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (epoch == 0 || epoch >= (1u << 31)) return hipErrorInvalidValue;  // 0: the zeroed array's epoch
+  hipLaunchKernelGGL(route_scan_kernel, dim3(gbdt_route_scan_tiles(n)), dim3(256), 0, s, bins, rows, node_pos, split,
+                     t_feat, t_bin, F, n, h0, L, flag, sc, status, ticket, epoch, fault);
   return hipGetLastError();
 }
 

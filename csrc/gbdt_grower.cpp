@@ -82,6 +82,10 @@ class GbdtGrower {
     node_pos_next_ = at::empty({N_}, io);
     flag_ = at::empty({N_}, io);
     sc_ = at::empty({N_}, io);
+    // fused route + scan (csrc/gbdt.hip route_scan_kernel): look-back words, tile ticket, fault count
+    scan_status_ = at::zeros({std::max(1, kdl::gbdt_route_scan_tiles(N_))}, io.dtype(at::kLong));
+    scan_ticket_ = at::zeros({1}, io);
+    scan_fault_ = at::zeros({1}, io);
     for (int d = 0; d <= D_; ++d) {
       lo_.push_back(at::zeros({1LL << d}, io));
       hi_.push_back(at::zeros({1LL << d}, io));
@@ -153,10 +157,22 @@ class GbdtGrower {
                         last ? nullptr : ip(exists_[d + 1]), stream()),
        "gbdt_decide");
     if (last) return at::Tensor();
-    ck(kdl::gbdt_route_flags(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_pos_), ip(split_), ip(feat_),
-                             ip(tbin_), F_, N_, h0, L, ip(flag_), stream()),
-       "gbdt_route_flags");
-    at::cumsum_out(sc_, flag_, 0, at::kInt);
+    if (route_scan_on()) {
+      if (++scan_epoch_ >= (1u << 31)) {  // epochs wrapped: start the words over
+        scan_status_.zero_();
+        scan_epoch_ = 1;
+      }
+      ck(kdl::gbdt_route_scan(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_pos_), ip(split_), ip(feat_), ip(tbin_),
+                              F_, N_, h0, L, ip(flag_), ip(sc_),
+                              reinterpret_cast<unsigned long long*>(scan_status_.data_ptr<int64_t>()),
+                              reinterpret_cast<unsigned*>(ip(scan_ticket_)), scan_epoch_, ip(scan_fault_), stream()),
+         "gbdt_route_scan");
+    } else {
+      ck(kdl::gbdt_route_flags(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_pos_), ip(split_), ip(feat_),
+                               ip(tbin_), F_, N_, h0, L, ip(flag_), stream()),
+         "gbdt_route_flags");
+      at::cumsum_out(sc_, flag_, 0, at::kInt);
+    }
     ck(kdl::gbdt_partition(ip(rows_), ip(node_pos_), ip(split_), ip(lo_[d]), ip(hi_[d]), ip(flag_), ip(sc_), N_,
                            h0, L, ip(rows_next_), ip(node_pos_next_), stream()),
        "gbdt_partition");
@@ -234,6 +250,8 @@ class GbdtGrower {
   // (feature, split_bin, threshold, value) heap arrays of the current tree
   std::vector<at::Tensor> tree() const { return {feat_, tbin_, thr_, val_}; }
   std::vector<int64_t> stats() const { return {builds_, subtracted_}; }
+  // look-backs of the fused route + scan that timed out (syncs; expected 0)
+  int64_t scan_faults() const { return scan_fault_.item<int>(); }
   int64_t rows_per_chunk() const { return rpb_; }
 
  private:
@@ -245,13 +263,65 @@ class GbdtGrower {
   std::vector<at::Tensor> lo_, hi_, exists_;
   at::Tensor split_, gain_, sbin_, gl_, hl_, tot_, feat_, tbin_, thr_, val_;
   at::Tensor hist_cur_, hist_next_, built_, cnt_, build_child_, blo_, bhi_, chunk_off_, gh_max_;
+  at::Tensor scan_status_, scan_ticket_, scan_fault_;
+  uint32_t scan_epoch_ = 0;
+  // KDL_TUNE gbdt_route_scan (default 0): 1 = the fused route + look-back scan (one launch; measured
+  // slower: 59.9 us per level against 23.0 + 14.6 for route_flags + the device scan, 941-952 vs
+  // 1,053-1,064 boosting rounds/s at 2M x 28 -- the look-back's chain of cross-XCD atomic round trips
+  // over 977 tiles; profiles/r06_gbdt_route_scan.txt); 0 = route_flags + a device scan
+  static bool route_scan_on() {
+    if (g_route_scan < 0) g_route_scan = kdl::tune_int("gbdt_route_scan", 0);
+    return g_route_scan != 0;
+  }
+
+ public:
+  static int g_route_scan;
 };
+
+int GbdtGrower::g_route_scan = -1;
+
+// (flag, inclusive scan of flag) of one level's routing, by the fused route + look-back scan
+// (``fused``) or by route_flags + a device scan: the test hook of route_scan_kernel.  ``calls``
+// > 1 repeats the fused launch on one status array (epochs 1, 2, ...): the last result returned.
+std::vector<at::Tensor> gbdt_route_scan_test(const at::Tensor& bins, const at::Tensor& rows,
+                                             const at::Tensor& node_pos, const at::Tensor& split,
+                                             const at::Tensor& t_feat, const at::Tensor& t_bin, int64_t h0,
+                                             int64_t L, bool fused, int64_t calls) {
+  TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.dim() == 2 && bins.is_contiguous(),
+              "gbdt_route_scan_test: uint8 bins [N, F]");
+  for (const at::Tensor* t : {&rows, &node_pos, &split, &t_feat, &t_bin})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous(), "gbdt_route_scan_test: int32");
+  const int n = static_cast<int>(rows.numel()), F = static_cast<int>(bins.size(1));
+  TORCH_CHECK(node_pos.numel() == n && split.numel() >= L && t_feat.numel() >= h0 + L && t_bin.numel() >= h0 + L,
+              "gbdt_route_scan_test: sizes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
+  auto flag = at::empty({n}, rows.options()), sc = at::empty({n}, rows.options());
+  if (!fused) {
+    ck(kdl::gbdt_route_flags(bins.data_ptr<uint8_t>(), ip(rows), ip(node_pos), ip(split), ip(t_feat), ip(t_bin), F,
+                             n, static_cast<int>(h0), static_cast<int>(L), ip(flag), stream()),
+       "gbdt_route_flags");
+    at::cumsum_out(sc, flag, 0, at::kInt);
+    return {flag, sc};
+  }
+  auto status = at::zeros({std::max(1, kdl::gbdt_route_scan_tiles(n))}, rows.options().dtype(at::kLong));
+  auto ticket = at::zeros({1}, rows.options()), fault = at::zeros({1}, rows.options());
+  for (int64_t c = 1; c <= std::max<int64_t>(calls, 1); ++c)
+    ck(kdl::gbdt_route_scan(bins.data_ptr<uint8_t>(), ip(rows), ip(node_pos), ip(split), ip(t_feat), ip(t_bin), F, n,
+                            static_cast<int>(h0), static_cast<int>(L), ip(flag), ip(sc),
+                            reinterpret_cast<unsigned long long*>(status.data_ptr<int64_t>()),
+                            reinterpret_cast<unsigned*>(ip(ticket)), static_cast<uint32_t>(c), ip(fault), stream()),
+       "gbdt_route_scan");
+  TORCH_CHECK(fault.item<int>() == 0, "gbdt_route_scan_test: look-back timeouts");
+  TORCH_CHECK(ticket.item<int>() == 0, "gbdt_route_scan_test: the tile ticket was not re-armed");
+  return {flag, sc};
+}
 
 at::Tensor gbdt_quantise(const at::Tensor& X, const at::Tensor& cuts, int64_t num_bins) {
   TORCH_CHECK(X.is_cuda() && X.dim() == 2, "gbdt_quantise: X [N, F] on the GPU");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   auto x = X.to(at::kFloat).contiguous();
-  auto c = cuts.to(at::kFloat).contiguous();
+  // the cuts may come from a host fit (fit_cuts on a CPU X): the kernel reads them on X's device
+  auto c = cuts.to(X.device(), at::kFloat).contiguous();
   TORCH_CHECK(c.dim() == 2 && c.size(0) == x.size(1), "gbdt_quantise: cuts [F, ncut]");
   TORCH_CHECK(num_bins >= 2 && num_bins <= 256, "gbdt_quantise: 2 <= num_bins <= 256");
   auto out = at::empty(x.sizes(), x.options().dtype(at::kByte));
@@ -279,6 +349,12 @@ void register_gbdt(pybind11::module& m) {
       .def("heap_packed", &GbdtGrower::heap_packed)
       .def("tree", &GbdtGrower::tree)
       .def("stats", &GbdtGrower::stats)
-      .def("rows_per_chunk", &GbdtGrower::rows_per_chunk);
+      .def("rows_per_chunk", &GbdtGrower::rows_per_chunk)
+      .def("scan_faults", &GbdtGrower::scan_faults)
+      .def_static("set_route_scan", [](int v) { GbdtGrower::g_route_scan = v; },
+                  "1: fused route + look-back scan, 0: route_flags + device scan, -1: KDL_TUNE gbdt_route_scan");
   m.def("gbdt_quantise", &gbdt_quantise, "GBDT feature quantisation (bins = #cuts < x, clamped)");
+  m.def("gbdt_route_scan_test", &gbdt_route_scan_test, "(flag, inclusive scan) of a level's routing: fused or two-pass",
+        py::arg("bins"), py::arg("rows"), py::arg("node_pos"), py::arg("split"), py::arg("t_feat"), py::arg("t_bin"),
+        py::arg("h0"), py::arg("L"), py::arg("fused"), py::arg("calls") = 1);
 }

@@ -181,6 +181,15 @@ hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot,
 hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos,
                             const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
                             int L, int32_t* flag, hipStream_t s);
+// route + inclusive scan of the flags in one launch (single-pass, decoupled look-back): flag and
+// sc as gbdt_route_flags + an inclusive scan.  status: gbdt_route_scan_tiles(n) zeroed words;
+// ticket: one zeroed counter (re-armed by the kernel); epoch: 1, 2, ... per call on that status
+// array (< 2^31); fault: counts look-backs that timed out (expected 0)
+int gbdt_route_scan_tiles(int n);
+hipError_t gbdt_route_scan(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos, const int32_t* split,
+                           const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0, int L, int32_t* flag,
+                           int32_t* sc, unsigned long long* status, unsigned* ticket, uint32_t epoch, int* fault,
+                           hipStream_t s);
 hipError_t gbdt_partition(const int32_t* rows, const int32_t* node_pos, const int32_t* split, const int32_t* lo,
                           const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
                           int32_t* rows_next, int32_t* node_pos_next, hipStream_t s);

@@ -425,6 +425,8 @@ class HistGBDT:
             self.cuts = host_cuts["c"].to(self.device)
         elif self.cuts is None:
             self.fit_cuts(X)
+        if self.cuts.device != self.device:  # cuts fitted on a host copy (fit_cuts on a CPU X)
+            self.cuts = self.cuts.to(self.device)
         tb = self._sync_time()
         bins = self.quantise(X).contiguous()
         n = X.shape[0]
@@ -468,6 +470,11 @@ class HistGBDT:
             b, s = grower.stats()
             self.stats["hist_builds"] += b
             self.stats["hist_subtracted"] += s
+            # the fused route + scan's look-back never timed out (a timeout means
+            # its partition was wrong: fail loudly rather than return bad trees)
+            faults = grower.scan_faults()
+            if faults:
+                raise RuntimeError(f"GBDT route+scan: {faults} look-back timeouts (csrc/gbdt.hip route_scan_kernel)")
         return pred
 
     def predict_margin(self, X: torch.Tensor) -> torch.Tensor:

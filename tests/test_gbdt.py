@@ -255,6 +255,55 @@ def test_host_cuts_bitwise_equal_fit_cuts(n, F, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,L", [(2_000_000, 32), (2048 * 37 + 5, 8), (300_000, 1), (1000, 4), (2048 * 130, 64)])
+def test_gpu_fused_route_scan_matches_two_pass(n, L):
+    """The fused route + look-back scan (one launch, csrc/gbdt.hip route_scan_kernel)
+    == route_flags + a device scan, bit for bit: many tiles (look-back windows
+    of 64 predecessors and more), a ragged last tile, positions of non-split
+    nodes and of other levels, and repeated launches on one status array (the
+    epoch advancing over the previous launch's words, the ticket re-armed)."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g = torch.Generator().manual_seed(n % 1000 + L)
+    F, h0 = 28, L - 1
+    bins = torch.randint(0, 256, (n, F), generator=g, dtype=torch.uint8)
+    rows = torch.randperm(n, generator=g).int()
+    node_pos = (h0 + torch.randint(0, L, (n,), generator=g)).int()
+    node_pos[::97] = h0 + L  # a deeper level's position: never routed here
+    split = (torch.rand(L, generator=g) < 0.8).int()
+    heap = 2 * (h0 + L) + 3
+    t_feat = torch.randint(0, F, (heap,), generator=g).int()
+    t_bin = torch.randint(0, 255, (heap,), generator=g).int()
+    args = [t.cuda() for t in (bins, rows, node_pos, split, t_feat, t_bin)]
+    ref_f, ref_s = ext.gbdt_route_scan_test(*args, h0, L, False)
+    for calls in (1, 3):
+        f, sc = ext.gbdt_route_scan_test(*args, h0, L, True, calls)
+        assert torch.equal(f, ref_f) and torch.equal(sc, ref_s), calls
+    assert int(ref_s[-1]) == int(ref_f.sum())
+
+
+@pytest.mark.gpu
+def test_gpu_fused_route_scan_fit_agrees():
+    """A whole fit with the fused route + scan grows the two-pass fit's trees (up to
+    near-ties of the fp32 flush order) and raises no look-back fault."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    X, y = _data(300_000, 12, seed=9)
+    res = {}
+    try:
+        for mode in (0, 1):
+            ext.GbdtGrower.set_route_scan(mode)
+            m = HistGBDT(GBDTParams(objective="binary:logistic", n_estimators=4, max_depth=6, max_bin=64), "cuda")
+            m.fit_cuts(X, sample=len(X))
+            pred = m.fit(X, y)
+            res[mode] = (m.metric(pred, y.cuda()), m.trees[0][0])
+    finally:
+        ext.GbdtGrower.set_route_scan(-1)
+    assert res[1][1].feature[:7] == res[0][1].feature[:7]  # the first levels of the first tree
+    assert abs(res[1][0]["accuracy"] - res[0][0]["accuracy"]) < 2e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("F", [28, 12, 64, 100, 7])
 def test_gpu_row_per_lane_hist_equals_slot_kernel(F):
     """The row-per-lane build (dword bin loads, g / h quantised once per row)
