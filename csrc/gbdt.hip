@@ -486,20 +486,43 @@ __global__ __launch_bounds__(256) void decide_kernel(
 // row at position p, moved with the rows by partition_kernel): a coalesced read
 // where a row-indexed node id was a dependent random gather (both kernels are
 // latency-bound: waves parked ~90 % of their cycles, scripts/gpu_r06_gbdt_pmc.sh).
+// kRouteItems positions per thread (strided by the block width: coalesced), every
+// level of the dependent load chain (row / node -> split, feature, bin -> the
+// row's bin code) issued for all items before the next level is used
+constexpr int kRouteItems = 4;
+
+// The bin code of (row, f) is bins[row * rs + f * fs]: row-major [N, F] (rs = F,
+// fs = 1) or the grower's feature-major copy [F, N] (rs = 1, fs = N) -- a node's
+// rows keep their original order (stable partitions), so at shallow levels
+// consecutive positions read nearby bytes of one feature's column instead of
+// one 64-B sector per position.
 __global__ __launch_bounds__(256) void route_flags_kernel(
     const uint8_t* __restrict__ bins, const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos,
     const int32_t* __restrict__ split, const int32_t* __restrict__ t_feat, const int32_t* __restrict__ t_bin,
-    int F, int n, int h0, int L, int32_t* __restrict__ flag) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
-  const int row = rows[p];
-  const int i = node_pos[p] - h0;
-  int r = 0;
-  if (i >= 0 && i < L && split[i]) {
-    const int h = h0 + i;
-    r = bins[static_cast<int64_t>(row) * F + t_feat[h]] > t_bin[h] ? 1 : 0;
+    int64_t rs, int64_t fs, int n, int h0, int L, int32_t* __restrict__ flag) {
+  const int p0 = blockIdx.x * 256 * kRouteItems + threadIdx.x;
+  int row[kRouteItems], i[kRouteItems], sp[kRouteItems], fe[kRouteItems], tb[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    row[k] = p < n ? rows[p] : 0;
+    i[k] = p < n ? node_pos[p] - h0 : -1;
   }
-  flag[p] = r;
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const bool in = i[k] >= 0 && i[k] < L;
+    sp[k] = in ? split[i[k]] : 0;
+    fe[k] = in ? t_feat[h0 + i[k]] : 0;
+    tb[k] = in ? t_bin[h0 + i[k]] : 0;
+  }
+  int b[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) b[k] = sp[k] ? bins[row[k] * rs + fe[k] * fs] : 0;
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    if (p < n) flag[p] = (sp[k] && b[k] > tb[k]) ? 1 : 0;
+  }
 }
 
 // Route + inclusive scan of the flags in one launch (replaces route_flags_kernel
@@ -632,35 +655,52 @@ __global__ __launch_bounds__(256) void route_scan_kernel(
 
 // stable in-segment partition by flag (sc = inclusive scan of flag over all
 // positions): left rows first, then right rows, each in their old order.
+// (kRouteItems positions per thread, each load level issued for all of them first)
 __global__ __launch_bounds__(256) void partition_kernel(
     const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ split,
     const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, const int32_t* __restrict__ flag,
     const int32_t* __restrict__ sc, int n, int h0, int L, int32_t* __restrict__ rows_next,
     int32_t* __restrict__ node_pos_next) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
-  const int row = rows[p];
-  const int hn = node_pos[p];
-  const int i = hn - h0;
-  if (i >= 0 && i < L && split[i]) {
-    const int s0 = lo[i], s1 = hi[i];
-    const int base = s0 > 0 ? sc[s0 - 1] : 0;
-    const int rb = sc[p] - flag[p] - base;  // right rows before p in the segment
-    const int rt = sc[s1 - 1] - base;
-    const int nl = (s1 - s0) - rt;
-    int np, child;
-    if (flag[p]) {
-      np = s0 + nl + rb;
-      child = 2 * hn + 2;
+  const int p0 = blockIdx.x * 256 * kRouteItems + threadIdx.x;
+  int row[kRouteItems], hn[kRouteItems], fl[kRouteItems], scp[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    const bool ok = p < n;
+    row[k] = ok ? rows[p] : 0;
+    hn[k] = ok ? node_pos[p] : -1;
+    fl[k] = ok ? flag[p] : 0;
+    scp[k] = ok ? sc[p] : 0;
+  }
+  int s0[kRouteItems], s1[kRouteItems], sp[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int i = hn[k] - h0;
+    const bool in = i >= 0 && i < L;
+    sp[k] = in ? split[i] : 0;
+    s0[k] = in ? lo[i] : 0;
+    s1[k] = in ? hi[i] : 0;
+  }
+  int base[kRouteItems], tot[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    base[k] = (sp[k] && s0[k] > 0) ? sc[s0[k] - 1] : 0;
+    tot[k] = sp[k] ? sc[s1[k] - 1] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    if (p >= n) continue;
+    if (sp[k]) {
+      const int rb = scp[k] - fl[k] - base[k];  // right rows before p in the segment
+      const int nl = (s1[k] - s0[k]) - (tot[k] - base[k]);
+      const int np = fl[k] ? s0[k] + nl + rb : s0[k] + (p - s0[k] - rb);
+      rows_next[np] = row[k];
+      node_pos_next[np] = fl[k] ? 2 * hn[k] + 2 : 2 * hn[k] + 1;
     } else {
-      np = s0 + (p - s0 - rb);
-      child = 2 * hn + 1;
+      rows_next[p] = row[k];
+      node_pos_next[p] = hn[k];
     }
-    rows_next[np] = row;
-    node_pos_next[np] = child;
-  } else {
-    rows_next[p] = row;
-    node_pos_next[p] = hn;
   }
 }
 
@@ -1007,10 +1047,11 @@ hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot,
 
 hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos,
                             const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
-                            int L, int32_t* flag, hipStream_t s) {
+                            int L, int32_t* flag, hipStream_t s, bool feature_major) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(route_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bins, rows, node_pos, split,
-                     t_feat, t_bin, F, n, h0, L, flag);
+  const int64_t rs = feature_major ? 1 : F, fs = feature_major ? n : 1;
+  hipLaunchKernelGGL(route_flags_kernel, dim3((n + 256 * kRouteItems - 1) / (256 * kRouteItems)), dim3(256), 0, s,
+                     bins, rows, node_pos, split, t_feat, t_bin, rs, fs, n, h0, L, flag);
   return hipGetLastError();
 }
 
@@ -1031,8 +1072,8 @@ hipError_t gbdt_partition(const int32_t* rows, const int32_t* node_pos, const in
                           const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
                           int32_t* rows_next, int32_t* node_pos_next, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(partition_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, node_pos, split, lo, hi,
-                     flag, sc, n, h0, L, rows_next, node_pos_next);
+  hipLaunchKernelGGL(partition_kernel, dim3((n + 256 * kRouteItems - 1) / (256 * kRouteItems)), dim3(256), 0, s, rows,
+                     node_pos, split, lo, hi, flag, sc, n, h0, L, rows_next, node_pos_next);
   return hipGetLastError();
 }
 

@@ -80,6 +80,8 @@ class GbdtGrower {
     node_of_row_ = at::zeros({N_}, io);
     node_pos_ = at::empty({N_}, io);
     node_pos_next_ = at::empty({N_}, io);
+    // feature-major copy of the bin codes for the routing passes (route_flags_kernel): N x F bytes
+    bins_t_ = bins_.t().contiguous();
     flag_ = at::empty({N_}, io);
     sc_ = at::empty({N_}, io);
     // fused route + scan (csrc/gbdt.hip route_scan_kernel): look-back words, tile ticket, fault count
@@ -168,8 +170,8 @@ class GbdtGrower {
                               reinterpret_cast<unsigned*>(ip(scan_ticket_)), scan_epoch_, ip(scan_fault_), stream()),
          "gbdt_route_scan");
     } else {
-      ck(kdl::gbdt_route_flags(bins_.data_ptr<uint8_t>(), ip(rows_), ip(node_pos_), ip(split_), ip(feat_),
-                               ip(tbin_), F_, N_, h0, L, ip(flag_), stream()),
+      ck(kdl::gbdt_route_flags(bins_t_.data_ptr<uint8_t>(), ip(rows_), ip(node_pos_), ip(split_), ip(feat_),
+                               ip(tbin_), F_, N_, h0, L, ip(flag_), stream(), true),
          "gbdt_route_flags");
       at::cumsum_out(sc_, flag_, 0, at::kInt);
     }
@@ -255,7 +257,7 @@ class GbdtGrower {
   int64_t rows_per_chunk() const { return rpb_; }
 
  private:
-  at::Tensor bins_, cuts_, grad_, hess_;
+  at::Tensor bins_, bins_t_, cuts_, grad_, hess_;
   int N_ = 0, F_ = 0, B_ = 0, D_ = 0, ncut_ = 0, rpb_ = 256;
   float lam_ = 1.f, gamma_ = 0.f, lr_ = 0.3f, mcw_ = 1.f;
   int64_t per_node_ = 0, builds_ = 0, subtracted_ = 0;
@@ -286,7 +288,7 @@ int GbdtGrower::g_route_scan = -1;
 std::vector<at::Tensor> gbdt_route_scan_test(const at::Tensor& bins, const at::Tensor& rows,
                                              const at::Tensor& node_pos, const at::Tensor& split,
                                              const at::Tensor& t_feat, const at::Tensor& t_bin, int64_t h0,
-                                             int64_t L, bool fused, int64_t calls) {
+                                             int64_t L, bool fused, int64_t calls, bool feature_major) {
   TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.dim() == 2 && bins.is_contiguous(),
               "gbdt_route_scan_test: uint8 bins [N, F]");
   for (const at::Tensor* t : {&rows, &node_pos, &split, &t_feat, &t_bin})
@@ -297,8 +299,9 @@ std::vector<at::Tensor> gbdt_route_scan_test(const at::Tensor& bins, const at::T
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
   auto flag = at::empty({n}, rows.options()), sc = at::empty({n}, rows.options());
   if (!fused) {
-    ck(kdl::gbdt_route_flags(bins.data_ptr<uint8_t>(), ip(rows), ip(node_pos), ip(split), ip(t_feat), ip(t_bin), F,
-                             n, static_cast<int>(h0), static_cast<int>(L), ip(flag), stream()),
+    at::Tensor b = feature_major ? bins.t().contiguous() : bins;
+    ck(kdl::gbdt_route_flags(b.data_ptr<uint8_t>(), ip(rows), ip(node_pos), ip(split), ip(t_feat), ip(t_bin), F,
+                             n, static_cast<int>(h0), static_cast<int>(L), ip(flag), stream(), feature_major),
        "gbdt_route_flags");
     at::cumsum_out(sc, flag, 0, at::kInt);
     return {flag, sc};
@@ -356,5 +359,5 @@ void register_gbdt(pybind11::module& m) {
   m.def("gbdt_quantise", &gbdt_quantise, "GBDT feature quantisation (bins = #cuts < x, clamped)");
   m.def("gbdt_route_scan_test", &gbdt_route_scan_test, "(flag, inclusive scan) of a level's routing: fused or two-pass",
         py::arg("bins"), py::arg("rows"), py::arg("node_pos"), py::arg("split"), py::arg("t_feat"), py::arg("t_bin"),
-        py::arg("h0"), py::arg("L"), py::arg("fused"), py::arg("calls") = 1);
+        py::arg("h0"), py::arg("L"), py::arg("fused"), py::arg("calls") = 1, py::arg("feature_major") = false);
 }

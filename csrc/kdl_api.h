@@ -177,10 +177,11 @@ hipError_t gbdt_decide(const float* gain, const int32_t* sbin, const float* tot,
                        const int32_t* exists, int L, int F, int ncut, int h0, int can_split, float lambda,
                        float gamma, float lr, int32_t* t_feat, int32_t* t_bin, float* t_thr, float* t_val,
                        int32_t* split, int32_t* exists_next, hipStream_t s);
-// node_pos: the heap node of the row at each POSITION (moved with the rows by gbdt_partition)
+// node_pos: the heap node of the row at each POSITION (moved with the rows by gbdt_partition);
+// feature_major: bins is the [F, N] copy (bins[f * n + row]), else [N, F]
 hipError_t gbdt_route_flags(const uint8_t* bins, const int32_t* rows, const int32_t* node_pos,
                             const int32_t* split, const int32_t* t_feat, const int32_t* t_bin, int F, int n, int h0,
-                            int L, int32_t* flag, hipStream_t s);
+                            int L, int32_t* flag, hipStream_t s, bool feature_major = false);
 // route + inclusive scan of the flags in one launch (single-pass, decoupled look-back): flag and
 // sc as gbdt_route_flags + an inclusive scan.  status: gbdt_route_scan_tiles(n) zeroed words;
 // ticket: one zeroed counter (re-armed by the kernel); epoch: 1, 2, ... per call on that status

@@ -276,6 +276,8 @@ def test_gpu_fused_route_scan_matches_two_pass(n, L):
     t_bin = torch.randint(0, 255, (heap,), generator=g).int()
     args = [t.cuda() for t in (bins, rows, node_pos, split, t_feat, t_bin)]
     ref_f, ref_s = ext.gbdt_route_scan_test(*args, h0, L, False)
+    fm_f, fm_s = ext.gbdt_route_scan_test(*args, h0, L, False, 1, True)  # the grower's feature-major bins
+    assert torch.equal(fm_f, ref_f) and torch.equal(fm_s, ref_s)
     for calls in (1, 3):
         f, sc = ext.gbdt_route_scan_test(*args, h0, L, True, calls)
         assert torch.equal(f, ref_f) and torch.equal(sc, ref_s), calls
