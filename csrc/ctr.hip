@@ -68,6 +68,55 @@ __device__ __forceinline__ float ordered_sum(const float* __restrict__ part, int
   return a;
 }
 
+// Ticketed hand-off of per-block partials to the last block to arrive (the
+// in-launch split reductions below).  sc1 = 0: plain partial stores, an agent
+// release fence before the ticket and an acquire in the last block -- the
+// release writes back every dirty line of the XCD's L2, ~6.5 us per block with
+// a freshly stored output tile (MI355X_MICROARCH.md).  sc1 = 1: partials stored
+// and read with agent-scope relaxed atomics (global_store / global_load sc1:
+// written through, read past L1), the ticket add after every storing wave's
+// vmcnt(0) and a barrier, no fence (the hand-off table's row 1).
+__device__ __forceinline__ void part_store(float* p, float v, int sc1) {
+  if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+__device__ __forceinline__ float part_sum(const float* __restrict__ part, int n, int64_t stride, int sc1) {
+  if (!sc1) return ordered_sum(part, n, stride);
+  float a = 0.f;
+  for (int r0 = 0; r0 < n; r0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      v[j] = r0 + j < n ? __hip_atomic_load(const_cast<float*>(part) + static_cast<int64_t>(r0 + j) * stride,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a += v[j];
+  }
+  return a;
+}
+
+// every thread, after its partial stores: true in the block that arrived last
+__device__ __forceinline__ bool handoff_last(unsigned* cnt, unsigned arrivals, int sc1, int* last) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (!sc1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const bool l = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1;
+    if (l && !sc1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *last = l;
+  }
+  __syncthreads();
+  return *last != 0;
+}
+
 // BM_ x BN_ tile (128x128, 128x64 or 64x64): 4 waves as 2x2, each wave
 // (BM_/2) x (BN_/2) = I x J MFMA 32x32 blocks.  A 4096-row batch gives a
 // 128x128 tiling only 64-256 tiles on 256 CUs (one wave per SIMD, nothing to
@@ -91,7 +140,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, const float* __restrict__ bias32,
     const bf16_t* __restrict__ bias16, bf16_t* __restrict__ C, int M, int N, int K, int tiles_n,
     const bf16_t* __restrict__ ymask = nullptr, float* __restrict__ part = nullptr, unsigned* __restrict__ cnt = nullptr,
-    bf16_t* __restrict__ db = nullptr) {
+    bf16_t* __restrict__ db = nullptr, int sc1 = 0) {
   constexpr int I = BM_ / 64, J = BN_ / 64;
   constexpr int SA = BM_ / 32, SB = BN_ / 32;  // 16-B chunks per thread per k-tile (rows x 8 chunks / 256)
   constexpr int SBT = BN_ + 32;                // BT: B image row (elements)
@@ -245,23 +294,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
       if (fh == 0) dred[wave >> 1][wn + j * 32 + fr] = cs[j];
     }
     __syncthreads();
-    if (t < BN_ && n0 + t < N) part[static_cast<int64_t>(tile_m) * N + n0 + t] = dred[0][t] + dred[1][t];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned tk = __hip_atomic_fetch_add(cnt + tile_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = tk == static_cast<unsigned>(tiles_m) - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    if (!last) return;
+    if (t < BN_ && n0 + t < N) part_store(part + static_cast<int64_t>(tile_m) * N + n0 + t, dred[0][t] + dred[1][t], sc1);
+    if (!handoff_last(cnt + tile_n, static_cast<unsigned>(tiles_m), sc1, &last)) return;
     if (t < BN_ && n0 + t < N) {
-      db[n0 + t] = f32_to_bf16(ordered_sum(part + n0 + t, tiles_m, N));  // tile order
+      db[n0 + t] = f32_to_bf16(part_sum(part + n0 + t, tiles_m, N, sc1));  // tile order
     }
     if (t == 0) __hip_atomic_store(cnt + tile_n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -312,7 +348,7 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
                                                              bf16_t* __restrict__ dz, float* __restrict__ part,
                                                              unsigned* __restrict__ cnt, bf16_t* __restrict__ db16,
                                                              float* __restrict__ db32, int M, int N,
-                                                             int rows_per_block) {
+                                                             int rows_per_block, int sc1) {
   __shared__ float red[8][32 * 8];
   __shared__ int last;
   const int cl = threadIdx.x & 31;        // column group within the block
@@ -364,24 +400,11 @@ __global__ __launch_bounds__(256) void relu_bwd_dbias_kernel(const bf16_t* __res
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) a += red[r][c];
-    part[static_cast<int64_t>(blockIdx.x) * N + col] = a;
+    part_store(part + static_cast<int64_t>(blockIdx.x) * N + col, a, sc1);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
+  if (!handoff_last(cnt + blockIdx.y, gridDim.x, sc1, &last)) return;
   if (col < N) {
-    const float a = ordered_sum(part + col, static_cast<int>(gridDim.x), N);
+    const float a = part_sum(part + col, static_cast<int>(gridDim.x), N, sc1);
     if (db16) db16[col] = f32_to_bf16(a);
     else db32[col] = a;
   }
@@ -861,7 +884,7 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
                                                            float* __restrict__ dw_part, float* __restrict__ db_part,
                                                            unsigned* __restrict__ cnt, bf16_t* __restrict__ dw,
                                                            bf16_t* __restrict__ db, float* __restrict__ dbx_part,
-                                                           bf16_t* __restrict__ dbx) {
+                                                           bf16_t* __restrict__ dbx, int sc1) {
   __shared__ float red[8][257];
   __shared__ float redx[MASK ? 8 : 1][MASK ? 256 : 1];
   __shared__ int last;
@@ -909,50 +932,45 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
       float t = 0.f;
 #pragma unroll
       for (int r = 0; r < 8; ++r) t += red[r][c];
-      dw_part[static_cast<int64_t>(blockIdx.x) * K + kb + c] = t;
+      part_store(dw_part + static_cast<int64_t>(blockIdx.x) * K + kb + c, t, sc1);
       if constexpr (MASK) {
         float tx = 0.f;
 #pragma unroll
         for (int r = 0; r < 8; ++r) tx += redx[r][c];
-        dbx_part[static_cast<int64_t>(blockIdx.x) * K + kb + c] = tx;
+        part_store(dbx_part + static_cast<int64_t>(blockIdx.x) * K + kb + c, tx, sc1);
       }
     }
     if (kb == 0 && threadIdx.x == 0) {
       float t = 0.f;
 #pragma unroll
       for (int r = 0; r < 8; ++r) t += red[r][256];
-      db_part[blockIdx.x] = t;
+      part_store(db_part + blockIdx.x, t, sc1);
     }
     __syncthreads();
   }
   if (dw == nullptr) return;  // partials only (the caller sums them)
   // the last block to arrive sums the partials in block order into bf16 dw / db
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
+  if (!handoff_last(cnt, gridDim.x, sc1, &last)) return;
   for (int k = threadIdx.x; k < K; k += 256) {
-    const float t = ordered_sum(dw_part + k, static_cast<int>(gridDim.x), K);
+    const float t = part_sum(dw_part + k, static_cast<int>(gridDim.x), K, sc1);
     dw[k] = f32_to_bf16(t);
-    if constexpr (MASK) dbx[k] = f32_to_bf16(ordered_sum(dbx_part + k, static_cast<int>(gridDim.x), K));
+    if constexpr (MASK) dbx[k] = f32_to_bf16(part_sum(dbx_part + k, static_cast<int>(gridDim.x), K, sc1));
   }
   if (threadIdx.x == 0) {
-    const float t = ordered_sum(db_part, static_cast<int>(gridDim.x), 1);
+    const float t = part_sum(db_part, static_cast<int>(gridDim.x), 1, sc1);
     db[0] = f32_to_bf16(t);
     __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 }  // namespace
+
+// the split reductions' hand-off (handoff_last): KDL_TUNE ctr_handoff 1 = sc1 partials, no
+// fences; 0 = release / acquire fences
+static int handoff_sc1() {
+  static const int v = tune_int("ctr_handoff", 0) != 0 ? 1 : 0;
+  return v;
+}
 
 int head_bce_fwd_blocks(int M) { return (M + 4 * kHeadRowsPerWave - 1) / (4 * kHeadRowsPerWave); }
 
@@ -983,11 +1001,12 @@ hipError_t head_bce_bwd(const void* x, const void* w, const float* dlogit, float
     hipLaunchKernelGGL(head_bce_bwd_kernel<true>, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
                        static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx),
                        dw_part, db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), dbx_part,
-                       static_cast<bf16_t*>(dbx));
+                       static_cast<bf16_t*>(dbx), handoff_sc1());
   else
     hipLaunchKernelGGL(head_bce_bwd_kernel<false>, dim3(nb), dim3(256), 0, s, static_cast<const bf16_t*>(x),
                        static_cast<const bf16_t*>(w), dlogit, scale, gscale, M, K, rpb, static_cast<bf16_t*>(dx),
-                       dw_part, db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), nullptr, nullptr);
+                       dw_part, db_part, cnt, static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), nullptr, nullptr,
+                       handoff_sc1());
   return hipGetLastError();
 }
 
@@ -1091,7 +1110,7 @@ hipError_t gemm_dgrad_relu(const void* A, const void* B, const void* y, void* C,
   do {                                                                                                           \
     const int tn = (N + TN - 1) / TN, tm = (M + TM - 1) / TM;                                                    \
     hipLaunchKernelGGL((gemm_bias_act_kernel<false, TM, TN, true, true>), dim3(tn * tm), dim3(kThreads), 0, s, a, b, \
-                       nullptr, nullptr, c, M, N, K, tn, ym, part, cnt, d);                                      \
+                       nullptr, nullptr, c, M, N, K, tn, ym, part, cnt, d, handoff_sc1());                       \
   } while (0)
   if (cfg == 0) CTR_LAUNCH_DM(128, 128);
   else if (cfg == 1) CTR_LAUNCH_DM(128, 64);
@@ -1128,7 +1147,7 @@ hipError_t relu_bwd_dbias(const void* dy, const void* y, void* dz, float* part, 
   hipLaunchKernelGGL(relu_bwd_dbias_kernel, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dy),
                      static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dz), part, cnt,
                      db_bf16 ? static_cast<bf16_t*>(db) : nullptr, db_bf16 ? nullptr : static_cast<float*>(db), M, N,
-                     rows_per_block);
+                     rows_per_block, handoff_sc1());
   return hipGetLastError();
 }
 
