@@ -17,11 +17,11 @@ MI355X-first re-design:
   (``segment_reduce``) so only one row per unique id crosses xGMI.
 * **Dense tower on MFMA.**  ``FusedLinear`` runs forward as the hand-written
   ``gemm_bias_act`` kernel (v_mfma_f32_32x32x16_bf16, bias + ReLU fused in the
-  epilogue; the wide layers on the LDS-DMA igemm loop); backward fuses
-  ReLU-mask + bias-gradient (``relu_bwd_dbias``; opt-in: folded into the
-  launch that produces the gradient, ``head_bce_bwd`` relu_x /
-  ``gemm_dgrad_relu``), runs dx on ``gemm_bias_act`` and dW on the LDS-DMA
-  weight-gradient kernel
+  epilogue; the wide layers on the LDS-DMA igemm loop); the training step
+  folds each ReLU mask + bias gradient into the launch that produces the
+  gradient (``head_bce_bwd`` relu_x, ``gemm_dgrad_relu``: dx = dz W masked,
+  with its column sums; the autograd path keeps ``relu_bwd_dbias``), and dW
+  runs on the LDS-DMA weight-gradient kernel
   (csrc/wgrad_dma.hip); the 1-wide logit layer is fused with the sigmoid-BCE
   loss (``head_bce_fwd/bwd``: a GEMV per row + loss + dlogit in one pass,
   dx / dw / db in one backward pass) -- no vendor GEMM in the step.
@@ -152,12 +152,13 @@ _FUSED_RELU_BWD = []
 def _fused_relu_bwd() -> bool:
     if not _FUSED_RELU_BWD:
         from ..utils.tune import tune
-        # default off: each fused launch ends in a ticketed cross-block reduction
-        # whose agent release writes back the freshly stored gradient tile -- the
-        # 1024- / 512-wide data gradients ran 32.7 / 23.4 us against 14 / 7 us
-        # unfused + relu_bwd_dbias, and the step 10.94-10.96 vs 11.01-11.02 M
-        # samples/s (profiles/r06_ctr_fused_relu_bwd.txt)
-        _FUSED_RELU_BWD.append(bool(tune("ctr_fused_relu_bwd", 0)))
+        # each fused launch ends in a ticketed cross-block reduction: with the
+        # release / acquire hand-off (KDL_TUNE ctr_handoff=0) the release wrote
+        # back the freshly stored gradient tile and the fusion lost (10.94-10.96
+        # vs 11.01-11.02 M samples/s, profiles/r06_ctr_fused_relu_bwd.txt); with
+        # the fence-free sc1 hand-off (default) it wins: 11.54-11.58 vs 11.43-11.47
+        # (profiles/r06_ctr_handoff.txt)
+        _FUSED_RELU_BWD.append(bool(tune("ctr_fused_relu_bwd", 1)))
     return _FUSED_RELU_BWD[0]
 
 
@@ -250,10 +251,10 @@ class DenseTower(nn.Module):
         one = getattr(self, "_one", None)
         if one is None or one.device != x.device:
             one = self._one = torch.ones(1, device=x.device)
-        # KDL_TUNE ctr_fused_relu_bwd=1: every ReLU backward and bias gradient
-        # fused into the launch that produces the gradient (head backward, then
-        # each layer's data-gradient GEMM): dz is the pre-activation gradient of
-        # layer i, db its bias grad
+        # every ReLU backward and bias gradient fused into the launch that
+        # produces the gradient (head backward, then each layer's data-gradient
+        # GEMM): dz is the pre-activation gradient of layer i, db its bias grad
+        # (KDL_TUNE ctr_fused_relu_bwd=0: the relu_bwd_dbias pass above)
         if not _fused_relu_bwd():  # A/B: the separate relu_bwd_dbias pass per layer
             dy, dw, db = _head_bwd(acts[-1], hw, hb.dtype, dlogit, one)
             for p, g in ((hw, dw), (hb, db)):

@@ -24,7 +24,7 @@ p2p_timeout_s       300         P2P all-reduce bounded-wait timeout
 progress_min_s      0.2         seconds between rank progress-file writes
 ctr_a2a_slack       0           CTR exchange capacity = slack x recent fill (0: exact)
 ctr_a2a_strict      1           raise on a CTR exchange overflow (0: lossy, counted)
-ctr_fused_relu_bwd  0           CTR tower: ReLU backward + bias grads inside the producing launches
+ctr_fused_relu_bwd  1           CTR tower: ReLU backward + bias grads inside the producing launches
 ==================  ==========  ================================================
 """
 from __future__ import annotations
