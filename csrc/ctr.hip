@@ -117,6 +117,19 @@ __device__ __forceinline__ bool handoff_last(unsigned* cnt, unsigned arrivals, i
   return *last != 0;
 }
 
+// 8 bf16 <-> 8 fp32 through one 16-B register
+__device__ __forceinline__ void u4_to_f8(const uint4 v, float (&o)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 f8_to_u4(const float (&o)[8]) {
+  return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
+}
+
 // BM_ x BN_ tile (128x128, 128x64 or 64x64): 4 waves as 2x2, each wave
 // (BM_/2) x (BN_/2) = I x J MFMA 32x32 blocks.  A 4096-row batch gives a
 // 128x128 tiling only 64-256 tiles on 256 CUs (one wave per SIMD, nothing to
@@ -262,60 +275,104 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
     if (kt + 1 < nk) swrite(cur ^ 1);
     __syncthreads();
   }
-  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  if constexpr (DM) {
-    __shared__ float dred[2][BN_];  // column sums of the two wave rows (wm halves)
-    __shared__ int last;
-    float cs[J];
+  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // N % 8 == 0 (every DM / BT launch): the tile goes through LDS (the K-loop
+  // buffers are free: the last iteration ended in a barrier) and leaves as
+  // 16-B row chunks -- the lanes of a 32x32 block hold one column each, so a
+  // direct store is a 2-byte store per element (and DM's mask a 2-byte load).
+  const bool vec = (N & 7) == 0;
+  if (vec) {
+    constexpr int LDC = BN_ + 8;
+    static_assert(BM_ * LDC <= 2 * (BOFF + BSZ), "C tile fits the K-loop buffers");
+    bf16_t* Cs = &lds[0][0];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int col = n0 + wn + j * 32 + fr;
-      cs[j] = 0.f;
-      bf16_t yv[I][16];
+      const int cl = wn + j * 32 + fr;
+      float bv = 0.f;
+      if constexpr (!DM) {
+        if (n0 + cl < N) bv = bias32 ? bias32[n0 + cl] : bias16 ? bf16_to_f32(bias16[n0 + cl]) : 0.f;
+      }
 #pragma unroll
       for (int i = 0; i < I; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          yv[i][r] = (row < M && col < N) ? ymask[static_cast<int64_t>(row) * N + col] : bf16_t(0);
+          float v = acc[i][j][r] + bv;  // one rounding, after bias and ReLU (as the direct path)
+          if (RELU) v = v > 0.f ? v : 0.f;
+          Cs[(wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh) * LDC + cl] = f32_to_bf16(v);
         }
+    }
+    __syncthreads();
+    constexpr int CPR = BN_ / 8, RPP = kThreads / CPR, NP = BM_ / RPP;
+    const int ec = t % CPR, er0 = t / CPR;
+    const int col = n0 + ec * 8;
+    uint4 yv[NP];
+    if constexpr (DM) {
 #pragma unroll
-      for (int i = 0; i < I; ++i)
+      for (int ps = 0; ps < NP; ++ps) {
+        const int row = m0 + ps * RPP + er0;
+        yv[ps] = (row < M && col < N) ? *reinterpret_cast<const uint4*>(ymask + static_cast<int64_t>(row) * N + col)
+                                      : make_uint4(0, 0, 0, 0);
+      }
+    }
+    float cs8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs8[k] = 0.f;
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps) {
+      const int rl = ps * RPP + er0, row = m0 + rl;
+      if (row < M && col < N) {
+        uint4 v = *reinterpret_cast<const uint4*>(&Cs[rl * LDC + ec * 8]);
+        if constexpr (DM) {
+          float x[8], yy[8];
+          u4_to_f8(v, x);
+          u4_to_f8(yv[ps], yy);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            x[k] = yy[k] > 0.f ? x[k] : 0.f;
+            cs8[k] += x[k];
+          }
+          v = f8_to_u4(x);
+        }
+        *reinterpret_cast<uint4*>(C + static_cast<int64_t>(row) * N + col) = v;
+      }
+    }
+    if constexpr (DM) {
+      // column sums: the RPP row groups folded in order through LDS (after
+      // every thread's tile reads), then the ticketed cross-tile reduction
+      __shared__ int last;
+      float* red = reinterpret_cast<float*>(&lds[0][0]);  // [RPP][BN_]
+      static_assert(RPP * BN_ * 4 <= 2 * (BOFF + BSZ) * 2, "column-sum scratch fits");
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[er0 * BN_ + ec * 8 + k] = cs8[k];
+      __syncthreads();
+      if (t < BN_ && n0 + t < N) {
+        float a = 0.f;
+        for (int rr = 0; rr < RPP; ++rr) a += red[rr * BN_ + t];
+        part_store(part + static_cast<int64_t>(tile_m) * N + n0 + t, a, sc1);
+      }
+      if (!handoff_last(cnt + tile_n, static_cast<unsigned>(tiles_m), sc1, &last)) return;
+      if (t < BN_ && n0 + t < N) db[n0 + t] = f32_to_bf16(part_sum(part + n0 + t, tiles_m, N, sc1));  // tile order
+      if (t == 0) __hip_atomic_store(cnt + tile_n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if constexpr (!DM) {  // ragged N (the forward path only): element stores
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int col = n0 + wn + j * 32 + fr;
+      float bv = 0.f;
+      if (col < N) bv = bias32 ? bias32[col] : bias16 ? bf16_to_f32(bias16[col]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
           if (row < M && col < N) {
-            const bf16_t v = bf16_to_f32(yv[i][r]) > 0.f ? f32_to_bf16(acc[i][j][r]) : bf16_t(0);
-            C[static_cast<int64_t>(row) * N + col] = v;
-            cs[j] += bf16_to_f32(v);
+            float v = acc[i][j][r] + bv;
+            if (RELU) v = v > 0.f ? v : 0.f;
+            C[static_cast<int64_t>(row) * N + col] = f32_to_bf16(v);
           }
-        }
-      cs[j] += __shfl_xor(cs[j], 32, 64);  // lanes fr and fr + 32 hold the same column
-      if (fh == 0) dred[wave >> 1][wn + j * 32 + fr] = cs[j];
-    }
-    __syncthreads();
-    if (t < BN_ && n0 + t < N) part_store(part + static_cast<int64_t>(tile_m) * N + n0 + t, dred[0][t] + dred[1][t], sc1);
-    if (!handoff_last(cnt + tile_n, static_cast<unsigned>(tiles_m), sc1, &last)) return;
-    if (t < BN_ && n0 + t < N) {
-      db[n0 + t] = f32_to_bf16(part_sum(part + n0 + t, tiles_m, N, sc1));  // tile order
-    }
-    if (t == 0) __hip_atomic_store(cnt + tile_n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int col = n0 + wn + j * 32 + fr;
-    float bv = 0.f;
-    if (col < N) bv = bias32 ? bias32[col] : bias16 ? bf16_to_f32(bias16[col]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < I; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        if (row < M && col < N) {
-          float v = acc[i][j][r] + bv;
-          if (RELU) v = v > 0.f ? v : 0.f;
-          C[static_cast<int64_t>(row) * N + col] = f32_to_bf16(v);
         }
       }
     }
@@ -326,17 +383,6 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_bias_act_kernel(
 // dz = dy * (y > 0) (bf16 out), dbias[n] += sum_m dz[m, n]; 16 B along N per lane.
 // 8 bf16 <-> 8 fp32 through one 16-B register (the loads of a round are raw
 // uint4 so every one is issued before the first conversion)
-__device__ __forceinline__ void u4_to_f8(const uint4 v, float (&o)[8]) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    o[2 * i] = __uint_as_float(w[i] << 16);
-    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-__device__ __forceinline__ uint4 f8_to_u4(const float (&o)[8]) {
-  return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
-}
 
 // Row-block partial column sums go to part[blockIdx.x][N]; the last block of a
 // column block to arrive (agent-scope release + ticket; acquire in the
