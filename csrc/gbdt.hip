@@ -704,6 +704,189 @@ __global__ __launch_bounds__(256) void partition_kernel(
   }
 }
 
+// ---- one level's routing + stable partition in three launches: route_count
+// routes each tile of kTilePos positions and writes, besides the flags, the
+// tile-local inclusive scan of the flags and the tile's total; level_plan (one
+// block) scans the tile totals into tile offsets, so the global count of
+// right-goers before position x is P(x) = tile_off[tile(x - 1)] + tincl[x - 1],
+// and takes each node's right count P(hi) - P(lo) and base P(lo) from its
+// segment ends, then writes the child segments (children_kernel's outputs);
+// partition places every row as partition_kernel does, from tile_off + tincl.
+// Replaces route_flags, the two-launch device scan, partition and children.
+constexpr int kTilePos = 256 * kRouteItems;  // positions per tile (one block)
+
+__device__ __forceinline__ int block_incl_scan256(int v, int* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(x, o, 64);
+    if (lane >= o) x += u;
+  }
+  __syncthreads();  // wsum reuse across calls
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < w) x += wsum[k];
+  return x;  // inclusive; wsum[0..3] hold the wave totals (block total = their sum)
+}
+
+__global__ __launch_bounds__(256) void route_count_kernel(
+    const uint8_t* __restrict__ bins, const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos,
+    const int32_t* __restrict__ split, const int32_t* __restrict__ t_feat, const int32_t* __restrict__ t_bin,
+    int64_t rs, int64_t fs, int n, int h0, int L, int32_t* __restrict__ flag, int32_t* __restrict__ tincl,
+    int32_t* __restrict__ tile_cnt) {
+  __shared__ int wsum[4];
+  const int p0 = blockIdx.x * kTilePos + threadIdx.x;
+  int row[kRouteItems], i[kRouteItems], sp[kRouteItems], fe[kRouteItems], tb[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    row[k] = p < n ? rows[p] : 0;
+    i[k] = p < n ? node_pos[p] - h0 : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const bool in = i[k] >= 0 && i[k] < L;
+    sp[k] = in ? split[i[k]] : 0;
+    fe[k] = in ? t_feat[h0 + i[k]] : 0;
+    tb[k] = in ? t_bin[h0 + i[k]] : 0;
+  }
+  int b[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) b[k] = sp[k] ? bins[row[k] * rs + fe[k] * fs] : 0;
+  int before = 0;  // right-goers of this tile before position p0 + 256 k (k-major, then thread order)
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    const int f = (sp[k] && b[k] > tb[k]) ? 1 : 0;
+    const int incl = before + block_incl_scan256(f, wsum);
+    before += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (p < n) {
+      flag[p] = f;
+      tincl[p] = incl;
+    }
+  }
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = before;
+}
+
+// one block of 1024 threads: tile offsets (exclusive scan of tile_cnt), each
+// node's base P(lo) and right count P(hi) - P(lo), the children's segments /
+// counts / built-child choice as children_kernel
+__global__ __launch_bounds__(1024) void level_plan_kernel(
+    const int32_t* __restrict__ tile_cnt, int ntiles, int32_t* __restrict__ tile_off, const int32_t* __restrict__ tincl,
+    const int32_t* __restrict__ split, const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, int L,
+    int32_t* __restrict__ node_base, int32_t* __restrict__ node_r, int32_t* __restrict__ lo_next,
+    int32_t* __restrict__ hi_next, float* __restrict__ cnt, int pick, int32_t* __restrict__ build_child,
+    int32_t* __restrict__ blo, int32_t* __restrict__ bhi) {
+  __shared__ int wsum[16];
+  __shared__ int s_carry;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) s_carry = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < ntiles; b0 += 1024) {
+    const int j = b0 + t;
+    const int v = j < ntiles ? tile_cnt[j] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(x, o, 64);
+      if (lane >= o) x += u;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int pre = s_carry, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) pre += wsum[k];
+      tot += wsum[k];
+    }
+    if (j < ntiles) tile_off[j] = pre + x - v;
+    __syncthreads();
+    if (t == 0) s_carry += tot;
+    __syncthreads();
+  }
+  // (tile_off is read back below by other threads: the loop's last barrier orders it)
+  auto P = [&](int x) {  // right-goers in positions [0, x)
+    if (x <= 0) return 0;
+    return tile_off[(x - 1) / kTilePos] + tincl[x - 1];
+  };
+  for (int i = t; i < L; i += 1024) {
+    int a0 = 0, a1 = 0, b0 = 0, b1 = 0, base = 0, r = 0;
+    if (split[i] && hi[i] > lo[i]) {  // a node split on the global histogram may own no rows here
+      const int s0 = lo[i], s1 = hi[i];
+      base = P(s0);
+      r = P(s1) - base;
+      const int nl = (s1 - s0) - r;
+      a0 = s0;
+      a1 = s0 + nl;
+      b0 = s0 + nl;
+      b1 = s1;
+    }
+    node_base[i] = base;
+    node_r[i] = r;
+    lo_next[2 * i] = a0;
+    hi_next[2 * i] = a1;
+    lo_next[2 * i + 1] = b0;
+    hi_next[2 * i + 1] = b1;
+    cnt[2 * i] = static_cast<float>(a1 - a0);
+    cnt[2 * i + 1] = static_cast<float>(b1 - b0);
+    if (pick) {
+      const int c = (a1 - a0) <= (b1 - b0) ? 0 : 1;
+      build_child[i] = 2 * i + c;
+      blo[i] = c ? b0 : a0;
+      bhi[i] = c ? b1 : a1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void partition_tiles_kernel(
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ split,
+    const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, const int32_t* __restrict__ flag,
+    const int32_t* __restrict__ tincl, const int32_t* __restrict__ tile_off, const int32_t* __restrict__ node_base,
+    const int32_t* __restrict__ node_r, int n, int h0, int L, int32_t* __restrict__ rows_next,
+    int32_t* __restrict__ node_pos_next) {
+  const int p0 = blockIdx.x * kTilePos + threadIdx.x;
+  const int toff = tile_off[blockIdx.x];
+  int row[kRouteItems], hn[kRouteItems], fl[kRouteItems], inc[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    const bool ok = p < n;
+    row[k] = ok ? rows[p] : 0;
+    hn[k] = ok ? node_pos[p] : -1;
+    fl[k] = ok ? flag[p] : 0;
+    inc[k] = ok ? tincl[p] : 0;
+  }
+  int s0[kRouteItems], s1[kRouteItems], sp[kRouteItems], nb[kRouteItems], nr[kRouteItems];
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int i = hn[k] - h0;
+    const bool in = i >= 0 && i < L;
+    sp[k] = in ? split[i] : 0;
+    s0[k] = sp[k] ? lo[i] : 0;
+    s1[k] = sp[k] ? hi[i] : 0;
+    nb[k] = sp[k] ? node_base[i] : 0;
+    nr[k] = sp[k] ? node_r[i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kRouteItems; ++k) {
+    const int p = p0 + k * 256;
+    if (p >= n) continue;
+    if (sp[k]) {
+      const int r_in = toff + inc[k] - fl[k] - nb[k];  // right rows before p in the segment
+      const int nl = (s1[k] - s0[k]) - nr[k];
+      const int np = fl[k] ? s0[k] + nl + r_in : s0[k] + (p - s0[k] - r_in);
+      rows_next[np] = row[k];
+      node_pos_next[np] = fl[k] ? 2 * hn[k] + 2 : 2 * hn[k] + 1;
+    } else {
+      rows_next[p] = row[k];
+      node_pos_next[p] = hn[k];
+    }
+  }
+}
+
 // thread per parent i: child segments and counts; when ``pick`` (counts are
 // already global) also the built (smaller) child and its segment.
 __global__ __launch_bounds__(256) void children_kernel(
@@ -1074,6 +1257,27 @@ hipError_t gbdt_partition(const int32_t* rows, const int32_t* node_pos, const in
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(partition_kernel, dim3((n + 256 * kRouteItems - 1) / (256 * kRouteItems)), dim3(256), 0, s, rows,
                      node_pos, split, lo, hi, flag, sc, n, h0, L, rows_next, node_pos_next);
+  return hipGetLastError();
+}
+
+int gbdt_level_tiles(int n) { return (n + kTilePos - 1) / kTilePos; }
+
+hipError_t gbdt_route_partition(const uint8_t* bins, bool feature_major, int F, const int32_t* rows,
+                                const int32_t* node_pos, const int32_t* split, const int32_t* t_feat,
+                                const int32_t* t_bin, const int32_t* lo, const int32_t* hi, int n, int h0, int L,
+                                int32_t* flag, int32_t* tincl, int32_t* tile_cnt, int32_t* tile_off,
+                                int32_t* node_base, int32_t* node_r, int32_t* rows_next, int32_t* node_pos_next,
+                                int32_t* lo_next, int32_t* hi_next, float* cnt, int pick, int32_t* build_child,
+                                int32_t* blo, int32_t* bhi, hipStream_t s) {
+  if (n <= 0 || L <= 0) return hipSuccess;
+  const int nt = gbdt_level_tiles(n);
+  const int64_t rs = feature_major ? 1 : F, fs = feature_major ? n : 1;
+  hipLaunchKernelGGL(route_count_kernel, dim3(nt), dim3(256), 0, s, bins, rows, node_pos, split, t_feat, t_bin, rs, fs,
+                     n, h0, L, flag, tincl, tile_cnt);
+  hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(1024), 0, s, tile_cnt, nt, tile_off, tincl, split, lo, hi, L,
+                     node_base, node_r, lo_next, hi_next, cnt, pick, build_child, blo, bhi);
+  hipLaunchKernelGGL(partition_tiles_kernel, dim3(nt), dim3(256), 0, s, rows, node_pos, split, lo, hi, flag, tincl,
+                     tile_off, node_base, node_r, n, h0, L, rows_next, node_pos_next);
   return hipGetLastError();
 }
 

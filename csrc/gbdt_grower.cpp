@@ -88,6 +88,12 @@ class GbdtGrower {
     scan_status_ = at::zeros({std::max(1, kdl::gbdt_route_scan_tiles(N_))}, io.dtype(at::kLong));
     scan_ticket_ = at::zeros({1}, io);
     scan_fault_ = at::zeros({1}, io);
+    // the three-launch level (gbdt_route_partition): tile counts / offsets (sc_ holds the
+    // tile-local scan there), node bases and right counts
+    tile_cnt_ = at::empty({std::max(1, kdl::gbdt_level_tiles(N_))}, io);
+    tile_off_ = at::empty({std::max(1, kdl::gbdt_level_tiles(N_))}, io);
+    node_base_ = at::empty({maxL}, io);
+    node_r_ = at::empty({maxL}, io);
     for (int d = 0; d <= D_; ++d) {
       lo_.push_back(at::zeros({1LL << d}, io));
       hi_.push_back(at::zeros({1LL << d}, io));
@@ -159,6 +165,19 @@ class GbdtGrower {
                         last ? nullptr : ip(exists_[d + 1]), stream()),
        "gbdt_decide");
     if (last) return at::Tensor();
+    if (route_plan_on()) {
+      // route + per-tile / per-node counts, one-block plan (tile offsets, node bases, child
+      // segments), partition: three launches instead of route + scan (2) + partition + children
+      ck(kdl::gbdt_route_partition(bins_t_.data_ptr<uint8_t>(), true, F_, ip(rows_), ip(node_pos_), ip(split_),
+                                   ip(feat_), ip(tbin_), ip(lo_[d]), ip(hi_[d]), N_, h0, L, ip(flag_), ip(sc_),
+                                   ip(tile_cnt_), ip(tile_off_), ip(node_base_), ip(node_r_), ip(rows_next_),
+                                   ip(node_pos_next_), ip(lo_[d + 1]), ip(hi_[d + 1]), fp(cnt_), pick ? 1 : 0,
+                                   ip(build_child_), ip(blo_), ip(bhi_), stream()),
+         "gbdt_route_partition");
+      std::swap(rows_, rows_next_);
+      std::swap(node_pos_, node_pos_next_);
+      return cnt_.narrow(0, 0, 2 * L);
+    }
     if (route_scan_on()) {
       if (++scan_epoch_ >= (1u << 31)) {  // epochs wrapped: start the words over
         scan_status_.zero_();
@@ -265,12 +284,17 @@ class GbdtGrower {
   std::vector<at::Tensor> lo_, hi_, exists_;
   at::Tensor split_, gain_, sbin_, gl_, hl_, tot_, feat_, tbin_, thr_, val_;
   at::Tensor hist_cur_, hist_next_, built_, cnt_, build_child_, blo_, bhi_, chunk_off_, gh_max_;
-  at::Tensor scan_status_, scan_ticket_, scan_fault_;
+  at::Tensor scan_status_, scan_ticket_, scan_fault_, tile_cnt_, tile_off_, node_base_, node_r_;
   uint32_t scan_epoch_ = 0;
   // KDL_TUNE gbdt_route_scan (default 0): 1 = the fused route + look-back scan (one launch; measured
   // slower: 59.9 us per level against 23.0 + 14.6 for route_flags + the device scan, 941-952 vs
   // 1,053-1,064 boosting rounds/s at 2M x 28 -- the look-back's chain of cross-XCD atomic round trips
   // over 977 tiles; profiles/r06_gbdt_route_scan.txt); 0 = route_flags + a device scan
+  // KDL_TUNE gbdt_route_plan (default 1): the three-launch level (route + counts, plan, partition)
+  static bool route_plan_on() {
+    if (g_route_plan < 0) g_route_plan = kdl::tune_int("gbdt_route_plan", 1);
+    return g_route_plan != 0;
+  }
   static bool route_scan_on() {
     if (g_route_scan < 0) g_route_scan = kdl::tune_int("gbdt_route_scan", 0);
     return g_route_scan != 0;
@@ -278,9 +302,11 @@ class GbdtGrower {
 
  public:
   static int g_route_scan;
+  static int g_route_plan;
 };
 
 int GbdtGrower::g_route_scan = -1;
+int GbdtGrower::g_route_plan = -1;
 
 // (flag, inclusive scan of flag) of one level's routing, by the fused route + look-back scan
 // (``fused``) or by route_flags + a device scan: the test hook of route_scan_kernel.  ``calls``
@@ -319,6 +345,48 @@ std::vector<at::Tensor> gbdt_route_scan_test(const at::Tensor& bins, const at::T
   return {flag, sc};
 }
 
+// One level's (rows_next, node_pos_next, lo_next, hi_next, child counts) by the three-launch path
+// (``plan``) or by route_flags + scan + partition + children: the test hook of gbdt_route_partition.
+std::vector<at::Tensor> gbdt_level_test(const at::Tensor& bins, const at::Tensor& rows, const at::Tensor& node_pos,
+                                        const at::Tensor& split, const at::Tensor& t_feat, const at::Tensor& t_bin,
+                                        const at::Tensor& lo, const at::Tensor& hi, int64_t h0, int64_t L, bool plan) {
+  TORCH_CHECK(bins.is_cuda() && bins.scalar_type() == at::kByte && bins.dim() == 2 && bins.is_contiguous(),
+              "gbdt_level_test: uint8 bins [N, F]");
+  for (const at::Tensor* t : {&rows, &node_pos, &split, &t_feat, &t_bin, &lo, &hi})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous(), "gbdt_level_test: int32");
+  const int n = static_cast<int>(rows.numel()), F = static_cast<int>(bins.size(1));
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bins.device());
+  auto io = rows.options();
+  auto rn = at::empty({n}, io), pn = at::empty({n}, io), flag = at::empty({n}, io);
+  auto lon = at::zeros({2 * L}, io), hin = at::zeros({2 * L}, io), bc = at::zeros({L}, io);
+  auto blo = at::zeros({L}, io), bhi = at::zeros({L}, io);
+  auto cnt = at::zeros({2 * L}, io.dtype(at::kFloat));
+  if (plan) {
+    auto bt = bins.t().contiguous();
+    const int nt = std::max(1, kdl::gbdt_level_tiles(n));
+    auto tc = at::empty({nt}, io), to = at::empty({nt}, io), ti = at::empty({n}, io);
+    auto nb = at::empty({L}, io), nrr = at::empty({L}, io);
+    ck(kdl::gbdt_route_partition(bt.data_ptr<uint8_t>(), true, F, ip(rows), ip(node_pos), ip(split), ip(t_feat),
+                                 ip(t_bin), ip(lo), ip(hi), n, static_cast<int>(h0), static_cast<int>(L), ip(flag),
+                                 ip(ti), ip(tc), ip(to), ip(nb), ip(nrr), ip(rn), ip(pn), ip(lon), ip(hin), fp(cnt), 1,
+                                 ip(bc), ip(blo), ip(bhi), stream()),
+       "gbdt_route_partition");
+  } else {
+    auto sc = at::empty({n}, io);
+    ck(kdl::gbdt_route_flags(bins.data_ptr<uint8_t>(), ip(rows), ip(node_pos), ip(split), ip(t_feat), ip(t_bin), F, n,
+                             static_cast<int>(h0), static_cast<int>(L), ip(flag), stream()),
+       "gbdt_route_flags");
+    at::cumsum_out(sc, flag, 0, at::kInt);
+    ck(kdl::gbdt_partition(ip(rows), ip(node_pos), ip(split), ip(lo), ip(hi), ip(flag), ip(sc), n,
+                           static_cast<int>(h0), static_cast<int>(L), ip(rn), ip(pn), stream()),
+       "gbdt_partition");
+    ck(kdl::gbdt_children(ip(split), ip(lo), ip(hi), ip(sc), static_cast<int>(L), ip(lon), ip(hin), fp(cnt), 1,
+                          ip(bc), ip(blo), ip(bhi), stream()),
+       "gbdt_children");
+  }
+  return {rn, pn, lon, hin, cnt, bc, blo, bhi};
+}
+
 at::Tensor gbdt_quantise(const at::Tensor& X, const at::Tensor& cuts, int64_t num_bins) {
   TORCH_CHECK(X.is_cuda() && X.dim() == 2, "gbdt_quantise: X [N, F] on the GPU");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
@@ -354,9 +422,13 @@ void register_gbdt(pybind11::module& m) {
       .def("stats", &GbdtGrower::stats)
       .def("rows_per_chunk", &GbdtGrower::rows_per_chunk)
       .def("scan_faults", &GbdtGrower::scan_faults)
+      .def_static("set_route_plan", [](int v) { GbdtGrower::g_route_plan = v; },
+                  "1: the three-launch level (route + counts, plan, partition), 0: route / scan / partition / "
+                  "children, -1: KDL_TUNE gbdt_route_plan")
       .def_static("set_route_scan", [](int v) { GbdtGrower::g_route_scan = v; },
                   "1: fused route + look-back scan, 0: route_flags + device scan, -1: KDL_TUNE gbdt_route_scan");
   m.def("gbdt_quantise", &gbdt_quantise, "GBDT feature quantisation (bins = #cuts < x, clamped)");
+  m.def("gbdt_level_test", &gbdt_level_test, "one level's partition + child segments: three-launch plan or scan path");
   m.def("gbdt_route_scan_test", &gbdt_route_scan_test, "(flag, inclusive scan) of a level's routing: fused or two-pass",
         py::arg("bins"), py::arg("rows"), py::arg("node_pos"), py::arg("split"), py::arg("t_feat"), py::arg("t_bin"),
         py::arg("h0"), py::arg("L"), py::arg("fused"), py::arg("calls") = 1, py::arg("feature_major") = false);

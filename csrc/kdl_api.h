@@ -194,6 +194,18 @@ hipError_t gbdt_route_scan(const uint8_t* bins, const int32_t* rows, const int32
 hipError_t gbdt_partition(const int32_t* rows, const int32_t* node_pos, const int32_t* split, const int32_t* lo,
                           const int32_t* hi, const int32_t* flag, const int32_t* sc, int n, int h0, int L,
                           int32_t* rows_next, int32_t* node_pos_next, hipStream_t s);
+// a level's routing + stable partition + child segments in three launches (route_count_kernel,
+// level_plan_kernel, partition_tiles_kernel): the outputs of route_flags + scan + partition +
+// children.  tincl: n ints (the tile-local scan); tile_cnt / tile_off: gbdt_level_tiles(n) ints;
+// node_base / node_r: L ints
+int gbdt_level_tiles(int n);
+hipError_t gbdt_route_partition(const uint8_t* bins, bool feature_major, int F, const int32_t* rows,
+                                const int32_t* node_pos, const int32_t* split, const int32_t* t_feat,
+                                const int32_t* t_bin, const int32_t* lo, const int32_t* hi, int n, int h0, int L,
+                                int32_t* flag, int32_t* tincl, int32_t* tile_cnt, int32_t* tile_off,
+                                int32_t* node_base, int32_t* node_r, int32_t* rows_next, int32_t* node_pos_next,
+                                int32_t* lo_next, int32_t* hi_next, float* cnt, int pick, int32_t* build_child,
+                                int32_t* blo, int32_t* bhi, hipStream_t s);
 hipError_t gbdt_children(const int32_t* split, const int32_t* lo, const int32_t* hi, const int32_t* sc, int L,
                          int32_t* lo_next, int32_t* hi_next, float* cnt, int pick, int32_t* build_child,
                          int32_t* blo, int32_t* bhi, hipStream_t s);

@@ -285,6 +285,41 @@ def test_gpu_fused_route_scan_matches_two_pass(n, L):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,L", [(2_000_000, 32), (1024 * 37 + 5, 8), (300_000, 1), (1000, 4), (1024 * 130, 64)])
+def test_gpu_three_launch_level_matches_scan_path(n, L):
+    """The three-launch level (route + tile / node counts, one-block plan, per-tile
+    rescan + partition) moves every row to the scan path's position and writes the
+    same child segments / counts / built-child choice, bit for bit -- segments in
+    heap order with positions of non-split nodes and of a shallower leaf between
+    them, nodes owning no rows, a ragged last tile."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    g = torch.Generator().manual_seed(n % 997 + L)
+    F, h0 = 28, L - 1
+    bins = torch.randint(0, 256, (n, F), generator=g, dtype=torch.uint8)
+    rows = torch.randperm(n, generator=g).int()
+    # level segments in heap order, a shallower leaf's rows in front of them
+    lead = n // 7
+    cuts = torch.sort(torch.randint(lead, n + 1, (L - 1,), generator=g)).values
+    bounds = torch.cat([torch.tensor([lead]), cuts, torch.tensor([n])])
+    if L > 2:
+        bounds[2] = bounds[1]  # node 1 owns no rows
+    lo, hi = bounds[:-1].int(), bounds[1:].int()
+    node_pos = torch.full((n,), max(h0 - 1, 0) if h0 > 0 else -5, dtype=torch.int32)
+    for i in range(L):
+        node_pos[lo[i]:hi[i]] = h0 + i
+    split = (torch.rand(L, generator=g) < 0.8).int()
+    heap = 2 * (h0 + L) + 3
+    t_feat = torch.randint(0, F, (heap,), generator=g).int()
+    t_bin = torch.randint(0, 255, (heap,), generator=g).int()
+    args = [t.cuda() for t in (bins, rows, node_pos, split, t_feat, t_bin, lo, hi)]
+    ref = ext.gbdt_level_test(*args, h0, L, False)
+    got = ext.gbdt_level_test(*args, h0, L, True)
+    for a, b, name in zip(got, ref, ("rows", "node_pos", "lo", "hi", "cnt", "build_child", "blo", "bhi")):
+        assert torch.equal(a, b), name
+
+
+@pytest.mark.gpu
 def test_gpu_fused_route_scan_fit_agrees():
     """A whole fit with the fused route + scan grows the two-pass fit's trees (up to
     near-ties of the fp32 flush order) and raises no look-back fault."""
