@@ -303,14 +303,19 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_wq_kernel(
 // per level (nb <= kPlanMax).
 constexpr int kPlanMax = 1024;
 
-template <int U, int NW>
+// P64: g and h packed into one 64-bit LDS add (ds_add_u64): g's fixed-point
+// value in the high word (two's complement, |block sum| < 2^31), h's in the low
+// word (non-negative, block sum <= 2^30: no carry into g) -- half the LDS atomics
+template <int U, int NW, bool P64 = false>
 __global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
     const uint8_t* __restrict__ bins, const float* __restrict__ grad, const float* __restrict__ hess,
     int64_t gh_stride, const int32_t* __restrict__ rows, const int32_t* __restrict__ blo,
     const int32_t* __restrict__ bhi, int nb, int F, int B, int rpb, int fp,
     const float* __restrict__ gh_max, float* __restrict__ hist, int flush) {
-  extern __shared__ int qlds[];
-  __shared__ int s_off[kPlanMax + 1];
+  // 16-B aligned: the dynamic planes start after the static s_off, and P64's
+  // 8-byte LDS atomics fault on a 4-byte-aligned address
+  extern __shared__ __attribute__((aligned(16))) int qlds[];
+  __shared__ __attribute__((aligned(16))) int s_off[kPlanMax + 4];
   const int t = threadIdx.x;
   if (t < 64) {  // wave 0: inclusive wave scans, 64 nodes at a time
     int carry = 0;
@@ -378,8 +383,14 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e = (4 * k + q) * B + ((w[u][k] >> (8 * q)) & 255u);
-          atomicAdd(qlds + e, qg[u]);
-          atomicAdd(qh_pl + e, qh[u]);
+          if constexpr (P64) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(qlds) + e,
+                      (static_cast<unsigned long long>(static_cast<uint32_t>(qg[u])) << 32) |
+                          static_cast<uint32_t>(qh[u]));
+          } else {
+            atomicAdd(qlds + e, qg[u]);
+            atomicAdd(qh_pl + e, qh[u]);
+          }
         }
       }
     }
@@ -392,7 +403,15 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
   float* out = hist + (static_cast<int64_t>(j) * F + f0) * B * 2;
   const float ig = sg > 0.f ? 1.f / sg : 0.f, ih = sh > 0.f ? 1.f / sh : 0.f;
   for (int i = t; i < nf * B; i += kHistBlock) {
-    const int vg = qlds[i], vh = qh_pl[i];
+    int vg, vh;
+    if constexpr (P64) {
+      const unsigned long long v = reinterpret_cast<const unsigned long long*>(qlds)[i];
+      vg = static_cast<int>(static_cast<uint32_t>(v >> 32));
+      vh = static_cast<int>(static_cast<uint32_t>(v));
+    } else {
+      vg = qlds[i];
+      vh = qh_pl[i];
+    }
     if (vg != 0) __hip_atomic_fetch_add(out + 2 * i, static_cast<float>(vg) * ig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (vh != 0) __hip_atomic_fetch_add(out + 2 * i + 1, static_cast<float>(vh) * ih, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1141,11 +1160,11 @@ static hipError_t hist_lds_attr() {
   return hipSuccess;
 }
 
-template <int U, int NW>
+template <int U, int NW, bool P64>
 static hipError_t rows_lds_attr() {
   static bool attr_set = false;
   if (!attr_set) {
-    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_rows_kernel<U, NW>),
+    RETURN_IF_HIP_ERR(hipFuncSetAttribute(reinterpret_cast<const void*>(hist_build_rows_kernel<U, NW, P64>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                           static_cast<int>(kFTile * 256 * 2 * sizeof(int))));
     attr_set = true;
@@ -1189,20 +1208,25 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
   if (rows_u > 0 && F % 4 == 0 && fp >= 4 && nb <= kPlanMax) {
     const int nf0 = F < fp ? F : fp;  // the first (largest) tile's planes
     const size_t lds_r = static_cast<size_t>(nf0) * B * 2 * sizeof(int);
-#define HIST_ROWS_LAUNCH(U, NW)                                                                                        \
-  RETURN_IF_HIP_ERR((rows_lds_attr<U, NW>()));                                                                        \
-  hipLaunchKernelGGL((hist_build_rows_kernel<U, NW>), grid, dim3(kHistBlock), lds_r, s, bins, grad, hess, gh_stride, \
-                     rows, blo, bhi, nb, F, B, rpb, fp, gh_max, hist, noflush ? 0 : 1)
-#define HIST_ROWS_BY_U(U)                  \
-  switch (fp / 4) {                         \
-    case 1: HIST_ROWS_LAUNCH(U, 1); break;     \
-    case 2: HIST_ROWS_LAUNCH(U, 2); break;     \
-    case 4: HIST_ROWS_LAUNCH(U, 4); break;     \
-    case 8: HIST_ROWS_LAUNCH(U, 8); break;     \
-    default: HIST_ROWS_LAUNCH(U, 16); break;   \
+#define HIST_ROWS_LAUNCH(U, NW, P)                                                                                     \
+  RETURN_IF_HIP_ERR((rows_lds_attr<U, NW, P>()));                                                                     \
+  hipLaunchKernelGGL((hist_build_rows_kernel<U, NW, P>), grid, dim3(kHistBlock), lds_r, s, bins, grad, hess,         \
+                     gh_stride, rows, blo, bhi, nb, F, B, rpb, fp, gh_max, hist, noflush ? 0 : 1)
+#define HIST_ROWS_BY_U(U, P)                  \
+  switch (fp / 4) {                            \
+    case 1: HIST_ROWS_LAUNCH(U, 1, P); break;     \
+    case 2: HIST_ROWS_LAUNCH(U, 2, P); break;     \
+    case 4: HIST_ROWS_LAUNCH(U, 4, P); break;     \
+    case 8: HIST_ROWS_LAUNCH(U, 8, P); break;     \
+    default: HIST_ROWS_LAUNCH(U, 16, P); break;   \
   }
-    if (rows_u >= 8) { HIST_ROWS_BY_U(8) }
-    else { HIST_ROWS_BY_U(4) }
+    // g and h in one 64-bit LDS add (4 rows in flight; the hessians of every objective here
+    // are >= 0, as P64 needs): 1,500-1,501 -> 1,564-1,568 boosting rounds/s at 2M x 28
+    // (profiles/r06_gbdt_pack64.txt); KDL_TUNE gbdt_pack64=0: two 32-bit adds
+    static const bool pack64 = tune_int("gbdt_pack64", 1) != 0;
+    if (pack64) { HIST_ROWS_BY_U(4, true) }
+    else if (rows_u >= 8) { HIST_ROWS_BY_U(8, false) }
+    else { HIST_ROWS_BY_U(4, false) }
 #undef HIST_ROWS_BY_U
 #undef HIST_ROWS_LAUNCH
     return hipGetLastError();
