@@ -1220,11 +1220,12 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
     case 8: HIST_ROWS_LAUNCH(U, 8, P); break;     \
     default: HIST_ROWS_LAUNCH(U, 16, P); break;   \
   }
-    // g and h in one 64-bit LDS add (4 rows in flight; the hessians of every objective here
+    // g and h in one 64-bit LDS add (the hessians of every objective here
     // are >= 0, as P64 needs): 1,500-1,501 -> 1,564-1,568 boosting rounds/s at 2M x 28
     // (profiles/r06_gbdt_pack64.txt); KDL_TUNE gbdt_pack64=0: two 32-bit adds
     static const bool pack64 = tune_int("gbdt_pack64", 1) != 0;
-    if (pack64) { HIST_ROWS_BY_U(4, true) }
+    if (pack64 && rows_u >= 8) { HIST_ROWS_BY_U(8, true) }
+    else if (pack64) { HIST_ROWS_BY_U(4, true) }
     else if (rows_u >= 8) { HIST_ROWS_BY_U(8, false) }
     else { HIST_ROWS_BY_U(4, false) }
 #undef HIST_ROWS_BY_U
