@@ -75,7 +75,10 @@ __device__ __forceinline__ float ordered_sum(const float* __restrict__ part, int
 // a freshly stored output tile (MI355X_MICROARCH.md).  sc1 = 1: partials stored
 // and read with agent-scope relaxed atomics (global_store / global_load sc1:
 // written through, read past L1), the ticket add after every storing wave's
-// vmcnt(0) and a barrier, no fence (the hand-off table's row 1).
+// vmcnt(0) and a barrier, no fence (the hand-off table's row 1; that row was
+// measured at one workgroup per CU, these kernels run two or more: the CTR GPU
+// tests -- bitwise / fp32-truth checks of every reduction, repeated launches --
+// pass under it, and KDL_TUNE ctr_handoff=0 restores the fenced form).
 __device__ __forceinline__ void part_store(float* p, float v, int sc1) {
   if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;

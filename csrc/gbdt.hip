@@ -384,9 +384,11 @@ __global__ __launch_bounds__(kHistBlock) void hist_build_rows_kernel(
         for (int q = 0; q < 4; ++q) {
           const int e = (4 * k + q) * B + ((w[u][k] >> (8 * q)) & 255u);
           if constexpr (P64) {
+            // (a negative hessian -- no objective here produces one -- is clamped to 0
+            // rather than borrowing from g's word)
             atomicAdd(reinterpret_cast<unsigned long long*>(qlds) + e,
                       (static_cast<unsigned long long>(static_cast<uint32_t>(qg[u])) << 32) |
-                          static_cast<uint32_t>(qh[u]));
+                          static_cast<uint32_t>(qh[u] > 0 ? qh[u] : 0));
           } else {
             atomicAdd(qlds + e, qg[u]);
             atomicAdd(qh_pl + e, qh[u]);
