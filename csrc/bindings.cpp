@@ -1795,6 +1795,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("ctr_tile_for", &kdl::ctr_tile_for, "the gemm_bias_act tile picked for an M x N output");
   m.def("set_ctr_igemm", &kdl::set_ctr_igemm, "forward gemm_bias_act on igemm: mode 0 off / 1 by tile count / 2 always; cfg -1 by shape",
         py::arg("mode"), py::arg("cfg") = -1);
+  m.def("set_ctr_handoff", &kdl::set_ctr_handoff,
+        "split-reduction hand-off: 1 = sc1 partials without fences, 0 = fenced, -1 = the KDL_TUNE value");
   m.def("ctr_igemm_cfg_for", &kdl::ctr_igemm_cfg_for, "igemm cfg serving a forward M x N x K gemm_bias_act (-1: none)");
   m.def("gemm_dgrad_relu", &gemm_dgrad_relu, "(dz W) * [y > 0] and its column sums (bf16): data gradient through a ReLU + bias gradient, one launch");
   m.def("relu_bwd_dbias", &relu_bwd_dbias, "ReLU backward (mask from output) + bias gradient (deterministic; bf16 or fp32)",

@@ -1017,10 +1017,12 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
 // the split reductions' hand-off (handoff_last): KDL_TUNE ctr_handoff 1 (default) = sc1
 // partials, no fences; 0 = release / acquire fences.  CTR step 11.34-11.38 -> 11.43-11.47 M
 // samples/s, and with the fused ReLU backward 11.54-11.58 (profiles/r06_ctr_handoff.txt)
+static int g_handoff = -1;  // -1: the KDL_TUNE value (read once); set_ctr_handoff overrides
 static int handoff_sc1() {
-  static const int v = tune_int("ctr_handoff", 1) != 0 ? 1 : 0;
-  return v;
+  if (g_handoff < 0) g_handoff = tune_int("ctr_handoff", 1) != 0 ? 1 : 0;
+  return g_handoff;
 }
+void set_ctr_handoff(int sc1) { g_handoff = sc1 < 0 ? -1 : (sc1 != 0 ? 1 : 0); }
 
 int head_bce_fwd_blocks(int M) { return (M + 4 * kHeadRowsPerWave - 1) / (4 * kHeadRowsPerWave); }
 

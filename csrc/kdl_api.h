@@ -228,6 +228,8 @@ int ctr_tile_for(int M, int N);
 // forward gemm_bias_act on the LDS-DMA igemm loop: 0 off, 1 by tile count, 2 every
 // K % 64 / N % 64 shape; cfg -1 by shape (igemm tile configs 0-4)
 void set_ctr_igemm(int mode, int cfg);
+// the split reductions' hand-off: 1 = sc1 partials, no fences; 0 = fenced; -1 = KDL_TUNE ctr_handoff
+void set_ctr_handoff(int sc1);
 int ctr_igemm_cfg_for(int M, int N, int K);  // -1: the register-staged kernel
 // part: relu_bwd_dbias_parts(M, N) x [N] fp32 scratch; cnt: (N + 255) / 256 counters,
 // zero before the first call (the kernel re-arms them); db: [N] bf16 (db_bf16) or fp32

@@ -1094,6 +1094,38 @@ def test_head_bwd_relu_mask_matches_unfused():
 
 
 @pytest.mark.gpu
+def test_split_reduction_handoff_modes_agree_bitwise():
+    """The fenced hand-off (KDL_TUNE ctr_handoff=0, the fallback) and the default
+    sc1 hand-off sum the same partials in the same order: every split-reduction
+    launch gives the same bits under both, over repeated launches."""
+    from kubedl_amd.ops import _ext
+    ext = _ext.load()
+    torch.manual_seed(5)
+    M, K, N = 4096, 512, 1024
+    dz = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(K, N, device="cuda") / K ** 0.5).bfloat16()
+    y = torch.randn(M, N, device="cuda").relu().bfloat16()
+    x = torch.randn(M, 256, device="cuda").relu().bfloat16()
+    hw = (torch.randn(256, device="cuda") / 16).bfloat16()
+    dlogit = torch.randn(M, device="cuda")
+    one = torch.ones(1, device="cuda")
+    runs = {}
+    try:
+        for sc1 in (1, 0, 1, 0):
+            ext.set_ctr_handoff(sc1)
+            c, db = ext.gemm_dgrad_relu(dz, w, y)
+            r, dbr = ext.relu_bwd_dbias(c, y, True)
+            h = ext.head_bce_bwd(x, hw, dlogit, 1.0 / M, one, True)
+            got = [c, db, r, dbr] + list(h)
+            if sc1 in runs:
+                assert all(torch.equal(a, b) for a, b in zip(runs[sc1], got)), sc1
+            runs[sc1] = got
+    finally:
+        ext.set_ctr_handoff(-1)
+    assert all(torch.equal(a, b) for a, b in zip(runs[0], runs[1]))
+
+
+@pytest.mark.gpu
 def test_ctr_fixed_exchange_world1_rehearsal_bit_exact():
     """The world-1 rehearsal of the PS + worker exchange (force_fixed, one owner,
     RCCL all-to-alls on a 1-rank group) trains to the same table, Adagrad state
