@@ -1786,6 +1786,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gbdt_grad_hess", &gbdt_grad_hess, "boosting round gradient + hessian in one launch (0 reg, 1 logistic, 2 softmax)");
   m.def("gbdt_hist", &gbdt_hist, "GBDT per-node gradient/hessian histograms (LDS atomics)");
   m.def("gbdt_hist_quant", &gbdt_hist_quant, "the device grower's quantised (fixed-point) histograms (test hook)");
+  m.def("set_gbdt_pack64", &kdl::set_gbdt_pack64, "row-per-lane hist: 1 packed 64-bit LDS add, 0 two 32-bit adds, -1 KDL_TUNE");
   m.def("set_gbdt_hist_rows", &kdl::set_gbdt_hist_rows, "quantised hist kernel: 0 slot, 4 / 8 row-per-lane (rows in flight), -2 KDL_TUNE");
   m.def("gbdt_split", &gbdt_split, "GBDT best split per (node, feature)");
   m.def("gbdt_route", &gbdt_route, "GBDT row routing (1 = right child)");

@@ -1189,6 +1189,8 @@ hipError_t gbdt_gh_absmax(const float* grad, const float* hess, int n, float* ou
 
 static int g_hist_rows = -2;  // -2: KDL_TUNE gbdt_hist_rows
 void set_gbdt_hist_rows(int u) { g_hist_rows = u; }
+static int g_pack64 = -1;  // -1: KDL_TUNE gbdt_pack64
+void set_gbdt_pack64(int p) { g_pack64 = p < 0 ? -1 : (p != 0 ? 1 : 0); }
 
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
@@ -1225,7 +1227,8 @@ hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hes
     // g and h in one 64-bit LDS add (the hessians of every objective here
     // are >= 0, as P64 needs): 1,500-1,501 -> 1,564-1,568 boosting rounds/s at 2M x 28
     // (profiles/r06_gbdt_pack64.txt); KDL_TUNE gbdt_pack64=0: two 32-bit adds
-    static const bool pack64 = tune_int("gbdt_pack64", 1) != 0;
+    if (g_pack64 < 0) g_pack64 = tune_int("gbdt_pack64", 1) != 0 ? 1 : 0;
+    const bool pack64 = g_pack64 != 0;
     if (pack64 && rows_u >= 8) { HIST_ROWS_BY_U(8, true) }
     else if (pack64) { HIST_ROWS_BY_U(4, true) }
     else if (rows_u >= 8) { HIST_ROWS_BY_U(8, false) }

@@ -170,6 +170,8 @@ hipError_t gbdt_heap_pack(const int32_t* feat, const int32_t* tbin, const float*
 // quantised histogram build: 0 = slot kernel (a wave = 64 / fp rows x fp features), 4 | 8 = row-per-lane
 // kernel with that many rows in flight per lane (F % 4 == 0); -2 = KDL_TUNE gbdt_hist_rows
 void set_gbdt_hist_rows(int u);
+// row-per-lane build: 1 = g and h in one 64-bit LDS add, 0 = two 32-bit adds, -1 = KDL_TUNE gbdt_pack64
+void set_gbdt_pack64(int p);
 hipError_t gbdt_hist_wq(const uint8_t* bins, const float* grad, const float* hess, int64_t gh_stride,
                         const int32_t* rows, const int32_t* blo, const int32_t* bhi, int32_t* chunk_off, int nb,
                         int max_chunks, int rpb, int F, int B, const float* gh_max, float* hist, hipStream_t s);

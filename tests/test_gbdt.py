@@ -345,7 +345,8 @@ def test_gpu_fused_route_scan_fit_agrees():
 def test_gpu_row_per_lane_hist_equals_slot_kernel(F):
     """The row-per-lane build (dword bin loads, g / h quantised once per row)
     sums the same fixed-point integers per block as the slot kernel: equal up to
-    the order of the fp32 flush atomics.  F = 7 (not a multiple of 4) runs the
+    the order of the fp32 flush atomics, with g and h in one packed 64-bit LDS
+    add or two 32-bit ones.  F = 7 (not a multiple of 4) runs the
     slot kernel in both; F = 100 has a 36-feature second tile; F = 64 a 128 KiB
     LDS tile."""
     from kubedl_amd.ops import _ext
@@ -364,10 +365,13 @@ def test_gpu_row_per_lane_hist_equals_slot_kernel(F):
         slot = ext.gbdt_hist_quant(*args).cpu()
         outs = []
         for u in (4, 8):
-            ext.set_gbdt_hist_rows(u)
-            outs.append(ext.gbdt_hist_quant(*args).cpu())
+            for pack in (1, 0):  # g and h in one 64-bit LDS add (default) / two 32-bit adds
+                ext.set_gbdt_hist_rows(u)
+                ext.set_gbdt_pack64(pack)
+                outs.append(ext.gbdt_hist_quant(*args).cpu())
     finally:
         ext.set_gbdt_hist_rows(-2)
+        ext.set_gbdt_pack64(-1)
     for got in outs:
         torch.testing.assert_close(got, slot, rtol=1e-5, atol=1e-5)
     # and both are the histogram: counts of the hot bin
