@@ -934,9 +934,14 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
                                                            unsigned* __restrict__ cnt, bf16_t* __restrict__ dw,
                                                            bf16_t* __restrict__ db, float* __restrict__ dbx_part,
                                                            bf16_t* __restrict__ dbx, int sc1) {
-  __shared__ float red[8][257];
-  __shared__ float redx[MASK ? 8 : 1][MASK ? 256 : 1];
+  // per-row-lane partials, column c at hidx(c): a lane's 8 columns leave as two
+  // 16-B writes into contiguous runs (the half-columns 4..7 a 32-bank offset away),
+  // where 8 scalar writes at a 32-B lane stride conflicted 8 ways; [288] = g sum
+  constexpr int kRS = 292;
+  __shared__ __attribute__((aligned(16))) float red[8][kRS];
+  __shared__ __attribute__((aligned(16))) float redx[MASK ? 8 : 1][MASK ? kRS : 4];
   __shared__ int last;
+  auto hidx = [](int c) { return ((c & 7) >> 2) * 160 + (c >> 3) * 4 + (c & 3); };
   if (gscale != nullptr) scale *= gscale[0];  // upstream gradient of the loss, read on the device
   const int rl = threadIdx.x >> 5, cg = threadIdx.x & 31;
   const int m0 = blockIdx.x * rpb;
@@ -949,50 +954,67 @@ __global__ __launch_bounds__(256) void head_bce_bwd_kernel(const bf16_t* __restr
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s[i] = 0.f; sx[i] = 0.f; }
     if (on) Vec<bf16_t, 8>::load(w + k, wv8);
-    for (int m = m0 + rl; m < m1; m += 8) {
-      const float g = dlogit[m] * scale;
-      if (kb == 0 && cg == 0) gsum += g;
-      if (!on) continue;
-      float xv[8], d[8];
-      const int64_t o = static_cast<int64_t>(m) * K + k;
-      Vec<bf16_t, 8>::load(x + o, xv);
+    // RB of the thread's rows (stride 8) per batch, every row's dlogit and x loads
+    // issued before the first use: one memory latency per batch, not one per row
+    // (a 64-row block is one batch; the row-serial loop took 16 us for 4096 x 256)
+    constexpr int RB = 8;
+    for (int mb = m0 + rl; mb < m1; mb += 8 * RB) {
+      float gr[RB];
+      uint4 xr[RB];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        s[i] += g * xv[i];
-        d[i] = g * wv8[i];
-        if constexpr (MASK) {
-          d[i] = xv[i] > 0.f ? bf16_to_f32(f32_to_bf16(d[i])) : 0.f;  // the stored (rounded) value
-          sx[i] += d[i];
-        }
+      for (int r = 0; r < RB; ++r) {
+        const int m = mb + 8 * r;
+        const bool ok = m < m1;
+        gr[r] = ok ? dlogit[m] : 0.f;
+        xr[r] = (ok && on) ? *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(m) * K + k) : make_uint4(0, 0, 0, 0);
       }
-      Vec<bf16_t, 8>::store(dx + o, d);
-    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[rl][cg * 8 + i] = s[i];
+      for (int r = 0; r < RB; ++r) {
+        const int m = mb + 8 * r;
+        if (m >= m1) break;  // (rows ascend: the rest of the batch is past the block)
+        const float g = gr[r] * scale;
+        if (kb == 0 && cg == 0) gsum += g;
+        if (!on) continue;
+        float xv[8], d[8];
+        u4_to_f8(xr[r], xv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s[i] += g * xv[i];
+          d[i] = g * wv8[i];
+          if constexpr (MASK) {
+            d[i] = xv[i] > 0.f ? bf16_to_f32(f32_to_bf16(d[i])) : 0.f;  // the stored (rounded) value
+            sx[i] += d[i];
+          }
+        }
+        Vec<bf16_t, 8>::store(dx + static_cast<int64_t>(m) * K + k, d);
+      }
+    }
+    *reinterpret_cast<float4*>(&red[rl][cg * 4]) = make_float4(s[0], s[1], s[2], s[3]);
+    *reinterpret_cast<float4*>(&red[rl][160 + cg * 4]) = make_float4(s[4], s[5], s[6], s[7]);
     if constexpr (MASK) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) redx[rl][cg * 8 + i] = sx[i];
+      *reinterpret_cast<float4*>(&redx[rl][cg * 4]) = make_float4(sx[0], sx[1], sx[2], sx[3]);
+      *reinterpret_cast<float4*>(&redx[rl][160 + cg * 4]) = make_float4(sx[4], sx[5], sx[6], sx[7]);
     }
-    if (kb == 0 && cg == 0) red[rl][256] = gsum;
+    if (kb == 0 && cg == 0) red[rl][288] = gsum;
     __syncthreads();
     // fixed-order sum over the 8 row lanes
     const int c = threadIdx.x;  // 0..255 -> column kb + c
     if (kb + c < K) {
       float t = 0.f;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) t += red[r][c];
+      for (int r = 0; r < 8; ++r) t += red[r][hidx(c)];
       part_store(dw_part + static_cast<int64_t>(blockIdx.x) * K + kb + c, t, sc1);
       if constexpr (MASK) {
         float tx = 0.f;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) tx += redx[r][c];
+        for (int r = 0; r < 8; ++r) tx += redx[r][hidx(c)];
         part_store(dbx_part + static_cast<int64_t>(blockIdx.x) * K + kb + c, tx, sc1);
       }
     }
     if (kb == 0 && threadIdx.x == 0) {
       float t = 0.f;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) t += red[r][256];
+      for (int r = 0; r < 8; ++r) t += red[r][288];
       part_store(db_part + blockIdx.x, t, sc1);
     }
     __syncthreads();
