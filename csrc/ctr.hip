@@ -844,7 +844,7 @@ __global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restr
                                                            const float* __restrict__ y, int M, int K,
                                                            float* __restrict__ logit, float* __restrict__ dlogit,
                                                            float* __restrict__ loss_part, unsigned* __restrict__ cnt,
-                                                           float* __restrict__ loss) {
+                                                           float* __restrict__ loss, int sc1) {
   constexpr int R = kHeadRowsPerWave;
   __shared__ float wave_loss[4];
   __shared__ int last;
@@ -891,22 +891,15 @@ __global__ __launch_bounds__(256) void head_bce_fwd_kernel(const bf16_t* __restr
   }
   if (lane == 0) wave_loss[wv] = l;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    loss_part[blockIdx.x] = (wave_loss[0] + wave_loss[1]) + (wave_loss[2] + wave_loss[3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
+  // the hand-off of the block sums (handoff_last: with sc1 no release fence, which
+  // wrote back the L2 lines the logit / dlogit stores had just dirtied)
+  if (threadIdx.x == 0)
+    part_store(loss_part + blockIdx.x, (wave_loss[0] + wave_loss[1]) + (wave_loss[2] + wave_loss[3]), sc1);
+  if (!handoff_last(cnt, gridDim.x, sc1, &last)) return;
   // fixed order: 256 strided partial sums, then the 4 waves' in LDS order
   float a = 0.f;
-  for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += 256) a += loss_part[i];
+  for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += 256)
+    a += sc1 ? __hip_atomic_load(loss_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : loss_part[i];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
   if (lane == 0) wave_loss[wv] = a;
@@ -1053,7 +1046,8 @@ hipError_t head_bce_fwd(const void* x, const void* w, const void* b, bool b_bf16
   if (M <= 0) return hipSuccess;
   hipLaunchKernelGGL(head_bce_fwd_kernel, dim3(head_bce_fwd_blocks(M)), dim3(256), 0, s, static_cast<const bf16_t*>(x),
                      static_cast<const bf16_t*>(w), b_bf16 ? nullptr : static_cast<const float*>(b),
-                     b_bf16 ? static_cast<const bf16_t*>(b) : nullptr, y, M, K, logit, dlogit, loss_part, cnt, loss);
+                     b_bf16 ? static_cast<const bf16_t*>(b) : nullptr, y, M, K, logit, dlogit, loss_part, cnt, loss,
+                     handoff_sc1());
   return hipGetLastError();
 }
 

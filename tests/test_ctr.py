@@ -1109,6 +1109,8 @@ def test_split_reduction_handoff_modes_agree_bitwise():
     hw = (torch.randn(256, device="cuda") / 16).bfloat16()
     dlogit = torch.randn(M, device="cuda")
     one = torch.ones(1, device="cuda")
+    hb = torch.randn(1, device="cuda")
+    yl = torch.randint(0, 2, (M,), device="cuda").float()
     runs = {}
     try:
         for sc1 in (1, 0, 1, 0):
@@ -1116,7 +1118,8 @@ def test_split_reduction_handoff_modes_agree_bitwise():
             c, db = ext.gemm_dgrad_relu(dz, w, y)
             r, dbr = ext.relu_bwd_dbias(c, y, True)
             h = ext.head_bce_bwd(x, hw, dlogit, 1.0 / M, one, True)
-            got = [c, db, r, dbr] + list(h)
+            f = ext.head_bce_fwd(x, hw, hb, yl)
+            got = [c, db, r, dbr] + list(h) + list(f)
             if sc1 in runs:
                 assert all(torch.equal(a, b) for a, b in zip(runs[sc1], got)), sc1
             runs[sc1] = got
