@@ -10,7 +10,7 @@ tail -1 gpurun_out/r06/ctr_head_tests.log
 rm -rf gpurun_out/r06/ctr_head_prof
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r06/ctr_head_prof -o run -- python3 -m kubedl_amd.workers.xdl_ctr --steps 200 --warmup 20 > gpurun_out/r06/ctr_head_prof.log 2>&1 || { tail -5 gpurun_out/r06/ctr_head_prof.log; exit 1; }
 f=$(find gpurun_out/r06/ctr_head_prof -name '*kernel_stats.csv' | head -1)
-grep -i "head_bce" "$f" | cut -c1-200
+grep -i -E "head_bce|segment_reduce" "$f" | cut -c1-200
 for i in 1 2; do
   for ex in auto fixed; do
     [ $ex = fixed ] && [ $i = 2 ] && continue
