@@ -7,8 +7,8 @@
 //   igemm_rounds, igemm_cfg, igemm_price (timing only: 1 drops A's loads, 2 B's),
 //   wgrad_big, wgrad_blocks, wgrad_red_blocks, price_wgrad_reduce (timing only: 0 skips),
 //   halo, halo_pro, halo_wg_blocks, bn_min_rows, igemm_n256, gbdt_rpb, gbdt_unroll, gbdt_ftile,
-//   gbdt_hist_rows, gbdt_route_scan, gbdt_route_plan, gbdt_price_noflush (timing only), ctr_tile (CTR GEMM tile, -1 by
-//   shape), ctr_igemm, ctr_igemm_cfg, ctr_handoff (docs/startup_flags.md).
+//   gbdt_hist_rows, gbdt_route_scan, gbdt_route_plan, gbdt_pack64, gbdt_price_noflush (timing only), gram_blocks,
+//   ctr_tile (CTR GEMM tile, -1 by shape), ctr_igemm, ctr_igemm_cfg, ctr_handoff, ctr_head_rpb (docs/startup_flags.md).
 #pragma once
 
 #include <cstdlib>
