@@ -1052,10 +1052,10 @@ hipError_t head_bce_fwd(const void* x, const void* w, const void* b, bool b_bf16
 }
 
 int head_bce_bwd_blocks(int M) {
-  // 64 rows per block, at most 1024 partials (KDL_TUNE ctr_head_rpb: 32 / 16 rows measured
-  // 0.5 / 4 % slower per CTR step -- more blocks, more ticket atomics on one word;
-  // profiles/r06_ctr_small.txt)
-  static const int rpb = [] { const int v = tune_int("ctr_head_rpb", 64); return v < 8 ? 8 : v; }();
+  // 128 rows per block, at most 1024 partials (KDL_TUNE ctr_head_rpb: with the batched row
+  // loads 128 rows measured +0.3 % per CTR step over 64 and 32 rows -2 to -9 %: more blocks,
+  // more ticket atomics on one word; profiles/r06_ctr_rpb2.txt, r06_ctr_small.txt)
+  static const int rpb = [] { const int v = tune_int("ctr_head_rpb", 128); return v < 8 ? 8 : v; }();
   int nb = (M + rpb - 1) / rpb;
   return nb < 1024 ? nb : 1024;
 }
